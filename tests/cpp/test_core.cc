@@ -1,0 +1,295 @@
+// Core library tests: YAML/JSON, matchers, tar/gzip, hashing, CLI parser.
+#include <unistd.h>
+
+#include "core/cli.h"
+#include "core/codec.h"
+#include "core/fs.h"
+#include "core/match.h"
+#include "core/proc.h"
+#include "core/strutil.h"
+#include "core/value.h"
+#include "testing.h"
+
+using namespace ds;
+
+TEST(yaml_basic_map_and_seq) {
+  Value v = yaml_parse(
+      "version: v1alpha2\n"
+      "cluster:\n"
+      "  namespace: test   # comment\n"
+      "dev:\n"
+      "  sync:\n"
+      "  - containerPath: /app\n"
+      "    localSubPath: ./\n"
+      "    uploadExcludePaths:\n"
+      "    - Dockerfile\n"
+      "    - node_modules/\n"
+      "  ports:\n"
+      "    - portMappings:\n"
+      "        - localPort: 3000\n"
+      "          remotePort: 3000\n");
+  EXPECT_EQ(v.get("version").as_string(), std::string("v1alpha2"));
+  EXPECT_EQ(v.at_path("cluster.namespace").as_string(), std::string("test"));
+  const Value& sync = v.at_path("dev.sync");
+  EXPECT_TRUE(sync.is_seq());
+  EXPECT_EQ(sync.size(), (size_t)1);
+  EXPECT_EQ(sync[0].get("containerPath").as_string(), std::string("/app"));
+  EXPECT_EQ(sync[0].get("uploadExcludePaths").size(), (size_t)2);
+  const Value& pm = v.at_path("dev.ports")[0].get("portMappings")[0];
+  EXPECT_EQ(pm.get("localPort").as_int(), (int64_t)3000);
+  EXPECT_TRUE(pm.get("localPort").is_int());
+}
+
+TEST(yaml_scalars_and_quotes) {
+  Value v = yaml_parse(
+      "a: \"123\"\n"
+      "b: 123\n"
+      "c: 'it''s'\n"
+      "d: true\n"
+      "e: ~\n"
+      "f: \"line\\nbreak\"\n"
+      "g: 1.5\n"
+      "h: [a, 'b', {x: 1}]\n"
+      "i: {k: v, n: 2}\n"
+      "j: \"999999999999\"\n"
+      "k: http://example.com:8080/x\n");
+  EXPECT_TRUE(v.get("a").is_string());
+  EXPECT_TRUE(v.get("b").is_int());
+  EXPECT_EQ(v.get("c").as_string(), std::string("it's"));
+  EXPECT_TRUE(v.get("d").as_bool());
+  EXPECT_TRUE(v.get("e").is_null());
+  EXPECT_EQ(v.get("f").as_string(), std::string("line\nbreak"));
+  EXPECT_TRUE(v.get("g").is_float());
+  EXPECT_EQ(v.get("h").size(), (size_t)3);
+  EXPECT_EQ(v.get("h")[2].get("x").as_int(), (int64_t)1);
+  EXPECT_EQ(v.get("i").get("n").as_int(), (int64_t)2);
+  EXPECT_EQ(v.get("k").as_string(), std::string("http://example.com:8080/x"));
+}
+
+TEST(yaml_block_scalars_and_anchors) {
+  Value v = yaml_parse(
+      "lit: |\n"
+      "  line1\n"
+      "  line2\n"
+      "fold: >-\n"
+      "  a\n"
+      "  b\n"
+      "base: &b\n"
+      "  x: 1\n"
+      "derived:\n"
+      "  <<: *b\n"
+      "  y: 2\n");
+  EXPECT_EQ(v.get("lit").as_string(), std::string("line1\nline2\n"));
+  EXPECT_EQ(v.get("fold").as_string(), std::string("a b"));
+  EXPECT_EQ(v.get("derived").get("x").as_int(), (int64_t)1);
+  EXPECT_EQ(v.get("derived").get("y").as_int(), (int64_t)2);
+}
+
+TEST(yaml_multi_document) {
+  auto docs = yaml_parse_all("a: 1\n---\nb: 2\n---\n# only comment\n---\nc: 3\n");
+  EXPECT_EQ(docs.size(), (size_t)4);
+  EXPECT_EQ(docs[1].get("b").as_int(), (int64_t)2);
+  EXPECT_TRUE(docs[2].is_null());
+}
+
+TEST(yaml_roundtrip) {
+  std::string src =
+      "version: v1alpha2\n"
+      "images:\n"
+      "  default:\n"
+      "    image: dscr.io/user/devspace\n"
+      "    createPullSecret: true\n"
+      "deployments:\n"
+      "- name: devspace-app\n"
+      "  helm:\n"
+      "    chartPath: ./chart\n"
+      "dev:\n"
+      "  overrideImages:\n"
+      "  - name: default\n"
+      "    entrypoint:\n"
+      "    - sleep\n"
+      "    - \"999999999999\"\n";
+  Value v = yaml_parse(src);
+  std::string out = yaml_dump(v);
+  EXPECT_EQ(out, src);
+  Value v2 = yaml_parse(out);
+  EXPECT_TRUE(v == v2);
+  Value ml = Value::map();
+  ml["s"] = "a\nb\n";
+  ml["e"] = "";
+  ml["n"] = "true";
+  Value back = yaml_parse(yaml_dump(ml));
+  EXPECT_EQ(back.get("s").as_string(), std::string("a\nb\n"));
+  EXPECT_TRUE(back.get("e").is_string());
+  EXPECT_TRUE(back.get("n").is_string());
+}
+
+TEST(json_roundtrip) {
+  Value v = json_parse("{\"a\": [1, 2.5, \"x\\u00e9\", true, null], \"b\": {\"c\": \"d\"}}");
+  EXPECT_EQ(v.get("a")[2].as_string(), std::string("x\xc3\xa9"));
+  std::string d = json_dump(v);
+  EXPECT_TRUE(json_parse(d) == v);
+  EXPECT_EQ(json_dump(json_parse("{}")), std::string("{}"));
+}
+
+TEST(merge_semantics) {
+  // config/configutil/merge_test.go:10 TestSimpleMerge — maps merge, slices replace.
+  Value base = yaml_parse("a: 1\nm:\n  x: 1\n  y: [1, 2]\n");
+  Value over = yaml_parse("b: 2\nm:\n  y: [3]\n  z: 4\n");
+  merge_into(base, over);
+  EXPECT_EQ(base.get("a").as_int(), (int64_t)1);
+  EXPECT_EQ(base.get("b").as_int(), (int64_t)2);
+  EXPECT_EQ(base.at_path("m.x").as_int(), (int64_t)1);
+  EXPECT_EQ(base.at_path("m.y").size(), (size_t)1);
+  EXPECT_EQ(base.at_path("m.z").as_int(), (int64_t)4);
+}
+
+TEST(gitignore_matcher) {
+  GitIgnore gi({"/.devspace/logs", "node_modules/", "*.pyc", "ignoreFileLocal", "testFolder/deep", "!keep.pyc"});
+  EXPECT_TRUE(gi.matches("/.devspace/logs"));
+  EXPECT_TRUE(gi.matches("/.devspace/logs/sync.log"));
+  EXPECT_TRUE(!gi.matches("/x/.devspace/logs"));
+  EXPECT_TRUE(gi.matches("/node_modules/"));
+  EXPECT_TRUE(gi.matches("/node_modules/a/b.js"));
+  EXPECT_TRUE(gi.matches("/a/b/c.pyc"));
+  EXPECT_TRUE(!gi.matches("/a/keep.pyc"));
+  EXPECT_TRUE(gi.matches("/ignoreFileLocal"));
+  EXPECT_TRUE(gi.matches("/testFolder/ignoreFileLocal"));
+  EXPECT_TRUE(!gi.matches("/ignoreFileLocalX"));
+  EXPECT_TRUE(gi.matches("/testFolder/deep/x"));
+  GitIgnore g2({"Dockerfile", ".devspace/", "chart/"});
+  EXPECT_TRUE(g2.matches("/Dockerfile"));
+  EXPECT_TRUE(g2.matches("/chart/templates/a.yaml"));
+  EXPECT_TRUE(g2.matches("/.devspace/config.yaml"));
+  EXPECT_TRUE(!g2.matches("/index.js"));
+  GitIgnore g3({"**/tmp", "logs/**"});
+  EXPECT_TRUE(g3.matches("/a/b/tmp"));
+  EXPECT_TRUE(g3.matches("/logs/x/y"));
+}
+
+TEST(docker_ignore_and_glob) {
+  DockerIgnore di({"node_modules", "*.log", "!important.log", "build/**/*.o"});
+  EXPECT_TRUE(di.matches("node_modules"));
+  EXPECT_TRUE(di.matches("node_modules/x/y.js"));
+  EXPECT_TRUE(di.matches("a.log"));
+  EXPECT_TRUE(!di.matches("important.log"));
+  EXPECT_TRUE(di.matches("build/a/b/c.o"));
+  EXPECT_TRUE(!di.matches("src/a.js"));
+  EXPECT_TRUE(glob_match("chart/**", "chart/templates/a.yaml"));
+  EXPECT_TRUE(glob_match("kube/*.yaml", "kube/dep.yaml"));
+  EXPECT_TRUE(!glob_match("kube/*.yaml", "kube/x/dep.yaml"));
+  EXPECT_TRUE(glob_match("**/*.{yaml,yml}", "a/b/c.yml"));
+  EXPECT_TRUE(path_match("[a-c]?.txt", "bx.txt"));
+}
+
+TEST(tar_gzip_roundtrip) {
+  std::string out;
+  {
+    GzipWriter gz(string_sink(&out), 1);
+    TarWriter tw([&](const char* d, size_t n) { return gz.write(d, n); });
+    TarEntry f;
+    f.name = "dir/file.txt";
+    f.mode = 0640;
+    f.mtime = 1500000000;
+    tw.add_file(f, "hello world");
+    TarEntry d;
+    d.name = "emptydir";
+    d.mtime = 1500000001;
+    d.mode = 0755;
+    tw.add_dir(d);
+    TarEntry lf;
+    lf.name = std::string(150, 'x') + "/long.txt";
+    tw.add_file(lf, std::string(1000, 'z'));
+    tw.finish();
+    gz.finish();
+  }
+  GzipReader gr(string_source(&out));
+  TarReader tr([&](char* b, size_t n) { return gr.read(b, n); });
+  TarEntry e;
+  EXPECT_TRUE(tr.next(&e));
+  EXPECT_EQ(e.name, std::string("dir/file.txt"));
+  EXPECT_EQ(e.mode, (uint32_t)0640);
+  EXPECT_EQ(e.mtime, (int64_t)1500000000);
+  EXPECT_EQ(tr.read_all(), std::string("hello world"));
+  EXPECT_TRUE(tr.next(&e));
+  EXPECT_EQ(e.type, '5');
+  EXPECT_TRUE(tr.next(&e));
+  EXPECT_EQ(e.name.size(), (size_t)159);
+  EXPECT_EQ(tr.read_all().size(), (size_t)1000);
+  EXPECT_TRUE(!tr.next(&e));
+}
+
+TEST(tar_interop_with_gnu_tar) {
+  if (which("tar").empty()) return;
+  std::string dir = fs::make_temp_dir();
+  fs::write_file(fs::join(dir, "src/a.txt"), "A");
+  fs::write_file(fs::join(dir, "src/sub/b.txt"), "BB");
+  RunResult r = run({"tar", "-czf", fs::join(dir, "x.tgz"), "-C", fs::join(dir, "src"), "."});
+  EXPECT_EQ(r.code, 0);
+  std::string data = fs::read_file(fs::join(dir, "x.tgz"));
+  GzipReader gr(string_source(&data));
+  TarReader tr([&](char* b, size_t n) { return gr.read(b, n); });
+  TarEntry e;
+  int files = 0;
+  while (tr.next(&e))
+    if (e.type == '0') ++files;
+  EXPECT_EQ(files, 2);
+  // and the other direction: our archive extracts with GNU tar
+  std::string ours;
+  {
+    GzipWriter gz(string_sink(&ours));
+    TarWriter tw([&](const char* d, size_t n) { return gz.write(d, n); });
+    TarEntry f;
+    f.name = "deep/dir/" + std::string(120, 'q') + ".txt";
+    f.mode = 0644;
+    tw.add_file(f, "payload");
+    tw.finish();
+    gz.finish();
+  }
+  fs::write_file(fs::join(dir, "ours.tgz"), ours);
+  fs::mkdirs(fs::join(dir, "out"));
+  r = run({"tar", "-xzf", fs::join(dir, "ours.tgz"), "-C", fs::join(dir, "out")});
+  EXPECT_EQ(r.code, 0);
+  EXPECT_EQ(fs::read_file(fs::join(dir, "out/deep/dir/" + std::string(120, 'q') + ".txt")), std::string("payload"));
+  fs::remove_all(dir);
+}
+
+TEST(hash_and_encodings) {
+  EXPECT_EQ(sha256_hex("abc"), std::string("ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"));
+  EXPECT_EQ(base64_encode("hello"), std::string("aGVsbG8="));
+  EXPECT_EQ(base64_decode("aGVsbG8="), std::string("hello"));
+  EXPECT_EQ(base64_decode(base64_encode(std::string("\xff\xfe\x01", 3), true)), std::string("\xff\xfe\x01", 3));
+  std::string r = random_string(7);
+  EXPECT_EQ(r.size(), (size_t)7);
+  for (char c : r) EXPECT_TRUE(std::isalnum((unsigned char)c));
+}
+
+TEST(cli_flags) {
+  cli::Command root("devspace", "root");
+  root.persistent_bool("debug", "", false, "debug");
+  auto dev = std::make_unique<cli::Command>("dev", "start dev");
+  std::string seen;
+  dev->boolean("force-build", "b", false, "force build")
+      .boolean("sync", "", true, "sync")
+      .str("namespace", "n", "", "ns")
+      .slice("exclude", "", "excludes")
+      .integer("lines", "", 200, "lines");
+  dev->run = [&](cli::Command& c, const std::vector<std::string>& args) {
+    seen = std::to_string(c.get_bool("force-build")) + std::to_string(c.get_bool("sync")) + c.get_str("namespace") +
+           std::to_string(c.get_slice("exclude").size()) + std::to_string(c.get_int("lines")) +
+           std::to_string(args.size()) + std::to_string(c.get_bool("debug"));
+    return 0;
+  };
+  dev->aliases = {"up"};
+  root.add(std::move(dev));
+  EXPECT_EQ(root.execute({"up", "-b", "--sync=false", "-n", "ns1", "--exclude", "a,b", "--lines=5", "x", "--debug"}), 0);
+  EXPECT_EQ(seen, std::string("10ns12511"));
+}
+
+TEST(fs_paths) {
+  EXPECT_EQ(fs::clean("/a/b/../c/./d/"), std::string("/a/c/d"));
+  EXPECT_EQ(fs::dirname("/a/b/c"), std::string("/a/b"));
+  EXPECT_EQ(fs::basename("/a/b/c/"), std::string("c"));
+  EXPECT_EQ(fs::relative("/a/b", "/a/b/c/d"), std::string("c/d"));
+  EXPECT_EQ(fs::join("a/", "/b"), std::string("a/b"));
+}
