@@ -1,1 +1,288 @@
-int main() { return 0; }
+// devspace-helper — static in-container sync agent (SURVEY.md §7.6 "optional static helper").
+//
+// Replaces the reference's per-operation shell scripts (sync/upstream.go:387, downstream.go:373)
+// and the 1.3 s full `find` poll with a persistent process speaking a framed protocol on
+// stdin/stdout and pushing inotify change notifications on stderr:
+//
+//   request  := op:u8  len:u32be  payload[len]
+//   'U' payload=tar.gz          -> extract under <dest> (tar xzpf semantics)   reply "OK\n" | "ERR msg\n"
+//   'R' payload=rel\n...        -> rm -rf <dest><rel>                          reply "OK\n"
+//   'S' (empty)                 -> "<abs>///size,mtime,hexmode,perm,uid,gid\n"... then "DONE\n"
+//   'D' payload=rel\n...        -> "SIZE n\n" + n bytes tar.gz (relative member names)
+//   'W' (empty)                 -> start watching; "E\n" on stderr after changes settle
+//   'Q'                          -> exit
+//
+// Built with -static so it runs in any x86_64 container image (no libc/zlib dependency).
+#include <fcntl.h>
+#include <poll.h>
+#include <signal.h>
+#include <sys/inotify.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "core/codec.h"
+#include "core/fs.h"
+#include "core/proc.h"
+#include "core/strutil.h"
+
+using namespace ds;
+
+static std::string g_dest;
+static std::atomic<long> g_suppress_until_us{0};
+
+static long now_us() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1000000L + ts.tv_nsec / 1000;
+}
+
+static bool reply(const std::string& s) { return write_all(1, s); }
+
+static std::string safe_join(const std::string& rel_in) {
+  std::string rel = rel_in;
+  while (starts_with(rel, "./")) rel = rel.substr(2);
+  std::string c = fs::clean("/" + rel);  // strips any ".." escaping the root
+  return c == "/" ? g_dest : g_dest + c;
+}
+
+static std::string op_extract(const std::string& payload) {
+  GzipReader gz(string_source(&payload));
+  TarReader tr([&](char* b, size_t n) { return gz.read(b, n); });
+  TarEntry e;
+  bool root = ::geteuid() == 0;
+  try {
+    while (tr.next(&e)) {
+      std::string out = safe_join(e.name);
+      if (e.type == '5') {
+        fs::mkdirs(out, 0755);
+        ::chmod(out.c_str(), e.mode & 07777);
+        if (root) {
+          int ignored = ::lchown(out.c_str(), e.uid, e.gid);
+          (void)ignored;
+        }
+        fs::set_mtime(out, e.mtime);
+        continue;
+      }
+      if (e.type == '2') {
+        fs::mkdirs(fs::dirname(out));
+        ::unlink(out.c_str());
+        int ignored = ::symlink(e.linkname.c_str(), out.c_str());
+        (void)ignored;
+        continue;
+      }
+      if (e.type != '0' && e.type != '7') {
+        tr.skip();
+        continue;
+      }
+      fs::mkdirs(fs::dirname(out));
+      std::string tmp = out + ".devspace-tmp";
+      int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0600);
+      if (fd < 0) return std::string("ERR open ") + out + ": " + std::strerror(errno);
+      char buf[1 << 16];
+      while (true) {
+        ssize_t n = tr.read(buf, sizeof(buf));
+        if (n <= 0) break;
+        if (!write_all(fd, buf, (size_t)n)) {
+          ::close(fd);
+          return "ERR write " + out;
+        }
+      }
+      ::fchmod(fd, e.mode & 07777);
+      if (root) {
+        int ignored = ::fchown(fd, e.uid, e.gid);
+        (void)ignored;
+      }
+      ::close(fd);
+      fs::set_mtime(tmp, e.mtime);
+      if (::rename(tmp.c_str(), out.c_str()) != 0) {
+        // target may be a directory being replaced by a file
+        fs::remove_all(out);
+        if (::rename(tmp.c_str(), out.c_str()) != 0) return "ERR rename " + out;
+      }
+    }
+  } catch (const std::exception& ex) {
+    return std::string("ERR ") + ex.what();
+  }
+  return "OK";
+}
+
+static void scan_rec(const std::string& p, std::string& out, std::set<std::pair<uint64_t, uint64_t>>& seen,
+                     int depth) {
+  struct stat lst;
+  if (::lstat(p.c_str(), &lst) != 0) return;
+  struct stat st = lst;
+  if (S_ISLNK(lst.st_mode)) {
+    if (::stat(p.c_str(), &st) != 0) st = lst;
+  }
+  // like `find -L ... -exec stat -c` : stat of the path itself (links reported as links)
+  out += p + "///" + std::to_string((long long)lst.st_size) + "," + std::to_string((long long)lst.st_mtim.tv_sec) +
+         "," + strfmt("%x", (unsigned)lst.st_mode) + "," + strfmt("%o", (unsigned)(lst.st_mode & 07777)) + "," +
+         std::to_string(lst.st_uid) + "," + std::to_string(lst.st_gid) + "\n";
+  if (S_ISDIR(st.st_mode) && depth < 128) {
+    auto key = std::make_pair((uint64_t)st.st_dev, (uint64_t)st.st_ino);
+    if (seen.count(key)) return;
+    seen.insert(key);
+    for (auto& e : fs::list_dir(p)) scan_rec(p + "/" + e.name, out, seen, depth + 1);
+  }
+}
+
+static std::string op_scan() {
+  fs::mkdirs(g_dest);
+  std::string out;
+  std::set<std::pair<uint64_t, uint64_t>> seen;
+  scan_rec(g_dest, out, seen, 0);
+  out += "DONE\n";
+  return out;
+}
+
+static void op_remove(const std::string& payload) {
+  for (auto& rel : split(payload, "\n")) {
+    if (rel.empty()) continue;
+    std::string p = safe_join(rel);
+    if (p == g_dest) continue;
+    fs::remove_all(p);
+  }
+}
+
+static std::string op_download(const std::string& payload) {
+  std::string out;
+  GzipWriter gz(string_sink(&out), 1);
+  TarWriter tw([&](const char* d, size_t n) { return gz.write(d, n); });
+  for (auto& rel : split(payload, "\n")) {
+    if (rel.empty()) continue;
+    std::string p = safe_join(rel);
+    fs::StatInfo st = fs::stat(p);
+    if (!st.exists || st.is_dir) continue;
+    TarEntry e;
+    e.name = rel[0] == '/' ? rel.substr(1) : rel;
+    e.mode = st.mode & 07777;
+    e.uid = st.uid;
+    e.gid = st.gid;
+    e.size = st.size;
+    e.mtime = st.mtime_sec;
+    tw.add_file_from_path(e, p);
+  }
+  tw.finish();
+  gz.finish();
+  return out;
+}
+
+static void add_watch_rec(int fd, const std::string& dir, std::map<int, std::string>& wds, int depth) {
+  int wd = inotify_add_watch(fd, dir.c_str(),
+                             IN_CREATE | IN_DELETE | IN_CLOSE_WRITE | IN_MOVED_FROM | IN_MOVED_TO | IN_ATTRIB);
+  if (wd < 0) return;
+  wds[wd] = dir;
+  if (depth > 64) return;
+  for (auto& e : fs::list_dir(dir))
+    if (e.is_dir && !e.is_symlink) add_watch_rec(fd, dir + "/" + e.name, wds, depth + 1);
+}
+
+static void watch_loop() {
+  int fd = inotify_init1(IN_CLOEXEC);
+  if (fd < 0) return;
+  std::map<int, std::string> wds;
+  fs::mkdirs(g_dest);
+  add_watch_rec(fd, g_dest, wds, 0);
+  alignas(struct inotify_event) char buf[1 << 16];
+  while (true) {
+    ssize_t n = ::read(fd, buf, sizeof(buf));
+    if (n <= 0) {
+      if (errno == EINTR) continue;
+      break;
+    }
+    bool changed = false;
+    for (char* p = buf; p < buf + n;) {
+      auto* ev = (struct inotify_event*)p;
+      p += sizeof(struct inotify_event) + ev->len;
+      std::string name = ev->len ? std::string(ev->name) : "";
+      if (ends_with(name, ".devspace-tmp")) continue;
+      if ((ev->mask & IN_ISDIR) && (ev->mask & (IN_CREATE | IN_MOVED_TO))) {
+        auto it = wds.find(ev->wd);
+        if (it != wds.end()) add_watch_rec(fd, it->second + "/" + name, wds, 0);
+      }
+      if (ev->mask & IN_IGNORED) {
+        wds.erase(ev->wd);
+        continue;
+      }
+      changed = true;
+    }
+    if (!changed) continue;
+    // settle: wait until no events for 20 ms, then notify once
+    while (true) {
+      struct pollfd pf{fd, POLLIN, 0};
+      if (::poll(&pf, 1, 20) <= 0) break;
+      ssize_t m = ::read(fd, buf, sizeof(buf));
+      if (m <= 0) break;
+      for (char* p = buf; p < buf + m;) {
+        auto* ev = (struct inotify_event*)p;
+        p += sizeof(struct inotify_event) + ev->len;
+        if ((ev->mask & IN_ISDIR) && (ev->mask & (IN_CREATE | IN_MOVED_TO))) {
+          auto it = wds.find(ev->wd);
+          if (it != wds.end()) add_watch_rec(fd, it->second + "/" + std::string(ev->name), wds, 0);
+        }
+      }
+    }
+    if (now_us() < g_suppress_until_us.load()) continue;  // our own writes
+    write_all(2, "E\n");
+  }
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3 || std::string(argv[1]) != "serve") {
+    std::fprintf(stderr, "usage: devspace-helper serve <dest>\n");
+    return 2;
+  }
+  signal(SIGPIPE, SIG_IGN);
+  g_dest = fs::clean(argv[2]);
+  fs::mkdirs(g_dest);
+  reply("HELPER READY\n");
+  std::thread watcher;
+  while (true) {
+    unsigned char hdr[5];
+    if (!read_exact(0, hdr, 5)) break;
+    uint32_t len = ((uint32_t)hdr[1] << 24) | ((uint32_t)hdr[2] << 16) | ((uint32_t)hdr[3] << 8) | hdr[4];
+    std::string payload(len, '\0');
+    if (len && !read_exact(0, &payload[0], len)) break;
+    switch (hdr[0]) {
+      case 'U': {
+        g_suppress_until_us = now_us() + 60000000L;
+        std::string r = op_extract(payload);
+        g_suppress_until_us = now_us() + 40000;  // ignore the echo of our own extraction
+        reply(r + "\n");
+        break;
+      }
+      case 'R':
+        g_suppress_until_us = now_us() + 60000000L;
+        op_remove(payload);
+        g_suppress_until_us = now_us() + 40000;
+        reply("OK\n");
+        break;
+      case 'S': reply(op_scan()); break;
+      case 'D': {
+        std::string a = op_download(payload);
+        reply("SIZE " + std::to_string(a.size()) + "\n");
+        write_all(1, a);
+        break;
+      }
+      case 'W':
+        if (!watcher.joinable()) {
+          watcher = std::thread(watch_loop);
+          watcher.detach();
+        }
+        break;
+      case 'Q': return 0;
+      default: reply("ERR unknown op\n");
+    }
+  }
+  return 0;
+}

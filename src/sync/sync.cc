@@ -1,0 +1,1479 @@
+#include "sync/sync.h"
+
+#include <signal.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+
+#include "core/strutil.h"
+
+namespace ds {
+namespace sync {
+
+static const char* kStart = "START";
+static const char* kDone = "DONE";
+static const char* kError = "ERROR";
+static const size_t kInitialUpstreamBatch = 1000;  // sync_config.go:20
+
+static long mono_us() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1000000L + ts.tv_nsec / 1000;
+}
+
+static void sleep_ms(int ms) { std::this_thread::sleep_for(std::chrono::milliseconds(ms)); }
+
+Mode parse_mode(const std::string& s_in) {
+  std::string s = to_lower(s_in);
+  if (s.empty()) {
+    const char* e = getenv("DEVSPACE_SYNC_MODE");
+    if (e && *e) s = to_lower(e);
+  }
+  if (s == "compat" || s == "reference") return Mode::Compat;
+  if (s == "helper") return Mode::Helper;
+  return Mode::Fast;
+}
+
+const char* mode_name(Mode m) {
+  switch (m) {
+    case Mode::Compat: return "compat";
+    case Mode::Fast: return "fast";
+    case Mode::Helper: return "helper";
+  }
+  return "?";
+}
+
+struct SyncError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// ============================================================ file info / index
+
+std::optional<FileInfo> parse_file_line(const std::string& line, const std::string& dest) {
+  auto t = split(line, "///");
+  if (t.size() != 2) throw SyncError("[Downstream] Wrong fileline: " + line);
+  if (t[0].size() <= dest.size()) return std::nullopt;
+  FileInfo f;
+  f.name = t[0].substr(dest.size());
+  auto p = split(t[1], ",");
+  if (p.size() != 6) throw SyncError("[Downstream] Wrong fileline: " + line);
+  int64_t v;
+  if (!parse_int64(p[0], &v)) throw SyncError("[Downstream] Wrong fileline: " + line);
+  f.size = v;
+  if (!parse_int64(p[1], &v)) throw SyncError("[Downstream] Wrong fileline: " + line);
+  f.mtime = v;
+  unsigned long raw = std::strtoul(p[2].c_str(), nullptr, 16);
+  f.is_symlink = (raw & 0120000) == 0120000;
+  f.is_dir = (raw & 040000) == 040000 && !f.is_symlink;
+  f.remote_mode = std::strtol(p[3].c_str(), nullptr, 8);
+  f.remote_uid = std::atoi(p[4].c_str());
+  f.remote_gid = std::atoi(p[5].c_str());
+  f.has_remote_attrs = true;
+  return f;
+}
+
+void FileIndex::create_dir(const std::string& dirpath) {
+  if (dirpath == "/" || dirpath.empty() || dirpath == ".") return;
+  auto parts = split(dirpath, "/");
+  for (size_t i = parts.size(); i > 1; --i) {
+    std::vector<std::string> sub(parts.begin(), parts.begin() + i);
+    std::string p = join(sub, "/");
+    if (p.empty()) continue;
+    if (!files.count(p)) {
+      FileInfo f;
+      f.name = p;
+      f.is_dir = true;
+      files[p] = f;
+    }
+  }
+}
+
+void FileIndex::remove_dir(const std::string& dirpath) {
+  auto it = files.find(dirpath);
+  if (it == files.end()) return;
+  files.erase(it);
+  std::string prefix = dirpath + "/";
+  auto lo = files.lower_bound(prefix);
+  auto hi = lo;
+  while (hi != files.end() && starts_with(hi->first, prefix)) ++hi;
+  files.erase(lo, hi);
+}
+
+// ============================================================ session setup
+
+Session::Session(Options opts, std::shared_ptr<Transport> transport)
+    : o_(std::move(opts)), transport_(std::move(transport)), mode_(o_.mode) {}
+
+Session::~Session() { stop(); }
+
+void Session::logf(const std::string& msg) {
+  if (o_.silent || !log_) return;
+  std::map<std::string, std::string> f{{"local", o_.watch_path}, {"container", o_.dest_path}};
+  if (!o_.pod_name.empty()) f["pod"] = o_.pod_name;
+  log_->emit("info", msg, f);
+}
+
+void Session::log_error(const std::string& msg) {
+  if (!log_) return;
+  std::map<std::string, std::string> f{{"local", o_.watch_path}, {"container", o_.dest_path}};
+  if (!o_.pod_name.empty()) f["pod"] = o_.pod_name;
+  log_->emit("error", msg, f);
+}
+
+std::string Session::remote(const std::string& p) const {
+  std::string pre = transport_ ? transport_->path_prefix() : "";
+  if (pre.empty()) return p;
+  return fs::clean(pre + "/" + p);
+}
+
+void Session::setup() {
+  std::string real = fs::realpath(o_.watch_path);
+  if (real.empty()) throw SyncError("lstat " + o_.watch_path + ": no such file or directory");
+  o_.watch_path = real;
+  // exclude the sync log to prevent an endless upstream loop (sync_config.go:116)
+  o_.exclude_paths.push_back("/.devspace/logs");
+  ignore_ = GitIgnore(o_.exclude_paths);
+  has_ignore_ = !ignore_.empty();
+  download_ignore_ = GitIgnore(o_.download_exclude_paths);
+  has_download_ignore_ = !download_ignore_.empty();
+  upload_ignore_ = GitIgnore(o_.upload_exclude_paths);
+  has_upload_ignore_ = !upload_ignore_.empty();
+  if (!o_.silent) {
+    // rotate sync.log into sync.log.old once per process (sync/util.go:305)
+    static std::once_flag rotated;
+    std::string logfile = fs::join(log::logdir(), o_.sync_log_name + ".log");
+    std::call_once(rotated, [&] {
+      std::string data;
+      if (fs::read_file(logfile, &data)) {
+        fs::append_file(logfile + ".old", data);
+        fs::remove(logfile);
+      }
+    });
+    log_ = log::file_logger(o_.sync_log_name);
+  }
+  switch (mode_) {
+    case Mode::Compat:
+      window_ms_ = 600;
+      poll_ms_ = 1300;
+      break;
+    case Mode::Fast:
+      window_ms_ = 15;
+      poll_ms_ = 250;
+      break;
+    case Mode::Helper:
+      window_ms_ = 10;
+      poll_ms_ = 2000;  // fallback poll; events normally drive downstream
+      break;
+  }
+  if (o_.upstream_window_ms >= 0) window_ms_ = o_.upstream_window_ms;
+  if (o_.downstream_poll_ms >= 0) poll_ms_ = o_.downstream_poll_ms;
+  dest_ = remote(o_.dest_path);
+}
+
+// ============================================================ helper bootstrap
+
+static void put_u32(std::string& s, uint32_t v) {
+  s.push_back((char)(v >> 24));
+  s.push_back((char)(v >> 16));
+  s.push_back((char)(v >> 8));
+  s.push_back((char)v);
+}
+
+static std::string frame(char op, const std::string& payload) {
+  std::string f;
+  f.reserve(payload.size() + 5);
+  f.push_back(op);
+  put_u32(f, (uint32_t)payload.size());
+  f += payload;
+  return f;
+}
+
+bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out) {
+  // Probe architecture + writable /tmp, upload the static helper once (content-addressed),
+  // then exec it in place of the shell.
+  if (o_.helper_path.empty() || !fs::is_file(o_.helper_path)) return false;
+  std::string bin;
+  if (!fs::read_file(o_.helper_path, &bin)) return false;
+  std::string name = "/tmp/devspace-helper-" + sha256_hex(bin).substr(0, 16);
+  std::string probe = "if [ \"$(uname -m 2>/dev/null)\" = x86_64 ] && mkdir -p /tmp && [ -w /tmp ]; then if [ -x " +
+                      name + " ]; then echo HAVE; else echo NEED; fi; else echo NOHELPER; fi\n";
+  if (!write_all(sh->in(), probe)) return false;
+  std::string line;
+  if (!out.read_line(&line, 15000)) return false;
+  if (line == "NOHELPER") return false;
+  if (line == "NEED") {
+    std::string up = "echo " + std::string(kStart) + "; head -c " + std::to_string(bin.size()) + " > " + name +
+                     ".tmp && chmod +x " + name + ".tmp && mv " + name + ".tmp " + name + "; echo " + kDone + "\n";
+    if (!write_all(sh->in(), up)) return false;
+    if (!out.wait_for(kStart, 15000)) return false;
+    if (!write_all(sh->in(), bin)) return false;
+    if (!out.wait_for(kDone, 30000)) return false;
+  }
+  std::string exec = "exec " + name + " serve " + shell_quote(dest_) + " 2>&1 1>&3 3>&- || echo HELPERFAIL\n";
+  // keep stderr separate: exec with fds as-is
+  exec = "mkdir -p " + shell_quote(dest_) + " && exec " + name + " serve " + shell_quote(dest_) +
+         " || echo HELPERFAIL\n";
+  if (!write_all(sh->in(), exec)) return false;
+  if (!out.read_line(&line, 15000)) return false;
+  return line == "HELPER READY";
+}
+
+void Session::open_up_shell() {
+  std::lock_guard<std::mutex> g(up_shell_mu_);
+  up_shell_ = transport_->open({"sh"});
+  up_out_.reset(up_shell_->out());
+  up_helper_ = false;
+  if (mode_ == Mode::Helper) {
+    up_helper_ = start_helper(up_shell_, up_out_);
+    if (!up_helper_) {
+      logf("[Sync] Helper unavailable, falling back to fast POSIX protocol");
+      up_shell_->close();
+      up_shell_ = transport_->open({"sh"});
+      up_out_.reset(up_shell_->out());
+    }
+  }
+}
+
+void Session::open_down_shell() {
+  std::lock_guard<std::mutex> g(down_shell_mu_);
+  down_shell_ = transport_->open({"sh"});
+  down_out_.reset(down_shell_->out());
+  down_err_.reset(down_shell_->err());
+  down_helper_ = false;
+  if (mode_ == Mode::Helper) {
+    down_helper_ = start_helper(down_shell_, down_out_);
+    if (!down_helper_) {
+      down_shell_->close();
+      down_shell_ = transport_->open({"sh"});
+      down_out_.reset(down_shell_->out());
+      down_err_.reset(down_shell_->err());
+    } else {
+      // subscribe to container-side change events (pushed on stderr)
+      write_all(down_shell_->in(), frame('W', ""));
+    }
+  }
+}
+
+void Session::open_shells() {
+  open_up_shell();
+  open_down_shell();
+}
+
+// ============================================================ rules (evaluater.go)
+
+bool Session::should_remove_remote(const std::string& rel) {
+  if (has_ignore_ && ignore_.matches(rel)) return false;
+  if (has_upload_ignore_ && upload_ignore_.matches(rel)) return false;
+  FileInfo* f = index_.find(rel);
+  if (!f) return false;
+  if (f->is_symlink) return false;
+  return true;
+}
+
+bool Session::should_upload(const std::string& rel, const fs::StatInfo& st, bool initial) {
+  if (!st.exists) return false;
+  if (has_ignore_ && ignore_.matches(rel)) return false;
+  if (st.is_symlink) return false;
+  FileInfo* f = index_.find(rel);
+  if (f) {
+    if (st.is_dir) return false;
+    if (f->is_symlink) return false;
+    if (initial) {
+      if (st.mtime_rounded() <= f->mtime) return false;
+    } else {
+      if (st.mtime_rounded() == f->mtime && st.size == f->size) return false;
+    }
+  }
+  return true;
+}
+
+bool Session::should_download(const FileInfo& fi) {
+  if (has_ignore_ && ignore_.matches(fi.name)) return false;
+  if (has_download_ignore_ && download_ignore_.matches(fi.name)) return false;
+  if (fi.is_symlink) return false;
+  FileInfo* f = index_.find(fi.name);
+  if (f) {
+    if (!fi.is_dir) {
+      if (fi.mtime > f->mtime) return true;
+      if (fi.mtime == f->mtime && fi.size != f->size) return true;
+    }
+    return false;
+  }
+  return true;
+}
+
+bool Session::should_remove_local(const std::string& abs, const FileInfo& fi) {
+  if (has_download_ignore_ && download_ignore_.matches(fi.name)) return false;
+  fs::StatInfo st = fs::stat(abs);
+  if (!st.exists) return false;
+  FileInfo* f = index_.find(fi.name);
+  if (!f) return false;
+  if (st.is_dir != f->is_dir || st.is_dir != fi.is_dir) {
+    logf("Skip " + abs + " because stat returned unequal isdir with fileMap");
+    return false;
+  }
+  if (!fi.is_dir) {
+    if (fi.mtime == f->mtime && fi.size == f->size) {
+      if (st.mtime_rounded() <= fi.mtime) return true;
+      logf(strfmt("Skip %s because stat.ModTime() %lld is greater than fileInformation.Mtime %lld", abs.c_str(),
+                  (long long)st.mtime_rounded(), (long long)fi.mtime));
+    } else {
+      logf("Skip " + abs + " because Mtime or Size is unequal between fileInformation and fileMap");
+    }
+    return false;
+  }
+  return true;
+}
+
+// ============================================================ symlinks
+
+std::optional<fs::StatInfo> Session::add_symlink(const std::string& rel, const std::string& abs) {
+  std::string target = fs::realpath(abs);
+  if (target.empty()) {
+    logf("Warning: resolving symlink of " + abs);
+    return std::nullopt;
+  }
+  fs::StatInfo st = fs::stat(target);
+  if (!st.exists) {
+    logf("Warning: stating symlink " + target);
+    return std::nullopt;
+  }
+  std::lock_guard<std::mutex> g(symlink_mu_);
+  if (symlinks_.count(abs)) return st;
+  if (has_ignore_ && ignore_.matches(rel)) return std::nullopt;
+  std::string pattern = st.is_dir ? target + "/**" : target;
+  std::string link = abs;
+  auto w = std::make_unique<PollWatcher>(
+      std::vector<std::string>{pattern},
+      [this, link, target](const std::vector<std::string>& changed, const std::vector<std::string>& deleted) {
+        for (auto& p : changed) {
+          UpEvent e;
+          e.abs_path = link + p.substr(target.size());
+          push_event(e);
+        }
+        for (auto& p : deleted) {
+          UpEvent e;
+          e.abs_path = link + p.substr(target.size());
+          push_event(e);
+        }
+      },
+      500);
+  w->start();
+  symlinks_[abs] = std::move(w);
+  symlink_targets_[abs] = target;
+  return st;
+}
+
+void Session::remove_symlinks(const std::string& abs) {
+  std::lock_guard<std::mutex> g(symlink_mu_);
+  for (auto it = symlinks_.begin(); it != symlinks_.end();) {
+    if (it->first == abs || starts_with(it->first, abs + "/")) {
+      it->second->stop();
+      symlink_targets_.erase(it->first);
+      it = symlinks_.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
+
+// ============================================================ upstream
+
+void Session::push_event(UpEvent e) {
+  if (!e.t_us) e.t_us = mono_us();
+  {
+    std::lock_guard<std::mutex> g(q_mu_);
+    queue_.push_back(std::move(e));
+  }
+  q_cv_.notify_one();
+}
+
+void Session::start_watcher() {
+  watcher_ = std::make_unique<InotifyWatcher>();
+  std::string err;
+  bool ok = watcher_->start(
+      o_.watch_path,
+      [this](const std::string& path) {
+        if (path.empty()) {
+          // queue overflow: rescan everything
+          UpEvent e;
+          e.abs_path = o_.watch_path;
+          push_event(e);
+          return;
+        }
+        UpEvent e;
+        e.abs_path = path;
+        push_event(e);
+      },
+      &err);
+  if (!ok) throw SyncError("cannot watch " + o_.watch_path + ": " + err);
+}
+
+std::optional<FileInfo> Session::evaluate_change(const std::string& rel, const std::string& abs) {
+  fs::StatInfo st = fs::stat(abs);
+  if (st.exists) {
+    if (has_upload_ignore_ && upload_ignore_.matches(rel)) {
+      FileInfo* f = index_.find(rel);
+      if (f && f->mtime < st.mtime_rounded()) {
+        FileInfo n;
+        n.name = rel;
+        n.mtime = st.mtime_rounded();
+        n.size = st.size;
+        n.is_dir = st.is_dir;
+        index_.files[rel] = n;
+      }
+      return std::nullopt;
+    }
+    fs::StatInfo lst = fs::lstat(abs);
+    if (lst.is_symlink) {
+      bool existed;
+      {
+        std::lock_guard<std::mutex> g(symlink_mu_);
+        existed = symlinks_.count(abs) > 0;
+      }
+      auto s2 = add_symlink(rel, abs);
+      if (!s2) return std::nullopt;
+      st = *s2;
+      if (!existed && st.is_dir) {
+        // crawl linked tree (symlink.go:96)
+        std::string target = fs::realpath(abs);
+        fs::walk(target, [&](const std::string& p, const fs::StatInfo&) {
+          UpEvent e;
+          e.abs_path = abs + p.substr(target.size());
+          push_event(e);
+          return true;
+        });
+      }
+    }
+    if (should_upload(rel, st, false)) {
+      FileInfo f;
+      f.name = rel;
+      f.mtime = st.mtime_rounded();
+      f.size = st.size;
+      f.is_dir = st.is_dir;
+      return f;
+    }
+    return std::nullopt;
+  }
+  remove_symlinks(abs);
+  if (should_remove_remote(rel)) {
+    FileInfo f;
+    f.name = rel;
+    return f;
+  }
+  return std::nullopt;
+}
+
+void Session::upstream_loop() {
+  while (!stopping_ && !failed_) {
+    std::vector<UpEvent> batch;
+    {
+      std::unique_lock<std::mutex> lk(q_mu_);
+      q_cv_.wait_for(lk, std::chrono::milliseconds(200), [this] { return !queue_.empty() || stopping_ || failed_; });
+      if (queue_.empty()) continue;
+    }
+    std::vector<FileInfo> changes;
+    std::map<std::string, size_t> pos;
+    long first_us = 0;
+    long batch_start_us = mono_us();
+    size_t last_count = 0;
+    bool first = true;
+    while (!stopping_ && !failed_) {
+      std::vector<UpEvent> evs;
+      {
+        std::unique_lock<std::mutex> lk(q_mu_);
+        if (!first) {
+          q_cv_.wait_for(lk, std::chrono::milliseconds(window_ms_),
+                         [this] { return !queue_.empty() || stopping_ || failed_; });
+        }
+        evs.assign(std::make_move_iterator(queue_.begin()), std::make_move_iterator(queue_.end()));
+        queue_.clear();
+      }
+      first = false;
+      if (evs.empty()) {
+        if (!changes.empty()) break;  // quiet window elapsed
+        break;
+      }
+      if (!first_us) first_us = evs.front().t_us;
+      {
+        std::lock_guard<std::mutex> g(index_.mu);
+        for (auto& ev : evs) {
+          std::optional<FileInfo> fi;
+          if (ev.has_info) {
+            fi = ev.info;
+          } else {
+            if (!starts_with(ev.abs_path, o_.watch_path)) continue;
+            std::string rel = ev.abs_path.substr(o_.watch_path.size());
+            rel = replace_all(rel, "//", "/");
+            if (rel.empty()) {
+              // root itself (rescan request): diff the whole tree
+              continue;
+            }
+            fi = evaluate_change(rel, ev.abs_path);
+          }
+          if (!fi) continue;
+          auto it = pos.find(fi->name);
+          if (it != pos.end()) {
+            changes[it->second] = *fi;
+          } else {
+            pos[fi->name] = changes.size();
+            changes.push_back(*fi);
+          }
+        }
+      }
+      // compat: stop gathering when a window passed without new changes (upstream.go:148)
+      if (mode_ == Mode::Compat) {
+        if (!changes.empty() && changes.size() == last_count) break;
+        last_count = changes.size();
+      } else if (mono_us() - batch_start_us > 500000) {
+        break;  // cap coalescing under continuous writes
+      }
+    }
+    if (changes.empty() || stopping_ || failed_) continue;
+    try {
+      apply_upstream(changes, first_us);
+    } catch (const std::exception& e) {
+      fail(e.what());
+      return;
+    }
+  }
+}
+
+void Session::apply_upstream(std::vector<FileInfo>& changes, long first_event_us) {
+  std::vector<FileInfo> creates, removes;
+  for (auto& c : changes) (c.mtime > 0 ? creates : removes).push_back(c);
+  if (!removes.empty()) apply_removes(removes);
+  if (!creates.empty()) apply_creates(creates);
+  logf(strfmt("[Upstream] Successfully processed %zu change(s)", changes.size()));
+  std::lock_guard<std::mutex> g(stats_mu_);
+  stats_.upstream_batches++;
+  stats_.upstream_changes += changes.size();
+  if (first_event_us) stats_.last_upload_ms = (double)(mono_us() - first_event_us) / 1000.0;
+}
+
+bool Session::wait_ack(LineReader& r, const std::string& keyword, bool partial, std::string* before,
+                       int timeout_ms) {
+  long deadline = mono_us() + (long)timeout_ms * 1000;
+  while (!stopping_) {
+    if (r.wait_for(keyword, 200, before, partial)) return true;
+    if (r.eof()) throw SyncError("stream closed unexpectedly while waiting for " + keyword);
+    if (mono_us() > deadline) throw SyncError("timeout waiting for " + keyword);
+  }
+  throw SyncError("sync stopped");
+}
+
+void Session::apply_removes(const std::vector<FileInfo>& files) {
+  std::lock_guard<std::mutex> ig(index_.mu);
+  logf(strfmt("[Upstream] Handling %zu removes", files.size()));
+  std::lock_guard<std::mutex> sg(up_shell_mu_);
+  for (size_t i = 0; i < files.size(); i += 50) {
+    std::vector<std::string> args;
+    std::string helper_payload;
+    for (size_t j = 0; j < 50 && i + j < files.size(); ++j) {
+      const std::string& rel = files[i + j].name;
+      FileInfo* f = index_.find(rel);
+      if (!f) continue;
+      args.push_back(shell_quote(dest_ + rel));
+      helper_payload += rel + "\n";
+      if (f->is_dir)
+        index_.remove_dir(rel);
+      else
+        index_.files.erase(rel);
+      if (o_.verbose || files.size() <= 3) logf("[Upstream] Remove " + rel);
+    }
+    if (args.empty()) continue;
+    if (up_helper_) {
+      if (!write_all(up_shell_->in(), frame('R', helper_payload))) throw SyncError("upstream: write failed");
+      wait_ack(up_out_, "OK", false);
+    } else if (mode_ == Mode::Compat) {
+      std::string cmd = "rm -R " + join(args, " ") + "  >/dev/null 2>/dev/null && printf \"" + kDone +
+                        "\" || printf \"" + kDone + "\"\n";
+      if (!write_all(up_shell_->in(), cmd)) throw SyncError("upstream: write failed");
+      wait_ack(up_out_, kDone, true);
+    } else {
+      std::string cmd = "rm -R " + join(args, " ") + " >/dev/null 2>&1; echo " + kDone + "\n";
+      if (!write_all(up_shell_->in(), cmd)) throw SyncError("upstream: write failed");
+      wait_ack(up_out_, kDone, false);
+    }
+  }
+}
+
+void Session::recursive_tar(const std::string& rel, std::map<std::string, FileInfo>* written, TarWriter* tw,
+                            int depth) {
+  if (depth > 64 || written->count(rel)) return;
+  bool excluded = false;
+  {
+    std::lock_guard<std::mutex> g(index_.mu);
+    if (has_ignore_ && ignore_.matches(rel)) excluded = true;
+    if (has_upload_ignore_ && upload_ignore_.matches(rel)) excluded = true;
+  }
+  if (excluded) return;
+  std::string abs = o_.watch_path + rel;
+  fs::StatInfo st = fs::stat(abs);  // follows symlinks like the reference (os.Stat)
+  if (!st.exists) {
+    logf("[Upstream] Couldn't stat file " + abs);
+    return;
+  }
+  FileInfo fi;
+  fi.name = rel;
+  fi.size = st.size;
+  fi.mtime = st.mtime_rounded();
+  fi.is_dir = st.is_dir;
+  uint32_t mode = st.mode & 07777;
+  uint32_t uid = st.uid, gid = st.gid;
+  {
+    std::lock_guard<std::mutex> g(index_.mu);
+    if (FileInfo* known = index_.find(rel)) {
+      fi.remote_mode = known->remote_mode;
+      fi.remote_uid = known->remote_uid;
+      fi.remote_gid = known->remote_gid;
+      fi.has_remote_attrs = known->has_remote_attrs;
+      if (known->has_remote_attrs) {
+        mode = (uint32_t)known->remote_mode;
+        uid = (uint32_t)known->remote_uid;
+        gid = (uint32_t)known->remote_gid;
+      }
+    }
+  }
+  std::string name = rel.empty() ? "" : rel.substr(1);
+  if (st.is_dir) {
+    auto entries = fs::list_dir(abs);
+    if (entries.empty() && !rel.empty()) {
+      TarEntry e;
+      e.name = name;
+      e.mode = mode;
+      e.uid = uid;
+      e.gid = gid;
+      e.mtime = st.mtime_sec;
+      tw->add_dir(e);
+      (*written)[rel] = fi;
+    }
+    for (auto& e : entries) recursive_tar(rel + "/" + e.name, written, tw, depth + 1);
+    return;
+  }
+  TarEntry e;
+  e.name = name;
+  e.mode = mode;
+  e.uid = uid;
+  e.gid = gid;
+  e.size = st.size;
+  e.mtime = st.mtime_sec;
+  if (!tw->add_file_from_path(e, abs)) {
+    logf("[Upstream] Couldn't read file " + abs);
+    return;
+  }
+  (*written)[rel] = fi;
+}
+
+std::string Session::build_archive(const std::vector<FileInfo>& files, std::map<std::string, FileInfo>* written) {
+  std::string out;
+  int level = mode_ == Mode::Compat ? 6 : 1;
+  GzipWriter gz(string_sink(&out), level);
+  TarWriter tw([&](const char* d, size_t n) { return gz.write(d, n); });
+  for (auto& f : files)
+    if (!written->count(f.name)) recursive_tar(f.name, written, &tw, 0);
+  tw.finish();
+  gz.finish();
+  return out;
+}
+
+void Session::upload_archive(const std::string& archive) {
+  const std::string size = std::to_string(archive.size());
+  int fd = up_shell_->in();
+  auto send_payload = [&]() {
+    if (o_.upstream_limit > 0) {
+      RateLimiter rl(o_.upstream_limit);
+      for (size_t off = 0; off < archive.size(); off += 16384) {
+        size_t n = std::min<size_t>(16384, archive.size() - off);
+        rl.take(n);
+        if (!write_all(fd, archive.data() + off, n)) throw SyncError("upstream: write failed");
+      }
+    } else if (!write_all(fd, archive)) {
+      throw SyncError("upstream: write failed");
+    }
+  };
+  if (up_helper_) {
+    if (o_.upstream_limit > 0) {
+      std::string hdr = frame('U', "");
+      hdr.resize(1);
+      put_u32(hdr, (uint32_t)archive.size());
+      if (!write_all(fd, hdr)) throw SyncError("upstream: write failed");
+      send_payload();
+    } else if (!write_all(fd, frame('U', archive))) {
+      throw SyncError("upstream: write failed");
+    }
+    std::string line;
+    long deadline = mono_us() + 120000000L;
+    while (!up_out_.read_line(&line, 200)) {
+      if (up_out_.eof() || stopping_) throw SyncError("upstream: helper stream closed");
+      if (mono_us() > deadline) throw SyncError("upstream: helper timeout");
+    }
+    if (line != "OK") throw SyncError("upstream: helper error: " + line);
+    return;
+  }
+  std::string qdest = shell_quote(dest_);
+  if (mode_ == Mode::Compat) {
+    // byte-for-byte reference protocol (sync/upstream.go:387-411)
+    std::string cmd = "fileSize=" + size + R"(;
+					tmpFile="/tmp/devspace-upstream";
+					mkdir -p /tmp;
+					mkdir -p ')" + dest_ + R"(';
+
+					pid=$$;
+					cat </proc/$pid/fd/0 >"$tmpFile" &
+					ddPid=$!;
+
+					echo "START";
+
+					while true; do
+							bytesRead=$(stat -c "%s" "$tmpFile" 2>/dev/null || printf "0");
+
+							if [ "$bytesRead" = "$fileSize" ]; then
+									kill $ddPid;
+									break;
+							fi;
+
+							sleep 0.1;
+					done;
+
+					tar xzpf "$tmpFile" -C ')" + dest_ + R"(/.' 2>/tmp/devspace-upstream-error;
+					echo "DONE";
+		)";
+    if (!write_all(fd, cmd)) throw SyncError("upstream: write failed");
+    wait_ack(up_out_, kStart, false);
+    send_payload();
+    wait_ack(up_out_, kDone, false);
+    return;
+  }
+  std::string cmd = "mkdir -p " + qdest + " && echo " + kStart + " && head -c " + size + " | tar xzpf - -C " +
+                    shell_quote(dest_ + "/.") + " 2>/tmp/devspace-upstream-error; echo " + kDone + "\n";
+  if (!write_all(fd, cmd)) throw SyncError("upstream: write failed");
+  wait_ack(up_out_, kStart, false);
+  send_payload();
+  wait_ack(up_out_, kDone, false);
+}
+
+void Session::apply_creates(const std::vector<FileInfo>& files) {
+  std::map<std::string, FileInfo> written;
+  std::string archive = build_archive(files, &written);
+  if (written.empty()) return;
+  if (o_.verbose || written.size() <= 3) {
+    for (auto& kv : written) logf((kv.second.is_dir ? "[Upstream] Create Folder " : "[Upstream] Create File ") + kv.first);
+  }
+  std::lock_guard<std::mutex> ig(index_.mu);
+  logf(strfmt("[Upstream] Upload %zu create changes (size %zu)", written.size(), archive.size()));
+  {
+    std::lock_guard<std::mutex> sg(up_shell_mu_);
+    upload_archive(archive);
+  }
+  for (auto& kv : written) {
+    index_.create_dir(fs::dirname(kv.first));
+    FileInfo f = kv.second;
+    if (FileInfo* old = index_.find(kv.first)) {
+      if (!f.has_remote_attrs && old->has_remote_attrs) {
+        f.remote_mode = old->remote_mode;
+        f.remote_uid = old->remote_uid;
+        f.remote_gid = old->remote_gid;
+        f.has_remote_attrs = true;
+      }
+    }
+    index_.files[kv.first] = f;
+  }
+  std::lock_guard<std::mutex> g(stats_mu_);
+  stats_.bytes_up += archive.size();
+}
+
+void Session::send_changes_to_upstream(std::vector<FileInfo> changes) {
+  for (size_t j = 0; j < changes.size(); j += kInitialUpstreamBatch) {
+    while (!stopping_) {
+      {
+        std::lock_guard<std::mutex> g(q_mu_);
+        if (queue_.empty()) break;
+      }
+      sleep_ms(mode_ == Mode::Compat ? 1000 : 20);
+    }
+    std::vector<FileInfo> batch;
+    {
+      std::lock_guard<std::mutex> g(index_.mu);
+      for (size_t i = j; i < j + kInitialUpstreamBatch && i < changes.size(); ++i) {
+        FileInfo* f = index_.find(changes[i].name);
+        if (!f || changes[i].mtime > f->mtime) batch.push_back(changes[i]);
+      }
+    }
+    for (auto& c : batch) {
+      UpEvent e;
+      e.has_info = true;
+      e.info = c;
+      e.abs_path = o_.watch_path + c.name;
+      push_event(e);
+    }
+  }
+}
+
+// ============================================================ initial sync
+
+void Session::diff_server_client(const std::string& abs, std::vector<FileInfo>* send,
+                                 std::map<std::string, FileInfo>* download, bool dont_send) {
+  std::string rel = abs.substr(o_.watch_path.size());
+  fs::StatInfo st = fs::stat(abs);
+  if (!st.exists) return;
+  download->erase(rel);
+  if (has_upload_ignore_ && upload_ignore_.matches(rel)) {
+    std::lock_guard<std::mutex> g(index_.mu);
+    FileInfo* f = index_.find(rel);
+    if (f && f->mtime < st.mtime_rounded()) {
+      FileInfo n;
+      n.name = rel;
+      n.mtime = st.mtime_rounded();
+      n.size = st.size;
+      n.is_dir = st.is_dir;
+      index_.files[rel] = n;
+    }
+    dont_send = true;
+  }
+  if (!dont_send) {
+    fs::StatInfo lst = fs::lstat(abs);
+    if (lst.is_symlink) {
+      auto s2 = add_symlink(rel, abs);
+      if (!s2) return;
+      st = *s2;
+      logf("Symlink at " + abs);
+    }
+  }
+  if (st.is_dir) {
+    auto entries = fs::list_dir(abs);
+    if (entries.empty() && !rel.empty() && !dont_send) {
+      bool up;
+      {
+        std::lock_guard<std::mutex> g(index_.mu);
+        up = should_upload(rel, st, true);
+      }
+      if (up) {
+        FileInfo f;
+        f.name = rel;
+        f.mtime = st.mtime_rounded();
+        f.size = st.size;
+        f.is_dir = true;
+        send->push_back(f);
+      }
+    }
+    for (auto& e : entries) diff_server_client(abs + "/" + e.name, send, download, dont_send);
+    return;
+  }
+  if (!dont_send) {
+    bool up;
+    {
+      std::lock_guard<std::mutex> g(index_.mu);
+      up = should_upload(rel, st, true);
+    }
+    if (up) {
+      FileInfo f;
+      f.name = rel;
+      f.mtime = st.mtime_rounded();
+      f.size = st.size;
+      send->push_back(f);
+    }
+  }
+}
+
+std::map<std::string, FileInfo> Session::clone_index() {
+  std::lock_guard<std::mutex> g(index_.mu);
+  std::map<std::string, FileInfo> out;
+  for (auto& kv : index_.files) {
+    if (kv.second.is_symlink) continue;
+    FileInfo f;
+    f.name = kv.second.name;
+    f.size = kv.second.size;
+    f.mtime = kv.second.mtime;
+    f.is_dir = kv.second.is_dir;
+    out[kv.first] = f;
+  }
+  return out;
+}
+
+void Session::initial_sync() {
+  // populate the index from the remote tree (downstream.go:84)
+  auto creates = collect_changes(nullptr);
+  {
+    std::lock_guard<std::mutex> g(index_.mu);
+    for (auto& f : creates)
+      if (!index_.files.count(f.name)) index_.files[f.name] = f;
+  }
+  std::vector<FileInfo> local_changes;
+  auto remote_only = clone_index();
+  diff_server_client(o_.watch_path, &local_changes, &remote_only, false);
+  if (!local_changes.empty()) send_changes_to_upstream(std::move(local_changes));
+  if (!remote_only.empty()) {
+    std::vector<FileInfo> dl;
+    for (auto& kv : remote_only) dl.push_back(kv.second);
+    std::map<std::string, FileInfo> none;
+    apply_downstream(dl, none);
+  }
+}
+
+// ============================================================ downstream
+
+std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* removes) {
+  std::vector<FileInfo> creates;
+  bool dest_found = false;
+  std::lock_guard<std::mutex> sg(down_shell_mu_);
+  std::string qd = shell_quote(dest_);
+  if (down_helper_) {
+    if (!write_all(down_shell_->in(), frame('S', ""))) throw SyncError("downstream: write failed");
+  } else if (mode_ == Mode::Compat) {
+    std::string cmd = "mkdir -p '" + dest_ + "' && find -L '" + dest_ +
+                      "' -exec stat -c \"%n///%s,%Y,%f,%a,%u,%g\" {} + 2>/dev/null && echo -n \"" + kDone +
+                      "\" || echo -n \"" + kError + "\"\n";
+    if (!write_all(down_shell_->in(), cmd)) throw SyncError("downstream: write failed");
+  } else {
+    std::string cmd = "mkdir -p " + qd + " && find -L " + qd +
+                      " -exec stat -c '%n///%s,%Y,%f,%a,%u,%g' {} + 2>/dev/null && echo " + kDone + " || echo " +
+                      kError + "\n";
+    if (!write_all(down_shell_->in(), cmd)) throw SyncError("downstream: write failed");
+  }
+  RateLimiter rl(o_.downstream_limit);
+  long deadline = mono_us() + 300000000L;
+  bool partial_ok = mode_ == Mode::Compat && !down_helper_;
+  while (true) {
+    std::string line;
+    if (!down_out_.read_line(&line, 200)) {
+      if (down_out_.eof()) throw SyncError("\n[Downstream] Stream closed unexpectedly");
+      if (stopping_) throw SyncError("sync stopped");
+      if (partial_ok) {
+        std::string rest = down_out_.take_buffer();
+        if (rest == kDone) break;
+        if (rest == kError) {
+          sleep_ms(4000);
+          return collect_changes(removes);
+        }
+        // put back partial data
+        if (!rest.empty()) {
+          // no-op: the remaining buffer is an incomplete line; re-append by reading more
+          std::string more;
+          while (!down_out_.read_line(&more, 200)) {
+            if (down_out_.eof()) throw SyncError("\n[Downstream] Stream closed unexpectedly");
+            std::string r2 = down_out_.take_buffer();
+            rest += r2;
+            if (rest == kDone || rest == kError) break;
+          }
+          if (rest == kDone) break;
+          if (rest == kError) {
+            sleep_ms(4000);
+            return collect_changes(removes);
+          }
+          line = rest + more;
+        } else {
+          if (mono_us() > deadline) throw SyncError("downstream: scan timeout");
+          continue;
+        }
+      } else {
+        if (mono_us() > deadline) throw SyncError("downstream: scan timeout");
+        continue;
+      }
+    }
+    if (o_.downstream_limit > 0) rl.take(line.size() + 1);
+    if (line == kDone) break;
+    if (line == kError) {
+      sleep_ms(4000);
+      return collect_changes(removes);
+    }
+    if (line.empty()) continue;
+    // compat acks have no newline: a "DONE" may be glued to nothing else, handled above
+    std::optional<FileInfo> fi;
+    try {
+      fi = parse_file_line(line, dest_);
+    } catch (const SyncError&) {
+      if (ends_with(line, kDone) && line.find("///") == std::string::npos) break;
+      throw;
+    }
+    if (!fi) {
+      dest_found = true;
+      continue;
+    }
+    std::lock_guard<std::mutex> ig(index_.mu);
+    if (removes) removes->erase(fi->name);
+    if (FileInfo* known = index_.find(fi->name)) {
+      known->remote_mode = fi->remote_mode;
+      known->remote_uid = fi->remote_uid;
+      known->remote_gid = fi->remote_gid;
+      known->has_remote_attrs = true;
+    }
+    if (fi->is_symlink) index_.files[fi->name] = *fi;
+    if (should_download(*fi)) creates.push_back(*fi);
+  }
+  if (!dest_found) throw SyncError("DestPath not found, find command did not execute correctly");
+  return creates;
+}
+
+std::string Session::download_files(const std::vector<FileInfo>& files) {
+  int64_t total = 0;
+  for (auto& f : files) total += f.size;
+  if (files.size() > 3) logf(strfmt("[Downstream] Download %zu files (size: %lld)", files.size(), (long long)total));
+  std::string list;
+  for (auto& f : files) {
+    if (files.size() <= 3 || o_.verbose)
+      logf(strfmt("[Downstream] Download file %s, size: %lld", f.name.c_str(), (long long)f.size));
+    list += dest_ + f.name + "\n";
+  }
+  std::string archive;
+  std::lock_guard<std::mutex> sg(down_shell_mu_);
+  int fd = down_shell_->in();
+  if (down_helper_) {
+    std::string rels;
+    for (auto& f : files) rels += f.name + "\n";
+    if (!write_all(fd, frame('D', rels))) throw SyncError("downstream: write failed");
+    std::string line;
+    long deadline = mono_us() + 120000000L;
+    while (!down_out_.read_line(&line, 200)) {
+      if (down_out_.eof() || stopping_) throw SyncError("downstream: helper stream closed");
+      if (mono_us() > deadline) throw SyncError("downstream: helper timeout");
+    }
+    if (!starts_with(line, "SIZE ")) throw SyncError("downstream: helper error: " + line);
+    int64_t n = std::atoll(line.substr(5).c_str());
+    if (!down_out_.read_exact(&archive, (size_t)n, 120000)) throw SyncError("downstream: short read");
+    return archive;
+  }
+  if (mode_ == Mode::Compat) {
+    std::string cmd = "fileSize=" + std::to_string(list.size()) + R"(;
+					tmpFileInput="/tmp/devspace-downstream-input";
+					tmpFileOutput="/tmp/devspace-downstream-output";
+					mkdir -p /tmp;
+
+					pid=$$;
+					cat </proc/$pid/fd/0 >"$tmpFileInput" &
+					ddPid=$!;
+
+					echo "START";
+
+					while true; do
+							bytesRead=$(stat -c "%s" "$tmpFileInput" 2>/dev/null || printf "0");
+
+							if [ "$bytesRead" = "$fileSize" ]; then
+									kill $ddPid;
+									break;
+							fi;
+
+							sleep 0.1;
+					done;
+					tar -czf "$tmpFileOutput" -T "$tmpFileInput" 2>/tmp/devspace-downstream-error;
+					(>&2 echo "START");
+					(>&2 echo $(stat -c "%s" "$tmpFileOutput"));
+					(>&2 echo "DONE");
+					cat "$tmpFileOutput";
+		)";
+    if (!write_all(fd, cmd)) throw SyncError("downstream: write failed");
+    wait_ack(down_out_, kStart, false);
+    if (!write_all(fd, list)) throw SyncError("downstream: write failed");
+    std::string before;
+    wait_ack(down_err_, kDone, false, &before);
+    auto lines = split(trim(before), "\n");
+    if (lines.empty()) throw SyncError("[Downstream] Cannot find size");
+    int64_t n = std::atoll(lines.back().c_str());
+    if (n == 0) throw SyncError("[Downstream] Empty tar");
+    if (!down_out_.read_to(
+            (size_t)n,
+            [&](const char* d, size_t k) {
+              archive.append(d, k);
+              return true;
+            },
+            120000, o_.downstream_limit))
+      throw SyncError("[Downstream] Downloaded tar has wrong filesize");
+    return archive;
+  }
+  // fast POSIX: relative member names via -C, size line then payload on stdout
+  std::vector<std::string> args;
+  for (auto& f : files) args.push_back(shell_quote("." + f.name));
+  std::string cmd = "f=/tmp/devspace-downstream-$$; tar -czf \"$f\" -C " + shell_quote(dest_) + " -- " +
+                    join(args, " ") + " 2>/tmp/devspace-downstream-error; echo \"SIZE $(stat -c %s \"$f\" 2>/dev/null || echo 0)\"; cat \"$f\"; rm -f \"$f\"\n";
+  if (!write_all(fd, cmd)) throw SyncError("downstream: write failed");
+  std::string line;
+  long deadline = mono_us() + 120000000L;
+  while (!down_out_.read_line(&line, 200)) {
+    if (down_out_.eof() || stopping_) throw SyncError("downstream: stream closed");
+    if (mono_us() > deadline) throw SyncError("downstream: timeout");
+  }
+  if (!starts_with(line, "SIZE ")) throw SyncError("downstream: unexpected reply: " + line);
+  int64_t n = std::atoll(line.substr(5).c_str());
+  if (n == 0) throw SyncError("[Downstream] Empty tar");
+  if (!down_out_.read_to(
+          (size_t)n,
+          [&](const char* d, size_t k) {
+            archive.append(d, k);
+            return true;
+          },
+          120000, o_.downstream_limit))
+    throw SyncError("[Downstream] Downloaded tar has wrong filesize");
+  return archive;
+}
+
+void Session::untar_all(const std::string& archive) {
+  GzipReader gz(string_source(&archive));
+  TarReader tr([&](char* b, size_t n) { return gz.read(b, n); });
+  TarEntry e;
+  int count = 0;
+  while (true) {
+    std::lock_guard<std::mutex> ig(index_.mu);
+    if (!tr.next(&e)) break;
+    std::string name = e.name;
+    if (starts_with(name, "./")) name = name.substr(1);
+    if (!starts_with(name, "/")) name = "/" + name;
+    std::string rel = name;
+    // compat archives carry absolute container paths (tar strips the leading "/")
+    if (starts_with(rel, dest_ + "/") || rel == dest_) rel = rel.substr(dest_.size());
+    if (!rel.empty() && rel.back() == '/') rel.pop_back();
+    if (rel.empty()) continue;
+    std::string out = o_.watch_path + rel;
+    fs::StatInfo st = fs::stat(out);
+    if (st.exists && st.mtime_rounded() > e.mtime) {
+      FileInfo f;
+      f.name = rel;
+      f.mtime = st.mtime_rounded();
+      f.size = st.size;
+      f.is_dir = st.is_dir;
+      index_.files[rel] = f;
+      logf("[Downstream] Don't override " + rel + " because file has newer mTime timestamp");
+      tr.skip();
+      continue;
+    }
+    fs::mkdirs(fs::dirname(out));
+    if (e.type == '5') {
+      fs::mkdirs(out);
+      index_.create_dir(rel);
+      continue;
+    }
+    if (e.type != '0' && e.type != '7') {
+      tr.skip();
+      continue;
+    }
+    index_.create_dir(fs::dirname(rel));
+    std::string data = tr.read_all();
+    try {
+      fs::write_file(out, data, (int)(e.mode & 07777 ? e.mode & 07777 : 0644));
+    } catch (...) {
+      sleep_ms(mode_ == Mode::Compat ? 5000 : 200);  // retry once (tar.go:97)
+      fs::write_file(out, data, 0644);
+    }
+    if (st.exists) ::chmod(out.c_str(), st.mode & 07777);
+    fs::set_mtime(out, e.mtime, 0);
+    FileInfo f;
+    f.name = rel;
+    f.mtime = e.mtime;
+    f.size = (int64_t)data.size();
+    index_.files[rel] = f;
+    if (++count % 500 == 0) logf(strfmt("[Downstream] Untared %d files...", count));
+  }
+}
+
+void Session::delete_safe_recursive(const std::string& rel, std::map<std::string, FileInfo>& removes) {
+  std::string abs = o_.watch_path + rel;
+  if (!index_.find(rel) || !removes.count(rel)) {
+    logf("[Downstream] Skip delete directory " + rel);
+    return;
+  }
+  for (auto& e : fs::list_dir(abs)) {
+    std::string child = rel + "/" + e.name;
+    FileInfo* f = index_.find(child);
+    if (f) {
+      FileInfo copy = *f;
+      if (should_remove_local(abs + "/" + e.name, copy)) {
+        if (e.is_dir && !e.is_symlink)
+          delete_safe_recursive(child, removes);
+        else if (!fs::remove(abs + "/" + e.name))
+          logf("[Downstream] Skip file delete " + child);
+      } else {
+        logf("[Downstream] Skip delete " + child);
+      }
+    } else {
+      logf("[Downstream] Skip delete " + child);
+    }
+    index_.files.erase(child);
+  }
+  if (::rmdir(abs.c_str()) != 0) logf("[Downstream] Skip delete directory " + rel + ", because it is not empty");
+  index_.files.erase(rel);
+}
+
+void Session::remove_files_and_folders(std::map<std::string, FileInfo>& removes) {
+  std::lock_guard<std::mutex> ig(index_.mu);
+  if (removes.size() > 3) logf(strfmt("[Downstream] Remove %zu files", removes.size()));
+  for (auto& kv : removes) {
+    std::string abs = o_.watch_path + kv.first;
+    if (should_remove_local(abs, kv.second)) {
+      if (removes.size() <= 3 || o_.verbose) logf("[Downstream] Remove " + kv.first);
+      if (kv.second.is_dir)
+        delete_safe_recursive(kv.first, removes);
+      else if (!fs::remove(abs) && fs::exists(abs))
+        logf("[Downstream] Skip file delete " + kv.first);
+    }
+    index_.files.erase(kv.first);
+  }
+}
+
+void Session::create_folders(const std::vector<FileInfo>& dirs) {
+  std::lock_guard<std::mutex> ig(index_.mu);
+  if (dirs.size() > 3) logf(strfmt("[Downstream] Create %zu folders", dirs.size()));
+  for (auto& d : dirs) {
+    if (dirs.size() <= 3 || o_.verbose) logf("[Downstream] Create folder: " + d.name);
+    fs::mkdirs(o_.watch_path + d.name);
+    if (!index_.find(d.name)) index_.create_dir(d.name);
+  }
+}
+
+void Session::apply_downstream(const std::vector<FileInfo>& creates, std::map<std::string, FileInfo>& removes) {
+  std::vector<FileInfo> files, dirs;
+  for (auto& c : creates) (c.is_dir ? dirs : files).push_back(c);
+  std::string archive;
+  if (!files.empty()) {
+    // batch very long lists (argv limits in fast mode)
+    if (mode_ != Mode::Compat && !down_helper_ && files.size() > 500) {
+      for (size_t i = 0; i < files.size(); i += 500) {
+        std::vector<FileInfo> part(files.begin() + i, files.begin() + std::min(files.size(), i + 500));
+        std::string a = download_files(part);
+        untar_all(a);
+        std::lock_guard<std::mutex> g(stats_mu_);
+        stats_.bytes_down += a.size();
+      }
+    } else {
+      archive = download_files(files);
+    }
+  }
+  remove_files_and_folders(removes);
+  create_folders(dirs);
+  if (!archive.empty()) {
+    untar_all(archive);
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.bytes_down += archive.size();
+  }
+  logf(strfmt("[Downstream] Successfully processed %zu change(s)", creates.size() + removes.size()));
+  std::lock_guard<std::mutex> g(stats_mu_);
+  stats_.downstream_batches++;
+  stats_.downstream_changes += creates.size() + removes.size();
+}
+
+void Session::downstream_loop() {
+  size_t last_amount = 0;
+  while (!stopping_ && !failed_) {
+    auto removes = clone_index();
+    std::vector<FileInfo> creates;
+    try {
+      creates = collect_changes(&removes);
+      size_t amount = creates.size() + removes.size();
+      bool apply;
+      if (down_helper_)
+        apply = amount > 0;  // event-driven: the helper only signals after writes settle
+      else
+        apply = last_amount > 0 && amount == last_amount;  // stability rule (downstream.go:117)
+      if (apply) apply_downstream(creates, removes);
+      last_amount = amount;
+    } catch (const std::exception& e) {
+      fail(e.what());
+      return;
+    }
+    // wait for the next poll (or a container-side event in helper mode)
+    long until = mono_us() + (long)poll_ms_ * 1000;
+    while (!stopping_ && !failed_ && mono_us() < until) {
+      if (down_helper_) {
+        std::string ev;
+        if (down_err_.read_line(&ev, 50)) {
+          if (ev == "E") {
+            // coalesce bursts of events
+            while (down_err_.read_line(&ev, 15)) {
+            }
+            break;
+          }
+        } else if (down_err_.eof()) {
+          fail("downstream: helper event stream closed");
+          return;
+        }
+      } else {
+        sleep_ms(std::min<int>(50, poll_ms_));
+      }
+    }
+  }
+}
+
+// ============================================================ lifecycle
+
+void Session::start_loops(bool upstream, bool downstream) {
+  if (upstream) up_thread_ = std::thread([this] { upstream_loop(); });
+  if (downstream) down_thread_ = std::thread([this] { downstream_loop(); });
+}
+
+void Session::fail(const std::string& err) {
+  if (stopping_) return;
+  {
+    std::lock_guard<std::mutex> g(state_mu_);
+    if (failed_) return;
+    failed_ = true;
+    pending_failure_ = err;
+  }
+  state_cv_.notify_all();
+  q_cv_.notify_all();
+}
+
+void Session::stop_loops() {
+  q_cv_.notify_all();
+  if (up_shell_) up_shell_->terminate();
+  if (down_shell_) down_shell_->terminate();
+  if (up_thread_.joinable() && up_thread_.get_id() != std::this_thread::get_id()) up_thread_.join();
+  if (down_thread_.joinable() && down_thread_.get_id() != std::this_thread::get_id()) down_thread_.join();
+  if (up_shell_) up_shell_->close();
+  if (down_shell_) down_shell_->close();
+}
+
+void Session::supervise() {
+  // initial sync + downstream run on their own thread; the supervisor handles failures.
+  auto run_initial = [this]() -> bool {
+    try {
+      initial_sync();
+      logf("[Sync] Initial sync completed");
+      {
+        std::lock_guard<std::mutex> g(state_mu_);
+        initial_done_ = true;
+      }
+      state_cv_.notify_all();
+      if (o_.on_initial_sync_done) o_.on_initial_sync_done();
+      return true;
+    } catch (const std::exception& e) {
+      fail(e.what());
+      return false;
+    }
+  };
+  logf("[Sync] Start syncing");
+  up_thread_ = std::thread([this] { upstream_loop(); });
+  down_thread_ = std::thread([this, run_initial] {
+    if (run_initial()) downstream_loop();
+  });
+  while (true) {
+    std::string err;
+    {
+      std::unique_lock<std::mutex> lk(state_mu_);
+      state_cv_.wait(lk, [this] { return stopping_ || failed_; });
+      if (stopping_) return;
+      err = pending_failure_;
+    }
+    log_error("Error: " + err);
+    bool can_reconnect = mode_ != Mode::Compat && o_.reconnect && reconnects_ < o_.max_reconnects;
+    if (!can_reconnect) {
+      {
+        std::lock_guard<std::mutex> g(state_mu_);
+        error_ = err;
+      }
+      running_ = false;
+      if (o_.on_error) o_.on_error(err);
+      state_cv_.notify_all();
+      return;
+    }
+    ++reconnects_;
+    {
+      std::lock_guard<std::mutex> g(stats_mu_);
+      stats_.reconnects++;
+    }
+    logf(strfmt("[Sync] Stream failed (%s), reconnecting (attempt %d)", err.c_str(), reconnects_));
+    stop_loops();
+    sleep_ms(std::min(200 * reconnects_, 2000));
+    try {
+      auto t = o_.reconnect();
+      if (!t) throw SyncError("no pod available");
+      transport_ = t;
+      dest_ = remote(o_.dest_path);
+      open_shells();
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> g(state_mu_);
+      pending_failure_ = e.what();
+      failed_ = true;
+      continue;
+    }
+    {
+      std::lock_guard<std::mutex> g(state_mu_);
+      failed_ = false;
+      pending_failure_.clear();
+    }
+    up_thread_ = std::thread([this] { upstream_loop(); });
+    down_thread_ = std::thread([this, run_initial] {
+      if (run_initial()) downstream_loop();
+    });
+  }
+}
+
+void Session::start() {
+  setup();
+  open_shells();
+  start_watcher();
+  running_ = true;
+  supervisor_ = std::thread([this] { supervise(); });
+}
+
+bool Session::wait_initial_sync(int timeout_ms) {
+  std::unique_lock<std::mutex> lk(state_mu_);
+  return state_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms),
+                            [this] { return initial_done_ || !error_.empty(); }) &&
+         initial_done_;
+}
+
+std::string Session::error() {
+  std::lock_guard<std::mutex> g(state_mu_);
+  return error_;
+}
+
+Stats Session::stats() {
+  std::lock_guard<std::mutex> g(stats_mu_);
+  return stats_;
+}
+
+void Session::stop(const std::string& fatal_error) {
+  if (stopping_.exchange(true)) return;
+  {
+    std::lock_guard<std::mutex> g(state_mu_);
+    if (!fatal_error.empty()) error_ = fatal_error;
+  }
+  state_cv_.notify_all();
+  q_cv_.notify_all();
+  {
+    std::lock_guard<std::mutex> g(symlink_mu_);
+    for (auto& kv : symlinks_) kv.second->stop();
+    symlinks_.clear();
+  }
+  if (watcher_) watcher_->stop();
+  if (supervisor_.joinable()) supervisor_.join();
+  stop_loops();
+  running_ = false;
+  logf("[Sync] Sync stopped");
+  if (!fatal_error.empty()) log_error("Error: " + fatal_error);
+}
+
+// ============================================================ one-shot copy
+
+void Session::copy_to_container(std::shared_ptr<Transport> t, const std::string& local_path,
+                                const std::string& container_path, std::vector<std::string> excludes, Mode mode) {
+  fs::StatInfo st = fs::lstat(local_path);
+  if (!st.exists) throw SyncError("lstat " + local_path + ": no such file or directory");
+  std::string root = local_path;
+  if (!st.is_dir) {
+    root = fs::dirname(local_path);
+    for (auto& e : fs::list_dir(root))
+      if (fs::join(root, e.name) != local_path) excludes.push_back("/" + e.name);
+  }
+  Options o;
+  o.watch_path = root;
+  o.dest_path = container_path;
+  o.exclude_paths = excludes;
+  o.silent = true;
+  o.mode = mode == Mode::Helper ? Mode::Fast : mode;
+  Session s(o, t);
+  s.setup();
+  s.open_up_shell();
+  FileInfo rootinfo;
+  rootinfo.name = "";
+  rootinfo.is_dir = true;
+  rootinfo.mtime = 1;
+  s.apply_creates({rootinfo});
+  s.stopping_ = true;
+  if (s.up_shell_) s.up_shell_->close();
+}
+
+}  // namespace sync
+}  // namespace ds

@@ -1,0 +1,227 @@
+// Bidirectional local <-> container file sync (the reference's hot path, sync/*.go).
+//
+// Same decision rules as the reference (Appendix A of SURVEY.md: sync/evaluater.go,
+// sync/tar.go untar rules, sync/file_index.go bookkeeping) with three wire protocols:
+//   Mode::Compat — byte-for-byte the reference's POSIX scripts and timing constants
+//                  (600 ms upload window, 1300 ms downstream poll + stability rule,
+//                  `sleep 0.1` receive polling). Used as the reference-equivalent baseline.
+//   Mode::Fast   — POSIX-only but streamed: inotify + ~15 ms coalescing, `head -c N | tar x`
+//                  (no temp files / polling), newline acks, 250 ms downstream poll.
+//   Mode::Helper — uploads a static helper (src/helper) into the container that speaks a
+//                  framed binary protocol and pushes inotify events for event-driven
+//                  downstream; falls back to Fast when it cannot run.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "core/codec.h"
+#include "core/fs.h"
+#include "core/log.h"
+#include "core/match.h"
+#include "core/watch.h"
+#include "sync/transport.h"
+
+namespace ds {
+namespace sync {
+
+enum class Mode { Compat, Fast, Helper };
+Mode parse_mode(const std::string& s);  // compat|fast|helper (default fast); env DEVSPACE_SYNC_MODE
+const char* mode_name(Mode m);
+
+struct FileInfo {
+  std::string name;  // relative to the sync root, with leading "/" ("" = root)
+  int64_t size = 0;
+  int64_t mtime = 0;  // seconds (rounded for local files); 0 marks a remove change
+  bool is_dir = false;
+  bool is_symlink = false;
+  int64_t remote_mode = 0;
+  int remote_uid = 0, remote_gid = 0;
+  bool has_remote_attrs = false;
+};
+
+// Parses one `stat -c "%n///%s,%Y,%f,%a,%u,%g"` line (sync/file_information.go:62).
+// Returns nullopt for the dest path itself; throws on malformed lines.
+std::optional<FileInfo> parse_file_line(const std::string& line, const std::string& dest_path);
+
+// Shared index of known files (sync/file_index.go). Ordered so subtree removal is
+// O(log n + k) instead of the reference's O(n) scan.
+class FileIndex {
+ public:
+  std::mutex mu;
+  std::map<std::string, FileInfo> files;
+  FileInfo* find(const std::string& name) {
+    auto it = files.find(name);
+    return it == files.end() ? nullptr : &it->second;
+  }
+  // Adds every ancestor directory of dirpath (lock held by caller).
+  void create_dir(const std::string& dirpath);
+  // Removes dirpath and its subtree (lock held by caller).
+  void remove_dir(const std::string& dirpath);
+};
+
+struct Options {
+  std::string watch_path;      // local directory
+  std::string dest_path;       // container path (logical, e.g. /app)
+  std::string pod_name;        // for log context
+  std::vector<std::string> exclude_paths, download_exclude_paths, upload_exclude_paths;
+  int64_t upstream_limit = 0;    // bytes/s
+  int64_t downstream_limit = 0;  // bytes/s
+  bool verbose = false;
+  bool silent = false;  // no sync.log entries (CopyToContainer)
+  Mode mode = Mode::Fast;
+  std::string helper_path;  // static helper binary (Mode::Helper)
+  // Timing knobs (defaults depend on mode; <0 = mode default)
+  int upstream_window_ms = -1;
+  int downstream_poll_ms = -1;
+  // Reconnect: when set, a dead stream triggers a transport refresh (e.g. pick the newest
+  // running pod again) instead of a fatal stop (the reference log.Fatalf's, sync_config.go:481).
+  std::function<std::shared_ptr<Transport>()> reconnect;
+  int max_reconnects = 10;
+  std::function<void(const std::string&)> on_error;
+  std::function<void()> on_initial_sync_done;
+  std::string sync_log_name = "sync";
+};
+
+struct Stats {
+  uint64_t upstream_batches = 0, upstream_changes = 0;
+  uint64_t downstream_batches = 0, downstream_changes = 0;
+  uint64_t reconnects = 0;
+  double last_upload_ms = 0;  // first event -> remote ack
+  uint64_t bytes_up = 0, bytes_down = 0;
+};
+
+class Session {
+ public:
+  Session(Options opts, std::shared_ptr<Transport> transport);
+  ~Session();
+  Session(const Session&) = delete;
+
+  void start();  // setup + shells + watcher + threads (initial sync runs asynchronously)
+  void stop(const std::string& fatal_error = "");
+  bool wait_initial_sync(int timeout_ms);
+  bool running() const { return running_; }
+  std::string error();
+  Stats stats();
+  const Options& options() const { return o_; }
+  Mode effective_mode() const { return mode_; }
+
+  // --- pieces exposed for tests (the reference tests drive setup/initialSync directly)
+  void setup();
+  void open_shells();
+  void start_watcher();
+  void initial_sync();
+  void start_loops(bool upstream, bool downstream);
+  FileIndex& index() { return index_; }
+
+  // One-shot upload of a local folder/file (sync/util.go:21 CopyToContainer).
+  static void copy_to_container(std::shared_ptr<Transport> t, const std::string& local_path,
+                                const std::string& container_path, std::vector<std::string> excludes,
+                                Mode mode = Mode::Fast);
+
+ private:
+  struct UpEvent {
+    std::string abs_path;
+    bool has_info = false;
+    FileInfo info;
+    long t_us = 0;
+  };
+
+  // logging
+  void logf(const std::string& msg);
+  void log_error(const std::string& msg);
+
+  // rules (sync/evaluater.go) — index lock held
+  bool should_remove_remote(const std::string& rel);
+  bool should_upload(const std::string& rel, const fs::StatInfo& st, bool initial);
+  bool should_download(const FileInfo& f);
+  bool should_remove_local(const std::string& abs, const FileInfo& f);
+
+  // upstream
+  void push_event(UpEvent e);
+  void upstream_loop();
+  std::optional<FileInfo> evaluate_change(const std::string& rel, const std::string& abs);
+  void apply_upstream(std::vector<FileInfo>& changes, long first_event_us);
+  void apply_removes(const std::vector<FileInfo>& removes);
+  void apply_creates(const std::vector<FileInfo>& creates);
+  std::string build_archive(const std::vector<FileInfo>& files, std::map<std::string, FileInfo>* written);
+  void recursive_tar(const std::string& rel, std::map<std::string, FileInfo>* written, TarWriter* tw, int depth);
+  bool wait_ack(LineReader& r, const std::string& keyword, bool partial, std::string* before = nullptr,
+                int timeout_ms = 120000);
+  void stop_loops();
+  void upload_archive(const std::string& archive);
+  void send_changes_to_upstream(std::vector<FileInfo> changes);
+  void diff_server_client(const std::string& abs, std::vector<FileInfo>* send,
+                          std::map<std::string, FileInfo>* download, bool dont_send);
+
+  // downstream
+  void downstream_loop();
+  std::vector<FileInfo> collect_changes(std::map<std::string, FileInfo>* removes);
+  void apply_downstream(const std::vector<FileInfo>& creates, std::map<std::string, FileInfo>& removes);
+  std::string download_files(const std::vector<FileInfo>& files);
+  void untar_all(const std::string& archive);
+  void remove_files_and_folders(std::map<std::string, FileInfo>& removes);
+  void delete_safe_recursive(const std::string& rel, std::map<std::string, FileInfo>& removes);
+  void create_folders(const std::vector<FileInfo>& dirs);
+  std::map<std::string, FileInfo> clone_index();
+
+  // symlinks (sync/symlink.go)
+  std::optional<fs::StatInfo> add_symlink(const std::string& rel, const std::string& abs);
+  void remove_symlinks(const std::string& abs);
+
+  // shells / modes
+  std::string remote(const std::string& container_path) const;  // apply transport prefix
+  void open_up_shell();
+  void open_down_shell();
+  bool start_helper(std::unique_ptr<Shell>& sh, LineReader& out);
+  void fail(const std::string& err);  // stream failure -> reconnect or stop
+  void supervise();
+
+  Options o_;
+  std::shared_ptr<Transport> transport_;
+  Mode mode_;
+  std::string dest_;  // shell-visible dest path
+  int window_ms_ = 15, poll_ms_ = 250;
+  FileIndex index_;
+  GitIgnore ignore_, download_ignore_, upload_ignore_;
+  bool has_ignore_ = false, has_download_ignore_ = false, has_upload_ignore_ = false;
+  std::shared_ptr<log::FileLogger> log_;
+
+  std::unique_ptr<Shell> up_shell_, down_shell_;
+  LineReader up_out_, down_out_, down_err_;
+  bool up_helper_ = false, down_helper_ = false;
+  std::mutex up_shell_mu_, down_shell_mu_;
+
+  std::unique_ptr<InotifyWatcher> watcher_;
+  std::map<std::string, std::unique_ptr<PollWatcher>> symlinks_;  // abs symlink path -> target watcher
+  std::map<std::string, std::string> symlink_targets_;
+  std::mutex symlink_mu_;
+
+  std::mutex q_mu_;
+  std::condition_variable q_cv_;
+  std::deque<UpEvent> queue_;
+
+  std::thread up_thread_, down_thread_, supervisor_;
+  std::atomic<bool> running_{false}, stopping_{false};
+  std::atomic<bool> failed_{false};
+  std::mutex state_mu_;
+  std::condition_variable state_cv_;
+  bool initial_done_ = false;
+  std::string error_;
+  Stats stats_;
+  std::mutex stats_mu_;
+  std::string pending_failure_;
+  int reconnects_ = 0;
+};
+
+}  // namespace sync
+}  // namespace ds

@@ -1,4 +1,7 @@
+#include <signal.h>
+
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <exception>
 
@@ -14,6 +17,8 @@ std::vector<Case>& registry() {
 
 int main(int argc, char** argv) {
   std::string filter = argc > 1 ? argv[1] : "";
+  signal(SIGPIPE, SIG_IGN);
+  setvbuf(stdout, nullptr, _IOLBF, 0);
   ds::log::set_fatal_throws(true);
   int pass = 0, fail = 0;
   for (auto& c : dstest::registry()) {

@@ -1,0 +1,383 @@
+// Sync engine behaviour matrix — port of sync/sync_config_test.go (TestInitialSync,
+// TestNormalSync incl. remove/rename matrix) and sync/util_test.go (TestCopyToContainerTestable),
+// run over the local-shell transport in every protocol mode.
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <regex>
+#include <thread>
+
+#include "core/fs.h"
+#include "core/log.h"
+#include "core/strutil.h"
+#include "sync/sync.h"
+#include "testing.h"
+
+using namespace ds;
+using namespace ds::sync;
+
+namespace {
+
+enum Edit { InRemote = 0, InLocal = 1, Outside = 2 };
+struct Case {
+  std::string path;
+  bool in_local;
+  bool in_remote;
+  Edit edit;
+};
+using Cases = std::vector<Case>;
+const char* kContents = "TestContents";
+
+struct Dirs {
+  std::string remote, local, outside;
+  Dirs() {
+    remote = fs::realpath(fs::make_temp_dir("remote-"));
+    local = fs::realpath(fs::make_temp_dir("local-"));
+    outside = fs::realpath(fs::make_temp_dir("outside-"));
+  }
+  ~Dirs() {
+    fs::remove_all(remote);
+    fs::remove_all(local);
+    fs::remove_all(outside);
+  }
+  std::string parent(Edit e) const { return e == InLocal ? local : e == InRemote ? remote : outside; }
+};
+
+Cases make_remote(Cases c) {
+  Cases out = c;
+  for (auto f : c) {
+    if (contains(f.path, "Upload"))
+      f.path = replace_all(f.path, "Upload", "Download");
+    else if (contains(f.path, "Download"))
+      f.path = replace_all(f.path, "Download", "Upload");
+    out.push_back({replace_all(f.path, "Local", "Remote"), f.in_remote, f.in_local, InRemote});
+  }
+  return out;
+}
+
+Cases make_deep(Cases c) {
+  Cases out = c;
+  for (auto& f : c) {
+    if (f.path == "testFolder") continue;
+    out.push_back({"testFolder/" + f.path, f.in_local, f.in_remote, f.edit});
+  }
+  return out;
+}
+
+void basic(Cases* files, Cases* folders) {
+  *files = {{"testFileLocal", true, true, InLocal},
+            {"ignoreFileLocal", true, false, InLocal},
+            {"noDownloadFileLocal", true, true, InLocal},
+            {"noUploadFileLocal", true, false, InLocal}};
+  *folders = {{"testFolder", true, true, InLocal},
+              {"testFolderLocal", true, true, InLocal},
+              {"ignoreFolderLocal", true, false, InLocal},
+              {"noDownloadFolderLocal", true, true, InLocal},
+              {"noUploadFolderLocal", true, false, InLocal}};
+  *files = make_deep(make_remote(*files));
+  *folders = make_deep(make_remote(*folders));
+}
+
+void remove_and_rename(Cases* files, Cases* folders) {
+  static const std::regex fully("(testFolder/)?(testFile|testFolder)(Local|Remote)$");
+  for (Cases* arr : {files, folders}) {
+    Cases out = *arr;
+    for (auto& f : *arr) {
+      if (f.path == "testFolder") continue;
+      out.push_back({f.path + "_Remove", f.in_local, f.in_remote, f.edit});
+      out.push_back({f.path + "_RenameToFullContext", f.in_local, f.in_remote, f.edit});
+      if (std::regex_search(f.path, fully)) {
+        for (const char* s : {"_RenameToOutside", "_RenameToIgnore", "_RenameToNoDownload", "_RenameToNoUpload"})
+          out.push_back({f.path + s, f.in_local, f.in_remote, f.edit});
+      }
+    }
+    *arr = out;
+  }
+  Cases rf = {{"testFileOutsideToLocal_RenameToFullContext", false, false, Outside},
+              {"testFileOutsideToRemote_RenameToFullContext", false, false, Outside}};
+  Cases rd = {{"testFolderOutsideToLocal_RenameToFullContext", false, false, Outside},
+              {"testFolderOutsideToRemote_RenameToFullContext", false, false, Outside},
+              {"testFolder", true, true, Outside}};
+  for (auto& c : make_deep(rf)) files->push_back(c);
+  for (auto& c : make_deep(rd)) folders->push_back(c);
+}
+
+void set_excludes(Options* o, const Cases& all) {
+  o->exclude_paths.clear();
+  o->download_exclude_paths.clear();
+  o->upload_exclude_paths.clear();
+  for (auto& c : all) {
+    if (contains(c.path, "ignore"))
+      o->exclude_paths.push_back(c.path);
+    else if (contains(c.path, "noDownload"))
+      o->download_exclude_paths.push_back(c.path);
+    else if (contains(c.path, "noUpload"))
+      o->upload_exclude_paths.push_back(c.path);
+    else if (ends_with(c.path, "_RenameToIgnore"))
+      o->exclude_paths.push_back(c.path + "After");
+    else if (ends_with(c.path, "_RenameToNoDownload"))
+      o->download_exclude_paths.push_back(c.path + "After");
+    else if (ends_with(c.path, "_RenameToNoUpload"))
+      o->upload_exclude_paths.push_back(c.path + "After");
+  }
+}
+
+void create_all(const Dirs& d, const Cases& files, const Cases& folders) {
+  for (auto& f : folders) fs::mkdirs(fs::join(d.parent(f.edit), f.path));
+  for (auto& f : files) fs::write_file(fs::join(d.parent(f.edit), f.path), kContents, 0666);
+}
+
+void remove_some(const Dirs& d, Cases* files, Cases* folders) {
+  for (auto& pair : {std::make_pair(d.remote, std::string("Remote_Remove")),
+                     std::make_pair(d.local, std::string("Local_Remove"))}) {
+    std::vector<std::string> victims;
+    fs::walk(pair.first, [&](const std::string& p, const fs::StatInfo&) {
+      if (ends_with(p, pair.second)) victims.push_back(p);
+      return true;
+    });
+    for (auto& v : victims) fs::remove_all(v);
+  }
+  for (Cases* arr : {files, folders})
+    for (auto& f : *arr)
+      if (ends_with(f.path, "_Remove")) f.in_local = f.in_remote = false;
+}
+
+void rename_some(const Dirs& d, Cases* files, Cases* folders) {
+  for (Cases* arr : {files, folders}) {
+    for (auto& f : *arr) {
+      if (!contains(f.path, "_Rename")) continue;
+      std::string from = fs::join(d.parent(f.edit), f.path);
+      std::string to_parent;
+      if (ends_with(f.path, "_RenameToOutside"))
+        to_parent = d.outside;
+      else if (contains(f.path, "Local_Rename"))
+        to_parent = d.local;
+      else if (contains(f.path, "Remote_Rename"))
+        to_parent = d.remote;
+      f.path += "After";
+      std::string to = fs::join(to_parent, f.path);
+      if (!fs::rename(from, to)) throw std::runtime_error("rename failed " + from + " -> " + to);
+      if (ends_with(f.path, "_RenameToFullContextAfter")) {
+        f.in_local = f.in_remote = true;
+      } else if (ends_with(f.path, "_RenameToNoDownloadAfter")) {
+        f.in_remote = true;
+        f.in_local = f.edit == InLocal;
+      } else if (ends_with(f.path, "_RenameToNoUploadAfter")) {
+        f.in_local = true;
+        f.in_remote = f.edit == InRemote;
+      } else if (ends_with(f.path, "_RenameToIgnoreAfter")) {
+        f.in_local = f.edit == InLocal;
+        f.in_remote = f.edit == InRemote;
+      } else if (ends_with(f.path, "_RenameToOutsideAfter")) {
+        f.in_local = f.in_remote = false;
+      }
+    }
+  }
+}
+
+std::string check_once(const Dirs& d, const Cases& files, const Cases& folders) {
+  std::string errs;
+  auto chk = [&](const Case& c, bool dir) {
+    for (int side = 0; side < 2; ++side) {
+      std::string root = side == 0 ? d.local : d.remote;
+      bool want = side == 0 ? c.in_local : c.in_remote;
+      std::string p = fs::join(root, c.path);
+      fs::StatInfo st = fs::stat(p);
+      if (want && !st.exists) errs += (side ? "remote missing " : "local missing ") + c.path + "\n";
+      if (!want && st.exists) errs += (side ? "remote unexpected " : "local unexpected ") + c.path + "\n";
+      if (want && st.exists && !dir) {
+        std::string data;
+        fs::read_file(p, &data);
+        if (data != kContents) errs += "bad contents " + p + "\n";
+      }
+      if (want && st.exists && dir != st.is_dir) errs += "wrong type " + p + "\n";
+    }
+  };
+  for (auto& f : files) chk(f, false);
+  for (auto& f : folders) chk(f, true);
+  return errs;
+}
+
+void check_eventually(const Dirs& d, const Cases& files, const Cases& folders, int timeout_ms) {
+  auto t0 = std::chrono::steady_clock::now();
+  std::string errs;
+  while (true) {
+    errs = check_once(d, files, folders);
+    if (errs.empty()) return;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) break;
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  }
+  throw dstest::Failure{"sync matrix mismatch:\n" + errs};
+}
+
+Options base_options(const Dirs& d, Mode m) {
+  Options o;
+  o.watch_path = d.local;
+  o.dest_path = d.remote;
+  o.verbose = true;
+  o.mode = m;
+  o.helper_path = fs::join(fs::dirname(fs::realpath("/proc/self/exe")), "devspace-helper");
+  o.sync_log_name = "sync-test";
+  return o;
+}
+
+void run_initial(Mode m) {
+  log::logdir() = fs::make_temp_dir("synclogs-");
+  Dirs d;
+  Cases files, folders;
+  basic(&files, &folders);
+  Options o = base_options(d, m);
+  Cases all = files;
+  all.insert(all.end(), folders.begin(), folders.end());
+  set_excludes(&o, all);
+  Session s(o, std::make_shared<LocalShellTransport>());
+  s.setup();
+  s.open_shells();
+  create_all(d, files, folders);
+  s.start_watcher();
+  s.start_loops(true, false);
+  s.initial_sync();
+  check_eventually(d, files, folders, 10000);
+  s.stop();
+}
+
+void run_normal(Mode m) {
+  log::logdir() = fs::make_temp_dir("synclogs-");
+  Dirs d;
+  Cases files, folders;
+  basic(&files, &folders);
+  remove_and_rename(&files, &folders);
+  std::stable_sort(folders.begin(), folders.end(),
+                   [](const Case& a, const Case& b) { return a.path.size() < b.path.size(); });
+  Options o = base_options(d, m);
+  Cases all = files;
+  all.insert(all.end(), folders.begin(), folders.end());
+  set_excludes(&o, all);
+  Session s(o, std::make_shared<LocalShellTransport>());
+  s.start();
+  EXPECT_TRUE(s.wait_initial_sync(15000));
+  create_all(d, files, folders);
+  check_eventually(d, files, folders, 15000);
+  remove_some(d, &files, &folders);
+  check_eventually(d, files, folders, 15000);
+  rename_some(d, &files, &folders);
+  check_eventually(d, files, folders, 25000);
+  EXPECT_TRUE(s.running());
+  s.stop();
+}
+
+}  // namespace
+
+TEST(sync_file_index) {
+  // TestCreateDirInFileMap / TestRemoveDirInFileMap
+  FileIndex idx;
+  idx.create_dir("/TestDir1/TestDir2/TestDir3/TestDir4");
+  EXPECT_EQ(idx.files.size(), (size_t)4);
+  FileIndex idx2;
+  FileInfo a;
+  a.name = "/TestDir";
+  a.is_dir = true;
+  idx2.files[a.name] = a;
+  FileInfo b;
+  b.name = "/TestDir/File1";
+  b.size = 1234;
+  b.mtime = 1234;
+  idx2.files[b.name] = b;
+  FileInfo c;
+  c.name = "/TestDir2";
+  c.is_dir = true;
+  idx2.files[c.name] = c;
+  idx2.remove_dir("/TestDir");
+  EXPECT_EQ(idx2.files.size(), (size_t)1);
+}
+
+TEST(sync_parse_file_line) {
+  auto f = parse_file_line("/app/src/a.js///12,1500000000,81a4,644,0,0", "/app");
+  EXPECT_TRUE(f.has_value());
+  EXPECT_EQ(f->name, std::string("/src/a.js"));
+  EXPECT_EQ(f->size, (int64_t)12);
+  EXPECT_TRUE(!f->is_dir);
+  EXPECT_EQ(f->remote_mode, (int64_t)0644);
+  auto d = parse_file_line("/app/src///4096,1500000000,41ed,755,1000,1000", "/app");
+  EXPECT_TRUE(d->is_dir);
+  EXPECT_TRUE(!parse_file_line("/app///4096,1,41ed,755,0,0", "/app").has_value());
+  EXPECT_THROWS(parse_file_line("garbage", "/app"));
+}
+
+TEST(sync_copy_to_container) {
+  Dirs d;
+  fs::write_file(fs::join(d.local, "testFile1"), kContents);
+  fs::write_file(fs::join(d.local, "testFile2"), kContents);
+  fs::write_file(fs::join(d.local, "ignoredFile"), kContents);
+  fs::mkdirs(fs::join(d.local, "testFolder"));
+  fs::mkdirs(fs::join(d.local, "testFolder2"));
+  fs::mkdirs(fs::join(d.local, "ignoredFolder"));
+  fs::write_file(fs::join(d.local, "testFolder/testFile1"), kContents);
+  fs::write_file(fs::join(d.local, "testFolder/testFile2"), kContents);
+  fs::write_file(fs::join(d.local, "testFolder/ignoredFile"), kContents);
+  fs::write_file(fs::join(d.local, "ignoredFolder/testFile1"), kContents);
+  for (Mode m : {Mode::Compat, Mode::Fast}) {
+    fs::remove_all(d.remote);
+    fs::mkdirs(d.remote);
+    Session::copy_to_container(std::make_shared<LocalShellTransport>(), d.local, d.remote,
+                               {"ignoredFile", "ignoredFolder", "testFolder/ignoredFile"}, m);
+    Cases files = {{"testFile1", true, true, InLocal},         {"testFile2", true, true, InLocal},
+                   {"ignoredFile", true, false, InLocal},      {"testFolder/testFile1", true, true, InLocal},
+                   {"testFolder/testFile2", true, true, InLocal}, {"testFolder/ignoredFile", true, false, InLocal},
+                   {"ignoredFolder/testFile1", true, false, InLocal}};
+    Cases folders = {{"testFolder", true, true, InLocal},
+                     {"testFolder2", true, true, InLocal},
+                     {"ignoredFolder", true, false, InLocal}};
+    check_eventually(d, files, folders, 10000);
+  }
+}
+
+TEST(sync_initial_fast) { run_initial(Mode::Fast); }
+TEST(sync_initial_compat) { run_initial(Mode::Compat); }
+TEST(sync_initial_helper) { run_initial(Mode::Helper); }
+TEST(sync_normal_fast) { run_normal(Mode::Fast); }
+TEST(sync_normal_helper) { run_normal(Mode::Helper); }
+TEST(sync_normal_compat) { run_normal(Mode::Compat); }
+
+TEST(sync_reconnect_after_stream_drop) {
+  log::logdir() = fs::make_temp_dir("synclogs-");
+  Dirs d;
+  Options o = base_options(d, Mode::Fast);
+  FaultPlan plan;
+  plan.kill_after_stdin_bytes = 64;  // first upstream shell dies mid-command
+  plan.only_shell = 1;
+  auto faulty = std::make_shared<FaultInjectingTransport>(std::make_shared<LocalShellTransport>(), plan);
+  o.reconnect = [] { return std::make_shared<LocalShellTransport>(); };
+  Session s(o, faulty);
+  s.start();
+  fs::write_file(fs::join(d.local, "a.txt"), kContents);
+  Cases files = {{"a.txt", true, true, InLocal}};
+  check_eventually(d, files, {}, 15000);
+  EXPECT_TRUE(s.stats().reconnects >= 1);
+  EXPECT_TRUE(s.running());
+  s.stop();
+}
+
+TEST(sync_corrupt_ack_is_fatal_without_reconnect) {
+  log::logdir() = fs::make_temp_dir("synclogs-");
+  Dirs d;
+  Options o = base_options(d, Mode::Fast);
+  FaultPlan plan;
+  plan.corrupt_from = "DONE";
+  plan.corrupt_to = "DXNE";
+  plan.only_shell = 2;  // downstream shell: scan ack never matches -> stream ends in error
+  plan.kill_after_stdin_bytes = 0;
+  auto faulty = std::make_shared<FaultInjectingTransport>(std::make_shared<LocalShellTransport>(), plan);
+  std::string err;
+  o.on_error = [&](const std::string& e) { err = e; };
+  Session s(o, faulty);
+  s.start();
+  // the corrupted ack turns into a parse failure of the scan
+  auto t0 = std::chrono::steady_clock::now();
+  while (s.running() && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10))
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  EXPECT_TRUE(!s.running());
+  EXPECT_TRUE(!err.empty());
+  s.stop();
+}
