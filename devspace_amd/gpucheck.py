@@ -1,0 +1,125 @@
+"""In-pod GPU check used by `devspace analyze` for MI355X pods.
+
+Kubernetes only knows that `amd.com/gpu: N` was scheduled; this reports what the container
+can actually use: device nodes (/dev/kfd, /dev/dri), visible devices, and for each device a
+measured MFMA self-test, HBM3E copy bandwidth and bf16 MFMA throughput (HIP kernels in
+devspace_amd/ops/gpuprobe.hip), compared against MI355X expectations.
+
+    python -m devspace_amd.gpucheck [--quick] [--json]
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+# MI355X reference figures (MI355X_MICROARCH.md: 8 TB/s HBM spec, ~6.3 TB/s achievable float4
+# copy; ~2.5 PF dense bf16 spec).
+HBM_EXPECTED_GBPS = 6300.0
+BF16_PEAK_TFLOPS = 2500.0
+HBM_BYTES_PER_GPU = 288 * 10**9
+
+
+class Probe:
+    def __init__(self, path=None):
+        from devspace_amd.ops import build as ops_build
+
+        path = path or ops_build.lib_path()
+        if not os.path.exists(path):
+            ops_build.build()
+        self.lib = ctypes.CDLL(path)
+        self.lib.gp_device_count.restype = ctypes.c_int
+        self.lib.gp_device_info.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        self.lib.gp_device_info.restype = ctypes.c_int
+        self.lib.gp_mfma_selftest.argtypes = [ctypes.c_int]
+        self.lib.gp_mfma_selftest.restype = ctypes.c_double
+        self.lib.gp_hbm_copy_gbps.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int]
+        self.lib.gp_hbm_copy_gbps.restype = ctypes.c_double
+        self.lib.gp_mfma_bf16_tflops.argtypes = [ctypes.c_int, ctypes.c_int]
+        self.lib.gp_mfma_bf16_tflops.restype = ctypes.c_double
+        self.lib.gp_last_error.restype = ctypes.c_char_p
+
+    def count(self):
+        return self.lib.gp_device_count()
+
+    def info(self, dev):
+        buf = ctypes.create_string_buffer(2048)
+        if self.lib.gp_device_info(dev, buf, len(buf)) != 0:
+            raise RuntimeError(self.lib.gp_last_error().decode())
+        return json.loads(buf.value.decode())
+
+    def selftest(self, dev):
+        return self.lib.gp_mfma_selftest(dev)
+
+    def hbm_gbps(self, dev, nbytes=1 << 30, iters=10):
+        return self.lib.gp_hbm_copy_gbps(dev, nbytes, iters)
+
+    def mfma_tflops(self, dev, iters=20000):
+        return self.lib.gp_mfma_bf16_tflops(dev, iters)
+
+
+def device_nodes():
+    return {
+        "/dev/kfd": os.path.exists("/dev/kfd"),
+        "/dev/dri": os.path.isdir("/dev/dri"),
+        "HIP_VISIBLE_DEVICES": os.environ.get("HIP_VISIBLE_DEVICES"),
+        "ROCR_VISIBLE_DEVICES": os.environ.get("ROCR_VISIBLE_DEVICES"),
+    }
+
+
+def run(quick=False):
+    report = {"nodes": device_nodes(), "devices": [], "problems": []}
+    if not report["nodes"]["/dev/kfd"]:
+        report["problems"].append("/dev/kfd missing: the pod did not get the AMD GPU device plugin's devices")
+    try:
+        probe = Probe()
+    except OSError as e:
+        report["problems"].append(f"cannot load HIP runtime / probe library: {e}")
+        return report
+    n = probe.count()
+    if n == 0:
+        report["problems"].append("no HIP devices visible (check amd.com/gpu request and HIP_VISIBLE_DEVICES)")
+    for d in range(n):
+        info = probe.info(d)
+        err = probe.selftest(d)
+        info["mfma_selftest_max_abs_err"] = err
+        if err != 0.0:
+            report["problems"].append(f"gpu{d}: MFMA self-test failed (max abs err {err})")
+        if not quick:
+            gbps = probe.hbm_gbps(d)
+            tf = probe.mfma_tflops(d)
+            info["hbm_copy_gbps"] = round(gbps, 1)
+            info["hbm_copy_pct_of_achievable"] = round(100.0 * gbps / HBM_EXPECTED_GBPS, 1)
+            info["mfma_bf16_tflops"] = round(tf, 1)
+            info["mfma_bf16_pct_of_peak"] = round(100.0 * tf / BF16_PEAK_TFLOPS, 1)
+            if "gfx950" in info.get("arch", "") and gbps < 0.5 * HBM_EXPECTED_GBPS:
+                report["problems"].append(f"gpu{d}: HBM bandwidth {gbps:.0f} GB/s is below 50% of expected")
+        report["devices"].append(info)
+    return report
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="devspace_amd.gpucheck")
+    ap.add_argument("--quick", action="store_true", help="self-test only, no bandwidth/throughput runs")
+    ap.add_argument("--json", action="store_true")
+    args = ap.parse_args(argv)
+    rep = run(quick=args.quick)
+    if args.json:
+        print(json.dumps(rep))
+    else:
+        for dev in rep["devices"]:
+            print(
+                f"gpu{dev['index']}: {dev['name']} {dev['arch']} CUs={dev['compute_units']} "
+                f"HBM={dev['hbm_total_bytes'] / 1e9:.0f}GB selftest_err={dev['mfma_selftest_max_abs_err']} "
+                f"hbm={dev.get('hbm_copy_gbps')}GB/s mfma_bf16={dev.get('mfma_bf16_tflops')}TF/s"
+            )
+        for p in rep["problems"]:
+            print(f"problem: {p}")
+    return 1 if rep["problems"] else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,202 @@
+// GPU health / sizing probe for MI355X dev pods (gfx950, CDNA4).
+//
+// `devspace analyze` (reference: pkg/devspace/analyze) reports why a pod is unhealthy; for
+// GPU pods the question "did this pod get a working, full-speed MI355X?" needs a device-side
+// answer: a scheduling success with a wedged/throttled GPU, a missing /dev/kfd or a wrong
+// HIP_VISIBLE_DEVICES still looks "Running" to Kubernetes. This library measures, per device:
+//   * MFMA correctness: one 32x32x16 bf16 tile against an exact host reference (identity A,
+//     asymmetric B so a row/col swap cannot pass),
+//   * HBM3E streaming bandwidth: float4 grid-stride copy, >>256 workgroups,
+//   * dense bf16 MFMA throughput: register-resident v_mfma_f32_32x32x16_bf16 chains with
+//     independent accumulators (one wave per SIMD class of measurement).
+// Exposed through a C ABI and loaded with ctypes by devspace_amd/gpucheck.py.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+#define CHECK(x)                                                                      \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) {                                                           \
+      std::snprintf(g_err, sizeof(g_err), "%s failed: %s", #x, hipGetErrorString(e_)); \
+      return -1;                                                                      \
+    }                                                                                 \
+  } while (0)
+
+static char g_err[512];
+
+// ------------------------------------------------------------------ kernels
+
+// One wave: D(32x32) = A(32x16) * B(16x32) with the gfx950 bf16 fragment maps
+// (lane l: r = l&31, h = l>>5 holds A[r][8h+j], B[8h+j][r]; D col = l&31,
+// row = (reg&3) + 8*(reg>>2) + 4*h).
+__global__ void __launch_bounds__(64) mfma_tile_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                       float* __restrict__ D) {
+  const int l = threadIdx.x;
+  const int r = l & 31, h = l >> 5;
+  bf16x8 a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = (__bf16)A[r * 16 + 8 * h + j];
+    b[j] = (__bf16)B[(8 * h + j) * 32 + r];
+  }
+  f32x16 acc = {};
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    D[row * 32 + r] = acc[reg];
+  }
+}
+
+// Streaming copy: 16-byte vectors, grid-stride.
+__global__ void __launch_bounds__(256) copy_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+
+// Register-resident MFMA chain: 4 independent accumulators per wave hide the MFMA latency.
+__global__ void __launch_bounds__(256) mfma_rate_kernel(float* __restrict__ out, int iters, float seed) {
+  bf16x8 a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = (__bf16)(seed + 0.001f * (threadIdx.x + j));
+    b[j] = (__bf16)(seed - 0.002f * j);
+  }
+  f32x16 c0 = {}, c1 = {}, c2 = {}, c3 = {};
+  for (int it = 0; it < iters; ++it) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c3, 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s += c0[r] + c1[r] + c2[r] + c3[r];
+  if (s == 1234.5678f) out[blockIdx.x] = s;  // practically never true; keeps the chain live
+}
+
+// ------------------------------------------------------------------ C ABI
+
+extern "C" {
+
+const char* gp_last_error() { return g_err; }
+
+int gp_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// Writes a JSON object describing device `dev`.
+int gp_device_info(int dev, char* buf, int cap) {
+  hipDeviceProp_t p;
+  CHECK(hipGetDeviceProperties(&p, dev));
+  size_t free_b = 0, total_b = 0;
+  CHECK(hipSetDevice(dev));
+  CHECK(hipMemGetInfo(&free_b, &total_b));
+  std::snprintf(buf, cap,
+                "{\"index\": %d, \"name\": \"%s\", \"arch\": \"%s\", \"compute_units\": %d, "
+                "\"clock_mhz\": %d, \"hbm_total_bytes\": %zu, \"hbm_free_bytes\": %zu, \"pci_bus\": %d, "
+                "\"lds_per_cu_bytes\": %zu, \"warp_size\": %d}",
+                dev, p.name, p.gcnArchName, p.multiProcessorCount, p.clockRate / 1000, total_b, free_b, p.pciBusID,
+                (size_t)p.maxSharedMemoryPerMultiProcessor, p.warpSize);
+  return 0;
+}
+
+// Returns max |D - A*B| for one MFMA tile (0.0 on a healthy device), or -1 on error.
+double gp_mfma_selftest(int dev) {
+  if (hipSetDevice(dev) != hipSuccess) return -1;
+  std::vector<float> A(32 * 16, 0.f), B(16 * 32), D(32 * 32, -1.f);
+  for (int i = 0; i < 16; ++i) A[i * 16 + i] = 1.f;  // identity on the first 16 rows
+  for (int k = 0; k < 16; ++k)
+    for (int j = 0; j < 32; ++j) B[k * 32 + j] = (float)((k * 7 + j * 3) % 64 - 17);  // asymmetric, bf16-exact
+  float *dA, *dB, *dD;
+  if (hipMalloc(&dA, A.size() * 4) || hipMalloc(&dB, B.size() * 4) || hipMalloc(&dD, D.size() * 4)) return -1;
+  hipMemcpy(dA, A.data(), A.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(dB, B.data(), B.size() * 4, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(mfma_tile_kernel, dim3(1), dim3(64), 0, 0, dA, dB, dD);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  hipMemcpy(D.data(), dD, D.size() * 4, hipMemcpyDeviceToHost);
+  hipFree(dA);
+  hipFree(dB);
+  hipFree(dD);
+  double err = 0;
+  for (int i = 0; i < 32; ++i)
+    for (int j = 0; j < 32; ++j) {
+      double want = i < 16 ? B[i * 32 + j] : 0.0;
+      double d = D[i * 32 + j] - want;
+      err = std::max(err, d < 0 ? -d : d);
+    }
+  return err;
+}
+
+// HBM copy bandwidth in GB/s (bytes read + written per second).
+double gp_hbm_copy_gbps(int dev, size_t bytes, int iters) {
+  if (hipSetDevice(dev) != hipSuccess) return -1;
+  size_t n = bytes / sizeof(f32x4);
+  f32x4 *src = nullptr, *dst = nullptr;
+  if (hipMalloc(&src, n * sizeof(f32x4)) != hipSuccess) return -1;
+  if (hipMalloc(&dst, n * sizeof(f32x4)) != hipSuccess) {
+    hipFree(src);
+    return -1;
+  }
+  hipMemset(src, 1, n * sizeof(f32x4));
+  hipDeviceProp_t p;
+  hipGetDeviceProperties(&p, dev);
+  // >>256 workgroups: 16 resident blocks of 256 threads per CU
+  dim3 grid(p.multiProcessorCount * 16), block(256);
+  hipLaunchKernelGGL(copy_kernel, grid, block, 0, 0, src, dst, n);  // warm-up
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0);
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(copy_kernel, grid, block, 0, 0, src, dst, n);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0;
+  hipEventElapsedTime(&ms, e0, e1);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(src);
+  hipFree(dst);
+  if (ms <= 0) return -1;
+  return (2.0 * (double)n * sizeof(f32x4) * iters) / (ms * 1e-3) / 1e9;
+}
+
+// Dense bf16 MFMA rate in TFLOP/s.
+double gp_mfma_bf16_tflops(int dev, int iters) {
+  if (hipSetDevice(dev) != hipSuccess) return -1;
+  hipDeviceProp_t p;
+  hipGetDeviceProperties(&p, dev);
+  float* out;
+  if (hipMalloc(&out, 1 << 20) != hipSuccess) return -1;
+  // 4 waves per block (one per SIMD), 2 blocks per CU
+  dim3 grid(p.multiProcessorCount * 2), block(256);
+  hipLaunchKernelGGL(mfma_rate_kernel, grid, block, 0, 0, out, 64, 1.0f);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(mfma_rate_kernel, grid, block, 0, 0, out, iters, 1.0f);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0;
+  hipEventElapsedTime(&ms, e0, e1);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(out);
+  if (ms <= 0) return -1;
+  double waves = (double)grid.x * (block.x / 64);
+  double flops = waves * iters * 4.0 * (2.0 * 32 * 32 * 16);
+  return flops / (ms * 1e-3) / 1e12;
+}
+
+}  // extern "C"

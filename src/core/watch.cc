@@ -69,7 +69,7 @@ void InotifyWatcher::add_recursive(const std::string& dir, bool emit_existing) {
   for (auto& e : fs::list_dir(dir)) {
     std::string p = fs::join(dir, e.name);
     // Entries created between mkdir and add_watch would otherwise be missed.
-    if (emit_existing && cb_) cb_(p);
+    if (emit_existing && cb_) cb_(p, true);
     if (e.is_dir && !e.is_symlink) add_recursive(p, emit_existing);
   }
 }
@@ -92,7 +92,7 @@ void InotifyWatcher::loop() {
         auto* ev = (struct inotify_event*)p;
         p += sizeof(struct inotify_event) + ev->len;
         if (ev->mask & IN_Q_OVERFLOW) {
-          if (cb_) cb_("");
+          if (cb_) cb_("", true);
           continue;
         }
         std::string dir;
@@ -110,11 +110,11 @@ void InotifyWatcher::loop() {
         }
         std::string path = ev->len ? fs::join(dir, std::string(ev->name)) : dir;
         if ((ev->mask & (IN_DELETE_SELF | IN_MOVE_SELF)) && path == root_) {
-          if (cb_) cb_(path);
+          if (cb_) cb_(path, true);
           continue;
         }
         if ((ev->mask & IN_ISDIR) && (ev->mask & (IN_CREATE | IN_MOVED_TO))) {
-          if (cb_) cb_(path);
+          if (cb_) cb_(path, true);
           add_recursive(path, true);
           continue;
         }
@@ -132,7 +132,8 @@ void InotifyWatcher::loop() {
           }
         }
         if (ev->mask & (IN_DELETE_SELF | IN_MOVE_SELF)) continue;
-        if (cb_) cb_(path);
+        bool settled = (ev->mask & (IN_CLOSE_WRITE | IN_MOVED_TO | IN_MOVED_FROM | IN_DELETE)) != 0;
+        if (cb_) cb_(path, settled);
       }
     }
   }

@@ -21,8 +21,9 @@ namespace ds {
 class InotifyWatcher {
  public:
   // Callback receives absolute paths of changed entries (created/modified/removed/moved).
-  // `overflow` is signalled with an empty path: the consumer should rescan.
-  using Callback = std::function<void(const std::string& path)>;
+  // `overflow` is signalled with an empty path: the consumer should rescan. `settled` is true
+  // for events that mark a finished write (close-after-write, rename-into, delete, mkdir).
+  using Callback = std::function<void(const std::string& path, bool settled)>;
   InotifyWatcher() = default;
   ~InotifyWatcher();
   bool start(const std::string& root, Callback cb, std::string* err = nullptr);

@@ -56,8 +56,11 @@ static std::string safe_join(const std::string& rel_in) {
 }
 
 static std::string op_extract(const std::string& payload) {
+  // gzip or plain tar (small edits are shipped uncompressed)
+  bool gzipped = payload.size() >= 2 && (unsigned char)payload[0] == 0x1f && (unsigned char)payload[1] == 0x8b;
   GzipReader gz(string_source(&payload));
-  TarReader tr([&](char* b, size_t n) { return gz.read(b, n); });
+  Source raw = string_source(&payload);
+  TarReader tr([&](char* b, size_t n) { return gzipped ? gz.read(b, n) : raw(b, n); });
   TarEntry e;
   bool root = ::geteuid() == 0;
   try {

@@ -1,2 +1,198 @@
+// Python bindings for the native engine (devspace_amd._native).
+// Used by the workload-side hot-reload runner (inotify watcher), the benchmark harness
+// (sync sessions driven in-process) and the pytest suite.
+#include <pybind11/functional.h>
 #include <pybind11/pybind11.h>
-PYBIND11_MODULE(_native, m) {}
+#include <pybind11/stl.h>
+
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+
+#include "config/config.h"
+#include "core/codec.h"
+#include "core/fs.h"
+#include "core/log.h"
+#include "core/match.h"
+#include "core/value.h"
+#include "core/watch.h"
+#include "sync/sync.h"
+
+namespace py = pybind11;
+using namespace ds;
+
+static py::object to_py(const Value& v) {
+  switch (v.type()) {
+    case Value::Type::Null: return py::none();
+    case Value::Type::Bool: return py::bool_(v.as_bool());
+    case Value::Type::Int: return py::int_(v.as_int());
+    case Value::Type::Float: return py::float_(v.as_double());
+    case Value::Type::String: return py::str(v.str());
+    case Value::Type::Seq: {
+      py::list l;
+      for (auto& it : v.items()) l.append(to_py(it));
+      return l;
+    }
+    case Value::Type::Map: {
+      py::dict d;
+      for (auto& e : v.entries()) d[py::str(e.first)] = to_py(e.second);
+      return d;
+    }
+  }
+  return py::none();
+}
+
+static Value from_py(const py::handle& o) {
+  if (o.is_none()) return Value();
+  if (py::isinstance<py::bool_>(o)) return Value(o.cast<bool>());
+  if (py::isinstance<py::int_>(o)) return Value((int64_t)o.cast<long long>());
+  if (py::isinstance<py::float_>(o)) return Value(o.cast<double>());
+  if (py::isinstance<py::str>(o)) return Value(o.cast<std::string>());
+  if (py::isinstance<py::dict>(o)) {
+    Value m = Value::map();
+    for (auto item : o.cast<py::dict>()) m[py::str(item.first).cast<std::string>()] = from_py(item.second);
+    return m;
+  }
+  if (py::isinstance<py::list>(o) || py::isinstance<py::tuple>(o)) {
+    Value s = Value::seq();
+    for (auto item : o) s.push(from_py(item));
+    return s;
+  }
+  return Value(py::str(o).cast<std::string>());
+}
+
+// Inotify watcher with a queue drained from Python (no callbacks across threads).
+class PyWatcher {
+ public:
+  explicit PyWatcher(const std::string& root) {
+    std::string err;
+    if (!w_.start(
+            root,
+            [this](const std::string& p, bool) {
+              {
+                std::lock_guard<std::mutex> g(mu_);
+                q_.push_back(p);
+              }
+              cv_.notify_all();
+            },
+            &err))
+      throw std::runtime_error(err);
+  }
+  std::vector<std::string> poll(int timeout_ms) {
+    py::gil_scoped_release nogil;
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [this] { return !q_.empty(); });
+    std::vector<std::string> out(q_.begin(), q_.end());
+    q_.clear();
+    return out;
+  }
+  void close() { w_.stop(); }
+
+ private:
+  InotifyWatcher w_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::string> q_;
+};
+
+class PySync {
+ public:
+  PySync(const std::string& watch_path, const std::string& dest_path, const std::string& mode,
+         std::vector<std::string> exclude, std::vector<std::string> download_exclude,
+         std::vector<std::string> upload_exclude, const std::string& helper_path, const std::string& log_dir,
+         const std::string& pod_name) {
+    sync::Options o;
+    o.watch_path = watch_path;
+    o.dest_path = dest_path;
+    o.mode = sync::parse_mode(mode);
+    o.exclude_paths = std::move(exclude);
+    o.download_exclude_paths = std::move(download_exclude);
+    o.upload_exclude_paths = std::move(upload_exclude);
+    o.helper_path = helper_path;
+    o.pod_name = pod_name;
+    if (!log_dir.empty()) log::logdir() = log_dir;
+    o.reconnect = [] { return std::make_shared<sync::LocalShellTransport>(); };
+    s_ = std::make_unique<sync::Session>(o, std::make_shared<sync::LocalShellTransport>());
+  }
+  void start() {
+    py::gil_scoped_release nogil;
+    s_->start();
+  }
+  bool wait_initial_sync(int ms) {
+    py::gil_scoped_release nogil;
+    return s_->wait_initial_sync(ms);
+  }
+  void stop() {
+    py::gil_scoped_release nogil;
+    s_->stop();
+  }
+  bool running() { return s_->running(); }
+  std::string error() { return s_->error(); }
+  std::string mode() { return sync::mode_name(s_->effective_mode()); }
+  py::dict stats() {
+    auto st = s_->stats();
+    py::dict d;
+    d["upstream_batches"] = st.upstream_batches;
+    d["upstream_changes"] = st.upstream_changes;
+    d["downstream_batches"] = st.downstream_batches;
+    d["downstream_changes"] = st.downstream_changes;
+    d["reconnects"] = st.reconnects;
+    d["last_upload_ms"] = st.last_upload_ms;
+    d["bytes_up"] = st.bytes_up;
+    d["bytes_down"] = st.bytes_down;
+    return d;
+  }
+
+ private:
+  std::unique_ptr<sync::Session> s_;
+};
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "devspace native engine (C++17) bindings";
+  log::set_fatal_throws(true);
+  m.def("yaml_parse", [](const std::string& s) { return to_py(yaml_parse(s)); });
+  m.def("yaml_parse_all", [](const std::string& s) {
+    py::list l;
+    for (auto& d : yaml_parse_all(s)) l.append(to_py(d));
+    return l;
+  });
+  m.def("yaml_dump", [](py::object o) { return yaml_dump(from_py(o)); });
+  m.def("json_dump", [](py::object o) { return json_dump(from_py(o)); });
+  m.def("sha256_hex", [](py::bytes b) { return sha256_hex(std::string(b)); });
+  m.def("gitignore_match", [](std::vector<std::string> pats, const std::string& path) {
+    return GitIgnore(pats).matches(path);
+  });
+  m.def("dockerignore_match", [](std::vector<std::string> pats, const std::string& path) {
+    return DockerIgnore(pats).matches(path);
+  });
+  m.def("glob_match", &glob_match);
+  m.def("parse_config", [](py::object data) { return to_py(config::parse_versioned(from_py(data))); });
+  m.def("copy_to_container",
+        [](const std::string& local, const std::string& container, std::vector<std::string> excludes,
+           const std::string& mode) {
+          py::gil_scoped_release nogil;
+          sync::Session::copy_to_container(std::make_shared<sync::LocalShellTransport>(), local, container,
+                                           excludes, sync::parse_mode(mode));
+        },
+        py::arg("local"), py::arg("container"), py::arg("excludes") = std::vector<std::string>{},
+        py::arg("mode") = "fast");
+  py::class_<PyWatcher>(m, "Watcher")
+      .def(py::init<const std::string&>())
+      .def("poll", &PyWatcher::poll, py::arg("timeout_ms") = 1000)
+      .def("close", &PyWatcher::close);
+  py::class_<PySync>(m, "SyncSession")
+      .def(py::init<const std::string&, const std::string&, const std::string&, std::vector<std::string>,
+                    std::vector<std::string>, std::vector<std::string>, const std::string&, const std::string&,
+                    const std::string&>(),
+           py::arg("watch_path"), py::arg("dest_path"), py::arg("mode") = "fast",
+           py::arg("exclude") = std::vector<std::string>{}, py::arg("download_exclude") = std::vector<std::string>{},
+           py::arg("upload_exclude") = std::vector<std::string>{}, py::arg("helper_path") = "",
+           py::arg("log_dir") = "", py::arg("pod_name") = "")
+      .def("start", &PySync::start)
+      .def("wait_initial_sync", &PySync::wait_initial_sync, py::arg("timeout_ms") = 30000)
+      .def("stop", &PySync::stop)
+      .def("running", &PySync::running)
+      .def("error", &PySync::error)
+      .def("mode", &PySync::mode)
+      .def("stats", &PySync::stats);
+}

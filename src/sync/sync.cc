@@ -34,8 +34,8 @@ Mode parse_mode(const std::string& s_in) {
     if (e && *e) s = to_lower(e);
   }
   if (s == "compat" || s == "reference") return Mode::Compat;
-  if (s == "helper") return Mode::Helper;
-  return Mode::Fast;
+  if (s == "fast" || s == "posix") return Mode::Fast;
+  return Mode::Helper;  // default: helper with automatic fallback to fast POSIX
 }
 
 const char* mode_name(Mode m) {
@@ -236,6 +236,11 @@ void Session::open_up_shell() {
       up_out_.reset(up_shell_->out());
     }
   }
+  if (mode_ != Mode::Compat && !up_helper_) {
+    // create the destination once instead of per upload
+    write_all(up_shell_->in(), "mkdir -p " + shell_quote(dest_) + "; echo " + kDone + "\n");
+    wait_ack(up_out_, kDone, false, nullptr, 30000);
+  }
 }
 
 void Session::open_down_shell() {
@@ -285,7 +290,11 @@ bool Session::should_upload(const std::string& rel, const fs::StatInfo& st, bool
     if (initial) {
       if (st.mtime_rounded() <= f->mtime) return false;
     } else {
-      if (st.mtime_rounded() == f->mtime && st.size == f->size) return false;
+      if (mode_ != Mode::Compat && f->local_mtime_ns) {
+        if (st.mtime_sec * 1000000000LL + st.mtime_nsec == f->local_mtime_ns && st.size == f->size) return false;
+      } else if (st.mtime_rounded() == f->mtime && st.size == f->size) {
+        return false;
+      }
     }
   }
   return true;
@@ -397,7 +406,7 @@ void Session::start_watcher() {
   std::string err;
   bool ok = watcher_->start(
       o_.watch_path,
-      [this](const std::string& path) {
+      [this](const std::string& path, bool settled) {
         if (path.empty()) {
           // queue overflow: rescan everything
           UpEvent e;
@@ -407,6 +416,7 @@ void Session::start_watcher() {
         }
         UpEvent e;
         e.abs_path = path;
+        e.settled = settled;
         push_event(e);
       },
       &err);
@@ -482,13 +492,16 @@ void Session::upstream_loop() {
     long batch_start_us = mono_us();
     size_t last_count = 0;
     bool first = true;
+    bool last_settled = false;
     while (!stopping_ && !failed_) {
       std::vector<UpEvent> evs;
       {
         std::unique_lock<std::mutex> lk(q_mu_);
         if (!first) {
-          q_cv_.wait_for(lk, std::chrono::milliseconds(window_ms_),
-                         [this] { return !queue_.empty() || stopping_ || failed_; });
+          // Fast modes: a finished write (close/rename/delete) only needs a 1 ms grace period
+          // to absorb its sibling events; partial writes wait the full quiet window.
+          int w = (mode_ != Mode::Compat && last_settled) ? std::min(window_ms_, 1) : window_ms_;
+          q_cv_.wait_for(lk, std::chrono::milliseconds(w), [this] { return !queue_.empty() || stopping_ || failed_; });
         }
         evs.assign(std::make_move_iterator(queue_.begin()), std::make_move_iterator(queue_.end()));
         queue_.clear();
@@ -499,6 +512,7 @@ void Session::upstream_loop() {
         break;
       }
       if (!first_us) first_us = evs.front().t_us;
+      last_settled = evs.back().settled || evs.back().has_info;
       {
         std::lock_guard<std::mutex> g(index_.mu);
         for (auto& ev : evs) {
@@ -517,7 +531,9 @@ void Session::upstream_loop() {
           }
           if (!fi) continue;
           auto it = pos.find(fi->name);
-          if (it != pos.end()) {
+          if (mode_ == Mode::Compat) {
+            changes.push_back(*fi);  // the reference appends duplicates (upstream.go:140)
+          } else if (it != pos.end()) {
             changes[it->second] = *fi;
           } else {
             pos[fi->name] = changes.size();
@@ -623,6 +639,7 @@ void Session::recursive_tar(const std::string& rel, std::map<std::string, FileIn
   fi.size = st.size;
   fi.mtime = st.mtime_rounded();
   fi.is_dir = st.is_dir;
+  if (mode_ != Mode::Compat) fi.local_mtime_ns = st.mtime_sec * 1000000000LL + st.mtime_nsec;
   uint32_t mode = st.mode & 07777;
   uint32_t uid = st.uid, gid = st.gid;
   {
@@ -670,16 +687,18 @@ void Session::recursive_tar(const std::string& rel, std::map<std::string, FileIn
 }
 
 std::string Session::build_archive(const std::vector<FileInfo>& files, std::map<std::string, FileInfo>* written) {
-  std::string out;
-  int level = mode_ == Mode::Compat ? 6 : 1;
-  GzipWriter gz(string_sink(&out), level);
-  TarWriter tw([&](const char* d, size_t n) { return gz.write(d, n); });
+  std::string raw;
+  TarWriter tw(string_sink(&raw));
   for (auto& f : files)
     if (!written->count(f.name)) recursive_tar(f.name, written, &tw, 0);
   tw.finish();
-  gz.finish();
-  return out;
+  // The reference always gzips (sync/tar.go:146). Small edits are latency-bound, not
+  // bandwidth-bound: fast modes ship them as plain tar (no gzip process on either side).
+  if (mode_ != Mode::Compat && raw.size() <= 256 * 1024) return raw;
+  return gzip_compress(raw, mode_ == Mode::Compat ? 6 : 1);
 }
+
+static bool is_gzip(const std::string& a) { return a.size() >= 2 && (unsigned char)a[0] == 0x1f && (unsigned char)a[1] == 0x8b; }
 
 void Session::upload_archive(const std::string& archive) {
   const std::string size = std::to_string(archive.size());
@@ -749,8 +768,10 @@ void Session::upload_archive(const std::string& archive) {
     wait_ack(up_out_, kDone, false);
     return;
   }
-  std::string cmd = "mkdir -p " + qdest + " && echo " + kStart + " && head -c " + size + " | tar xzpf - -C " +
-                    shell_quote(dest_ + "/.") + " 2>/tmp/devspace-upstream-error; echo " + kDone + "\n";
+  (void)qdest;  // dest is created once when the shell opens
+  std::string cmd = "echo " + std::string(kStart) + " && head -c " + size + " | tar " +
+                    (is_gzip(archive) ? "xzpf" : "xpf") + " - -C " + shell_quote(dest_ + "/.") +
+                    " 2>/tmp/devspace-upstream-error; echo " + kDone + "\n";
   if (!write_all(fd, cmd)) throw SyncError("upstream: write failed");
   wait_ack(up_out_, kStart, false);
   send_payload();
@@ -1163,6 +1184,7 @@ void Session::untar_all(const std::string& archive) {
     f.name = rel;
     f.mtime = e.mtime;
     f.size = (int64_t)data.size();
+    if (mode_ != Mode::Compat) f.local_mtime_ns = e.mtime * 1000000000LL;
     index_.files[rel] = f;
     if (++count % 500 == 0) logf(strfmt("[Downstream] Untared %d files...", count));
   }

@@ -47,6 +47,9 @@ struct FileInfo {
   int64_t remote_mode = 0;
   int remote_uid = 0, remote_gid = 0;
   bool has_remote_attrs = false;
+  // Local nanosecond mtime at the last upload/download (non-compat modes only): detects two
+  // same-size edits within one second, which the reference's rounded mtimes miss.
+  int64_t local_mtime_ns = 0;
 };
 
 // Parses one `stat -c "%n///%s,%Y,%f,%a,%u,%g"` line (sync/file_information.go:62).
@@ -134,6 +137,7 @@ class Session {
     bool has_info = false;
     FileInfo info;
     long t_us = 0;
+    bool settled = false;
   };
 
   // logging

@@ -1,0 +1,32 @@
+"""bench.py contract: one JSON line with the driver's fields."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+
+def _run(args, timeout):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = r.stdout.strip().splitlines()[-1]
+    return json.loads(line)
+
+
+def test_bench_cpu_tiny():
+    d = _run(["--steps", "3", "--warmup", "1", "--ref-steps", "1", "--tiny"], 600)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "config"):
+        assert k in d
+    assert d["higher_is_better"] is False
+    assert d["value"] > 0
+    assert d["reference_equivalent_p50_ms"] > d["value"]
+
+
+@pytest.mark.gpu
+def test_bench_gpu_short():
+    d = _run(["--steps", "3", "--warmup", "1", "--ref-steps", "1"], 900)
+    assert d["n_gpus"] >= 1 and d["value"] > 0
