@@ -112,8 +112,11 @@ def _wait_file_contains(path, needle, timeout=60.0):
     raise TimeoutError(f"{needle} never reached {path}")
 
 
-def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False):
-    """Runs the edit->reload loop against a local pod directory; returns latency samples."""
+def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False, timed_start=None, timed_end=None):
+    """Runs the edit->reload loop against a local pod directory; returns latency samples.
+
+    `timed_start`/`timed_end` are invoked right before the first and after the last timed
+    step (after warmup), so the caller can bracket exactly K steps with barriers."""
     from devspace_amd import _native
 
     proj = os.path.join(workdir, f"proj-{sync_mode}-{'restart' if restart else 'hot'}")
@@ -156,6 +159,8 @@ def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False):
         proj_file = os.path.join(proj, "train.py")
         pod_file = os.path.join(pod, "train.py")
         for i in range(warmup + steps):
+            if i == warmup and timed_start:
+                timed_start()
             # alternate marker lengths so consecutive edits always differ in size (the
             # reference-equivalent mode compares rounded mtimes + size, like the reference)
             marker = f"e{i}" + ("_" * (i % 2))
@@ -167,6 +172,8 @@ def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False):
             if i >= warmup:
                 samples.append((t1 - t0) * 1000.0)
                 sync_samples.append((t_sync - t0) * 1000.0)
+        if timed_end:
+            timed_end()
         stats = sess.stats()
     finally:
         try:
@@ -230,15 +237,25 @@ def main():
     workdir = tempfile.mkdtemp(prefix="devspace-bench-")
     result = {}
     deploy_s = None
+    clock = {}
+
+    def timed_start():
+        barrier_sync()
+        clock["t0"] = time.perf_counter()
+
+    def timed_end():
+        barrier_sync()
+        clock["t1"] = time.perf_counter()
+
     try:
         if rank == 0:
             deploy_s = deploy_wall_clock(workdir)
-        barrier_sync()
-        t_start = time.perf_counter()
-        if rank == 0:
-            result = inner_loop(workdir, args.sync_mode, False, nproc, args.steps, args.warmup, tiny=args.tiny)
-        barrier_sync()
-        elapsed = time.perf_counter() - t_start
+            result = inner_loop(workdir, args.sync_mode, False, nproc, args.steps, args.warmup, tiny=args.tiny,
+                                timed_start=timed_start, timed_end=timed_end)
+        else:
+            timed_start()
+            timed_end()
+        elapsed = clock["t1"] - clock["t0"]
         ref = None
         if rank == 0 and args.ref_steps > 0:
             ref = inner_loop(workdir, "compat", True, nproc, args.ref_steps, 1, tiny=args.tiny)
@@ -263,7 +280,7 @@ def main():
         "n_gpus": nproc,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_total / max(1, args.steps + args.warmup), 2),
+        "ms_per_step": round(ms_total / max(1, args.steps), 2),
         "higher_is_better": False,
         "scaling": "weak",
         "vs_baseline": None,
