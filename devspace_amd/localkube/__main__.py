@@ -1,0 +1,34 @@
+"""python -m devspace_amd.localkube up --state DIR [--port P] [--gpus N] [--kubeconfig PATH]"""
+import argparse
+import os
+import signal
+import sys
+import threading
+
+from .cluster import LocalCluster
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="devspace_amd.localkube")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    up = sub.add_parser("up", help="run the local cluster in the foreground")
+    up.add_argument("--state", required=True)
+    up.add_argument("--port", type=int, default=0)
+    up.add_argument("--gpus", type=int, default=None)
+    up.add_argument("--kubeconfig", default="")
+    up.add_argument("--namespace", default="default")
+    args = ap.parse_args(argv)
+    c = LocalCluster(args.state, port=args.port, gpus=args.gpus).start()
+    kc = args.kubeconfig or os.path.join(args.state, "kubeconfig")
+    c.write_kubeconfig(kc, args.namespace)
+    print(f"ready server={c.server} kubeconfig={kc} docker=unix://{c.docker_sock} gpus={c.gpus}", flush=True)
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    signal.signal(signal.SIGINT, lambda *_: stop.set())
+    stop.wait()
+    c.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,410 @@
+"""Kubernetes API server subset (REST + WebSocket exec/attach/port-forward + logs).
+
+Enough of the API surface for every call the devspace CLI makes:
+CRUD on any resource kind (core + named groups), label/field selectors, graceful pod
+deletion with ownerReference cascade, pod logs (tail / follow / previous), exec and attach on
+the v4.channel.k8s.io WebSocket protocol (with TTY + resize), and WebSocket port-forwarding.
+"""
+
+from __future__ import annotations
+
+import asyncio
+import fcntl
+import json
+import os
+import pty
+import struct
+import termios
+
+from aiohttp import WSMsgType, web
+
+from .store import CLUSTER_SCOPED, ApiError
+
+GROUP_KINDS = {
+    "apps": {"deployments", "statefulsets", "replicasets", "daemonsets", "controllerrevisions"},
+    "batch": {"jobs", "cronjobs"},
+    "rbac.authorization.k8s.io": {"roles", "rolebindings", "clusterroles", "clusterrolebindings"},
+    "autoscaling": {"horizontalpodautoscalers"},
+    "networking.k8s.io": {"ingresses", "networkpolicies"},
+    "extensions": {"deployments", "ingresses", "replicasets", "daemonsets"},
+}
+
+
+def _err(e: ApiError):
+    return web.json_response(e.status(), status=e.code)
+
+
+def _exit_status(code):
+    if code == 0:
+        return {"metadata": {}, "status": "Success"}
+    return {"metadata": {}, "status": "Failure", "message": f"command terminated with non-zero exit code: {code}",
+            "reason": "NonZeroExitCode", "details": {"causes": [{"reason": "ExitCode", "message": str(code)}]}}
+
+
+class ApiServer:
+    def __init__(self, store, kubelet):
+        self.store = store
+        self.kubelet = kubelet
+
+    def app(self):
+        app = web.Application(client_max_size=256 * 1024 * 1024)
+        app.router.add_get("/version", self.version)
+        app.router.add_get("/api", self.api_versions)
+        app.router.add_get("/apis", self.api_groups)
+        app.router.add_get("/healthz", self.healthz)
+        app.router.add_route("*", "/api/{version}/{tail:.*}", self.dispatch_core)
+        app.router.add_route("*", "/apis/{group}/{version}/{tail:.*}", self.dispatch_group)
+        return app
+
+    async def healthz(self, request):
+        return web.Response(text="ok")
+
+    async def version(self, request):
+        return web.json_response({"major": "1", "minor": "29", "gitVersion": "v1.29.0-devspace-local",
+                                  "platform": "linux/amd64"})
+
+    async def api_versions(self, request):
+        return web.json_response({"kind": "APIVersions", "versions": ["v1"]})
+
+    async def api_groups(self, request):
+        groups = [{"name": g, "versions": [{"groupVersion": f"{g}/v1", "version": "v1"}]} for g in GROUP_KINDS]
+        return web.json_response({"kind": "APIGroupList", "groups": groups})
+
+    async def dispatch_core(self, request):
+        return await self._dispatch(request, "", request.match_info["version"])
+
+    async def dispatch_group(self, request):
+        return await self._dispatch(request, request.match_info["group"], request.match_info["version"])
+
+    async def _dispatch(self, request, group, version):
+        segs = [s for s in request.match_info["tail"].split("/") if s]
+        api_version = version if not group else f"{group}/{version}"
+        ns = name = sub = None
+        if len(segs) >= 2 and segs[0] == "namespaces" and len(segs) >= 3:
+            ns, resource = segs[1], segs[2]
+            name = segs[3] if len(segs) > 3 else None
+            sub = segs[4] if len(segs) > 4 else None
+        else:
+            resource = segs[0] if segs else ""
+            name = segs[1] if len(segs) > 1 else None
+            sub = segs[2] if len(segs) > 2 else None
+        if group == "extensions":
+            group = "apps" if resource in GROUP_KINDS["apps"] else "networking.k8s.io"
+        try:
+            if sub in ("exec", "attach") and resource == "pods":
+                return await self.exec_ws(request, ns, name, sub)
+            if sub == "portforward" and resource == "pods":
+                return await self.portforward_ws(request, ns, name)
+            if sub == "log" and resource == "pods":
+                return await self.logs(request, ns, name)
+            m = request.method
+            if name is None:
+                if m == "GET":
+                    return self.list(request, group, resource, ns, api_version)
+                if m == "POST":
+                    body = await request.json()
+                    if resource == "namespaces":
+                        ns = ""
+                    obj = self.store.create(group, resource, ns or body.get("metadata", {}).get("namespace") or "default",
+                                            body, api_version)
+                    return web.json_response(obj, status=201)
+                if m == "DELETE":
+                    for o in self.store.list(group, resource, ns, request.query.get("labelSelector", "")):
+                        self._delete(group, resource, o["metadata"].get("namespace"), o["metadata"]["name"])
+                    return web.json_response({"kind": "Status", "status": "Success"})
+            else:
+                if sub == "status" and m in ("PUT", "PATCH"):
+                    body = await request.json()
+                    o = self.store.update_status(group, resource, ns, name, body.get("status", {}))
+                    if o is None:
+                        raise ApiError(404, "NotFound", f'{resource} "{name}" not found')
+                    return web.json_response(o)
+                if m == "GET":
+                    return web.json_response(self.store.get(group, resource, ns, name))
+                if m == "PUT":
+                    body = await request.json()
+                    return web.json_response(self.store.replace(group, resource, ns, name, body))
+                if m == "PATCH":
+                    body = await request.json()
+                    return web.json_response(self.store.patch(group, resource, ns, name, body))
+                if m == "DELETE":
+                    o = self._delete(group, resource, ns, name)
+                    return web.json_response(o)
+            return web.json_response({"kind": "Status", "status": "Failure", "message": "method not allowed",
+                                      "code": 405}, status=405)
+        except ApiError as e:
+            return _err(e)
+        except (ValueError, json.JSONDecodeError) as e:
+            return _err(ApiError(400, "BadRequest", str(e)))
+
+    def _delete(self, group, resource, ns, name):
+        if resource == "pods":
+            return self.store.mark_deleting(group, resource, ns, name)
+        obj = self.store.get(group, resource, ns, name)
+        if resource == "namespaces":
+            for (g, r, n, nm), _ in list(self.store.objs.items()):
+                if n == name and r not in CLUSTER_SCOPED:
+                    if r == "pods":
+                        self.store.mark_deleting(g, r, n, nm)
+                    else:
+                        try:
+                            self.store.delete(g, r, n, nm)
+                        except ApiError:
+                            pass
+        # cascade to owned objects (pods of deployments/statefulsets)
+        for key, o in self.store.owned_by(obj["metadata"]["uid"]):
+            g, r, n, nm = key
+            if r == "pods":
+                self.store.mark_deleting(g, r, n, nm)
+            else:
+                try:
+                    self.store.delete(g, r, n, nm)
+                except ApiError:
+                    pass
+        return self.store.delete(group, resource, ns, name)
+
+    def list(self, request, group, resource, ns, api_version):
+        field = None
+        fs = request.query.get("fieldSelector", "")
+        if fs:
+            conds = [c.split("=", 1) for c in fs.split(",") if "=" in c]
+
+            def field(o, conds=conds):
+                for k, v in conds:
+                    cur = o
+                    for part in k.split("."):
+                        cur = cur.get(part, {}) if isinstance(cur, dict) else {}
+                    if str(cur) != v:
+                        return False
+                return True
+
+        items = self.store.list(group, resource, ns, request.query.get("labelSelector", ""), field)
+        kind = (items[0]["kind"] if items else resource[:1].upper() + resource[1:-1]) + "List"
+        return web.json_response({"kind": kind, "apiVersion": api_version, "metadata": {"resourceVersion": "1"},
+                                  "items": items})
+
+    # ------------------------------------------------------------------ logs
+
+    async def logs(self, request, ns, name):
+        self.store.get("", "pods", ns, name)
+        rt, c = self.kubelet.container(ns, name, request.query.get("container"))
+        if c is None:
+            raise ApiError(400, "BadRequest", f'container "{request.query.get("container")}" is not valid for pod {name}')
+        tail = int(request.query.get("tailLines", "-1") or -1)
+        follow = request.query.get("follow") in ("true", "1")
+        data = b""
+        if os.path.exists(c.log_path):
+            with open(c.log_path, "rb") as f:
+                data = f.read()
+        if tail >= 0:
+            lines = data.splitlines(keepends=True)
+            data = b"".join(lines[-tail:]) if tail else b""
+        if not follow:
+            return web.Response(body=data, content_type="text/plain")
+        resp = web.StreamResponse(headers={"Content-Type": "text/plain"})
+        await resp.prepare(request)
+        await resp.write(data)
+        pos = os.path.getsize(c.log_path) if os.path.exists(c.log_path) else 0
+        while (ns, name) in self.kubelet.pods:
+            try:
+                size = os.path.getsize(c.log_path)
+            except OSError:
+                break
+            if size > pos:
+                with open(c.log_path, "rb") as f:
+                    f.seek(pos)
+                    chunk = f.read(size - pos)
+                pos = size
+                await resp.write(chunk)
+            await asyncio.sleep(0.02)
+        await resp.write_eof()
+        return resp
+
+    # ------------------------------------------------------------------ exec / attach
+
+    async def exec_ws(self, request, ns, name, kind):
+        pod = self.store.get("", "pods", ns, name)
+        rt, c = self.kubelet.container(ns, name, request.query.get("container"))
+        if c is None or "running" not in (c.state or {}):
+            raise ApiError(400, "BadRequest", f"container not found or not running in pod {name}")
+        ws = web.WebSocketResponse(protocols=("v4.channel.k8s.io", "channel.k8s.io"), max_msg_size=0)
+        await ws.prepare(request)
+        tty = request.query.get("tty") in ("true", "1")
+        if kind == "attach":
+            await self._attach(ws, c)
+            return ws
+        cmd = request.query.getall("command", [])
+        env = self.kubelet._env(rt, c)
+        cwd = self.kubelet.workdir(c)
+        os.makedirs(cwd, exist_ok=True)
+        master = None
+        try:
+            if tty:
+                master, slave = pty.openpty()
+                proc = await asyncio.create_subprocess_exec(*cmd, cwd=cwd, env=env, stdin=slave, stdout=slave,
+                                                            stderr=slave, start_new_session=True)
+                os.close(slave)
+            else:
+                proc = await asyncio.create_subprocess_exec(*cmd, cwd=cwd, env=env, stdin=asyncio.subprocess.PIPE,
+                                                            stdout=asyncio.subprocess.PIPE,
+                                                            stderr=asyncio.subprocess.PIPE, start_new_session=True)
+        except (FileNotFoundError, PermissionError) as e:
+            await ws.send_bytes(b"\x03" + json.dumps({"status": "Failure", "message": str(e), "reason": "InternalError"}).encode())
+            await ws.close()
+            return ws
+        loop = asyncio.get_running_loop()
+
+        async def pump(reader, ch):
+            while True:
+                data = await reader.read(65536)
+                if not data:
+                    break
+                await ws.send_bytes(bytes([ch]) + data)
+
+        tasks = []
+        if tty:
+            q = asyncio.Queue()
+
+            def on_readable():
+                try:
+                    data = os.read(master, 65536)
+                except OSError:
+                    data = b""
+                if not data:
+                    try:
+                        loop.remove_reader(master)
+                    except Exception:
+                        pass
+                q.put_nowait(data)
+
+            loop.add_reader(master, on_readable)
+
+            async def pump_pty():
+                while True:
+                    try:
+                        data = await q.get()
+                    except Exception:
+                        break
+                    if not data:
+                        break
+                    await ws.send_bytes(b"\x01" + data)
+
+            tasks.append(asyncio.create_task(pump_pty()))
+        else:
+            tasks.append(asyncio.create_task(pump(proc.stdout, 1)))
+            tasks.append(asyncio.create_task(pump(proc.stderr, 2)))
+
+        async def read_ws():
+            async for msg in ws:
+                if msg.type != WSMsgType.BINARY or not msg.data:
+                    continue
+                ch, data = msg.data[0], msg.data[1:]
+                if ch == 0:
+                    if tty:
+                        os.write(master, data)
+                    elif proc.stdin and not proc.stdin.is_closing():
+                        try:
+                            proc.stdin.write(data)
+                            await proc.stdin.drain()
+                        except (ConnectionResetError, BrokenPipeError):
+                            pass
+                elif ch == 4 and tty:
+                    try:
+                        sz = json.loads(data.decode())
+                        fcntl.ioctl(master, termios.TIOCSWINSZ, struct.pack("HHHH", sz["Height"], sz["Width"], 0, 0))
+                    except Exception:
+                        pass
+            # client went away: stop the process
+            if proc.returncode is None:
+                try:
+                    os.killpg(proc.pid, 9)
+                except ProcessLookupError:
+                    pass
+
+        reader = asyncio.create_task(read_ws())
+        code = await proc.wait()
+        if tty:
+            try:
+                await asyncio.sleep(0.05)
+                loop.remove_reader(master)
+            except Exception:
+                pass
+            try:
+                while True:
+                    rest = os.read(master, 65536)
+                    if not rest:
+                        break
+                    await ws.send_bytes(b"\x01" + rest)
+            except OSError:
+                pass
+            q.put_nowait(b"")
+        await asyncio.gather(*tasks, return_exceptions=True)
+        if not ws.closed:
+            await ws.send_bytes(b"\x03" + json.dumps(_exit_status(code)).encode())
+            await ws.close()
+        reader.cancel()
+        if master is not None:
+            try:
+                os.close(master)
+            except OSError:
+                pass
+        return ws
+
+    async def _attach(self, ws, c):
+        pos = os.path.getsize(c.log_path) if os.path.exists(c.log_path) else 0
+
+        async def drain():
+            async for _ in ws:
+                pass
+
+        reader = asyncio.create_task(drain())
+        while not ws.closed and c.proc is not None:
+            try:
+                size = os.path.getsize(c.log_path)
+            except OSError:
+                break
+            if size > pos:
+                with open(c.log_path, "rb") as f:
+                    f.seek(pos)
+                    chunk = f.read(size - pos)
+                pos = size
+                await ws.send_bytes(b"\x01" + chunk)
+            await asyncio.sleep(0.02)
+        if not ws.closed:
+            await ws.send_bytes(b"\x03" + json.dumps(_exit_status(0)).encode())
+            await ws.close()
+        reader.cancel()
+
+    # ------------------------------------------------------------------ port-forward
+
+    async def portforward_ws(self, request, ns, name):
+        self.store.get("", "pods", ns, name)
+        port = int(request.query.get("ports", "0").split(",")[0])
+        ws = web.WebSocketResponse(protocols=("v4.channel.k8s.io", "portforward.k8s.io"), max_msg_size=0)
+        await ws.prepare(request)
+        hdr = struct.pack("<H", port)
+        await ws.send_bytes(b"\x00" + hdr)
+        await ws.send_bytes(b"\x01" + hdr)
+        try:
+            reader, writer = await asyncio.open_connection("127.0.0.1", port)
+        except OSError as e:
+            await ws.send_bytes(b"\x01" + f"error forwarding port {port} to pod {name}: {e}".encode())
+            await ws.close()
+            return ws
+
+        async def up():
+            while True:
+                data = await reader.read(65536)
+                if not data:
+                    break
+                await ws.send_bytes(b"\x00" + data)
+            await ws.close()
+
+        t = asyncio.create_task(up())
+        async for msg in ws:
+            if msg.type == WSMsgType.BINARY and msg.data and msg.data[0] == 0:
+                writer.write(msg.data[1:])
+                await writer.drain()
+        writer.close()
+        t.cancel()
+        return ws

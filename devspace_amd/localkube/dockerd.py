@@ -1,0 +1,318 @@
+"""Docker Engine API subset over a unix socket + local image store / registry.
+
+Serves what the devspace builder needs (reference: builder/docker/docker.go): /_ping,
+/version, /info, /auth, /build (tar context + Dockerfile), /images/{name}/push,
+/images/{name}/tag, /images/{name}/json. Images are directories (rootfs + config.json); a
+Dockerfile is interpreted instruction by instruction (FROM/WORKDIR/COPY/ADD/ENV/ARG/EXPOSE/
+CMD/ENTRYPOINT/LABEL/USER; RUN is recorded but not executed — no network on the box).
+"""
+
+from __future__ import annotations
+
+import gzip
+import hashlib
+import io
+import json
+import os
+import re
+import shlex
+import shutil
+import tarfile
+import tempfile
+
+from aiohttp import web
+
+
+def normalize(ref: str):
+    """'docker.io/library/node:8' -> ('node', '8'); digests dropped."""
+    ref = ref.split("@")[0]
+    name, tag = ref, "latest"
+    last = ref.rsplit("/", 1)[-1]
+    if ":" in last:
+        name, tag = ref.rsplit(":", 1)
+    for p in ("docker.io/library/", "docker.io/", "index.docker.io/library/", "library/"):
+        if name.startswith(p):
+            name = name[len(p):]
+    return name, tag
+
+
+class ImageStore:
+    def __init__(self, root):
+        self.root = root
+        os.makedirs(os.path.join(root, "images"), exist_ok=True)
+        os.makedirs(os.path.join(root, "registry"), exist_ok=True)
+
+    def _dir(self, kind, ref):
+        name, tag = normalize(ref)
+        return os.path.join(self.root, kind, name.replace("/", "__"), tag)
+
+    def local(self, ref):
+        d = self._dir("images", ref)
+        return d if os.path.exists(os.path.join(d, "config.json")) else None
+
+    def resolve(self, ref):
+        """Registry first (what a node would pull), then the daemon's local images."""
+        for kind in ("registry", "images"):
+            d = self._dir(kind, ref)
+            if os.path.exists(os.path.join(d, "config.json")):
+                with open(os.path.join(d, "config.json")) as f:
+                    cfg = json.load(f)
+                return {"config": cfg, "rootfs": os.path.join(d, "rootfs"), "dir": d}
+        return None
+
+    def save(self, ref, rootfs_src, config):
+        d = self._dir("images", ref)
+        if os.path.exists(d):
+            shutil.rmtree(d)
+        os.makedirs(d)
+        shutil.copytree(rootfs_src, os.path.join(d, "rootfs"), symlinks=True)
+        with open(os.path.join(d, "config.json"), "w") as f:
+            json.dump(config, f)
+        return d
+
+    def push(self, ref):
+        src = self.local(ref)
+        if not src:
+            return False
+        dst = self._dir("registry", ref)
+        if os.path.exists(dst):
+            shutil.rmtree(dst)
+        shutil.copytree(src, dst, symlinks=True)
+        return True
+
+    def tag(self, src_ref, dst_ref):
+        src = self.local(src_ref)
+        if not src:
+            return False
+        dst = self._dir("images", dst_ref)
+        if os.path.exists(dst):
+            shutil.rmtree(dst)
+        shutil.copytree(src, dst, symlinks=True)
+        return True
+
+
+def _parse_dockerfile(text):
+    lines, cur = [], ""
+    for raw in text.splitlines():
+        s = raw.rstrip()
+        if not cur and (not s.strip() or s.strip().startswith("#")):
+            continue
+        if s.endswith("\\"):
+            cur += s[:-1] + " "
+            continue
+        cur += s
+        lines.append(cur.strip())
+        cur = ""
+    if cur.strip():
+        lines.append(cur.strip())
+    out = []
+    for l in lines:
+        parts = l.split(None, 1)
+        out.append((parts[0].upper(), parts[1] if len(parts) > 1 else ""))
+    return out
+
+
+def _exec_form(arg):
+    arg = arg.strip()
+    if arg.startswith("["):
+        try:
+            return json.loads(arg)
+        except ValueError:
+            pass
+    return ["/bin/sh", "-c", arg]
+
+
+def build_image(store, context_dir, dockerfile, tag, buildargs=None, target=None, log=print):
+    with open(os.path.join(context_dir, dockerfile)) as f:
+        instrs = _parse_dockerfile(f.read())
+    args = dict(buildargs or {})
+    stages = {}
+    work = tempfile.mkdtemp(prefix="lk-build-")
+    rootfs = os.path.join(work, "rootfs")
+    os.makedirs(rootfs)
+    config = {"Env": [], "Cmd": None, "Entrypoint": None, "WorkingDir": "/", "ExposedPorts": {}, "Labels": {}}
+    stage_name = None
+    total = len(instrs)
+
+    def subst(s):
+        env = dict(args)
+        for kv in config["Env"]:
+            k, _, v = kv.partition("=")
+            env[k] = v
+        return re.sub(r"\$\{?([A-Za-z_][A-Za-z0-9_]*)\}?", lambda m: env.get(m.group(1), m.group(0)), s)
+
+    for i, (op, arg) in enumerate(instrs, 1):
+        log(f"Step {i}/{total} : {op} {arg}")
+        if op == "FROM":
+            if stage_name and target and stage_name == target:
+                break
+            parts = arg.split()
+            base = subst(parts[0])
+            stage_name = parts[2] if len(parts) >= 3 and parts[1].lower() == "as" else None
+            shutil.rmtree(rootfs)
+            os.makedirs(rootfs)
+            config = {"Env": [], "Cmd": None, "Entrypoint": None, "WorkingDir": "/", "ExposedPorts": {}, "Labels": {}}
+            if base in stages:
+                shutil.copytree(stages[base]["rootfs"], rootfs, dirs_exist_ok=True, symlinks=True)
+                config = json.loads(json.dumps(stages[base]["config"]))
+            else:
+                img = store.resolve(base)
+                if img:
+                    shutil.copytree(img["rootfs"], rootfs, dirs_exist_ok=True, symlinks=True)
+                    config.update(img["config"])
+                else:
+                    log(f" ---> using host runtime for base image {base}")
+        elif op == "WORKDIR":
+            wd = subst(arg)
+            config["WorkingDir"] = wd if wd.startswith("/") else os.path.join(config["WorkingDir"], wd)
+            os.makedirs(os.path.join(rootfs, config["WorkingDir"].lstrip("/")), exist_ok=True)
+        elif op in ("COPY", "ADD"):
+            toks = [t for t in shlex.split(subst(arg)) if not t.startswith("--chown") and not t.startswith("--chmod")]
+            from_stage = None
+            if toks and toks[0].startswith("--from="):
+                from_stage = toks.pop(0).split("=", 1)[1]
+            if toks and toks[0].startswith("["):
+                toks = json.loads(" ".join(toks))
+            srcs, dst = toks[:-1], toks[-1]
+            base_src = stages[from_stage]["rootfs"] if from_stage in stages else context_dir
+            dst_abs = dst if dst.startswith("/") else os.path.join(config["WorkingDir"], dst)
+            dst_path = os.path.join(rootfs, dst_abs.lstrip("/"))
+            for s in srcs:
+                sp = os.path.normpath(os.path.join(base_src, s.lstrip("/") if from_stage else s))
+                if os.path.isdir(sp):
+                    shutil.copytree(sp, dst_path, dirs_exist_ok=True, symlinks=True)
+                elif os.path.exists(sp):
+                    if dst.endswith("/") or len(srcs) > 1 or os.path.isdir(dst_path):
+                        os.makedirs(dst_path, exist_ok=True)
+                        shutil.copy2(sp, os.path.join(dst_path, os.path.basename(sp)))
+                    else:
+                        os.makedirs(os.path.dirname(dst_path), exist_ok=True)
+                        shutil.copy2(sp, dst_path)
+                else:
+                    raise RuntimeError(f"COPY failed: stat {s}: file does not exist")
+        elif op == "ENV":
+            a = subst(arg)
+            if "=" in a.split()[0]:
+                for kv in shlex.split(a):
+                    k, _, v = kv.partition("=")
+                    config["Env"] = [e for e in config["Env"] if not e.startswith(k + "=")] + [f"{k}={v}"]
+            else:
+                k, _, v = a.partition(" ")
+                config["Env"] = [e for e in config["Env"] if not e.startswith(k + "=")] + [f"{k}={v.strip()}"]
+        elif op == "ARG":
+            k, _, v = arg.partition("=")
+            args.setdefault(k.strip(), v.strip())
+        elif op == "EXPOSE":
+            for p in arg.split():
+                config["ExposedPorts"][p if "/" in p else p + "/tcp"] = {}
+        elif op == "CMD":
+            config["Cmd"] = _exec_form(subst(arg))
+        elif op == "ENTRYPOINT":
+            config["Entrypoint"] = _exec_form(subst(arg))
+        elif op == "LABEL":
+            for kv in shlex.split(arg):
+                k, _, v = kv.partition("=")
+                config["Labels"][k] = v
+        elif op == "RUN":
+            log(" ---> RUN recorded, not executed by the local builder (no network on this host)")
+        if stage_name:
+            stages[stage_name] = {"rootfs": rootfs + "-" + stage_name, "config": json.loads(json.dumps(config))}
+            if os.path.exists(stages[stage_name]["rootfs"]):
+                shutil.rmtree(stages[stage_name]["rootfs"])
+            shutil.copytree(rootfs, stages[stage_name]["rootfs"], symlinks=True)
+    store.save(tag, rootfs, config)
+    shutil.rmtree(work, ignore_errors=True)
+    return "sha256:" + hashlib.sha256(json.dumps(config, sort_keys=True).encode() + tag.encode()).hexdigest()
+
+
+def make_app(store: ImageStore):
+    app = web.Application(client_max_size=1024 ** 3)
+
+    async def ping(request):
+        return web.Response(text="OK")
+
+    async def version(request):
+        return web.json_response({"Version": "24.0.0-devspace-local", "ApiVersion": "1.43", "Os": "linux",
+                                  "Arch": "amd64"})
+
+    async def info(request):
+        return web.json_response({"Name": "devspace-local", "ServerVersion": "24.0.0-devspace-local",
+                                  "IndexServerAddress": "https://index.docker.io/v1/"})
+
+    async def auth(request):
+        return web.json_response({"Status": "Login Succeeded", "IdentityToken": ""})
+
+    async def build(request):
+        q = request.query
+        tag = q.get("t", "")
+        dockerfile = q.get("dockerfile", "Dockerfile")
+        buildargs = json.loads(q.get("buildargs", "{}") or "{}")
+        target = q.get("target") or None
+        body = await request.read()
+        if body[:2] == b"\x1f\x8b":
+            body = gzip.decompress(body)
+        ctx = tempfile.mkdtemp(prefix="lk-ctx-")
+        resp = web.StreamResponse(headers={"Content-Type": "application/json"})
+        await resp.prepare(request)
+
+        async def emit(obj):
+            await resp.write((json.dumps(obj) + "\r\n").encode())
+
+        try:
+            with tarfile.open(fileobj=io.BytesIO(body)) as tf:
+                tf.extractall(ctx, filter="fully_trusted") if hasattr(tarfile, "data_filter") else tf.extractall(ctx)
+            logs = []
+            image_id = build_image(store, ctx, dockerfile, tag, buildargs, target, log=logs.append)
+            for l in logs:
+                await emit({"stream": l + "\n"})
+            await emit({"aux": {"ID": image_id}})
+            await emit({"stream": f"Successfully built {image_id[7:19]}\n"})
+            await emit({"stream": f"Successfully tagged {tag}\n"})
+        except Exception as e:
+            await emit({"errorDetail": {"message": str(e)}, "error": str(e)})
+        finally:
+            shutil.rmtree(ctx, ignore_errors=True)
+        await resp.write_eof()
+        return resp
+
+    async def push(request):
+        name = request.match_info["name"]
+        tag = request.query.get("tag", "latest")
+        ref = f"{name}:{tag}"
+        resp = web.StreamResponse(headers={"Content-Type": "application/json"})
+        await resp.prepare(request)
+        if store.push(ref):
+            await resp.write(json.dumps({"status": f"The push refers to repository [{name}]"}).encode() + b"\r\n")
+            await resp.write(json.dumps({"status": "Pushed", "id": tag}).encode() + b"\r\n")
+            await resp.write(json.dumps({"status": f"{tag}: digest: sha256:{hashlib.sha256(ref.encode()).hexdigest()} size: 1"}).encode() + b"\r\n")
+        else:
+            msg = f"An image does not exist locally with the tag: {name}"
+            await resp.write(json.dumps({"errorDetail": {"message": msg}, "error": msg}).encode() + b"\r\n")
+        await resp.write_eof()
+        return resp
+
+    async def tag_image(request):
+        name = request.match_info["name"]
+        repo, tag = request.query.get("repo"), request.query.get("tag", "latest")
+        if not store.tag(name, f"{repo}:{tag}"):
+            return web.json_response({"message": f"No such image: {name}"}, status=404)
+        return web.Response(status=201)
+
+    async def inspect(request):
+        name = request.match_info["name"]
+        img = store.resolve(name)
+        if not img:
+            return web.json_response({"message": f"No such image: {name}"}, status=404)
+        return web.json_response({"Id": "sha256:" + hashlib.sha256(name.encode()).hexdigest(), "Config": img["config"],
+                                  "RepoTags": [name]})
+
+    for prefix in ("", "/v{ver}"):
+        app.router.add_get(prefix + "/_ping", ping)  # add_get also registers HEAD
+        app.router.add_get(prefix + "/version", version)
+        app.router.add_get(prefix + "/info", info)
+        app.router.add_post(prefix + "/auth", auth)
+        app.router.add_post(prefix + "/build", build)
+        app.router.add_post(prefix + "/images/{name:.+}/push", push)
+        app.router.add_post(prefix + "/images/{name:.+}/tag", tag_image)
+        app.router.add_get(prefix + "/images/{name:.+}/json", inspect)
+    return app

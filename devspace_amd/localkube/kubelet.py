@@ -1,0 +1,498 @@
+"""Process kubelet + workload controllers for the local cluster.
+
+Pods are host processes: each container gets a rootfs directory (copied from the local image
+store), runs with its working directory mapped under that root, logs to a file, and is
+restarted per restartPolicy with CrashLoopBackOff semantics. `amd.com/gpu` requests are
+scheduled against the node's GPUs and exposed via HIP_VISIBLE_DEVICES (one process per GPU
+inside the pod is the workload's business — see devspace_amd.runner).
+"""
+
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import json
+import os
+import shutil
+import signal
+import time
+
+from .store import ApiError, now_rfc3339
+
+LOCAL_ROOTS_ANNOTATION = "devspace.sh/local-roots"
+GPU_ANNOTATION = "devspace.sh/gpus"
+GPU_RESOURCE = "amd.com/gpu"
+
+# Images that stand for "the host runtime" (the local cluster runs workloads on the host's
+# python/node/rocm stack instead of pulling layers).
+HOST_IMAGES = ("rocm/pytorch", "rocm/dev", "python", "node", "ubuntu", "debian", "busybox", "alpine",
+               "devspace-local/runtime", "gcr.io/kaniko-project/executor")
+
+
+def _gpu_request(container):
+    res = container.get("resources") or {}
+    for part in ("limits", "requests"):
+        v = (res.get(part) or {}).get(GPU_RESOURCE)
+        if v is not None:
+            try:
+                return int(str(v))
+            except ValueError:
+                return 0
+    return 0
+
+
+def template_hash(template):
+    return hashlib.sha256(json.dumps(template, sort_keys=True).encode()).hexdigest()[:10]
+
+
+class Container:
+    def __init__(self, name, spec, root):
+        self.name = name
+        self.spec = spec
+        self.root = root
+        self.proc = None
+        self.restarts = 0
+        self.state = {"waiting": {"reason": "ContainerCreating"}}
+        self.last_state = {}
+        self.next_start = 0.0
+        self.log_path = root + ".log"
+        self.started_at = None
+        self.image_config = {}
+        self.fatal = None  # waiting reason that will not recover (ErrImagePull, ...)
+
+
+class PodRuntime:
+    def __init__(self, ns, name, uid, base):
+        self.ns, self.name, self.uid = ns, name, uid
+        self.dir = os.path.join(base, f"{ns}_{name}_{uid[:8]}")
+        self.containers = {}
+        self.gpus = []
+        self.deleting = False
+
+
+class Kubelet:
+    def __init__(self, store, images, state_dir, node_name="devspace-local", gpus=0, extra_env=None):
+        self.store = store
+        self.images = images
+        self.state_dir = state_dir
+        self.node_name = node_name
+        self.gpus_total = gpus
+        self.gpus_free = list(range(gpus))
+        self.pods = {}  # (ns, name) -> PodRuntime
+        self.extra_env = extra_env or {}
+        self.pods_dir = os.path.join(state_dir, "pods")
+        os.makedirs(self.pods_dir, exist_ok=True)
+        self._stop = False
+
+    # ------------------------------------------------------------ node
+
+    def register_node(self):
+        node = {
+            "apiVersion": "v1",
+            "kind": "Node",
+            "metadata": {
+                "name": self.node_name,
+                "labels": {
+                    "kubernetes.io/hostname": self.node_name,
+                    "beta.amd.com/gpu.family.AI": "1" if self.gpus_total else "0",
+                    "amd.com/gpu.product-name": "AMD_Instinct_MI355X" if self.gpus_total else "",
+                    "amd.com/gpu.device-id": "75a3" if self.gpus_total else "",
+                },
+            },
+            "status": {
+                "capacity": {"cpu": str(os.cpu_count() or 1), "memory": "64Gi", GPU_RESOURCE: str(self.gpus_total)},
+                "allocatable": {"cpu": str(os.cpu_count() or 1), "memory": "64Gi", GPU_RESOURCE: str(self.gpus_total)},
+                "conditions": [{"type": "Ready", "status": "True"}],
+                "nodeInfo": {"kubeletVersion": "v1.29.0-devspace-local", "osImage": "local processes"},
+            },
+        }
+        try:
+            self.store.create("", "nodes", "", node, "v1")
+        except ApiError:
+            pass
+
+    # ------------------------------------------------------------ events
+
+    def event(self, obj, reason, message, etype="Normal"):
+        md = obj["metadata"]
+        ns = md.get("namespace", "default")
+        name = f"{md['name']}.{int(time.time() * 1e6):x}"
+        ev = {
+            "apiVersion": "v1",
+            "kind": "Event",
+            "metadata": {"name": name, "namespace": ns},
+            "involvedObject": {"kind": obj.get("kind", "Pod"), "name": md["name"], "namespace": ns,
+                               "uid": md.get("uid"), "apiVersion": obj.get("apiVersion", "v1")},
+            "reason": reason,
+            "message": message,
+            "type": etype,
+            "count": 1,
+            "firstTimestamp": now_rfc3339(),
+            "lastTimestamp": now_rfc3339(),
+            "source": {"component": "kubelet", "host": self.node_name},
+        }
+        try:
+            self.store.create("", "events", ns, ev, "v1")
+        except ApiError:
+            pass
+
+    # ------------------------------------------------------------ controllers
+
+    def reconcile_workloads(self):
+        for group, resource in (("apps", "deployments"), ("apps", "statefulsets"), ("apps", "replicasets"),
+                                ("apps", "daemonsets")):
+            for obj in self.store.list(group, resource):
+                self._reconcile_one(group, resource, obj)
+
+    def _reconcile_one(self, group, resource, obj):
+        md = obj["metadata"]
+        ns = md["namespace"]
+        spec = obj.get("spec", {})
+        template = spec.get("template", {})
+        replicas = 1 if resource == "daemonsets" else int(spec.get("replicas", 1) if spec.get("replicas") is not None else 1)
+        h = template_hash(template)
+        owned = [o for (k, o) in self.store.owned_by(md["uid"]) if k[1] == "pods"]
+        current = [p for p in owned if p["metadata"].get("labels", {}).get("pod-template-hash") == h
+                   and not p["metadata"].get("deletionTimestamp")]
+        stale = [p for p in owned if p["metadata"].get("labels", {}).get("pod-template-hash") != h]
+        for p in stale:  # Recreate strategy: the local cluster has no surge capacity worth modelling
+            if not p["metadata"].get("deletionTimestamp"):
+                self.store.mark_deleting("", "pods", ns, p["metadata"]["name"])
+        for p in current[replicas:]:
+            self.store.mark_deleting("", "pods", ns, p["metadata"]["name"])
+        current = current[:replicas]
+        names = {p["metadata"]["name"] for p in current}
+        for i in range(len(current), replicas):
+            if resource == "statefulsets":
+                name = f"{md['name']}-{i}"
+                while name in names:
+                    i += 1
+                    name = f"{md['name']}-{i}"
+                if self.store.try_get("", "pods", ns, name):
+                    continue  # old ordinal still terminating
+            else:
+                name = f"{md['name']}-{h[:8]}-{os.urandom(3).hex()[:5]}"
+            names.add(name)
+            pmd = dict(template.get("metadata") or {})
+            labels = dict(pmd.get("labels") or {})
+            labels["pod-template-hash"] = h
+            pod = {
+                "apiVersion": "v1",
+                "kind": "Pod",
+                "metadata": {
+                    "name": name,
+                    "namespace": ns,
+                    "labels": labels,
+                    "annotations": dict(pmd.get("annotations") or {}),
+                    "ownerReferences": [{"apiVersion": obj.get("apiVersion", "apps/v1"), "kind": obj.get("kind"),
+                                         "name": md["name"], "uid": md["uid"], "controller": True}],
+                },
+                "spec": json.loads(json.dumps(template.get("spec") or {})),
+                "status": {"phase": "Pending"},
+            }
+            try:
+                self.store.create("", "pods", ns, pod, "v1")
+                self.event(obj, "SuccessfulCreate", f"Created pod: {name}")
+            except ApiError:
+                pass
+        ready = 0
+        for p in current:
+            st = p.get("status", {})
+            if st.get("phase") == "Running" and all(c.get("ready") for c in st.get("containerStatuses", []) or [{}]):
+                ready += 1
+        status = {"observedGeneration": md.get("generation", 1), "replicas": len(current),
+                  "readyReplicas": ready, "availableReplicas": ready, "updatedReplicas": len(current),
+                  "currentReplicas": len(current)}
+        if obj.get("status") != status:
+            self.store.update_status(group, resource, ns, md["name"], status)
+
+    def reconcile_pvcs(self):
+        for pvc in self.store.list("", "persistentvolumeclaims"):
+            if (pvc.get("status") or {}).get("phase") != "Bound":
+                self.store.update_status("", "persistentvolumeclaims", pvc["metadata"]["namespace"],
+                                         pvc["metadata"]["name"], {"phase": "Bound"})
+
+    # ------------------------------------------------------------ pods
+
+    async def reconcile_pods(self):
+        seen = set()
+        for pod in self.store.list("", "pods"):
+            md = pod["metadata"]
+            key = (md["namespace"], md["name"])
+            seen.add(key)
+            rt = self.pods.get(key)
+            if md.get("deletionTimestamp"):
+                await self._delete_pod(key, pod)
+                continue
+            if rt is None:
+                rt = self._admit(pod)
+                if rt is None:
+                    continue
+            await self._sync_containers(rt, pod)
+        for key in list(self.pods):
+            if key not in seen:  # removed from the store without graceful deletion
+                await self._kill_pod(self.pods.pop(key), 0)
+
+    def _admit(self, pod):
+        md = pod["metadata"]
+        containers = pod.get("spec", {}).get("containers", []) or []
+        want = sum(_gpu_request(c) for c in containers)
+        if want > len(self.gpus_free):
+            st = pod.get("status") or {}
+            if st.get("reason") != "Unschedulable":
+                msg = f"0/1 nodes are available: 1 Insufficient {GPU_RESOURCE}."
+                self.store.update_status("", "pods", md["namespace"], md["name"], {
+                    "phase": "Pending", "conditions": [{"type": "PodScheduled", "status": "False",
+                                                        "reason": "Unschedulable", "message": msg}]})
+                self.event(pod, "FailedScheduling", msg, "Warning")
+            return None
+        rt = PodRuntime(md["namespace"], md["name"], md["uid"], self.pods_dir)
+        rt.gpus = [self.gpus_free.pop(0) for _ in range(want)]
+        os.makedirs(rt.dir, exist_ok=True)
+        roots = {}
+        for c in containers:
+            root = os.path.join(rt.dir, c["name"])
+            os.makedirs(root, exist_ok=True)
+            rt.containers[c["name"]] = Container(c["name"], c, root)
+            roots[c["name"]] = root
+
+        def annotate(o):
+            o["metadata"].setdefault("annotations", {})[LOCAL_ROOTS_ANNOTATION] = json.dumps(roots)
+            if rt.gpus:
+                o["metadata"]["annotations"][GPU_ANNOTATION] = ",".join(map(str, rt.gpus))
+            o["spec"]["nodeName"] = self.node_name
+
+        self.store.mutate("", "pods", md["namespace"], md["name"], annotate)
+        self.event(pod, "Scheduled", f"Successfully assigned {md['namespace']}/{md['name']} to {self.node_name}")
+        self.pods[(md["namespace"], md["name"])] = rt
+        return rt
+
+    def _prepare_rootfs(self, rt, c, pod):
+        image = c.spec.get("image", "")
+        img = self.images.resolve(image)
+        if img is None:
+            if not image or not any(image.split("@")[0].split(":")[0].endswith(h) or image.startswith(h)
+                                    for h in HOST_IMAGES):
+                return "ErrImagePull", f'Failed to pull image "{image}": not found in the local registry'
+            img = {"config": {}, "rootfs": None}
+        else:
+            self.event(pod, "Pulled", f'Container image "{image}" present in local registry')
+        c.image_config = img.get("config") or {}
+        if img.get("rootfs") and os.path.isdir(img["rootfs"]):
+            shutil.copytree(img["rootfs"], c.root, symlinks=True, dirs_exist_ok=True)
+        for vm in c.spec.get("volumeMounts") or []:
+            self._mount(rt, pod, c, vm)
+        return None, None
+
+    def _mount(self, rt, pod, c, vm):
+        vols = {v["name"]: v for v in pod.get("spec", {}).get("volumes") or []}
+        v = vols.get(vm.get("name"), {})
+        target = os.path.join(c.root, vm.get("mountPath", "/").lstrip("/"))
+        if v.get("persistentVolumeClaim"):
+            src = os.path.join(self.state_dir, "volumes", rt.ns, v["persistentVolumeClaim"]["claimName"],
+                               (vm.get("subPath") or "").lstrip("/"))
+        else:
+            src = os.path.join(rt.dir, "volumes", vm.get("name", "v"), (vm.get("subPath") or "").lstrip("/"))
+        os.makedirs(src, exist_ok=True)
+        if os.path.islink(target) or os.path.exists(target):
+            return
+        os.makedirs(os.path.dirname(target), exist_ok=True)
+        os.symlink(src, target)
+
+    def _argv(self, c):
+        spec, cfg = c.spec, c.image_config
+        cmd, args = spec.get("command"), spec.get("args")
+        if cmd:
+            argv = list(cmd) + list(args or [])
+        elif args:
+            argv = list(cfg.get("Entrypoint") or []) + list(args)
+        else:
+            argv = list(cfg.get("Entrypoint") or []) + list(cfg.get("Cmd") or [])
+        out = []
+        for a in argv:
+            a = str(a)
+            if a.startswith("/") and len(a) > 1:
+                first = a.lstrip("/").split("/", 1)[0]
+                if first and os.path.exists(os.path.join(c.root, first)):
+                    a = os.path.join(c.root, a.lstrip("/"))
+            out.append(a)
+        return out
+
+    def _env(self, rt, c):
+        env = dict(os.environ)
+        env.update(self.extra_env)
+        for kv in c.image_config.get("Env") or []:
+            if "=" in kv:
+                k, v = kv.split("=", 1)
+                env[k] = v
+        for e in c.spec.get("env") or []:
+            if "value" in e:
+                env[e["name"]] = str(e["value"])
+        env["HOSTNAME"] = rt.name
+        env["DEVSPACE_CONTAINER_ROOT"] = c.root
+        env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, rt.gpus)) if rt.gpus else env.get("HIP_VISIBLE_DEVICES", "")
+        if not rt.gpus:
+            env["HIP_VISIBLE_DEVICES"] = "-1" if self.gpus_total else env["HIP_VISIBLE_DEVICES"]
+        if not env["HIP_VISIBLE_DEVICES"]:
+            env.pop("HIP_VISIBLE_DEVICES")
+        return env
+
+    def workdir(self, c):
+        wd = c.spec.get("workingDir") or c.image_config.get("WorkingDir") or "/"
+        return os.path.join(c.root, wd.lstrip("/"))
+
+    async def _start(self, rt, c, pod):
+        argv = self._argv(c)
+        if not argv:
+            c.state = {"waiting": {"reason": "CreateContainerConfigError", "message": "no command specified"}}
+            c.fatal = "CreateContainerConfigError"
+            return
+        cwd = self.workdir(c)
+        os.makedirs(cwd, exist_ok=True)
+        logf = open(c.log_path, "ab", buffering=0)
+        try:
+            c.proc = await asyncio.create_subprocess_exec(*argv, cwd=cwd, env=self._env(rt, c), stdout=logf,
+                                                          stderr=logf, stdin=asyncio.subprocess.DEVNULL,
+                                                          start_new_session=True)
+        except (FileNotFoundError, PermissionError) as e:
+            c.state = {"waiting": {"reason": "RunContainerError", "message": str(e)}}
+            c.next_start = time.time() + min(30.0, 0.5 * (2 ** c.restarts))
+            c.restarts += 1
+            logf.close()
+            self.event(pod, "Failed", f"Error: {e}", "Warning")
+            return
+        finally:
+            if c.proc is not None:
+                logf.close()
+        c.started_at = now_rfc3339()
+        c.state = {"running": {"startedAt": c.started_at}}
+        self.event(pod, "Started", f"Started container {c.name}")
+
+    async def _sync_containers(self, rt, pod):
+        changed = False
+        for name, c in rt.containers.items():
+            if c.fatal:
+                continue
+            if c.proc is None and c.started_at is None and c.restarts == 0 and not c.next_start:
+                reason, msg = self._prepare_rootfs(rt, c, pod)
+                if reason:
+                    c.state = {"waiting": {"reason": reason, "message": msg}}
+                    c.fatal = reason
+                    self.event(pod, "Failed", msg, "Warning")
+                    changed = True
+                    continue
+                await self._start(rt, c, pod)
+                changed = True
+            elif c.proc is not None and c.proc.returncode is not None:
+                code = c.proc.returncode
+                c.last_state = {"terminated": {"exitCode": code, "reason": "Completed" if code == 0 else "Error",
+                                               "startedAt": c.started_at, "finishedAt": now_rfc3339()}}
+                c.proc = None
+                policy = pod.get("spec", {}).get("restartPolicy", "Always")
+                if policy == "Never" or (policy == "OnFailure" and code == 0):
+                    c.state = dict(c.last_state)
+                else:
+                    c.restarts += 1
+                    delay = min(30.0, 0.5 * (2 ** (c.restarts - 1)))
+                    c.next_start = time.time() + delay
+                    c.state = {"waiting": {"reason": "CrashLoopBackOff",
+                                           "message": f"back-off {delay:.1f}s restarting failed container={name}"}}
+                    self.event(pod, "BackOff", f"Back-off restarting failed container {name}", "Warning")
+                changed = True
+            elif c.proc is None and c.next_start and time.time() >= c.next_start:
+                c.next_start = 0.0
+                await self._start(rt, c, pod)
+                changed = True
+        if changed or not (pod.get("status") or {}).get("containerStatuses"):
+            self._write_status(rt, pod)
+
+    def _write_status(self, rt, pod):
+        statuses = []
+        all_running = True
+        any_fatal = None
+        for c in rt.containers.values():
+            running = "running" in c.state
+            all_running &= running
+            if c.fatal:
+                any_fatal = c.fatal
+            statuses.append({"name": c.name, "ready": running, "restartCount": c.restarts,
+                             "image": c.spec.get("image", ""), "imageID": "", "containerID": f"local://{c.name}",
+                             "state": c.state, "lastState": c.last_state, "started": running})
+        phase = "Running" if all_running else "Pending"
+        if not all_running and any("terminated" in s["state"] for s in statuses) and all(
+                "terminated" in s["state"] for s in statuses):
+            phase = "Succeeded" if all(s["state"]["terminated"]["exitCode"] == 0 for s in statuses) else "Failed"
+        status = {
+            "phase": phase,
+            "hostIP": "127.0.0.1",
+            "podIP": "127.0.0.1",
+            "startTime": pod["metadata"].get("creationTimestamp"),
+            "conditions": [{"type": "PodScheduled", "status": "True"},
+                           {"type": "Ready", "status": "True" if all_running else "False"},
+                           {"type": "ContainersReady", "status": "True" if all_running else "False"}],
+            "containerStatuses": statuses,
+        }
+        self.store.update_status("", "pods", rt.ns, rt.name, status)
+
+    async def _kill_pod(self, rt, grace):
+        procs = [c.proc for c in rt.containers.values() if c.proc and c.proc.returncode is None]
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        deadline = time.time() + grace
+        for p in procs:
+            try:
+                await asyncio.wait_for(p.wait(), timeout=max(0.05, deadline - time.time()))
+            except asyncio.TimeoutError:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                await p.wait()
+        self.gpus_free.extend(rt.gpus)
+        self.gpus_free.sort()
+        rt.gpus = []
+        shutil.rmtree(rt.dir, ignore_errors=True)
+        for c in rt.containers.values():
+            try:
+                os.unlink(c.log_path)
+            except OSError:
+                pass
+
+    async def _delete_pod(self, key, pod):
+        rt = self.pods.pop(key, None)
+        if rt is not None:
+            grace = min(5, int(pod.get("spec", {}).get("terminationGracePeriodSeconds", 5) or 0))
+            await self._kill_pod(rt, grace)
+        try:
+            self.store.delete("", "pods", key[0], key[1])
+        except ApiError:
+            pass
+
+    # ------------------------------------------------------------ helpers for the API server
+
+    def container(self, ns, pod, name):
+        rt = self.pods.get((ns, pod))
+        if rt is None:
+            return None, None
+        if not name:
+            name = next(iter(rt.containers), None)
+        return rt, rt.containers.get(name)
+
+    async def run(self):
+        self.register_node()
+        while not self._stop:
+            try:
+                self.reconcile_workloads()
+                self.reconcile_pvcs()
+                await self.reconcile_pods()
+            except Exception as e:  # keep the node alive; surface in the log
+                print(f"[localkube] reconcile error: {e!r}", flush=True)
+            await asyncio.sleep(0.05)
+
+    async def shutdown(self):
+        self._stop = True
+        for key in list(self.pods):
+            await self._kill_pod(self.pods.pop(key), 1)

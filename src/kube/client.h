@@ -1,0 +1,157 @@
+// Kubernetes API client: REST over HTTP/1.1(+TLS), exec/attach/port-forward over the
+// WebSocket channel protocols (v4.channel.k8s.io, portforward.k8s.io), pod status logic.
+//
+// Reference equivalents: kubectl/client.go (NewClient, getClientConfig, GetNewestRunningPod,
+// GetPodStatus), kubectl/exec.go (ExecStream*), kubectl/attach.go, kubectl/logs.go,
+// kubectl/util.go (EnsureDefaultNamespace, EnsureGoogleCloudClusterRoleBinding),
+// kubectl/client.go:356 (NewPortForwarder). client-go/SPDY are replaced by native code.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <memory>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "core/net.h"
+#include "core/proc.h"
+#include "core/value.h"
+#include "kube/kubeconfig.h"
+#include "sync/transport.h"
+
+namespace ds {
+namespace kube {
+
+struct ApiError : std::runtime_error {
+  int code;
+  std::string reason;
+  ApiError(int c, const std::string& r, const std::string& msg) : std::runtime_error(msg), code(c), reason(r) {}
+  bool not_found() const { return code == 404; }
+  bool conflict() const { return code == 409; }
+};
+
+// Pod status string exactly like `kubectl get pods` (kubectl/client.go:224 GetPodStatus).
+std::string pod_status(const Value& pod);
+bool pod_status_is_fatal(const std::string& status);
+
+// REST path for a manifest object (apiVersion/kind/namespace/name).
+std::string resource_path(const std::string& api_version, const std::string& kind, const std::string& ns,
+                          const std::string& name = "");
+std::string plural_of(const std::string& kind);
+bool is_cluster_scoped(const std::string& kind);
+
+class ExecSession;
+
+class Client {
+ public:
+  explicit Client(RestConfig cfg);
+  // getClientConfig semantics (kubectl/client.go:63): devspace config cluster.* or kube
+  // context (optionally switching the current context in ~/.kube/config).
+  static std::shared_ptr<Client> from_devspace_config(const Value& cfg, bool switch_context = false);
+
+  const RestConfig& rest() const { return cfg_; }
+  std::string default_namespace() const { return cfg_.namespace_.empty() ? "default" : cfg_.namespace_; }
+  bool is_local_cluster() const;  // devspace local cluster (process pods)
+  bool is_minikube() const { return cfg_.context == "minikube"; }
+
+  // REST (JSON bodies). Throw ApiError on non-2xx.
+  Value get(const std::string& path);
+  Value post(const std::string& path, const Value& body);
+  Value put(const std::string& path, const Value& body);
+  Value patch(const std::string& path, const Value& body,
+              const std::string& type = "application/merge-patch+json");
+  Value del(const std::string& path, const Value& body = Value());
+  // Returns nullopt for 404.
+  std::optional<Value> try_get(const std::string& path);
+  net::Response raw(const std::string& method, const std::string& path, const std::string& body = "",
+                    const std::string& content_type = "application/json", int timeout_ms = 60000);
+  // Stream a GET (logs -f, watch).
+  int stream(const std::string& path, const std::function<bool(const std::string&)>& on_data, int timeout_ms = -1);
+
+  // Pods
+  std::vector<Value> list_pods(const std::string& ns, const std::string& label_selector);
+  // Newest pod by creationTimestamp that is Running; fails fast on fatal states
+  // (kubectl/client.go:171). poll_ms: 1000 reproduces the reference's 1 s sleeps.
+  Value newest_running_pod(const std::string& ns, const std::string& label_selector, int max_wait_ms,
+                           int poll_ms = 100);
+  std::string logs(const std::string& ns, const std::string& pod, const std::string& container, int tail,
+                   bool previous = false);
+
+  // Namespaces / RBAC helpers (kubectl/util.go)
+  void ensure_namespace(const std::string& ns);
+  void ensure_gcloud_cluster_role_binding();
+
+  // Apply a manifest (create or replace; services keep their clusterIP; immutable-field
+  // conflicts fall back to delete + create, i.e. `kubectl apply --force`).
+  Value apply(Value obj, const std::string& default_ns);
+  bool delete_object(const Value& obj, const std::string& default_ns);
+
+  // Streams
+  std::unique_ptr<ExecSession> exec(const std::string& ns, const std::string& pod, const std::string& container,
+                                    const std::vector<std::string>& cmd, bool tty, bool stdin = true);
+  std::unique_ptr<ExecSession> attach(const std::string& ns, const std::string& pod, const std::string& container,
+                                      bool tty, bool stdin = false);
+  std::unique_ptr<net::WebSocket> portforward(const std::string& ns, const std::string& pod, int port);
+
+  net::HttpClient& http() { return http_; }
+
+ private:
+  void refresh_exec_token();
+  RestConfig cfg_;
+  net::HttpClient http_;
+};
+
+// A running exec/attach: stdin/stdout/stderr exposed as pipes (so the sync engine and the
+// terminal proxy can poll() them), remote exit code from the error channel.
+class ExecSession : public sync::Shell {
+ public:
+  ExecSession(std::unique_ptr<net::WebSocket> ws, bool tty);
+  ~ExecSession() override;
+  int in() override { return in_w_.get(); }
+  int out() override { return out_r_.get(); }
+  int err() override { return err_r_.get(); }
+  bool alive() override { return !done_; }
+  void terminate() override;
+  void close() override;
+  void resize(int width, int height);
+  // Waits for the remote process; returns its exit code (or -1 if unknown / stream died).
+  int wait(int timeout_ms = -1);
+  std::string error_message();
+
+ private:
+  void pump_in();
+  void pump_out();
+  std::unique_ptr<net::WebSocket> ws_;
+  bool tty_;
+  Fd in_r_, in_w_, out_r_, out_w_, err_r_, err_w_;
+  std::thread t_in_, t_out_;
+  std::atomic<bool> done_{false};
+  std::atomic<int> exit_code_{-1};
+  std::string error_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+};
+
+// sync::Transport running `sh` in a pod container via exec. Pods of the devspace local
+// cluster carry the annotation devspace.sh/local-root; container paths are mapped under it.
+class ExecTransport : public sync::Transport {
+ public:
+  ExecTransport(std::shared_ptr<Client> c, Value pod, std::string container);
+  std::unique_ptr<sync::Shell> open(const std::vector<std::string>& argv) override;
+  std::string describe() const override { return "exec(" + pod_name_ + "/" + container_ + ")"; }
+  std::string path_prefix() const override { return prefix_; }
+
+ private:
+  std::shared_ptr<Client> c_;
+  std::string ns_, pod_name_, container_, prefix_;
+};
+
+extern const char* const kLocalRootAnnotation;  // "devspace.sh/local-root"
+
+}  // namespace kube
+}  // namespace ds
