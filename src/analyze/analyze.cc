@@ -1,0 +1,292 @@
+#include "analyze/analyze.h"
+
+#include <time.h>
+
+#include <chrono>
+#include <regex>
+#include <thread>
+
+#include "core/log.h"
+#include "core/strutil.h"
+
+namespace ds {
+namespace analyze {
+
+static const int kHeaderWidth = 52;
+static const std::string kPad = "  ";
+
+static int64_t parse_time(const std::string& ts) {
+  struct tm t{};
+  if (ts.size() < 19 || !strptime(ts.c_str(), "%Y-%m-%dT%H:%M:%S", &t)) return 0;
+  return (int64_t)timegm(&t);
+}
+
+static std::string human_age(int64_t secs) {
+  if (secs < 0) secs = 0;
+  if (secs < 60) return std::to_string(secs) + "s";
+  if (secs < 3600) return std::to_string(secs / 60) + "m" + std::to_string(secs % 60) + "s";
+  return std::to_string(secs / 3600) + "h" + std::to_string((secs % 3600) / 60) + "m";
+}
+
+static bool is_okay(const std::string& s) { return s == "Completed" || s == "Running"; }
+
+std::vector<std::string> events_problems(kube::Client& k, const std::string& ns) {
+  std::vector<std::string> out;
+  Value evs = k.get("/api/v1/namespaces/" + ns + "/events");
+  for (auto& e : evs.get("items").items()) {
+    if (e.get("type").as_string() == "Normal") continue;
+    const Value& io = e.get("involvedObject");
+    std::string av = io.get("apiVersion").as_string("v1");
+    std::string path = kube::resource_path(av, io.get("kind").as_string(), ns, io.get("name").as_string());
+    if (!k.try_get(path)) continue;  // only objects that still exist
+    std::string header = log::color(e.get("type").as_string() + " - " + io.get("kind").as_string() + " " +
+                                        io.get("name").as_string() + ": ",
+                                    "202+b");
+    out.push_back(kPad + header + "\n" + kPad + std::to_string(e.get("count").as_int(1)) + "x " +
+                  e.get("message").as_string() + " \n");
+  }
+  return out;
+}
+
+bool log_has_gpu_runtime_error(const std::string& text, std::string* match) {
+  static const std::regex re(
+      "(hipErrorNoDevice|hipErrorInvalidDevice|hipErrorOutOfMemory|HIP error|HSA_STATUS_ERROR[A-Z_]*|"
+      "No HIP GPUs are available|RuntimeError: No CUDA GPUs are available|"
+      "rccl.*(error|failed)|NCCL error|ncclSystemError|ncclInternalError|ncclUnhandledCudaError|"
+      "amdgpu.ids: No such file|Unable to open /dev/kfd|/dev/kfd: (Permission denied|No such file)|"
+      "torch.OutOfMemoryError|HIP out of memory)",
+      std::regex::icase);
+  std::smatch m;
+  if (std::regex_search(text, m, re)) {
+    if (match) *match = m.str(0);
+    // amdgpu.ids is a benign warning on most images
+    if (contains(m.str(0), "amdgpu.ids")) return false;
+    return true;
+  }
+  return false;
+}
+
+static int64_t gpu_request(const Value& pod) {
+  int64_t n = 0;
+  for (auto& c : pod.at_path("spec.containers").items()) {
+    const Value& lim = c.at_path("resources.limits").get("amd.com/gpu");
+    const Value& req = c.at_path("resources.requests").get("amd.com/gpu");
+    n += !lim.is_null() ? lim.as_int() : req.as_int();
+  }
+  return n;
+}
+
+std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, const std::vector<Value>& pods,
+                                      const Options& o) {
+  std::vector<std::string> out;
+  int64_t requested = 0;
+  for (auto& p : pods) requested += gpu_request(p);
+  if (requested == 0) return out;
+  // node capacity as advertised by the AMD GPU device plugin
+  int64_t max_alloc = 0, total = 0;
+  std::vector<std::string> products;
+  try {
+    for (auto& n : k.get("/api/v1/nodes").get("items").items()) {
+      int64_t a = n.at_path("status.allocatable").get("amd.com/gpu").as_int(0);
+      total += a;
+      max_alloc = std::max(max_alloc, a);
+      std::string prod = n.at_path("metadata.labels").get("amd.com/gpu.product-name").as_string();
+      if (!prod.empty()) products.push_back(prod);
+    }
+  } catch (const std::exception&) {
+    // listing nodes may be forbidden for namespace-scoped users
+    max_alloc = -1;
+  }
+  if (max_alloc == 0)
+    out.push_back(kPad + log::color("GPU: ", "202+b") +
+                  "no node advertises amd.com/gpu — is the AMD GPU device plugin DaemonSet running?\n");
+  for (auto& p : pods) {
+    int64_t want = gpu_request(p);
+    if (want == 0) continue;
+    std::string name = p.at_path("metadata.name").as_string();
+    if (max_alloc > 0 && want > max_alloc)
+      out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + " requests amd.com/gpu: " +
+                    std::to_string(want) + " but the largest node has " + std::to_string(max_alloc) +
+                    " (MI355X nodes expose 8 GPUs; HBM is not a schedulable resource)\n");
+    for (auto& c : p.at_path("status.containerStatuses").items()) {
+      bool crashed = c.get("restartCount").as_int() > 0 || !c.at_path("state.terminated").is_null();
+      if (!crashed) continue;
+      std::string text;
+      try {
+        text = k.logs(ns, name, c.get("name").as_string(), 200, c.get("restartCount").as_int() > 0);
+      } catch (...) {
+        continue;
+      }
+      std::string m;
+      if (log_has_gpu_runtime_error(text, &m))
+        out.push_back(kPad + log::color("GPU: ", "202+b") + "container " + c.get("name").as_string() + " of pod " +
+                      name + " failed with a ROCm/HIP/RCCL error: " + m + "\n");
+    }
+    if (o.gpu_probe && kube::pod_status(p) == "Running") {
+      std::string c = p.at_path("spec.containers")[0].get("name").as_string();
+      try {
+        auto s = k.exec(ns, name, c, {"sh", "-c", "ls /dev/kfd >/dev/null 2>&1 || echo NOKFD; python3 -m devspace_amd.gpucheck --quick --json 2>/dev/null || true"}, false, false);
+        s->close_stdin_if_any();
+        std::string outp = read_all(s->out());
+        s->wait(60000);
+        if (contains(outp, "NOKFD") && !contains(outp, "\"devices\": [{"))
+          out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + " has no /dev/kfd (GPU not attached)\n");
+        size_t j = outp.find('{');
+        if (j != std::string::npos) {
+          Value rep = json_parse(outp.substr(j));
+          for (auto& pr : rep.get("problems").items())
+            out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + pr.as_string() + "\n");
+        }
+      } catch (const std::exception& e) {
+        log::debug(std::string("gpu probe failed: ") + e.what());
+      }
+    }
+  }
+  return out;
+}
+
+std::vector<std::string> pods_problems(kube::Client& k, const std::string& ns, const Options& o,
+                                       std::vector<Value>* pods_out) {
+  std::vector<std::string> out;
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<Value> pods;
+  while (true) {
+    pods = k.list_pods(ns, "");
+    bool waiting = false;
+    int64_t now = (int64_t)time(nullptr);
+    for (auto& p : pods) {
+      std::string st = kube::pod_status(p);
+      int64_t age = now - parse_time(p.at_path("metadata.creationTimestamp").as_string());
+      if (st == "ContainerCreating" || st == "Pending" || st == "Terminating" || age < o.min_pod_age_s) {
+        // Pending because of GPU scheduling will not resolve by waiting
+        if (st == "Pending" && contains(p.at_path("status.conditions").size() ? json_dump(p.at_path("status.conditions")) : "",
+                                        "Unschedulable"))
+          continue;
+        waiting = true;
+      }
+    }
+    auto el = std::chrono::duration_cast<std::chrono::seconds>(std::chrono::steady_clock::now() - t0).count();
+    if (!o.wait || !waiting || el >= o.wait_timeout_s) break;
+    log::start_wait("Waiting for pods to become ready");
+    std::this_thread::sleep_for(std::chrono::milliseconds(500));
+  }
+  log::stop_wait();
+  int64_t now = (int64_t)time(nullptr);
+  for (auto& p : pods) {
+    std::string name = p.at_path("metadata.name").as_string();
+    std::string st = kube::pod_status(p);
+    std::vector<std::string> cps;
+    int ready = 0, total = 0;
+    bool problem = !is_okay(st) && !starts_with(st, "Init");
+    for (auto& c : p.at_path("status.containerStatuses").items()) {
+      ++total;
+      if (c.get("ready").as_bool()) ++ready;
+      std::vector<std::string> lines;
+      bool cp = false;
+      int64_t restarts = c.get("restartCount").as_int();
+      const Value& last = c.at_path("lastState.terminated");
+      if (restarts > 0 && last.is_map() &&
+          (restarts > 4 || now - parse_time(last.get("finishedAt").as_string()) < 7200)) {
+        cp = true;
+        lines.push_back("        Restarts: " + log::color(std::to_string(restarts), "red+b"));
+        lines.push_back("        Last Restart: " +
+                        log::color(human_age(now - parse_time(last.get("finishedAt").as_string())), "white+b") + " ago");
+        if (last.get("exitCode").as_int() != 0) {
+          lines.push_back("        Last Exit: " + log::color(last.get("reason").as_string(), "red+b") + " (Code: " +
+                          log::color(std::to_string(last.get("exitCode").as_int()), "red+b") + ")");
+          try {
+            std::string lg = k.logs(ns, name, c.get("name").as_string(), 50, true);
+            if (!lg.empty()) lines.push_back("        Last Execution Log: \n" + lg);
+          } catch (...) {
+          }
+        }
+      }
+      if (!c.get("ready").as_bool()) {
+        cp = true;
+        const Value& term = c.at_path("state.terminated");
+        const Value& wait = c.at_path("state.waiting");
+        if (term.is_map()) {
+          lines.push_back("        Status: " + log::color("Terminated", "red+b") + " (reason: " +
+                          log::color(term.get("reason").as_string(), "red+b") + ")");
+        } else if (wait.is_map()) {
+          lines.push_back("        Status: " + log::color("Waiting", "red+b") + " (reason: " +
+                          log::color(wait.get("reason").as_string(), "red+b") + ")");
+          if (!wait.get("message").as_string().empty())
+            lines.push_back("        Message: " + log::color(wait.get("message").as_string(), "white+b"));
+        }
+      }
+      if (cp) {
+        problem = true;
+        cps.push_back("      - Container: " + log::color(c.get("name").as_string(), "white+b"));
+        for (auto& l : lines) cps.push_back(l);
+      }
+    }
+    if (st == "Pending") {
+      for (auto& cond : p.at_path("status.conditions").items())
+        if (cond.get("reason").as_string() == "Unschedulable")
+          cps.push_back("      - Scheduling: " + log::color(cond.get("message").as_string(), "red+b"));
+    }
+    if (!problem) continue;
+    std::string color = is_okay(st) ? "green+b" : kube::pod_status_is_fatal(st) ? "red+b" : "yellow+b";
+    std::string s = kPad + "Pod " + log::color(name, "white+b") + ":\n";
+    s += kPad + "    Status: " + log::color(st, color) + "\n";
+    s += kPad + "    Created: " + log::color(human_age(now - parse_time(p.at_path("metadata.creationTimestamp").as_string())), "white+b") + " ago\n";
+    if (total > 0) {
+      std::string r = std::to_string(ready);
+      if (ready != total) r = log::color(r, "red+b");
+      s += kPad + "    Container: " + r + "/" + std::to_string(total) + " running\n";
+    }
+    if (!cps.empty()) {
+      s += kPad + "    Problems: \n";
+      for (auto& l : cps) s += kPad + l + "\n";
+    }
+    out.push_back(s);
+  }
+  if (pods_out) *pods_out = pods;
+  return out;
+}
+
+std::vector<ReportItem> create_report(kube::Client& k, const std::string& ns, const Options& o) {
+  std::vector<ReportItem> report;
+  log::start_wait("Analyzing events");
+  std::vector<std::string> ev;
+  try {
+    ev = events_problems(k, ns);
+  } catch (const std::exception& e) {
+    log::stop_wait();
+    throw std::runtime_error(std::string("Error during analyzing events: ") + e.what());
+  }
+  log::stop_wait();
+  if (!ev.empty()) report.push_back({"Events", ev});
+  std::vector<Value> pods;
+  auto pp = pods_problems(k, ns, o, &pods);
+  if (!pp.empty()) report.push_back({"Pods", pp});
+  auto gp = gpu_problems(k, ns, pods, o);
+  if (!gp.empty()) report.push_back({"GPUs", gp});
+  return report;
+}
+
+std::string report_to_string(const std::vector<ReportItem>& report) {
+  if (report.empty())
+    return "\n" + kPad + "No problems found.\n" + kPad + "Run `" + log::color("devspace logs -p", "white+b") +
+           "` if you want show pod logs\n\n";
+  std::string out = "\n";
+  for (auto& item : report) {
+    std::string header = " " + item.name + " (" + std::to_string(item.problems.size()) + " potential issue(s)) ";
+    if (header.size() % 2 == 1) header += " ";
+    int padding = kHeaderWidth - (int)header.size();
+    header = std::string(padding / 2, ' ') + header + std::string(padding / 2, ' ');
+    out += log::color(kPad + std::string(kHeaderWidth, '=') + "\n" + kPad + header + "\n" + kPad +
+                          std::string(kHeaderWidth, '=') + "\n",
+                      "green+b");
+    for (auto& p : item.problems) out += p + "\n";
+  }
+  return out;
+}
+
+std::string analyze(kube::Client& k, const std::string& ns, const Options& o) {
+  return report_to_string(create_report(k, ns, o));
+}
+
+}  // namespace analyze
+}  // namespace ds

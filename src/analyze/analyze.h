@@ -1,0 +1,39 @@
+// Namespace problem report (pkg/devspace/analyze): non-Normal events of live objects,
+// pods with abnormal status, restarts, crash logs — plus MI355X checks: GPU scheduling
+// (Insufficient amd.com/gpu, node allocatable), missing device plugin, ROCm/HIP/RCCL
+// start-up errors in container logs, and (optionally) an in-pod GPU probe.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kube/client.h"
+
+namespace ds {
+namespace analyze {
+
+struct ReportItem {
+  std::string name;
+  std::vector<std::string> problems;
+};
+
+struct Options {
+  bool wait = true;          // wait for pods leaving ContainerCreating/Pending/Terminating
+  int wait_timeout_s = 120;  // analyze/pods.go:19
+  int min_pod_age_s = 20;    // analyze/pods.go:16
+  bool gpu_probe = false;    // exec the GPU probe inside GPU pods
+};
+
+std::vector<ReportItem> create_report(kube::Client& k, const std::string& ns, const Options& o);
+std::string report_to_string(const std::vector<ReportItem>& report);
+// Used by Helm deploy errors ("timed out waiting") to explain the failure.
+std::string analyze(kube::Client& k, const std::string& ns, const Options& o);
+
+// Helpers exposed for tests
+std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, const std::vector<Value>& pods,
+                                      const Options& o);
+bool log_has_gpu_runtime_error(const std::string& log, std::string* match);
+
+}  // namespace analyze
+}  // namespace ds

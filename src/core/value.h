@@ -87,6 +87,8 @@ class Value {
   size_t size() const { return is_seq() ? seq_.size() : is_map() ? map_.size() : 0; }
   const Value& operator[](size_t i) const { return seq_.at(i); }
   Value& operator[](size_t i) { return seq_.at(i); }
+  const Value& operator[](int i) const { return seq_.at((size_t)i); }
+  Value& operator[](int i) { return seq_.at((size_t)i); }
 
   // Map access
   const MapT& entries() const { return map_; }

@@ -1,0 +1,1076 @@
+#include "deploy/gotemplate.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <ctime>
+#include <regex>
+#include <sstream>
+#include <vector>
+
+#include "core/codec.h"
+#include "core/strutil.h"
+
+namespace ds {
+namespace tmpl {
+
+// ============================================================== lexer for actions
+
+namespace {
+
+enum class T { Ident, Field, Var, Str, Num, Bool, Nil, LParen, RParen, Pipe, Declare, Assign, Comma, Dot, End };
+
+struct Tok {
+  T t;
+  std::string s;
+};
+
+std::vector<Tok> lex_action(const std::string& a) {
+  std::vector<Tok> out;
+  size_t i = 0;
+  auto is_id = [](char c) { return std::isalnum((unsigned char)c) || c == '_'; };
+  while (i < a.size()) {
+    char c = a[i];
+    if (std::isspace((unsigned char)c)) {
+      ++i;
+      continue;
+    }
+    if (c == '(') {
+      out.push_back({T::LParen, "("});
+      ++i;
+    } else if (c == ')') {
+      out.push_back({T::RParen, ")"});
+      ++i;
+      // field chain after a paren: ").Foo"
+    } else if (c == '|') {
+      out.push_back({T::Pipe, "|"});
+      ++i;
+    } else if (c == ',') {
+      out.push_back({T::Comma, ","});
+      ++i;
+    } else if (c == ':' && i + 1 < a.size() && a[i + 1] == '=') {
+      out.push_back({T::Declare, ":="});
+      i += 2;
+    } else if (c == '=') {
+      out.push_back({T::Assign, "="});
+      ++i;
+    } else if (c == '"') {
+      std::string s;
+      ++i;
+      while (i < a.size() && a[i] != '"') {
+        if (a[i] == '\\' && i + 1 < a.size()) {
+          char e = a[++i];
+          switch (e) {
+            case 'n': s.push_back('\n'); break;
+            case 't': s.push_back('\t'); break;
+            case 'r': s.push_back('\r'); break;
+            case '\\': s.push_back('\\'); break;
+            case '"': s.push_back('"'); break;
+            default: s.push_back('\\'); s.push_back(e);
+          }
+          ++i;
+          continue;
+        }
+        s.push_back(a[i++]);
+      }
+      ++i;
+      out.push_back({T::Str, s});
+    } else if (c == '`') {
+      size_t e = a.find('`', i + 1);
+      if (e == std::string::npos) throw TemplateError("unterminated raw string");
+      out.push_back({T::Str, a.substr(i + 1, e - i - 1)});
+      i = e + 1;
+    } else if (c == '\'') {
+      // char constant -> number
+      size_t e = a.find('\'', i + 1);
+      out.push_back({T::Num, std::to_string((int)(unsigned char)a[i + 1])});
+      i = e + 1;
+    } else if (c == '.' ) {
+      if (i + 1 < a.size() && is_id(a[i + 1]) && !std::isdigit((unsigned char)a[i + 1])) {
+        size_t e = i + 1;
+        while (e < a.size() && (is_id(a[e]) || (a[e] == '.' && e + 1 < a.size() && is_id(a[e + 1])))) ++e;
+        out.push_back({T::Field, a.substr(i, e - i)});
+        i = e;
+      } else if (i + 1 < a.size() && std::isdigit((unsigned char)a[i + 1])) {
+        size_t e = i + 1;
+        while (e < a.size() && (std::isdigit((unsigned char)a[e]) || a[e] == 'e')) ++e;
+        out.push_back({T::Num, "0" + a.substr(i, e - i)});
+        i = e;
+      } else {
+        out.push_back({T::Dot, "."});
+        ++i;
+      }
+    } else if (c == '$') {
+      size_t e = i + 1;
+      while (e < a.size() && (is_id(a[e]) || (a[e] == '.' && e + 1 < a.size() && is_id(a[e + 1])))) ++e;
+      out.push_back({T::Var, a.substr(i, e - i)});
+      i = e;
+    } else if (std::isdigit((unsigned char)c) || ((c == '-' || c == '+') && i + 1 < a.size() && std::isdigit((unsigned char)a[i + 1]))) {
+      size_t e = i + 1;
+      while (e < a.size() && (std::isalnum((unsigned char)a[e]) || a[e] == '.' || a[e] == '_' ||
+                              ((a[e] == '-' || a[e] == '+') && (a[e - 1] == 'e' || a[e - 1] == 'E'))))
+        ++e;
+      out.push_back({T::Num, a.substr(i, e - i)});
+      i = e;
+    } else if (is_id(c)) {
+      size_t e = i;
+      while (e < a.size() && is_id(a[e])) ++e;
+      std::string id = a.substr(i, e - i);
+      if (id == "true" || id == "false")
+        out.push_back({T::Bool, id});
+      else if (id == "nil")
+        out.push_back({T::Nil, id});
+      else
+        out.push_back({T::Ident, id});
+      i = e;
+    } else {
+      throw TemplateError(std::string("unexpected character '") + c + "' in action: " + a);
+    }
+  }
+  out.push_back({T::End, ""});
+  return out;
+}
+
+// ============================================================== AST
+
+struct Pipeline;
+struct Arg {
+  enum Kind { Field, Var, Lit, Ident, Sub, Dot } kind;
+  std::string name;  // field chain ".a.b", var "$x.a", ident
+  Value lit;
+  std::shared_ptr<Pipeline> sub;
+  std::string chain;  // field chain applied after a sub-pipeline
+};
+
+struct Command {
+  std::vector<Arg> args;
+};
+
+struct Pipeline {
+  std::vector<std::string> decl;  // variable names
+  bool assign = false;            // "=" instead of ":="
+  std::vector<Command> cmds;
+};
+
+struct Node {
+  enum Kind { Text, Action, If, Range, With, Template, List } kind;
+  std::string text;
+  std::shared_ptr<Pipeline> pipe;
+  std::vector<std::shared_ptr<Node>> body, else_body;
+  std::string name;  // template name
+};
+using NodeP = std::shared_ptr<Node>;
+
+class PipeParser {
+ public:
+  explicit PipeParser(std::vector<Tok> toks) : t_(std::move(toks)) {}
+  std::shared_ptr<Pipeline> parse_pipeline(bool allow_decl = true) {
+    auto p = std::make_shared<Pipeline>();
+    if (allow_decl) {
+      // lookahead: $a [, $b] := | =
+      size_t save = i_;
+      std::vector<std::string> vars;
+      while (t_[i_].t == T::Var) {
+        vars.push_back(t_[i_].s);
+        ++i_;
+        if (t_[i_].t == T::Comma) {
+          ++i_;
+          continue;
+        }
+        break;
+      }
+      if (!vars.empty() && (t_[i_].t == T::Declare || t_[i_].t == T::Assign)) {
+        p->assign = t_[i_].t == T::Assign;
+        p->decl = vars;
+        ++i_;
+      } else {
+        i_ = save;
+      }
+    }
+    while (true) {
+      Command c;
+      while (t_[i_].t != T::Pipe && t_[i_].t != T::End && t_[i_].t != T::RParen) c.args.push_back(parse_arg());
+      if (c.args.empty()) throw TemplateError("missing value for command");
+      p->cmds.push_back(std::move(c));
+      if (t_[i_].t == T::Pipe) {
+        ++i_;
+        continue;
+      }
+      break;
+    }
+    return p;
+  }
+  bool at_end() const { return t_[i_].t == T::End; }
+  const Tok& peek() const { return t_[i_]; }
+  Tok next() { return t_[i_++]; }
+
+ private:
+  Arg parse_arg() {
+    const Tok& k = t_[i_++];
+    Arg a;
+    switch (k.t) {
+      case T::Field: a.kind = Arg::Field; a.name = k.s; break;
+      case T::Var: a.kind = Arg::Var; a.name = k.s; break;
+      case T::Dot: a.kind = Arg::Dot; break;
+      case T::Ident: a.kind = Arg::Ident; a.name = k.s; break;
+      case T::Str: {
+        a.kind = Arg::Lit;
+        a.lit = Value(k.s);
+        a.lit.set_quoted(true);
+        break;
+      }
+      case T::Num: {
+        a.kind = Arg::Lit;
+        int64_t iv;
+        double dv;
+        std::string s = k.s;
+        if (parse_int64(s, &iv))
+          a.lit = Value(iv);
+        else if (starts_with(s, "0x") || starts_with(s, "0X"))
+          a.lit = Value((int64_t)std::strtoll(s.c_str() + 2, nullptr, 16));
+        else if (parse_double(s, &dv))
+          a.lit = Value(dv);
+        else
+          throw TemplateError("bad number: " + s);
+        break;
+      }
+      case T::Bool: a.kind = Arg::Lit; a.lit = Value(k.s == "true"); break;
+      case T::Nil: a.kind = Arg::Lit; break;
+      case T::LParen: {
+        a.kind = Arg::Sub;
+        a.sub = parse_pipeline(false);
+        if (t_[i_].t != T::RParen) throw TemplateError("unclosed parenthesis");
+        ++i_;
+        if (t_[i_].t == T::Field) a.chain = t_[i_++].s;
+        break;
+      }
+      default: throw TemplateError("unexpected token '" + k.s + "' in pipeline");
+    }
+    return a;
+  }
+  std::vector<Tok> t_;
+  size_t i_ = 0;
+};
+
+struct Segment {
+  bool action;
+  std::string s;
+};
+
+std::vector<Segment> split_segments(const std::string& src) {
+  std::vector<Segment> out;
+  size_t i = 0;
+  bool trim_next = false;
+  while (i < src.size()) {
+    size_t open = src.find("{{", i);
+    std::string text = src.substr(i, open == std::string::npos ? std::string::npos : open - i);
+    if (trim_next) text = trim_left(text, " \t\r\n");
+    if (open == std::string::npos) {
+      out.push_back({false, text});
+      break;
+    }
+    size_t body_start = open + 2;
+    bool trim_left_ws = body_start + 1 < src.size() && src[body_start] == '-' &&
+                        (src[body_start + 1] == ' ' || src[body_start + 1] == '\t' || src[body_start + 1] == '\n');
+    if (trim_left_ws) {
+      text = trim_right(text, " \t\r\n");
+      body_start += 1;
+    }
+    out.push_back({false, text});
+    // find closing "}}" outside string literals
+    size_t j = body_start;
+    char q = 0;
+    while (j + 1 < src.size()) {
+      char c = src[j];
+      if (q) {
+        if (c == '\\' && q == '"') {
+          j += 2;
+          continue;
+        }
+        if (c == q) q = 0;
+        ++j;
+        continue;
+      }
+      if (c == '"' || c == '`') {
+        q = c;
+        ++j;
+        continue;
+      }
+      if (c == '}' && src[j + 1] == '}') break;
+      ++j;
+    }
+    if (j + 1 >= src.size()) throw TemplateError("unclosed action");
+    size_t body_end = j;
+    trim_next = false;
+    if (body_end > body_start && src[body_end - 1] == '-' && body_end >= 2 &&
+        (src[body_end - 2] == ' ' || src[body_end - 2] == '\t' || src[body_end - 2] == '\n')) {
+      trim_next = true;
+      body_end -= 1;
+    }
+    out.push_back({true, src.substr(body_start, body_end - body_start)});
+    i = j + 2;
+  }
+  return out;
+}
+
+}  // namespace
+
+// ============================================================== engine
+
+struct Engine::Impl {
+  std::map<std::string, std::vector<NodeP>> templates;
+  Engine* owner = nullptr;
+
+  // ---------------------------------------------------------- parse
+  std::vector<NodeP> parse(const std::string& name, const std::string& src) {
+    auto segs = split_segments(src);
+    size_t pos = 0;
+    std::string stop;
+    auto body = parse_list(name, segs, pos, &stop);
+    if (!stop.empty()) throw TemplateError(name + ": unexpected {{" + stop + "}}");
+    return body;
+  }
+
+  // Parses until {{end}} / {{else ...}}; the terminating keyword action text goes to *stop.
+  std::vector<NodeP> parse_list(const std::string& tname, const std::vector<Segment>& segs, size_t& pos,
+                                std::string* stop) {
+    std::vector<NodeP> out;
+    while (pos < segs.size()) {
+      const Segment& s = segs[pos++];
+      if (!s.action) {
+        if (!s.s.empty()) {
+          auto n = std::make_shared<Node>();
+          n->kind = Node::Text;
+          n->text = s.s;
+          out.push_back(n);
+        }
+        continue;
+      }
+      std::string a = trim(s.s);
+      if (starts_with(a, "/*")) continue;  // comment
+      std::string kw = a.substr(0, a.find_first_of(" \t\n("));
+      if (kw == "end" || kw == "else") {
+        *stop = a;
+        return out;
+      }
+      if (kw == "if" || kw == "with" || kw == "range") {
+        out.push_back(parse_control(tname, kw, a.substr(kw.size()), segs, pos));
+        continue;
+      }
+      if (kw == "define" || kw == "block") {
+        PipeParser pp(lex_action(a.substr(kw.size())));
+        Tok nm = pp.next();
+        if (nm.t != T::Str) throw TemplateError("define requires a name");
+        std::string st;
+        auto body = parse_list(tname, segs, pos, &st);
+        if (trim(st) != "end") throw TemplateError("define " + nm.s + " missing end");
+        templates[nm.s] = body;
+        if (kw == "block") {
+          auto n = std::make_shared<Node>();
+          n->kind = Node::Template;
+          n->name = nm.s;
+          n->pipe = pp.at_end() ? nullptr : pp.parse_pipeline(false);
+          out.push_back(n);
+        }
+        continue;
+      }
+      if (kw == "template") {
+        PipeParser pp(lex_action(a.substr(kw.size())));
+        Tok nm = pp.next();
+        if (nm.t != T::Str) throw TemplateError("template requires a name");
+        auto n = std::make_shared<Node>();
+        n->kind = Node::Template;
+        n->name = nm.s;
+        n->pipe = pp.at_end() ? nullptr : pp.parse_pipeline(false);
+        out.push_back(n);
+        continue;
+      }
+      auto n = std::make_shared<Node>();
+      n->kind = Node::Action;
+      PipeParser pp(lex_action(a));
+      n->pipe = pp.parse_pipeline(true);
+      if (!pp.at_end()) throw TemplateError("unexpected '" + pp.peek().s + "' in action: " + a);
+      out.push_back(n);
+    }
+    if (stop) stop->clear();
+    return out;
+  }
+
+  NodeP parse_control(const std::string& tname, const std::string& kw, const std::string& rest,
+                      const std::vector<Segment>& segs, size_t& pos) {
+    auto n = std::make_shared<Node>();
+    n->kind = kw == "if" ? Node::If : kw == "with" ? Node::With : Node::Range;
+    PipeParser pp(lex_action(rest));
+    n->pipe = pp.parse_pipeline(true);
+    std::string st;
+    n->body = parse_list(tname, segs, pos, &st);
+    if (st.empty()) throw TemplateError(tname + ": unexpected EOF in " + kw);
+    if (trim(st) == "end") return n;
+    // else / else if / else with
+    std::string after = trim(trim(st).substr(4));
+    if (after.empty()) {
+      std::string st2;
+      n->else_body = parse_list(tname, segs, pos, &st2);
+      if (trim(st2) != "end") throw TemplateError(tname + ": expected end after else");
+      return n;
+    }
+    std::string kw2 = after.substr(0, after.find_first_of(" \t\n("));
+    if (kw2 == "if" || kw2 == "with") {
+      // "else if" chains share a single end
+      n->else_body.push_back(parse_control(tname, kw2, after.substr(kw2.size()), segs, pos));
+      return n;
+    }
+    throw TemplateError(tname + ": bad else clause: " + st);
+  }
+
+  // ---------------------------------------------------------- evaluation
+
+  struct Scope {
+    std::vector<std::pair<std::string, Value>> vars;
+    Value dot;
+  };
+
+  static bool truth(const Value& v) {
+    switch (v.type()) {
+      case Value::Type::Null: return false;
+      case Value::Type::Bool: return v.as_bool();
+      case Value::Type::Int: return v.as_int() != 0;
+      case Value::Type::Float: return v.as_double() != 0;
+      case Value::Type::String: return !v.str().empty();
+      case Value::Type::Seq: return v.size() > 0;
+      case Value::Type::Map: return v.size() > 0;
+    }
+    return false;
+  }
+
+  static std::string fmt_float(double d) {
+    if (d == std::floor(d) && std::fabs(d) < 1e21) {
+      if (std::fabs(d) >= 1e21) return strfmt("%g", d);
+      return strfmt("%.0f", d);
+    }
+    for (int p = 1; p <= 17; ++p) {
+      std::string s = strfmt("%.*g", p, d);
+      if (std::strtod(s.c_str(), nullptr) == d) return s;
+    }
+    return strfmt("%g", d);
+  }
+
+  static std::string print_value(const Value& v) {
+    switch (v.type()) {
+      case Value::Type::Null: return "";
+      case Value::Type::Float: return fmt_float(v.as_double());
+      case Value::Type::Seq: {
+        std::vector<std::string> parts;
+        for (auto& it : v.items()) parts.push_back(it.is_null() ? "<nil>" : print_value(it));
+        return "[" + join(parts, " ") + "]";
+      }
+      case Value::Type::Map: {
+        auto keys = v.keys();
+        std::sort(keys.begin(), keys.end());
+        std::vector<std::string> parts;
+        for (auto& k : keys) parts.push_back(k + ":" + print_value(v.get(k)));
+        return "map[" + join(parts, " ") + "]";
+      }
+      default: return v.as_string();
+    }
+  }
+
+  static Value field_chain(Value cur, const std::string& chain) {
+    for (auto& part : split(chain, ".")) {
+      if (part.empty()) continue;
+      if (cur.is_map()) {
+        const Value* n = cur.find(part);
+        cur = n ? *n : Value();
+      } else {
+        return Value();  // missingkey=zero semantics (Helm)
+      }
+    }
+    return cur;
+  }
+
+  Value lookup_var(const Scope& sc, const std::string& ref) {
+    std::string name = ref;
+    std::string chain;
+    size_t dot = ref.find('.');
+    if (dot != std::string::npos) {
+      name = ref.substr(0, dot);
+      chain = ref.substr(dot);
+    }
+    for (auto it = sc.vars.rbegin(); it != sc.vars.rend(); ++it)
+      if (it->first == name) return field_chain(it->second, chain);
+    throw TemplateError("undefined variable: " + name);
+  }
+
+  Value eval_arg(Scope& sc, const Arg& a) {
+    switch (a.kind) {
+      case Arg::Field: return field_chain(sc.dot, a.name);
+      case Arg::Var: return lookup_var(sc, a.name);
+      case Arg::Lit: return a.lit;
+      case Arg::Dot: return sc.dot;
+      case Arg::Sub: return field_chain(eval_pipeline(sc, *a.sub, false), a.chain);
+      case Arg::Ident: return call(sc, a.name, {}, nullptr);
+    }
+    return Value();
+  }
+
+  Value eval_pipeline(Scope& sc, const Pipeline& p, bool declare_in_scope) {
+    Value last;
+    bool have_last = false;
+    for (auto& c : p.cmds) {
+      const Arg& first = c.args[0];
+      if (first.kind == Arg::Ident) {
+        std::vector<Value> args;
+        for (size_t i = 1; i < c.args.size(); ++i) args.push_back(eval_arg(sc, c.args[i]));
+        last = call(sc, first.name, std::move(args), have_last ? &last : nullptr);
+      } else {
+        if (c.args.size() > 1) throw TemplateError("can't give argument to non-function");
+        if (have_last) throw TemplateError("can't pipe into non-function");
+        last = eval_arg(sc, first);
+      }
+      have_last = true;
+    }
+    if (!p.decl.empty() && declare_in_scope) {
+      if (p.assign) {
+        for (auto it = sc.vars.rbegin(); it != sc.vars.rend(); ++it)
+          if (it->first == p.decl[0]) {
+            it->second = last;
+            return last;
+          }
+        throw TemplateError("undefined variable: " + p.decl[0]);
+      }
+      sc.vars.emplace_back(p.decl[0], last);
+    }
+    return last;
+  }
+
+  // ---------------------------------------------------------- functions
+
+  static bool cmp_eq(const Value& a, const Value& b) {
+    if (a.is_number() && b.is_number()) return a.as_double() == b.as_double();
+    if (a.is_null() || b.is_null()) return a.is_null() && b.is_null();
+    if (a.is_scalar() && b.is_scalar()) {
+      if (a.type() != b.type()) return false;
+      return a.as_string() == b.as_string();
+    }
+    return a == b;
+  }
+
+  static int cmp_order(const Value& a, const Value& b) {
+    if (a.is_number() && b.is_number()) {
+      double x = a.as_double(), y = b.as_double();
+      return x < y ? -1 : x > y ? 1 : 0;
+    }
+    if (a.is_string() && b.is_string()) return a.str() < b.str() ? -1 : a.str() > b.str() ? 1 : 0;
+    if (a.is_null() || b.is_null()) throw TemplateError("incompatible types for comparison");
+    std::string x = a.as_string(), y = b.as_string();
+    return x < y ? -1 : x > y ? 1 : 0;
+  }
+
+  static std::string go_quote(const std::string& s) {
+    std::string out = "\"";
+    for (unsigned char c : s) {
+      switch (c) {
+        case '"': out += "\\\""; break;
+        case '\\': out += "\\\\"; break;
+        case '\n': out += "\\n"; break;
+        case '\t': out += "\\t"; break;
+        case '\r': out += "\\r"; break;
+        default:
+          if (c < 0x20)
+            out += strfmt("\\x%02x", c);
+          else
+            out.push_back((char)c);
+      }
+    }
+    return out + "\"";
+  }
+
+  static std::string strval(const Value& v) { return v.is_null() ? "" : print_value(v); }
+
+  static std::string indent_str(int n, const std::string& s) {
+    std::string pad(n, ' ');
+    std::string out = pad;
+    for (char c : s) {
+      out.push_back(c);
+      if (c == '\n') out += pad;
+    }
+    return out;
+  }
+
+  static std::string go_printf(const std::string& f, const std::vector<Value>& args) {
+    std::string out;
+    size_t ai = 0;
+    for (size_t i = 0; i < f.size(); ++i) {
+      if (f[i] != '%') {
+        out.push_back(f[i]);
+        continue;
+      }
+      if (i + 1 >= f.size()) break;
+      size_t j = i + 1;
+      std::string flags;
+      while (j < f.size() && std::strchr("+-# 0123456789.", f[j])) flags.push_back(f[j++]);
+      char verb = f[j];
+      i = j;
+      if (verb == '%') {
+        out.push_back('%');
+        continue;
+      }
+      Value a = ai < args.size() ? args[ai++] : Value();
+      switch (verb) {
+        case 'd': out += strfmt(("%" + flags + "lld").c_str(), (long long)a.as_int()); break;
+        case 'f': case 'e': case 'g':
+          out += strfmt(("%" + flags + std::string(1, verb)).c_str(), a.as_double());
+          break;
+        case 'x': out += a.is_number() ? strfmt("%llx", (long long)a.as_int()) : hex_encode(strval(a)); break;
+        case 'q': out += go_quote(strval(a)); break;
+        case 't': out += a.as_bool() ? "true" : "false"; break;
+        default: {
+          std::string s = strval(a);
+          if (!flags.empty() && std::isdigit((unsigned char)flags.back()))
+            out += strfmt(("%" + flags + "s").c_str(), s.c_str());
+          else
+            out += s;
+        }
+      }
+    }
+    return out;
+  }
+
+  std::string render_nodes(Scope& sc, const std::vector<NodeP>& nodes) {
+    std::string out;
+    for (auto& n : nodes) exec_node(sc, *n, out);
+    return out;
+  }
+
+  std::string include(const std::string& name, const Value& dot) {
+    auto it = templates.find(name);
+    if (it == templates.end()) throw TemplateError("template: no template \"" + name + "\" associated");
+    Scope sc;
+    sc.dot = dot;
+    sc.vars.emplace_back("$", dot);
+    return render_nodes(sc, it->second);
+  }
+
+  Value call(Scope& sc, const std::string& fn, std::vector<Value> args, const Value* piped) {
+    if (piped) args.push_back(*piped);
+    auto need = [&](size_t n) {
+      if (args.size() < n) throw TemplateError("wrong number of args for " + fn);
+    };
+    auto S = [](std::string s) {
+      Value v(std::move(s));
+      return v;
+    };
+    if (fn == "eq") {
+      need(2);
+      for (size_t i = 1; i < args.size(); ++i)
+        if (cmp_eq(args[0], args[i])) return Value(true);
+      return Value(false);
+    }
+    if (fn == "ne") { need(2); return Value(!cmp_eq(args[0], args[1])); }
+    if (fn == "lt") { need(2); return Value(cmp_order(args[0], args[1]) < 0); }
+    if (fn == "le") { need(2); return Value(cmp_order(args[0], args[1]) <= 0); }
+    if (fn == "gt") { need(2); return Value(cmp_order(args[0], args[1]) > 0); }
+    if (fn == "ge") { need(2); return Value(cmp_order(args[0], args[1]) >= 0); }
+    if (fn == "and") {
+      for (auto& a : args)
+        if (!truth(a)) return a;
+      return args.empty() ? Value() : args.back();
+    }
+    if (fn == "or") {
+      for (auto& a : args)
+        if (truth(a)) return a;
+      return args.empty() ? Value() : args.back();
+    }
+    if (fn == "not") { need(1); return Value(!truth(args[0])); }
+    if (fn == "len") {
+      need(1);
+      const Value& v = args[0];
+      return Value((int64_t)(v.is_string() ? v.str().size() : v.size()));
+    }
+    if (fn == "index") {
+      need(1);
+      Value cur = args[0];
+      for (size_t i = 1; i < args.size(); ++i) {
+        if (cur.is_map())
+          cur = cur.get(args[i].as_string());
+        else if (cur.is_seq()) {
+          int64_t k = args[i].as_int();
+          if (k < 0 || k >= (int64_t)cur.size()) throw TemplateError("index out of range");
+          cur = cur[(size_t)k];
+        } else
+          return Value();
+      }
+      return cur;
+    }
+    if (fn == "print" || fn == "println") {
+      std::string s;
+      for (size_t i = 0; i < args.size(); ++i) {
+        if (i && fn == "println") s += " ";
+        if (i && fn == "print" && !args[i].is_string() && !args[i - 1].is_string()) s += " ";
+        s += strval(args[i]);
+      }
+      if (fn == "println") s += "\n";
+      return S(s);
+    }
+    if (fn == "printf") {
+      need(1);
+      std::vector<Value> rest(args.begin() + 1, args.end());
+      return S(go_printf(args[0].as_string(), rest));
+    }
+    if (fn == "default") {
+      need(1);
+      if (args.size() == 1) return args[0];
+      return truth(args[1]) ? args[1] : args[0];
+    }
+    if (fn == "empty") { need(1); return Value(!truth(args[0])); }
+    if (fn == "coalesce") {
+      for (auto& a : args)
+        if (truth(a)) return a;
+      return Value();
+    }
+    if (fn == "ternary") { need(3); return truth(args[2]) ? args[0] : args[1]; }
+    if (fn == "required") {
+      need(2);
+      if (args[1].is_null() || (args[1].is_string() && args[1].str().empty())) throw TemplateError(args[0].as_string());
+      return args[1];
+    }
+    if (fn == "fail") { need(1); throw TemplateError(args[0].as_string()); }
+    if (fn == "quote" || fn == "squote") {
+      std::vector<std::string> parts;
+      for (auto& a : args) {
+        if (a.is_null()) continue;
+        parts.push_back(fn == "quote" ? go_quote(strval(a)) : "'" + strval(a) + "'");
+      }
+      return S(join(parts, " "));
+    }
+    if (fn == "toYaml") {
+      need(1);
+      if (args[0].is_null()) return S("null");
+      std::string y = yaml_dump(args[0]);
+      if (ends_with(y, "\n")) y.pop_back();
+      return S(y);
+    }
+    if (fn == "toJson" || fn == "toRawJson" || fn == "mustToJson") { need(1); return S(json_dump(args[0])); }
+    if (fn == "toPrettyJson") { need(1); return S(json_dump(args[0], 2)); }
+    if (fn == "fromYaml") { need(1); return yaml_parse(args[0].as_string()); }
+    if (fn == "fromJson") { need(1); return json_parse(args[0].as_string()); }
+    if (fn == "indent") { need(2); return S(indent_str((int)args[0].as_int(), strval(args[1]))); }
+    if (fn == "nindent") { need(2); return S("\n" + indent_str((int)args[0].as_int(), strval(args[1]))); }
+    if (fn == "trim") { need(1); return S(trim(strval(args[0]), " \t\r\n")); }
+    if (fn == "trimAll") { need(2); return S(trim(strval(args[1]), args[0].as_string())); }
+    if (fn == "trimPrefix") {
+      need(2);
+      std::string s = strval(args[1]);
+      return S(starts_with(s, args[0].as_string()) ? s.substr(args[0].as_string().size()) : s);
+    }
+    if (fn == "trimSuffix") {
+      need(2);
+      std::string s = strval(args[1]);
+      return S(ends_with(s, args[0].as_string()) ? s.substr(0, s.size() - args[0].as_string().size()) : s);
+    }
+    if (fn == "upper") { need(1); return S(to_upper(strval(args[0]))); }
+    if (fn == "lower") { need(1); return S(to_lower(strval(args[0]))); }
+    if (fn == "title") {
+      need(1);
+      std::string s = strval(args[0]);
+      bool up = true;
+      for (auto& c : s) {
+        if (up && std::isalpha((unsigned char)c)) c = (char)std::toupper((unsigned char)c);
+        up = std::isspace((unsigned char)c);
+      }
+      return S(s);
+    }
+    if (fn == "replace") { need(3); return S(replace_all(strval(args[2]), args[0].as_string(), args[1].as_string())); }
+    if (fn == "contains") { need(2); return Value(contains(strval(args[1]), args[0].as_string())); }
+    if (fn == "hasPrefix") { need(2); return Value(starts_with(strval(args[1]), args[0].as_string())); }
+    if (fn == "hasSuffix") { need(2); return Value(ends_with(strval(args[1]), args[0].as_string())); }
+    if (fn == "trunc") {
+      need(2);
+      std::string s = strval(args[1]);
+      int64_t n = args[0].as_int();
+      if (n >= 0) return S(s.substr(0, std::min<size_t>((size_t)n, s.size())));
+      size_t k = (size_t)(-n);
+      return S(k >= s.size() ? s : s.substr(s.size() - k));
+    }
+    if (fn == "repeat") {
+      need(2);
+      std::string o;
+      for (int64_t i = 0; i < args[0].as_int(); ++i) o += strval(args[1]);
+      return S(o);
+    }
+    if (fn == "join") {
+      need(2);
+      std::vector<std::string> parts;
+      for (auto& it : args[1].items()) parts.push_back(strval(it));
+      return S(join(parts, args[0].as_string()));
+    }
+    if (fn == "split" || fn == "splitList") {
+      need(2);
+      auto parts = split(strval(args[1]), args[0].as_string());
+      if (fn == "splitList") return Value::strings(parts);
+      Value m = Value::map();
+      for (size_t i = 0; i < parts.size(); ++i) m["_" + std::to_string(i)] = parts[i];
+      return m;
+    }
+    if (fn == "list" || fn == "tuple") {
+      Value l = Value::seq();
+      for (auto& a : args) l.push(a);
+      return l;
+    }
+    if (fn == "dict") {
+      Value m = Value::map();
+      for (size_t i = 0; i + 1 < args.size(); i += 2) m[args[i].as_string()] = args[i + 1];
+      return m;
+    }
+    if (fn == "get") { need(2); return args[0].get(args[1].as_string()); }
+    if (fn == "hasKey") { need(2); return Value(args[0].has(args[1].as_string())); }
+    if (fn == "set") { need(3); Value m = args[0]; m[args[1].as_string()] = args[2]; return m; }
+    if (fn == "unset") { need(2); Value m = args[0]; m.erase(args[1].as_string()); return m; }
+    if (fn == "keys") {
+      Value l = Value::seq();
+      for (auto& a : args)
+        for (auto& k : a.keys()) l.push(Value(k));
+      return l;
+    }
+    if (fn == "values") {
+      need(1);
+      Value l = Value::seq();
+      for (auto& e : args[0].entries()) l.push(e.second);
+      return l;
+    }
+    if (fn == "merge" || fn == "mergeOverwrite") {
+      need(1);
+      Value out = Value::map();
+      if (fn == "merge") {
+        for (auto it = args.rbegin(); it != args.rend(); ++it) merge_into(out, *it);
+      } else {
+        for (auto& a : args) merge_into(out, a);
+      }
+      return out;
+    }
+    if (fn == "first") { need(1); return args[0].size() ? args[0][(size_t)0] : Value(); }
+    if (fn == "last") { need(1); return args[0].size() ? args[0][args[0].size() - 1] : Value(); }
+    if (fn == "has") {
+      need(2);
+      for (auto& it : args[1].items())
+        if (cmp_eq(it, args[0])) return Value(true);
+      return Value(false);
+    }
+    if (fn == "int" || fn == "int64" || fn == "atoi") { need(1); return Value(args[0].as_int()); }
+    if (fn == "float64") { need(1); return Value(args[0].as_double()); }
+    if (fn == "toString") { need(1); return S(strval(args[0])); }
+    if (fn == "toStrings") {
+      Value l = Value::seq();
+      for (auto& it : args[0].items()) l.push(Value(strval(it)));
+      return l;
+    }
+    auto arith = [&](auto op) -> Value {
+      need(1);
+      bool f = false;
+      for (auto& a : args) f |= a.is_float();
+      if (f) {
+        double r = args[0].as_double();
+        for (size_t i = 1; i < args.size(); ++i) r = op(r, args[i].as_double());
+        return Value(r);
+      }
+      int64_t r = args[0].as_int();
+      for (size_t i = 1; i < args.size(); ++i) r = (int64_t)op((double)r, (double)args[i].as_int());
+      return Value(r);
+    };
+    if (fn == "add") return arith([](double a, double b) { return a + b; });
+    if (fn == "sub") return arith([](double a, double b) { return a - b; });
+    if (fn == "mul") return arith([](double a, double b) { return a * b; });
+    if (fn == "div") {
+      need(2);
+      if (args[1].as_double() == 0) throw TemplateError("division by zero");
+      if (args[0].is_int() && args[1].is_int()) return Value(args[0].as_int() / args[1].as_int());
+      return Value(args[0].as_double() / args[1].as_double());
+    }
+    if (fn == "mod") { need(2); return Value(args[1].as_int() ? args[0].as_int() % args[1].as_int() : 0); }
+    if (fn == "max" || fn == "min") {
+      need(1);
+      Value best = args[0];
+      for (auto& a : args)
+        if ((fn == "max") ? cmp_order(a, best) > 0 : cmp_order(a, best) < 0) best = a;
+      return best;
+    }
+    if (fn == "until") {
+      need(1);
+      Value l = Value::seq();
+      for (int64_t i = 0; i < args[0].as_int(); ++i) l.push(Value(i));
+      return l;
+    }
+    if (fn == "b64enc") { need(1); return S(base64_encode(strval(args[0]))); }
+    if (fn == "b64dec") { need(1); return S(base64_decode(strval(args[0]))); }
+    if (fn == "sha256sum") { need(1); return S(sha256_hex(strval(args[0]))); }
+    if (fn == "kindIs") {
+      need(2);
+      std::string k = args[0].as_string();
+      const Value& v = args[1];
+      std::string kind = v.is_map() ? "map" : v.is_seq() ? "slice" : v.is_string() ? "string" : v.is_int() ? "int64"
+                         : v.is_float() ? "float64" : v.is_bool() ? "bool" : "invalid";
+      return Value(kind == k || (k == "int" && kind == "int64"));
+    }
+    if (fn == "typeOf") {
+      need(1);
+      const Value& v = args[0];
+      return S(v.is_map() ? "map[string]interface {}" : v.is_seq() ? "[]interface {}" : v.is_string() ? "string"
+               : v.is_int() ? "int64" : v.is_float() ? "float64" : v.is_bool() ? "bool" : "<nil>");
+    }
+    if (fn == "regexMatch") { need(2); return Value(std::regex_search(strval(args[1]), std::regex(args[0].as_string()))); }
+    if (fn == "regexReplaceAll") {
+      need(3);
+      return S(std::regex_replace(strval(args[1]), std::regex(args[0].as_string()), args[2].as_string()));
+    }
+    if (fn == "semverCompare") {
+      need(2);
+      // supports ">=1.2.3", "<1.x" style with numeric major/minor/patch
+      std::string c = trim(args[0].as_string());
+      std::string op;
+      while (!c.empty() && std::strchr("<>=!~^", c[0])) op.push_back(c[0]), c.erase(0, 1);
+      auto parse = [](std::string v) {
+        if (!v.empty() && v[0] == 'v') v.erase(0, 1);
+        auto p = split(v.substr(0, v.find_first_of("-+")), ".");
+        std::vector<int64_t> n;
+        for (auto& x : p) n.push_back(std::atoll(x.c_str()));
+        while (n.size() < 3) n.push_back(0);
+        return n;
+      };
+      auto a = parse(args[1].as_string()), b = parse(c);
+      int r = a < b ? -1 : a > b ? 1 : 0;
+      if (op.empty() || op == "=") return Value(r == 0);
+      if (op == ">=") return Value(r >= 0);
+      if (op == ">") return Value(r > 0);
+      if (op == "<=") return Value(r <= 0);
+      if (op == "<") return Value(r < 0);
+      if (op == "!=") return Value(r != 0);
+      return Value(r >= 0);
+    }
+    if (fn == "include") { need(2); return S(include(args[0].as_string(), args[1])); }
+    if (fn == "tpl") {
+      need(2);
+      std::string nm = "tpl-" + sha256_hex(args[0].as_string()).substr(0, 12);
+      if (!templates.count(nm)) templates[nm] = parse(nm, args[0].as_string());
+      return S(include(nm, args[1]));
+    }
+    if (fn == "lookup") {
+      need(4);
+      if (owner->lookup) return owner->lookup(args[0].as_string(), args[1].as_string(), args[2].as_string(), args[3].as_string());
+      return Value::map();
+    }
+    if (fn == "now") return S(std::to_string((long long)std::time(nullptr)));
+    if (fn == "date") {
+      need(1);
+      std::time_t t = std::time(nullptr);
+      char buf[64];
+      std::strftime(buf, sizeof(buf), "%Y-%m-%d", std::gmtime(&t));
+      return S(buf);
+    }
+    if (fn == "uuidv4") {
+      std::string h = hex_encode(random_string(16));
+      return S(h.substr(0, 8) + "-" + h.substr(8, 4) + "-4" + h.substr(13, 3) + "-a" + h.substr(17, 3) + "-" + h.substr(20, 12));
+    }
+    if (fn == "randAlphaNum" || fn == "randAlpha") { need(1); return S(random_string((size_t)args[0].as_int())); }
+    throw TemplateError("function \"" + fn + "\" not defined");
+  }
+
+  void exec_node(Scope& sc, const Node& n, std::string& out) {
+    switch (n.kind) {
+      case Node::Text: out += n.text; return;
+      case Node::Action: {
+        Value v = eval_pipeline(sc, *n.pipe, true);
+        if (n.pipe->decl.empty()) out += print_value(v);
+        return;
+      }
+      case Node::If: {
+        size_t mark = sc.vars.size();
+        Value v = eval_pipeline(sc, *n.pipe, true);
+        if (truth(v))
+          out += render_nodes(sc, n.body);
+        else
+          out += render_nodes(sc, n.else_body);
+        sc.vars.resize(mark);
+        return;
+      }
+      case Node::With: {
+        size_t mark = sc.vars.size();
+        Value v = eval_pipeline(sc, *n.pipe, true);
+        if (truth(v)) {
+          Value saved = sc.dot;
+          sc.dot = v;
+          out += render_nodes(sc, n.body);
+          sc.dot = saved;
+        } else {
+          out += render_nodes(sc, n.else_body);
+        }
+        sc.vars.resize(mark);
+        return;
+      }
+      case Node::Range: {
+        Pipeline p = *n.pipe;
+        std::vector<std::string> decl = p.decl;
+        p.decl.clear();
+        Value v = eval_pipeline(sc, p, false);
+        std::vector<std::pair<Value, Value>> items;
+        if (v.is_seq()) {
+          for (size_t i = 0; i < v.size(); ++i) items.emplace_back(Value((int64_t)i), v[i]);
+        } else if (v.is_map()) {
+          auto keys = v.keys();
+          std::sort(keys.begin(), keys.end());
+          for (auto& k : keys) items.emplace_back(Value(k), v.get(k));
+        } else if (v.is_int()) {
+          for (int64_t i = 0; i < v.as_int(); ++i) items.emplace_back(Value(i), Value(i));
+        }
+        if (items.empty()) {
+          out += render_nodes(sc, n.else_body);
+          return;
+        }
+        Value saved = sc.dot;
+        for (auto& kv : items) {
+          size_t mark = sc.vars.size();
+          if (decl.size() == 1) sc.vars.emplace_back(decl[0], kv.second);
+          if (decl.size() >= 2) {
+            sc.vars.emplace_back(decl[0], kv.first);
+            sc.vars.emplace_back(decl[1], kv.second);
+          }
+          sc.dot = kv.second;
+          out += render_nodes(sc, n.body);
+          // assignments with "=" to outer vars must survive: only drop the loop's own vars
+          sc.vars.resize(mark);
+        }
+        sc.dot = saved;
+        return;
+      }
+      case Node::Template: {
+        Value dot = n.pipe ? eval_pipeline(sc, *n.pipe, false) : Value();
+        out += include(n.name, dot);
+        return;
+      }
+      case Node::List: out += render_nodes(sc, n.body); return;
+    }
+  }
+};
+
+Engine::Engine() : impl_(std::make_unique<Impl>()) { impl_->owner = this; }
+Engine::~Engine() = default;
+
+void Engine::add(const std::string& name, const std::string& text) {
+  try {
+    impl_->templates[name] = impl_->parse(name, text);
+  } catch (const TemplateError& e) {
+    throw TemplateError("parse error in " + name + ": " + e.what());
+  }
+}
+
+bool Engine::has(const std::string& name) const { return impl_->templates.count(name) > 0; }
+
+std::string Engine::execute(const std::string& name, const Value& dot) {
+  try {
+    return impl_->include(name, dot);
+  } catch (const TemplateError& e) {
+    throw TemplateError("render error in " + name + ": " + e.what());
+  }
+}
+
+}  // namespace tmpl
+}  // namespace ds

@@ -119,6 +119,7 @@ class ExecSession : public sync::Shell {
   void terminate() override;
   void close() override;
   void resize(int width, int height);
+  void close_stdin_if_any() { in_w_.reset(); }
   // Waits for the remote process; returns its exit code (or -1 if unknown / stream died).
   int wait(int timeout_ms = -1);
   std::string error_message();

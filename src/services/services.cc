@@ -1,0 +1,428 @@
+#include "services/services.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <signal.h>
+#include <sys/ioctl.h>
+#include <sys/socket.h>
+#include <termios.h>
+#include <unistd.h>
+
+#include <cstring>
+
+#include "core/fs.h"
+#include "core/log.h"
+#include "core/prompt.h"
+#include "core/strutil.h"
+
+namespace ds {
+namespace services {
+
+// ---------------------------------------------------------------- selection
+
+Target resolve_target(const Value& cfg, const std::string& selector_flag, const std::string& label_selector_flag,
+                      const std::string& namespace_flag, const std::string& container_flag) {
+  Target t;
+  const Value& term = cfg.at_path("dev.terminal");
+  std::string sel_name = selector_flag.empty() ? term.get("selector").as_string("default") : selector_flag;
+  const Value* sel = config::find_selector(cfg, sel_name);
+  if (!sel && !selector_flag.empty()) throw std::runtime_error("Error resolving service name: Unable to find selector: " + sel_name);
+  t.namespace_ = config::default_namespace(cfg);
+  if (!namespace_flag.empty())
+    t.namespace_ = namespace_flag;
+  else if (sel && !sel->get("namespace").as_string().empty())
+    t.namespace_ = sel->get("namespace").as_string();
+  else if (!term.get("namespace").as_string().empty())
+    t.namespace_ = term.get("namespace").as_string();
+  if (!label_selector_flag.empty())
+    t.label_selector = label_selector_flag;
+  else if (sel && sel->get("labelSelector").is_map())
+    t.label_selector = config::label_selector_from(sel->get("labelSelector")).to_query();
+  else if (term.get("labelSelector").is_map())
+    t.label_selector = config::label_selector_from(term.get("labelSelector")).to_query();
+  else
+    t.label_selector = "app.kubernetes.io/name=" + config::first_helm_deployment(cfg);
+  if (!container_flag.empty())
+    t.container = container_flag;
+  else if (sel && !sel->get("containerName").as_string().empty())
+    t.container = sel->get("containerName").as_string();
+  else
+    t.container = term.get("containerName").as_string();
+  return t;
+}
+
+Value select_pod(kube::Client& k, const std::string& ns, const std::string& label_selector) {
+  auto pods = k.list_pods(ns, label_selector);
+  std::vector<Value> running;
+  for (auto& p : pods)
+    if (kube::pod_status(p) == "Running") running.push_back(p);
+  if (running.empty()) throw std::runtime_error("Couldn't find a running pod in namespace " + ns);
+  if (running.size() == 1) return running[0];
+  std::vector<std::string> names;
+  for (auto& p : running) names.push_back(p.at_path("metadata.name").as_string());
+  std::string pick = prompt::select("Select a pod", names, names[0]);
+  for (auto& p : running)
+    if (p.at_path("metadata.name").as_string() == pick) return p;
+  return running[0];
+}
+
+std::string select_container(const Value& pod, const std::string& preferred) {
+  const Value& cs = pod.at_path("spec.containers");
+  if (cs.size() == 0) throw std::runtime_error("pod has no containers");
+  if (!preferred.empty()) {
+    for (auto& c : cs.items())
+      if (c.get("name").as_string() == preferred) return preferred;
+    throw std::runtime_error("container " + preferred + " wasn't found in pod " + pod.at_path("metadata.name").as_string());
+  }
+  return cs[0].get("name").as_string();
+}
+
+// ---------------------------------------------------------------- sync
+
+std::vector<std::unique_ptr<sync::Session>> start_sync(const Value& cfg, std::shared_ptr<kube::Client> k,
+                                                        const SyncOptions& o) {
+  std::vector<std::unique_ptr<sync::Session>> out;
+  for (auto& sp : cfg.at_path("dev.sync").items()) {
+    std::string local = fs::abs_path(sp.get("localSubPath").as_string("./"));
+    config::SelectorRef ref = config::resolve_selector(cfg, sp);
+    std::string sel = ref.labels.to_query();
+    log::start_wait("Sync: Waiting for pods...");
+    Value pod;
+    try {
+      pod = k->newest_running_pod(ref.namespace_, sel, o.pod_wait_ms, o.poll_ms);
+    } catch (const std::exception& e) {
+      log::stop_wait();
+      throw std::runtime_error(std::string("Unable to list devspace pods: ") + e.what());
+    }
+    log::stop_wait();
+    std::string container;
+    try {
+      container = select_container(pod, ref.container);
+    } catch (const std::exception& e) {
+      log::warn(std::string("Couldn't start sync: ") + e.what());
+      continue;
+    }
+    sync::Options so;
+    so.watch_path = local;
+    so.dest_path = sp.get("containerPath").as_string();
+    so.pod_name = pod.at_path("metadata.name").as_string();
+    so.verbose = o.verbose;
+    so.mode = o.mode;
+    so.helper_path = o.helper_path;
+    for (auto& e : sp.get("excludePaths").items()) so.exclude_paths.push_back(e.as_string());
+    for (auto& e : sp.get("downloadExcludePaths").items()) so.download_exclude_paths.push_back(e.as_string());
+    for (auto& e : sp.get("uploadExcludePaths").items()) so.upload_exclude_paths.push_back(e.as_string());
+    if (!sp.at_path("bandwidthLimits.download").is_null())
+      so.downstream_limit = sp.at_path("bandwidthLimits.download").as_int() * 1024;
+    if (!sp.at_path("bandwidthLimits.upload").is_null())
+      so.upstream_limit = sp.at_path("bandwidthLimits.upload").as_int() * 1024;
+    // Reconnect to the newest running pod when the stream dies (the reference exits,
+    // sync/sync_config.go:481).
+    std::string ns = ref.namespace_;
+    int poll = o.poll_ms;
+    so.reconnect = [k, ns, sel, container, poll]() -> std::shared_ptr<sync::Transport> {
+      Value p = k->newest_running_pod(ns, sel, 120000, poll);
+      return std::make_shared<kube::ExecTransport>(k, p, container);
+    };
+    so.on_error = [local](const std::string& err) {
+      log::error("[Sync] Fatal sync error: " + err + ". For more information check .devspace/logs/sync.log");
+    };
+    auto s = std::make_unique<sync::Session>(so, std::make_shared<kube::ExecTransport>(k, pod, container));
+    try {
+      s->start();
+    } catch (const std::exception& e) {
+      throw std::runtime_error(std::string("Sync error: ") + e.what());
+    }
+    log::done("Sync started on " + local + " <-> " + so.dest_path + " (Pod: " + ns + "/" + so.pod_name + ")");
+    out.push_back(std::move(s));
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------- port forwarding
+
+PortForwarder::PortForwarder(std::shared_ptr<kube::Client> k, Value pod, std::vector<std::pair<int, int>> ports,
+                             std::vector<std::string> addresses)
+    : k_(std::move(k)), pod_(std::move(pod)), ports_(std::move(ports)), addrs_(std::move(addresses)) {}
+
+PortForwarder::~PortForwarder() { close(); }
+
+std::string PortForwarder::describe() const {
+  std::vector<std::string> p;
+  for (auto& pr : ports_) p.push_back(std::to_string(pr.first) + ":" + std::to_string(pr.second));
+  return join(p, ", ");
+}
+
+void PortForwarder::start() {
+  for (size_t i = 0; i < ports_.size(); ++i) {
+    int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    int one = 1;
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    struct sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)ports_[i].first);
+    std::string addr = i < addrs_.size() && !addrs_[i].empty() ? addrs_[i] : "127.0.0.1";
+    if (addr == "localhost") addr = "127.0.0.1";
+    if (inet_pton(AF_INET, addr.c_str(), &a.sin_addr) != 1) a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (::bind(fd, (struct sockaddr*)&a, sizeof(a)) != 0 || ::listen(fd, 64) != 0) {
+      std::string e = std::strerror(errno);
+      ::close(fd);
+      throw std::runtime_error("Unable to listen on port " + std::to_string(ports_[i].first) + ": " + e);
+    }
+    listeners_.push_back(fd);
+    int rp = ports_[i].second;
+    threads_.emplace_back([this, fd, rp] { accept_loop(fd, rp); });
+  }
+}
+
+void PortForwarder::accept_loop(int lfd, int remote_port) {
+  while (!stop_) {
+    struct pollfd pf{lfd, POLLIN, 0};
+    if (::poll(&pf, 1, 200) <= 0) continue;
+    int c = ::accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
+    if (c < 0) continue;
+    std::thread([this, c, remote_port] { handle(c, remote_port); }).detach();
+  }
+}
+
+void PortForwarder::handle(int cfd, int remote_port) {
+  std::unique_ptr<net::WebSocket> ws;
+  try {
+    ws = k_->portforward(pod_.at_path("metadata.namespace").as_string(), pod_.at_path("metadata.name").as_string(),
+                         remote_port);
+  } catch (const std::exception& e) {
+    log::file_logger("portforwarding")->emit("error", std::string("Error forwarding ports: ") + e.what(), {});
+    ::close(cfd);
+    return;
+  }
+  std::atomic<bool> done{false};
+  std::thread down([&] {
+    std::string msg;
+    bool first_data = true, first_err = true;
+    while (ws->recv(&msg)) {
+      if (msg.empty()) continue;
+      unsigned char ch = (unsigned char)msg[0];
+      std::string data = msg.substr(1);
+      // each channel's first frame carries the port number (2 bytes LE)
+      if (ch == 0 && first_data) {
+        first_data = false;
+        if (data.size() == 2) continue;
+      }
+      if (ch == 1 && first_err) {
+        first_err = false;
+        if (data.size() == 2) continue;
+      }
+      if (ch == 0) {
+        if (!write_all(cfd, data)) break;
+      } else if (ch == 1 && !data.empty()) {
+        log::file_logger("portforwarding")->emit("error", data, {});
+      }
+    }
+    done = true;
+    ::shutdown(cfd, SHUT_RDWR);
+  });
+  char buf[65536];
+  buf[0] = 0;
+  while (!done && !stop_) {
+    struct pollfd pf{cfd, POLLIN, 0};
+    int r = ::poll(&pf, 1, 200);
+    if (r == 0) continue;
+    ssize_t n = ::recv(cfd, buf + 1, sizeof(buf) - 1, 0);
+    if (n <= 0) break;
+    if (!ws->send(std::string(buf, (size_t)n + 1))) break;
+  }
+  ws->close();
+  down.join();
+  ::close(cfd);
+}
+
+void PortForwarder::close() {
+  if (stop_.exchange(true)) return;
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  for (int fd : listeners_) ::close(fd);
+  listeners_.clear();
+}
+
+std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& cfg, std::shared_ptr<kube::Client> k,
+                                                                  int pod_wait_ms, int poll_ms) {
+  std::vector<std::unique_ptr<PortForwarder>> out;
+  for (auto& pf : cfg.at_path("dev.ports").items()) {
+    config::SelectorRef ref = config::resolve_selector(cfg, pf);
+    log::start_wait("Port-Forwarding: Waiting for pods...");
+    Value pod;
+    try {
+      pod = k->newest_running_pod(ref.namespace_, ref.labels.to_query(), pod_wait_ms, poll_ms);
+    } catch (const std::exception& e) {
+      log::stop_wait();
+      throw std::runtime_error(std::string("Error starting port-forwarding: Unable to list devspace pods: ") + e.what());
+    }
+    log::stop_wait();
+    std::vector<std::pair<int, int>> ports;
+    std::vector<std::string> addrs;
+    for (auto& m : pf.get("portMappings").items()) {
+      ports.emplace_back((int)m.get("localPort").as_int(), (int)m.get("remotePort").as_int());
+      addrs.push_back(m.get("bindAddress").as_string("127.0.0.1"));
+    }
+    auto fwd = std::make_unique<PortForwarder>(k, pod, ports, addrs);
+    fwd->start();
+    log::done("Port forwarding started on " + fwd->describe());
+    out.push_back(std::move(fwd));
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------- terminal / attach / logs
+
+namespace {
+
+struct RawTty {
+  bool active = false;
+  struct termios saved{};
+  RawTty() {
+    if (!::isatty(0)) return;
+    if (tcgetattr(0, &saved) != 0) return;
+    struct termios raw = saved;
+    cfmakeraw(&raw);
+    tcsetattr(0, TCSANOW, &raw);
+    active = true;
+  }
+  ~RawTty() {
+    if (active) tcsetattr(0, TCSANOW, &saved);
+  }
+};
+
+std::atomic<bool> g_winch{false};
+
+void pump_session(kube::ExecSession& s, bool tty, bool forward_stdin, const std::function<bool()>& interrupt) {
+  std::atomic<bool> out_done{false};
+  std::thread t_out([&] {
+    char buf[65536];
+    while (true) {
+      ssize_t n = read_some(s.out(), buf, sizeof(buf));
+      if (n <= 0) break;
+      write_all(1, buf, (size_t)n);
+    }
+    out_done = true;
+  });
+  std::thread t_err([&] {
+    char buf[65536];
+    while (true) {
+      ssize_t n = read_some(s.err(), buf, sizeof(buf));
+      if (n <= 0) break;
+      write_all(2, buf, (size_t)n);
+    }
+  });
+  auto old = signal(SIGWINCH, [](int) { g_winch = true; });
+  auto send_size = [&] {
+    struct winsize ws{};
+    if (ioctl(1, TIOCGWINSZ, &ws) == 0 && ws.ws_col) s.resize(ws.ws_col, ws.ws_row);
+  };
+  if (tty) send_size();
+  char buf[4096];
+  while (!out_done) {
+    if (interrupt && interrupt()) {
+      s.terminate();
+      break;
+    }
+    if (g_winch.exchange(false) && tty) send_size();
+    if (!forward_stdin) {
+      usleep(50000);
+      continue;
+    }
+    struct pollfd pf{0, POLLIN, 0};
+    int r = ::poll(&pf, 1, 100);
+    if (r <= 0) continue;
+    ssize_t n = ::read(0, buf, sizeof(buf));
+    if (n <= 0) {
+      s.close_stdin_if_any();
+      forward_stdin = false;
+      continue;
+    }
+    if (!write_all(s.in(), buf, (size_t)n)) break;
+  }
+  signal(SIGWINCH, old);
+  t_out.join();
+  t_err.join();
+}
+
+Value find_pod(const Value& cfg, kube::Client& k, const Target& t, bool pick, int wait_ms) {
+  if (pick) return select_pod(k, t.namespace_, t.label_selector);
+  try {
+    return k.newest_running_pod(t.namespace_, t.label_selector, wait_ms, 100);
+  } catch (const std::exception&) {
+    return select_pod(k, t.namespace_, t.label_selector);
+  }
+}
+
+}  // namespace
+
+int start_terminal(const Value& cfg, std::shared_ptr<kube::Client> k, const std::string& selector,
+                   const std::string& container, const std::string& label_selector, const std::string& ns, bool pick,
+                   std::vector<std::string> cmd, const std::function<bool()>& interrupt) {
+  Target t = resolve_target(cfg, selector, label_selector, ns, container);
+  log::start_wait("Terminal: Waiting for pods...");
+  Value pod;
+  try {
+    pod = find_pod(cfg, *k, t, pick, 5000);
+  } catch (...) {
+    log::stop_wait();
+    throw;
+  }
+  log::stop_wait();
+  std::string c = select_container(pod, t.container);
+  if (cmd.empty()) {
+    for (auto& s : cfg.at_path("dev.terminal.command").items()) cmd.push_back(s.as_string());
+  }
+  if (cmd.empty()) cmd = {"sh", "-c", "command -v bash >/dev/null 2>&1 && exec bash || exec sh"};
+  bool tty = ::isatty(0) && ::isatty(1);
+  auto s = k->exec(pod.at_path("metadata.namespace").as_string(), pod.at_path("metadata.name").as_string(), c, cmd,
+                   tty, true);
+  {
+    RawTty raw;
+    pump_session(*s, tty, true, interrupt);
+  }
+  int code = s->wait(2000);
+  s->close();
+  return code < 0 ? 0 : code;  // CodeExitError is not a devspace failure (terminal.go:104)
+}
+
+int start_attach(const Value& cfg, std::shared_ptr<kube::Client> k, const std::string& selector,
+                 const std::string& container, const std::string& label_selector, const std::string& ns,
+                 const std::function<bool()>& interrupt) {
+  Target t = resolve_target(cfg, selector, label_selector, ns, container);
+  Value pod = find_pod(cfg, *k, t, false, 5000);
+  std::string c = select_container(pod, t.container);
+  auto s = k->attach(pod.at_path("metadata.namespace").as_string(), pod.at_path("metadata.name").as_string(), c, true,
+                     false);
+  log::info("Attached to container " + c + " of pod " + pod.at_path("metadata.name").as_string());
+  pump_session(*s, false, false, interrupt);
+  int code = s->wait(2000);
+  s->close();
+  return code;
+}
+
+int start_logs(const Value& cfg, std::shared_ptr<kube::Client> k, const std::string& selector,
+               const std::string& container, const std::string& label_selector, const std::string& ns, bool pick,
+               bool follow, int tail, const std::function<bool()>& interrupt) {
+  Target t = resolve_target(cfg, selector, label_selector, ns, container);
+  Value pod = pick ? select_pod(*k, t.namespace_, t.label_selector) : find_pod(cfg, *k, t, false, 5000);
+  std::string c = select_container(pod, t.container);
+  std::string pns = pod.at_path("metadata.namespace").as_string(), pname = pod.at_path("metadata.name").as_string();
+  if (!follow) {
+    log::get().write(k->logs(pns, pname, c, tail));
+    return 0;
+  }
+  std::string path = "/api/v1/namespaces/" + pns + "/pods/" + pname + "/log?container=" + net::url_encode(c) +
+                     "&follow=true&tailLines=" + std::to_string(tail);
+  k->stream(path, [&](const std::string& d) {
+    log::get().write(d);
+    return !(interrupt && interrupt());
+  });
+  return 0;
+}
+
+}  // namespace services
+}  // namespace ds

@@ -1,0 +1,84 @@
+// Dev-time services on selected pods (pkg/devspace/services/*.go): sync, port-forwarding,
+// terminal, attach, logs, and pod/container selection.
+#pragma once
+
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "config/config.h"
+#include "kube/client.h"
+#include "sync/sync.h"
+
+namespace ds {
+namespace services {
+
+struct Target {
+  std::string namespace_, label_selector, container;
+};
+
+// services/attach.go:75 getSelectorNamespaceLabelSelector + container preference.
+Target resolve_target(const Value& cfg, const std::string& selector_flag, const std::string& label_selector_flag,
+                      const std::string& namespace_flag, const std::string& container_flag);
+
+// Interactive pod/container pick among running pods (services/pod_selector.go).
+Value select_pod(kube::Client& k, const std::string& ns, const std::string& label_selector);
+std::string select_container(const Value& pod, const std::string& preferred);
+
+struct SyncOptions {
+  bool verbose = false;
+  sync::Mode mode = sync::Mode::Helper;
+  std::string helper_path;
+  int pod_wait_ms = 120000;
+  int poll_ms = 100;  // pod discovery poll (1000 = reference timing)
+};
+
+std::vector<std::unique_ptr<sync::Session>> start_sync(const Value& cfg, std::shared_ptr<kube::Client> k,
+                                                        const SyncOptions& o);
+
+class PortForwarder {
+ public:
+  PortForwarder(std::shared_ptr<kube::Client> k, Value pod, std::vector<std::pair<int, int>> ports,
+                std::vector<std::string> addresses);
+  ~PortForwarder();
+  // Binds all listeners; throws on failure.
+  void start();
+  void close();
+  std::string describe() const;
+
+ private:
+  void accept_loop(int lfd, int remote_port);
+  void handle(int cfd, int remote_port);
+  std::shared_ptr<kube::Client> k_;
+  Value pod_;
+  std::vector<std::pair<int, int>> ports_;
+  std::vector<std::string> addrs_;
+  std::vector<int> listeners_;
+  std::vector<std::thread> threads_;
+  std::atomic<bool> stop_{false};
+};
+
+std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& cfg, std::shared_ptr<kube::Client> k,
+                                                                  int pod_wait_ms = 120000, int poll_ms = 100);
+
+// Runs an interactive command in the container with a TTY when stdin is a terminal
+// (services/terminal.go). `interrupt` is polled; returns the remote exit code.
+int start_terminal(const Value& cfg, std::shared_ptr<kube::Client> k, const std::string& selector,
+                   const std::string& container, const std::string& label_selector, const std::string& ns, bool pick,
+                   std::vector<std::string> cmd, const std::function<bool()>& interrupt);
+
+// Attach to the container output (services/attach.go:18).
+int start_attach(const Value& cfg, std::shared_ptr<kube::Client> k, const std::string& selector,
+                 const std::string& container, const std::string& label_selector, const std::string& ns,
+                 const std::function<bool()>& interrupt);
+
+// Print last N lines, optionally follow (services/logs.go:17).
+int start_logs(const Value& cfg, std::shared_ptr<kube::Client> k, const std::string& selector,
+               const std::string& container, const std::string& label_selector, const std::string& ns, bool pick,
+               bool follow, int tail, const std::function<bool()>& interrupt);
+
+}  // namespace services
+}  // namespace ds
