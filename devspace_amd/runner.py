@@ -262,7 +262,10 @@ def _spawn_group(args, port):
             MASTER_PORT=str(port),
             HSA_ENABLE_IPC_MODE_LEGACY=env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
         )
-        cmd = [sys.executable, "-m", "devspace_amd.runner", "--worker"] + _forward(args)
+        # Installed as a package (-m devspace_amd.runner) or vendored as a single file into a
+        # project by `devspace init` (rocm-pytorch template).
+        me = ["-m", "devspace_amd.runner"] if __package__ else [os.path.abspath(__file__)]
+        cmd = [sys.executable] + me + ["--worker"] + _forward(args)
         procs.append(subprocess.Popen(cmd, env=env))
     return procs
 

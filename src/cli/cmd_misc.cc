@@ -1,0 +1,276 @@
+// install / upgrade / login / version, plus two hidden helpers: `sync` (a standalone sync
+// session against one pod, the engine behind `devspace dev`) and `local-cluster` (starts the
+// bundled single-node API server + process kubelet for offline use and tests).
+//
+// Reference: cmd/install.go:40 (add executable dir to PATH), cmd/upgrade.go:39 +
+// pkg/devspace/upgrade/upgrade.go:67 (self-update), cmd/login.go:48 (cloud.ReLogin).
+#include <limits.h>
+#include <signal.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <thread>
+
+#include "cli/common.h"
+#include "cloud/cloud.h"
+#include "core/fs.h"
+#include "core/log.h"
+#include "core/proc.h"
+#include "core/strutil.h"
+#include "deploy/helmrepo.h"
+#include "services/services.h"
+#include "sync/sync.h"
+
+namespace ds {
+namespace cmd {
+
+namespace {
+
+using Args = std::vector<std::string>;
+
+std::string self_exe() {
+  char buf[PATH_MAX];
+  ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);
+  if (n <= 0) return "";
+  buf[n] = 0;
+  return buf;
+}
+
+// envutil.AddToPath: append an export line to the user's shell profile (idempotent).
+int run_install(cli::Command&, const Args&) {
+  std::string dir = fs::dirname(self_exe());
+  if (dir.empty()) log::fatal("Unable to get executable path");
+  std::string line = "export PATH=\"$PATH:" + dir + "\"  # added by devspace install";
+  bool any = false;
+  for (const char* rc : {".bashrc", ".zshrc", ".profile"}) {
+    std::string p = fs::join(fs::home_dir(), rc);
+    if (!fs::exists(p) && std::string(rc) != ".profile") continue;
+    std::string data;
+    fs::read_file(p, &data);
+    if (contains(data, line)) {
+      any = true;
+      continue;
+    }
+    fs::append_file(p, (data.empty() || data.back() == '\n' ? "" : "\n") + line + "\n");
+    any = true;
+  }
+  if (!any) log::fatal("Unable to add devspace install dir to path");
+  log::done("Added " + dir + " to PATH (open a new shell to use `devspace`)");
+  return 0;
+}
+
+// Versions compare like semver; a pre-release suffix sorts before the release.
+int compare_release(const std::string& a, const std::string& b) {
+  auto core = [](const std::string& v) { return split(trim_left(v, "v"), "-")[0]; };
+  int c = helmrepo::compare_versions(core(a), core(b));
+  if (c != 0) return c;
+  bool pa = contains(a, "-"), pb = contains(b, "-");
+  return pa == pb ? 0 : (pa ? -1 : 1);
+}
+
+// Self-update from a release source: a local binary (--from) or a URL serving
+// "<url>/latest" (version text) and "<url>/devspace-linux-amd64" (DEVSPACE_RELEASE_URL).
+int run_upgrade(cli::Command& c, const Args&) {
+  log::start_file_logging();
+  std::string from = c.get_str("from");
+  std::string url = getenv("DEVSPACE_RELEASE_URL") ? getenv("DEVSPACE_RELEASE_URL") : "";
+  std::string tmp;
+  std::string newest;
+  try {
+    if (!from.empty()) {
+      RunResult r = run({from, "version"}, "", {}, 20000);
+      if (r.code != 0) throw std::runtime_error(from + " is not a devspace binary");
+      newest = trim(r.out);
+      auto sp = newest.rfind(' ');
+      if (sp != std::string::npos) newest = newest.substr(sp + 1);
+      tmp = from;
+    } else if (!url.empty()) {
+      newest = trim(helmrepo::fetch(trim_right(url, "/") + "/latest"));
+    } else {
+      throw std::runtime_error(
+          "no release source configured (use --from <binary> or set DEVSPACE_RELEASE_URL); this build has no "
+          "network access to a release server");
+    }
+    if (compare_release(newest, kVersion) <= 0) {
+      log::info(std::string("Current binary is the latest version: ") + kVersion);
+      return 0;
+    }
+    log::info("Downloading newest version...");
+    std::string exe = self_exe();
+    std::string staged = exe + ".new";
+    if (!from.empty())
+      fs::copy(tmp, staged, true);
+    else
+      fs::write_file(staged, helmrepo::fetch(trim_right(url, "/") + "/devspace-linux-amd64"), 0755);
+    chmod(staged.c_str(), 0755);
+    if (!fs::rename(staged, exe)) throw std::runtime_error("cannot replace " + exe);
+    log::info("Successfully updated to version " + newest);
+  } catch (const std::exception& e) {
+    log::fatal(std::string("Couldn't upgrade: ") + e.what());
+  }
+  return 0;
+}
+
+int run_login(cli::Command& c, const Args&) {
+  std::string name = c.get_str("provider");
+  try {
+    auto ps = cloud::load_providers();
+    if (!ps.count(name)) throw std::runtime_error("Cloud provider " + name + " not found");
+    if (!c.get_str("token").empty()) {
+      ps[name].token = c.get_str("token");
+      cloud::save_providers(ps);
+    } else {
+      ps[name].token.clear();
+      cloud::save_providers(ps);
+    }
+    cloud::ensure_logged_in(name);
+  } catch (const std::exception& e) {
+    log::fatal(std::string("Error logging in: ") + e.what());
+  }
+  log::info("Successful logged into " + name);
+  return 0;
+}
+
+// Standalone sync (hidden): local dir <-> container path of one pod (or the newest running
+// pod of a label selector). Runs until interrupted or --once finishes the initial sync.
+int run_sync(cli::Command& c, const Args&) {
+  Session s;
+  bool have_root = config::set_devspace_root();
+  Value cfg = Value::map();
+  try {
+    if (have_root) cfg = s.ctx.get();
+    s.kube = kube::Client::from_devspace_config(cfg, false);
+  } catch (const std::exception& e) {
+    log::fatal(e.what());
+  }
+  std::string ns = c.get_str("namespace").empty() ? config::default_namespace(cfg) : c.get_str("namespace");
+  Value pod;
+  try {
+    if (!c.get_str("pod").empty())
+      pod = s.kube->get("/api/v1/namespaces/" + ns + "/pods/" + c.get_str("pod"));
+    else
+      pod = s.kube->newest_running_pod(ns, c.get_str("label-selector"), 120000);
+  } catch (const std::exception& e) {
+    log::fatal(std::string("Unable to find pod: ") + e.what());
+  }
+  std::string container = c.get_str("container-name");
+  if (container.empty()) container = pod.at_path("spec.containers")[0].get("name").as_string();
+  sync::Options o;
+  o.watch_path = fs::abs_path(c.get_str("local"));
+  o.dest_path = c.get_str("container");
+  o.pod_name = pod.at_path("metadata.name").as_string();
+  o.exclude_paths = c.get_slice("exclude");
+  o.verbose = c.get_bool("verbose");
+  o.helper_path = helper_path();
+  o.mode = sync::parse_mode(c.get_str("mode").empty() ? (fs::is_file(o.helper_path) ? "helper" : "fast")
+                                                      : c.get_str("mode"));
+  auto transport = std::make_shared<kube::ExecTransport>(s.kube, pod, container);
+  sync::Session session(o, transport);
+  try {
+    session.start();
+    session.wait_initial_sync(-1);
+  } catch (const std::exception& e) {
+    log::fatal(std::string("Sync error: ") + e.what());
+  }
+  log::done("Sync started on " + o.watch_path + " <-> " + o.dest_path + " (pod " + o.pod_name + ", mode " +
+            sync::mode_name(session.effective_mode()) + ")");
+  if (c.get_bool("once")) {
+    session.stop();
+    return 0;
+  }
+  while (!interrupted() && session.running()) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  std::string err = session.error();
+  session.stop();
+  if (!err.empty()) log::fatal("Sync error: " + err);
+  return 0;
+}
+
+// Starts the bundled local cluster in the foreground (python3 -m devspace_amd.localkube up).
+int run_local_cluster(cli::Command& c, const Args&) {
+  std::string root = fs::dirname(fs::dirname(self_exe()));  // <repo>/bin/devspace -> <repo>
+  std::vector<std::string> argv = {"python3", "-m", "devspace_amd.localkube", "up", "--state", c.get_str("state")};
+  if (c.get_int("port")) argv.insert(argv.end(), {"--port", std::to_string(c.get_int("port"))});
+  if (c.changed("gpus")) argv.insert(argv.end(), {"--gpus", std::to_string(c.get_int("gpus"))});
+  if (!c.get_str("namespace").empty()) argv.insert(argv.end(), {"--namespace", c.get_str("namespace")});
+  ProcOptions o;
+  o.pipe_stdout = o.pipe_stderr = false;
+  const char* pp = getenv("PYTHONPATH");
+  o.env = {{"PYTHONPATH", root + (pp && *pp ? ":" + std::string(pp) : "")}};
+  Process p;
+  p.start(argv, o);
+  while (!interrupted() && p.running()) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  if (p.running()) p.kill(SIGTERM);
+  return p.wait();
+}
+
+}  // namespace
+
+void register_misc(cli::Command& root) {
+  {
+    auto c = std::make_unique<cli::Command>("install", "Installs the DevSpace.cli",
+                                            "Adds the directory of the devspace binary to PATH in your shell profile");
+    c->max_args = 0;
+    c->run = run_install;
+    root.add(std::move(c));
+  }
+  {
+    auto c = std::make_unique<cli::Command>("upgrade", "Upgrade the DevSpace.cli to the newest version",
+                                            "Upgrades the DevSpace.cli to the newest version");
+    c->max_args = 0;
+    c->str("from", "", "", "Path of a newer devspace binary to install");
+    c->run = run_upgrade;
+    root.add(std::move(c));
+  }
+  {
+    auto c = std::make_unique<cli::Command>(
+        "login", "Log into DevSpace.cloud",
+        "If no --token is supplied the browser will be opened\nand the login page is shown\n\nExample:\ndevspace "
+        "login\ndevspace login --token 123456789");
+    c->max_args = 0;
+    c->str("token", "", "", "Token to use for login")
+        .str("provider", "", cloud::kDefaultProviderName, "Cloud provider to use");
+    c->run = run_login;
+    root.add(std::move(c));
+  }
+  {
+    auto c = std::make_unique<cli::Command>("version", "Prints the devspace version");
+    c->max_args = 0;
+    c->run = [](cli::Command&, const Args&) {
+      log::get().write(std::string("devspace version ") + kVersion + "\n");
+      return 0;
+    };
+    root.add(std::move(c));
+  }
+  {
+    auto c = std::make_unique<cli::Command>("sync", "Starts a bi-directional sync with a container");
+    c->hidden = true;
+    c->max_args = 0;
+    c->str("local", "", ".", "Local directory")
+        .str("container", "", "/app", "Container path")
+        .str("pod", "", "", "Pod name (default: newest running pod matching --label-selector)")
+        .str("label-selector", "l", "", "Label selector")
+        .str("namespace", "n", "", "Namespace")
+        .str("container-name", "c", "", "Container name")
+        .str("mode", "", "", "Sync protocol: compat | fast | helper")
+        .slice("exclude", "e", "Exclude paths (gitignore syntax)")
+        .boolean("verbose", "", false, "Log every change")
+        .boolean("once", "", false, "Exit after the initial sync");
+    c->run = run_sync;
+    root.add(std::move(c));
+  }
+  {
+    auto c = std::make_unique<cli::Command>("local-cluster", "Runs the bundled single-node cluster");
+    c->hidden = true;
+    c->max_args = 0;
+    c->str("state", "", ".devspace-cluster", "State directory")
+        .integer("port", "", 0, "API server port (0 = random)")
+        .integer("gpus", "", 0, "amd.com/gpu capacity (default: detected)")
+        .str("namespace", "", "", "Namespace for the kube context");
+    c->run = run_local_cluster;
+    root.add(std::move(c));
+  }
+}
+
+}  // namespace cmd
+}  // namespace ds

@@ -310,7 +310,7 @@ std::string token_account(const std::string& jwt) {
 }
 
 void configure(config::Context& ctx, const std::string& space_name) {
-  Value& cfg = const_cast<Value&>(ctx.get(true));
+  Value& cfg = ctx.mutable_config();
   std::string provider = cfg.at_path("cluster.cloudProvider").as_string();
   if (provider.empty()) return;
   Provider p = ensure_logged_in(provider);

@@ -98,6 +98,12 @@ class Context {
   bool config_exists() const;
   // Loads the config (base + overrides when with_overrides). Cached; throws ConfigError.
   const Value& get(bool with_overrides = true);
+  // The loaded (merged) config for in-memory adjustments by command flags (--namespace,
+  // --kube-context, --docker-target, cloud space injection). Not saved.
+  Value& mutable_config() {
+    get(true);
+    return config_;
+  }
   // The base config (no overrides), mutable for add/remove/configure commands.
   Value& base();
   // Validation (ValidateOnce, get.go:234) — throws ConfigError with the reference's messages.

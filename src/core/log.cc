@@ -4,6 +4,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <cstdarg>
 #include <cstdio>
 #include <iostream>
 
@@ -268,6 +269,38 @@ std::shared_ptr<FileLogger> file_logger(const std::string& name) {
 
 void start_file_logging() {
   if (auto* s = stdout_logger()) s->set_file_logger(file_logger("default"));
+}
+
+}  // namespace log
+}  // namespace ds
+
+namespace ds {
+namespace log {
+
+static std::string vformat(const char* fmt, va_list ap) {
+  va_list ap2;
+  va_copy(ap2, ap);
+  int n = vsnprintf(nullptr, 0, fmt, ap2);
+  va_end(ap2);
+  std::string out(n > 0 ? n : 0, '\0');
+  if (n > 0) vsnprintf(&out[0], n + 1, fmt, ap);
+  return out;
+}
+
+void donef(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  std::string m = vformat(fmt, ap);
+  va_end(ap);
+  done(m);
+}
+
+void infof(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  std::string m = vformat(fmt, ap);
+  va_end(ap);
+  info(m);
 }
 
 }  // namespace log

@@ -130,6 +130,8 @@ inline void stop_wait() { get().stop_wait(); }
 inline void print_table(const std::vector<std::string>& h, const std::vector<std::vector<std::string>>& r) {
   get().print_table(h, r);
 }
+void donef(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+void infof(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 
 // ANSI colouring helper ("green+b", "red+b", "cyan+b", "white+b", "166+b").
 std::string color(const std::string& text, const std::string& spec);

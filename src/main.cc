@@ -1,1 +1,15 @@
-int main() { return 0; }
+// devspace CLI entry point (main.go / cmd/root.go:35 Execute).
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cli/common.h"
+#include "core/log.h"
+
+int main(int argc, char** argv) {
+  ds::cmd::install_signal_handlers();
+  std::vector<std::string> args(argv + 1, argv + argc);
+  if (args.size() == 1 && (args[0] == "--version" || args[0] == "-v")) args[0] = "version";
+  auto root = ds::cmd::make_root();
+  return root->execute(args);
+}
