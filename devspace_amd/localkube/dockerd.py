@@ -9,6 +9,7 @@ CMD/ENTRYPOINT/LABEL/USER; RUN is recorded but not executed — no network on th
 
 from __future__ import annotations
 
+import glob
 import gzip
 import hashlib
 import io
@@ -177,8 +178,21 @@ def build_image(store, context_dir, dockerfile, tag, buildargs=None, target=None
             base_src = stages[from_stage]["rootfs"] if from_stage in stages else context_dir
             dst_abs = dst if dst.startswith("/") else os.path.join(config["WorkingDir"], dst)
             dst_path = os.path.join(rootfs, dst_abs.lstrip("/"))
+            expanded = []
             for s in srcs:
-                sp = os.path.normpath(os.path.join(base_src, s.lstrip("/") if from_stage else s))
+                pat = os.path.join(base_src, s.lstrip("/") if from_stage else s)
+                if any(ch in s for ch in "*?["):
+                    hits = sorted(glob.glob(pat))
+                    if not hits:
+                        raise RuntimeError(f"COPY failed: no source files were specified ({s})")
+                    expanded.extend(hits)
+                    if len(hits) > 1 and not dst.endswith("/"):
+                        dst = dst + "/"
+                else:
+                    expanded.append(pat)
+            for sp in expanded:
+                s = os.path.relpath(sp, base_src)
+                sp = os.path.normpath(sp)
                 if os.path.isdir(sp):
                     shutil.copytree(sp, dst_path, dirs_exist_ok=True, symlinks=True)
                 elif os.path.exists(sp):

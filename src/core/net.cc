@@ -360,7 +360,9 @@ bool read_response_head(Conn& c, Response* r, std::string* rest, int timeout_ms)
 }
 
 static std::string build_request(const HttpClient& h, const Request& r) {
-  std::string path = h.url().path + r.path;
+  std::string base = h.url().path;
+  if (!base.empty() && base.back() == '/' && !r.path.empty() && r.path[0] == '/') base.pop_back();
+  std::string path = base + r.path;
   if (path.empty()) path = "/";
   std::string host = h.url().unix_path.empty() ? h.url().host : "localhost";
   std::string out = r.method + " " + path + " HTTP/1.1\r\nHost: " + host + "\r\n";

@@ -115,8 +115,7 @@ std::string ask(const Params& p) {
       } catch (const std::regex_error&) {
       }
     }
-    if (ans.empty() && !tty) throw PromptError("empty answer for: " + q);
-    if (ans.empty()) continue;
+    // No validation pattern = "^.*$" (stdin.go:40): an empty answer is a valid answer.
     return ans;
   }
 }

@@ -5,6 +5,7 @@
 #include <set>
 #include <thread>
 
+#include "analyze/analyze.h"
 #include "core/codec.h"
 #include "core/fs.h"
 #include "core/log.h"
@@ -254,8 +255,20 @@ std::string Client::wait_ready(const std::vector<Value>& objs, const std::string
           pending = kind + " " + name + " not found";
           break;
         }
+        // The controller must have seen the new spec before readiness counts (rollout status).
+        if (kind != "ReplicaSet" &&
+            cur->at_path("status.observedGeneration").as_int(0) < cur->at_path("metadata.generation").as_int(1)) {
+          pending = kind + " " + name + ": waiting for the controller to observe generation " +
+                    std::to_string(cur->at_path("metadata.generation").as_int(1));
+          break;
+        }
         int64_t want = cur->at_path("spec.replicas").as_int(1);
         if (kind == "DaemonSet") want = cur->at_path("status.desiredNumberScheduled").as_int(1);
+        if (kind == "Deployment" && cur->at_path("status.updatedReplicas").as_int(0) < want) {
+          pending = kind + " " + name + ": " + std::to_string(cur->at_path("status.updatedReplicas").as_int(0)) + "/" +
+                    std::to_string(want) + " updated";
+          break;
+        }
         int64_t ready = cur->at_path("status.readyReplicas").as_int(0);
         if (kind == "DaemonSet") ready = cur->at_path("status.numberReady").as_int(0);
         if (ready < want) {
@@ -333,6 +346,18 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
       }
     }
     if (wait) err = wait_ready(objs, ns, timeout_s > 0 ? timeout_s : 40);
+    // install.go:181 analyzeError: a wait timeout is explained by an analyze report of the
+    // namespace; no problems found means the release is fine (just slow).
+    if (contains(err, "timed out waiting")) {
+      try {
+        analyze::Options ao;
+        ao.wait = false;
+        auto report = analyze::create_report(*k_, ns, ao);
+        err = report.empty() ? "" : analyze::report_to_string(report);
+      } catch (const std::exception& e) {
+        log::warn(std::string("Error creating analyze report: ") + e.what());
+      }
+    }
   } catch (const std::exception& e) {
     err = e.what();
   }

@@ -167,8 +167,16 @@ void PortForwarder::start() {
     if (addr == "localhost") addr = "127.0.0.1";
     if (inet_pton(AF_INET, addr.c_str(), &a.sin_addr) != 1) a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
     if (::bind(fd, (struct sockaddr*)&a, sizeof(a)) != 0 || ::listen(fd, 64) != 0) {
-      std::string e = std::strerror(errno);
+      int err = errno;
+      std::string e = std::strerror(err);
       ::close(fd);
+      // Pods of the bundled local cluster share the host network: a same-number mapping is
+      // already served by the container itself.
+      if (err == EADDRINUSE && k_->is_local_cluster() && ports_[i].first == ports_[i].second) {
+        log::info("Port " + std::to_string(ports_[i].first) +
+                  " is served directly by the pod (local cluster shares the host network)");
+        continue;
+      }
       throw std::runtime_error("Unable to listen on port " + std::to_string(ports_[i].first) + ": " + e);
     }
     listeners_.push_back(fd);

@@ -24,3 +24,60 @@ def native_build():
 @pytest.fixture
 def devspace_bin():
     return os.path.join(ROOT, "bin", "devspace")
+
+
+class DevspaceEnv:
+    """A running local cluster plus an isolated HOME/KUBECONFIG for `devspace` invocations."""
+
+    def __init__(self, cluster, base):
+        import subprocess  # noqa: F401
+
+        self.cluster = cluster
+        self.base = base
+        self.home = os.path.join(base, "home")
+        os.makedirs(self.home, exist_ok=True)
+        self.kubeconfig = cluster.write_kubeconfig(os.path.join(self.home, ".kube", "config"))
+        self.env = dict(os.environ)
+        self.env.update(cluster.env(self.kubeconfig))
+        self.env.update(HOME=self.home, DEVSPACE_NONINTERACTIVE="1", PYTHONPATH=ROOT)
+        self.bin = os.path.join(ROOT, "bin", "devspace")
+
+    def run(self, args, cwd, input=None, timeout=120, check=True):
+        import subprocess
+
+        p = subprocess.run([self.bin] + list(args), cwd=cwd, env=self.env, input=input, capture_output=True,
+                           text=True, timeout=timeout)
+        if check and p.returncode != 0:
+            raise AssertionError(f"devspace {' '.join(args)} failed rc={p.returncode}\n{p.stdout}\n{p.stderr}")
+        return p
+
+    def popen(self, args, cwd):
+        import subprocess
+
+        return subprocess.Popen([self.bin] + list(args), cwd=cwd, env=self.env, stdout=subprocess.PIPE,
+                                stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, text=True,
+                                start_new_session=True)
+
+    def pods(self, namespace, selector=""):
+        return self.cluster.store.list("", "pods", namespace, selector)
+
+    def project(self, example, dst_name=None):
+        import shutil
+
+        dst = os.path.join(self.base, dst_name or example)
+        if os.path.exists(dst):
+            shutil.rmtree(dst)
+        shutil.copytree(os.path.join(ROOT, "examples", example), dst, symlinks=True)
+        return dst
+
+
+@pytest.fixture(scope="module")
+def localkube(tmp_path_factory):
+    from devspace_amd.localkube import LocalCluster
+
+    base = str(tmp_path_factory.mktemp("lk"))
+    cluster = LocalCluster(os.path.join(base, "state"), gpus=int(os.environ.get("LK_GPUS", "0"))).start()
+    try:
+        yield DevspaceEnv(cluster, base)
+    finally:
+        cluster.stop()
