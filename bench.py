@@ -2,24 +2,29 @@
 """Inner-loop benchmark: edit -> pod hot-reload latency (+ deploy wall-clock) on MI355X.
 
 BASELINE.json metric: "inner-loop p50 ms (edit->pod hot-reload) + deploy wall-clock s".
-The pod is the rocm/pytorch example (examples/rocm-pytorch/train.py, a bf16 TinyLM training
-loop) served by the local-pod backend: `devspace deploy` against the bundled local cluster
-(fake Kubernetes API server + process kubelet + Docker-API image builder, all on this host —
-no k8s/network on the GPU box), then `devspace dev` syncs the project into the pod while the
-workload runs under devspace_amd.runner on N GPUs (one process per GPU, RCCL over xGMI).
 
-One timed "step" = edit train.py locally -> change synced into the pod -> runner swaps code ->
-first training step with the new code completes on every GPU (rank 0 prints the marker).
+Everything goes through the real `devspace` CLI against the bundled local cluster (fake
+Kubernetes API server + process kubelet advertising amd.com/gpu + Docker Engine API builder,
+all on this host — the GPU box has no k8s/Docker/network):
 
-Two columns are reported (BASELINE.md "How the rebuild will be compared"):
-  value                          this framework (fast sync protocol + warm hot-reload)
-  reference_equivalent_p50_ms    same hardware, reference constants: compat sync protocol
-                                 (600 ms window, sleep-0.1 receive polling) + cold restart
-                                 of the workload on change (nodemon-style, as the reference)
+  1. deploy wall-clock: `devspace deploy` of examples/quickstart on a fresh cluster (image
+     build + push + Helm install + rollout wait), cold and forced-warm.
+  2. inner loop: examples/rocm-pytorch (bf16 TinyLM training pod, amd.com/gpu: N, one process
+     per GPU under devspace_amd.runner with an RCCL process group) is deployed with
+     `devspace deploy`, then `devspace dev` syncs the project into the pod over the exec
+     WebSocket and attaches to its output. One timed step = edit train.py locally -> change
+     synced into the pod -> runner swaps code at the step boundary -> first training step with
+     the new code finishes on every GPU -> its log line reaches `devspace dev`'s terminal.
+
+Reported columns (BASELINE.md "How the rebuild will be compared"):
+  value                        this framework (`devspace dev`: helper sync + warm hot-reload)
+  reference_equivalent_p50_ms  same hardware, reference constants: compat sync protocol
+                               (600 ms batching window, 1.3 s poll) + cold restart of the
+                               workload on change (nodemon-style, as the reference's examples)
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 For N>1 the driver launches one bench rank per GPU with torch.distributed.run; rank 0 drives
-the dev loop for a pod requesting amd.com/gpu: N, the other ranks join the barriers.
+the dev loop for a pod requesting amd.com/gpu: N; the other ranks join the timing barriers.
 """
 
 from __future__ import annotations
@@ -30,7 +35,6 @@ import os
 import re
 import shutil
 import signal
-import statistics
 import subprocess
 import sys
 import tempfile
@@ -41,6 +45,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "inner-loop p50 ms (edit->pod hot-reload) + deploy wall-clock s, quickstart"
+TINY = (("VOCAB", 256), ("DIM", 64), ("HEADS", 4), ("LAYERS", 1), ("SEQ", 32), ("BATCH", 2))
 
 
 def _pct(xs, q):
@@ -50,6 +55,11 @@ def _pct(xs, q):
     k = (len(xs) - 1) * q
     lo, hi = int(k), min(int(k) + 1, len(xs) - 1)
     return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
+
+
+def _log(msg):
+    sys.stderr.write(f"[bench] {msg}\n")
+    sys.stderr.flush()
 
 
 class LineTail:
@@ -85,9 +95,13 @@ class LineTail:
                         return t, line, i
                 left = deadline - time.monotonic()
                 if left <= 0:
-                    tail = "\n".join(l for _, l in self.lines[-20:])
+                    tail = "\n".join(l for _, l in self.lines[-30:])
                     raise TimeoutError(f"timed out waiting for /{pattern}/; last output:\n{tail}")
                 self.cv.wait(left)
+
+    def size(self):
+        with self.cv:
+            return len(self.lines)
 
 
 def _set_marker(path, marker):
@@ -98,7 +112,14 @@ def _set_marker(path, marker):
         f.write(src)
 
 
-def _wait_file_contains(path, needle, timeout=60.0):
+def _shrink(path):
+    s = open(path).read()
+    for k, v in TINY:
+        s = re.sub(rf"^{k} = \d+$", f"{k} = {v}", s, flags=re.M)
+    open(path, "w").write(s)
+
+
+def _wait_file_contains(path, needle, timeout=60.0, interval=0.0002):
     deadline = time.monotonic() + timeout
     nb = needle.encode()
     while time.monotonic() < deadline:
@@ -108,38 +129,111 @@ def _wait_file_contains(path, needle, timeout=60.0):
                     return time.perf_counter()
         except OSError:
             pass
-        time.sleep(0.0002)
+        time.sleep(interval)
     raise TimeoutError(f"{needle} never reached {path}")
 
 
-def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False, timed_start=None, timed_end=None):
-    """Runs the edit->reload loop against a local pod directory; returns latency samples.
+def _killpg(p, grace=15):
+    if p is None or p.poll() is not None:
+        return
+    try:
+        os.killpg(p.pid, signal.SIGINT)
+        p.wait(grace)
+    except (ProcessLookupError, subprocess.TimeoutExpired):
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        p.wait()
 
-    `timed_start`/`timed_end` are invoked right before the first and after the last timed
-    step (after warmup), so the caller can bracket exactly K steps with barriers."""
+
+# ---------------------------------------------------------------------------- full CLI path
+
+
+def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, timed_end=None):
+    """`devspace deploy` + `devspace dev` of examples/rocm-pytorch on the local cluster."""
+    from devspace_amd.localkube import LocalCluster
+    from devspace_amd.localkube.bench import devspace_env, run_devspace
+
+    base = os.path.join(workdir, "dev-bench")
+    proj = os.path.join(base, "rocm-pytorch")
+    shutil.copytree(os.path.join(ROOT, "examples", "rocm-pytorch"), proj, symlinks=True)
+    train = os.path.join(proj, "train.py")
+    if tiny:
+        _shrink(train)
+    values = os.path.join(proj, "chart", "values.yaml")
+    v = open(values).read()
+    v = re.sub(r"gpu: \d+", f"gpu: {gpus}", v)
+    open(values, "w").write(v)
+
+    cluster = LocalCluster(os.path.join(base, "cluster"), gpus=gpus).start()
+    dev = None
+    try:
+        env = devspace_env(cluster, base)
+        env["DEVSPACE_NPROC"] = str(nproc)  # used when the pod requests no GPU (CPU smoke)
+        cluster.kubelet.extra_env["DEVSPACE_NPROC"] = str(nproc)
+        # `devspace dev` builds (dev image cache), deploys the chart, waits for the rollout,
+        # then starts sync + attach on the newest running pod.
+        t_dev = time.perf_counter()
+        dev = subprocess.Popen([os.path.join(ROOT, "bin", "devspace"), "dev", "--terminal=false",
+                                "--portforwarding=false"], cwd=proj, env=env, stdout=subprocess.PIPE,
+                               stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, start_new_session=True)
+        tail = LineTail(dev.stdout, echo_prefix="[dev] ")
+        _, line, idx = tail.wait_for(r"Sync started on", timeout=900)
+        deploy_s = time.perf_counter() - t_dev
+        ns, pod_name = re.search(r"Pod: ([^/\s]+)/([^)\s]+)", line).groups()
+        pod = cluster.store.get("", "pods", ns, pod_name)
+        cname = pod["spec"]["containers"][0]["name"]
+        root = json.loads(pod["metadata"]["annotations"]["devspace.sh/local-roots"])[cname]
+        _log(f"dev: pod {pod_name} synced after {deploy_s:.2f}s")
+        _, _, idx = tail.wait_for(r"Attached to container", start_index=idx, timeout=120)
+        _wait_file_contains(root + ".log", "[devspace-runner] started gen=", timeout=900, interval=0.05)
+        _log("runner up")
+        mode = os.environ.get("DEVSPACE_SYNC_MODE") or (
+            "helper" if os.path.exists(os.path.join(ROOT, "bin", "devspace-helper")) else "fast")
+        pod_file = os.path.join(root, "app", "train.py")
+        samples, sync_samples = [], []
+        for i in range(warmup + steps):
+            if i == warmup and timed_start:
+                timed_start()
+            marker = f"e{i}" + ("_" * (i % 2))
+            t0 = time.perf_counter()
+            _set_marker(train, marker)
+            t_sync = _wait_file_contains(pod_file, f'MARKER = "{marker}"')
+            pat = rf"\[devspace-runner\] (reloaded|started) gen=\d+ marker={re.escape(marker)} "
+            t1, _, idx = tail.wait_for(pat, start_index=idx, timeout=600)
+            if i >= warmup:
+                samples.append((t1 - t0) * 1000.0)
+                sync_samples.append((t_sync - t0) * 1000.0)
+        if timed_end:
+            timed_end()
+        return {"reload_ms": samples, "sync_ms": sync_samples, "mode": mode, "pod_deploy_s": deploy_s}
+    finally:
+        _killpg(dev)
+        cluster.stop()
+
+
+# ---------------------------------------------------------------------------- reference-equivalent
+
+
+def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False):
+    """Edit -> reload against a pod directory through the sync engine directly.
+
+    Used for the reference-equivalent column: compat sync protocol (the reference's shell
+    scripts and timing constants) + cold restart of the workload on every change."""
     from devspace_amd import _native
 
-    proj = os.path.join(workdir, f"proj-{sync_mode}-{'restart' if restart else 'hot'}")
-    pod = os.path.join(workdir, f"pod-{sync_mode}-{'restart' if restart else 'hot'}", "app")
+    tag = f"{sync_mode}-{'restart' if restart else 'hot'}"
+    proj = os.path.join(workdir, f"proj-{tag}")
+    pod = os.path.join(workdir, f"pod-{tag}", "app")
     os.makedirs(proj, exist_ok=True)
     os.makedirs(pod, exist_ok=True)
     shutil.copy(os.path.join(ROOT, "examples", "rocm-pytorch", "train.py"), os.path.join(proj, "train.py"))
     if tiny:
-        p = os.path.join(proj, "train.py")
-        s = open(p).read()
-        for k, v in (("VOCAB", 256), ("DIM", 64), ("HEADS", 4), ("LAYERS", 1), ("SEQ", 32), ("BATCH", 2)):
-            s = re.sub(rf"^{k} = \d+$", f"{k} = {v}", s, flags=re.M)
-        open(p, "w").write(s)
-    helper = os.path.join(ROOT, "bin", "devspace-helper")
-    sess = _native.SyncSession(
-        proj,
-        pod,
-        mode=sync_mode,
-        exclude=["__pycache__/", "*.pyc"],
-        helper_path=helper,
-        log_dir=os.path.join(workdir, "logs"),
-        pod_name=f"bench-{sync_mode}",
-    )
+        _shrink(os.path.join(proj, "train.py"))
+    sess = _native.SyncSession(proj, pod, mode=sync_mode, exclude=["__pycache__/", "*.pyc"],
+                               helper_path=os.path.join(ROOT, "bin", "devspace-helper"),
+                               log_dir=os.path.join(workdir, "logs"), pod_name=f"bench-{sync_mode}")
     sess.start()
     if not sess.wait_initial_sync(60000):
         raise RuntimeError(f"initial sync failed: {sess.error()}")
@@ -152,17 +246,14 @@ def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False, ti
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     runner = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, start_new_session=True)
-    tail = LineTail(runner.stdout, echo_prefix=f"[{sync_mode}] ")
+    tail = LineTail(runner.stdout, echo_prefix=f"[{tag}] ")
     samples, sync_samples = [], []
     try:
         _, _, idx = tail.wait_for(r"\[devspace-runner\] started gen=\d+ marker=v0", timeout=600)
-        proj_file = os.path.join(proj, "train.py")
-        pod_file = os.path.join(pod, "train.py")
+        proj_file, pod_file = os.path.join(proj, "train.py"), os.path.join(pod, "train.py")
         for i in range(warmup + steps):
-            if i == warmup and timed_start:
-                timed_start()
-            # alternate marker lengths so consecutive edits always differ in size (the
-            # reference-equivalent mode compares rounded mtimes + size, like the reference)
+            # alternate marker lengths so consecutive edits always differ in size (compat mode
+            # compares rounded mtimes + size, like the reference)
             marker = f"e{i}" + ("_" * (i % 2))
             t0 = time.perf_counter()
             _set_marker(proj_file, marker)
@@ -172,9 +263,6 @@ def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False, ti
             if i >= warmup:
                 samples.append((t1 - t0) * 1000.0)
                 sync_samples.append((t_sync - t0) * 1000.0)
-        if timed_end:
-            timed_end()
-        stats = sess.stats()
     finally:
         try:
             os.killpg(runner.pid, signal.SIGTERM)
@@ -186,20 +274,10 @@ def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False, ti
             os.killpg(runner.pid, signal.SIGKILL)
             runner.wait()
         sess.stop()
-    return {"reload_ms": samples, "sync_ms": sync_samples, "sync_stats": stats, "mode": sess.mode()}
+    return {"reload_ms": samples, "sync_ms": sync_samples, "mode": sess.mode()}
 
 
-def deploy_wall_clock(workdir):
-    """`devspace deploy` of the quickstart-style project against the local cluster (seconds)."""
-    try:
-        from devspace_amd.localkube import bench_deploy
-    except Exception:
-        return None
-    try:
-        return bench_deploy(workdir)
-    except Exception as e:  # reported, not fatal for the latency metric
-        sys.stderr.write(f"deploy benchmark failed: {e}\n")
-        return None
+# ---------------------------------------------------------------------------- main
 
 
 def main():
@@ -207,8 +285,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--ref-steps", type=int, default=5, help="timed steps for the reference-equivalent run")
-    ap.add_argument("--sync-mode", default="fast", choices=["fast", "helper", "compat"])
+    ap.add_argument("--ref-steps", type=int, default=3, help="timed steps for the reference-equivalent run (0=skip)")
+    ap.add_argument("--no-deploy-bench", action="store_true", help="skip the quickstart deploy wall-clock")
     ap.add_argument("--tiny", action="store_true", help="tiny model (CPU smoke only)")
     args = ap.parse_args()
 
@@ -224,6 +302,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
+        # bench ranks only coordinate timing; the workload's own RCCL group lives in the pod
         dist.init_process_group("gloo", rank=rank, world_size=world)
         pg = dist
 
@@ -233,10 +312,12 @@ def main():
         if cuda:
             torch.cuda.synchronize()
 
-    nproc = max(args.gpus, world) if cuda else 1
+    nproc = max(args.gpus, world)
+    gpus = nproc if cuda else 0
+    if not cuda:
+        nproc = 1
     workdir = tempfile.mkdtemp(prefix="devspace-bench-")
-    result = {}
-    deploy_s = None
+    result, ref, deploy = {}, None, None
     clock = {}
 
     def timed_start():
@@ -249,17 +330,25 @@ def main():
 
     try:
         if rank == 0:
-            deploy_s = deploy_wall_clock(workdir)
-            result = inner_loop(workdir, args.sync_mode, False, nproc, args.steps, args.warmup, tiny=args.tiny,
-                                timed_start=timed_start, timed_end=timed_end)
+            if not args.no_deploy_bench:
+                try:
+                    deploy = __import__("devspace_amd.localkube.bench", fromlist=["bench_deploy"]).bench_deploy(workdir)
+                    _log(f"quickstart deploy cold {deploy['cold_s']:.3f}s warm {deploy['warm_s']:.3f}s")
+                except Exception as e:  # reported, not fatal for the latency metric
+                    _log(f"deploy benchmark failed: {e}")
+            result = dev_loop(workdir, nproc, gpus, args.steps, args.warmup, tiny=args.tiny,
+                              timed_start=timed_start, timed_end=timed_end)
         else:
             timed_start()
             timed_end()
         elapsed = clock["t1"] - clock["t0"]
-        ref = None
         if rank == 0 and args.ref_steps > 0:
-            ref = inner_loop(workdir, "compat", True, nproc, args.ref_steps, 1, tiny=args.tiny)
-        barrier_sync()
+            try:
+                ref = inner_loop(workdir, "compat", True, nproc, args.ref_steps, 1, tiny=args.tiny)
+            except Exception as e:
+                _log(f"reference-equivalent run failed: {e}")
+        if pg is not None:
+            pg.barrier()
     finally:
         shutil.rmtree(workdir, ignore_errors=True)
 
@@ -285,26 +374,28 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (random tokens; random-init TinyLM weights)",
+        "data": "synthetic (random tokens; random-init TinyLM weights; examples/quickstart + examples/rocm-pytorch)",
         "config": {
-            "model": "examples/rocm-pytorch TinyLM (4x1024, 67M params) hot-reload pod",
+            "model": "examples/rocm-pytorch TinyLM (4x1024) hot-reload pod" + (" [tiny]" if args.tiny else ""),
             "global_batch": 8 * nproc,
             "seq_len": 512,
             "parallelism": f"dp{nproc}",
+            "path": "devspace deploy + devspace dev (exec-WebSocket sync + attach) on the local-pod backend",
             "sync_mode": result["mode"],
-            "backend": "local-pod (fake k8s API + process kubelet)",
         },
         "p50_ms": round(p50, 2),
         "p90_ms": round(_pct(result["reload_ms"], 0.9), 2),
         "sync_p50_ms": round(_pct(result["sync_ms"], 0.5), 2),
-        "deploy_wall_clock_s": None if deploy_s is None else round(deploy_s, 3),
+        "deploy_wall_clock_s": None if not deploy else round(deploy["cold_s"], 3),
+        "deploy_warm_wall_clock_s": None if not deploy else round(deploy["warm_s"], 3),
+        "gpu_pod_deploy_s": round(result["pod_deploy_s"], 3),
     }
     if ref:
         rp50 = _pct(ref["reload_ms"], 0.5)
         out["reference_equivalent_p50_ms"] = round(rp50, 2)
         out["reference_equivalent_sync_p50_ms"] = round(_pct(ref["sync_ms"], 0.5), 2)
         out["speedup_vs_reference_equivalent"] = round(rp50 / p50, 2) if p50 else None
-    print(json.dumps(out))
+    print(json.dumps(out), flush=True)
     if pg is not None:
         pg.destroy_process_group()
     return 0

@@ -1,0 +1,55 @@
+"""Deploy wall-clock of the quickstart example through the real CLI (BASELINE metric part 2).
+
+`devspace deploy` of examples/quickstart against a fresh local cluster: image build via the
+Docker Engine API, push, native Helm install, and helm-style rollout wait until the pod runs.
+A second, forced redeploy (`-d`) measures the warm path (no rebuild, chart re-install).
+"""
+
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import time
+
+from .cluster import LocalCluster
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def devspace_env(cluster, base):
+    home = os.path.join(base, "home")
+    os.makedirs(home, exist_ok=True)
+    kc = cluster.write_kubeconfig(os.path.join(home, ".kube", "config"))
+    env = dict(os.environ)
+    env.update(cluster.env(kc))
+    env.update(HOME=home, DEVSPACE_NONINTERACTIVE="1", PYTHONPATH=ROOT + os.pathsep + env.get("PYTHONPATH", ""))
+    return env
+
+
+def run_devspace(args, cwd, env, timeout=300):
+    t0 = time.perf_counter()
+    p = subprocess.run([os.path.join(ROOT, "bin", "devspace")] + list(args), cwd=cwd, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    dt = time.perf_counter() - t0
+    if p.returncode != 0:
+        raise RuntimeError(f"devspace {' '.join(args)} failed ({p.returncode}):\n{p.stdout}\n{p.stderr}")
+    return dt, p.stdout
+
+
+def bench_deploy(workdir, example="quickstart"):
+    base = os.path.join(workdir, "deploy-bench")
+    os.makedirs(base, exist_ok=True)
+    proj = os.path.join(base, example)
+    shutil.copytree(os.path.join(ROOT, "examples", example), proj, symlinks=True)
+    cluster = LocalCluster(os.path.join(base, "cluster"), gpus=0).start()
+    try:
+        env = devspace_env(cluster, base)
+        cold, out = run_devspace(["deploy"], proj, env)
+        if "Successfully deployed!" not in out:
+            raise RuntimeError(out)
+        warm, _ = run_devspace(["deploy", "-d"], proj, env)
+        run_devspace(["purge"], proj, env)
+        return {"cold_s": cold, "warm_s": warm}
+    finally:
+        cluster.stop()
