@@ -1,0 +1,227 @@
+// Go-template engine, Helm chart rendering (the embedded component chart), generator language
+// detection and config mutations (configure/*).
+#include <algorithm>
+
+#include "config/config.h"
+#include "configure/configure.h"
+#include "core/fs.h"
+#include "core/strutil.h"
+#include "deploy/gotemplate.h"
+#include "deploy/helm.h"
+#include "deploy/helmrepo.h"
+#include "generator/generator.h"
+#include "testing.h"
+
+using namespace ds;
+
+static std::string render_tmpl(const std::string& src, const Value& data) {
+  tmpl::Engine e;
+  e.add("t", src);
+  return e.execute("t", data);
+}
+
+TEST(gotemplate_basics) {
+  Value d = yaml_parse("name: app\nitems: [a, b]\nm: {x: 1, z: 2}\nflag: false\nn: 3\n");
+  EXPECT_EQ(render_tmpl("{{ .name | upper }}", d), std::string("APP"));
+  EXPECT_EQ(render_tmpl("{{ range $i, $v := .items }}{{ $i }}={{ $v }};{{ end }}", d), std::string("0=a;1=b;"));
+  EXPECT_EQ(render_tmpl("{{ range $k, $v := .m }}{{ $k }}{{ $v }}{{ end }}", d), std::string("x1z2"));
+  EXPECT_EQ(render_tmpl("{{ if .flag }}yes{{ else }}no{{ end }}", d), std::string("no"));
+  EXPECT_EQ(render_tmpl("{{ default \"z\" .missing }}", d), std::string("z"));
+  EXPECT_EQ(render_tmpl("{{- $x := 1 }}{{ $x = add $x .n }}{{ $x }}", d), std::string("4"));
+  EXPECT_EQ(render_tmpl("{{ toYaml .m | nindent 2 }}", d), std::string("\n  x: 1\n  z: 2"));
+  EXPECT_EQ(render_tmpl("{{ printf \"%s-%d\" .name .n }}", d), std::string("app-3"));
+  EXPECT_EQ(render_tmpl("{{ if and .m .m.x }}ok{{ end }}", d), std::string("ok"));
+  EXPECT_EQ(render_tmpl("{{ if and .nothing .nothing.deep }}bad{{ else }}ok{{ end }}", d), std::string("ok"));
+  EXPECT_EQ(render_tmpl("{{ list 1 2 3 | len }}", d), std::string("3"));
+  EXPECT_EQ(render_tmpl("{{ define \"p\" }}[{{ . }}]{{ end }}{{ include \"p\" .name }}", d), std::string("[app]"));
+}
+
+static Value component_values(int gpus, bool with_volume, int max_replicas) {
+  std::string y =
+      "components:\n"
+      "- name: default\n"
+      "  replicas: 1\n"
+      "  containers:\n"
+      "  - image: reg/app:tag\n"
+      "    resources:\n"
+      "      limits:\n"
+      "        cpu: \"2\"\n"
+      "        ephemeralStorage: 1Gi\n"
+      "        gpu: " + std::to_string(gpus) + "\n"
+      "      requests:\n"
+      "        memory: 1Gi\n"
+      "    env:\n"
+      "    - name: A\n"
+      "      value: b\n";
+  if (with_volume)
+    y += "    volumeMounts:\n    - containerPath: /data\n      volume:\n        name: data\n        subPath: /d\n";
+  if (max_replicas) y += "  autoScaling:\n    horizontal:\n      maxReplicas: " + std::to_string(max_replicas) +
+                         "\n      averageCPU: 80\n";
+  y += "  service:\n    name: external\n    ports:\n    - externalPort: 80\n      containerPort: 3000\n";
+  y += with_volume ? "volumes:\n- name: data\n  size: 2Gi\n" : "volumes: []\n";
+  y += "pullSecrets: [devspace-auth-reg]\n";
+  return yaml_parse(y);
+}
+
+static const Value* find_kind(const std::vector<Value>& objs, const std::string& kind) {
+  for (auto& o : objs)
+    if (o.get("kind").as_string() == kind) return &o;
+  return nullptr;
+}
+
+TEST(component_chart_cpu_deployment) {
+  helm::Chart c = helm::load_chart(std::string(DEVSPACE_SOURCE_DIR) + "/templates/_base/chart");
+  helm::RenderOptions o;
+  o.release_name = "devspace-app";
+  o.namespace_ = "ns";
+  auto objs = helm::render(c, component_values(0, false, 0), o);
+  const Value* d = find_kind(objs, "Deployment");
+  EXPECT_TRUE(d != nullptr);
+  EXPECT_TRUE(find_kind(objs, "StatefulSet") == nullptr);
+  EXPECT_TRUE(find_kind(objs, "HorizontalPodAutoscaler") == nullptr);
+  const Value& ct = d->at_path("spec.template.spec.containers")[0];
+  EXPECT_EQ(ct.get("image").as_string(), std::string("reg/app:tag"));
+  EXPECT_TRUE(ct.at_path("resources.limits").find("amd.com/gpu") == nullptr);
+  EXPECT_EQ(ct.at_path("resources.limits.ephemeral-storage").as_string(), std::string("1Gi"));
+  EXPECT_EQ(ct.at_path("resources.requests.memory").as_string(), std::string("1Gi"));
+  EXPECT_EQ(d->at_path("spec.template.metadata.labels.app.kubernetes.io/name").as_string(""), std::string(""));
+  const Value& labels = d->at_path("spec.template.metadata.labels");
+  EXPECT_EQ(labels.get("app.kubernetes.io/name").as_string(), std::string("devspace-app"));
+  EXPECT_EQ(labels.get("app.kubernetes.io/component").as_string(), std::string("default"));
+  EXPECT_EQ(d->at_path("spec.template.spec.imagePullSecrets")[0].get("name").as_string(),
+            std::string("devspace-auth-reg"));
+  const Value* svc = find_kind(objs, "Service");
+  EXPECT_TRUE(svc != nullptr);
+  EXPECT_EQ(svc->at_path("spec.ports")[0].get("targetPort").as_int(), (int64_t)3000);
+  // install order: Service before Deployment
+  auto si = std::find_if(objs.begin(), objs.end(), [](const Value& v) { return v.get("kind").as_string() == "Service"; });
+  auto di = std::find_if(objs.begin(), objs.end(), [](const Value& v) { return v.get("kind").as_string() == "Deployment"; });
+  EXPECT_TRUE(si < di);
+}
+
+TEST(component_chart_gpu_statefulset_hpa) {
+  helm::Chart c = helm::load_chart(std::string(DEVSPACE_SOURCE_DIR) + "/templates/_base/chart");
+  helm::RenderOptions o;
+  o.release_name = "train";
+  auto objs = helm::render(c, component_values(8, true, 4), o);
+  const Value* s = find_kind(objs, "StatefulSet");
+  EXPECT_TRUE(s != nullptr);
+  EXPECT_TRUE(find_kind(objs, "Deployment") == nullptr);
+  EXPECT_EQ(s->at_path("spec.serviceName").as_string(), std::string("external"));
+  const Value& ct = s->at_path("spec.template.spec.containers")[0];
+  EXPECT_EQ(ct.at_path("resources.limits").get("amd.com/gpu").as_int(), (int64_t)8);
+  bool nproc = false, shm = false;
+  for (auto& e : ct.get("env").items())
+    if (e.get("name").as_string() == "DEVSPACE_NPROC") nproc = e.get("value").as_string() == "8";
+  for (auto& m : ct.get("volumeMounts").items())
+    if (m.get("mountPath").as_string() == "/dev/shm") shm = true;
+  EXPECT_TRUE(nproc);
+  EXPECT_TRUE(shm);
+  const Value* pvc = find_kind(objs, "PersistentVolumeClaim");
+  EXPECT_TRUE(pvc != nullptr);
+  EXPECT_EQ(pvc->at_path("spec.resources.requests.storage").as_string(), std::string("2Gi"));
+  const Value* hpa = find_kind(objs, "HorizontalPodAutoscaler");
+  EXPECT_TRUE(hpa != nullptr);
+  EXPECT_EQ(hpa->at_path("spec.maxReplicas").as_int(), (int64_t)4);
+}
+
+TEST(generator_detects_languages) {
+  std::string d = fs::make_temp_dir("gen-");
+  generator::ChartGenerator g(d);
+  auto langs = g.supported_languages();
+  EXPECT_TRUE(std::find(langs.begin(), langs.end(), "rocm-pytorch") != langs.end());
+  EXPECT_TRUE(std::find(langs.begin(), langs.end(), "javascript") != langs.end());
+  EXPECT_EQ(g.detect_language(), std::string(""));
+  fs::write_file(fs::join(d, "index.js"), std::string(300, 'x'));
+  fs::write_file(fs::join(d, "node_modules/dep/big.py"), std::string(5000, 'x'));  // vendored: ignored
+  EXPECT_EQ(g.detect_language(), std::string("javascript"));
+  fs::write_file(fs::join(d, "tool.py"), "print(1)\n" + std::string(500, '#'));
+  EXPECT_EQ(g.detect_language(), std::string("python"));
+  fs::write_file(fs::join(d, "train.py"), "import torch\n");
+  EXPECT_EQ(g.detect_language(), std::string("rocm-pytorch"));
+  g.create_chart("rocm-pytorch", false);
+  EXPECT_TRUE(fs::exists(fs::join(d, "chart/Chart.yaml")));
+  EXPECT_TRUE(fs::exists(fs::join(d, "chart/templates/deployments.yaml")));
+  EXPECT_TRUE(contains(fs::read_file(fs::join(d, "Dockerfile")), "rocm/pytorch"));
+  EXPECT_TRUE(contains(fs::read_file(fs::join(d, "devspace_runner.py")), "Hot-reload runner"));
+  // no overwrite of user files
+  EXPECT_TRUE(contains(fs::read_file(fs::join(d, "train.py")), "import torch"));
+  fs::remove_all(d);
+}
+
+TEST(configure_mutations) {
+  std::string d = fs::make_temp_dir("cfg-");
+  std::string old = fs::cwd();
+  fs::chdir(d);
+  fs::write_file(".devspace/config.yaml",
+                 "version: v1alpha2\ndeployments:\n- name: app\n  helm:\n    chartPath: ./chart\n"
+                 "dev:\n  selectors:\n  - name: default\n    labelSelector:\n      app: web\n");
+  {
+    config::Context ctx;
+    configure::add_port(ctx, "", "", "", "8080,9000:90");
+  }
+  {
+    config::Context ctx;
+    const Value& p = ctx.base().at_path("dev.ports");
+    EXPECT_EQ(p.size(), (size_t)1);
+    EXPECT_EQ(p[0].get("labelSelector").get("app").as_string(), std::string("web"));
+    EXPECT_EQ(p[0].get("portMappings")[1].get("remotePort").as_int(), (int64_t)90);
+    configure::add_port(ctx, "", "app=web", "", "7000");  // same selector: appended
+  }
+  {
+    config::Context ctx;
+    EXPECT_EQ(ctx.base().at_path("dev.ports")[0].get("portMappings").size(), (size_t)3);
+    configure::remove_port(ctx, false, "", "8080,90");
+  }
+  {
+    config::Context ctx;
+    auto& pm = ctx.base().at_path("dev.ports")[0].get("portMappings");
+    EXPECT_EQ(pm.size(), (size_t)1);
+    EXPECT_EQ(pm[0].get("localPort").as_int(), (int64_t)7000);
+    EXPECT_THROWS(configure::add_sync(ctx, "./", "relative", "", "", "", ""));
+    configure::add_sync(ctx, "./src", "/app/src", "", "", "a/, b", "");
+    configure::add_deployment(ctx, "k", "", "kube/*.yaml, more.yaml", "");
+    EXPECT_THROWS(configure::add_deployment(ctx, "k", "", "x.yaml", ""));
+    EXPECT_THROWS(configure::add_deployment(ctx, "z", "", "x.yaml", "./c"));
+  }
+  {
+    config::Context ctx;
+    const Value& s = ctx.base().at_path("dev.sync")[0];
+    EXPECT_EQ(s.get("excludePaths")[1].as_string(), std::string("b"));
+    EXPECT_EQ(s.get("labelSelector").get("app").as_string(), std::string("web"));
+    EXPECT_EQ(ctx.base().get("deployments")[1].at_path("kubectl.manifests")[1].as_string(), std::string("more.yaml"));
+    configure::remove_deployment(ctx, false, "k");
+    configure::remove_sync(ctx, false, "", "/app/src", "");
+  }
+  {
+    config::Context ctx;
+    EXPECT_EQ(ctx.base().get("deployments").size(), (size_t)1);
+    EXPECT_EQ(ctx.base().at_path("dev.sync").size(), (size_t)0);
+  }
+  EXPECT_THROWS(configure::parse_selectors("a=b,c"));
+  EXPECT_THROWS(configure::parse_port_mappings("1:2:3"));
+  fs::chdir(old);
+  fs::remove_all(d);
+}
+
+TEST(helmrepo_versions_and_search) {
+  EXPECT_EQ(helmrepo::compare_versions("1.10.0", "1.9.3"), 1);
+  EXPECT_EQ(helmrepo::compare_versions("v2.0", "2.0.0"), 0);
+  EXPECT_EQ(helmrepo::compare_versions("0.1.0", "0.1.1"), -1);
+  std::string home = fs::make_temp_dir("helmhome-");
+  setenv("DEVSPACE_HELM_HOME", home.c_str(), 1);
+  std::string repo = fs::make_temp_dir("repo-");
+  fs::write_file(fs::join(repo, "index.yaml"),
+                 "apiVersion: v1\nentries:\n  mysql:\n  - name: mysql\n    version: 0.9.0\n    appVersion: 5.7.1\n"
+                 "    urls: [mysql-0.9.0.tgz]\n  - name: mysql\n    version: 0.10.2\n    appVersion: 5.7.14\n"
+                 "    urls: [mysql-0.10.2.tgz]\n");
+  helmrepo::add_repo({"local", "file://" + repo});
+  helmrepo::update();
+  auto v = helmrepo::search("mysql");
+  EXPECT_EQ(v.version, std::string("0.10.2"));
+  EXPECT_EQ(helmrepo::search("mysql", "", "5.7.1").version, std::string("0.9.0"));
+  EXPECT_THROWS(helmrepo::search("nope"));
+  unsetenv("DEVSPACE_HELM_HOME");
+  fs::remove_all(home);
+  fs::remove_all(repo);
+}
