@@ -233,7 +233,7 @@ class ApiServer:
         if kind == "attach":
             await self._attach(ws, c)
             return ws
-        cmd = request.query.getall("command", [])
+        cmd = self.kubelet.map_argv(c, request.query.getall("command", []))
         env = self.kubelet._env(rt, c)
         cwd = self.kubelet.workdir(c)
         os.makedirs(cwd, exist_ok=True)

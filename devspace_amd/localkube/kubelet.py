@@ -15,6 +15,7 @@ import json
 import os
 import shutil
 import signal
+import sys
 import time
 
 from .store import ApiError, now_rfc3339
@@ -27,6 +28,13 @@ GPU_RESOURCE = "amd.com/gpu"
 # python/node/rocm stack instead of pulling layers).
 HOST_IMAGES = ("rocm/pytorch", "rocm/dev", "python", "node", "ubuntu", "debian", "busybox", "alpine",
                "devspace-local/runtime", "gcr.io/kaniko-project/executor")
+
+# Binaries of tool images that exist on the host under another name / as an emulation.
+RUNTIME_ALIASES = {
+    "/busybox/sleep": ("sleep",),
+    "/busybox/sh": ("sh",),
+    "/kaniko/executor": (sys.executable, "-m", "devspace_amd.localkube.kaniko"),
+}
 
 
 def _gpu_request(container):
@@ -308,10 +316,18 @@ class Kubelet:
             argv = list(cfg.get("Entrypoint") or []) + list(args)
         else:
             argv = list(cfg.get("Entrypoint") or []) + list(cfg.get("Cmd") or [])
+        return self.map_argv(c, argv)
+
+    def map_argv(self, c, argv):
+        """Container paths -> host paths under the container root, plus runtime aliases for the
+        well-known tool images (busybox shell utils, the kaniko executor)."""
+        argv = [str(a) for a in argv]
+        if argv and argv[0] in RUNTIME_ALIASES:
+            argv = list(RUNTIME_ALIASES[argv[0]]) + argv[1:]
         out = []
         for a in argv:
             a = str(a)
-            if a.startswith("/") and len(a) > 1:
+            if a.startswith("/") and len(a) > 1 and not a.startswith(c.root + "/") and a != sys.executable:
                 first = a.lstrip("/").split("/", 1)[0]
                 if first and os.path.exists(os.path.join(c.root, first)):
                     a = os.path.join(c.root, a.lstrip("/"))
@@ -330,6 +346,7 @@ class Kubelet:
                 env[e["name"]] = str(e["value"])
         env["HOSTNAME"] = rt.name
         env["DEVSPACE_CONTAINER_ROOT"] = c.root
+        env["DEVSPACE_LOCAL_IMAGES"] = self.images.root  # used by the kaniko emulation
         env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, rt.gpus)) if rt.gpus else env.get("HIP_VISIBLE_DEVICES", "")
         if not rt.gpus:
             env["HIP_VISIBLE_DEVICES"] = "-1" if self.gpus_total else env["HIP_VISIBLE_DEVICES"]

@@ -415,7 +415,8 @@ std::unique_ptr<cli::Command> make_list() {
         if (chart.empty()) continue;
         std::string req = fs::join(chart, "requirements.yaml");
         if (!fs::exists(req)) continue;
-        for (auto& dep : yaml_load_file(req).get("dependencies").items())
+        Value reqs = yaml_load_file(req);
+        for (auto& dep : reqs.get("dependencies").items())
           rows.push_back({dep.get("name").as_string(), dep.get("version").as_string(),
                           dep.get("repository").as_string()});
       }

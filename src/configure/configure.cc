@@ -467,7 +467,7 @@ void add_package(config::Context& ctx, const std::string& name, const std::strin
   Value values = fs::exists(values_path) ? yaml_load_file(values_path) : Value::map();
   if (!values.is_map() || !values.has(cv.name)) {
     std::string defaults = package_default_values(cv.name);
-    fs::append_file(values_path, std::string(kPackageComment) + cv.name + ":" + (defaults.empty() ? "{}" : defaults) + "\n");
+    fs::append_file(values_path, std::string(kPackageComment) + cv.name + ":" + (defaults.empty() ? " {}" : defaults) + "\n");
   }
   Value& cfg = ctx.base();
   if (!selector_named(cfg, cv.name)) {
@@ -481,7 +481,33 @@ void add_package(config::Context& ctx, const std::string& name, const std::strin
   save(ctx);
   log::done("Successfully added package " + cv.name + ", you can now modify the configuration in '" + chart +
             "/values.yaml'");
-  (void)skip_question;
+  if (!skip_question) {
+    prompt::Params q;
+    q.question = "Do you want to open the package README to see configuration options?";
+    q.default_value = "yes";
+    q.options = {"yes", "no"};
+    if (prompt::ask(q) == "yes") {
+      // package.go:506 showReadme: <chart>/charts/<name>-<version>.tgz -> <name>/README.md
+      std::string tgz = fs::join(chart, "charts", cv.name + "-" + cv.version + ".tgz");
+      std::string readme = extract_from_tgz(tgz, cv.name + "/README.md");
+      if (readme.empty())
+        log::warn("The package has no README.md");
+      else
+        log::get().write("\n" + readme + "\n");
+    }
+  }
+}
+
+std::string extract_from_tgz(const std::string& tgz_path, const std::string& member) {
+  std::string data;
+  if (!fs::read_file(tgz_path, &data)) return "";
+  GzipReader gz(string_source(&data));
+  TarReader tr([&](char* b, size_t n) { return gz.read(b, n); });
+  TarEntry te;
+  while (tr.next(&te)) {
+    if (fs::clean(te.name) == fs::clean(member)) return tr.read_all();
+  }
+  return "";
 }
 
 void remove_package(config::Context& ctx, bool all, const std::string& deployment, const std::string& name) {

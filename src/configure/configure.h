@@ -51,6 +51,9 @@ void remove_package(config::Context& ctx, bool all, const std::string& deploymen
 std::string package_default_values(const std::string& name);
 Value package_default_selector(const std::string& name, const std::string& deployment);
 
+// One member of a .tgz as a string ("" if absent) — util/tar/tar.go:64.
+std::string extract_from_tgz(const std::string& tgz_path, const std::string& member);
+
 // Image name + pull secret configuration during init (init_image.go:18).
 void init_image(config::Context& ctx, const std::string& docker_username, bool is_cloud);
 

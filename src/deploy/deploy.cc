@@ -9,6 +9,7 @@
 #include "core/match.h"
 #include "core/proc.h"
 #include "core/strutil.h"
+#include "core/trace.h"
 #include "deploy/helm.h"
 
 namespace ds {
@@ -283,6 +284,7 @@ void deploy_all(const Value& cfg, config::Generated& gen, std::shared_ptr<kube::
     else
       log::info("Deploying " + name + " with helm");
     auto dep = make_deployer(cfg, d, kube);
+    trace::Span span("deploy", {{"deployment", name}, {"engine", d.get("kubectl").is_map() ? "kubectl" : "helm"}});
     try {
       dep->deploy(gen, is_dev, force);
     } catch (const std::exception& e) {

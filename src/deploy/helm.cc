@@ -10,6 +10,7 @@
 #include "core/fs.h"
 #include "core/log.h"
 #include "core/strutil.h"
+#include "core/trace.h"
 #include "deploy/gotemplate.h"
 
 namespace ds {
@@ -345,7 +346,10 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
         if (!keep.count(object_key(d))) k_->delete_object(d, ns);
       }
     }
-    if (wait) err = wait_ready(objs, ns, timeout_s > 0 ? timeout_s : 40);
+    if (wait) {
+      trace::Span wspan("deploy.helm_wait", {{"release", name}});
+      err = wait_ready(objs, ns, timeout_s > 0 ? timeout_s : 40);
+    }
     // install.go:181 analyzeError: a wait timeout is explained by an analyze report of the
     // namespace; no problems found means the release is fine (just slow).
     if (contains(err, "timed out waiting")) {

@@ -10,6 +10,7 @@
 #include <cstring>
 
 #include "core/strutil.h"
+#include "core/trace.h"
 
 namespace ds {
 namespace sync {
@@ -560,6 +561,7 @@ void Session::upstream_loop() {
 }
 
 void Session::apply_upstream(std::vector<FileInfo>& changes, long first_event_us) {
+  trace::Span span("sync.upstream_batch", {{"changes", std::to_string(changes.size())}, {"dest", o_.dest_path}});
   std::vector<FileInfo> creates, removes;
   for (auto& c : changes) (c.mtime > 0 ? creates : removes).push_back(c);
   if (!removes.empty()) apply_removes(removes);
@@ -917,6 +919,7 @@ std::map<std::string, FileInfo> Session::clone_index() {
 }
 
 void Session::initial_sync() {
+  trace::Span span("sync.initial", {{"dest", o_.dest_path}});
   // populate the index from the remote tree (downstream.go:84)
   auto creates = collect_changes(nullptr);
   {
@@ -1245,6 +1248,8 @@ void Session::create_folders(const std::vector<FileInfo>& dirs) {
 }
 
 void Session::apply_downstream(const std::vector<FileInfo>& creates, std::map<std::string, FileInfo>& removes) {
+  trace::Span span("sync.downstream_batch",
+                   {{"changes", std::to_string(creates.size() + removes.size())}, {"dest", o_.dest_path}});
   std::vector<FileInfo> files, dirs;
   for (auto& c : creates) (c.is_dir ? dirs : files).push_back(c);
   std::string archive;

@@ -41,6 +41,12 @@ def test_quickstart_deploy_logs_enter_analyze_purge(localkube):
     proj = lk.project("quickstart")
     out = lk.run(["deploy"], proj).stdout
     assert "Successfully deployed!" in out
+    import json
+
+    spans = [json.loads(l) for l in open(os.path.join(proj, ".devspace", "logs", "trace.jsonl"))]
+    names = {s["span"] for s in spans}
+    assert {"image.build", "image.push", "deploy", "deploy.helm_wait"} <= names, names
+    assert all(s["dur_us"] >= 0 for s in spans)
     pods = wait_for(lambda: running(lk.pods("quickstart")), what="quickstart pod")
     assert pods[0]["spec"]["containers"][0]["image"].startswith("devspace-local/quickstart:")
 
@@ -243,3 +249,92 @@ def test_multi_deployment_example(localkube, example):
     php = wait_for(lambda: lk.pods("microservices", "release=devspace-php"), what="php pod")
     assert php[0]["spec"]["containers"][0]["image"].startswith("devspace-local/ms-php")
     lk.run(["purge"], proj)
+
+
+def test_kaniko_in_cluster_build(localkube):
+    lk = localkube
+    proj = lk.project("kaniko")
+    env_backup = lk.env.pop("DOCKER_HOST")
+    try:
+        out = lk.run(["deploy"], proj, timeout=180).stdout
+    finally:
+        lk.env["DOCKER_HOST"] = env_backup
+    assert "with engine 'kaniko'" in out
+    assert "Done building image" in out, out
+    pods = wait_for(lambda: running(lk.pods("kaniko", "app.kubernetes.io/component=default")), what="app pod")
+    assert pods[0]["spec"]["containers"][0]["image"].startswith("devspace-local/kaniko-app:")
+    # the build pod is deleted after the build
+    wait_for(lambda: not lk.pods("kaniko", "devspace-build-id"), what="build pod cleanup")
+    lk.run(["purge"], proj)
+
+
+def _make_chart_repo(base):
+    """file:// helm repository with one chart (cache-0.3.1: a Deployment + Service)."""
+    import io
+    import tarfile
+
+    repo = os.path.join(base, "chart-repo")
+    os.makedirs(repo, exist_ok=True)
+    files = {
+        "cache/Chart.yaml": "apiVersion: v1\nname: cache\nversion: 0.3.1\nappVersion: 7.2.0\n",
+        "cache/values.yaml": "image: devspace-local/cache-server\nport: 6379\n",
+        "cache/README.md": "# cache\nSet `cache.port` to change the port.\n",
+        "cache/templates/deployment.yaml": (
+            "apiVersion: apps/v1\nkind: Deployment\nmetadata:\n  name: {{ .Release.Name }}-cache\n"
+            "spec:\n  replicas: 1\n  selector:\n    matchLabels: {app: {{ .Release.Name }}-cache}\n"
+            "  template:\n    metadata:\n      labels: {app: {{ .Release.Name }}-cache}\n    spec:\n"
+            "      containers:\n      - name: cache\n        image: {{ .Values.image }}\n"
+            "        args: [\"--port\", \"{{ .Values.port }}\"]\n"),
+    }
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w:gz") as tf:
+        for name, data in files.items():
+            ti = tarfile.TarInfo(name)
+            ti.size = len(data.encode())
+            tf.addfile(ti, io.BytesIO(data.encode()))
+    with open(os.path.join(repo, "cache-0.3.1.tgz"), "wb") as f:
+        f.write(buf.getvalue())
+    with open(os.path.join(repo, "index.yaml"), "w") as f:
+        f.write("apiVersion: v1\nentries:\n  cache:\n  - name: cache\n    version: 0.3.1\n    appVersion: 7.2.0\n"
+                "    description: in-memory cache\n    urls: [cache-0.3.1.tgz]\n")
+    return repo
+
+
+def test_add_list_remove_package_from_chart_repo(localkube):
+    lk = localkube
+    proj = lk.project("quickstart", "quickstart-pkg")
+    repo = _make_chart_repo(lk.base)
+    helm_home = os.path.join(lk.base, "helm-home")
+    os.makedirs(helm_home, exist_ok=True)
+    with open(os.path.join(helm_home, "repositories.yaml"), "w") as f:
+        f.write(f"apiVersion: v1\nrepositories:\n- name: local\n  url: file://{repo}\n")
+    lk.env["DEVSPACE_HELM_HOME"] = helm_home
+    try:
+        listing = lk.run(["add", "package"], proj).stdout
+        assert "cache" in listing and "0.3.1" in listing
+        out = lk.run(["add", "package", "cache"], proj, input="yes\n").stdout
+        assert "Successfully added package cache" in out
+        assert "Set `cache.port`" in out  # README shown
+        chart = os.path.join(proj, "chart")
+        assert os.path.exists(os.path.join(chart, "charts", "cache-0.3.1.tgz"))
+        assert "name: cache" in open(os.path.join(chart, "requirements.yaml")).read()
+        assert "\ncache:" in open(os.path.join(chart, "values.yaml")).read()
+        assert "name: cache" in open(os.path.join(proj, ".devspace", "config.yaml")).read()
+        assert "cache" in lk.run(["list", "packages"], proj).stdout
+        p = lk.run(["add", "package", "cache", "--skip-question"], proj, check=False)
+        assert p.returncode != 0 and "already added" in p.stdout + p.stderr
+
+        cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+        cfg = open(cfg_path).read().replace("chartPath: ./chart", "chartPath: ./chart\n    wait: false")
+        open(cfg_path, "w").write(cfg)
+        lk.run(["deploy"], proj)
+        dep = lk.cluster.store.try_get("apps", "deployments", "quickstart", "devspace-app-cache")
+        assert dep is not None
+        assert dep["spec"]["template"]["spec"]["containers"][0]["args"] == ["--port", "6379"]
+
+        lk.run(["remove", "package", "cache"], proj)
+        assert not os.path.exists(os.path.join(chart, "charts", "cache-0.3.1.tgz"))
+        assert "cache" not in open(os.path.join(chart, "requirements.yaml")).read()
+        lk.run(["purge"], proj)
+    finally:
+        lk.env.pop("DEVSPACE_HELM_HOME", None)
