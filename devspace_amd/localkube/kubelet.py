@@ -29,6 +29,12 @@ GPU_RESOURCE = "amd.com/gpu"
 HOST_IMAGES = ("rocm/pytorch", "rocm/dev", "python", "node", "ubuntu", "debian", "busybox", "alpine",
                "devspace-local/runtime", "gcr.io/kaniko-project/executor")
 
+HOST_ONLY_ENV = {"RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                 "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT", "KUBECONFIG",
+                 "DOCKER_HOST", "DOCKER_CERT_PATH", "DOCKER_TLS_VERIFY", "HIP_VISIBLE_DEVICES",
+                 "CUDA_VISIBLE_DEVICES", "DEVSPACE_NONINTERACTIVE"}
+HOST_ONLY_ENV_PREFIXES = ("TORCHELASTIC_", "TORCH_ELASTIC_", "PET_")
+
 # Binaries of tool images that exist on the host under another name / as an emulation.
 RUNTIME_ALIASES = {
     "/busybox/sleep": ("sleep",),
@@ -335,7 +341,10 @@ class Kubelet:
         return out
 
     def _env(self, rt, c):
-        env = dict(os.environ)
+        # Containers do not inherit the launcher's process-group / client configuration (a pod
+        # started from a torchrun'd process must not join that rendezvous).
+        env = {k: v for k, v in os.environ.items()
+               if k not in HOST_ONLY_ENV and not k.startswith(HOST_ONLY_ENV_PREFIXES)}
         env.update(self.extra_env)
         for kv in c.image_config.get("Env") or []:
             if "=" in kv:
@@ -347,11 +356,15 @@ class Kubelet:
         env["HOSTNAME"] = rt.name
         env["DEVSPACE_CONTAINER_ROOT"] = c.root
         env["DEVSPACE_LOCAL_IMAGES"] = self.images.root  # used by the kaniko emulation
-        env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, rt.gpus)) if rt.gpus else env.get("HIP_VISIBLE_DEVICES", "")
-        if not rt.gpus:
-            env["HIP_VISIBLE_DEVICES"] = "-1" if self.gpus_total else env["HIP_VISIBLE_DEVICES"]
-        if not env["HIP_VISIBLE_DEVICES"]:
-            env.pop("HIP_VISIBLE_DEVICES")
+        # Node GPU index i is the i-th device this node process may use (the device plugin's
+        # view): map through the host's own HIP_VISIBLE_DEVICES when it restricts devices.
+        host_vis = [v.strip() for v in os.environ.get("HIP_VISIBLE_DEVICES", "").split(",") if v.strip()]
+        if rt.gpus:
+            env["HIP_VISIBLE_DEVICES"] = ",".join(host_vis[g] if g < len(host_vis) else str(g) for g in rt.gpus)
+        elif self.gpus_total:
+            env["HIP_VISIBLE_DEVICES"] = "-1"  # no amd.com/gpu request: no GPU access
+        elif host_vis:
+            env["HIP_VISIBLE_DEVICES"] = ",".join(host_vis)
         return env
 
     def workdir(self, c):

@@ -26,6 +26,20 @@ def test_bench_cpu_tiny():
     assert d["reference_equivalent_p50_ms"] > d["value"]
 
 
+def test_bench_torchrun_two_ranks_cpu():
+    """The driver's N>1 launch shape (torchrun, one rank per GPU) on CPU with gloo: rank 0
+    drives the dev loop, rank 1 joins the timing barriers; exactly one JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29655", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--tiny", "--ref-steps", "0", "--no-deploy-bench"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["steps"] == 2 and d["value"] > 0
+
+
 @pytest.mark.gpu
 def test_bench_gpu_short():
     d = _run(["--steps", "3", "--warmup", "1", "--ref-steps", "1"], 900)
