@@ -157,6 +157,12 @@ void replace_placeholders(Value& cfg, InitState& st) {
   data = replace_all(data, "#port#", st.port);
   data = replace_all(data, "#gpus#", st.gpus);
   fs::write_file("chart/values.yaml", data);
+  // ROCm base image pin (the box may have no network: pick a tag that is pre-pulled)
+  std::string df;
+  if (fs::read_file("Dockerfile", &df) && contains(df, "#rocm-image#")) {
+    const char* img = getenv("DEVSPACE_ROCM_IMAGE");
+    fs::write_file("Dockerfile", replace_all(df, "#rocm-image#", img && *img ? img : "rocm/pytorch:latest"));
+  }
 }
 
 int run_init(cli::Command& c, const std::vector<std::string>&) {
@@ -217,9 +223,10 @@ int run_init(cli::Command& c, const std::vector<std::string>&) {
     st.language = prompt::ask(p);
     if (st.language == "rocm-pytorch") {
       prompt::Params g;
-      g.question = "How many AMD Instinct GPUs (amd.com/gpu) should the container request? (Default: 1)";
+      // HBM (288 GB per MI355X) is not a schedulable resource: GPUs are requested whole.
+      g.question = "How many MI355X GPUs (amd.com/gpu, 1-8) should the container request? (Default: 1)";
       g.default_value = "1";
-      g.validation_regex = "[0-9]+";
+      g.validation_regex = "[1-8]";
       st.gpus = prompt::ask(g);
     }
   }

@@ -188,6 +188,7 @@ class KubectlDeployer : public Deployer {
     log::start_wait("Loading manifests");
     auto docs = kubectl_manifests(d_, gen, is_dev);
     log::stop_wait();
+    k_->check_gpu_requests(docs);
     std::string ns = deployment_ns(cfg_, d_);
     std::string cmd = d_.at_path("kubectl.cmdPath").as_string();
     if (!cmd.empty()) {

@@ -314,6 +314,7 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
   std::stable_sort(objs.begin(), objs.end(), [](const Value& a, const Value& b) {
     return kind_order(a.get("kind").as_string()) < kind_order(b.get("kind").as_string());
   });
+  k_->check_gpu_requests(objs);
   for (auto& o : objs) {
     o["metadata"]["labels"]["app.kubernetes.io/managed-by"] = o.at_path("metadata.labels").get("app.kubernetes.io/managed-by").is_null()
                                                                   ? Value("Helm")

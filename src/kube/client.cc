@@ -302,6 +302,55 @@ void Client::ensure_namespace(const std::string& ns) {
   }
 }
 
+static int64_t pod_gpu_request(const Value& pod_spec) {
+  int64_t n = 0;
+  for (auto& c : pod_spec.get("containers").items()) {
+    const Value* lim = c.at_path("resources.limits").find("amd.com/gpu");
+    const Value* req = c.at_path("resources.requests").find("amd.com/gpu");
+    const Value* v = lim ? lim : req;
+    int64_t x = 0;
+    if (v && (v->is_int() || parse_int64(v->as_string(), &x))) n += v->is_int() ? v->as_int() : x;
+  }
+  return n;
+}
+
+std::string Client::check_gpu_requests(const std::vector<Value>& objs) {
+  int64_t want = 0;
+  std::string who;
+  for (auto& o : objs) {
+    const Value& spec = o.get("kind").as_string() == "Pod" ? o.get("spec") : o.at_path("spec.template.spec");
+    if (!spec.is_map()) continue;
+    int64_t n = pod_gpu_request(spec);
+    if (n > want) {
+      want = n;
+      who = o.get("kind").as_string() + " " + o.at_path("metadata.name").as_string();
+    }
+  }
+  if (want == 0) return "";
+  int64_t best = 0;
+  try {
+    Value nodes = get("/api/v1/nodes");
+    for (auto& n : nodes.get("items").items()) {
+      int64_t a = 0;
+      const Value& v = n.at_path("status.allocatable").get("amd.com/gpu");
+      if (v.is_int()) a = v.as_int();
+      else parse_int64(v.as_string(), &a);
+      best = std::max(best, a);
+    }
+  } catch (const std::exception&) {
+    return "";  // no permission to list nodes: nothing to say
+  }
+  std::string msg;
+  if (best == 0)
+    msg = who + " requests " + std::to_string(want) +
+          " amd.com/gpu but no node advertises amd.com/gpu (is the AMD GPU device plugin running?)";
+  else if (want > best)
+    msg = who + " requests " + std::to_string(want) + " amd.com/gpu but the largest node offers " +
+          std::to_string(best) + " — the pod cannot be scheduled";
+  if (!msg.empty()) log::warn(msg);
+  return msg;
+}
+
 void Client::ensure_gcloud_cluster_role_binding() {
   // kubectl/util.go:47 — GKE users need cluster-admin to create RBAC for the dev pods.
   if (!starts_with(cfg_.context, "gke_") || which("gcloud").empty()) return;

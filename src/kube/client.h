@@ -85,6 +85,10 @@ class Client {
   // Namespaces / RBAC helpers (kubectl/util.go)
   void ensure_namespace(const std::string& ns);
   void ensure_gcloud_cluster_role_binding();
+  // Largest per-pod amd.com/gpu request among workload manifests vs. the largest node
+  // allocatable (AMD device plugin); warns before deploying something unschedulable.
+  // Returns the warning text ("" when fine).
+  std::string check_gpu_requests(const std::vector<Value>& objs);
 
   // Apply a manifest (create or replace; services keep their clusterIP; immutable-field
   // conflicts fall back to delete + create, i.e. `kubectl apply --force`).

@@ -117,6 +117,10 @@ TEST(component_chart_gpu_statefulset_hpa) {
     if (m.get("mountPath").as_string() == "/dev/shm") shm = true;
   EXPECT_TRUE(nproc);
   EXPECT_TRUE(shm);
+  std::string shm_size;
+  for (auto& v : s->at_path("spec.template.spec.volumes").items())
+    if (v.get("name").as_string() == "dshm") shm_size = v.at_path("emptyDir.sizeLimit").as_string();
+  EXPECT_EQ(shm_size, std::string("128Gi"));
   const Value* pvc = find_kind(objs, "PersistentVolumeClaim");
   EXPECT_TRUE(pvc != nullptr);
   EXPECT_EQ(pvc->at_path("spec.resources.requests.storage").as_string(), std::string("2Gi"));

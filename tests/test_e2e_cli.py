@@ -176,6 +176,7 @@ def test_init_detects_rocm_pytorch_and_requests_gpus(localkube):
     p = lk.run(["deploy"], proj, check=False, timeout=120)
     assert p.returncode != 0
     assert "amd.com/gpu" in p.stdout + p.stderr, p.stdout + p.stderr
+    assert "no node advertises amd.com/gpu" in p.stdout + p.stderr  # pre-deploy capacity check
     # without waiting the release stays and the pending pod can be inspected
     open(cfg_path, "w").write(cfg.replace("timeout: 3", "wait: false"))
     lk.run(["deploy", "-d"], proj, timeout=120)
