@@ -115,16 +115,7 @@ int run_upgrade(cli::Command& c, const Args&) {
 int run_login(cli::Command& c, const Args&) {
   std::string name = c.get_str("provider");
   try {
-    auto ps = cloud::load_providers();
-    if (!ps.count(name)) throw std::runtime_error("Cloud provider " + name + " not found");
-    if (!c.get_str("token").empty()) {
-      ps[name].token = c.get_str("token");
-      cloud::save_providers(ps);
-    } else {
-      ps[name].token.clear();
-      cloud::save_providers(ps);
-    }
-    cloud::ensure_logged_in(name);
+    cloud::login(name, c.get_str("token"));
   } catch (const std::exception& e) {
     log::fatal(std::string("Error logging in: ") + e.what());
   }

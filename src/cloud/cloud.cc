@@ -263,24 +263,31 @@ Provider ensure_logged_in(const std::string& name) {
                                for (auto& kv : ps) n.push_back(kv.first);
                                return join(n, ", ");
                              }());
-  if (it->second.token.empty()) {
+  if (it->second.token.empty()) return login(name, "");
+  return it->second;
+}
+
+Provider login(const std::string& name, const std::string& token) {
+  auto ps = load_providers();
+  auto it = ps.find(name);
+  if (it == ps.end()) throw std::runtime_error("Cloud provider " + name + " not found");
+  it->second.token = token.empty() ? Client(it->second).login_via_browser() : token;
+  save_providers(ps);
+  // cloud/registry.go:27 LoginIntoRegistries: docker credentials for every provider registry
+  try {
     Client c(it->second);
-    it->second.token = c.login_via_browser();
-    try {
-      Client c2(it->second);
-      for (auto& reg : c2.registries()) {
-        build::DockerConfigFile dcf = build::DockerConfigFile::load();
-        build::AuthConfig a;
-        a.server_address = reg;
-        a.username = token_account(it->second.token);
-        a.password = it->second.token;
-        dcf.store(a);
-        dcf.save();
-      }
-    } catch (const std::exception& e) {
-      log::warn(std::string("Error logging into docker registries: ") + e.what());
+    build::DockerConfigFile dcf = build::DockerConfigFile::load();
+    for (auto& reg : c.registries()) {
+      build::AuthConfig a;
+      a.server_address = reg;
+      a.username = token_account(it->second.token);
+      a.password = it->second.token;
+      a.auth = base64_encode(a.username + ":" + a.password);
+      dcf.store(a);
     }
-    save_providers(ps);
+    dcf.save();
+  } catch (const std::exception& e) {
+    log::warn(std::string("Error logging into docker registries: ") + e.what());
   }
   return it->second;
 }

@@ -55,6 +55,9 @@ class Client {
 
 // Returns the provider (logging in when no token is stored).
 Provider ensure_logged_in(const std::string& provider_name);
+// (Re)login with a token, or via the browser when empty (cloud.ReLogin), then log docker into
+// the provider's registries.
+Provider login(const std::string& provider_name, const std::string& token);
 // cloud/configure.go:79 — no-op without cluster.cloudProvider.
 void configure(config::Context& ctx, const std::string& space_name = "");
 std::string kube_context_for(const Space& s);
