@@ -38,6 +38,9 @@ class Probe:
         self.lib.gp_mfma_selftest.restype = ctypes.c_double
         self.lib.gp_hbm_copy_gbps.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int]
         self.lib.gp_hbm_copy_gbps.restype = ctypes.c_double
+        self.lib.gp_hbm_copy_gbps_cfg.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_int, ctypes.c_int]
+        self.lib.gp_hbm_copy_gbps_cfg.restype = ctypes.c_double
         self.lib.gp_mfma_bf16_tflops.argtypes = [ctypes.c_int, ctypes.c_int]
         self.lib.gp_mfma_bf16_tflops.restype = ctypes.c_double
         self.lib.gp_last_error.restype = ctypes.c_char_p
@@ -56,6 +59,9 @@ class Probe:
 
     def hbm_gbps(self, dev, nbytes=1 << 30, iters=10):
         return self.lib.gp_hbm_copy_gbps(dev, nbytes, iters)
+
+    def hbm_gbps_cfg(self, dev, unroll, nontemporal, blocks_per_cu, nbytes=1 << 30, iters=10):
+        return self.lib.gp_hbm_copy_gbps_cfg(dev, nbytes, iters, unroll, int(nontemporal), blocks_per_cu)
 
     def mfma_tflops(self, dev, iters=20000):
         return self.lib.gp_mfma_bf16_tflops(dev, iters)
@@ -101,11 +107,30 @@ def run(quick=False):
     return report
 
 
+def sweep_copy(dev=0, nbytes=1 << 30):
+    """Copy-kernel configuration sweep (unroll x nontemporal x blocks/CU) -> list of rows."""
+    probe = Probe()
+    rows = []
+    for unroll in (1, 2, 4, 8):
+        for nt in (False, True):
+            for bpc in (2, 4, 8, 16):
+                gbps = probe.hbm_gbps_cfg(dev, unroll, nt, bpc, nbytes=nbytes)
+                rows.append({"unroll": unroll, "nontemporal": nt, "blocks_per_cu": bpc, "gbps": round(gbps, 1)})
+    return rows
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="devspace_amd.gpucheck")
     ap.add_argument("--quick", action="store_true", help="self-test only, no bandwidth/throughput runs")
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--sweep-copy", action="store_true", help="HBM copy kernel tuning sweep on gpu0")
     args = ap.parse_args(argv)
+    if args.sweep_copy:
+        rows = sweep_copy()
+        for r in sorted(rows, key=lambda r: -r["gbps"]):
+            print(f"unroll={r['unroll']} nt={int(r['nontemporal'])} blocks/CU={r['blocks_per_cu']:>2} "
+                  f"{r['gbps']:8.1f} GB/s ({100.0 * r['gbps'] / HBM_EXPECTED_GBPS:5.1f}% of achievable)")
+        return 0
     rep = run(quick=args.quick)
     if args.json:
         print(json.dumps(rep))

@@ -55,11 +55,41 @@ __global__ void __launch_bounds__(64) mfma_tile_kernel(const float* __restrict__
   }
 }
 
-// Streaming copy: 16-byte vectors, grid-stride.
+// Streaming copy: 16-byte vectors (global_load/store_dwordx4), grid-stride, U independent
+// vectors in flight per lane before the first store (keeps ~U*4 KiB of HBM reads outstanding
+// per wave), nontemporal hints so the one-touch stream does not thrash L2/MALL.
+template <int U, bool NT>
 __global__ void __launch_bounds__(256) copy_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst, size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(&src[i + u * stride]) : src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (NT)
+        __builtin_nontemporal_store(v[u], &dst[i + u * stride]);
+      else
+        dst[i + u * stride] = v[u];
+    }
+  }
   for (; i < n; i += stride) dst[i] = src[i];
+}
+
+using copy_fn = void (*)(const f32x4*, f32x4*, size_t);
+static copy_fn pick_copy(int unroll, int nt) {
+  switch (unroll * 2 + (nt ? 1 : 0)) {
+    case 2: return copy_kernel<1, false>;
+    case 3: return copy_kernel<1, true>;
+    case 4: return copy_kernel<2, false>;
+    case 5: return copy_kernel<2, true>;
+    case 8: return copy_kernel<4, false>;
+    case 9: return copy_kernel<4, true>;
+    case 16: return copy_kernel<8, false>;
+    case 17: return copy_kernel<8, true>;
+    default: return nullptr;
+  }
 }
 
 // Register-resident MFMA chain: 4 independent accumulators per wave hide the MFMA latency.
@@ -138,9 +168,10 @@ double gp_mfma_selftest(int dev) {
   return err;
 }
 
-// HBM copy bandwidth in GB/s (bytes read + written per second).
-double gp_hbm_copy_gbps(int dev, size_t bytes, int iters) {
-  if (hipSetDevice(dev) != hipSuccess) return -1;
+// HBM copy bandwidth in GB/s for one kernel configuration (used by the tuning sweep).
+double gp_hbm_copy_gbps_cfg(int dev, size_t bytes, int iters, int unroll, int nontemporal, int blocks_per_cu) {
+  copy_fn fn = pick_copy(unroll, nontemporal);
+  if (!fn || blocks_per_cu < 1 || hipSetDevice(dev) != hipSuccess) return -1;
   size_t n = bytes / sizeof(f32x4);
   f32x4 *src = nullptr, *dst = nullptr;
   if (hipMalloc(&src, n * sizeof(f32x4)) != hipSuccess) return -1;
@@ -151,14 +182,13 @@ double gp_hbm_copy_gbps(int dev, size_t bytes, int iters) {
   hipMemset(src, 1, n * sizeof(f32x4));
   hipDeviceProp_t p;
   hipGetDeviceProperties(&p, dev);
-  // >>256 workgroups: 16 resident blocks of 256 threads per CU
-  dim3 grid(p.multiProcessorCount * 16), block(256);
-  hipLaunchKernelGGL(copy_kernel, grid, block, 0, 0, src, dst, n);  // warm-up
+  dim3 grid(p.multiProcessorCount * blocks_per_cu), block(256);
+  hipLaunchKernelGGL(fn, grid, block, 0, 0, src, dst, n);  // warm-up
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   hipEventRecord(e0);
-  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(copy_kernel, grid, block, 0, 0, src, dst, n);
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(fn, grid, block, 0, 0, src, dst, n);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0;
@@ -169,6 +199,11 @@ double gp_hbm_copy_gbps(int dev, size_t bytes, int iters) {
   hipFree(dst);
   if (ms <= 0) return -1;
   return (2.0 * (double)n * sizeof(f32x4) * iters) / (ms * 1e-3) / 1e9;
+}
+
+// HBM copy bandwidth in GB/s (bytes read + written per second), default configuration.
+double gp_hbm_copy_gbps(int dev, size_t bytes, int iters) {
+  return gp_hbm_copy_gbps_cfg(dev, bytes, iters, 4, 1, 8);
 }
 
 // Dense bf16 MFMA rate in TFLOP/s.

@@ -1,0 +1,166 @@
+"""Dev services end to end: port-forwarding, interactive terminal (PTY), logs --follow, and the
+dev auto-reload loop (redeploy on change), against the local cluster."""
+
+import os
+import pty
+import re
+import select
+import signal
+import socket
+import subprocess
+import time
+import urllib.request
+
+import yaml
+
+from test_e2e_cli import running, wait_for
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _stop(p, sig=signal.SIGINT):
+    try:
+        os.killpg(p.pid, sig)
+        out, _ = p.communicate(timeout=30)
+    except Exception:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, _ = p.communicate()
+    return out
+
+
+def test_dev_port_forwarding_reaches_app(localkube):
+    lk = localkube
+    proj = lk.project("quickstart", "quickstart-pf")
+    remote = _free_port()  # pods share the host network here: use a free port for the app
+    local = _free_port()
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    cfg["cluster"]["namespace"] = "pf"
+    cfg["dev"].pop("overrideImages")  # run the app itself in dev mode
+    cfg["dev"]["ports"][0]["portMappings"] = [{"localPort": local, "remotePort": remote}]
+    open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    values = os.path.join(proj, "chart", "values.yaml")
+    v = yaml.safe_load(open(values))
+    v["components"][0]["containers"][0]["env"] = [{"name": "PORT", "value": str(remote)}]
+    open(values, "w").write(yaml.safe_dump(v))
+    dev = lk.popen(["dev", "--terminal=false"], proj)
+    try:
+        wait_for(lambda: running(lk.pods("pf")), timeout=60, what="pod")
+
+        def fetch():
+            try:
+                return urllib.request.urlopen(f"http://127.0.0.1:{local}/", timeout=2).read().decode()
+            except Exception:
+                return None
+
+        body = wait_for(fetch, timeout=30, what="forwarded response")
+        assert body.startswith("Hello from default-"), body
+        # many connections through the forwarder (one WebSocket stream each)
+        for _ in range(20):
+            assert fetch().startswith("Hello from")
+    finally:
+        out = _stop(dev)
+    assert f"Port forwarding started on {local}:{remote}" in out, out
+    lk.run(["purge"], proj)
+
+
+def test_enter_interactive_pty(localkube):
+    lk = localkube
+    proj = lk.project("quickstart", "quickstart-tty")
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    cfg["cluster"]["namespace"] = "tty"
+    open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    lk.run(["deploy"], proj)
+    wait_for(lambda: running(lk.pods("tty")), what="pod")
+    master, slave = pty.openpty()
+    p = subprocess.Popen([lk.bin, "enter"], cwd=proj, env=lk.env, stdin=slave, stdout=slave, stderr=slave,
+                         start_new_session=True)
+    os.close(slave)
+    buf = b""
+
+    def read_until(pat, timeout=20):
+        nonlocal buf
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            if re.search(pat, buf):
+                return True
+            r, _, _ = select.select([master], [], [], 0.2)
+            if r:
+                try:
+                    buf += os.read(master, 65536)
+                except OSError:
+                    break
+        return re.search(pat, buf) is not None
+
+    try:
+        time.sleep(1.0)
+        os.write(master, b"echo tty-$((40+2)); tty -s && echo IS_A_TTY\n")
+        assert read_until(rb"tty-42"), buf
+        assert read_until(rb"IS_A_TTY"), buf
+        os.write(master, b"exit 3\n")
+        assert p.wait(20) == 3
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGKILL)
+        os.close(master)
+    lk.run(["purge"], proj)
+
+
+def test_logs_follow_streams_new_lines(localkube):
+    lk = localkube
+    proj = lk.project("quickstart", "quickstart-logs")
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    cfg["cluster"]["namespace"] = "logsf"
+    open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    values = os.path.join(proj, "chart", "values.yaml")
+    v = yaml.safe_load(open(values))
+    v["components"][0]["containers"][0]["command"] = ["sh", "-c",
+                                                       "i=0; while true; do echo tick-$i; i=$((i+1)); sleep 0.2; done"]
+    open(values, "w").write(yaml.safe_dump(v))
+    lk.run(["deploy"], proj)
+    wait_for(lambda: running(lk.pods("logsf")), what="pod")
+    p = lk.popen(["logs", "-f", "--lines", "1"], proj)
+    try:
+        seen = []
+        deadline = time.time() + 20
+        while time.time() < deadline and len(seen) < 5:
+            line = p.stdout.readline()
+            if line.startswith("tick-"):
+                seen.append(int(line.strip().split("-")[1]))
+        assert len(seen) >= 5, seen
+        assert seen == sorted(seen) and seen[-1] - seen[0] == len(seen) - 1
+    finally:
+        _stop(p)
+    lk.run(["purge"], proj)
+
+
+def test_dev_auto_reload_redeploys_on_change(localkube):
+    lk = localkube
+    proj = lk.project("redeploy-instead-of-hot-reload")
+    dev = lk.popen(["dev"], proj)
+    try:
+        pods = wait_for(lambda: running(lk.pods("redeploy")), timeout=60, what="first pod")
+        first = pods[0]["metadata"]["name"]
+        time.sleep(1.5)  # let the poll watcher take its baseline
+        with open(os.path.join(proj, "server.py"), "a") as f:
+            f.write("\n# change\n")
+
+        def new_pod():
+            ps = running(lk.pods("redeploy"))
+            return [p for p in ps if p["metadata"]["name"] != first]
+
+        pods = wait_for(new_pod, timeout=60, what="redeployed pod")
+        assert pods[0]["spec"]["containers"][0]["image"] != "devspace-local/redeploy"
+    finally:
+        out = _stop(dev)
+    assert "Change detected, will reload in 2 seconds" in out, out
+    assert out.count("Building image") >= 2, out
+    lk.run(["purge"], proj)
