@@ -12,9 +12,12 @@ capacity equal to the visible GPUs (KFD topology), like the AMD GPU device plugi
 from __future__ import annotations
 
 import asyncio
+import base64
 import glob
 import os
 import socket
+import ssl
+import subprocess
 import threading
 import time
 
@@ -54,9 +57,37 @@ def free_port():
     return p
 
 
+def make_pki(d):
+    """Self-signed CA + server cert (127.0.0.1/localhost) + client cert, via the openssl CLI."""
+    os.makedirs(d, exist_ok=True)
+
+    def ossl(*args):
+        subprocess.run(["openssl"] + list(args), check=True, capture_output=True)
+
+    ossl("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-days", "2", "-subj", "/CN=devspace-local-ca",
+         "-keyout", f"{d}/ca.key", "-out", f"{d}/ca.crt")
+    ext = f"{d}/san.ext"
+    with open(ext, "w") as f:
+        f.write("subjectAltName=IP:127.0.0.1,DNS:localhost\n")
+    for name, subj, extra in (("server", "/CN=127.0.0.1", ["-extfile", ext]),
+                              ("client", "/CN=devspace-user/O=system:masters", [])):
+        ossl("req", "-newkey", "rsa:2048", "-nodes", "-subj", subj, "-keyout", f"{d}/{name}.key",
+             "-out", f"{d}/{name}.csr")
+        ossl("x509", "-req", "-in", f"{d}/{name}.csr", "-CA", f"{d}/ca.crt", "-CAkey", f"{d}/ca.key",
+             "-CAcreateserial", "-days", "2", "-out", f"{d}/{name}.crt", *extra)
+    return d
+
+
+def _b64file(path):
+    with open(path, "rb") as f:
+        return base64.b64encode(f.read()).decode()
+
+
 class LocalCluster:
-    def __init__(self, state_dir, port=0, gpus=None, context="devspace-local", extra_env=None):
+    def __init__(self, state_dir, port=0, gpus=None, context="devspace-local", extra_env=None, tls=False):
         self.state_dir = os.path.abspath(state_dir)
+        self.tls = tls
+        self.pki = make_pki(os.path.join(self.state_dir, "pki")) if tls else None
         os.makedirs(self.state_dir, exist_ok=True)
         self.port = port or free_port()
         self.gpus = detect_gpus() if gpus is None else gpus
@@ -76,21 +107,35 @@ class LocalCluster:
 
     @property
     def server(self):
-        return f"http://127.0.0.1:{self.port}"
+        return f"{'https' if self.tls else 'http'}://127.0.0.1:{self.port}"
 
     def kubeconfig_yaml(self, namespace="default"):
+        cluster = f"    server: {self.server}\n"
+        user = "    token: devspace-local-token\n"
+        if self.tls:  # verify the server against our CA and authenticate with a client cert
+            cluster += f"    certificate-authority-data: {_b64file(os.path.join(self.pki, 'ca.crt'))}\n"
+            user = (f"    client-certificate-data: {_b64file(os.path.join(self.pki, 'client.crt'))}\n"
+                    f"    client-key-data: {_b64file(os.path.join(self.pki, 'client.key'))}\n")
         return (
             "apiVersion: v1\nkind: Config\n"
             f"current-context: {self.context}\n"
             "clusters:\n"
-            f"- name: {self.context}\n  cluster:\n    server: {self.server}\n"
+            f"- name: {self.context}\n  cluster:\n{cluster}"
             "contexts:\n"
             f"- name: {self.context}\n  context:\n    cluster: {self.context}\n    user: {self.context}\n"
             f"    namespace: {namespace}\n"
             "users:\n"
-            f"- name: {self.context}\n  user:\n    token: devspace-local-token\n"
+            f"- name: {self.context}\n  user:\n{user}"
             "preferences: {}\n"
         )
+
+    def _ssl_context(self):
+        if not self.tls:
+            return None
+        ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH, cafile=os.path.join(self.pki, "ca.crt"))
+        ctx.load_cert_chain(os.path.join(self.pki, "server.crt"), os.path.join(self.pki, "server.key"))
+        ctx.verify_mode = ssl.CERT_REQUIRED  # mTLS: clients must present a cert signed by our CA
+        return ctx
 
     def write_kubeconfig(self, path, namespace="default"):
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
@@ -105,7 +150,7 @@ class LocalCluster:
     async def _amain(self):
         api_runner = web.AppRunner(self.api.app(), access_log=None)
         await api_runner.setup()
-        await web.TCPSite(api_runner, "127.0.0.1", self.port).start()
+        await web.TCPSite(api_runner, "127.0.0.1", self.port, ssl_context=self._ssl_context()).start()
         if os.path.exists(self.docker_sock):
             os.unlink(self.docker_sock)
         d_runner = web.AppRunner(make_app(self.images), access_log=None)
