@@ -18,5 +18,12 @@ build_and_run() {
   ASAN_OPTIONS="detect_leaks=1:halt_on_error=1" UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1" \
     "$dir/bin/devspace_tests" "${@:4}"
 }
-build_and_run thread "$ROOT/build-tsan" "${TSAN_CXX:-/opt/rocm/llvm/bin/clang++}" "$@"
-build_and_run address,undefined "$ROOT/build-asan" "${ASAN_CXX:-g++}" "$@"
+build_and_run thread "$ROOT/build/tsan" "${TSAN_CXX:-/opt/rocm/llvm/bin/clang++}" "$@"
+build_and_run address,undefined "$ROOT/build/asan" "${ASAN_CXX:-g++}" "$@"
+# The CLI itself under both sanitizers, driven by the end-to-end suite (local cluster).
+for b in tsan asan; do
+  echo "== e2e with build/$b/bin/devspace"
+  DEVSPACE_BIN="$ROOT/build/$b/bin/devspace" TSAN_OPTIONS="halt_on_error=1" ASAN_OPTIONS="detect_leaks=0:halt_on_error=1" \
+    python3 -m pytest -q -x "$ROOT/tests/test_e2e_cli.py" "$ROOT/tests/test_e2e_services.py" \
+      "$ROOT/tests/test_e2e_tls.py" "$ROOT/tests/test_cloud_cli.py" 2>&1 | tail -1
+done

@@ -86,7 +86,8 @@ std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, co
   int64_t max_alloc = 0, total = 0;
   std::vector<std::string> products;
   try {
-    for (auto& n : k.get("/api/v1/nodes").get("items").items()) {
+    Value nodes = k.get("/api/v1/nodes");
+    for (auto& n : nodes.get("items").items()) {
       int64_t a = n.at_path("status.allocatable").get("amd.com/gpu").as_int(0);
       total += a;
       max_alloc = std::max(max_alloc, a);

@@ -40,7 +40,8 @@ class DevspaceEnv:
         self.env = dict(os.environ)
         self.env.update(cluster.env(self.kubeconfig))
         self.env.update(HOME=self.home, DEVSPACE_NONINTERACTIVE="1", PYTHONPATH=ROOT)
-        self.bin = os.path.join(ROOT, "bin", "devspace")
+        # DEVSPACE_BIN: run the e2e suite against another build (e.g. build/asan/bin/devspace)
+        self.bin = os.environ.get("DEVSPACE_BIN") or os.path.join(ROOT, "bin", "devspace")
 
     def run(self, args, cwd, input=None, timeout=120, check=True):
         import subprocess
