@@ -114,7 +114,8 @@ std::unique_ptr<cli::Command> make_add() {
         .str("tag", "", "", "The tag of the image")
         .str("context", "", "", "The path of the images' context")
         .str("dockerfile", "", "", "The path of the images' dockerfile")
-        .str("buildengine", "", "", "Specify which engine should build the file. Should match this regex: docker|kaniko");
+        .str("buildengine", "", "", "Specify which engine should build the file. Should match this regex: docker|kaniko")
+        .required("image");
     add->add(std::move(c));
   }
   {
