@@ -193,6 +193,7 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
             "helper" if os.path.exists(os.path.join(ROOT, "bin", "devspace-helper")) else "fast")
         pod_file = os.path.join(root, "app", "train.py")
         samples, sync_samples = [], []
+        parts = {"pickup_ms": [], "step_ms": [], "code_swap_ms": [], "log_delivery_ms": []}
         for i in range(warmup + steps):
             if i == warmup and timed_start:
                 timed_start()
@@ -201,13 +202,22 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
             _set_marker(train, marker)
             t_sync = _wait_file_contains(pod_file, f'MARKER = "{marker}"')
             pat = rf"\[devspace-runner\] (reloaded|started) gen=\d+ marker={re.escape(marker)} "
-            t1, _, idx = tail.wait_for(pat, start_index=idx, timeout=600)
+            t1, line, idx = tail.wait_for(pat, start_index=idx, timeout=600)
             if i >= warmup:
                 samples.append((t1 - t0) * 1000.0)
                 sync_samples.append((t_sync - t0) * 1000.0)
+                # where the time goes: runner-side pickup (change seen -> new step done),
+                # delivery (runner print -> line in `devspace dev` output; same host clock)
+                f = dict(re.findall(r"(\w+_ms|t_mono)=([\d.]+)", line))
+                if "t_mono" in f:
+                    parts["pickup_ms"].append(float(f["pickup_ms"]))
+                    parts["step_ms"].append(float(f["step_ms"]))
+                    parts["code_swap_ms"].append(float(f["reload_ms"]))
+                    parts["log_delivery_ms"].append((t1 - float(f["t_mono"])) * 1000.0)
         if timed_end:
             timed_end()
-        return {"reload_ms": samples, "sync_ms": sync_samples, "mode": mode, "pod_deploy_s": deploy_s}
+        return {"reload_ms": samples, "sync_ms": sync_samples, "mode": mode, "pod_deploy_s": deploy_s,
+                "parts": parts}
     finally:
         _killpg(dev)
         cluster.stop()
@@ -390,6 +400,15 @@ def main():
         "deploy_warm_wall_clock_s": None if not deploy else round(deploy["warm_s"], 3),
         "gpu_pod_deploy_s": round(result["pod_deploy_s"], 3),
     }
+    parts = {k: round(_pct(v, 0.5), 2) for k, v in result.get("parts", {}).items() if v}
+    if parts:
+        # p50 components of one reload: sync (edit -> bytes in the pod) -> pickup (runner sees
+        # the change -> in-flight step drains -> code swap -> first new step done) -> log
+        # delivery back to `devspace dev`; other = inotify wake-ups + scheduling slack
+        parts["sync_ms"] = out["sync_p50_ms"]
+        parts["other_ms"] = round(
+            max(0.0, p50 - parts["sync_ms"] - parts.get("pickup_ms", 0) - parts.get("log_delivery_ms", 0)), 2)
+        out["breakdown_p50"] = parts
     if ref:
         rp50 = _pct(ref["reload_ms"], 0.5)
         out["reference_equivalent_p50_ms"] = round(rp50, 2)

@@ -192,10 +192,12 @@ class ApiServer:
             raise ApiError(400, "BadRequest", f'container "{request.query.get("container")}" is not valid for pod {name}')
         tail = int(request.query.get("tailLines", "-1") or -1)
         follow = request.query.get("follow") in ("true", "1")
+        q = c.subscribe() if follow else None
         data = b""
         if os.path.exists(c.log_path):
             with open(c.log_path, "rb") as f:
                 data = f.read()
+        seen = len(data)
         if tail >= 0:
             lines = data.splitlines(keepends=True)
             data = b"".join(lines[-tail:]) if tail else b""
@@ -204,20 +206,30 @@ class ApiServer:
         resp = web.StreamResponse(headers={"Content-Type": "text/plain"})
         await resp.prepare(request)
         await resp.write(data)
-        pos = os.path.getsize(c.log_path) if os.path.exists(c.log_path) else 0
-        while (ns, name) in self.kubelet.pods:
-            try:
-                size = os.path.getsize(c.log_path)
-            except OSError:
-                break
-            if size > pos:
-                with open(c.log_path, "rb") as f:
-                    f.seek(pos)
-                    chunk = f.read(size - pos)
-                pos = size
+        try:
+            # stream new output as the container writes it (chunks already in `data` skipped)
+            while (ns, name) in self.kubelet.pods:
+                try:
+                    off, chunk = await asyncio.wait_for(q.get(), 0.5)
+                except asyncio.TimeoutError:
+                    continue
+                if off is None:
+                    continue  # process ended; a restarted container keeps appending
+                end = off + len(chunk)
+                if end <= seen:
+                    continue
+                if off < seen:
+                    chunk = chunk[seen - off:]
+                seen = end
                 await resp.write(chunk)
-            await asyncio.sleep(0.02)
-        await resp.write_eof()
+        except (ConnectionResetError, asyncio.CancelledError):
+            pass
+        finally:
+            c.unsubscribe(q)
+        try:
+            await resp.write_eof()
+        except ConnectionResetError:
+            pass
         return resp
 
     # ------------------------------------------------------------------ exec / attach
@@ -351,27 +363,27 @@ class ApiServer:
         return ws
 
     async def _attach(self, ws, c):
-        pos = os.path.getsize(c.log_path) if os.path.exists(c.log_path) else 0
+        # output produced after the attach, streamed as the pump reads it from the container
+        q = c.subscribe()
 
         async def drain():
             async for _ in ws:
                 pass
 
         reader = asyncio.create_task(drain())
-        while not ws.closed and c.proc is not None:
-            try:
-                size = os.path.getsize(c.log_path)
-            except OSError:
-                break
-            if size > pos:
-                with open(c.log_path, "rb") as f:
-                    f.seek(pos)
-                    chunk = f.read(size - pos)
-                pos = size
+        try:
+            while not ws.closed and c.proc is not None:
+                try:
+                    off, chunk = await asyncio.wait_for(q.get(), 0.5)
+                except asyncio.TimeoutError:
+                    continue
+                if off is None:
+                    break  # the attached process exited
                 await ws.send_bytes(b"\x01" + chunk)
-            # container runtimes stream attach output as it is written; 2 ms polling keeps
-            # the emulation's added latency well below the sync/reload path being measured
-            await asyncio.sleep(0.002)
+        except (ConnectionResetError, asyncio.CancelledError):
+            pass
+        finally:
+            c.unsubscribe(q)
         if not ws.closed:
             await ws.send_bytes(b"\x03" + json.dumps(_exit_status(0)).encode())
             await ws.close()

@@ -73,6 +73,34 @@ class Container:
         self.started_at = None
         self.image_config = {}
         self.fatal = None  # waiting reason that will not recover (ErrImagePull, ...)
+        # Output streaming (like a CRI log pipe): the pump appends to the log file and pushes
+        # (offset, chunk) to attach/follow subscribers as soon as the process writes it;
+        # (None, None) marks the end of this process' output.
+        self.subscribers = set()
+        self.log_size = os.path.getsize(self.log_path) if os.path.exists(self.log_path) else 0
+        self.pump = None
+
+    def subscribe(self):
+        q = asyncio.Queue()
+        self.subscribers.add(q)
+        return q
+
+    def unsubscribe(self, q):
+        self.subscribers.discard(q)
+
+    async def pump_output(self, stream):
+        with open(self.log_path, "ab", buffering=0) as logf:
+            while True:
+                chunk = await stream.read(65536)
+                if not chunk:
+                    break
+                logf.write(chunk)
+                off = self.log_size
+                self.log_size += len(chunk)
+                for q in list(self.subscribers):
+                    q.put_nowait((off, chunk))
+        for q in list(self.subscribers):
+            q.put_nowait((None, None))
 
 
 class PodRuntime:
@@ -379,21 +407,18 @@ class Kubelet:
             return
         cwd = self.workdir(c)
         os.makedirs(cwd, exist_ok=True)
-        logf = open(c.log_path, "ab", buffering=0)
         try:
-            c.proc = await asyncio.create_subprocess_exec(*argv, cwd=cwd, env=self._env(rt, c), stdout=logf,
-                                                          stderr=logf, stdin=asyncio.subprocess.DEVNULL,
-                                                          start_new_session=True)
+            c.proc = await asyncio.create_subprocess_exec(*argv, cwd=cwd, env=self._env(rt, c),
+                                                          stdout=asyncio.subprocess.PIPE,
+                                                          stderr=asyncio.subprocess.STDOUT,
+                                                          stdin=asyncio.subprocess.DEVNULL, start_new_session=True)
         except (FileNotFoundError, PermissionError) as e:
             c.state = {"waiting": {"reason": "RunContainerError", "message": str(e)}}
             c.next_start = time.time() + min(30.0, 0.5 * (2 ** c.restarts))
             c.restarts += 1
-            logf.close()
             self.event(pod, "Failed", f"Error: {e}", "Warning")
             return
-        finally:
-            if c.proc is not None:
-                logf.close()
+        c.pump = asyncio.create_task(c.pump_output(c.proc.stdout))
         c.started_at = now_rfc3339()
         c.state = {"running": {"startedAt": c.started_at}}
         self.event(pod, "Started", f"Started container {c.name}")

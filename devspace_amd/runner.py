@@ -33,6 +33,7 @@ import os
 import signal
 import subprocess
 import sys
+import threading
 import time
 import traceback
 import types
@@ -106,17 +107,79 @@ class Context:
             _log(msg)
 
 
-def load_module(path: str, generation: int) -> types.ModuleType:
-    """Compile the user file into a fresh module object (no import cache involved)."""
+def load_module(path: str, generation: int, feed=None) -> types.ModuleType:
+    """Compile the user file into a fresh module object (no import cache involved). When the
+    change feed already compiled exactly these bytes in the background, that code is used."""
     with open(path, "rb") as f:
         src = f.read()
     name = f"devspace_user_{generation}"
     mod = types.ModuleType(name)
     mod.__file__ = path
-    code = compile(src, path, "exec")
+    code = feed.prepared_for(src) if feed is not None else None
+    if code is None:
+        code = compile(src, path, "exec")
     exec(code, mod.__dict__)  # noqa: S102 - executing the user's own synced code is the point
     mod.__devspace_digest__ = hashlib.sha256(src).hexdigest()[:8]
     return mod
+
+
+class ChangeFeed:
+    """Watches the synced directory on a background thread (the native inotify poll releases
+    the GIL) and pre-compiles the entry file as soon as it changes, so the code swap at the next
+    step boundary only has to exec it — the compile overlaps the in-flight GPU step."""
+
+    def __init__(self, watcher, entry):
+        self.watcher = watcher
+        self.entry = entry
+        self.cv = threading.Condition()
+        self.count = 0
+        self.first_t = None
+        self.prepared = None
+        self.stop = False
+        self.thread = threading.Thread(target=self._run, name="devspace-change-feed", daemon=True)
+        self.thread.start()
+
+    def _run(self):
+        while not self.stop:
+            try:
+                changed = [p for p in self.watcher.poll(100) if not _ignored(p)]
+            except Exception:  # pragma: no cover - watcher died; keep the loop alive
+                time.sleep(0.05)
+                continue
+            if not changed:
+                continue
+            t = time.perf_counter()
+            prep = None
+            try:
+                with open(self.entry, "rb") as f:
+                    src = f.read()
+                prep = (src, compile(src, self.entry, "exec"))
+            except Exception:  # syntax errors surface (with traceback) at the reload itself
+                prep = None
+            with self.cv:
+                self.count += 1
+                if self.first_t is None:
+                    self.first_t = t
+                self.prepared = prep
+                self.cv.notify_all()
+
+    def take(self, timeout_s=0.0):
+        """(number of change batches since the last call, perf_counter of the first one)."""
+        with self.cv:
+            if self.count == 0 and timeout_s > 0:
+                self.cv.wait(timeout_s)
+            n, t = self.count, self.first_t
+            self.count, self.first_t = 0, None
+            return n, t
+
+    def prepared_for(self, src):
+        with self.cv:
+            p = self.prepared
+        return p[1] if p is not None and p[0] == src else None
+
+    def close(self):
+        self.stop = True
+        self.thread.join(1.0)
 
 
 def _ignored(p: str) -> bool:
@@ -146,6 +209,7 @@ def worker_main(args) -> int:
     entry = os.path.abspath(args.entry)
     watch_dir = os.path.abspath(args.watch or os.path.dirname(entry))
     watcher = make_watcher(watch_dir)
+    feed = ChangeFeed(watcher, entry)
 
     gen = 1
     t_start = time.perf_counter()
@@ -179,12 +243,12 @@ def worker_main(args) -> int:
     signal.signal(signal.SIGTERM, _term)
     while not stop:
         # 1. pick up local change notifications (non-blocking while training; blocking when idle)
-        timeout = 0 if (not script_mode and args.train) else 50
-        changed = [p for p in watcher.poll(timeout) if not _ignored(p)]
-        if changed:
+        timeout = 0 if (not script_mode and args.train) else 0.05
+        n_changes, t_first = feed.take(timeout)
+        if n_changes:
             pending_gen += 1
             if reload_t0 is None:
-                reload_t0 = time.perf_counter()
+                reload_t0 = t_first
         # 2. ranks agree on the newest generation (keeps collectives in `step` matched)
         target = pending_gen
         if ctl is not None:
@@ -195,7 +259,7 @@ def worker_main(args) -> int:
         if target > gen:
             t_reload = time.perf_counter()
             try:
-                new_mod = load_module(entry, target)
+                new_mod = load_module(entry, target, feed)
                 new_setup_version = getattr(new_mod, "SETUP_VERSION", None)
                 if hasattr(new_mod, "setup") and (state is None or new_setup_version != setup_version):
                     state = new_mod.setup(ctx)
@@ -227,7 +291,7 @@ def worker_main(args) -> int:
             ctx.log(
                 f"reloaded gen={gen} marker={getattr(mod, 'MARKER', '')} digest={mod.__devspace_digest__} "
                 f"step={ctx.step} loss={loss} step_ms={step_ms:.2f} reload_ms={reload_ms:.2f} "
-                f"pickup_ms={since:.2f}"
+                f"pickup_ms={since:.2f} t_mono={time.perf_counter():.6f}"
             )
             continue
         if script_mode or not args.train:
@@ -244,6 +308,7 @@ def worker_main(args) -> int:
             ctx.log(f"step={ctx.step} gen={gen} loss={metrics.get('loss') if isinstance(metrics, dict) else None}")
         if max_steps and ctx.step >= max_steps:
             break
+    feed.close()
     watcher.close()
     if dist is not None and dist.is_initialized():
         dist.destroy_process_group()
