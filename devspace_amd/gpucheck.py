@@ -113,7 +113,7 @@ def sweep_copy(dev=0, nbytes=1 << 30):
     rows = []
     for unroll in (1, 2, 4, 8):
         for nt in (False, True):
-            for bpc in (2, 4, 8, 16):
+            for bpc in (1, 2, 3, 4, 8, 16):
                 gbps = probe.hbm_gbps_cfg(dev, unroll, nt, bpc, nbytes=nbytes)
                 rows.append({"unroll": unroll, "nontemporal": nt, "blocks_per_cu": bpc, "gbps": round(gbps, 1)})
     return rows

@@ -202,8 +202,11 @@ double gp_hbm_copy_gbps_cfg(int dev, size_t bytes, int iters, int unroll, int no
 }
 
 // HBM copy bandwidth in GB/s (bytes read + written per second), default configuration.
+// Tuned on MI355X (profiles/r1_hbm_copy_sweep.txt): 2 x dwordx4 in flight per lane,
+// nontemporal, 2 workgroups of 256 per CU -> 6.0 TB/s (95% of the 6.3 TB/s achievable copy);
+// more resident waves (8-16 WG/CU) thrash the HBM channels and drop to 4.3-5.2 TB/s.
 double gp_hbm_copy_gbps(int dev, size_t bytes, int iters) {
-  return gp_hbm_copy_gbps_cfg(dev, bytes, iters, 4, 1, 8);
+  return gp_hbm_copy_gbps_cfg(dev, bytes, iters, 2, 1, 2);
 }
 
 // Dense bf16 MFMA rate in TFLOP/s.
