@@ -80,6 +80,7 @@ void pipeline(Session& s, bool is_dev, bool force_build, bool force_deploy, cons
   bo.is_dev = is_dev;
   bo.force_rebuild = force_build;
   bo.docker_target = docker_target;
+  bo.interrupted = [] { return interrupted().load(); };
   bool rebuilt = build::build_all(s.cfg(), gen, s.kube, bo);
   if (rebuilt) s.ctx.save_generated();
   if (s.cfg().get("deployments").size() > 0 || !is_dev) {
