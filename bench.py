@@ -32,6 +32,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import random
 import re
 import shutil
 import signal
@@ -45,6 +46,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "inner-loop p50 ms (edit->pod hot-reload) + deploy wall-clock s, quickstart"
+EDIT_JITTER_S = 0.010  # uniform think time before each edit (> 2 training steps of the example)
 TINY = (("VOCAB", 256), ("DIM", 64), ("HEADS", 4), ("LAYERS", 1), ("SEQ", 32), ("BATCH", 2))
 
 
@@ -193,11 +195,17 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
             "helper" if os.path.exists(os.path.join(ROOT, "bin", "devspace-helper")) else "fast")
         pod_file = os.path.join(root, "app", "train.py")
         samples, sync_samples = [], []
-        parts = {"pickup_ms": [], "step_ms": [], "code_swap_ms": [], "log_delivery_ms": []}
+        parts = {"pickup_ms": [], "inflight_ms": [], "step_ms": [], "code_swap_ms": [], "log_delivery_ms": [],
+             "train_period_ms": []}
+        rng = random.Random(1234)
         for i in range(warmup + steps):
             if i == warmup and timed_start:
                 timed_start()
             marker = f"e{i}" + ("_" * (i % 2))
+            # think time before each edit: a developer's save lands at a random point of the
+            # pod's training step, not right after the previous reload's log line (that would
+            # fix the phase and always wait out the same share of the in-flight step)
+            time.sleep(rng.uniform(0.0, EDIT_JITTER_S))
             t0 = time.perf_counter()
             _set_marker(train, marker)
             t_sync = _wait_file_contains(pod_file, f'MARKER = "{marker}"')
@@ -213,6 +221,9 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
                     parts["pickup_ms"].append(float(f["pickup_ms"]))
                     parts["step_ms"].append(float(f["step_ms"]))
                     parts["code_swap_ms"].append(float(f["reload_ms"]))
+                    if "inflight_ms" in f:
+                        parts["inflight_ms"].append(float(f["inflight_ms"]))
+                        parts["train_period_ms"].append(float(f["period_ms"]))
                     parts["log_delivery_ms"].append((t1 - float(f["t_mono"])) * 1000.0)
         if timed_end:
             timed_end()
@@ -261,10 +272,12 @@ def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False):
     try:
         _, _, idx = tail.wait_for(r"\[devspace-runner\] started gen=\d+ marker=v0", timeout=600)
         proj_file, pod_file = os.path.join(proj, "train.py"), os.path.join(pod, "train.py")
+        rng = random.Random(1234)
         for i in range(warmup + steps):
             # alternate marker lengths so consecutive edits always differ in size (compat mode
             # compares rounded mtimes + size, like the reference)
             marker = f"e{i}" + ("_" * (i % 2))
+            time.sleep(rng.uniform(0.0, EDIT_JITTER_S))
             t0 = time.perf_counter()
             _set_marker(proj_file, marker)
             t_sync = _wait_file_contains(pod_file, f'MARKER = "{marker}"')
@@ -343,7 +356,8 @@ def main():
             if not args.no_deploy_bench:
                 try:
                     deploy = __import__("devspace_amd.localkube.bench", fromlist=["bench_deploy"]).bench_deploy(workdir)
-                    _log(f"quickstart deploy cold {deploy['cold_s']:.3f}s warm {deploy['warm_s']:.3f}s")
+                    _log(f"quickstart deploy cold {deploy['cold_s']:.3f}s warm {deploy['warm_s']:.3f}s "
+                         f"phases {deploy.get('cold_phases_ms')}")
                 except Exception as e:  # reported, not fatal for the latency metric
                     _log(f"deploy benchmark failed: {e}")
             result = dev_loop(workdir, nproc, gpus, args.steps, args.warmup, tiny=args.tiny,
@@ -399,6 +413,7 @@ def main():
         "deploy_wall_clock_s": None if not deploy else round(deploy["cold_s"], 3),
         "deploy_warm_wall_clock_s": None if not deploy else round(deploy["warm_s"], 3),
         "gpu_pod_deploy_s": round(result["pod_deploy_s"], 3),
+        "deploy_cold_phases_ms": None if not deploy else deploy.get("cold_phases_ms"),
     }
     parts = {k: round(_pct(v, 0.5), 2) for k, v in result.get("parts", {}).items() if v}
     if parts:

@@ -37,6 +37,21 @@ def run_devspace(args, cwd, env, timeout=300):
     return dt, p.stdout
 
 
+def _phases(trace_path):
+    """Per-phase milliseconds of one CLI run from .devspace/logs/trace.jsonl."""
+    import json
+
+    out = {}
+    try:
+        with open(trace_path) as f:
+            for line in f:
+                s = json.loads(line)
+                out[s["span"]] = round(out.get(s["span"], 0.0) + s["dur_us"] / 1000.0, 2)
+    except OSError:
+        pass
+    return out
+
+
 def bench_deploy(workdir, example="quickstart"):
     base = os.path.join(workdir, "deploy-bench")
     os.makedirs(base, exist_ok=True)
@@ -45,11 +60,13 @@ def bench_deploy(workdir, example="quickstart"):
     cluster = LocalCluster(os.path.join(base, "cluster"), gpus=0).start()
     try:
         env = devspace_env(cluster, base)
+        trace = os.path.join(proj, ".devspace", "logs", "trace.jsonl")
         cold, out = run_devspace(["deploy"], proj, env)
         if "Successfully deployed!" not in out:
             raise RuntimeError(out)
+        phases = _phases(trace)
         warm, _ = run_devspace(["deploy", "-d"], proj, env)
         run_devspace(["purge"], proj, env)
-        return {"cold_s": cold, "warm_s": warm}
+        return {"cold_s": cold, "warm_s": warm, "cold_phases_ms": phases}
     finally:
         cluster.stop()

@@ -1,8 +1,14 @@
-"""Compile the HIP sources in this directory for gfx950 (in-tree .so, travels with the repo)."""
+"""Compile the HIP sources in this directory for gfx950 (in-tree .so files that travel with the repo).
+
+* gpuprobe.hip  -> libgpuprobe.so           C ABI, loaded with ctypes by devspace_amd.gpucheck
+* fused_ops.hip -> _fused_ops<EXT_SUFFIX>   PyTorch extension (ATen + pybind11), compiled directly
+                                            with hipcc against the installed torch headers/libs
+"""
 
 import os
 import shutil
 import subprocess
+import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
@@ -19,13 +25,51 @@ def lib_path(name="gpuprobe"):
     return os.path.join(HERE, f"lib{name}.so")
 
 
-def build(verbose=False, force=False):
-    src = os.path.join(HERE, "gpuprobe.hip")
-    out = lib_path()
-    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
-        return out
-    cmd = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wno-unused-value", "-o", out, src]
+def fused_path():
+    return os.path.join(HERE, "_fused_ops" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _stale(out, *srcs):
+    return not os.path.exists(out) or any(os.path.getmtime(out) < os.path.getmtime(s) for s in srcs)
+
+
+def _run(cmd, verbose):
     if verbose:
         print("+", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+
+
+def build_probe(verbose=False, force=False):
+    src = os.path.join(HERE, "gpuprobe.hip")
+    out = lib_path()
+    if force or _stale(out, src):
+        _run([hipcc(), "-O3", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wno-unused-value", "-o", out, src],
+             verbose)
+    return out
+
+
+def build_fused(verbose=False, force=False):
+    import torch  # headers + libraries of the torch this extension is loaded into
+
+    src = os.path.join(HERE, "fused_ops.hip")
+    out = fused_path()
+    if not (force or _stale(out, src)):
+        return out
+    troot = os.path.dirname(torch.__file__)
+    tlib = os.path.join(troot, "lib")
+    cxx11 = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
+           "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_fused_ops", "-DTORCH_API_INCLUDE_EXTENSION_H",
+           f"-D_GLIBCXX_USE_CXX11_ABI={cxx11}", "-Wno-unused-result",
+           "-I" + os.path.join(troot, "include"), "-I" + os.path.join(troot, "include", "torch", "csrc", "api", "include"),
+           "-I" + sysconfig.get_paths()["include"], src,
+           "-L" + tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+           "-Wl,-rpath," + tlib, "-o", out]
+    _run(cmd, verbose)
+    return out
+
+
+def build(verbose=False, force=False):
+    out = build_probe(verbose=verbose, force=force)
+    build_fused(verbose=verbose, force=force)
     return out

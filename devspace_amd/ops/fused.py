@@ -1,0 +1,142 @@
+"""Autograd wrappers around the gfx950 fused ops (fused_ops.hip).
+
+    from devspace_amd.ops import fused
+    norm = fused.RMSNorm(dim)             # drop-in for nn.RMSNorm
+    y = fused.swiglu(h)                   # silu(h[..., :H]) * h[..., H:]
+    loss = fused.cross_entropy(logits, t) # mean CE on bf16 logits [N, V]
+
+On a GPU the HIP kernels are mandatory: if the in-tree extension is missing or broken the
+first call raises (no silent eager fallback). On CPU tensors (tests, CPU smoke runs) the plain
+PyTorch formulation is used.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+_ext = None
+_ext_error = None
+
+
+def ext():
+    """The compiled extension module (raises with the build error on a GPU box)."""
+    global _ext, _ext_error
+    if _ext is None and _ext_error is None:
+        try:
+            from devspace_amd.ops import _fused_ops  # noqa: WPS433
+
+            _ext = _fused_ops
+        except ImportError as e:  # pragma: no cover - depends on the build
+            _ext_error = e
+    if _ext is None:
+        raise RuntimeError(f"devspace_amd fused HIP ops are not built ({_ext_error}); run "
+                           "`python -c 'import __graft_entry__ as g; g.build()'`")
+    return _ext
+
+
+def _use_hip(t: torch.Tensor) -> bool:
+    return t.is_cuda and t.dtype == torch.bfloat16
+
+
+# ------------------------------------------------------------------------------ ops
+# The differentiable entry points are C++ autograd nodes inside the extension (no Python on
+# the forward/backward path of the training step).
+
+
+def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float | None = None) -> torch.Tensor:
+    if eps is None:
+        eps = torch.finfo(x.dtype).eps
+    if _use_hip(x) and weight.dtype == torch.bfloat16 and ext().rmsnorm_supported(x.shape[-1]):
+        return ext().rms_norm(x, weight, float(eps))
+    return F.rms_norm(x, (x.shape[-1],), weight, eps)
+
+
+class RMSNorm(nn.Module):
+    """nn.RMSNorm(dim) with the fused HIP forward/backward (same parameters, same eps default)."""
+
+    def __init__(self, dim: int, eps: float | None = None):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x):
+        return rms_norm(x, self.weight, self.eps)
+
+
+def swiglu(h: torch.Tensor) -> torch.Tensor:
+    """silu(g) * u for h = cat([g, u], -1) (the gate/up projection output)."""
+    if _use_hip(h) and h.shape[-1] % 4 == 0:
+        return ext().swiglu(h)
+    g, u = h.chunk(2, dim=-1)
+    return F.silu(g) * u
+
+
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+    """Mean cross-entropy of [N, V] logits (computed in fp32 from bf16 logits, no fp32 copy)."""
+    if _use_hip(logits) and logits.dim() == 2 and logits.shape[1] % 8 == 0 and target.dtype == torch.long:
+        return ext().cross_entropy(logits, target, int(ignore_index))
+    return F.cross_entropy(logits.float(), target, ignore_index=ignore_index)
+
+
+# ------------------------------------------------------------------------------ AdamW
+
+
+def _hip_ok(t: torch.Tensor) -> bool:
+    return _use_hip(t) and t.is_contiguous() and t.data_ptr() % 16 == 0
+
+
+class AdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW (decoupled weight decay, no amsgrad) with a multi-tensor HIP update for
+    bf16 GPU parameters: one launch per <= 48 tensors, moments kept in the parameter dtype like
+    torch's fused AdamW. Other parameters (CPU, fp32, non-contiguous) take the same math in
+    plain PyTorch ops."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        if lr < 0 or eps < 0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
+            raise ValueError("invalid AdamW hyper-parameters")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+            buckets = {}  # step -> lists for one multi-tensor launch
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("AdamW does not support sparse gradients")
+                st = self.state[p]
+                if not st:
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                g = p.grad
+                if all(_hip_ok(t) for t in (p, g, st["exp_avg"], st["exp_avg_sq"])):
+                    b = buckets.setdefault(st["step"], ([], [], [], []))
+                    for lst, t in zip(b, (p, g, st["exp_avg"], st["exp_avg_sq"])):
+                        lst.append(t)
+                else:
+                    _adamw_eager(p, g, st["exp_avg"], st["exp_avg_sq"], lr, b1, b2, eps, wd, st["step"])
+            for step, (ps, gs, ms, vs) in buckets.items():
+                ext().adamw_step(ps, gs, ms, vs, lr, b1, b2, eps, wd, step)
+        return loss
+
+
+def _adamw_eager(p, g, m, v, lr, b1, b2, eps, wd, step):
+    pf, gf = p.float(), g.float()
+    mf = m.float().mul_(b1).add_(gf, alpha=1 - b1)
+    vf = v.float().mul_(b2).addcmul_(gf, gf, value=1 - b2)
+    pf.mul_(1 - lr * wd)
+    denom = vf.sqrt().div_((1 - b2 ** step) ** 0.5).add_(eps)
+    pf.addcdiv_(mf, denom, value=-lr / (1 - b1 ** step))
+    p.copy_(pf)
+    m.copy_(mf)
+    v.copy_(vf)

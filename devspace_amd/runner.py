@@ -231,6 +231,8 @@ def worker_main(args) -> int:
     )
     pending_gen = gen
     reload_t0 = None
+    period_ema = None  # steady-state loop period (ms), reported with each reload
+    t_iter = time.perf_counter()
     last_print_step = 0
     max_steps = args.max_steps
     script_mode = not hasattr(mod, "step")
@@ -258,6 +260,7 @@ def worker_main(args) -> int:
             pending_gen = max(pending_gen, target)
         if target > gen:
             t_reload = time.perf_counter()
+            wait_ms = (t_reload - reload_t0) * 1000.0 if reload_t0 else 0.0
             try:
                 new_mod = load_module(entry, target, feed)
                 new_setup_version = getattr(new_mod, "SETUP_VERSION", None)
@@ -291,8 +294,10 @@ def worker_main(args) -> int:
             ctx.log(
                 f"reloaded gen={gen} marker={getattr(mod, 'MARKER', '')} digest={mod.__devspace_digest__} "
                 f"step={ctx.step} loss={loss} step_ms={step_ms:.2f} reload_ms={reload_ms:.2f} "
-                f"pickup_ms={since:.2f} t_mono={time.perf_counter():.6f}"
+                f"pickup_ms={since:.2f} inflight_ms={wait_ms:.2f} period_ms={period_ema or 0.0:.2f} "
+                f"t_mono={time.perf_counter():.6f}"
             )
+            t_iter = time.perf_counter()
             continue
         if script_mode or not args.train:
             continue
@@ -303,6 +308,10 @@ def worker_main(args) -> int:
             ctx.log(f"step failed gen={gen}:\n{traceback.format_exc()}")
             time.sleep(0.2)
             continue
+        now = time.perf_counter()
+        dt = (now - t_iter) * 1000.0
+        t_iter = now
+        period_ema = dt if period_ema is None else 0.9 * period_ema + 0.1 * dt
         if args.log_every and ctx.step - last_print_step >= args.log_every:
             last_print_step = ctx.step
             ctx.log(f"step={ctx.step} gen={gen} loss={metrics.get('loss') if isinstance(metrics, dict) else None}")

@@ -9,6 +9,19 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+try:  # gfx950 fused HIP kernels (RMSNorm, SwiGLU, cross-entropy) shipped with devspace_amd
+    from devspace_amd.ops.fused import AdamW, RMSNorm, cross_entropy, swiglu
+except ImportError:  # plain PyTorch when the package is not in the image
+    RMSNorm = nn.RMSNorm
+    AdamW = None
+
+    def swiglu(h):
+        g, u = h.chunk(2, dim=-1)
+        return F.silu(g) * u
+
+    def cross_entropy(logits, target):
+        return F.cross_entropy(logits.float(), target)
+
 MARKER = "v0"
 SETUP_VERSION = 1  # bump to rebuild model/optimizer on the next reload
 
@@ -24,10 +37,10 @@ class Block(nn.Module):
     def __init__(self, dim, heads):
         super().__init__()
         self.heads = heads
-        self.norm1 = nn.RMSNorm(dim)
+        self.norm1 = RMSNorm(dim)
         self.qkv = nn.Linear(dim, 3 * dim, bias=False)
         self.proj = nn.Linear(dim, dim, bias=False)
-        self.norm2 = nn.RMSNorm(dim)
+        self.norm2 = RMSNorm(dim)
         self.up = nn.Linear(dim, 8 * dim // 3 * 2, bias=False)
         self.down = nn.Linear(8 * dim // 3, dim, bias=False)
 
@@ -36,8 +49,7 @@ class Block(nn.Module):
         q, k, v = self.qkv(self.norm1(x)).view(b, t, 3, self.heads, d // self.heads).unbind(2)
         a = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=True)
         x = x + self.proj(a.transpose(1, 2).reshape(b, t, d))
-        g, u = self.up(self.norm2(x)).chunk(2, dim=-1)
-        return x + self.down(F.silu(g) * u)
+        return x + self.down(swiglu(self.up(self.norm2(x))))
 
 
 class TinyLM(nn.Module):
@@ -45,7 +57,7 @@ class TinyLM(nn.Module):
         super().__init__()
         self.emb = nn.Embedding(VOCAB, DIM)
         self.blocks = nn.ModuleList([Block(DIM, HEADS) for _ in range(LAYERS)])
-        self.norm = nn.RMSNorm(DIM)
+        self.norm = RMSNorm(DIM)
         self.head = nn.Linear(DIM, VOCAB, bias=False)
 
     def forward(self, idx):
@@ -61,7 +73,10 @@ def setup(ctx):
     if ctx.distributed:
         # one process per GPU; big buckets -> few large RCCL all-reduces over xGMI
         model = nn.parallel.DistributedDataParallel(model, bucket_cap_mb=128, gradient_as_bucket_view=True)
-    opt = torch.optim.AdamW(model.parameters(), lr=3e-4, fused=ctx.device.type == "cuda")
+    if AdamW is not None:
+        opt = AdamW(model.parameters(), lr=3e-4)  # multi-tensor HIP update
+    else:
+        opt = torch.optim.AdamW(model.parameters(), lr=3e-4, fused=ctx.device.type == "cuda")
     data = torch.randint(0, VOCAB, (BATCH, SEQ + 1), device=ctx.device)
     return {"model": model, "opt": opt, "data": data}
 
@@ -69,7 +84,7 @@ def setup(ctx):
 def step(ctx, state):
     model, opt, data = state["model"], state["opt"], state["data"]
     logits = model(data[:, :-1])
-    loss = F.cross_entropy(logits.float().view(-1, VOCAB), data[:, 1:].reshape(-1))
+    loss = cross_entropy(logits.view(-1, VOCAB), data[:, 1:].reshape(-1))
     opt.zero_grad(set_to_none=True)
     loss.backward()
     opt.step()

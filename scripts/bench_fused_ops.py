@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""A/B of the gfx950 fused ops against the eager PyTorch op chains they replace, in one
+process with interleaved rounds (cdna_hip_programming.md §5.4 rule 24), on the shapes of the
+rocm-pytorch example (B*T = 4096 rows, D = 1024, H = 2730, V = 8192), plus the whole
+TinyLM training step built either way.
+
+    python scripts/bench_fused_ops.py [--rounds 10] [--json out.json]
+"""
+
+import argparse
+import importlib.util
+import json
+import os
+import statistics
+import sys
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from devspace_amd.ops import fused  # noqa: E402
+
+
+def timeit(fn, iters):
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    start.record()
+    for _ in range(iters):
+        fn()
+    end.record()
+    torch.cuda.synchronize()
+    return start.elapsed_time(end) * 1000.0 / iters  # us
+
+
+def op_cases(dev):
+    R, D, H, V = 4096, 1024, 2730, 8192
+    x = torch.randn(R, D, device=dev).bfloat16().requires_grad_()
+    w = torch.ones(D, device=dev).bfloat16().requires_grad_()
+    dy = torch.randn(R, D, device=dev).bfloat16()
+    h = torch.randn(R, 2 * H, device=dev).bfloat16().requires_grad_()
+    dyh = torch.randn(R, H, device=dev).bfloat16()
+    logits = torch.randn(R, V, device=dev).bfloat16().requires_grad_()
+    t = torch.randint(0, V, (R,), device=dev)
+    eps = torch.finfo(torch.bfloat16).eps
+
+    def rms_fused():
+        fused.rms_norm(x, w, eps).backward(dy)
+
+    def rms_eager():
+        F.rms_norm(x, (D,), w, eps).backward(dy)
+
+    def swiglu_fused():
+        fused.swiglu(h).backward(dyh)
+
+    def swiglu_eager():
+        g, u = h.chunk(2, -1)
+        (F.silu(g) * u).backward(dyh)
+
+    def ce_fused():
+        fused.cross_entropy(logits, t).backward()
+
+    def ce_eager():
+        F.cross_entropy(logits.float(), t).backward()
+
+    return {"rmsnorm fwd+bwd [4096x1024]": (rms_fused, rms_eager),
+            "swiglu fwd+bwd [4096x2x2730]": (swiglu_fused, swiglu_eager),
+            "cross_entropy fwd+bwd [4096x8192]": (ce_fused, ce_eager)}
+
+
+def load_train():
+    spec = importlib.util.spec_from_file_location("tinylm_ab", os.path.join(ROOT, "examples", "rocm-pytorch", "train.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def step_case(dev):
+    class Ctx:
+        rank, distributed, device = 0, False, dev
+
+    m_fused = load_train()
+    m_eager = load_train()
+    m_eager.RMSNorm = nn.RMSNorm
+
+    def sw(hh):
+        g, u = hh.chunk(2, dim=-1)
+        return F.silu(g) * u
+
+    m_eager.swiglu = sw
+    m_eager.cross_entropy = lambda lg, tg: F.cross_entropy(lg.float(), tg)
+    sf, se = m_fused.setup(Ctx()), m_eager.setup(Ctx())
+    return ("TinyLM train step (4x1024, B8xT512)", (lambda: m_fused.step(Ctx(), sf), lambda: m_eager.step(Ctx(), se)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    fused.ext()
+    cases = op_cases(dev)
+    name, fns = step_case(dev)
+    cases[name] = fns
+    res = {k: {"fused": [], "eager": []} for k in cases}
+    for _ in range(a.rounds):
+        for k, (f, e) in cases.items():
+            iters = 5 if k.startswith("TinyLM") else a.iters
+            res[k]["fused"].append(timeit(f, iters))
+            res[k]["eager"].append(timeit(e, iters))
+    out = {}
+    print(f"{'case':42s} {'fused_us':>10} {'eager_us':>10} {'speedup':>8}   (median of {a.rounds} interleaved rounds)")
+    for k, v in res.items():
+        fm, em = statistics.median(v["fused"]), statistics.median(v["eager"])
+        out[k] = {"fused_us": round(fm, 1), "eager_us": round(em, 1), "speedup": round(em / fm, 3),
+                  "fused_min_us": round(min(v["fused"]), 1), "eager_min_us": round(min(v["eager"]), 1)}
+        print(f"{k:42s} {fm:>10.1f} {em:>10.1f} {em / fm:>8.2f}x")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({"device": torch.cuda.get_device_name(0), "results": out}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -499,10 +499,12 @@ void Session::upstream_loop() {
       {
         std::unique_lock<std::mutex> lk(q_mu_);
         if (!first) {
-          // Fast modes: a finished write (close/rename/delete) only needs a 1 ms grace period
-          // to absorb its sibling events; partial writes wait the full quiet window.
-          int w = (mode_ != Mode::Compat && last_settled) ? std::min(window_ms_, 1) : window_ms_;
-          q_cv_.wait_for(lk, std::chrono::milliseconds(w), [this] { return !queue_.empty() || stopping_ || failed_; });
+          // Fast modes: a finished write (close/rename/delete) only needs a short grace period to
+          // absorb its sibling events (an editor's write-temp + rename arrive in the same inotify
+          // read, well inside 250 us); partial writes wait the full quiet window.
+          long w_us = (mode_ != Mode::Compat && last_settled) ? std::min<long>(window_ms_ * 1000L, 250)
+                                                               : window_ms_ * 1000L;
+          q_cv_.wait_for(lk, std::chrono::microseconds(w_us), [this] { return !queue_.empty() || stopping_ || failed_; });
         }
         evs.assign(std::make_move_iterator(queue_.begin()), std::make_move_iterator(queue_.end()));
         queue_.clear();
