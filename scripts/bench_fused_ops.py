@@ -65,7 +65,20 @@ def op_cases(dev):
     def ce_eager():
         F.cross_entropy(logits.float(), t).backward()
 
-    return {"rmsnorm fwd+bwd [4096x1024]": (rms_fused, rms_eager),
+    # optimizer: TinyLM-sized parameter set (67M bf16), grads fixed
+    shapes = [(8192, 1024), (8192, 1024)] + [(3072, 1024), (1024, 1024), (5460, 1024), (1024, 2730), (1024,),
+                                             (1024,)] * 4
+    params = [torch.randn(s, device=dev).bfloat16().requires_grad_() for s in shapes]
+    for q in params:
+        q.grad = torch.randn_like(q) * 1e-3
+    params_b = [q.detach().clone().requires_grad_() for q in params]
+    for q, r in zip(params, params_b):
+        r.grad = q.grad.clone()
+    opt_f = fused.AdamW(params, lr=1e-4)
+    opt_e = torch.optim.AdamW(params_b, lr=1e-4, fused=True)
+
+    return {"adamw step [67M bf16 params]": (opt_f.step, opt_e.step),
+            "rmsnorm fwd+bwd [4096x1024]": (rms_fused, rms_eager),
             "swiglu fwd+bwd [4096x2x2730]": (swiglu_fused, swiglu_eager),
             "cross_entropy fwd+bwd [4096x8192]": (ce_fused, ce_eager)}
 
