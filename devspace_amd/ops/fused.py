@@ -80,6 +80,24 @@ def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int 
     return F.cross_entropy(logits.float(), target, ignore_index=ignore_index)
 
 
+def attention(qkv: torch.Tensor, causal: bool = True, scale: float | None = None) -> torch.Tensor:
+    """Multi-head attention on the packed projection output qkv [B, T, 3, H, D] -> [B, T, H, D].
+
+    HIP flash attention (MFMA, fwd + bwd) for bf16, D == 64, T % 128 == 0; otherwise
+    F.scaled_dot_product_attention on transposed views."""
+    b, t, three, h, d = qkv.shape
+    if three != 3:
+        raise ValueError("qkv must be [B, T, 3, H, D]")
+    if scale is None:
+        scale = d ** -0.5
+    if _use_hip(qkv) and ext().attention_supported(qkv):
+        return ext().attention(qkv, bool(causal), float(scale))
+    q, k, v = qkv.unbind(2)
+    o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=causal,
+                                       scale=scale)
+    return o.transpose(1, 2)
+
+
 # ------------------------------------------------------------------------------ AdamW
 
 

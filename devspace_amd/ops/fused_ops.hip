@@ -450,6 +450,444 @@ __global__ void __launch_bounds__(kBlock) adamw_kernel(AdamTable t, AdamScalars 
   }
 }
 
+// ------------------------------------------------------------------------------ attention
+//
+// Flash attention (head dim 64, bf16 in/out, fp32 softmax/accumulators) on
+// v_mfma_f32_32x32x16_bf16, reading Q/K/V straight from the packed qkv projection output
+// [B, T, 3, H, 64] and writing O as [B, T, H, 64] (no transposes / stack copies around it).
+//
+// Forward (one workgroup = 128 queries of one (b, h), 4 waves x 32 queries; K/V tiles of 64
+// keys double-buffered in LDS, register-staged: the next tile's global loads are issued before
+// the current tile's MFMAs and written after them):
+//   S^T = K Q^T      keys on the MFMA rows, the wave's 32 queries on the lanes, so the online
+//                    softmax (max, exp2, sum) is lane-local plus one xor-32 exchange;
+//   O^T += V^T P^T   the P^T accumulators are the B operand as they stand (k order permuted,
+//                    cdna_hip_programming.md §3), V^T comes from ds_read_b64_tr_b16 reads of the
+//                    row-major V tile; O^T keeps the query on the lane, so the per-query rescale
+//                    is a scalar per lane.
+// LDS tiles use 128-B rows with a 16-B chunk XOR swizzle (chunk ^ ((row >> 1) & 7)): the
+// ds_read_b128 row reads of the 32x32x16 A operand are conflict-free.
+// Backward (FlashAttention-2 split, no atomics): a dK/dV kernel (workgroup = 128 keys, loops over
+// query tiles; S and dP with the key on the lane, dV^T += dO^T P and dK^T += Q^T dS from the
+// accumulators) and a dQ kernel (workgroup = 128 queries, loops over key tiles like the forward;
+// dQ^T += K^T dS^T), plus a rowsum(dO * O) preprocess.
+
+constexpr int kHD = 64;     // head dim
+constexpr int kQBlk = 128;  // queries (fwd / dQ) or keys (dK/dV) per workgroup
+constexpr int kTile = 64;   // keys (fwd / dQ) or queries (dK/dV) per LDS tile
+constexpr int kTileBytes = kTile * kHD * 2;
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) unsigned char lds_u8;
+
+__device__ __forceinline__ f32x16 mfma32(const u16x8& a, const u16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+
+// byte offset of 16-byte chunk `chunk` (0..7) of row `row` in a [64][64] bf16 LDS tile
+__device__ __forceinline__ int tile_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+__device__ __forceinline__ u16x8 lds_row8(const unsigned char* tile, int row, int chunk) {
+  return *reinterpret_cast<const u16x8*>(tile + tile_off(row, chunk));
+}
+
+// Transposed operand of a 32x32x16 MFMA from a row-major [rows][64] tile: lane (r = lane&31,
+// h = lane>>5) gets column col0 + r of rows {r0 + 4h + 0..3} (elements 0..3) and
+// {r0 + 8 + 4h + 0..3} (elements 4..7), i.e. the k order of an accumulator used as the other
+// operand (§3 "An accumulator tile as the next MFMA's operand"). Two ds_read_b64_tr_b16.
+__device__ __forceinline__ u16x8 lds_tr8(const unsigned char* tile, int r0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, hh = lane >> 5;
+  const int row = r0 + 4 * hh + (i >> 2);
+  const int col = col0 + 16 * (g & 1) + 4 * (i & 3);
+  const int off1 = tile_off(row, col >> 3) + ((col & 7) << 1);
+  const int off2 = tile_off(row + 8, col >> 3) + ((col & 7) << 1);
+  lds_u8* base = (lds_u8*)tile;
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off1));
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off2));
+  u16x8 o;
+  o[0] = a[0];
+  o[1] = a[1];
+  o[2] = a[2];
+  o[3] = a[3];
+  o[4] = b[0];
+  o[5] = b[1];
+  o[6] = b[2];
+  o[7] = b[3];
+  return o;
+}
+
+// accumulator registers 8s .. 8s+7 as a bf16 MFMA operand (k-step s of the accumulator's rows)
+__device__ __forceinline__ u16x8 acc_to_op(const f32x16& acc, int s) {
+  u16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2b(acc[8 * s + j]);
+  return o;
+}
+
+// row (within a 32x32 accumulator tile) held by register `reg` of lane half `hh`
+__device__ __forceinline__ int acc_row(int reg, int hh) { return (reg & 3) + 8 * (reg >> 2) + 4 * hh; }
+
+struct AttnParams {
+  const u16* q;
+  const u16* k;
+  const u16* v;
+  const u16* o;
+  const u16* dout;
+  u16* out;            // fwd: O; bwd: dQ (dq kernel) / dK (dkdv kernel)
+  u16* out2;           // bwd dkdv kernel: dV
+  const float* lse;    // [B, H, T] log2-domain LSE of the scaled scores
+  const float* delta;  // [B, H, T] rowsum(dO * O)
+  float* stat_out;     // fwd: lse; bwd preprocess: delta
+  int64_t sb, st, sh;  // q/k/v (and dq/dk/dv) strides in elements
+  int64_t ob, ot, oh;  // o / dout strides
+  int T, H;
+  float scale_log2;  // softmax scale * log2(e)
+  float scale;       // softmax scale
+};
+
+// 256 threads stage one [64][64] tile of two tensors (4 x 16 B per thread) through registers
+struct Stage {
+  u16x8 r[4];
+  __device__ __forceinline__ void load(const u16* a, const u16* b, int64_t base, int64_t st, int row0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = threadIdx.x + 256 * u;
+      const int row = (c >> 3) & 63, ch = c & 7;
+      const u16* src = ((c >> 9) ? b : a) + base + (int64_t)(row0 + row) * st + ch * 8;
+      r[u] = *reinterpret_cast<const u16x8*>(src);
+    }
+  }
+  __device__ __forceinline__ void store(unsigned char* ta, unsigned char* tb) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = threadIdx.x + 256 * u;
+      const int row = (c >> 3) & 63, ch = c & 7;
+      *reinterpret_cast<u16x8*>(((c >> 9) ? tb : ta) + tile_off(row, ch)) = r[u];
+    }
+  }
+};
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2][2][kTileBytes];  // [buf][K|V]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = p.T / kQBlk;
+  const int qb = CAUSAL ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // heaviest blocks first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int64_t base = (int64_t)b * p.sb + (int64_t)h * p.sh;
+  const int q = qb * kQBlk + wave * 32 + r;
+  u16x8 qf[4];
+  {
+    const u16* qrow = p.q + base + (int64_t)q * p.st;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const u16x8*>(qrow + 16 * s + 8 * hh);
+  }
+  f32x16 oacc[2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) oacc[nb][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int ntiles = CAUSAL ? (qb + 1) * (kQBlk / kTile) : p.T / kTile;
+  Stage stg;
+  stg.load(p.k, p.v, base, p.st, 0);
+  stg.store(smem[0][0], smem[0][1]);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) stg.load(p.k, p.v, base, p.st, (t + 1) * kTile);
+    const unsigned char* Ks = smem[buf][0];
+    const unsigned char* Vs = smem[buf][1];
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) sacc[kb] = mfma32(lds_row8(Ks, kb * 32 + r, 2 * s + hh), qf[s], sacc[kb]);
+    }
+    const int k0 = t * kTile;
+    float mt = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float x = sacc[kb][i] * p.scale_log2;
+        if (CAUSAL && k0 + kb * 32 + acc_row(i, hh) > q) x = -INFINITY;
+        sacc[kb][i] = x;
+        mt = fmaxf(mt, x);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = (m == -INFINITY) ? 0.f : exp2f(m - mn);
+    float ls = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float e = (mn == -INFINITY) ? 0.f : exp2f(sacc[kb][i] - mn);
+        sacc[kb][i] = e;
+        ls += e;
+      }
+    l = l * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[nb][i] *= alpha;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const u16x8 pb = acc_to_op(sacc[ks >> 1], ks & 1);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+        oacc[nb] = mfma32(lds_tr8(Vs, (ks >> 1) * 32 + 16 * (ks & 1), nb * 32, lane), pb, oacc[nb]);
+    }
+    if (t + 1 < ntiles) stg.store(smem[buf ^ 1][0], smem[buf ^ 1][1]);
+    __syncthreads();
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = 1.f / lt;
+  u16* orow = p.out + (int64_t)b * p.ob + (int64_t)h * p.oh + (int64_t)q * p.ot;
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16v<4> o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2b(oacc[nb][4 * g4 + j] * inv);
+      *reinterpret_cast<u16v<4>*>(orow + nb * 32 + 8 * g4 + 4 * hh) = o;
+    }
+  if (hh == 0) p.stat_out[((int64_t)b * p.H + h) * p.T + q] = m + __log2f(lt);
+}
+
+// delta[b, h, t] = sum_d dO * O (fp32); 8 lanes per row
+__global__ void __launch_bounds__(256) attn_bwd_pre_kernel(AttnParams p, int64_t rows) {
+  const int64_t row = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const int c = threadIdx.x & 7;
+  float s = 0.f;
+  if (row < rows) {
+    const int t = (int)(row % p.T);
+    const int64_t bh = row / p.T;
+    const int h = (int)(bh % p.H), b = (int)(bh / p.H);
+    const int64_t off = (int64_t)b * p.ob + (int64_t)h * p.oh + (int64_t)t * p.ot + c * 8;
+    u16x8 d = *reinterpret_cast<const u16x8*>(p.dout + off);
+    u16x8 o = *reinterpret_cast<const u16x8*>(p.o + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += b2f(d[j]) * b2f(o[j]);
+  }
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  if (row < rows && c == 0) p.stat_out[row] = s;
+}
+
+// dK, dV: workgroup = 128 keys (4 waves x 32, key on the lane), loop over 64-query tiles.
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2][2][kTileBytes];  // [buf][Q|dO]
+  __shared__ __attribute__((aligned(16))) float sstat[2][2][kTile];             // [buf][lse|delta]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int kblk = blockIdx.x;  // key blocks near 0 see the most queries: launched first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int64_t base = (int64_t)b * p.sb + (int64_t)h * p.sh;
+  const int64_t obase = (int64_t)b * p.ob + (int64_t)h * p.oh;
+  const int64_t sbase = ((int64_t)b * p.H + h) * p.T;
+  const int key = kblk * kQBlk + wave * 32 + r;
+  u16x8 kf[4], vf[4];
+  {
+    const u16* krow = p.k + base + (int64_t)key * p.st;
+    const u16* vrow = p.v + base + (int64_t)key * p.st;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = *reinterpret_cast<const u16x8*>(krow + 16 * s + 8 * hh);
+      vf[s] = *reinterpret_cast<const u16x8*>(vrow + 16 * s + 8 * hh);
+    }
+  }
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[nb][i] = dv[nb][i] = 0.f;
+  const int t0 = CAUSAL ? kblk * (kQBlk / kTile) : 0;
+  const int t1 = p.T / kTile;
+  // Q (q strides) and dO (o strides) tiles + the tile's lse / delta values
+  u16x8 rg[4];
+  float sv = 0.f;
+  auto load = [&](int t) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = threadIdx.x + 256 * u;
+      const int row = (c >> 3) & 63, ch = c & 7;
+      const int qrow = t * kTile + row;
+      rg[u] = (c >> 9) ? *reinterpret_cast<const u16x8*>(p.dout + obase + (int64_t)qrow * p.ot + ch * 8)
+                       : *reinterpret_cast<const u16x8*>(p.q + base + (int64_t)qrow * p.st + ch * 8);
+    }
+    if (threadIdx.x < 128) sv = (threadIdx.x < 64 ? p.lse : p.delta)[sbase + t * kTile + (threadIdx.x & 63)];
+  };
+  auto store = [&](int bufi) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = threadIdx.x + 256 * u;
+      const int row = (c >> 3) & 63, ch = c & 7;
+      *reinterpret_cast<u16x8*>(smem[bufi][c >> 9] + tile_off(row, ch)) = rg[u];
+    }
+    if (threadIdx.x < 128) sstat[bufi][threadIdx.x >> 6][threadIdx.x & 63] = sv;
+  };
+  if (t0 < t1) {
+    load(t0);
+    store(0);
+  }
+  __syncthreads();
+  for (int t = t0; t < t1; ++t) {
+    const int buf = (t - t0) & 1;
+    if (t + 1 < t1) load(t + 1);
+    const unsigned char* Qs = smem[buf][0];
+    const unsigned char* Ds = smem[buf][1];
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      f32x16 sacc, dpacc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sacc = mfma32(lds_row8(Qs, qs * 32 + r, 2 * s + hh), kf[s], sacc);
+        dpacc = mfma32(lds_row8(Ds, qs * 32 + r, 2 * s + hh), vf[s], dpacc);
+      }
+      // accumulator rows are queries qs*32 + acc_row(i, hh): 4 consecutive per register group
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int qi = qs * 32 + 8 * g4 + 4 * hh;
+        const float4 lse4 = *reinterpret_cast<const float4*>(&sstat[buf][0][qi]);
+        const float4 del4 = *reinterpret_cast<const float4*>(&sstat[buf][1][qi]);
+        const float ls[4] = {lse4.x, lse4.y, lse4.z, lse4.w};
+        const float dl[4] = {del4.x, del4.y, del4.z, del4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * g4 + j;
+          const int query = t * kTile + qi + j;
+          float pv = exp2f(sacc[i] * p.scale_log2 - ls[j]);
+          if (CAUSAL && key > query) pv = 0.f;
+          sacc[i] = pv;
+          dpacc[i] = pv * (dpacc[i] - dl[j]);
+        }
+      }
+#pragma unroll
+      for (int kss = 0; kss < 2; ++kss) {
+        const u16x8 pb = acc_to_op(sacc, kss);
+        const u16x8 db = acc_to_op(dpacc, kss);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          dv[nb] = mfma32(lds_tr8(Ds, qs * 32 + 16 * kss, nb * 32, lane), pb, dv[nb]);
+          dk[nb] = mfma32(lds_tr8(Qs, qs * 32 + 16 * kss, nb * 32, lane), db, dk[nb]);
+        }
+      }
+    }
+    if (t + 1 < t1) store(buf ^ 1);
+    __syncthreads();
+  }
+  u16* dkrow = p.out + base + (int64_t)key * p.st;
+  u16* dvrow = p.out2 + base + (int64_t)key * p.st;
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16v<4> ok, ov;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ok[j] = f2b(dk[nb][4 * g4 + j] * p.scale);
+        ov[j] = f2b(dv[nb][4 * g4 + j]);
+      }
+      *reinterpret_cast<u16v<4>*>(dkrow + nb * 32 + 8 * g4 + 4 * hh) = ok;
+      *reinterpret_cast<u16v<4>*>(dvrow + nb * 32 + 8 * g4 + 4 * hh) = ov;
+    }
+}
+
+// dQ: workgroup = 128 queries (query on the lane), loop over 64-key tiles like the forward.
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2][2][kTileBytes];  // [buf][K|V]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = p.T / kQBlk;
+  const int qb = CAUSAL ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int64_t base = (int64_t)b * p.sb + (int64_t)h * p.sh;
+  const int q = qb * kQBlk + wave * 32 + r;
+  u16x8 qf[4], df[4];
+  {
+    const u16* qrow = p.q + base + (int64_t)q * p.st;
+    const u16* drow = p.dout + (int64_t)b * p.ob + (int64_t)h * p.oh + (int64_t)q * p.ot;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = *reinterpret_cast<const u16x8*>(qrow + 16 * s + 8 * hh);
+      df[s] = *reinterpret_cast<const u16x8*>(drow + 16 * s + 8 * hh);
+    }
+  }
+  const int64_t sidx = ((int64_t)b * p.H + h) * p.T + q;
+  const float lse = p.lse[sidx], del = p.delta[sidx];
+  f32x16 dq[2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[nb][i] = 0.f;
+  const int ntiles = CAUSAL ? (qb + 1) * (kQBlk / kTile) : p.T / kTile;
+  Stage stg;
+  stg.load(p.k, p.v, base, p.st, 0);
+  stg.store(smem[0][0], smem[0][1]);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) stg.load(p.k, p.v, base, p.st, (t + 1) * kTile);
+    const unsigned char* Ks = smem[buf][0];
+    const unsigned char* Vs = smem[buf][1];
+    f32x16 sacc[2], dpacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[kb][i] = dpacc[kb][i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sacc[kb] = mfma32(lds_row8(Ks, kb * 32 + r, 2 * s + hh), qf[s], sacc[kb]);
+        dpacc[kb] = mfma32(lds_row8(Vs, kb * 32 + r, 2 * s + hh), df[s], dpacc[kb]);
+      }
+    }
+    const int k0 = t * kTile;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float pv = exp2f(sacc[kb][i] * p.scale_log2 - lse);
+        if (CAUSAL && k0 + kb * 32 + acc_row(i, hh) > q) pv = 0.f;
+        dpacc[kb][i] = pv * (dpacc[kb][i] - del);
+      }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const u16x8 db = acc_to_op(dpacc[ks >> 1], ks & 1);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+        dq[nb] = mfma32(lds_tr8(Ks, (ks >> 1) * 32 + 16 * (ks & 1), nb * 32, lane), db, dq[nb]);
+    }
+    if (t + 1 < ntiles) stg.store(smem[buf ^ 1][0], smem[buf ^ 1][1]);
+    __syncthreads();
+  }
+  u16* qrow = p.out + base + (int64_t)q * p.st;
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u16v<4> o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2b(dq[nb][4 * g4 + j] * p.scale);
+      *reinterpret_cast<u16v<4>*>(qrow + nb * 32 + 8 * g4 + 4 * hh) = o;
+    }
+}
+
 // ------------------------------------------------------------------------------ host side
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
@@ -657,6 +1095,86 @@ void adamw_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, s
   flush();
 }
 
+// packed qkv [B, T, 3, H, 64] bf16 -> (O [B, T, H, 64], lse [B, H, T] fp32 log2-domain)
+bool attention_supported(const at::Tensor& qkv) {
+  return qkv.dim() == 5 && qkv.size(2) == 3 && qkv.size(4) == kHD && qkv.size(1) % kQBlk == 0 && qkv.size(1) > 0;
+}
+
+AttnParams attn_params(const at::Tensor& qkv, double scale) {
+  AttnParams p{};
+  const int64_t T = qkv.size(1), H = qkv.size(3);
+  const u16* base = (const u16*)qkv.data_ptr();
+  p.q = base;
+  p.k = base + H * kHD;
+  p.v = base + 2 * H * kHD;
+  p.sb = T * 3 * H * kHD;
+  p.st = 3 * H * kHD;
+  p.sh = kHD;
+  p.ob = T * H * kHD;
+  p.ot = H * kHD;
+  p.oh = kHD;
+  p.T = (int)T;
+  p.H = (int)H;
+  p.scale = (float)scale;
+  p.scale_log2 = (float)(scale * 1.4426950408889634);
+  return p;
+}
+
+std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, bool causal, double scale) {
+  check_bf16(qkv, "qkv");
+  TORCH_CHECK(attention_supported(qkv), "attention: qkv must be [B, T, 3, H, 64] with T % 128 == 0");
+  const int64_t B = qkv.size(0), T = qkv.size(1), H = qkv.size(3);
+  auto out = at::empty({B, T, H, kHD}, qkv.options());
+  auto lse = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
+  AttnParams p = attn_params(qkv, scale);
+  p.out = (u16*)out.data_ptr();
+  p.stat_out = lse.data_ptr<float>();
+  dim3 grid((unsigned)(T / kQBlk), (unsigned)H, (unsigned)B);
+  if (causal)
+    hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, stream(), p);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, stream(), p);
+  LAUNCH_CHECK();
+  return {out, lse};
+}
+
+at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& lse,
+                    bool causal, double scale) {
+  check_bf16(dout, "grad");
+  check_bf16(qkv, "qkv");
+  check_bf16(out, "out");
+  TORCH_CHECK(dout.sizes() == out.sizes(), "attention: grad shape mismatch");
+  const int64_t B = qkv.size(0), T = qkv.size(1), H = qkv.size(3);
+  auto dqkv = at::empty_like(qkv);
+  auto delta = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
+  AttnParams p = attn_params(qkv, scale);
+  p.o = (const u16*)out.data_ptr();
+  p.dout = (const u16*)dout.data_ptr();
+  p.stat_out = delta.data_ptr<float>();
+  const int64_t rows = B * H * T;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, stream(), p, rows);
+  LAUNCH_CHECK();
+  p.lse = lse.data_ptr<float>();
+  p.delta = delta.data_ptr<float>();
+  u16* dbase = (u16*)dqkv.data_ptr();
+  dim3 grid((unsigned)(T / kQBlk), (unsigned)H, (unsigned)B);
+  p.out = dbase + H * kHD;       // dK slot of the packed gradient
+  p.out2 = dbase + 2 * H * kHD;  // dV slot
+  if (causal)
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, grid, dim3(256), 0, stream(), p);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, grid, dim3(256), 0, stream(), p);
+  LAUNCH_CHECK();
+  p.out = dbase;  // dQ slot
+  p.out2 = nullptr;
+  if (causal)
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, grid, dim3(256), 0, stream(), p);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, grid, dim3(256), 0, stream(), p);
+  LAUNCH_CHECK();
+  return dqkv;
+}
+
 // ------------------------------------------------------------------------------ autograd
 // C++ autograd nodes: one Python -> C++ call per op and no Python in the backward pass (a
 // Python autograd.Function costs tens of microseconds of CPU per call, which shows on a
@@ -713,6 +1231,27 @@ struct CrossEntropyFn : public torch::autograd::Function<CrossEntropyFn> {
   }
 };
 
+struct AttentionFn : public torch::autograd::Function<AttentionFn> {
+  static at::Tensor forward(AutogradContext* ctx, const at::Tensor& qkv, bool causal, double scale) {
+    auto qc = qkv.contiguous();
+    auto r = attn_fwd(qc, causal, scale);
+    ctx->save_for_backward({qc, r[0], r[1]});
+    ctx->saved_data["causal"] = causal;
+    ctx->saved_data["scale"] = scale;
+    return r[0];
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto s = ctx->get_saved_variables();
+    auto d = attn_bwd(grads[0].contiguous(), s[0], s[1], s[2], ctx->saved_data["causal"].toBool(),
+                      ctx->saved_data["scale"].toDouble());
+    return {d, at::Tensor(), at::Tensor()};
+  }
+};
+
+at::Tensor attention(const at::Tensor& qkv, bool causal, double scale) {
+  return AttentionFn::apply(qkv, causal, scale);
+}
+
 at::Tensor rms_norm(const at::Tensor& x, const at::Tensor& w, double eps) { return RMSNormFn::apply(x, w, eps); }
 at::Tensor swiglu(const at::Tensor& h) { return SwiGLUFn::apply(h); }
 at::Tensor cross_entropy(const at::Tensor& logits, const at::Tensor& tgt, int64_t ignore_index) {
@@ -729,6 +1268,10 @@ PYBIND11_MODULE(_fused_ops, m) {
   m.def("swiglu", &swiglu);
   m.def("cross_entropy", &cross_entropy);
   m.def("adamw_step", &adamw_step);
+  m.def("attention", &attention);
+  m.def("attention_supported", &attention_supported);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
   // raw kernels (tests / custom graphs)
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);

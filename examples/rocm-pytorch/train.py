@@ -9,11 +9,16 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-try:  # gfx950 fused HIP kernels (RMSNorm, SwiGLU, cross-entropy) shipped with devspace_amd
-    from devspace_amd.ops.fused import AdamW, RMSNorm, cross_entropy, swiglu
+try:  # gfx950 HIP kernels shipped with devspace_amd (attention, RMSNorm, SwiGLU, CE, AdamW)
+    from devspace_amd.ops.fused import AdamW, RMSNorm, attention, cross_entropy, swiglu
 except ImportError:  # plain PyTorch when the package is not in the image
     RMSNorm = nn.RMSNorm
     AdamW = None
+
+    def attention(qkv, causal=True):
+        q, k, v = qkv.unbind(2)
+        o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=causal)
+        return o.transpose(1, 2)
 
     def swiglu(h):
         g, u = h.chunk(2, dim=-1)
@@ -46,9 +51,9 @@ class Block(nn.Module):
 
     def forward(self, x):
         b, t, d = x.shape
-        q, k, v = self.qkv(self.norm1(x)).view(b, t, 3, self.heads, d // self.heads).unbind(2)
-        a = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=True)
-        x = x + self.proj(a.transpose(1, 2).reshape(b, t, d))
+        qkv = self.qkv(self.norm1(x)).view(b, t, 3, self.heads, d // self.heads)
+        a = attention(qkv, causal=True)  # [b, t, heads, head_dim]
+        x = x + self.proj(a.reshape(b, t, d))
         return x + self.down(swiglu(self.up(self.norm2(x))))
 
 

@@ -77,7 +77,19 @@ def op_cases(dev):
     opt_f = fused.AdamW(params, lr=1e-4)
     opt_e = torch.optim.AdamW(params_b, lr=1e-4, fused=True)
 
-    return {"adamw step [67M bf16 params]": (opt_f.step, opt_e.step),
+    qkv = torch.randn(8, 512, 3, 16, 64, device=dev).bfloat16().requires_grad_()
+    dattn = torch.randn(8, 512, 16, 64, device=dev).bfloat16()
+
+    def attn_fused():
+        fused.attention(qkv, causal=True).backward(dattn)
+
+    def attn_eager():
+        q, k, v = qkv.unbind(2)
+        o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=True)
+        o.transpose(1, 2).reshape(8, 512, 1024).backward(dattn.view(8, 512, 1024))
+
+    return {"attention fwd+bwd [8x512, 16 heads x 64]": (attn_fused, attn_eager),
+            "adamw step [67M bf16 params]": (opt_f.step, opt_e.step),
             "rmsnorm fwd+bwd [4096x1024]": (rms_fused, rms_eager),
             "swiglu fwd+bwd [4096x2x2730]": (swiglu_fused, swiglu_eager),
             "cross_entropy fwd+bwd [4096x8192]": (ce_fused, ce_eager)}
@@ -103,6 +115,7 @@ def step_case(dev):
         return F.silu(g) * u
 
     m_eager.swiglu = sw
+    m_eager.AdamW = None  # torch.optim.AdamW(fused=True)
     m_eager.cross_entropy = lambda lg, tg: F.cross_entropy(lg.float(), tg)
     sf, se = m_fused.setup(Ctx()), m_eager.setup(Ctx())
     return ("TinyLM train step (4x1024, B8xT512)", (lambda: m_fused.step(Ctx(), sf), lambda: m_eager.step(Ctx(), se)))

@@ -95,6 +95,39 @@ def test_cross_entropy_fwd_bwd(rows, vocab, ignore):
     torch.testing.assert_close(logits.grad.float() * n, lr.grad * n, atol=2e-3, rtol=2e-2)
 
 
+def _ref_attention(qkv, causal):
+    q, k, v = qkv.float().unbind(2)
+    o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=causal)
+    return o.transpose(1, 2)
+
+
+def test_attention_cpu_fallback_matches_sdpa():
+    torch.manual_seed(5)
+    qkv = torch.randn(2, 16, 3, 2, 8)
+    torch.testing.assert_close(fused.attention(qkv, causal=True), _ref_attention(qkv, True))
+
+
+@gpu
+@pytest.mark.parametrize("b,t,h,causal", [(2, 256, 3, True), (2, 256, 3, False), (8, 512, 16, True), (1, 1024, 2, True)])
+def test_attention_fwd_bwd(b, t, h, causal):
+    dev = _cuda()
+    torch.manual_seed(6)
+    qkv = torch.randn(b, t, 3, h, 64, device=dev).bfloat16().requires_grad_()
+    assert fused.ext().attention_supported(qkv)
+    o = fused.attention(qkv, causal=causal)
+    assert o.shape == (b, t, h, 64) and o.is_contiguous()
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr = qkv.detach().float().requires_grad_()
+    orf = _ref_attention(qr, causal)
+    orf.backward(do.float())
+    torch.testing.assert_close(o.float(), orf, atol=2e-2, rtol=2e-2)
+    for i, name in enumerate("qkv"):
+        g, gr = qkv.grad[:, :, i].float(), qr.grad[:, :, i]
+        err = (g - gr).abs().max() / gr.abs().max()
+        assert err < 3e-2, (name, float(err))
+
+
 def _adamw_pair(dev, dtype):
     torch.manual_seed(4)
     shapes = [(300, 64), (1024,), (7, 3), (8192, 16)]
