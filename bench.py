@@ -414,6 +414,7 @@ def main():
         "deploy_warm_wall_clock_s": None if not deploy else round(deploy["warm_s"], 3),
         "gpu_pod_deploy_s": round(result["pod_deploy_s"], 3),
         "deploy_cold_phases_ms": None if not deploy else deploy.get("cold_phases_ms"),
+        "deploy_host_runtime_prewarmed": None if not deploy else deploy.get("host_runtime_prewarmed"),
     }
     parts = {k: round(_pct(v, 0.5), 2) for k, v in result.get("parts", {}).items() if v}
     if parts:

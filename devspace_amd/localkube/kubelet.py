@@ -155,6 +155,16 @@ class Kubelet:
 
     # ------------------------------------------------------------ events
 
+    def _trace(self, what, **kw):
+        """Kubelet-side timings into LOCALKUBE_TRACE (same file as the store's object events)."""
+        path = os.environ.get("LOCALKUBE_TRACE")
+        if path:
+            rec = {"t_ms": round(time.time() * 1000.0, 2), "ev": what, "res": "kubelet", "name": kw.pop("pod", ""),
+                   "phase": None, "ready": None}
+            rec.update({k: round(v, 2) if isinstance(v, float) else v for k, v in kw.items()})
+            with open(path, "a") as f:
+                f.write(json.dumps(rec) + "\n")
+
     def event(self, obj, reason, message, etype="Normal"):
         md = obj["metadata"]
         ns = md.get("namespace", "default")
@@ -257,7 +267,9 @@ class Kubelet:
     # ------------------------------------------------------------ pods
 
     async def reconcile_pods(self):
+        """Returns True when a pod status was written (workload status needs a refresh)."""
         seen = set()
+        changed = False
         for pod in self.store.list("", "pods"):
             md = pod["metadata"]
             key = (md["namespace"], md["name"])
@@ -270,10 +282,11 @@ class Kubelet:
                 rt = self._admit(pod)
                 if rt is None:
                     continue
-            await self._sync_containers(rt, pod)
+            changed |= await self._sync_containers(rt, pod)
         for key in list(self.pods):
             if key not in seen:  # removed from the store without graceful deletion
                 await self._kill_pod(self.pods.pop(key), 0)
+        return changed
 
     def _admit(self, pod):
         md = pod["metadata"]
@@ -429,6 +442,7 @@ class Kubelet:
             if c.fatal:
                 continue
             if c.proc is None and c.started_at is None and c.restarts == 0 and not c.next_start:
+                t0 = time.perf_counter()
                 reason, msg = self._prepare_rootfs(rt, c, pod)
                 if reason:
                     c.state = {"waiting": {"reason": reason, "message": msg}}
@@ -436,7 +450,10 @@ class Kubelet:
                     self.event(pod, "Failed", msg, "Warning")
                     changed = True
                     continue
+                t1 = time.perf_counter()
                 await self._start(rt, c, pod)
+                self._trace("container_start", pod=rt.name, container=name, rootfs_ms=(t1 - t0) * 1e3,
+                            exec_ms=(time.perf_counter() - t1) * 1e3)
                 changed = True
             elif c.proc is not None and c.proc.returncode is not None:
                 code = c.proc.returncode
@@ -460,6 +477,8 @@ class Kubelet:
                 changed = True
         if changed or not (pod.get("status") or {}).get("containerStatuses"):
             self._write_status(rt, pod)
+            return True
+        return False
 
     def _write_status(self, rt, pod):
         statuses = []
@@ -506,6 +525,12 @@ class Kubelet:
                 except ProcessLookupError:
                     pass
                 await p.wait()
+        for c in rt.containers.values():  # drain the log pumps so no pipe outlives the pod
+            if getattr(c, "pump", None) is not None and not c.pump.done():
+                try:
+                    await asyncio.wait_for(asyncio.shield(c.pump), timeout=0.5)
+                except (asyncio.TimeoutError, asyncio.CancelledError):
+                    c.pump.cancel()
         self.gpus_free.extend(rt.gpus)
         self.gpus_free.sort()
         rt.gpus = []
@@ -537,15 +562,34 @@ class Kubelet:
         return rt, rt.containers.get(name)
 
     async def run(self):
+        """Reconcile loop: runs on every create/replace/delete in the store (no polling delay
+        between `helm install` and the pod starting) and at least every 50 ms (process exits,
+        restart back-offs). Workload status is refreshed after the pods in the same pass, so a
+        Deployment reports ready replicas as soon as its pod runs."""
         self.register_node()
-        while not self._stop:
-            try:
-                self.reconcile_workloads()
-                self.reconcile_pvcs()
-                await self.reconcile_pods()
-            except Exception as e:  # keep the node alive; surface in the log
-                print(f"[localkube] reconcile error: {e!r}", flush=True)
-            await asyncio.sleep(0.05)
+        loop = asyncio.get_running_loop()
+        wake = asyncio.Event()
+
+        def waker(_key):
+            loop.call_soon_threadsafe(wake.set)
+
+        self.store.wakers.append(waker)
+        try:
+            while not self._stop:
+                wake.clear()
+                try:
+                    self.reconcile_workloads()
+                    self.reconcile_pvcs()
+                    if await self.reconcile_pods():
+                        self.reconcile_workloads()
+                except Exception as e:  # keep the node alive; surface in the log
+                    print(f"[localkube] reconcile error: {e!r}", flush=True)
+                try:
+                    await asyncio.wait_for(wake.wait(), 0.05)
+                except asyncio.TimeoutError:
+                    pass
+        finally:
+            self.store.wakers.remove(waker)
 
     async def shutdown(self):
         self._stop = True

@@ -5,8 +5,11 @@ from __future__ import annotations
 import copy
 import datetime
 import itertools
+import json
+import os
 import re
 import threading
+import time
 import uuid
 
 CLUSTER_SCOPED = {"namespaces", "nodes", "persistentvolumes", "clusterroles", "clusterrolebindings", "storageclasses",
@@ -100,15 +103,47 @@ def merge_patch(target, patch):
     return out
 
 
+class _Tracer:
+    """LOCALKUBE_TRACE=<file>: one JSON line per object event with a ms wall-clock timestamp
+    (where a cluster-side wait goes: pod created -> started -> ready -> workload ready)."""
+
+    def __init__(self, path):
+        self.f = open(path, "a", buffering=1)
+
+    def __call__(self, ev, key, obj):
+        if key[1] in ("events", "secrets", "configmaps", "serviceaccounts"):
+            return
+        st = obj.get("status") or {}
+        rec = {"t_ms": round(time.time() * 1000.0, 2), "ev": ev, "res": key[1], "name": key[3],
+               "phase": st.get("phase"), "ready": st.get("readyReplicas")}
+        self.f.write(json.dumps(rec) + "\n")
+
+
 class Store:
     def __init__(self):
         self.lock = threading.RLock()
         self.objs = {}  # (group, resource, ns, name) -> obj
         self.rv = itertools.count(1)
         self.listeners = []  # callables(event, key, obj)
+        # callables(key) run on changes a controller must act on (creates, spec replaces,
+        # deletes) but not on status writes, so a controller's own status updates never
+        # re-trigger it
+        self.wakers = []
+        trace = os.environ.get("LOCALKUBE_TRACE")
+        if trace:
+            self.listeners.append(_Tracer(trace))
 
     def _key(self, group, resource, ns, name):
         return (group, resource, "" if resource in CLUSTER_SCOPED else (ns or "default"), name)
+
+    def _wake(self, key):
+        if key[1] == "events":
+            return
+        for fn in list(self.wakers):
+            try:
+                fn(key)
+            except Exception:  # pragma: no cover
+                pass
 
     def _notify(self, ev, key, obj):
         for fn in list(self.listeners):
@@ -171,6 +206,7 @@ class Store:
                 obj.setdefault("apiVersion", api_version)
             self.objs[key] = obj
             self._notify("ADDED", key, obj)
+            self._wake(key)
             return copy.deepcopy(obj)
 
     def replace(self, group, resource, ns, name, obj):
@@ -199,6 +235,7 @@ class Store:
             obj.setdefault("apiVersion", old.get("apiVersion"))
             self.objs[key] = obj
             self._notify("MODIFIED", key, obj)
+            self._wake(key)
             return copy.deepcopy(obj)
 
     def update_status(self, group, resource, ns, name, status):
@@ -240,6 +277,7 @@ class Store:
             if o is None:
                 raise ApiError(404, "NotFound", f'{resource} "{name}" not found')
             self._notify("DELETED", key, o)
+            self._wake(key)
             return o
 
     def mark_deleting(self, group, resource, ns, name):
@@ -252,6 +290,7 @@ class Store:
             o["metadata"].setdefault("deletionTimestamp", now_rfc3339())
             o["metadata"]["resourceVersion"] = str(next(self.rv))
             self._notify("MODIFIED", key, o)
+            self._wake(key)
             return copy.deepcopy(o)
 
     def owned_by(self, uid):

@@ -205,6 +205,15 @@ def worker_main(args) -> int:
 
         backend = "nccl" if device.type == "cuda" else "gloo"  # nccl == RCCL on ROCm
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    if device.type == "cuda" and args.gemm_tuning != "off":
+        try:
+            from devspace_amd.ops import gemm_tuning  # noqa: WPS433
+
+            rep = gemm_tuning.apply(args.gemm_tuning, device)
+        except ImportError:  # runner vendored without the package
+            rep = {"mode": args.gemm_tuning, "active": False, "entries": 0}
+        if rank == 0:
+            _log(f"gemm tuning mode={rep['mode']} active={rep['active']} entries={rep['entries']}")
     ctx = Context(rank, world, local_rank, device)
     entry = os.path.abspath(args.entry)
     watch_dir = os.path.abspath(args.watch or os.path.dirname(entry))
@@ -406,7 +415,8 @@ def supervisor_main(args) -> int:
 
 
 def _forward(args):
-    out = ["--watch", args.watch or "", "--log-every", str(args.log_every), "--max-steps", str(args.max_steps)]
+    out = ["--watch", args.watch or "", "--log-every", str(args.log_every), "--max-steps", str(args.max_steps),
+           "--gemm-tuning", args.gemm_tuning]
     if not args.train:
         out.append("--no-train")
     return out + [args.entry]
@@ -424,6 +434,9 @@ def parse_args(argv=None):
     p.add_argument("--no-train", dest="train", action="store_false", help="only run a step after each edit")
     p.add_argument("--restart", action="store_true", help="cold-restart on every change (reference behaviour)")
     p.add_argument("--keep-alive", action="store_true", help="in --restart mode, wait for edits after exit")
+    p.add_argument("--gemm-tuning", default=os.environ.get("DEVSPACE_GEMM_TUNING", "off"),
+                   choices=("off", "shipped", "online"),
+                   help="TunableOp GEMM selection (devspace_amd/ops/gemm_tuning.py)")
     p.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args(argv)
 

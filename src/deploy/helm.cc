@@ -244,6 +244,9 @@ static std::string object_key(const Value& o) {
 
 std::string Client::wait_ready(const std::vector<Value>& objs, const std::string& ns, int timeout_s) {
   auto t0 = std::chrono::steady_clock::now();
+  // Back-off polling: a pod that is up within a few ms is seen within a few ms, a slow rollout
+  // costs at most one GET per object every 250 ms (the reference polls through Tiller).
+  int delay_ms = 5;
   while (true) {
     std::string pending;
     for (auto& o : objs) {
@@ -287,7 +290,8 @@ std::string Client::wait_ready(const std::vector<Value>& objs, const std::string
     if (pending.empty()) return "";
     auto el = std::chrono::duration_cast<std::chrono::seconds>(std::chrono::steady_clock::now() - t0).count();
     if (el >= timeout_s) return "timed out waiting for the condition (" + pending + ")";
-    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
+    delay_ms = std::min(250, delay_ms * 3 / 2 + 1);
   }
 }
 

@@ -190,3 +190,32 @@ def test_tinylm_step_uses_fused_ops_and_trains():
     state = mod.setup(Ctx())
     losses = [mod.step(Ctx(), state)["loss"] for _ in range(8)]
     assert losses[-1] < losses[0], losses
+
+
+def test_gemm_tuning_modes_cpu():
+    from devspace_amd.ops import gemm_tuning
+
+    assert gemm_tuning.apply("off")["active"] is False
+    # no GPU here: every mode reports inactive instead of touching TunableOp
+    assert gemm_tuning.apply("shipped")["active"] is (torch.cuda.is_available() and torch.version.hip is not None
+                                                     and gemm_tuning._arch(0) == "gfx950")
+    with pytest.raises(ValueError):
+        gemm_tuning.apply("sometimes")
+    assert gemm_tuning._count(gemm_tuning.SHIPPED) > 0
+
+
+@gpu
+def test_gemm_tuning_shipped_table_loads_on_gfx950():
+    _cuda()
+    from devspace_amd.ops import gemm_tuning
+
+    if gemm_tuning._arch(0) != "gfx950":
+        pytest.skip("table is for gfx950")
+    rep = gemm_tuning.apply("shipped")
+    try:
+        assert rep["active"] and rep["entries"] >= 10
+        a = torch.randn(4096, 1024, device="cuda").bfloat16()
+        b = torch.randn(1024, 3072, device="cuda").bfloat16()
+        torch.testing.assert_close((a @ b).float(), a.float() @ b.float(), atol=0.5, rtol=2e-2)
+    finally:
+        torch.cuda.tunable.enable(False)
