@@ -508,17 +508,12 @@ __device__ __forceinline__ u16x8 lds_tr8(const unsigned char* tile, int r0, int 
   lds_u8* base = (lds_u8*)tile;
   s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off1));
   s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off2));
-  u16x8 o;
-  o[0] = a[0];
-  o[1] = a[1];
-  o[2] = a[2];
-  o[3] = a[3];
-  o[4] = b[0];
-  o[5] = b[1];
-  o[6] = b[2];
-  o[7] = b[3];
-  return o;
+  return __builtin_bit_cast(u16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
+
+// 2^x on the transcendental unit (v_exp_f32): no denormal-range fix-up (exp2f adds a compare,
+// a select and a v_ldexp per call); exp2(-inf) = 0, which the masked scores rely on.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // accumulator registers 8s .. 8s+7 as a bf16 MFMA operand (k-step s of the accumulator's rows)
 __device__ __forceinline__ u16x8 acc_to_op(const f32x16& acc, int s) {
@@ -580,7 +575,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
   const int qb = CAUSAL ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // heaviest blocks first
   const int h = blockIdx.y, b = blockIdx.z;
   const int64_t base = (int64_t)b * p.sb + (int64_t)h * p.sh;
-  const int q = qb * kQBlk + wave * 32 + r;
+  const int qw0 = qb * kQBlk + wave * 32;  // first query of this wave
+  const int q = qw0 + r;
   u16x8 qf[4];
   {
     const u16* qrow = p.q + base + (int64_t)q * p.st;
@@ -603,49 +599,59 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnParams p) {
     if (t + 1 < ntiles) stg.load(p.k, p.v, base, p.st, (t + 1) * kTile);
     const unsigned char* Ks = smem[buf][0];
     const unsigned char* Vs = smem[buf][1];
-    f32x16 sacc[2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) sacc[kb] = mfma32(lds_row8(Ks, kb * 32 + r, 2 * s + hh), qf[s], sacc[kb]);
-    }
     const int k0 = t * kTile;
-    float mt = -INFINITY;
+    // wave-uniform causal classes of this tile: all keys after all of the wave's queries
+    // (nothing to do), straddling the diagonal (mask), or fully visible (no per-element test)
+    if (!(CAUSAL && k0 > qw0 + 31)) {
+      f32x16 sacc[2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float x = sacc[kb][i] * p.scale_log2;
-        if (CAUSAL && k0 + kb * 32 + acc_row(i, hh) > q) x = -INFINITY;
-        sacc[kb][i] = x;
-        mt = fmaxf(mt, x);
+        for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
+      // k-step outer, key block inner: two independent MFMA chains issue back to back
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) sacc[kb] = mfma32(lds_row8(Ks, kb * 32 + r, 2 * s + hh), qf[s], sacc[kb]);
+      if (CAUSAL && k0 + kTile - 1 > qw0) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (k0 + kb * 32 + acc_row(i, hh) > q) sacc[kb][i] = -INFINITY;
       }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt);
-    const float alpha = (m == -INFINITY) ? 0.f : exp2f(m - mn);
-    float ls = 0.f;
+      // raw-score max (scale > 0), then p = 2^(s * scale_log2 - m) as one FMA + v_exp. Tile 0
+      // always holds key 0, so m is finite from the first tile on and no -inf guards are needed.
+      float mt = -INFINITY;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float e = (mn == -INFINITY) ? 0.f : exp2f(sacc[kb][i] - mn);
-        sacc[kb][i] = e;
-        ls += e;
-      }
-    l = l * alpha + ls;
-    m = mn;
+        for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[kb][i]);
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m, mt * p.scale_log2);
+      const float alpha = fast_exp2(m - mn);
+      float ls = 0.f;
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[nb][i] *= alpha;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const u16x8 pb = acc_to_op(sacc[ks >> 1], ks & 1);
+        for (int i = 0; i < 16; ++i) {
+          const float e = fast_exp2(__builtin_fmaf(sacc[kb][i], p.scale_log2, -mn));
+          sacc[kb][i] = e;
+          ls += e;
+        }
+      l = l * alpha + ls;
+      m = mn;
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb)
-        oacc[nb] = mfma32(lds_tr8(Vs, (ks >> 1) * 32 + 16 * (ks & 1), nb * 32, lane), pb, oacc[nb]);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[nb][i] *= alpha;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const u16x8 pb = acc_to_op(sacc[ks >> 1], ks & 1);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          oacc[nb] = mfma32(lds_tr8(Vs, (ks >> 1) * 32 + 16 * (ks & 1), nb * 32, lane), pb, oacc[nb]);
+      }
     }
     if (t + 1 < ntiles) stg.store(smem[buf ^ 1][0], smem[buf ^ 1][1]);
     __syncthreads();
@@ -698,7 +704,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnParams p) {
   const int64_t base = (int64_t)b * p.sb + (int64_t)h * p.sh;
   const int64_t obase = (int64_t)b * p.ob + (int64_t)h * p.oh;
   const int64_t sbase = ((int64_t)b * p.H + h) * p.T;
-  const int key = kblk * kQBlk + wave * 32 + r;
+  const int kw0 = kblk * kQBlk + wave * 32;  // first key of this wave
+  const int key = kw0 + r;
   u16x8 kf[4], vf[4];
   {
     const u16* krow = p.k + base + (int64_t)key * p.st;
@@ -751,6 +758,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnParams p) {
     const unsigned char* Ds = smem[buf][1];
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
+      const int qa = t * kTile + qs * 32;  // first query of this 32-query slice
+      if (CAUSAL && kw0 > qa + 31) continue;  // every key of the wave after every query: P = 0
+      const bool diag = CAUSAL && kw0 + 31 > qa;
       f32x16 sacc, dpacc;
 #pragma unroll
       for (int i = 0; i < 16; ++i) sacc[i] = dpacc[i] = 0.f;
@@ -770,9 +780,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnParams p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * g4 + j;
-          const int query = t * kTile + qi + j;
-          float pv = exp2f(sacc[i] * p.scale_log2 - ls[j]);
-          if (CAUSAL && key > query) pv = 0.f;
+          float pv = fast_exp2(__builtin_fmaf(sacc[i], p.scale_log2, -ls[j]));
+          if (diag && key > t * kTile + qi + j) pv = 0.f;
           sacc[i] = pv;
           dpacc[i] = pv * (dpacc[i] - dl[j]);
         }
@@ -818,7 +827,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnParams p) {
   const int qb = CAUSAL ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
   const int h = blockIdx.y, b = blockIdx.z;
   const int64_t base = (int64_t)b * p.sb + (int64_t)h * p.sh;
-  const int q = qb * kQBlk + wave * 32 + r;
+  const int qw0 = qb * kQBlk + wave * 32;
+  const int q = qw0 + r;
   u16x8 qf[4], df[4];
   {
     const u16* qrow = p.q + base + (int64_t)q * p.st;
@@ -846,32 +856,36 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnParams p) {
     if (t + 1 < ntiles) stg.load(p.k, p.v, base, p.st, (t + 1) * kTile);
     const unsigned char* Ks = smem[buf][0];
     const unsigned char* Vs = smem[buf][1];
-    f32x16 sacc[2], dpacc[2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[kb][i] = dpacc[kb][i] = 0.f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sacc[kb] = mfma32(lds_row8(Ks, kb * 32 + r, 2 * s + hh), qf[s], sacc[kb]);
-        dpacc[kb] = mfma32(lds_row8(Vs, kb * 32 + r, 2 * s + hh), df[s], dpacc[kb]);
-      }
-    }
     const int k0 = t * kTile;
+    if (!(CAUSAL && k0 > qw0 + 31)) {  // same wave-uniform tile classes as the forward
+      const bool diag = CAUSAL && k0 + kTile - 1 > qw0;
+      f32x16 sacc[2], dpacc[2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float pv = exp2f(sacc[kb][i] * p.scale_log2 - lse);
-        if (CAUSAL && k0 + kb * 32 + acc_row(i, hh) > q) pv = 0.f;
-        dpacc[kb][i] = pv * (dpacc[kb][i] - del);
+        for (int i = 0; i < 16; ++i) sacc[kb][i] = dpacc[kb][i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          sacc[kb] = mfma32(lds_row8(Ks, kb * 32 + r, 2 * s + hh), qf[s], sacc[kb]);
+          dpacc[kb] = mfma32(lds_row8(Vs, kb * 32 + r, 2 * s + hh), df[s], dpacc[kb]);
+        }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float pv = fast_exp2(__builtin_fmaf(sacc[kb][i], p.scale_log2, -lse));
+          if (diag && k0 + kb * 32 + acc_row(i, hh) > q) pv = 0.f;
+          dpacc[kb][i] = pv * (dpacc[kb][i] - del);
+        }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const u16x8 db = acc_to_op(dpacc[ks >> 1], ks & 1);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          dq[nb] = mfma32(lds_tr8(Ks, (ks >> 1) * 32 + 16 * (ks & 1), nb * 32, lane), db, dq[nb]);
       }
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const u16x8 db = acc_to_op(dpacc[ks >> 1], ks & 1);
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb)
-        dq[nb] = mfma32(lds_tr8(Ks, (ks >> 1) * 32 + 16 * (ks & 1), nb * 32, lane), db, dq[nb]);
     }
     if (t + 1 < ntiles) stg.store(smem[buf ^ 1][0], smem[buf ^ 1][1]);
     __syncthreads();

@@ -333,6 +333,16 @@ def worker_main(args) -> int:
     return 0
 
 
+def _free_port() -> int:
+    """An OS-assigned free TCP port on 127.0.0.1 for the group's rendezvous (never a fixed
+    range: the pod may itself run under a torchrun whose master port is in use)."""
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def _spawn_group(args, port):
     procs = []
     for r in range(max(1, args.nproc)):
@@ -371,7 +381,7 @@ def restart_main(args) -> int:
     edit kills the process group and cold-starts it. Kept as the reference-equivalent baseline."""
     watch_dir = os.path.abspath(args.watch or os.path.dirname(os.path.abspath(args.entry)))
     watcher = make_watcher(watch_dir)
-    port = args.port or (29500 + os.getpid() % 1000)
+    port = args.port or _free_port()
     procs = _spawn_group(args, port)
     try:
         while True:
@@ -379,7 +389,7 @@ def restart_main(args) -> int:
             if changed:
                 _log(f"change detected ({len(changed)} files), restarting")
                 _stop_group(procs)
-                port += 1
+                port = port + 1 if args.port else _free_port()
                 procs = _spawn_group(args, port)
             elif all(p.poll() is not None for p in procs) and not args.keep_alive:
                 return max(p.returncode for p in procs)
@@ -398,7 +408,7 @@ def supervisor_main(args) -> int:
         os.environ.setdefault("WORLD_SIZE", "1")
         os.environ.setdefault("LOCAL_RANK", "0")
         return worker_main(args)
-    port = args.port or (29500 + os.getpid() % 1000)
+    port = args.port or _free_port()
     restarts = 0
     while True:
         procs = _spawn_group(args, port)
@@ -411,7 +421,7 @@ def supervisor_main(args) -> int:
             return max(codes)
         restarts += 1
         _log(f"worker exited with {codes}; restarting process group ({restarts}/{args.max_restarts})")
-        port += 1
+        port = port + 1 if args.port else _free_port()
 
 
 def _forward(args):

@@ -21,10 +21,11 @@ def _tiny_copy(tmp_path):
     return p
 
 
-def _run_reload(tmp_path, extra_env=None):
+def _run_reload(tmp_path, extra_env=None, nproc=1):
     p = _tiny_copy(tmp_path)
     env = dict(os.environ, PYTHONPATH=ROOT, **(extra_env or {}))
-    proc = subprocess.Popen([sys.executable, "-u", "-m", "devspace_amd.runner", "--watch", str(tmp_path), str(p)],
+    proc = subprocess.Popen([sys.executable, "-u", "-m", "devspace_amd.runner", "--nproc", str(nproc), "--watch",
+                             str(tmp_path), str(p)],
                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, text=True)
     lines = []
     try:
@@ -54,7 +55,7 @@ def _run_reload(tmp_path, extra_env=None):
                 break
         assert any("reload failed" in l for l in lines)
         assert proc.poll() is None
-        return reload_line[0]
+        return reload_line[0] + "".join(l for l in lines if "started gen=1" in l)
     finally:
         proc.terminate()
         proc.wait(10)
@@ -63,6 +64,13 @@ def _run_reload(tmp_path, extra_env=None):
 def test_runner_hot_reload_cpu(tmp_path):
     line = _run_reload(tmp_path, {"HIP_VISIBLE_DEVICES": "-1", "CUDA_VISIBLE_DEVICES": "-1"})
     assert "gen=2" in line
+
+
+def test_runner_hot_reload_two_ranks_cpu(tmp_path):
+    """The N>1 path of the pod (one process per GPU, DDP, generation agreement by all-reduce),
+    rehearsed with two gloo ranks on the CPU."""
+    line = _run_reload(tmp_path, {"HIP_VISIBLE_DEVICES": "-1", "CUDA_VISIBLE_DEVICES": "-1"}, nproc=2)
+    assert "gen=2" in line and "world=2" in line
 
 
 @pytest.mark.gpu
