@@ -2,6 +2,7 @@
 
     from devspace_amd.ops import fused
     norm = fused.RMSNorm(dim)             # drop-in for nn.RMSNorm
+    x, h = fused.add_rms_norm(x, delta, norm.weight)  # x += delta; h = norm(x), one kernel
     y = fused.swiglu(h)                   # silu(h[..., :H]) * h[..., H:]
     loss = fused.cross_entropy(logits, t) # mean CE on bf16 logits [N, V]
 
@@ -51,6 +52,20 @@ def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float | None = None) ->
     if _use_hip(x) and weight.dtype == torch.bfloat16 and ext().rmsnorm_supported(x.shape[-1]):
         return ext().rms_norm(x, weight, float(eps))
     return F.rms_norm(x, (x.shape[-1],), weight, eps)
+
+
+def add_rms_norm(x: torch.Tensor, delta: torch.Tensor, weight: torch.Tensor, eps: float | None = None):
+    """Residual add fused into the following RMSNorm: returns (s, y) with s = x + delta and
+    y = rms_norm(s) * weight. On the GPU one kernel each way (no separate add kernel forward,
+    no gradient-accumulation add backward)."""
+    if eps is None:
+        eps = torch.finfo(x.dtype).eps
+    if (_use_hip(x) and delta.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and delta.shape == x.shape
+            and ext().rmsnorm_supported(x.shape[-1])):
+        s, y = ext().add_rms_norm(x, delta, weight, float(eps))
+        return s, y
+    s = x + delta
+    return s, F.rms_norm(s, (s.shape[-1],), weight, eps)
 
 
 class RMSNorm(nn.Module):

@@ -66,8 +66,11 @@ __device__ __forceinline__ void wave_lse(float& m, float& s) {
 // One wave per row; lane l owns 16-byte vectors l, l+64, ... (VPL of them, the last ones
 // masked when D/8 is not a multiple of 64) and keeps them in registers between the sum of
 // squares and the scaled store, so x is read once.
-template <int VPL>
-__global__ void __launch_bounds__(kBlock) rmsnorm_fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ w,
+// RES: fused residual add first, s = bf16(x + delta) is written to `sum` and normalised
+// (the transformer's `x = x + f(x); h = norm(x)` in one pass instead of an add kernel + norm).
+template <int VPL, bool RES>
+__global__ void __launch_bounds__(kBlock) rmsnorm_fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ delta,
+                                                            const u16* __restrict__ w, u16* __restrict__ sum,
                                                             u16* __restrict__ y, float* __restrict__ rstd, int R,
                                                             int D, float eps) {
   const int lane = threadIdx.x & 63;
@@ -75,13 +78,25 @@ __global__ void __launch_bounds__(kBlock) rmsnorm_fwd_kernel(const u16* __restri
   if (row >= R) return;
   const int nvec = D >> 3;
   const u16x8* xr = reinterpret_cast<const u16x8*>(x + (size_t)row * D);
-  u16x8 v[VPL];
-  float ss = 0.f;
+  u16x8 v[VPL], dv[VPL];
 #pragma unroll
   for (int k = 0; k < VPL; ++k) {
     const int i = lane + 64 * k;
     if (i < nvec) {
       v[k] = xr[i];
+      if (RES) dv[k] = reinterpret_cast<const u16x8*>(delta + (size_t)row * D)[i];
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+    const int i = lane + 64 * k;
+    if (i < nvec) {
+      if (RES) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = f2b(b2f(v[k][j]) + b2f(dv[k][j]));
+        reinterpret_cast<u16x8*>(sum + (size_t)row * D)[i] = v[k];
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float f = b2f(v[k][j]);
@@ -110,11 +125,14 @@ __global__ void __launch_bounds__(kBlock) rmsnorm_fwd_kernel(const u16* __restri
 // A block owns `rows_per_block` consecutive rows (its 4 waves stride over them); each lane
 // accumulates the weight-gradient of its columns in registers, the 4 waves are summed through
 // LDS and the block writes one fp32 partial row (reduced by col_sum_kernel).
-template <int VPL>
+// RES: the gradient arriving on the residual stream (dres) is added to dx before the single
+// bf16 rounding (the fused add's backward: d(x) = d(delta) = dres + norm'(dy)).
+template <int VPL, bool RES>
 __global__ void __launch_bounds__(kBlock) rmsnorm_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ x,
-                                                            const u16* __restrict__ w, const float* __restrict__ rstd,
-                                                            u16* __restrict__ dx, float* __restrict__ dw_part, int R,
-                                                            int D, int rows_per_block) {
+                                                            const u16* __restrict__ dres, const u16* __restrict__ w,
+                                                            const float* __restrict__ rstd, u16* __restrict__ dx,
+                                                            float* __restrict__ dw_part, int R, int D,
+                                                            int rows_per_block) {
   extern __shared__ float sdw[];  // [4][D]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nvec = D >> 3;
@@ -175,15 +193,19 @@ __global__ void __launch_bounds__(kBlock) rmsnorm_bwd_kernel(const u16* __restri
     const float r = rstd[row];
     const float c = dot * r * r * r * inv_d;
     u16x8* dxr = reinterpret_cast<u16x8*>(dx + (size_t)row * D);
+    const u16x8* drr = reinterpret_cast<const u16x8*>(dres + (size_t)row * D);
 #pragma unroll
     for (int k = 0; k < VPL; ++k) {
       const int i = lane + 64 * k;
       if (i < nvec) {
-        u16x8 o;
+        u16x8 o, rv;
+        if (RES) rv = drr[i];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float g = b2f(gv[k][j]), xf = b2f(xv[k][j]);
-          o[j] = f2b(r * g * b2f(wv[k][j]) - xf * c);
+          float d = r * g * b2f(wv[k][j]) - xf * c;
+          if (RES) d += b2f(rv[j]);
+          o[j] = f2b(d);
           acc[k][j] += g * xf * r;
         }
         dxr[i] = o;
@@ -927,34 +949,59 @@ int vpl_for(int D) {
 
 bool rmsnorm_supported(int64_t D) { return D % 8 == 0 && D >= 8 && vpl_for((int)D) > 0; }
 
-// x: [R, D] contiguous
-std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, double eps) {
+// x (and delta): [R, D] contiguous. Returns {y, rstd} or, with delta, {y, rstd, x + delta}.
+std::vector<at::Tensor> rmsnorm_fwd_impl(const at::Tensor& x, const at::Tensor* delta, const at::Tensor& w, double eps) {
   check_bf16(x, "x");
   check_bf16(w, "weight");
   const int D = (int)x.size(-1);
   TORCH_CHECK(w.numel() == D, "weight size mismatch");
   TORCH_CHECK(rmsnorm_supported(D), "rmsnorm: hidden size must be a multiple of 8 and <= 4096");
+  if (delta) {
+    check_bf16(*delta, "delta");
+    TORCH_CHECK(delta->sizes() == x.sizes(), "delta shape mismatch");
+  }
   const int R = (int)(x.numel() / D);
   auto y = at::empty_like(x);
   auto rstd = at::empty({R}, x.options().dtype(at::kFloat));
-  if (R == 0) return {y, rstd};
+  at::Tensor sum = delta ? at::empty_like(x) : at::Tensor();
+  std::vector<at::Tensor> out = {y, rstd};
+  if (delta) out.push_back(sum);
+  if (R == 0) return out;
   dim3 grid((R + 3) / 4), block(kBlock);
   auto launch = [&](auto kernel) {
-    hipLaunchKernelGGL(kernel, grid, block, 0, stream(), (const u16*)x.data_ptr(), (const u16*)w.data_ptr(),
-                       (u16*)y.data_ptr(), rstd.data_ptr<float>(), R, D, (float)eps);
+    hipLaunchKernelGGL(kernel, grid, block, 0, stream(), (const u16*)x.data_ptr(),
+                       delta ? (const u16*)delta->data_ptr() : nullptr, (const u16*)w.data_ptr(),
+                       delta ? (u16*)sum.data_ptr() : nullptr, (u16*)y.data_ptr(), rstd.data_ptr<float>(), R, D,
+                       (float)eps);
   };
-  switch (vpl_for(D)) {
-    case 1: launch(rmsnorm_fwd_kernel<1>); break;
-    case 2: launch(rmsnorm_fwd_kernel<2>); break;
-    case 4: launch(rmsnorm_fwd_kernel<4>); break;
-    default: launch(rmsnorm_fwd_kernel<8>); break;
+#define RMS_FWD_CASES(RES)                                \
+  switch (vpl_for(D)) {                                   \
+    case 1: launch(rmsnorm_fwd_kernel<1, RES>); break;    \
+    case 2: launch(rmsnorm_fwd_kernel<2, RES>); break;    \
+    case 4: launch(rmsnorm_fwd_kernel<4, RES>); break;    \
+    default: launch(rmsnorm_fwd_kernel<8, RES>); break;   \
   }
+  if (delta) {
+    RMS_FWD_CASES(true)
+  } else {
+    RMS_FWD_CASES(false)
+  }
+#undef RMS_FWD_CASES
   LAUNCH_CHECK();
-  return {y, rstd};
+  return out;
 }
 
-std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
-                                    const at::Tensor& rstd) {
+std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const at::Tensor& w, double eps) {
+  return rmsnorm_fwd_impl(x, nullptr, w, eps);
+}
+
+std::vector<at::Tensor> add_rmsnorm_fwd(const at::Tensor& x, const at::Tensor& delta, const at::Tensor& w, double eps) {
+  return rmsnorm_fwd_impl(x, &delta, w, eps);
+}
+
+// dres (optional): gradient already flowing on the residual stream, added into dx.
+std::vector<at::Tensor> rmsnorm_bwd_impl(const at::Tensor& dy, const at::Tensor& x, const at::Tensor* dres,
+                                         const at::Tensor& w, const at::Tensor& rstd) {
   check_bf16(dy, "grad");
   check_bf16(x, "x");
   check_bf16(w, "weight");
@@ -962,6 +1009,10 @@ std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, c
   const int R = (int)(x.numel() / D);
   TORCH_CHECK(rstd.numel() == R && rstd.scalar_type() == at::kFloat, "rstd mismatch");
   TORCH_CHECK(dy.numel() == x.numel(), "grad shape mismatch");
+  if (dres) {
+    check_bf16(*dres, "residual grad");
+    TORCH_CHECK(dres->numel() == x.numel(), "residual grad shape mismatch");
+  }
   auto dx = at::empty_like(x);
   auto dw = at::empty_like(w);
   if (R == 0) return {dx, dw.zero_()};
@@ -972,20 +1023,33 @@ std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, c
   const size_t lds = (size_t)4 * D * sizeof(float);
   auto launch = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, dim3(nblk), dim3(kBlock), lds, stream(), (const u16*)dy.data_ptr(),
-                       (const u16*)x.data_ptr(), (const u16*)w.data_ptr(), rstd.data_ptr<float>(), (u16*)dx.data_ptr(),
-                       part.data_ptr<float>(), R, D, rpb);
+                       (const u16*)x.data_ptr(), dres ? (const u16*)dres->data_ptr() : nullptr,
+                       (const u16*)w.data_ptr(), rstd.data_ptr<float>(), (u16*)dx.data_ptr(), part.data_ptr<float>(),
+                       R, D, rpb);
   };
-  switch (vpl_for(D)) {
-    case 1: launch(rmsnorm_bwd_kernel<1>); break;
-    case 2: launch(rmsnorm_bwd_kernel<2>); break;
-    case 4: launch(rmsnorm_bwd_kernel<4>); break;
-    default: launch(rmsnorm_bwd_kernel<8>); break;
+#define RMS_BWD_CASES(RES)                                \
+  switch (vpl_for(D)) {                                   \
+    case 1: launch(rmsnorm_bwd_kernel<1, RES>); break;    \
+    case 2: launch(rmsnorm_bwd_kernel<2, RES>); break;    \
+    case 4: launch(rmsnorm_bwd_kernel<4, RES>); break;    \
+    default: launch(rmsnorm_bwd_kernel<8, RES>); break;   \
   }
+  if (dres) {
+    RMS_BWD_CASES(true)
+  } else {
+    RMS_BWD_CASES(false)
+  }
+#undef RMS_BWD_CASES
   LAUNCH_CHECK();
   hipLaunchKernelGGL(col_sum_kernel, dim3((D + 31) / 32), dim3(1024), 0, stream(), part.data_ptr<float>(), nblk, D,
                      (u16*)dw.data_ptr());
   LAUNCH_CHECK();
   return {dx, dw};
+}
+
+std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                    const at::Tensor& rstd) {
+  return rmsnorm_bwd_impl(dy, x, nullptr, w, rstd);
 }
 
 at::Tensor swiglu_fwd(const at::Tensor& h) {
@@ -1216,6 +1280,31 @@ struct RMSNormFn : public torch::autograd::Function<RMSNormFn> {
   }
 };
 
+// (s, y) = (x + delta, rmsnorm(x + delta) * w). Backward: d = ds + norm'(dy) for both x and
+// delta (one kernel: the residual gradient is read inside the norm backward).
+struct AddRMSNormFn : public torch::autograd::Function<AddRMSNormFn> {
+  static variable_list forward(AutogradContext* ctx, const at::Tensor& x, const at::Tensor& delta, const at::Tensor& w,
+                               double eps) {
+    const int64_t D = x.size(-1);
+    auto x2 = x.contiguous().view({-1, D});
+    auto d2 = delta.contiguous().view({-1, D});
+    auto w2 = w.contiguous();
+    auto r = add_rmsnorm_fwd(x2, d2, w2, eps);
+    ctx->save_for_backward({r[2], w2, r[1]});
+    ctx->saved_data["shape"] = x.sizes().vec();
+    return {r[2].view(x.sizes()), r[0].view(x.sizes())};
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto s = ctx->get_saved_variables();
+    auto shape = ctx->saved_data["shape"].toIntVector();
+    at::Tensor dy = grads[1].defined() ? grads[1].contiguous().view_as(s[0]) : at::zeros_like(s[0]);
+    at::Tensor dres = grads[0].defined() ? grads[0].contiguous().view_as(s[0]) : at::Tensor();
+    auto r = rmsnorm_bwd_impl(dy, s[0], dres.defined() ? &dres : nullptr, s[1], s[2]);
+    auto dx = r[0].view(shape);
+    return {dx, dx, r[1], at::Tensor()};
+  }
+};
+
 struct SwiGLUFn : public torch::autograd::Function<SwiGLUFn> {
   static at::Tensor forward(AutogradContext* ctx, const at::Tensor& h) {
     auto hc = h.contiguous();
@@ -1267,6 +1356,10 @@ at::Tensor attention(const at::Tensor& qkv, bool causal, double scale) {
 }
 
 at::Tensor rms_norm(const at::Tensor& x, const at::Tensor& w, double eps) { return RMSNormFn::apply(x, w, eps); }
+
+std::vector<at::Tensor> add_rms_norm(const at::Tensor& x, const at::Tensor& delta, const at::Tensor& w, double eps) {
+  return AddRMSNormFn::apply(x, delta, w, eps);
+}
 at::Tensor swiglu(const at::Tensor& h) { return SwiGLUFn::apply(h); }
 at::Tensor cross_entropy(const at::Tensor& logits, const at::Tensor& tgt, int64_t ignore_index) {
   return CrossEntropyFn::apply(logits, tgt, ignore_index);
@@ -1279,6 +1372,8 @@ PYBIND11_MODULE(_fused_ops, m) {
   m.def("rmsnorm_supported", &rmsnorm_supported);
   // differentiable entry points (C++ autograd)
   m.def("rms_norm", &rms_norm);
+  m.def("add_rms_norm", &add_rms_norm, "(x + delta, rmsnorm(x + delta) * w) with a fused backward");
+  m.def("add_rmsnorm_fwd", &add_rmsnorm_fwd);
   m.def("swiglu", &swiglu);
   m.def("cross_entropy", &cross_entropy);
   m.def("adamw_step", &adamw_step);

@@ -88,7 +88,19 @@ def op_cases(dev):
         o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=True)
         o.transpose(1, 2).reshape(8, 512, 1024).backward(dattn.view(8, 512, 1024))
 
+    xd = torch.randn(R, D, device=dev).bfloat16().requires_grad_()
+
+    def addnorm_fused():
+        s_, y_ = fused.add_rms_norm(x, xd, w, eps)
+        torch.autograd.backward([s_, y_], [dy, dy])
+
+    def addnorm_eager():
+        s_ = x + xd
+        y_ = F.rms_norm(s_, (D,), w, eps)
+        torch.autograd.backward([s_, y_], [dy, dy])
+
     return {"attention fwd+bwd [8x512, 16 heads x 64]": (attn_fused, attn_eager),
+            "residual add + rmsnorm fwd+bwd [4096x1024]": (addnorm_fused, addnorm_eager),
             "adamw step [67M bf16 params]": (opt_f.step, opt_e.step),
             "rmsnorm fwd+bwd [4096x1024]": (rms_fused, rms_eager),
             "swiglu fwd+bwd [4096x2x2730]": (swiglu_fused, swiglu_eager),
@@ -115,6 +127,12 @@ def step_case(dev):
         return F.silu(g) * u
 
     m_eager.swiglu = sw
+
+    def add_norm(x, d, w, eps=None):
+        s = x + d
+        return s, F.rms_norm(s, (s.shape[-1],), w, eps)
+
+    m_eager.add_rms_norm = add_norm
     m_eager.AdamW = None  # torch.optim.AdamW(fused=True)
     m_eager.cross_entropy = lambda lg, tg: F.cross_entropy(lg.float(), tg)
     sf, se = m_fused.setup(Ctx()), m_eager.setup(Ctx())

@@ -219,3 +219,36 @@ def test_gemm_tuning_shipped_table_loads_on_gfx950():
         torch.testing.assert_close((a @ b).float(), a.float() @ b.float(), atol=0.5, rtol=2e-2)
     finally:
         torch.cuda.tunable.enable(False)
+
+
+def test_add_rms_norm_cpu_fallback():
+    torch.manual_seed(7)
+    x, d, w = torch.randn(3, 5, 32), torch.randn(3, 5, 32), torch.randn(32)
+    s, y = fused.add_rms_norm(x, d, w, 1e-6)
+    torch.testing.assert_close(s, x + d)
+    torch.testing.assert_close(y, F.rms_norm(x + d, (32,), w, 1e-6))
+
+
+@gpu
+@pytest.mark.parametrize("rows,dim,use_ds", [(4096, 1024, True), (37, 768, True), (64, 1024, False)])
+def test_add_rms_norm_fwd_bwd(rows, dim, use_ds):
+    dev = _cuda()
+    torch.manual_seed(8)
+    x = torch.randn(rows, dim, device=dev).bfloat16().requires_grad_()
+    d = torch.randn(rows, dim, device=dev).bfloat16().requires_grad_()
+    w = (1 + 0.1 * torch.randn(dim, device=dev)).bfloat16().requires_grad_()
+    eps = torch.finfo(torch.bfloat16).eps
+    s, y = fused.add_rms_norm(x, d, w, eps)
+    dy, ds = torch.randn_like(y), torch.randn_like(s)
+    (((y.float() * dy.float()).sum() + (s.float() * ds.float()).sum()) if use_ds else (y.float() * dy.float()).sum()).backward()
+    xr, dr, wr = (t.detach().float().requires_grad_() for t in (x, d, w))
+    sr = (xr + dr).bfloat16().float()  # the fused kernel rounds s to bf16 like the eager add
+    yr = _ref_rmsnorm(sr, wr, eps)
+    loss = (yr * dy.float()).sum() + ((sr * ds.float()).sum() if use_ds else 0)
+    loss.backward()
+    torch.testing.assert_close(s.float(), (x.float() + d.float()), atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(y.float(), yr, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(d.grad.float(), dr.grad, atol=3e-2, rtol=3e-2)
+    err = (w.grad.float() - wr.grad).abs().max() / wr.grad.abs().max()
+    assert err < 2e-2, err
