@@ -1,0 +1,220 @@
+"""CLI surface parity with the reference (one row per command), plus the
+multi-config commands (`list configs`, `use config`, `list vars`) and the offline
+`install`/`upgrade`/`update config` paths that the e2e suites do not reach.
+
+Reference command registrations: cmd/init.go:67-105, cmd/deploy.go:38-64, cmd/dev.go:71-120,
+cmd/enter.go:33-61, cmd/logs.go:25-56, cmd/analyze.go:21-47, cmd/purge.go:34-62,
+cmd/reset.go:39-61, cmd/login.go:16-41, cmd/add/*.go, cmd/create/space.go:21-45,
+cmd/list/list.go:20-26, cmd/remove/remove.go:20-28, cmd/status/status.go:20-21,
+cmd/update/update.go:20, cmd/use/use.go:20-23. Config files: config/configs/schema.go:4-31,
+config/configutil/get.go:193-221, config/configutil/load.go:23-72.
+"""
+
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.environ.get("DEVSPACE_BIN") or os.path.join(ROOT, "bin", "devspace")
+
+# (command path, [(long flag, shorthand or None, default or None)]) — SURVEY.md §2.4.
+# `init --cloud` deliberately defaults to false (the hosted service is gone; PARITY.md).
+SURFACE = [
+    ("init", [("reconfigure", "r", None), ("overwrite", "o", None), ("templateRepoUrl", None, None),
+              ("templateRepoPath", None, None), ("cloud", None, None)]),
+    ("deploy", [("namespace", None, None), ("kube-context", None, None), ("config", None, ".devspace/config.yaml"),
+                ("docker-target", None, None), ("switch-context", None, None), ("force-build", "b", None),
+                ("force-deploy", "d", None)]),
+    ("dev", [("init-registries", None, "true"), ("force-build", "b", None), ("force-deploy", "d", None),
+             ("skip-pipeline", "x", None), ("sync", None, "true"), ("verbose-sync", None, None),
+             ("portforwarding", None, "true"), ("terminal", None, "true"), ("selector", "s", None),
+             ("container", "c", None), ("label-selector", "l", None), ("namespace", "n", None),
+             ("switch-context", None, None), ("exit-after-deploy", None, None), ("config", None, None)]),
+    ("up", [("force-build", "b", None), ("sync", None, "true")]),
+    ("enter", [("selector", "s", None), ("container", "c", None), ("label-selector", "l", None),
+               ("namespace", "n", None), ("switch-context", None, None), ("pick", "p", None), ("config", None, None)]),
+    ("logs", [("selector", "s", None), ("container", "c", None), ("label-selector", "l", None),
+              ("namespace", "n", None), ("pick", "p", None), ("follow", "f", None), ("lines", None, "200"),
+              ("config", None, None)]),
+    ("analyze", [("namespace", "n", None), ("wait", None, "true")]),
+    ("purge", [("deployment", "d", None), ("config", None, None)]),
+    ("down", [("deployment", "d", None)]),
+    ("reset", [("config", None, None)]),
+    ("install", []),
+    ("upgrade", []),
+    ("login", [("token", None, None), ("provider", None, "app.devspace.cloud")]),
+    ("add sync", [("local", None, None), ("container", None, None), ("label-selector", None, None),
+                  ("namespace", None, None), ("exclude", None, None), ("selector", None, None)]),
+    ("add selector", [("namespace", None, None), ("label-selector", None, None)]),
+    ("add provider", [("name", None, None)]),
+    ("add port", [("namespace", None, None), ("label-selector", None, None), ("selector", None, None)]),
+    ("add package", [("app-version", None, None), ("chart-version", None, None), ("deployment", "d", None),
+                     ("skip-question", None, None)]),
+    ("add image", [("image", None, None), ("tag", None, None), ("context", None, None), ("dockerfile", None, None),
+                   ("buildengine", None, None)]),
+    ("add deployment", [("namespace", None, None), ("manifests", None, None), ("chart", None, None)]),
+    ("create space", [("context", None, "true"), ("active", None, "true")]),
+    ("list sync", []), ("list spaces", [("name", None, None)]), ("list selectors", []), ("list ports", []),
+    ("list packages", []), ("list configs", []), ("list vars", []),
+    ("remove context", [("all", None, None)]), ("remove deployment", [("all", None, None)]),
+    ("remove image", [("all", None, None)]), ("remove package", [("all", None, None)]),
+    ("remove port", [("label-selector", None, None), ("all", None, None)]),
+    ("remove provider", []), ("remove selector", [("all", None, None)]),
+    ("remove space", [("id", None, None), ("provider", None, None), ("all", None, None)]),
+    ("remove sync", [("local", None, None), ("container", None, None), ("label-selector", None, None),
+                     ("all", None, None)]),
+    ("status sync", []), ("status deployments", []),
+    ("update config", []),
+    ("use config", []), ("use space", [("context", None, "true")]), ("use registry", []), ("use context", []),
+]
+
+
+def _help(path):
+    p = subprocess.run([BIN] + path.split() + ["--help"], capture_output=True, text=True, timeout=30,
+                       env=dict(os.environ, DEVSPACE_NONINTERACTIVE="1"))
+    assert p.returncode == 0, f"devspace {path} --help failed: {p.stdout}{p.stderr}"
+    return p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("path,flags", SURFACE, ids=[s[0].replace(" ", "_") for s in SURFACE])
+def test_command_and_flags_exist(path, flags):
+    out = _help(path)
+    assert f"devspace {path}" in out, out
+    for long, short, default in flags:
+        # cobra-style line: "  -b, --force-build   ..." or "      --sync   ... (default true)"
+        pat = (rf"^\s+-{short}, --{re.escape(long)}\b" if short else rf"^\s+--{re.escape(long)}\b")
+        lines = [l for l in out.splitlines() if re.search(pat, l)]
+        assert lines, f"devspace {path}: flag --{long}" + (f"/-{short}" if short else "") + f" missing\n{out}"
+        if default is not None:
+            assert f'(default {default})' in lines[0] or f'(default "{default}")' in lines[0], lines[0]
+
+
+def _project(tmp_path):
+    proj = tmp_path / "proj"
+    shutil.copytree(os.path.join(ROOT, "examples", "quickstart"), proj, symlinks=True)
+    return str(proj)
+
+
+def _run(args, cwd, home, env=None, check=True):
+    e = dict(os.environ, HOME=home, DEVSPACE_NONINTERACTIVE="1")
+    e.update(env or {})
+    p = subprocess.run([BIN] + args, cwd=cwd, env=e, capture_output=True, text=True, timeout=60)
+    if check:
+        assert p.returncode == 0, f"devspace {' '.join(args)} rc={p.returncode}\n{p.stdout}{p.stderr}"
+    return p
+
+
+def test_multi_config_list_use_and_vars(tmp_path):
+    """configs.yaml with a data override and a ${VAR}: list configs, use config, list vars
+    (DEVSPACE_VAR_<NAME> resolves the variable; the answer is cached in generated.yaml)."""
+    proj = _project(tmp_path)
+    home = str(tmp_path / "home")
+    os.makedirs(home)
+    dsdir = os.path.join(proj, ".devspace")
+    configs = {
+        "default": {"config": {"path": ".devspace/config.yaml"}},
+        "staging": {
+            "config": {"path": ".devspace/config.yaml"},
+            "vars": {"data": [{"name": "NS", "question": "Namespace?"}]},
+            "overrides": [{"data": {"cluster": {"namespace": "${NS}"}}}],
+        },
+    }
+    with open(os.path.join(dsdir, "configs.yaml"), "w") as f:
+        yaml.safe_dump(configs, f)
+
+    out = _run(["list", "configs"], proj, home).stdout
+    rows = {l.split()[0]: l.split() for l in out.splitlines() if l.strip().startswith(("default", "staging"))}
+    assert set(rows) == {"default", "staging"}, out
+    assert rows["staging"][2:] == [".devspace/config.yaml", "true", "1"], out
+
+    out = _run(["use", "config", "staging"], proj, home).stdout
+    assert "Successfully switched to config 'staging'" in out
+    gen = yaml.safe_load(open(os.path.join(dsdir, "generated.yaml")))
+    assert gen["activeConfig"] == "staging"
+    active = [l for l in _run(["list", "configs"], proj, home).stdout.splitlines() if "staging" in l][0]
+    assert "true" in active.split()[1]
+
+    out = _run(["list", "vars"], proj, home, env={"DEVSPACE_VAR_NS": "team-a"}).stdout
+    assert re.search(r"NS\s+team-a", out), out
+    # cached answer is reused without the env var
+    out = _run(["list", "vars"], proj, home).stdout
+    assert re.search(r"NS\s+team-a", out), out
+
+    p = _run(["use", "config", "nope"], proj, home, check=False)
+    assert p.returncode != 0 and "does not exist" in p.stdout + p.stderr
+
+
+def test_update_config_rewrites_v1alpha1(tmp_path):
+    """`update config` re-saves a v1alpha1 config in the latest schema (cmd/update/config.go)."""
+    proj = _project(tmp_path)
+    home = str(tmp_path / "home")
+    os.makedirs(home)
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    # v1alpha1 layout (config/versions/v1alpha1/schema.go): everything dev-related under
+    # `devSpace`, images reference `registries` by name, helm `devOverwrite`
+    old = {
+        "version": "v1alpha1",
+        "devSpace": {
+            "deployments": [{"name": "app", "helm": {"chartPath": "chart/", "devOverwrite": "dev-values.yaml"}}],
+            "services": [{"name": "default", "labelSelector": {"app": "web"}}],
+            "ports": [{"service": "default", "portMappings": [{"localPort": 3000, "remotePort": 3000}]}],
+        },
+        "images": {"default": {"name": "web", "registry": "local"}},
+        "registries": {"local": {"url": "registry.local:5000"}},
+    }
+    with open(cfg_path, "w") as f:
+        yaml.safe_dump(old, f)
+    out = _run(["update", "config"], proj, home).stdout
+    assert "Successfully converted" in out
+    new = yaml.safe_load(open(cfg_path))
+    assert new["version"] == "v1alpha2"
+    assert "devSpace" not in new and "registries" not in new
+    assert new["deployments"][0]["helm"]["overrides"] == ["dev-values.yaml"]
+    assert new["images"]["default"]["image"] == "registry.local:5000/web"
+    assert new["dev"]["selectors"][0]["name"] == "default"
+    assert new["dev"]["ports"][0]["selector"] == "default"
+    # the rewritten file loads strictly under the latest schema
+    assert "default" in _run(["list", "selectors"], proj, home).stdout
+
+
+def test_install_adds_path_idempotently(tmp_path):
+    home = str(tmp_path / "home")
+    os.makedirs(home)
+    open(os.path.join(home, ".bashrc"), "w").write("# rc\n")
+    for _ in range(2):
+        out = _run(["install"], str(tmp_path), home).stdout + ""
+    rc = open(os.path.join(home, ".bashrc")).read()
+    assert rc.count("added by devspace install") == 1, rc
+    assert os.path.dirname(os.path.realpath(BIN)) in rc or os.path.dirname(BIN) in rc
+    assert "added by devspace install" in open(os.path.join(home, ".profile")).read()
+    assert out is not None
+
+
+def test_upgrade_from_local_release(tmp_path):
+    """`upgrade --from <binary>`: replaces the running binary only when the candidate is newer."""
+    home = str(tmp_path / "home")
+    os.makedirs(home)
+    exe = tmp_path / "devspace"
+    shutil.copy2(BIN, exe)
+    ver = subprocess.run([str(exe), "version"], capture_output=True, text=True).stdout.strip().split()[-1]
+    # a "newer release": a script that reports a higher version
+    newer = tmp_path / "devspace-next"
+    newer.write_text("#!/bin/sh\necho 'devspace version v99.0.0'\n")
+    newer.chmod(0o755)
+    same = subprocess.run([str(exe), "upgrade", "--from", str(exe)], capture_output=True, text=True,
+                          env=dict(os.environ, HOME=home), timeout=60)
+    assert same.returncode == 0 and "latest version" in same.stdout + same.stderr, same.stdout + same.stderr
+    p = subprocess.run([str(exe), "upgrade", "--from", str(newer)], capture_output=True, text=True,
+                       env=dict(os.environ, HOME=home), timeout=60)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "Successfully updated to version v99.0.0" in p.stdout + p.stderr
+    assert "v99.0.0" in subprocess.run([str(exe)], capture_output=True, text=True).stdout
+    assert ver
+    no_src = subprocess.run([BIN, "upgrade"], capture_output=True, text=True,
+                            env={k: v for k, v in dict(os.environ, HOME=home).items() if k != "DEVSPACE_RELEASE_URL"},
+                            timeout=60)
+    assert no_src.returncode != 0 and "no release source" in no_src.stdout + no_src.stderr

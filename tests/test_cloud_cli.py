@@ -54,6 +54,21 @@ def test_cloud_space_lifecycle(localkube):
         assert not gen.get("space")
         lk.run(["use", "space", "dev1", "--context=false"], proj)
         lk.run(["use", "context", "dev1"], proj)
+        kc = yaml.safe_load(open(lk.kubeconfig))
+        assert kc["current-context"] == "devspace-dev1"
+        out = lk.run(["remove", "context", "dev1"], proj).stdout
+        assert "Successfully deleted kubectl context for space dev1" in out
+        kc = yaml.safe_load(open(lk.kubeconfig))
+        assert all(c["name"] != "devspace-dev1" for c in kc.get("contexts") or [])
+        lk.run(["use", "context"], proj)  # no arg: the space configured in generated.yaml
+        kc = yaml.safe_load(open(lk.kubeconfig))
+        assert kc["current-context"] == "devspace-dev1"
+
+        # use registry: docker credentials for the provider's account (cmd/use/registry.go)
+        out = lk.run(["use", "registry", "registry.other.cloud"], proj).stdout
+        assert "Successfully logged into registry registry.other.cloud" in out
+        auths = json.load(open(os.path.join(lk.home, ".docker", "config.json")))["auths"]
+        assert "registry.other.cloud" in auths and auths["registry.other.cloud"].get("auth")
 
         lk.run(["remove", "space", "dev1"], proj)
         assert not cloud.spaces
