@@ -105,6 +105,10 @@ def step(ctx, state):
     logits = model(data[:, :-1])
     loss = cross_entropy(logits.view(-1, VOCAB), data[:, 1:].reshape(-1))
     opt.zero_grad(set_to_none=True)
+    # Preemption point between forward and backward: when the next edit is already waiting,
+    # the runner drops the rest of this step (backward + update) instead of running it.
+    ctx.preempt_point()
     loss.backward()
     opt.step()
-    return {"loss": round(loss.item(), 4), "ppl": round(math.exp(min(20.0, loss.item())), 2)}
+    loss = loss.item()
+    return {"loss": round(loss, 4), "ppl": round(math.exp(min(20.0, loss)), 2)}

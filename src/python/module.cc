@@ -64,11 +64,14 @@ static Value from_py(const py::handle& o) {
 // Inotify watcher with a queue drained from Python (no callbacks across threads).
 class PyWatcher {
  public:
-  explicit PyWatcher(const std::string& root) {
+  // settled_only: report a path only once its write finished (close-after-write, rename into
+  // place, delete), not on every IN_MODIFY of a file still being written.
+  explicit PyWatcher(const std::string& root, bool settled_only = false) {
     std::string err;
     if (!w_.start(
             root,
-            [this](const std::string& p, bool) {
+            [this, settled_only](const std::string& p, bool settled) {
+              if (settled_only && !settled) return;
               {
                 std::lock_guard<std::mutex> g(mu_);
                 q_.push_back(p);
@@ -177,7 +180,7 @@ PYBIND11_MODULE(_native, m) {
         py::arg("local"), py::arg("container"), py::arg("excludes") = std::vector<std::string>{},
         py::arg("mode") = "fast");
   py::class_<PyWatcher>(m, "Watcher")
-      .def(py::init<const std::string&>())
+      .def(py::init<const std::string&, bool>(), py::arg("root"), py::arg("settled_only") = false)
       .def("poll", &PyWatcher::poll, py::arg("timeout_ms") = 1000)
       .def("close", &PyWatcher::close);
   py::class_<PySync>(m, "SyncSession")

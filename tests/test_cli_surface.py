@@ -206,15 +206,15 @@ def test_upgrade_from_local_release(tmp_path):
     newer.write_text("#!/bin/sh\necho 'devspace version v99.0.0'\n")
     newer.chmod(0o755)
     same = subprocess.run([str(exe), "upgrade", "--from", str(exe)], capture_output=True, text=True,
-                          env=dict(os.environ, HOME=home), timeout=60)
+                          env=dict(os.environ, HOME=home), timeout=60, cwd=tmp_path)
     assert same.returncode == 0 and "latest version" in same.stdout + same.stderr, same.stdout + same.stderr
     p = subprocess.run([str(exe), "upgrade", "--from", str(newer)], capture_output=True, text=True,
-                       env=dict(os.environ, HOME=home), timeout=60)
+                       env=dict(os.environ, HOME=home), timeout=60, cwd=tmp_path)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "Successfully updated to version v99.0.0" in p.stdout + p.stderr
     assert "v99.0.0" in subprocess.run([str(exe)], capture_output=True, text=True).stdout
     assert ver
     no_src = subprocess.run([BIN, "upgrade"], capture_output=True, text=True,
                             env={k: v for k, v in dict(os.environ, HOME=home).items() if k != "DEVSPACE_RELEASE_URL"},
-                            timeout=60)
+                            timeout=60, cwd=tmp_path)
     assert no_src.returncode != 0 and "no release source" in no_src.stdout + no_src.stderr

@@ -57,8 +57,16 @@ def _run_reload(tmp_path, extra_env=None, nproc=1):
         assert proc.poll() is None
         return reload_line[0] + "".join(l for l in lines if "started gen=1" in l)
     finally:
+        import psutil
+
+        kids = psutil.Process(proc.pid).children(recursive=True)
         proc.terminate()
         proc.wait(10)
+        # the ranks go with the supervisor (no orphaned workers left training)
+        _, alive = psutil.wait_procs(kids, timeout=20)
+        for k in alive:
+            k.kill()
+        assert not alive, f"workers outlived the supervisor: {alive}"
 
 
 def test_runner_hot_reload_cpu(tmp_path):
@@ -77,3 +85,127 @@ def test_runner_hot_reload_two_ranks_cpu(tmp_path):
 def test_runner_hot_reload_gpu(tmp_path):
     line = _run_reload(tmp_path)
     assert "gen=2" in line
+
+
+SLOW_STEP = '''
+import time
+MARKER = "v0"
+
+
+def setup(ctx):
+    return {"updates": 0}
+
+
+def step(ctx, state):
+    # a 0.8 s "step" with a preemption point every 10 ms, then the state update
+    for _ in range(80):
+        time.sleep(0.01)
+        ctx.preempt_point()
+    state["updates"] += 1
+    return {"loss": state["updates"]}
+'''
+
+
+SLOW_STEP_GPU = '''
+import torch
+MARKER = "v0"
+
+
+def setup(ctx):
+    a = torch.randn(4096, 4096, device=ctx.device, dtype=torch.bfloat16)
+    return {"a": a, "updates": 0}
+
+
+def step(ctx, state):
+    # ~0.4 s of queued matmuls, a preemption point (drains: the loop period is > 20 ms), then
+    # another ~0.4 s and the state update
+    a = state["a"]
+    for _ in range(1500):
+        b = a @ a
+    ctx.preempt_point()
+    for _ in range(1500):
+        b = a @ a
+    state["updates"] += 1
+    torch.cuda.synchronize()
+    return {"loss": state["updates"]}
+'''
+
+
+def _pickup_ms(tmp_path, preempt, src=SLOW_STEP, gpu=False):
+    p = tmp_path / "slow.py"
+    p.write_text(src)
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    if not gpu:
+        env.update(HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1")
+    cmd = [sys.executable, "-u", "-m", "devspace_amd.runner", "--watch", str(tmp_path), str(p)]
+    if not preempt:
+        cmd.insert(-1, "--no-preempt")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, text=True)
+    try:
+        lines = []
+        while True:
+            line = proc.stdout.readline()
+            assert line, "".join(lines)
+            lines.append(line)
+            if "started gen=1" in line:
+                break
+        time.sleep(0.3 if not gpu else 1.5)  # a few steps in: the loop period is known
+        p.write_text(src.replace('MARKER = "v0"', 'MARKER = "v1"'))
+        while True:
+            line = proc.stdout.readline()
+            assert line, "".join(lines)
+            lines.append(line)
+            if "marker=v1" in line:
+                break
+        f = dict(re.findall(r"(\w+_ms)=([\d.]+)", line))
+        # the abandoned step never reached its state update; the new step did
+        assert re.search(r"loss=(\d+)", line), line
+        if gpu:
+            return float(f["pickup_ms"]), float(f["period_ms"])
+        return float(f["inflight_ms"]), int(re.search(r"loss=(\d+)", line).group(1))
+    finally:
+        proc.terminate()
+        proc.wait(10)
+
+
+def test_preempt_point_cuts_inflight_wait(tmp_path):
+    """ctx.preempt_point(): an edit landing mid-step abandons the rest of the old step (before
+    its state update) instead of waiting for it; --no-preempt waits for the whole step."""
+    inflight, updates = _pickup_ms(tmp_path, preempt=True)
+    assert inflight < 200, inflight
+    # started step = 1 update; the preempted step added none; the new-code step adds one
+    assert updates == 2, updates
+    inflight_np, updates_np = _pickup_ms(tmp_path, preempt=False)
+    assert inflight_np > 250, inflight_np
+    assert updates_np == 3
+
+
+@pytest.mark.gpu
+def test_preempt_point_drains_gpu_queue(tmp_path):
+    """On the GPU the point drains the queued work while polling the change feed: an edit that
+    lands during the first half of a long step does not wait for the second half."""
+    pickup, period = _pickup_ms(tmp_path, preempt=True, src=SLOW_STEP_GPU, gpu=True)
+    assert period > 100, period
+    # edit -> new step done <= rest of the phase in flight (<= half a step) + one full new step;
+    # without the drain it is the rest of the whole step + one new step (up to two periods)
+    assert pickup < 1.6 * period, (pickup, period)
+
+
+def test_preempt_point_noop_without_feed():
+    from devspace_amd.runner import Context, Preempted
+
+    class Feed:
+        n = 0
+
+        def pending(self):
+            return self.n > 0
+
+    import torch
+
+    ctx = Context(0, 1, 0, torch.device("cpu"))
+    ctx.preempt_point()  # no feed attached: never raises
+    ctx._feed = Feed()
+    ctx.preempt_point()
+    ctx._feed.n = 1
+    with pytest.raises(Preempted):
+        ctx.preempt_point()
