@@ -187,6 +187,9 @@ def test_tinylm_step_uses_fused_ops_and_trains():
     class Ctx:
         rank, distributed, device = 0, False, dev
 
+        def preempt_point(self):  # runner.Context hook; nothing to preempt here
+            pass
+
     state = mod.setup(Ctx())
     losses = [mod.step(Ctx(), state)["loss"] for _ in range(8)]
     assert losses[-1] < losses[0], losses
