@@ -239,7 +239,8 @@ class ApiServer:
         rt, c = self.kubelet.container(ns, name, request.query.get("container"))
         if c is None or "running" not in (c.state or {}):
             raise ApiError(400, "BadRequest", f"container not found or not running in pod {name}")
-        ws = web.WebSocketResponse(protocols=("v4.channel.k8s.io", "channel.k8s.io"), max_msg_size=0)
+        ws = web.WebSocketResponse(protocols=("v5.channel.k8s.io", "v4.channel.k8s.io", "channel.k8s.io"),
+                                   max_msg_size=0)
         await ws.prepare(request)
         tty = request.query.get("tty") in ("true", "1")
         if kind == "attach":
@@ -311,6 +312,11 @@ class ApiServer:
                 if msg.type != WSMsgType.BINARY or not msg.data:
                     continue
                 ch, data = msg.data[0], msg.data[1:]
+                if ch == 255 and ws.ws_protocol == "v5.channel.k8s.io":
+                    # v5 CLOSE signal: half-close the named stream (only stdin is writable)
+                    if data[:1] == b"\x00" and not tty and proc.stdin and not proc.stdin.is_closing():
+                        proc.stdin.close()
+                    continue
                 if ch == 0:
                     if tty:
                         os.write(master, data)

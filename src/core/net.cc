@@ -7,13 +7,17 @@
 #include <netinet/tcp.h>
 #include <openssl/err.h>
 #include <openssl/pem.h>
+#include <openssl/sha.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 #include <poll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
 
+#include <chrono>
+#include <climits>
 #include <cstring>
 
 #include "core/codec.h"
@@ -22,7 +26,24 @@
 namespace ds {
 namespace net {
 
+Stats& stats() {
+  static Stats s;
+  return s;
+}
+
 namespace {
+
+int64_t mono_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// Remaining milliseconds until `deadline` (-1 = no deadline → -1 = wait forever).
+int remaining_ms(int64_t deadline) {
+  if (deadline < 0) return -1;
+  int64_t left = deadline - mono_ms();
+  return left < 0 ? 0 : (int)std::min<int64_t>(left, INT_MAX);
+}
 
 int wait_fd(int fd, short ev, int timeout_ms) {
   struct pollfd pf{fd, ev, 0};
@@ -33,8 +54,42 @@ int wait_fd(int fd, short ev, int timeout_ms) {
   }
 }
 
+// Waits for `ev` on fd or for a poke on the eventfd `wake` (drained here). >0 ready, 0 timeout.
+int wait_fd_or_wake(int fd, short ev, int wake, int timeout_ms) {
+  struct pollfd pf[2] = {{fd, ev, 0}, {wake, POLLIN, 0}};
+  while (true) {
+    int r = ::poll(pf, wake >= 0 ? 2 : 1, timeout_ms);
+    if (r < 0 && errno == EINTR) continue;
+    if (r > 0 && wake >= 0 && (pf[1].revents & POLLIN)) {
+      uint64_t v;
+      ssize_t got = ::read(wake, &v, sizeof(v));
+      (void)got;
+    }
+    return r;
+  }
+}
+
+void poke(int wake) {
+  if (wake < 0) return;
+  uint64_t one = 1;
+  ssize_t w = ::write(wake, &one, sizeof(one));
+  (void)w;
+}
+
+std::string ssl_error_string() {
+  std::string out;
+  while (unsigned long e = ERR_get_error()) {
+    char buf[256];
+    ERR_error_string_n(e, buf, sizeof(buf));
+    if (!out.empty()) out += "; ";
+    out += buf;
+  }
+  return out;
+}
+
 class PlainConn : public Conn {
  public:
+  using Conn::write_all;
   explicit PlainConn(int fd) : fd_(fd) {}
   ~PlainConn() override {
     if (fd_ >= 0) ::close(fd_);
@@ -66,6 +121,11 @@ class PlainConn : public Conn {
   }
   void shutdown() override { ::shutdown(fd_, SHUT_RDWR); }
   int fd() const override { return fd_; }
+  int release() {
+    int f = fd_;
+    fd_ = -1;
+    return f;
+  }
 
  private:
   int fd_;
@@ -94,122 +154,205 @@ SSL_CTX* make_ctx(const TlsOptions& t) {
   if (!t.cert_pem.empty() && !t.key_pem.empty()) {
     BIO* cb = BIO_new_mem_buf(t.cert_pem.data(), (int)t.cert_pem.size());
     X509* cert = PEM_read_bio_X509(cb, nullptr, nullptr, nullptr);
+    // intermediate certificates after the leaf go into the chain
+    std::vector<X509*> chain;
+    while (cert) {
+      X509* extra = PEM_read_bio_X509(cb, nullptr, nullptr, nullptr);
+      if (!extra) break;
+      chain.push_back(extra);
+    }
     BIO_free(cb);
+    ERR_clear_error();
     BIO* kb = BIO_new_mem_buf(t.key_pem.data(), (int)t.key_pem.size());
     EVP_PKEY* key = PEM_read_bio_PrivateKey(kb, nullptr, nullptr, nullptr);
     BIO_free(kb);
-    if (!cert || !key || SSL_CTX_use_certificate(ctx, cert) != 1 || SSL_CTX_use_PrivateKey(ctx, key) != 1) {
-      if (cert) X509_free(cert);
-      if (key) EVP_PKEY_free(key);
+    bool ok = cert && key && SSL_CTX_use_certificate(ctx, cert) == 1 && SSL_CTX_use_PrivateKey(ctx, key) == 1;
+    for (X509* x : chain) {
+      if (ok && SSL_CTX_add_extra_chain_cert(ctx, x) == 1) continue;  // ctx owns x now
+      X509_free(x);
+    }
+    if (cert) X509_free(cert);
+    if (key) EVP_PKEY_free(key);
+    if (!ok) {
       SSL_CTX_free(ctx);
       throw NetError("invalid client certificate/key");
     }
-    X509_free(cert);
-    EVP_PKEY_free(key);
   }
   return ctx;
 }
 
+// TLS over a non-blocking socket. SSL_read/SSL_write run under ssl_mu_ only for the duration
+// of the call; waiting (poll) happens with no lock held, so a reader blocked on an idle
+// stream never holds up a concurrent writer. A writer that makes OpenSSL buffer incoming
+// records (TLS 1.2 renegotiation) pokes the eventfd so the parked reader re-checks.
 class TlsConn : public Conn {
  public:
-  TlsConn(int fd, const TlsOptions& t) : fd_(fd) {
-    ctx_ = make_ctx(t);
-    ssl_ = SSL_new(ctx_);
-    SSL_set_fd(ssl_, fd_);
-    if (!t.server_name.empty()) {
-      SSL_set_tlsext_host_name(ssl_, t.server_name.c_str());
-      if (!t.insecure) {
-        X509_VERIFY_PARAM* param = SSL_get0_param(ssl_);
+  using Conn::write_all;
+  TlsConn(int fd, const TlsOptions& t, int timeout_ms) : fd_(fd) {
+    try {
+      int fl = fcntl(fd_, F_GETFL);
+      fcntl(fd_, F_SETFL, fl | O_NONBLOCK);
+      wake_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+      ctx_ = make_ctx(t);
+      ssl_ = SSL_new(ctx_);
+      if (!ssl_) throw NetError("SSL_new failed");
+      SSL_set_mode(ssl_, SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
+      SSL_set_fd(ssl_, fd_);
+      if (!t.server_name.empty()) {
         in6_addr a6;
         in_addr a4;
-        if (inet_pton(AF_INET, t.server_name.c_str(), &a4) == 1 || inet_pton(AF_INET6, t.server_name.c_str(), &a6) == 1)
-          X509_VERIFY_PARAM_set1_ip_asc(param, t.server_name.c_str());
-        else
-          X509_VERIFY_PARAM_set1_host(param, t.server_name.c_str(), 0);
+        bool is_ip = inet_pton(AF_INET, t.server_name.c_str(), &a4) == 1 ||
+                     inet_pton(AF_INET6, t.server_name.c_str(), &a6) == 1;
+        if (!is_ip) SSL_set_tlsext_host_name(ssl_, t.server_name.c_str());  // SNI must not carry an IP
+        if (!t.insecure) {
+          X509_VERIFY_PARAM* param = SSL_get0_param(ssl_);
+          if (is_ip)
+            X509_VERIFY_PARAM_set1_ip_asc(param, t.server_name.c_str());
+          else
+            X509_VERIFY_PARAM_set1_host(param, t.server_name.c_str(), 0);
+        }
       }
-    }
-    if (SSL_connect(ssl_) != 1) {
-      unsigned long e = ERR_get_error();
-      char buf[256];
-      ERR_error_string_n(e, buf, sizeof(buf));
-      throw NetError(std::string("tls handshake failed: ") + buf);
+      int64_t deadline = timeout_ms < 0 ? -1 : mono_ms() + timeout_ms;
+      while (true) {
+        ERR_clear_error();
+        int r = SSL_connect(ssl_);
+        if (r == 1) break;
+        int err = SSL_get_error(ssl_, r);
+        short ev = err == SSL_ERROR_WANT_READ ? POLLIN : err == SSL_ERROR_WANT_WRITE ? POLLOUT : 0;
+        if (!ev) {
+          std::string msg = ssl_error_string();
+          long vr = SSL_get_verify_result(ssl_);
+          if (vr != X509_V_OK) msg += std::string(" (certificate verify: ") + X509_verify_cert_error_string(vr) + ")";
+          if (msg.empty()) msg = err == SSL_ERROR_SYSCALL ? "connection closed by peer" : "unknown error";
+          throw NetError("tls handshake failed: " + msg);
+        }
+        int left = remaining_ms(deadline);
+        if (left == 0 || wait_fd(fd_, ev, left) == 0) throw NetError("tls handshake timed out");
+      }
+      stats().tls_handshakes++;
+    } catch (...) {
+      cleanup();
+      throw;
     }
   }
-  ~TlsConn() override {
-    if (ssl_) {
-      SSL_shutdown(ssl_);
-      SSL_free(ssl_);
-    }
-    if (ctx_) SSL_CTX_free(ctx_);
-    if (fd_ >= 0) ::close(fd_);
-  }
+  ~TlsConn() override { cleanup(); }
+
   ssize_t read(void* buf, size_t n, int timeout_ms) override {
     std::lock_guard<std::mutex> g(rmu_);
-    if (SSL_pending(ssl_) == 0 && timeout_ms >= 0) {
-      int r = wait_fd(fd_, POLLIN, timeout_ms);
-      if (r == 0) return -2;
-      if (r < 0) return -1;
-    }
+    int64_t deadline = timeout_ms < 0 ? -1 : mono_ms() + timeout_ms;
+    int want = (int)std::min<size_t>(n, INT_MAX);
     while (true) {
-      int r;
+      if (shut_.load()) return 0;
+      int r, err = 0;
+      unsigned long reason = 0;
       {
         std::lock_guard<std::mutex> s(ssl_mu_);
-        r = SSL_read(ssl_, buf, (int)n);
+        ERR_clear_error();
+        r = SSL_read(ssl_, buf, want);
+        if (r <= 0) {
+          err = SSL_get_error(ssl_, r);
+          reason = ERR_peek_error();
+        }
       }
       if (r > 0) return r;
-      int err;
-      {
-        std::lock_guard<std::mutex> s(ssl_mu_);
-        err = SSL_get_error(ssl_, r);
-      }
-      if (err == SSL_ERROR_ZERO_RETURN) return 0;
+      short ev;
       if (err == SSL_ERROR_WANT_READ) {
-        if (wait_fd(fd_, POLLIN, timeout_ms < 0 ? 1000 : timeout_ms) <= 0 && timeout_ms >= 0) return -2;
-        continue;
+        ev = POLLIN;
+      } else if (err == SSL_ERROR_WANT_WRITE) {
+        ev = POLLOUT;
+      } else if (err == SSL_ERROR_ZERO_RETURN || (err == SSL_ERROR_SYSCALL && reason == 0)) {
+        return 0;  // close_notify, or the peer dropped the TCP connection
+      } else {
+#ifdef SSL_R_UNEXPECTED_EOF_WHILE_READING
+        if (ERR_GET_REASON(reason) == SSL_R_UNEXPECTED_EOF_WHILE_READING) return 0;
+#endif
+        return -1;
       }
-      if (err == SSL_ERROR_SYSCALL && r == 0) return 0;
-      return -1;
+      int left = remaining_ms(deadline);
+      if (left == 0) return -2;
+      int pr = wait_fd_or_wake(fd_, ev, wake_, left);
+      if (pr == 0) return -2;
+      if (pr < 0) return -1;
     }
   }
+
   bool write_all(const void* d, size_t n) override {
     std::lock_guard<std::mutex> g(wmu_);
     const char* p = (const char*)d;
     while (n) {
-      int w;
+      if (shut_.load()) return false;
+      int w, err = 0;
+      bool pending;
       {
         std::lock_guard<std::mutex> s(ssl_mu_);
-        w = SSL_write(ssl_, p, (int)n);
+        ERR_clear_error();
+        w = SSL_write(ssl_, p, (int)std::min<size_t>(n, 1u << 30));
+        if (w <= 0) err = SSL_get_error(ssl_, w);
+        pending = SSL_has_pending(ssl_) == 1;
       }
-      if (w <= 0) {
-        int err;
-        {
-          std::lock_guard<std::mutex> s(ssl_mu_);
-          err = SSL_get_error(ssl_, w);
-        }
-        if (err == SSL_ERROR_WANT_WRITE || err == SSL_ERROR_WANT_READ) {
-          wait_fd(fd_, POLLOUT, 1000);
-          continue;
-        }
+      if (pending) poke(wake_);  // we pulled records the reader has to see
+      if (w > 0) {
+        p += w;
+        n -= (size_t)w;
+        continue;
+      }
+      if (err == SSL_ERROR_WANT_WRITE) {
+        if (wait_fd(fd_, POLLOUT, 1000) < 0) return false;
+      } else if (err == SSL_ERROR_WANT_READ) {
+        // handshake traffic the reader thread may consume first: re-check soon
+        if (wait_fd(fd_, POLLIN, 20) < 0) return false;
+      } else {
         return false;
       }
-      p += w;
-      n -= (size_t)w;
     }
     return true;
   }
-  void shutdown() override { ::shutdown(fd_, SHUT_RDWR); }
+
+  void shutdown() override {
+    shut_ = true;
+    ::shutdown(fd_, SHUT_RDWR);
+    poke(wake_);
+  }
   int fd() const override { return fd_; }
 
+  bool stale() override {
+    struct pollfd pf{fd_, POLLIN, 0};
+    int r = ::poll(&pf, 1, 0);
+    if (r == 0) return false;
+    if (r < 0 || (pf.revents & (POLLERR | POLLHUP | POLLNVAL))) return true;
+    // readable: TLS 1.3 session tickets are fine, application data or EOF is not
+    std::lock_guard<std::mutex> s(ssl_mu_);
+    char c;
+    ERR_clear_error();
+    int x = SSL_peek(ssl_, &c, 1);
+    if (x > 0) return true;
+    return SSL_get_error(ssl_, x) != SSL_ERROR_WANT_READ;
+  }
+
  private:
+  void cleanup() {
+    if (ssl_) {
+      SSL_shutdown(ssl_);  // best effort close_notify (non-blocking)
+      SSL_free(ssl_);
+      ssl_ = nullptr;
+    }
+    if (ctx_) SSL_CTX_free(ctx_);
+    ctx_ = nullptr;
+    if (fd_ >= 0) ::close(fd_);
+    fd_ = -1;
+    if (wake_ >= 0) ::close(wake_);
+    wake_ = -1;
+  }
   int fd_;
+  int wake_ = -1;
   SSL_CTX* ctx_ = nullptr;
   SSL* ssl_ = nullptr;
   std::mutex rmu_, wmu_, ssl_mu_;
+  std::atomic<bool> shut_{false};
 };
 
-}  // namespace
-
-std::unique_ptr<Conn> dial_tcp(const std::string& host, int port, const TlsOptions& tls, int timeout_ms) {
+// TCP connect with timeout; returns a blocking fd with TCP_NODELAY.
+int dial_fd(const std::string& host, int port, int timeout_ms) {
   struct addrinfo hints{};
   hints.ai_family = AF_UNSPEC;
   hints.ai_socktype = SOCK_STREAM;
@@ -250,10 +393,128 @@ std::unique_ptr<Conn> dial_tcp(const std::string& host, int port, const TlsOptio
   }
   freeaddrinfo(res);
   if (fd < 0) throw NetError("dial tcp " + host + ":" + std::to_string(port) + ": " + last_err);
+  stats().tcp_dials++;
+  return fd;
+}
+
+std::string host_port(const std::string& host, int port) {
+  bool v6 = host.find(':') != std::string::npos && host.front() != '[';
+  return (v6 ? "[" + host + "]" : host) + ":" + std::to_string(port);
+}
+
+// HTTP CONNECT tunnel through an http:// proxy; returns the tunnelled fd.
+int connect_via_proxy(const std::string& proxy_url, const std::string& host, int port, int timeout_ms) {
+  std::string rest = proxy_url;
+  size_t sp = rest.find("://");
+  std::string scheme = sp == std::string::npos ? "http" : to_lower(rest.substr(0, sp));
+  if (scheme != "http") throw NetError("unsupported proxy scheme " + scheme + " (only http:// proxies)");
+  std::string auth_hdr;
+  std::string authority = sp == std::string::npos ? rest : rest.substr(sp + 3);
+  authority = authority.substr(0, authority.find('/'));
+  size_t at = authority.rfind('@');
+  if (at != std::string::npos) {
+    auth_hdr = "Proxy-Authorization: Basic " + base64_encode(url_decode(authority.substr(0, at))) + "\r\n";
+  }
+  Url pu = Url::parse(proxy_url);
+  if (pu.port == 0 || pu.port == 443) pu.port = sp == std::string::npos || pu.port == 0 ? 80 : pu.port;
+  PlainConn pc(dial_fd(pu.host, pu.port, timeout_ms));
+  std::string target = host_port(host, port);
+  std::string req = "CONNECT " + target + " HTTP/1.1\r\nHost: " + target + "\r\n" + auth_hdr + "\r\n";
+  if (!pc.write_all(req)) throw NetError("proxy " + pu.host + ": write CONNECT failed");
+  Response resp;
+  std::string left;
+  if (!read_response_head(pc, &resp, &left, timeout_ms)) throw NetError("proxy " + pu.host + ": no CONNECT response");
+  if (resp.status != 200)
+    throw NetError("proxy " + pu.host + " refused CONNECT " + target + ": " + std::to_string(resp.status) + " " +
+                   resp.reason);
+  if (!left.empty()) throw NetError("proxy " + pu.host + ": unexpected bytes after CONNECT response");
+  stats().proxied++;
+  return pc.release();
+}
+
+bool parse_ipv4(const std::string& s, uint32_t* out) {
+  in_addr a;
+  if (inet_pton(AF_INET, s.c_str(), &a) != 1) return false;
+  *out = ntohl(a.s_addr);
+  return true;
+}
+
+}  // namespace
+
+bool Conn::stale() {
+  int f = fd();
+  if (f < 0) return true;
+  struct pollfd pf{f, POLLIN, 0};
+  return ::poll(&pf, 1, 0) != 0;  // EOF, error or unsolicited bytes
+}
+
+// ---------------------------------------------------------------- proxy
+
+bool no_proxy_matches(const std::string& no_proxy, const std::string& host_in, int port) {
+  std::string host = to_lower(host_in);
+  if (host.size() > 2 && host.front() == '[' && host.back() == ']') host = host.substr(1, host.size() - 2);
+  for (std::string e : split(no_proxy, ",")) {
+    e = to_lower(trim(e));
+    if (e.empty()) continue;
+    if (e == "*") return true;
+    // optional :port
+    int eport = 0;
+    size_t colon = e.rfind(':');
+    if (colon != std::string::npos && e.find(']') == std::string::npos && e.find(':') == colon &&
+        e.find('/') == std::string::npos) {
+      eport = std::atoi(e.substr(colon + 1).c_str());
+      e = e.substr(0, colon);
+    }
+    if (eport && eport != port) continue;
+    size_t slash = e.find('/');
+    if (slash != std::string::npos) {  // IPv4 CIDR
+      uint32_t net, ip;
+      int bits = std::atoi(e.substr(slash + 1).c_str());
+      if (parse_ipv4(e.substr(0, slash), &net) && parse_ipv4(host, &ip) && bits >= 0 && bits <= 32) {
+        uint32_t mask = bits == 0 ? 0 : 0xFFFFFFFFu << (32 - bits);
+        if ((net & mask) == (ip & mask)) return true;
+      }
+      continue;
+    }
+    if (e.front() == '.') e = e.substr(1);
+    if (host == e) return true;
+    if (host.size() > e.size() && ends_with(host, "." + e)) return true;
+  }
+  return false;
+}
+
+static std::string env_first(std::initializer_list<const char*> names) {
+  for (auto* n : names) {
+    const char* v = getenv(n);
+    if (v && *v) return v;
+  }
+  return "";
+}
+
+ProxyConfig ProxyConfig::from_env() {
+  ProxyConfig p;
+  p.https_proxy = env_first({"HTTPS_PROXY", "https_proxy", "ALL_PROXY", "all_proxy"});
+  p.http_proxy = env_first({"HTTP_PROXY", "http_proxy", "ALL_PROXY", "all_proxy"});
+  p.no_proxy = env_first({"NO_PROXY", "no_proxy"});
+  return p;
+}
+
+std::string ProxyConfig::proxy_for(const std::string& scheme, const std::string& host, int port) const {
+  std::string p = scheme == "https" || scheme == "wss" ? https_proxy : http_proxy;
+  if (p.empty()) return "";
+  if (no_proxy_matches(no_proxy, host, port)) return "";
+  return p;
+}
+
+std::unique_ptr<Conn> dial_tcp(const std::string& host, int port, const TlsOptions& tls, int timeout_ms,
+                               const std::string& proxy_url) {
+  int fd = proxy_url.empty() ? dial_fd(host, port, timeout_ms) : connect_via_proxy(proxy_url, host, port, timeout_ms);
   if (tls.enabled) {
     TlsOptions t = tls;
+    std::string h = host;
+    if (h.size() > 2 && h.front() == '[' && h.back() == ']') h = h.substr(1, h.size() - 2);
     if (t.server_name.empty()) t.server_name = h;
-    return std::make_unique<TlsConn>(fd, t);
+    return std::make_unique<TlsConn>(fd, t, timeout_ms);
   }
   return std::make_unique<PlainConn>(fd);
 }
@@ -320,16 +581,112 @@ std::string url_encode(const std::string& s) {
   return out;
 }
 
-HttpClient::HttpClient(const std::string& base_url, TlsOptions tls) : url_(Url::parse(base_url)), tls_(std::move(tls)) {
-  if (url_.scheme == "https" || url_.scheme == "wss") tls_.enabled = true;
+// ---------------------------------------------------------------- http client
+
+struct HttpClient::State {
+  TlsOptions tls;
+  mutable std::mutex mu;
+  std::map<std::string, std::string> headers;
+  std::vector<std::unique_ptr<Conn>> idle;
+  bool keepalive = true;
+  size_t max_idle = 8;
+  ProxyConfig proxy = ProxyConfig::from_env();
+};
+
+HttpClient::HttpClient() : st_(std::make_shared<State>()) {}
+
+HttpClient::HttpClient(const std::string& base_url, TlsOptions tls)
+    : url_(Url::parse(base_url)), st_(std::make_shared<State>()) {
+  st_->tls = std::move(tls);
+  if (url_.scheme == "https" || url_.scheme == "wss") st_->tls.enabled = true;
+}
+
+void HttpClient::set_header(const std::string& k, const std::string& v) {
+  std::lock_guard<std::mutex> g(st_->mu);
+  st_->headers[k] = v;
+}
+
+std::map<std::string, std::string> HttpClient::default_headers() const {
+  std::lock_guard<std::mutex> g(st_->mu);
+  return st_->headers;
+}
+
+void HttpClient::set_tls(TlsOptions tls) {
+  std::lock_guard<std::mutex> g(st_->mu);
+  bool en = st_->tls.enabled;
+  st_->tls = std::move(tls);
+  st_->tls.enabled = en;
+  st_->idle.clear();
+}
+
+void HttpClient::set_keepalive(bool on) {
+  std::lock_guard<std::mutex> g(st_->mu);
+  st_->keepalive = on;
+  if (!on) st_->idle.clear();
+}
+
+void HttpClient::set_proxy(ProxyConfig p) {
+  std::lock_guard<std::mutex> g(st_->mu);
+  st_->proxy = std::move(p);
+  st_->idle.clear();
+}
+
+size_t HttpClient::idle_connections() const {
+  std::lock_guard<std::mutex> g(st_->mu);
+  return st_->idle.size();
+}
+
+void HttpClient::close_idle() {
+  std::vector<std::unique_ptr<Conn>> drop;
+  std::lock_guard<std::mutex> g(st_->mu);
+  drop.swap(st_->idle);
 }
 
 std::unique_ptr<Conn> HttpClient::connect() {
-  if (!url_.unix_path.empty()) return dial_unix(url_.unix_path);
-  return dial_tcp(url_.host, url_.port, tls_);
+  if (!url_.unix_path.empty()) {
+    auto c = dial_unix(url_.unix_path);
+    stats().tcp_dials++;  // counted as a dial for reuse statistics
+    return c;
+  }
+  TlsOptions tls;
+  std::string proxy;
+  {
+    std::lock_guard<std::mutex> g(st_->mu);
+    tls = st_->tls;
+    proxy = st_->proxy.proxy_for(url_.scheme, url_.host, url_.port);
+  }
+  return dial_tcp(url_.host, url_.port, tls, 15000, proxy);
 }
 
-bool read_response_head(Conn& c, Response* r, std::string* rest, int timeout_ms) {
+std::unique_ptr<Conn> HttpClient::take_conn(bool* reused) {
+  std::vector<std::unique_ptr<Conn>> dead;
+  {
+    std::lock_guard<std::mutex> g(st_->mu);
+    while (!st_->idle.empty()) {
+      std::unique_ptr<Conn> c = std::move(st_->idle.back());
+      st_->idle.pop_back();
+      if (c->stale()) {
+        dead.push_back(std::move(c));
+        continue;
+      }
+      *reused = true;
+      stats().reused++;
+      return c;
+    }
+  }
+  *reused = false;
+  return connect();
+}
+
+void HttpClient::put_conn(std::unique_ptr<Conn> c) {
+  std::lock_guard<std::mutex> g(st_->mu);
+  if (!st_->keepalive || st_->idle.size() >= st_->max_idle) return;
+  st_->idle.push_back(std::move(c));
+}
+
+namespace {
+
+bool read_head(Conn& c, Response* r, std::string* rest, int timeout_ms, bool* got_any) {
   std::string buf = *rest;
   rest->clear();
   size_t end;
@@ -337,6 +694,7 @@ bool read_response_head(Conn& c, Response* r, std::string* rest, int timeout_ms)
     char tmp[8192];
     ssize_t n = c.read(tmp, sizeof(tmp), timeout_ms);
     if (n <= 0) return false;
+    if (got_any) *got_any = true;
     buf.append(tmp, (size_t)n);
     if (buf.size() > (1 << 20)) return false;
   }
@@ -346,6 +704,7 @@ bool read_response_head(Conn& c, Response* r, std::string* rest, int timeout_ms)
   if (lines.empty()) return false;
   auto sl = split(lines[0], " ");
   if (sl.size() < 2) return false;
+  r->version = sl[0];
   r->status = std::atoi(sl[1].c_str());
   if (sl.size() > 2) {
     std::vector<std::string> reason(sl.begin() + 2, sl.end());
@@ -359,73 +718,140 @@ bool read_response_head(Conn& c, Response* r, std::string* rest, int timeout_ms)
   return true;
 }
 
-static std::string build_request(const HttpClient& h, const Request& r) {
-  std::string base = h.url().path;
+std::string build_request(const Url& url, const std::map<std::string, std::string>& defaults, const Request& r,
+                          bool keepalive) {
+  std::string base = url.path;
   if (!base.empty() && base.back() == '/' && !r.path.empty() && r.path[0] == '/') base.pop_back();
   std::string path = base + r.path;
   if (path.empty()) path = "/";
-  std::string host = h.url().unix_path.empty() ? h.url().host : "localhost";
+  std::string host = url.unix_path.empty() ? url.host : "localhost";
+  if (url.unix_path.empty()) {
+    bool default_port = (url.port == 443 && (url.scheme == "https" || url.scheme == "wss")) ||
+                        (url.port == 80 && (url.scheme == "http" || url.scheme == "ws"));
+    if (!default_port && url.port) host = host_port(url.host, url.port);
+  }
   std::string out = r.method + " " + path + " HTTP/1.1\r\nHost: " + host + "\r\n";
-  std::map<std::string, std::string> hdrs;
-  for (auto& kv : h.default_headers()) hdrs[kv.first] = kv.second;
+  std::map<std::string, std::string> hdrs = defaults;
   for (auto& kv : r.headers) hdrs[kv.first] = kv.second;
   for (auto& kv : hdrs) out += kv.first + ": " + kv.second + "\r\n";
   if (!hdrs.count("Content-Length") && (!r.body.empty() || r.method == "POST" || r.method == "PUT" || r.method == "PATCH"))
     out += "Content-Length: " + std::to_string(r.body.size()) + "\r\n";
-  if (!hdrs.count("Connection")) out += "Connection: close\r\n";
+  if (!hdrs.count("Connection") && !keepalive) out += "Connection: close\r\n";
   out += "\r\n";
   return out;
 }
 
+}  // namespace
+
+bool read_response_head(Conn& c, Response* r, std::string* rest, int timeout_ms) {
+  return read_head(c, r, rest, timeout_ms, nullptr);
+}
+
 Response HttpClient::stream(Request r, const std::function<bool(const std::string&)>& on_data) {
-  auto c = connect();
-  if (!c->write_all(build_request(*this, r)) || (!r.body.empty() && !c->write_all(r.body)))
-    throw NetError("write request failed");
+  stats().requests++;
+  std::map<std::string, std::string> defaults;
+  bool keepalive;
+  {
+    std::lock_guard<std::mutex> g(st_->mu);
+    defaults = st_->headers;
+    keepalive = st_->keepalive;
+  }
+  std::string head = build_request(url_, defaults, r, keepalive);
+  std::unique_ptr<Conn> c;
   Response resp;
   std::string rest;
-  if (!read_response_head(*c, &resp, &rest, r.timeout_ms)) throw NetError("read response failed: " + r.path);
+  for (int attempt = 0;; ++attempt) {
+    bool reused = false;
+    c = take_conn(&reused);
+    bool wrote = c->write_all(head) && (r.body.empty() || c->write_all(r.body));
+    bool got_any = false;
+    resp = Response();
+    rest.clear();
+    if (wrote && read_head(*c, &resp, &rest, r.timeout_ms, &got_any)) break;
+    // a pooled connection the server closed while idle: retry once on a fresh one
+    if (reused && !got_any && attempt == 0) continue;
+    if (!wrote) throw NetError("write request failed: " + r.method + " " + r.path);
+    throw NetError("read response failed: " + r.path);
+  }
+  bool reusable = keepalive && resp.version == "HTTP/1.1" &&
+                  to_lower(resp.header("connection")).find("close") == std::string::npos;
+  if (r.method == "HEAD" || resp.status == 204 || resp.status == 304 || (resp.status >= 100 && resp.status < 200)) {
+    if (reusable && rest.empty()) put_conn(std::move(c));
+    return resp;
+  }
   bool chunked = to_lower(resp.header("transfer-encoding")).find("chunked") != std::string::npos;
   std::string cl = resp.header("content-length");
   int64_t remaining = cl.empty() ? -1 : std::atoll(cl.c_str());
-  if (r.method == "HEAD" || resp.status == 204 || resp.status == 304) return resp;
   auto deliver = [&](const std::string& d) { return d.empty() || on_data(d); };
   char tmp[65536];
   if (chunked) {
-    std::string buf = rest;
-    while (true) {
+    std::string buf = std::move(rest);
+    size_t off = 0;  // consumed prefix of buf
+    auto need = [&](size_t bytes) {
+      while (buf.size() - off < bytes) {
+        ssize_t n = c->read(tmp, sizeof(tmp), r.timeout_ms);
+        if (n <= 0) return false;
+        buf.append(tmp, (size_t)n);
+      }
+      return true;
+    };
+    auto line = [&](std::string* out) {
       size_t le;
-      while ((le = buf.find("\r\n")) == std::string::npos) {
+      while ((le = buf.find("\r\n", off)) == std::string::npos) {
         ssize_t n = c->read(tmp, sizeof(tmp), r.timeout_ms);
-        if (n <= 0) return resp;
+        if (n <= 0) return false;
         buf.append(tmp, (size_t)n);
       }
-      size_t sz = std::strtoul(buf.substr(0, le).c_str(), nullptr, 16);
-      buf.erase(0, le + 2);
-      if (sz == 0) return resp;
-      while (buf.size() < sz + 2) {
-        ssize_t n = c->read(tmp, sizeof(tmp), r.timeout_ms);
-        if (n <= 0) {
-          deliver(buf.substr(0, std::min(buf.size(), sz)));
-          return resp;
+      *out = buf.substr(off, le - off);
+      off = le + 2;
+      return true;
+    };
+    while (true) {
+      std::string sz_line;
+      if (!line(&sz_line)) return resp;
+      size_t sz = std::strtoul(sz_line.c_str(), nullptr, 16);
+      if (sz == 0) {
+        std::string trailer;
+        while (line(&trailer) && !trailer.empty()) {
         }
-        buf.append(tmp, (size_t)n);
+        if (trailer.empty() && off == buf.size() && reusable) put_conn(std::move(c));
+        return resp;
       }
-      if (!deliver(buf.substr(0, sz))) return resp;
-      buf.erase(0, sz + 2);
+      if (!need(sz + 2)) {
+        deliver(buf.substr(off, std::min(buf.size() - off, sz)));
+        return resp;
+      }
+      if (!deliver(buf.substr(off, sz))) return resp;
+      off += sz + 2;
+      if (off > (1 << 20)) {
+        buf.erase(0, off);
+        off = 0;
+      }
     }
   }
   if (!rest.empty()) {
-    if (remaining >= 0 && (int64_t)rest.size() > remaining) rest.resize((size_t)remaining);
+    if (remaining >= 0 && (int64_t)rest.size() > remaining) {
+      rest.resize((size_t)remaining);
+      reusable = false;
+    }
     if (remaining >= 0) remaining -= (int64_t)rest.size();
     if (!deliver(rest)) return resp;
   }
+  if (remaining < 0) reusable = false;  // body delimited by EOF
   while (remaining != 0) {
     size_t want = remaining > 0 ? (size_t)std::min<int64_t>(remaining, (int64_t)sizeof(tmp)) : sizeof(tmp);
     ssize_t n = c->read(tmp, want, r.timeout_ms);
-    if (n <= 0) break;
+    if (n <= 0) {
+      reusable = false;
+      break;
+    }
     if (remaining > 0) remaining -= n;
-    if (!deliver(std::string(tmp, (size_t)n))) break;
+    if (!deliver(std::string(tmp, (size_t)n))) {
+      if (remaining != 0) reusable = false;
+      break;
+    }
   }
+  if (reusable && remaining == 0) put_conn(std::move(c));
   return resp;
 }
 
@@ -441,6 +867,13 @@ Response HttpClient::request(Request r) {
 
 // ---------------------------------------------------------------- websocket
 
+std::string websocket_accept(const std::string& key) {
+  std::string in = key + "258EAFA5-E914-47DA-95CA-C5AB0DC85B11";
+  unsigned char md[SHA_DIGEST_LENGTH];
+  SHA1((const unsigned char*)in.data(), in.size(), md);
+  return base64_encode(std::string((const char*)md, sizeof(md)));
+}
+
 std::unique_ptr<WebSocket> WebSocket::connect(HttpClient& http, const std::string& path,
                                               const std::vector<std::string>& protocols, int timeout_ms) {
   auto c = http.connect();
@@ -453,7 +886,7 @@ std::unique_ptr<WebSocket> WebSocket::connect(HttpClient& http, const std::strin
                {"Sec-WebSocket-Version", "13"},
                {"Sec-WebSocket-Key", key}};
   if (!protocols.empty()) r.headers.push_back({"Sec-WebSocket-Protocol", join(protocols, ", ")});
-  std::string req = build_request(http, r);
+  std::string req = build_request(http.url(), http.default_headers(), r, true);
   if (!c->write_all(req)) throw NetError("websocket: write handshake failed");
   Response resp;
   std::string rest;
@@ -469,8 +902,8 @@ std::unique_ptr<WebSocket> WebSocket::connect(HttpClient& http, const std::strin
     }
     throw NetError("websocket upgrade failed: " + std::to_string(resp.status) + " " + resp.reason + ": " + body);
   }
-  Sha256 h;
-  (void)h;
+  if (resp.header("sec-websocket-accept") != websocket_accept(key))
+    throw NetError("websocket upgrade failed: bad Sec-WebSocket-Accept from server");
   auto ws = std::make_unique<WebSocket>(std::move(c), rest);
   ws->protocol_ = resp.header("sec-websocket-protocol");
   return ws;
@@ -484,8 +917,9 @@ bool WebSocket::send(const std::string& payload, Op op) {
   std::lock_guard<std::mutex> g(wmu_);
   if (closed_) return false;
   std::string f;
-  f.push_back((char)(0x80 | op));
   size_t n = payload.size();
+  f.reserve(n + 14);
+  f.push_back((char)(0x80 | op));
   if (n < 126) {
     f.push_back((char)(0x80 | n));
   } else if (n < 65536) {
@@ -500,19 +934,30 @@ bool WebSocket::send(const std::string& payload, Op op) {
   f += mask;
   size_t off = f.size();
   f.resize(off + n);
-  for (size_t i = 0; i < n; ++i) f[off + i] = (char)(payload[i] ^ mask[i & 3]);
+  const unsigned char* m = (const unsigned char*)mask.data();
+  const unsigned char* src = (const unsigned char*)payload.data();
+  unsigned char* dst = (unsigned char*)&f[off];
+  for (size_t i = 0; i < n; ++i) dst[i] = src[i] ^ m[i & 3];
   return c_->write_all(f);
 }
 
 bool WebSocket::read_exact(char* out, size_t n, int timeout_ms) {
-  while (buf_.size() < n) {
+  while (buf_.size() - buf_off_ < n) {
+    if (buf_off_ > 0 && buf_off_ >= buf_.size() / 2) {
+      buf_.erase(0, buf_off_);
+      buf_off_ = 0;
+    }
     char tmp[65536];
     ssize_t r = c_->read(tmp, sizeof(tmp), timeout_ms);
     if (r <= 0) return false;
     buf_.append(tmp, (size_t)r);
   }
-  std::memcpy(out, buf_.data(), n);
-  buf_.erase(0, n);
+  std::memcpy(out, buf_.data() + buf_off_, n);
+  buf_off_ += n;
+  if (buf_off_ == buf_.size()) {
+    buf_.clear();
+    buf_off_ = 0;
+  }
   return true;
 }
 
@@ -536,6 +981,13 @@ bool WebSocket::recv(std::string* payload, Op* op_out, int timeout_ms) {
       len = 0;
       for (int i = 0; i < 8; ++i) len = (len << 8) | e[i];
     }
+    if (len > kMaxFrame || msg.size() + len > kMaxFrame) {
+      // a frame this size is not a Kubernetes stream message: refuse instead of allocating it
+      send(std::string("\x03\xf1", 2), Close);  // 1009 message too big
+      std::lock_guard<std::mutex> g(wmu_);
+      closed_ = true;
+      return false;
+    }
     char mask[4] = {0, 0, 0, 0};
     if (masked && !read_exact(mask, 4, timeout_ms)) return false;
     std::string data(len, '\0');
@@ -543,6 +995,8 @@ bool WebSocket::recv(std::string* payload, Op* op_out, int timeout_ms) {
     if (masked)
       for (size_t i = 0; i < len; ++i) data[i] ^= mask[i & 3];
     if (op == Close) {
+      if (data.size() >= 2) close_code_ = ((unsigned char)data[0] << 8) | (unsigned char)data[1];
+      send(data.substr(0, 2), Close);  // echo the close (RFC 6455 §5.5.1)
       std::lock_guard<std::mutex> g(wmu_);
       closed_ = true;
       return false;

@@ -140,6 +140,21 @@ inline std::string shell_quote(const std::string& s) {
   return out;
 }
 
+// %XX decoding (userinfo of proxy URLs, query values).
+inline std::string url_decode(const std::string& s) {
+  std::string out;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size() && std::isxdigit((unsigned char)s[i + 1]) &&
+        std::isxdigit((unsigned char)s[i + 2])) {
+      out.push_back((char)std::stoi(s.substr(i + 1, 2), nullptr, 16));
+      i += 2;
+    } else {
+      out.push_back(s[i]);
+    }
+  }
+  return out;
+}
+
 template <typename... Args>
 std::string cat(Args&&... args) {
   std::ostringstream os;

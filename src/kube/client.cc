@@ -427,7 +427,7 @@ std::unique_ptr<ExecSession> Client::exec(const std::string& ns, const std::stri
                                           const std::vector<std::string>& cmd, bool tty, bool stdin) {
   std::string path = "/api/v1/namespaces/" + ns + "/pods/" + pod + "/exec" +
                      exec_query(container, cmd, tty, stdin, true, !tty);
-  auto ws = net::WebSocket::connect(http_, path, {"v4.channel.k8s.io", "channel.k8s.io"});
+  auto ws = net::WebSocket::connect(http_, path, {"v5.channel.k8s.io", "v4.channel.k8s.io", "channel.k8s.io"});
   return std::make_unique<ExecSession>(std::move(ws), tty);
 }
 
@@ -461,7 +461,12 @@ void ExecSession::pump_in() {
   buf[0] = 0;  // stdin channel
   while (true) {
     ssize_t n = read_some(in_r_.get(), buf + 1, sizeof(buf) - 1);
-    if (n <= 0) break;
+    if (n <= 0) {
+      // v5.channel.k8s.io (k8s >= 1.30) can half-close stdin: CLOSE signal [255, stream id].
+      // Older protocols have no EOF on stdin (as with kubectl over WebSockets).
+      if (n == 0 && ws_->protocol() == "v5.channel.k8s.io") ws_->send(std::string("\xff\x00", 2));
+      break;
+    }
     if (!ws_->send(std::string(buf, (size_t)n + 1))) break;
   }
 }
