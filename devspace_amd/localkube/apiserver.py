@@ -13,12 +13,15 @@ import fcntl
 import json
 import os
 import pty
+import copy
 import struct
 import termios
+import time
 
+import yaml
 from aiohttp import WSMsgType, web
 
-from .store import CLUSTER_SCOPED, ApiError
+from .store import CLUSTER_SCOPED, ApiError, labels_match, parse_selector
 
 GROUP_KINDS = {
     "apps": {"deployments", "statefulsets", "replicasets", "daemonsets", "controllerrevisions"},
@@ -100,6 +103,8 @@ class ApiServer:
             m = request.method
             if name is None:
                 if m == "GET":
+                    if request.query.get("watch") in ("1", "true"):
+                        return await self.watch(request, group, resource, ns)
                     return self.list(request, group, resource, ns, api_version)
                 if m == "POST":
                     body = await request.json()
@@ -125,8 +130,21 @@ class ApiServer:
                     body = await request.json()
                     return web.json_response(self.store.replace(group, resource, ns, name, body))
                 if m == "PATCH":
-                    body = await request.json()
-                    return web.json_response(self.store.patch(group, resource, ns, name, body))
+                    ct = request.content_type
+                    if ct == "application/apply-patch+yaml":
+                        manager = request.query.get("fieldManager")
+                        if not manager:
+                            raise ApiError(400, "BadRequest", "PATCH apply-patch+yaml requires fieldManager")
+                        body = yaml.safe_load(await request.text())
+                        obj, created = self.store.apply(group, resource, ns or "default", name, body, manager,
+                                                        request.query.get("force") in ("true", "1"), api_version)
+                        return web.json_response(obj, status=201 if created else 200)
+                    if ct in ("application/merge-patch+json", "application/strategic-merge-patch+json",
+                              "application/json"):
+                        body = await request.json()
+                        return web.json_response(self.store.patch(
+                            group, resource, ns, name, body, strategic=ct == "application/strategic-merge-patch+json"))
+                    raise ApiError(415, "UnsupportedMediaType", f"the body of the request was in an unknown format: {ct}")
                 if m == "DELETE":
                     o = self._delete(group, resource, ns, name)
                     return web.json_response(o)
@@ -140,6 +158,8 @@ class ApiServer:
     def _delete(self, group, resource, ns, name):
         if resource == "pods":
             return self.store.mark_deleting(group, resource, ns, name)
+        if resource == "persistentvolumeclaims":  # pvc-protection: finalized by the kubelet
+            return self.store.delete_or_finalize(group, resource, ns, name)
         obj = self.store.get(group, resource, ns, name)
         if resource == "namespaces":
             for (g, r, n, nm), _ in list(self.store.objs.items()):
@@ -178,10 +198,121 @@ class ApiServer:
                         return False
                 return True
 
-        items = self.store.list(group, resource, ns, request.query.get("labelSelector", ""), field)
+        with self.store.lock:
+            items = self.store.list(group, resource, ns, request.query.get("labelSelector", ""), field)
+            rv = str(self.store.last_rv)
         kind = (items[0]["kind"] if items else resource[:1].upper() + resource[1:-1]) + "List"
-        return web.json_response({"kind": kind, "apiVersion": api_version, "metadata": {"resourceVersion": "1"},
+        return web.json_response({"kind": kind, "apiVersion": api_version, "metadata": {"resourceVersion": rv},
                                   "items": items})
+
+    @staticmethod
+    def _field_filter(request):
+        fs = request.query.get("fieldSelector", "")
+        conds = [c.split("=", 1) for c in fs.split(",") if "=" in c]
+
+        def match(o):
+            for k, v in conds:
+                cur = o
+                for part in k.split("."):
+                    cur = cur.get(part, {}) if isinstance(cur, dict) else {}
+                if str(cur) != v:
+                    return False
+            return True
+
+        return match
+
+    # ------------------------------------------------------------------ watch
+
+    async def watch(self, request, group, resource, ns):
+        """?watch=1: newline-delimited WatchEvents, resumable from resourceVersion (410 when
+        the backlog no longer reaches back that far), ended after timeoutSeconds."""
+        reqs = parse_selector(request.query.get("labelSelector", ""))
+        field = self._field_filter(request)
+        timeout = float(request.query.get("timeoutSeconds", "1800") or 1800)
+        rv = request.query.get("resourceVersion", "")
+        loop = asyncio.get_running_loop()
+        q = asyncio.Queue()
+
+        def in_scope(key):
+            return key[0] == group and key[1] == resource and (
+                not ns or resource in CLUSTER_SCOPED or key[2] == ns)
+
+        def listener(ev, key, obj):
+            if in_scope(key):
+                loop.call_soon_threadsafe(q.put_nowait, (ev, key, copy.deepcopy(obj)))
+
+        def matches(o):
+            return labels_match((o.get("metadata") or {}).get("labels"), reqs) and field(o)
+
+        with self.store.lock:
+            self.store.listeners.append(listener)
+            if rv in ("", "0"):
+                backlog = [("ADDED", None, o) for o in self.store.list(group, resource, ns)]
+            else:
+                try:
+                    backlog = self.store.events_since(int(rv))
+                except ValueError:
+                    backlog = None
+                if backlog is not None:
+                    backlog = [(e, k, o) for (e, k, o) in backlog if in_scope(k)]
+            current = {(o["metadata"].get("namespace", ""), o["metadata"]["name"])
+                       for o in self.store.list(group, resource, ns) if matches(o)}
+        resp = web.StreamResponse(headers={"Content-Type": "application/json"})
+        resp.enable_chunked_encoding()
+        await resp.prepare(request)
+        visible = set(current) if rv not in ("", "0") else set()
+
+        async def send(ev, obj):
+            await resp.write((json.dumps({"type": ev, "object": obj}) + "\n").encode())
+
+        async def emit(ev, obj):
+            k = (obj["metadata"].get("namespace", ""), obj["metadata"]["name"])
+            if ev == "DELETED":
+                if k in visible or matches(obj):
+                    visible.discard(k)
+                    await send("DELETED", obj)
+                return
+            if matches(obj):
+                await send("MODIFIED" if k in visible and ev != "ADDED" else "ADDED", obj)
+                visible.add(k)
+            elif k in visible:  # no longer selected
+                visible.discard(k)
+                await send("DELETED", obj)
+
+        try:
+            if backlog is None:
+                await send("ERROR", {"kind": "Status", "apiVersion": "v1", "status": "Failure", "reason": "Expired",
+                                     "code": 410, "message": f"too old resource version: {rv}"})
+                return resp
+            for ev, _, obj in backlog:
+                await emit(ev, obj)
+            deadline = time.monotonic() + timeout
+            while True:
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    break
+                try:
+                    ev, _, obj = await asyncio.wait_for(q.get(), min(left, 0.25))
+                except asyncio.TimeoutError:
+                    # aiohttp does not cancel handlers when the client goes away: notice it here
+                    tr = request.transport
+                    if tr is None or tr.is_closing():
+                        break
+                    continue
+                if rv not in ("", "0") and int(obj["metadata"].get("resourceVersion", "0") or 0) <= int(rv):
+                    continue  # already replayed from the backlog
+                await emit(ev, obj)
+        except (ConnectionResetError, asyncio.CancelledError):
+            pass
+        finally:
+            with self.store.lock:
+                if listener in self.store.listeners:
+                    self.store.listeners.remove(listener)
+        try:
+            await resp.write_eof()
+        except ConnectionResetError:
+            pass
+        return resp
 
     # ------------------------------------------------------------------ logs
 
@@ -212,6 +343,9 @@ class ApiServer:
                 try:
                     off, chunk = await asyncio.wait_for(q.get(), 0.5)
                 except asyncio.TimeoutError:
+                    tr = request.transport
+                    if tr is None or tr.is_closing():  # follower went away
+                        break
                     continue
                 if off is None:
                     continue  # process ended; a restarted container keeps appending

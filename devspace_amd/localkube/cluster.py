@@ -166,10 +166,16 @@ class LocalCluster:
 
     def start(self):
         def run():
-            self.loop = asyncio.new_event_loop()
-            asyncio.set_event_loop(self.loop)
-            self.loop.run_until_complete(self._amain())
-            self.loop.run_forever()
+            loop = asyncio.new_event_loop()
+            self.loop = loop
+            asyncio.set_event_loop(loop)
+            loop.run_until_complete(self._amain())
+            loop.run_forever()
+            # stop() ran shutdown(): close transports and the loop from the loop's own thread
+            try:
+                loop.run_until_complete(loop.shutdown_asyncgens())
+            finally:
+                loop.close()
 
         self.thread = threading.Thread(target=run, daemon=True, name="localkube")
         self.thread.start()
@@ -187,6 +193,15 @@ class LocalCluster:
                 self._kubelet_task.cancel()
             for r in self._runners:
                 await r.cleanup()
+            # every task still pending (container output pumps, log followers, watches) is
+            # cancelled and awaited here, so nothing is destroyed pending when the loop closes
+            me = asyncio.current_task()
+            rest = [t for t in asyncio.all_tasks() if t is not me and not t.done()]
+            for t in rest:
+                t.cancel()
+            if rest:  # bounded: a handler that swallows one cancellation must not hang stop()
+                await asyncio.wait(rest, timeout=2.0)
+            await asyncio.sleep(0)  # let subprocess transports deliver their connection_lost
 
         fut = asyncio.run_coroutine_threadsafe(shutdown(), self.loop)
         try:

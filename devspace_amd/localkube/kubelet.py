@@ -259,10 +259,35 @@ class Kubelet:
             self.store.update_status(group, resource, ns, md["name"], status)
 
     def reconcile_pvcs(self):
+        """PV binder + pvc-protection: bind new claims to a local volume (the binder writes
+        spec.volumeName, as on a real cluster), release a deleted claim once no pod uses it."""
         for pvc in self.store.list("", "persistentvolumeclaims"):
+            md = pvc["metadata"]
+            ns, name = md["namespace"], md["name"]
+            if md.get("deletionTimestamp"):
+                in_use = any(
+                    v.get("persistentVolumeClaim", {}).get("claimName") == name
+                    for p in self.store.list("", "pods", ns)
+                    for v in (p.get("spec") or {}).get("volumes") or [])
+                if not in_use:
+                    try:
+                        self.store.delete("", "persistentvolumeclaims", ns, name)
+                    except ApiError:
+                        pass
+                continue
+            if not (pvc.get("spec") or {}).get("volumeName"):
+                vol = "pvc-" + md["uid"]
+
+                def bind(o, vol=vol):
+                    o.setdefault("spec", {})["volumeName"] = vol
+                    o.setdefault("metadata", {}).setdefault("annotations", {})[
+                        "pv.kubernetes.io/bind-completed"] = "yes"
+
+                self.store.mutate("", "persistentvolumeclaims", ns, name, bind)
             if (pvc.get("status") or {}).get("phase") != "Bound":
-                self.store.update_status("", "persistentvolumeclaims", pvc["metadata"]["namespace"],
-                                         pvc["metadata"]["name"], {"phase": "Bound"})
+                self.store.update_status("", "persistentvolumeclaims", ns, name,
+                                         {"phase": "Bound", "accessModes": (pvc.get("spec") or {}).get("accessModes"),
+                                          "capacity": ((pvc.get("spec") or {}).get("resources") or {}).get("requests")})
 
     # ------------------------------------------------------------ pods
 

@@ -3,6 +3,7 @@
 #include <time.h>
 
 #include <chrono>
+#include <map>
 #include <regex>
 #include <thread>
 
@@ -76,6 +77,87 @@ static int64_t gpu_request(const Value& pod) {
   return n;
 }
 
+// In-pod GPU probe that depends on nothing but a POSIX shell: device nodes, ROCm tools, and —
+// when python3 is there — the devspace gfx950 probe kernels (devspace_amd.gpucheck) or, in a
+// stock rocm/pytorch image without devspace_amd, a torch/HIP check (device count, arch, a bf16
+// matmul checked against fp32). Prints KEY=VALUE lines and at most one JSON report.
+const char* const kGpuProbeScript = R"SH(
+if [ -e /dev/kfd ]; then echo KFD=yes; else echo KFD=no; fi
+n=0; for d in /dev/dri/renderD*; do [ -e "$d" ] && n=$((n+1)); done; echo RENDER=$n
+echo "VISIBLE=${HIP_VISIBLE_DEVICES:-${ROCR_VISIBLE_DEVICES:-}}"
+if command -v rocminfo >/dev/null 2>&1; then echo "ROCMINFO=$(rocminfo 2>/dev/null | grep -c 'Name: *gfx')"; else echo ROCMINFO=absent; fi
+if command -v python3 >/dev/null 2>&1; then
+  if python3 -c 'import devspace_amd.gpucheck' >/dev/null 2>&1; then
+    echo PROBE=devspace; python3 -m devspace_amd.gpucheck --quick --json 2>/dev/null
+  else
+    echo PROBE=torch; python3 - <<'PY' 2>/dev/null || echo PROBE_FAILED=1
+import json
+rep = {"devices": [], "problems": []}
+try:
+    import torch
+except Exception as e:
+    rep["problems"].append("PyTorch is not importable (%s): only device nodes were checked" % e.__class__.__name__)
+    print(json.dumps(rep)); raise SystemExit(0)
+if not getattr(torch.version, "hip", None):
+    rep["problems"].append("PyTorch build is not ROCm (torch.version.hip is empty)")
+if not torch.cuda.is_available():
+    rep["problems"].append("torch.cuda.is_available() is False: the HIP runtime sees no GPU")
+else:
+    for i in range(torch.cuda.device_count()):
+        p = torch.cuda.get_device_properties(i)
+        d = {"index": i, "name": p.name, "arch": getattr(p, "gcnArchName", ""), "hbm_gb": round(p.total_memory / 1e9, 1)}
+        try:
+            a = torch.randn(256, 256, device="cuda:%d" % i)
+            b = torch.randn(256, 256, device="cuda:%d" % i)
+            ref = (a.cpu() @ b.cpu())
+            got = (a.bfloat16() @ b.bfloat16()).float().cpu()
+            err = float((got - ref).abs().max() / ref.abs().max())
+            d["matmul_rel_err"] = err
+            if err > 5e-2:
+                rep["problems"].append("GPU %d bf16 matmul mismatch (rel err %.3g)" % (i, err))
+        except Exception as e:
+            rep["problems"].append("GPU %d kernel launch failed: %s" % (i, e))
+        rep["devices"].append(d)
+print(json.dumps(rep))
+PY
+  fi
+else
+  echo PROBE=unavailable
+fi
+)SH";
+
+std::vector<std::string> probe_pod_gpus(kube::Client& k, const std::string& ns, const std::string& pod,
+                                        const std::string& container) {
+  auto s = k.exec(ns, pod, container, {"sh", "-c", kGpuProbeScript}, false, false);
+  s->close_stdin_if_any();
+  std::string outp = read_all(s->out());
+  s->wait(60000);
+  std::map<std::string, std::string> kv;
+  std::string json_text;
+  for (auto& line : split(outp, "\n")) {
+    std::string t = trim(line);
+    if (t.empty()) continue;
+    if (t[0] == '{') {
+      json_text = t;
+      continue;
+    }
+    size_t eq = t.find('=');
+    if (eq != std::string::npos && eq < 20) kv[t.substr(0, eq)] = t.substr(eq + 1);
+  }
+  std::vector<std::string> problems;
+  if (kv["KFD"] == "no")
+    problems.push_back("no /dev/kfd in the container (GPU not attached: amd.com/gpu request / device plugin?)");
+  else if (kv["RENDER"] == "0")
+    problems.push_back("/dev/kfd present but no /dev/dri/renderD* nodes (GPU not attached)");
+  if (!json_text.empty()) {
+    Value rep = json_parse(json_text);
+    for (auto& pr : rep.get("problems").items()) problems.push_back(pr.as_string());
+  } else if (kv["PROBE"] == "unavailable" || kv.count("PROBE_FAILED") || kv["PROBE"].empty()) {
+    problems.push_back("GPU probe unavailable (no python3 in the image): only device nodes were checked");
+  }
+  return problems;
+}
+
 std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, const std::vector<Value>& pods,
                                       const Options& o) {
   std::vector<std::string> out;
@@ -126,20 +208,11 @@ std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, co
     if (o.gpu_probe && kube::pod_status(p) == "Running") {
       std::string c = p.at_path("spec.containers")[0].get("name").as_string();
       try {
-        auto s = k.exec(ns, name, c, {"sh", "-c", "ls /dev/kfd >/dev/null 2>&1 || echo NOKFD; python3 -m devspace_amd.gpucheck --quick --json 2>/dev/null || true"}, false, false);
-        s->close_stdin_if_any();
-        std::string outp = read_all(s->out());
-        s->wait(60000);
-        if (contains(outp, "NOKFD") && !contains(outp, "\"devices\": [{"))
-          out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + " has no /dev/kfd (GPU not attached)\n");
-        size_t j = outp.find('{');
-        if (j != std::string::npos) {
-          Value rep = json_parse(outp.substr(j));
-          for (auto& pr : rep.get("problems").items())
-            out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + pr.as_string() + "\n");
-        }
+        for (auto& line : probe_pod_gpus(k, ns, name, c))
+          out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + line + "\n");
       } catch (const std::exception& e) {
-        log::debug(std::string("gpu probe failed: ") + e.what());
+        out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": GPU probe unavailable (" + e.what() +
+                      ")\n");
       }
     }
   }
@@ -149,27 +222,39 @@ std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, co
 std::vector<std::string> pods_problems(kube::Client& k, const std::string& ns, const Options& o,
                                        std::vector<Value>* pods_out) {
   std::vector<std::string> out;
+  // pods.go:50-117 waits (polling) while pods are starting or younger than min_pod_age_s; here
+  // state changes arrive by watch and the age threshold is slept to exactly.
   auto t0 = std::chrono::steady_clock::now();
+  auto deadline = t0 + std::chrono::seconds(o.wait_timeout_s);
   std::vector<Value> pods;
-  while (true) {
-    pods = k.list_pods(ns, "");
-    bool waiting = false;
-    int64_t now = (int64_t)time(nullptr);
-    for (auto& p : pods) {
+  auto state_waiting = [](const std::vector<Value>& ps) {
+    for (auto& p : ps) {
       std::string st = kube::pod_status(p);
-      int64_t age = now - parse_time(p.at_path("metadata.creationTimestamp").as_string());
-      if (st == "ContainerCreating" || st == "Pending" || st == "Terminating" || age < o.min_pod_age_s) {
+      if (st == "ContainerCreating" || st == "Pending" || st == "Terminating") {
         // Pending because of GPU scheduling will not resolve by waiting
-        if (st == "Pending" && contains(p.at_path("status.conditions").size() ? json_dump(p.at_path("status.conditions")) : "",
-                                        "Unschedulable"))
-          continue;
-        waiting = true;
+        if (st == "Pending" && contains(json_dump(p.at_path("status.conditions")), "Unschedulable")) continue;
+        return true;
       }
     }
-    auto el = std::chrono::duration_cast<std::chrono::seconds>(std::chrono::steady_clock::now() - t0).count();
-    if (!o.wait || !waiting || el >= o.wait_timeout_s) break;
+    return false;
+  };
+  while (true) {
+    pods = k.list_pods(ns, "");
+    int64_t now = (int64_t)time(nullptr);
+    int64_t age_wait_s = 0;
+    for (auto& p : pods)
+      age_wait_s = std::max(age_wait_s, o.min_pod_age_s - (now - parse_time(p.at_path("metadata.creationTimestamp").as_string())));
+    bool waiting = state_waiting(pods);
+    int64_t left_ms = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count();
+    if (!o.wait || (!waiting && age_wait_s <= 0) || left_ms <= 0) break;
     log::start_wait("Waiting for pods to become ready");
-    std::this_thread::sleep_for(std::chrono::milliseconds(500));
+    if (!waiting) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(std::min<int64_t>(left_ms, age_wait_s * 1000)));
+      continue;
+    }
+    int64_t budget = age_wait_s > 0 ? std::min<int64_t>(left_ms, age_wait_s * 1000) : left_ms;
+    k.list_watch("/api/v1/namespaces/" + ns + "/pods", "", (int)budget,
+                 [&](const std::vector<Value>& ps) { return !state_waiting(ps); });
   }
   log::stop_wait();
   int64_t now = (int64_t)time(nullptr);

@@ -34,6 +34,11 @@ std::string analyze(kube::Client& k, const std::string& ns, const Options& o);
 std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, const std::vector<Value>& pods,
                                       const Options& o);
 bool log_has_gpu_runtime_error(const std::string& log, std::string* match);
+// Runs the shell-only GPU probe in a container; returns the problems it found (empty = fine).
+// Works in images without devspace_amd (torch check) and without python3 (device nodes only,
+// reported as "probe unavailable").
+std::vector<std::string> probe_pod_gpus(kube::Client& k, const std::string& ns, const std::string& pod,
+                                        const std::string& container);
 
 }  // namespace analyze
 }  // namespace ds

@@ -66,6 +66,12 @@ void connect(Session& s, bool switch_context) {
   }
 }
 
+void set_apply_flags(Session& s, const cli::Command& c) {
+  kube::ApplyOptions ao;
+  ao.recreate_on_immutable = c.get_bool("force-recreate");
+  s.kube->set_apply_options(ao);
+}
+
 void print_space_domain(Session& s) {
   if (s.cfg().at_path("cluster.cloudProvider").is_null()) return;
   config::Generated& g = s.ctx.generated();
@@ -100,6 +106,7 @@ int run_deploy(cli::Command& c, const std::vector<std::string>& args) {
   }
   cloud_configure(s.ctx, args.empty() ? "" : args[0]);
   connect(s, c.get_bool("switch-context"));
+  set_apply_flags(s, c);
   try {
     build::init_registries(s.cfg(), s.kube, ns_of(s));
     pipeline(s, false, c.get_bool("force-build"), c.get_bool("force-deploy"), c.get_str("docker-target"));
@@ -155,6 +162,7 @@ int run_dev(cli::Command& c, const std::vector<std::string>& args) {
   open_project(s, c);
   cloud_configure(s.ctx);
   connect(s, c.get_bool("switch-context"));
+  set_apply_flags(s, c);
   if (c.get_bool("init-registries")) {
     try {
       build::init_registries(s.cfg(), s.kube, ns_of(s));
@@ -418,7 +426,9 @@ void register_core(cli::Command& root) {
         .str("docker-target", "", "", "The docker target to use for building")
         .boolean("switch-context", "", false, "Switches the kube context to the deploy context")
         .boolean("force-build", "b", false, "Forces to (re-)build every image")
-        .boolean("force-deploy", "d", false, "Forces to (re-)deploy every deployment");
+        .boolean("force-deploy", "d", false, "Forces to (re-)deploy every deployment")
+        .boolean("force-recreate", "", false,
+                 "Delete and re-create objects whose immutable fields changed (never PVCs, PVs or namespaces)");
     c->run = run_deploy;
     root.add(std::move(c));
   }
@@ -426,6 +436,8 @@ void register_core(cli::Command& root) {
     c.boolean("init-registries", "", true, "Initialize registries (and install internal one)")
         .boolean("force-build", "b", false, "Forces to build every image")
         .boolean("force-deploy", "d", false, "Forces to deploy every deployment")
+        .boolean("force-recreate", "", false,
+                 "Delete and re-create objects whose immutable fields changed (never PVCs, PVs or namespaces)")
         .boolean("skip-pipeline", "x", false, "Skips build & deployment and only starts sync, portforwarding & terminal")
         .boolean("sync", "", true, "Enable code synchronization")
         .boolean("verbose-sync", "", false, "When enabled the sync will log every file change")

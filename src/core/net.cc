@@ -782,7 +782,14 @@ Response HttpClient::stream(Request r, const std::function<bool(const std::strin
   bool chunked = to_lower(resp.header("transfer-encoding")).find("chunked") != std::string::npos;
   std::string cl = resp.header("content-length");
   int64_t remaining = cl.empty() ? -1 : std::atoll(cl.c_str());
-  auto deliver = [&](const std::string& d) { return d.empty() || on_data(d); };
+  std::string* err_body = r.errors_to_body && resp.status >= 400 ? &resp.body : nullptr;
+  auto deliver = [&](const std::string& d) {
+    if (err_body) {
+      if (err_body->size() < (1u << 20)) *err_body += d;
+      return true;
+    }
+    return d.empty() || on_data(d);
+  };
   char tmp[65536];
   if (chunked) {
     std::string buf = std::move(rest);
@@ -900,7 +907,8 @@ std::unique_ptr<WebSocket> WebSocket::connect(HttpClient& http, const std::strin
       if (n <= 0) break;
       body.append(tmp, (size_t)n);
     }
-    throw NetError("websocket upgrade failed: " + std::to_string(resp.status) + " " + resp.reason + ": " + body);
+    throw UpgradeError(resp.status,
+                       "websocket upgrade failed: " + std::to_string(resp.status) + " " + resp.reason + ": " + body);
   }
   if (resp.header("sec-websocket-accept") != websocket_accept(key))
     throw NetError("websocket upgrade failed: bad Sec-WebSocket-Accept from server");

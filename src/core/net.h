@@ -25,6 +25,12 @@ struct NetError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
+// A WebSocket upgrade answered with a non-101 status (e.g. 401 → refresh credentials).
+struct UpgradeError : NetError {
+  int status;
+  UpgradeError(int st, const std::string& msg) : NetError(msg), status(st) {}
+};
+
 struct TlsOptions {
   bool enabled = false;
   bool insecure = false;
@@ -91,6 +97,8 @@ struct Request {
   std::vector<std::pair<std::string, std::string>> headers;
   std::string body;
   int timeout_ms = 60000;
+  // stream(): for status >= 400 collect the body into Response::body instead of on_data
+  bool errors_to_body = false;
 };
 
 // Endpoint = where to connect + how (base URL, TLS, default headers, proxy). Copies share one

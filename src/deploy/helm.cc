@@ -242,57 +242,51 @@ static std::string object_key(const Value& o) {
          o.at_path("metadata.namespace").as_string() + "/" + o.at_path("metadata.name").as_string();
 }
 
+// Readiness of one workload object as `kubectl rollout status` sees it; "" when ready.
+static std::string not_ready_reason(const std::string& kind, const std::string& name, const std::optional<Value>& cur) {
+  if (!cur) return kind + " " + name + " not found";
+  if (kind == "PersistentVolumeClaim")
+    return cur->at_path("status.phase").as_string() == "Bound" ? "" : "PVC " + name + " not bound";
+  // The controller must have seen the new spec before readiness counts (rollout status).
+  if (kind != "ReplicaSet" &&
+      cur->at_path("status.observedGeneration").as_int(0) < cur->at_path("metadata.generation").as_int(1))
+    return kind + " " + name + ": waiting for the controller to observe generation " +
+           std::to_string(cur->at_path("metadata.generation").as_int(1));
+  int64_t want = cur->at_path("spec.replicas").as_int(1);
+  if (kind == "DaemonSet") want = cur->at_path("status.desiredNumberScheduled").as_int(1);
+  if (kind == "Deployment" && cur->at_path("status.updatedReplicas").as_int(0) < want)
+    return kind + " " + name + ": " + std::to_string(cur->at_path("status.updatedReplicas").as_int(0)) + "/" +
+           std::to_string(want) + " updated";
+  int64_t ready = cur->at_path("status.readyReplicas").as_int(0);
+  if (kind == "DaemonSet") ready = cur->at_path("status.numberReady").as_int(0);
+  if (ready < want) return kind + " " + name + ": " + std::to_string(ready) + "/" + std::to_string(want) + " ready";
+  return "";
+}
+
 std::string Client::wait_ready(const std::vector<Value>& objs, const std::string& ns, int timeout_s) {
-  auto t0 = std::chrono::steady_clock::now();
-  // Back-off polling: a pod that is up within a few ms is seen within a few ms, a slow rollout
-  // costs at most one GET per object every 250 ms (the reference polls through Tiller).
-  int delay_ms = 5;
-  while (true) {
-    std::string pending;
-    for (auto& o : objs) {
-      std::string kind = o.get("kind").as_string();
-      std::string name = o.at_path("metadata.name").as_string();
-      std::string ons = o.at_path("metadata.namespace").as_string(ns);
-      if (kind == "Deployment" || kind == "StatefulSet" || kind == "ReplicaSet" || kind == "DaemonSet") {
-        auto cur = k_->try_get(kube::resource_path(o.get("apiVersion").as_string(), kind, ons, name));
-        if (!cur) {
-          pending = kind + " " + name + " not found";
-          break;
-        }
-        // The controller must have seen the new spec before readiness counts (rollout status).
-        if (kind != "ReplicaSet" &&
-            cur->at_path("status.observedGeneration").as_int(0) < cur->at_path("metadata.generation").as_int(1)) {
-          pending = kind + " " + name + ": waiting for the controller to observe generation " +
-                    std::to_string(cur->at_path("metadata.generation").as_int(1));
-          break;
-        }
-        int64_t want = cur->at_path("spec.replicas").as_int(1);
-        if (kind == "DaemonSet") want = cur->at_path("status.desiredNumberScheduled").as_int(1);
-        if (kind == "Deployment" && cur->at_path("status.updatedReplicas").as_int(0) < want) {
-          pending = kind + " " + name + ": " + std::to_string(cur->at_path("status.updatedReplicas").as_int(0)) + "/" +
-                    std::to_string(want) + " updated";
-          break;
-        }
-        int64_t ready = cur->at_path("status.readyReplicas").as_int(0);
-        if (kind == "DaemonSet") ready = cur->at_path("status.numberReady").as_int(0);
-        if (ready < want) {
-          pending = kind + " " + name + ": " + std::to_string(ready) + "/" + std::to_string(want) + " ready";
-          break;
-        }
-      } else if (kind == "PersistentVolumeClaim") {
-        auto cur = k_->try_get("/api/v1/namespaces/" + ons + "/persistentvolumeclaims/" + name);
-        if (cur && cur->at_path("status.phase").as_string() != "Bound") {
-          pending = "PVC " + name + " not bound";
-          break;
-        }
-      }
-    }
-    if (pending.empty()) return "";
-    auto el = std::chrono::duration_cast<std::chrono::seconds>(std::chrono::steady_clock::now() - t0).count();
-    if (el >= timeout_s) return "timed out waiting for the condition (" + pending + ")";
-    std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
-    delay_ms = std::min(250, delay_ms * 3 / 2 + 1);
+  // One watch per workload object (fieldSelector=metadata.name), in manifest order: the
+  // status change that makes a rollout ready is seen the moment the API server commits it,
+  // with no polling; the total wait is bounded by the slowest object.
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
+  for (auto& o : objs) {
+    std::string kind = o.get("kind").as_string();
+    if (kind != "Deployment" && kind != "StatefulSet" && kind != "ReplicaSet" && kind != "DaemonSet" &&
+        kind != "PersistentVolumeClaim")
+      continue;
+    std::string name = o.at_path("metadata.name").as_string();
+    std::string ons = o.at_path("metadata.namespace").as_string(ns);
+    std::string path = kube::resource_path(o.get("apiVersion").as_string(), kind, ons, name);
+    int64_t left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count();
+    std::string pending = kind + " " + name + " not checked";
+    bool ok = left > 0 && k_->wait_object(path, (int)left, [&](const std::optional<Value>& cur) {
+      // a PVC that is gone (pvc-protection released it) is nothing to wait for
+      if (!cur && kind == "PersistentVolumeClaim") return true;
+      pending = not_ready_reason(kind, name, cur);
+      return pending.empty();
+    });
+    if (!ok) return "timed out waiting for the condition (" + pending + ")";
   }
+  return "";
 }
 
 Release Client::install_or_upgrade(const std::string& name, const std::string& ns_in, const std::string& chart_path,

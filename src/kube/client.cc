@@ -131,25 +131,126 @@ static net::TlsOptions tls_for(const RestConfig& c) {
   t.ca_pem = c.ca_pem;
   t.cert_pem = c.client_cert_pem;
   t.key_pem = c.client_key_pem;
+  t.server_name = c.tls_server_name;
+  return t;
+}
+
+static int64_t unix_now() { return (int64_t)::time(nullptr); }
+
+// RFC 3339 (UTC "Z" or numeric offset) → unix seconds; 0 if unparsable.
+static int64_t parse_rfc3339(const std::string& s) {
+  struct tm tm{};
+  const char* rest = strptime(s.c_str(), "%Y-%m-%dT%H:%M:%S", &tm);
+  if (!rest) return 0;
+  int64_t t = (int64_t)timegm(&tm);
+  while (*rest == '.' || std::isdigit((unsigned char)*rest)) ++rest;  // fractional seconds
+  if (*rest == '+' || *rest == '-') {
+    int sign = *rest == '-' ? -1 : 1;
+    int hh = 0, mm = 0;
+    if (sscanf(rest + 1, "%d:%d", &hh, &mm) >= 1) t -= sign * (hh * 3600 + mm * 60);
+  }
   return t;
 }
 
 Client::Client(RestConfig cfg) : cfg_(std::move(cfg)), http_(cfg_.server, tls_for(cfg_)) {
-  if (cfg_.token.empty() && !cfg_.exec_command.empty()) refresh_exec_token();
-  if (!cfg_.token.empty()) http_.set_header("Authorization", "Bearer " + cfg_.token);
-  if (!cfg_.username.empty())
-    http_.set_header("Authorization", "Basic " + base64_encode(cfg_.username + ":" + cfg_.password));
+  if (!cfg_.proxy_url.empty()) {
+    net::ProxyConfig p;
+    p.https_proxy = p.http_proxy = cfg_.proxy_url;
+    http_.set_proxy(p);
+  }
   http_.set_header("Accept", "application/json");
-  http_.set_header("User-Agent", "devspace-amd/0.1");
+  http_.set_header("User-Agent", "devspace-amd/0.2");
+  std::lock_guard<std::mutex> g(auth_mu_);
+  if (cfg_.token.empty() && !cfg_.exec_command.empty()) refresh_exec_credentials();
+  if (!cfg_.token_file.empty()) token_file_read_ = unix_now();
+  apply_auth_locked();
 }
 
-void Client::refresh_exec_token() {
+void Client::apply_auth_locked() {
+  if (!cfg_.token.empty())
+    http_.set_header("Authorization", "Bearer " + cfg_.token);
+  else if (!cfg_.username.empty())
+    http_.set_header("Authorization", "Basic " + base64_encode(cfg_.username + ":" + cfg_.password));
+}
+
+// client.authentication.k8s.io ExecCredential: the plugin gets KUBERNETES_EXEC_INFO and
+// answers with status.{token | clientCertificateData+clientKeyData, expirationTimestamp}.
+void Client::refresh_exec_credentials() {
   ProcOptions o;
   for (auto& kv : cfg_.exec_env) o.env[kv.first] = kv.second;
-  RunResult r = run(cfg_.exec_command, "", o, 30000);
-  if (r.code != 0) throw std::runtime_error("exec credential plugin failed: " + r.err);
+  Value info = Value::map();
+  info["apiVersion"] = cfg_.exec_api_version;
+  info["kind"] = "ExecCredential";
+  info["spec"]["interactive"] = false;
+  if (cfg_.exec_provide_cluster_info) {
+    info["spec"]["cluster"]["server"] = cfg_.server;
+    if (!cfg_.ca_pem.empty()) info["spec"]["cluster"]["certificate-authority-data"] = base64_encode(cfg_.ca_pem);
+    info["spec"]["cluster"]["insecure-skip-tls-verify"] = cfg_.insecure;
+  }
+  o.env["KUBERNETES_EXEC_INFO"] = json_dump(info);
+  RunResult r;
+  try {
+    r = run(cfg_.exec_command, "", o, 60000);
+  } catch (const std::exception& e) {
+    std::string hint = cfg_.exec_install_hint.empty() ? "" : "\n" + cfg_.exec_install_hint;
+    throw std::runtime_error("exec credential plugin " + cfg_.exec_command[0] + " failed to start: " + e.what() + hint);
+  }
+  if (r.code != 0) {
+    std::string hint = r.code == 127 && !cfg_.exec_install_hint.empty() ? "\n" + cfg_.exec_install_hint : "";
+    throw std::runtime_error("exec credential plugin failed: " + r.err + hint);
+  }
   Value v = json_parse(r.out);
-  cfg_.token = v.at_path("status.token").as_string();
+  const Value& st = v.get("status");
+  std::string tok = st.get("token").as_string();
+  std::string cert = st.get("clientCertificateData").as_string();
+  std::string key = st.get("clientKeyData").as_string();
+  if (tok.empty() && (cert.empty() || key.empty()))
+    throw std::runtime_error("exec credential plugin returned neither a token nor a client certificate");
+  cfg_.token = tok;
+  if (!cert.empty() && !key.empty() && (cert != cfg_.client_cert_pem || key != cfg_.client_key_pem)) {
+    cfg_.client_cert_pem = cert;
+    cfg_.client_key_pem = key;
+    http_.set_tls(tls_for(cfg_));  // new handshakes present the new certificate
+  }
+  std::string exp = st.get("expirationTimestamp").as_string();
+  token_expiry_ = exp.empty() ? 0 : parse_rfc3339(exp);
+  refreshes_++;
+}
+
+void Client::ensure_fresh_credentials() {
+  std::lock_guard<std::mutex> g(auth_mu_);
+  int64_t now = unix_now();
+  if (!cfg_.exec_command.empty() && token_expiry_ > 0 && now >= token_expiry_ - 10) {
+    refresh_exec_credentials();
+    apply_auth_locked();
+  }
+  if (!cfg_.token_file.empty() && now - token_file_read_ >= 60) {
+    std::string t;
+    token_file_read_ = now;
+    if (fs::read_file(cfg_.token_file, &t) && !trim(t).empty() && trim(t) != cfg_.token) {
+      cfg_.token = trim(t);
+      apply_auth_locked();
+    }
+  }
+}
+
+bool Client::refresh_after_unauthorized() {
+  std::lock_guard<std::mutex> g(auth_mu_);
+  if (!cfg_.exec_command.empty()) {
+    refresh_exec_credentials();
+    apply_auth_locked();
+    return true;
+  }
+  if (!cfg_.token_file.empty()) {
+    std::string t;
+    token_file_read_ = unix_now();
+    if (fs::read_file(cfg_.token_file, &t) && trim(t) != cfg_.token) {
+      cfg_.token = trim(t);
+      apply_auth_locked();
+      return true;
+    }
+  }
+  return false;
 }
 
 bool Client::is_local_cluster() const { return contains(cfg_.context, "devspace-local") || contains(cfg_.server, "127.0.0.1"); }
@@ -194,7 +295,10 @@ net::Response Client::raw(const std::string& method, const std::string& path, co
   r.body = body;
   r.timeout_ms = timeout_ms;
   if (!body.empty()) r.headers.push_back({"Content-Type", content_type});
-  return http_.request(r);
+  ensure_fresh_credentials();
+  net::Response resp = http_.request(r);
+  if (resp.status == 401 && refresh_after_unauthorized()) resp = http_.request(r);
+  return resp;
 }
 
 static Value check(const net::Response& r, const std::string& what) {
@@ -242,7 +346,12 @@ int Client::stream(const std::string& path, const std::function<bool(const std::
   net::Request r;
   r.path = path;
   r.timeout_ms = timeout_ms;
-  return http_.stream(r, on_data).status;
+  r.errors_to_body = true;
+  ensure_fresh_credentials();
+  net::Response resp = http_.stream(r, on_data);
+  if (resp.status == 401 && refresh_after_unauthorized()) resp = http_.stream(r, on_data);
+  if (resp.status >= 400) check(resp, "GET " + path);
+  return resp.status;
 }
 
 std::vector<Value> Client::list_pods(const std::string& ns, const std::string& sel) {
@@ -252,29 +361,176 @@ std::vector<Value> Client::list_pods(const std::string& ns, const std::string& s
   return v.get("items").items();
 }
 
-Value Client::newest_running_pod(const std::string& ns, const std::string& sel, int max_wait_ms, int poll_ms) {
-  auto t0 = std::chrono::steady_clock::now();
-  bool compat = poll_ms >= 1000;
+// ---------------------------------------------------------------- list + watch
+
+bool Client::list_watch(const std::string& collection, const std::string& query, int timeout_ms,
+                        const std::function<bool(const std::vector<Value>&)>& done) {
+  using clock = std::chrono::steady_clock;
+  auto deadline = clock::now() + std::chrono::milliseconds(timeout_ms);
+  auto left_ms = [&] {
+    return (int64_t)std::chrono::duration_cast<std::chrono::milliseconds>(deadline - clock::now()).count();
+  };
+  std::string sep = query.empty() ? "" : "&";
+  std::map<std::string, Value> objs;  // ns/name -> object
+  auto key_of = [](const Value& o) {
+    return o.at_path("metadata.namespace").as_string() + "/" + o.at_path("metadata.name").as_string();
+  };
+  auto snapshot = [&] {
+    std::vector<Value> v;
+    for (auto& kv : objs) v.push_back(kv.second);
+    std::stable_sort(v.begin(), v.end(), [](const Value& a, const Value& b) {
+      return a.at_path("metadata.creationTimestamp").as_string() < b.at_path("metadata.creationTimestamp").as_string();
+    });
+    return v;
+  };
+  bool watch_supported = true;
+  int poll_delay = 5;
   while (true) {
-    if (compat) sleep_ms(poll_ms);  // the reference sleeps before the first list
-    auto pods = list_pods(ns, sel);
-    const Value* newest = nullptr;
-    for (auto& p : pods) {
-      // (the reference keeps &pod of the range variable, i.e. the last pod; intent: newest)
-      if (!newest || p.at_path("metadata.creationTimestamp").as_string() >
-                         newest->at_path("metadata.creationTimestamp").as_string())
-        newest = &p;
+    Value list = get(collection + (query.empty() ? "" : "?" + query));
+    objs.clear();
+    for (auto& it : list.get("items").items()) objs[key_of(it)] = it;
+    if (done(snapshot())) return true;
+    std::string rv = list.at_path("metadata.resourceVersion").as_string();
+    if (!watch_supported) {
+      if (left_ms() <= 0) return false;
+      std::this_thread::sleep_for(std::chrono::milliseconds(std::min<int64_t>(poll_delay, left_ms())));
+      poll_delay = std::min(250, poll_delay * 3 / 2 + 1);
+      continue;
     }
-    if (newest) {
-      std::string s = pod_status(*newest);
-      if (s == "Running") return *newest;
-      if (pod_status_is_fatal(s)) throw std::runtime_error("Selected Pod(s) cannot start (Status: " + s + ")");
+    bool relist = false;
+    while (!relist) {
+      int64_t left = left_ms();
+      if (left <= 0) return false;
+      int64_t secs = std::max<int64_t>(1, (left + 999) / 1000);
+      std::string path = collection + "?" + query + sep + "watch=1&allowWatchBookmarks=true&timeoutSeconds=" +
+                         std::to_string(secs) + (rv.empty() ? "" : "&resourceVersion=" + rv);
+      std::string buf;
+      bool satisfied = false, bad = false;
+      try {
+        stream(path, [&](const std::string& chunk) {
+          buf += chunk;
+          size_t nl;
+          while ((nl = buf.find('\n')) != std::string::npos) {
+            std::string line = trim(buf.substr(0, nl));
+            buf.erase(0, nl + 1);
+            if (line.empty()) continue;
+            Value ev;
+            try {
+              ev = json_parse(line);
+            } catch (...) {
+              bad = true;
+              return false;
+            }
+            std::string type = ev.get("type").as_string();
+            const Value& obj = ev.get("object");
+            if (type.empty() || !obj.is_map()) {  // not a watch stream: server ignored watch=1
+              bad = true;
+              return false;
+            }
+            if (type == "ERROR") {
+              relist = true;  // 410 Gone (resourceVersion too old) or other: start over
+              return false;
+            }
+            std::string orv = obj.at_path("metadata.resourceVersion").as_string();
+            if (!orv.empty()) rv = orv;
+            if (type == "BOOKMARK") continue;
+            if (type == "DELETED")
+              objs.erase(key_of(obj));
+            else
+              objs[key_of(obj)] = obj;
+            if (done(snapshot())) {
+              satisfied = true;
+              return false;
+            }
+          }
+          return left_ms() > 0;
+        }, (int)std::min<int64_t>(left + 5000, INT32_MAX));
+      } catch (const ApiError& e) {
+        if (e.code == 410) {
+          relist = true;
+          continue;
+        }
+        if (e.code == 400 || e.code == 405 || e.code == 501) {
+          watch_supported = false;
+          relist = true;
+          continue;
+        }
+        throw;
+      } catch (const net::NetError&) {
+        relist = true;  // dropped connection: re-list
+        continue;
+      }
+      if (satisfied) return true;
+      if (bad) {
+        watch_supported = false;
+        relist = true;
+      }
+      // otherwise the server ended the watch (timeoutSeconds): watch again from rv
     }
-    sleep_ms(poll_ms);
-    auto el = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
-    if (el >= max_wait_ms)
-      throw std::runtime_error("Waiting for pod with selector " + sel + " in namespace " + ns + " timed out");
   }
+}
+
+bool Client::wait_object(const std::string& object_path, int timeout_ms,
+                         const std::function<bool(const std::optional<Value>&)>& pred) {
+  size_t slash = object_path.rfind('/');
+  std::string collection = object_path.substr(0, slash);
+  std::string name = object_path.substr(slash + 1);
+  return list_watch(collection, "fieldSelector=" + net::url_encode("metadata.name=" + name), timeout_ms,
+                    [&](const std::vector<Value>& objs) {
+                      for (auto& o : objs)
+                        if (o.at_path("metadata.name").as_string() == name) return pred(o);
+                      return pred(std::nullopt);
+                    });
+}
+
+static const Value* newest_of(const std::vector<Value>& pods) {
+  const Value* newest = nullptr;
+  for (auto& p : pods) {
+    // (the reference keeps &pod of the range variable, i.e. the last pod; intent: newest)
+    if (!p.at_path("metadata.deletionTimestamp").is_null()) continue;
+    if (!newest || p.at_path("metadata.creationTimestamp").as_string() >=
+                       newest->at_path("metadata.creationTimestamp").as_string())
+      newest = &p;
+  }
+  return newest;
+}
+
+Value Client::newest_running_pod(const std::string& ns, const std::string& sel, int max_wait_ms, int poll_ms) {
+  auto timeout_error = [&] {
+    return std::runtime_error("Waiting for pod with selector " + sel + " in namespace " + ns + " timed out");
+  };
+  if (poll_ms >= 1000) {
+    // reference-equivalent mode (kubectl/client.go:183-217): sleep, list, repeat
+    auto t0 = std::chrono::steady_clock::now();
+    while (true) {
+      sleep_ms(poll_ms);
+      auto pods = list_pods(ns, sel);
+      if (const Value* newest = newest_of(pods)) {
+        std::string s = pod_status(*newest);
+        if (s == "Running") return *newest;
+        if (pod_status_is_fatal(s)) throw std::runtime_error("Selected Pod(s) cannot start (Status: " + s + ")");
+      }
+      auto el = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+      if (el >= max_wait_ms) throw timeout_error();
+    }
+  }
+  // event driven: list once, then follow the watch (no sleeps)
+  Value found;
+  bool ok = list_watch("/api/v1/namespaces/" + ns + "/pods", sel.empty() ? "" : "labelSelector=" + net::url_encode(sel),
+                       max_wait_ms, [&](const std::vector<Value>& pods) {
+                         const Value* newest = newest_of(pods);
+                         if (!newest) return false;
+                         std::string s = pod_status(*newest);
+                         if (s == "Running") {
+                           found = *newest;
+                           return true;
+                         }
+                         if (pod_status_is_fatal(s))
+                           throw std::runtime_error("Selected Pod(s) cannot start (Status: " + s + ")");
+                         return false;
+                       });
+  if (!ok) throw timeout_error();
+  return found;
 }
 
 std::string Client::logs(const std::string& ns, const std::string& pod, const std::string& container, int tail,
@@ -370,7 +626,18 @@ void Client::ensure_gcloud_cluster_role_binding() {
   post("/apis/rbac.authorization.k8s.io/v1/clusterrolebindings", b);
 }
 
-Value Client::apply(Value obj, const std::string& default_ns) {
+bool never_recreate(const std::string& kind) {
+  return kind == "PersistentVolumeClaim" || kind == "PersistentVolume" || kind == "Namespace";
+}
+
+// Built-in kinds understand strategic merge patches; custom resources only JSON merge patches.
+static bool is_builtin_group(const std::string& api_version) {
+  if (api_version.find('/') == std::string::npos) return true;  // core
+  std::string g = api_version.substr(0, api_version.find('/'));
+  return g.find('.') == std::string::npos || ends_with(g, ".k8s.io");
+}
+
+Value Client::apply(Value obj, const std::string& default_ns, const ApplyOptions& opts) {
   std::string kind = obj.get("kind").as_string();
   std::string av = obj.get("apiVersion").as_string();
   std::string name = obj.at_path("metadata.name").as_string();
@@ -378,22 +645,42 @@ Value Client::apply(Value obj, const std::string& default_ns) {
   std::string ns = obj.at_path("metadata.namespace").as_string();
   if (ns.empty()) ns = default_ns;
   if (!is_cluster_scoped(kind)) obj["metadata"]["namespace"] = ns;
+  // server-managed metadata must not be part of an applied configuration
+  for (const char* k : {"resourceVersion", "uid", "creationTimestamp", "managedFields", "generation", "selfLink"})
+    obj["metadata"].erase(k);
+  obj.erase("status");
   std::string path = resource_path(av, kind, ns, name);
-  auto existing = try_get(path);
-  if (!existing) return post(resource_path(av, kind, ns), obj);
-  obj["metadata"]["resourceVersion"] = existing->at_path("metadata.resourceVersion");
-  if (kind == "Service" && !existing->at_path("spec.clusterIP").is_null())
-    obj["spec"]["clusterIP"] = existing->at_path("spec.clusterIP");
-  try {
-    return put(path, obj);
-  } catch (const ApiError& e) {
-    if (e.code != 422 && e.code != 409) throw;
-    // --force: delete and recreate
-    del(path);
-    obj["metadata"].erase("resourceVersion");
-    for (int i = 0; i < 50 && try_get(path); ++i) sleep_ms(100);
+  std::string body = json_dump(obj);  // JSON is YAML: valid apply-patch+yaml
+  net::Response r = raw("PATCH", path + "?fieldManager=" + net::url_encode(opts.field_manager) + "&force=true", body,
+                        "application/apply-patch+yaml");
+  if (r.status == 415 || r.status == 405 || (r.status == 400 && contains(r.body, "apply-patch"))) {
+    // No server-side apply (k8s < 1.16 or an aggregated API without it): create or patch.
+    auto existing = try_get(path);
+    if (!existing) return post(resource_path(av, kind, ns), obj);
+    std::string type = is_builtin_group(av) ? "application/strategic-merge-patch+json" : "application/merge-patch+json";
+    r = raw("PATCH", path, body, type);
+    if (r.status == 415 && type != "application/merge-patch+json") r = raw("PATCH", path, body, "application/merge-patch+json");
+  }
+  if (r.status >= 200 && r.status < 300) return check(r, "PATCH " + path);
+  if (r.status == 422 && opts.recreate_on_immutable && !never_recreate(kind)) {
+    // kubectl apply --force: delete, wait until gone, create
+    log::warn(kind + " " + name + ": immutable field changed, deleting and re-creating it");
+    delete_object(obj, ns);
+    if (!wait_object(path, 60000, [](const std::optional<Value>& o) { return !o.has_value(); }))
+      throw std::runtime_error(kind + " " + name + " was not deleted within 60s");
     return post(resource_path(av, kind, ns), obj);
   }
+  try {
+    check(r, "apply " + kind + " " + name);
+  } catch (const ApiError& e) {
+    if (e.code != 422) throw;
+    std::string hint = never_recreate(kind)
+                           ? " (" + kind + " fields are immutable once created; change them by hand or delete it)"
+                           : " (an immutable field changed; redeploy with --force-recreate to delete and re-create " +
+                                 kind + " " + name + ")";
+    throw ApiError(e.code, e.reason, std::string(e.what()) + hint);
+  }
+  return Value();
 }
 
 bool Client::delete_object(const Value& obj, const std::string& default_ns) {
@@ -427,7 +714,7 @@ std::unique_ptr<ExecSession> Client::exec(const std::string& ns, const std::stri
                                           const std::vector<std::string>& cmd, bool tty, bool stdin) {
   std::string path = "/api/v1/namespaces/" + ns + "/pods/" + pod + "/exec" +
                      exec_query(container, cmd, tty, stdin, true, !tty);
-  auto ws = net::WebSocket::connect(http_, path, {"v5.channel.k8s.io", "v4.channel.k8s.io", "channel.k8s.io"});
+  auto ws = ws_connect(path, {"v5.channel.k8s.io", "v4.channel.k8s.io", "channel.k8s.io"});
   return std::make_unique<ExecSession>(std::move(ws), tty);
 }
 
@@ -435,13 +722,23 @@ std::unique_ptr<ExecSession> Client::attach(const std::string& ns, const std::st
                                             bool tty, bool stdin) {
   std::string path = "/api/v1/namespaces/" + ns + "/pods/" + pod + "/attach" +
                      exec_query(container, {}, tty, stdin, true, !tty);
-  auto ws = net::WebSocket::connect(http_, path, {"v4.channel.k8s.io", "channel.k8s.io"});
+  auto ws = ws_connect(path, {"v4.channel.k8s.io", "channel.k8s.io"});
   return std::make_unique<ExecSession>(std::move(ws), tty);
 }
 
 std::unique_ptr<net::WebSocket> Client::portforward(const std::string& ns, const std::string& pod, int port) {
   std::string path = "/api/v1/namespaces/" + ns + "/pods/" + pod + "/portforward?ports=" + std::to_string(port);
-  return net::WebSocket::connect(http_, path, {"v4.channel.k8s.io", "portforward.k8s.io"});
+  return ws_connect(path, {"v4.channel.k8s.io", "portforward.k8s.io"});
+}
+
+std::unique_ptr<net::WebSocket> Client::ws_connect(const std::string& path, const std::vector<std::string>& protocols) {
+  ensure_fresh_credentials();
+  try {
+    return net::WebSocket::connect(http_, path, protocols);
+  } catch (const net::UpgradeError& e) {
+    if (e.status != 401 || !refresh_after_unauthorized()) throw;
+  }
+  return net::WebSocket::connect(http_, path, protocols);
 }
 
 // ---------------------------------------------------------------- exec session

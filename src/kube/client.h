@@ -33,7 +33,19 @@ struct ApiError : std::runtime_error {
   ApiError(int c, const std::string& r, const std::string& msg) : std::runtime_error(msg), code(c), reason(r) {}
   bool not_found() const { return code == 404; }
   bool conflict() const { return code == 409; }
+  bool invalid() const { return code == 422; }
 };
+
+// How `apply` treats an object whose changed fields the API server refuses as immutable.
+struct ApplyOptions {
+  // Delete and re-create the object (`kubectl apply --force`). Never done for
+  // PersistentVolumeClaims, PersistentVolumes or Namespaces (data / whole-namespace loss).
+  bool recreate_on_immutable = false;
+  std::string field_manager = "devspace";
+};
+
+// Kinds whose delete-and-recreate would destroy data: apply never recreates them.
+bool never_recreate(const std::string& kind);
 
 // Pod status string exactly like `kubectl get pods` (kubectl/client.go:224 GetPodStatus).
 std::string pod_status(const Value& pod);
@@ -73,6 +85,18 @@ class Client {
   // Stream a GET (logs -f, watch).
   int stream(const std::string& path, const std::function<bool(const std::string&)>& on_data, int timeout_ms = -1);
 
+  // List + watch (the client-go informer pattern without the cache): lists `collection`
+  // (a collection path, `query` without '?'), then follows `?watch=1` from the list's
+  // resourceVersion, re-listing on 410 Gone and re-watching when the server ends the watch.
+  // `done` sees the current object set (ordered by creationTimestamp) after the list and
+  // after every event; returns true as soon as `done` does, false on timeout. Servers without
+  // watch support are polled instead (back-off, 5 ms -> 250 ms).
+  bool list_watch(const std::string& collection, const std::string& query, int timeout_ms,
+                  const std::function<bool(const std::vector<Value>&)>& done);
+  // Waits until the single object at `object_path` satisfies `pred` (nullopt = absent).
+  bool wait_object(const std::string& object_path, int timeout_ms,
+                   const std::function<bool(const std::optional<Value>&)>& pred);
+
   // Pods
   std::vector<Value> list_pods(const std::string& ns, const std::string& label_selector);
   // Newest pod by creationTimestamp that is Running; fails fast on fatal states
@@ -90,9 +114,15 @@ class Client {
   // Returns the warning text ("" when fine).
   std::string check_gpu_requests(const std::vector<Value>& objs);
 
-  // Apply a manifest (create or replace; services keep their clusterIP; immutable-field
-  // conflicts fall back to delete + create, i.e. `kubectl apply --force`).
-  Value apply(Value obj, const std::string& default_ns);
+  // Server-side apply (PATCH application/apply-patch+yaml, fieldManager=devspace, force):
+  // fields set by other managers (the PV binder's spec.volumeName, a Service's clusterIP,
+  // the HPA's replicas) are left alone. Servers without SSA get a strategic-merge (built-in
+  // kinds) or JSON merge patch, or a create. Immutable-field rejections are reported, and only
+  // with opts.recreate_on_immutable turned into delete + create (never for never_recreate()).
+  Value apply(Value obj, const std::string& default_ns, const ApplyOptions& opts);
+  Value apply(Value obj, const std::string& default_ns) { return apply(std::move(obj), default_ns, apply_opts_); }
+  // Defaults for apply() (the CLI's --force-recreate).
+  void set_apply_options(const ApplyOptions& o) { apply_opts_ = o; }
   bool delete_object(const Value& obj, const std::string& default_ns);
 
   // Streams
@@ -104,10 +134,22 @@ class Client {
 
   net::HttpClient& http() { return http_; }
 
+  // Credential refresh (exec plugins: on expiry and on 401; tokenFile: every minute).
+  void ensure_fresh_credentials();
+  bool refresh_after_unauthorized();
+  int credential_refreshes() const { return refreshes_; }
+
  private:
-  void refresh_exec_token();
+  void refresh_exec_credentials();
+  void apply_auth_locked();
+  std::unique_ptr<net::WebSocket> ws_connect(const std::string& path, const std::vector<std::string>& protocols);
   RestConfig cfg_;
   net::HttpClient http_;
+  ApplyOptions apply_opts_;
+  std::mutex auth_mu_;
+  int64_t token_expiry_ = 0;      // unix seconds, 0 = no expiry
+  int64_t token_file_read_ = 0;   // unix seconds of the last tokenFile read
+  std::atomic<int> refreshes_{0};
 };
 
 // A running exec/attach: stdin/stdout/stderr exposed as pipes (so the sync engine and the

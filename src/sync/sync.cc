@@ -1136,6 +1136,12 @@ std::string Session::download_files(const std::vector<FileInfo>& files) {
   return archive;
 }
 
+bool has_dotdot_segment(const std::string& rel) {
+  for (auto& seg : split(rel, "/"))
+    if (seg == "..") return true;
+  return false;
+}
+
 void Session::untar_all(const std::string& archive) {
   GzipReader gz(string_source(&archive));
   TarReader tr([&](char* b, size_t n) { return gz.read(b, n); });
@@ -1152,6 +1158,12 @@ void Session::untar_all(const std::string& archive) {
     if (starts_with(rel, dest_ + "/") || rel == dest_) rel = rel.substr(dest_.size());
     if (!rel.empty() && rel.back() == '/') rel.pop_back();
     if (rel.empty()) continue;
+    if (has_dotdot_segment(rel)) {
+      // the archive comes from the container: never let it write outside the synced folder
+      logf("[Downstream] Skipping archive entry " + e.name + ": path escapes the sync directory");
+      tr.skip();
+      continue;
+    }
     std::string out = o_.watch_path + rel;
     fs::StatInfo st = fs::stat(out);
     if (st.exists && st.mtime_rounded() > e.mtime) {

@@ -125,6 +125,8 @@ class Session {
   void initial_sync();
   void start_loops(bool upstream, bool downstream);
   FileIndex& index() { return index_; }
+  // Extracts a downstream tar.gz (as received from the container) into the local folder.
+  void apply_downstream_archive(const std::string& archive) { untar_all(archive); }
 
   // One-shot upload of a local folder/file (sync/util.go:21 CopyToContainer).
   static void copy_to_container(std::shared_ptr<Transport> t, const std::string& local_path,
@@ -226,6 +228,10 @@ class Session {
   std::string pending_failure_;
   int reconnects_ = 0;
 };
+
+// True when a relative path has a ".." segment (archive entries from the container that
+// would land outside the synced folder are skipped).
+bool has_dotdot_segment(const std::string& rel);
 
 }  // namespace sync
 }  // namespace ds

@@ -381,3 +381,38 @@ TEST(sync_corrupt_ack_is_fatal_without_reconnect) {
   EXPECT_TRUE(!err.empty());
   s.stop();
 }
+
+// archive entries from the container must never be written outside the synced
+// folder (the reference's untar has the same gap; sync/tar.go:44).
+TEST(sync_downstream_archive_rejects_parent_segments) {
+  Dirs d;
+  std::string tar;
+  {
+    TarWriter tw(string_sink(&tar));
+    TarEntry ok;
+    ok.name = "ok.txt";
+    ok.mtime = 1500000000;
+    tw.add_file(ok, "fine");
+    TarEntry evil;
+    evil.name = "../" + fs::basename(d.outside) + "/escaped.txt";
+    evil.mtime = 1500000000;
+    tw.add_file(evil, "pwned");
+    TarEntry deep;
+    deep.name = "sub/../../escaped2.txt";
+    deep.mtime = 1500000000;
+    tw.add_file(deep, "pwned");
+    tw.finish();
+  }
+  Options o;
+  o.watch_path = d.local;
+  o.dest_path = d.remote;
+  o.mode = Mode::Fast;
+  Session s(o, std::make_shared<LocalShellTransport>());
+  s.setup();
+  s.apply_downstream_archive(gzip_compress(tar));
+  EXPECT_EQ(fs::read_file(fs::join(d.local, "ok.txt")), std::string("fine"));
+  EXPECT_TRUE(!fs::exists(fs::join(d.outside, "escaped.txt")));
+  EXPECT_TRUE(!fs::exists(fs::join(fs::dirname(d.local), "escaped2.txt")));
+  EXPECT_TRUE(has_dotdot_segment("/a/../b"));
+  EXPECT_TRUE(!has_dotdot_segment("/a/..b/c.."));
+}

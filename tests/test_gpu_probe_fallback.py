@@ -1,0 +1,75 @@
+"""`devspace analyze --gpu-probe` in a pod whose image has no devspace_amd (a stock
+rocm/pytorch image): the shell probe still checks device nodes and falls back to a torch/HIP
+check instead of silently reporting nothing (round-1 gap: it exec'd `python -m
+devspace_amd.gpucheck`, which exists only on the local cluster's host)."""
+
+import os
+
+import pytest
+
+from conftest import DevspaceEnv
+from test_e2e_cli import running, wait_for
+
+
+@pytest.fixture(scope="module")
+def gpu_node(tmp_path_factory):
+    from devspace_amd.localkube import LocalCluster
+
+    base = str(tmp_path_factory.mktemp("lkprobe"))
+    # advertise amd.com/gpu so GPU pods are scheduled even on a CPU-only host
+    cluster = LocalCluster(os.path.join(base, "state"), gpus=2).start()
+    try:
+        yield DevspaceEnv(cluster, base)
+    finally:
+        cluster.stop()
+
+
+def _gpu_pod(lk, ns, env):
+    store = lk.cluster.store
+    try:
+        store.create("", "namespaces", "", {"metadata": {"name": ns}}, "v1")
+    except Exception:
+        pass
+    store.create("", "pods", ns, {
+        "metadata": {"name": "trainer", "labels": {"app": "trainer"}},
+        "spec": {"containers": [{"name": "main", "image": "busybox", "command": ["sleep", "3600"], "env": env,
+                                 "resources": {"limits": {"amd.com/gpu": 1}}}]},
+    }, "v1")
+    wait_for(lambda: running(lk.pods(ns)), timeout=60, what="gpu pod")
+
+
+def test_probe_without_devspace_amd_in_image(gpu_node, tmp_path):
+    lk = gpu_node
+    # PYTHONPATH cleared: the container cannot import devspace_amd
+    _gpu_pod(lk, "probe-stock", [{"name": "PYTHONPATH", "value": ""}])
+    out = lk.run(["analyze", "-n", "probe-stock", "--wait=false", "--gpu-probe"], str(tmp_path), timeout=180).stdout
+    has_kfd = os.path.exists("/dev/kfd")
+    if not has_kfd:
+        assert "no /dev/kfd in the container" in out, out
+    try:
+        import torch
+
+        cuda = torch.cuda.is_available()
+    except Exception:
+        torch, cuda = None, False
+    if torch is None:
+        assert "PyTorch is not importable" in out, out
+    elif not cuda:
+        assert "torch.cuda.is_available() is False" in out, out
+    else:  # a real GPU: the torch fallback ran its bf16 matmul check and found nothing
+        assert "No problems found" in out or "GPU" not in out, out
+
+
+def test_probe_without_python_reports_unavailable(gpu_node, tmp_path):
+    lk = gpu_node
+    # PATH without python3: only the device-node checks can run, and the report says so
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    for tool in ("sh", "ls", "grep", "sleep", "cat"):
+        for d in ("/bin", "/usr/bin"):
+            if os.path.exists(os.path.join(d, tool)):
+                os.symlink(os.path.join(d, tool), bindir / tool)
+                break
+    _gpu_pod(lk, "probe-nopy", [{"name": "PATH", "value": str(bindir)}])
+    out = lk.run(["analyze", "-n", "probe-nopy", "--wait=false", "--gpu-probe"], str(tmp_path), timeout=180).stdout
+    assert "GPU probe unavailable (no python3 in the image)" in out, out

@@ -209,3 +209,59 @@ def test_preempt_point_noop_without_feed():
     ctx._feed.n = 1
     with pytest.raises(Preempted):
         ctx.preempt_point()
+
+
+def test_edit_during_slow_setup_is_picked_up(tmp_path):
+    """An edit that lands while setup() (or the first step) is still running must neither crash
+    the runner (the first step is outside the preemption handler) nor be lost."""
+    mod = tmp_path / "slow.py"
+    flag = tmp_path / "in_setup"
+    mod.write_text(
+        'import time\nMARKER = "v0"\n'
+        f'def setup(ctx):\n    open({str(flag)!r}, "w").close()\n    time.sleep(1.5)\n    return {{}}\n'
+        'def step(ctx, state):\n    ctx.preempt_point()\n    time.sleep(0.01)\n    ctx.preempt_point()\n'
+        '    return {"loss": 1.0}\n')
+    env = dict(os.environ, PYTHONPATH=ROOT, HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1")
+    proc = subprocess.Popen([sys.executable, "-u", "-m", "devspace_amd.runner", "--watch", str(tmp_path), str(mod)],
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, text=True)
+    lines = []
+    try:
+        t0 = time.time()
+        while not flag.exists() and time.time() - t0 < 120:
+            time.sleep(0.01)
+        assert flag.exists(), "setup never ran"
+        mod.write_text(mod.read_text().replace('MARKER = "v0"', 'MARKER = "during_setup"'))
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            line = proc.stdout.readline()
+            if not line:
+                break
+            lines.append(line)
+            if "marker=during_setup" in line:
+                break
+        assert any("marker=during_setup" in l for l in lines), "".join(lines)
+        assert proc.poll() is None, "".join(lines)
+        assert not any("Traceback" in l for l in lines), "".join(lines)
+    finally:
+        proc.terminate()
+        proc.wait(10)
+
+
+def test_preempted_is_not_swallowed_by_generic_handlers():
+    from devspace_amd.runner import Preempted
+
+    assert not issubclass(Preempted, Exception)
+    with pytest.raises(Preempted):
+        try:
+            raise Preempted()
+        except Exception:  # a user step's catch-all must let the preemption through
+            pass
+
+
+def test_vendored_runner_copies_match_the_package():
+    """`devspace init` (templates/rocm-pytorch) and examples/rocm-pytorch ship the runner as a
+    single file next to train.py, so the image does not need devspace_amd installed."""
+    src = open(os.path.join(ROOT, "devspace_amd", "runner.py")).read()
+    for copy in (os.path.join(ROOT, "templates", "rocm-pytorch", "devspace_runner.py"),
+                 os.path.join(ROOT, "examples", "rocm-pytorch", "devspace_runner.py")):
+        assert open(copy).read() == src, f"{copy} is out of date: cp devspace_amd/runner.py {copy}"
