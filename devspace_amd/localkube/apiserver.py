@@ -45,12 +45,29 @@ def _exit_status(code):
 
 
 class ApiServer:
-    def __init__(self, store, kubelet):
+    def __init__(self, store, kubelet, token_validator=None):
         self.store = store
         self.kubelet = kubelet
+        # token_validator(token) -> bool: when set, requests need a valid bearer token (or a
+        # verified client certificate on the TLS listener) — expired tokens get 401
+        self.token_validator = token_validator
+        self.auth_failures = 0
+
+    @web.middleware
+    async def _auth(self, request, handler):
+        if self.token_validator is not None:
+            tr = request.transport
+            peer_cert = tr.get_extra_info("peercert") if tr is not None else None
+            h = request.headers.get("Authorization", "")
+            if not peer_cert and not (h.startswith("Bearer ") and self.token_validator(h[7:])):
+                self.auth_failures += 1
+                return web.json_response({"kind": "Status", "apiVersion": "v1", "status": "Failure",
+                                          "message": "Unauthorized", "reason": "Unauthorized", "code": 401},
+                                         status=401)
+        return await handler(request)
 
     def app(self):
-        app = web.Application(client_max_size=256 * 1024 * 1024)
+        app = web.Application(client_max_size=256 * 1024 * 1024, middlewares=[self._auth])
         app.router.add_get("/version", self.version)
         app.router.add_get("/api", self.api_versions)
         app.router.add_get("/apis", self.api_groups)
@@ -400,6 +417,7 @@ class ApiServer:
             await ws.close()
             return ws
         loop = asyncio.get_running_loop()
+        c.exec_procs.add(proc)
 
         async def pump(reader, ch):
             while True:
@@ -475,6 +493,7 @@ class ApiServer:
 
         reader = asyncio.create_task(read_ws())
         code = await proc.wait()
+        c.exec_procs.discard(proc)
         if tty:
             try:
                 await asyncio.sleep(0.05)

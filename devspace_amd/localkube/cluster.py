@@ -84,7 +84,8 @@ def _b64file(path):
 
 
 class LocalCluster:
-    def __init__(self, state_dir, port=0, gpus=None, context="devspace-local", extra_env=None, tls=False):
+    def __init__(self, state_dir, port=0, gpus=None, context="devspace-local", extra_env=None, tls=False,
+                 token_validator=None):
         self.state_dir = os.path.abspath(state_dir)
         self.tls = tls
         self.pki = make_pki(os.path.join(self.state_dir, "pki")) if tls else None
@@ -97,7 +98,7 @@ class LocalCluster:
         env = {"PYTHONPATH": ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")}
         env.update(extra_env or {})
         self.kubelet = Kubelet(self.store, self.images, self.state_dir, gpus=self.gpus, extra_env=env)
-        self.api = ApiServer(self.store, self.kubelet)
+        self.api = ApiServer(self.store, self.kubelet, token_validator=token_validator)
         self.docker_sock = os.path.join(self.state_dir, "docker.sock")
         self.loop = None
         self.thread = None

@@ -65,6 +65,7 @@ class Container:
         self.spec = spec
         self.root = root
         self.proc = None
+        self.exec_procs = set()  # `kubectl exec` processes: killed with the container (cgroup)
         self.restarts = 0
         self.state = {"waiting": {"reason": "ContainerCreating"}}
         self.last_state = {}
@@ -534,6 +535,15 @@ class Kubelet:
         self.store.update_status("", "pods", rt.ns, rt.name, status)
 
     async def _kill_pod(self, rt, grace):
+        # exec'd processes die with the container, as in a real container cgroup: they must
+        # not outlive the pod and watch its filesystem being removed
+        for c in rt.containers.values():
+            for ep in list(c.exec_procs):
+                if ep.returncode is None:
+                    try:
+                        os.killpg(ep.pid, signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
         procs = [c.proc for c in rt.containers.values() if c.proc and c.proc.returncode is None]
         for p in procs:
             try:

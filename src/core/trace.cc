@@ -12,6 +12,9 @@
 namespace ds {
 namespace trace {
 
+// namespace scope: outlives atexit handlers registered from main() (the net.stats span)
+static std::mutex g_mu;
+
 bool enabled() {
   static const bool on = [] {
     const char* e = getenv("DEVSPACE_TRACE");
@@ -37,8 +40,7 @@ void emit(const std::string& name, int64_t start_us, int64_t dur_us, const std::
   v["dur_us"] = dur_us;
   v["pid"] = (int64_t)getpid();
   for (auto& kv : fields) v[kv.first] = kv.second;
-  static std::mutex mu;
-  std::lock_guard<std::mutex> g(mu);
+  std::lock_guard<std::mutex> g(g_mu);
   try {
     fs::append_file(fs::join(dir, "trace.jsonl"), json_dump(v) + "\n");
   } catch (...) {

@@ -220,7 +220,7 @@ void Client::refresh_exec_credentials() {
 void Client::ensure_fresh_credentials() {
   std::lock_guard<std::mutex> g(auth_mu_);
   int64_t now = unix_now();
-  if (!cfg_.exec_command.empty() && token_expiry_ > 0 && now >= token_expiry_ - 10) {
+  if (!cfg_.exec_command.empty() && token_expiry_ > 0 && now >= token_expiry_ - 1) {
     refresh_exec_credentials();
     apply_auth_locked();
   }

@@ -192,6 +192,7 @@ class ExecTransport : public sync::Transport {
   std::unique_ptr<sync::Shell> open(const std::vector<std::string>& argv) override;
   std::string describe() const override { return "exec(" + pod_name_ + "/" + container_ + ")"; }
   std::string path_prefix() const override { return prefix_; }
+  std::string pod_name() const override { return pod_name_; }
 
  private:
   std::shared_ptr<Client> c_;

@@ -111,17 +111,24 @@ Session::Session(Options opts, std::shared_ptr<Transport> transport)
 
 Session::~Session() { stop(); }
 
+std::string Session::pod_name() {
+  std::lock_guard<std::mutex> g(pod_mu_);
+  return o_.pod_name;
+}
+
 void Session::logf(const std::string& msg) {
   if (o_.silent || !log_) return;
   std::map<std::string, std::string> f{{"local", o_.watch_path}, {"container", o_.dest_path}};
-  if (!o_.pod_name.empty()) f["pod"] = o_.pod_name;
+  std::string pod = pod_name();
+  if (!pod.empty()) f["pod"] = pod;
   log_->emit("info", msg, f);
 }
 
 void Session::log_error(const std::string& msg) {
   if (!log_) return;
   std::map<std::string, std::string> f{{"local", o_.watch_path}, {"container", o_.dest_path}};
-  if (!o_.pod_name.empty()) f["pod"] = o_.pod_name;
+  std::string pod = pod_name();
+  if (!pod.empty()) f["pod"] = pod;
   log_->emit("error", msg, f);
 }
 
@@ -1421,7 +1428,12 @@ void Session::supervise() {
       if (!t) throw SyncError("no pod available");
       transport_ = t;
       dest_ = remote(o_.dest_path);
+      if (!t->pod_name().empty()) {
+        std::lock_guard<std::mutex> g(pod_mu_);
+        o_.pod_name = t->pod_name();  // `status sync` shows the pod the sync now talks to
+      }
       open_shells();
+      logf("[Sync] Reconnected to " + t->describe());
     } catch (const std::exception& e) {
       std::lock_guard<std::mutex> g(state_mu_);
       pending_failure_ = e.what();

@@ -116,6 +116,7 @@ class Session {
   std::string error();
   Stats stats();
   const Options& options() const { return o_; }
+  std::string pod_name();  // current pod (changes when a reconnect picks a new one)
   Mode effective_mode() const { return mode_; }
 
   // --- pieces exposed for tests (the reference tests drive setup/initialSync directly)
@@ -219,6 +220,7 @@ class Session {
   std::thread up_thread_, down_thread_, supervisor_;
   std::atomic<bool> running_{false}, stopping_{false};
   std::atomic<bool> failed_{false};
+  std::mutex pod_mu_;
   std::mutex state_mu_;
   std::condition_variable state_cv_;
   bool initial_done_ = false;

@@ -39,6 +39,8 @@ class Transport {
   // Prefix that maps container paths to what the shell sees (local-pod backend roots
   // every pod under a directory; real containers use "").
   virtual std::string path_prefix() const { return ""; }
+  // Pod behind this transport ("" when not a pod).
+  virtual std::string pod_name() const { return ""; }
 };
 
 // Runs commands as local processes (optionally chrooted-by-convention under `root`).

@@ -85,3 +85,77 @@ TEST(analyze_gpu_runtime_log_matcher) {
   EXPECT_TRUE(analyze::log_has_gpu_runtime_error("hipErrorNoDevice", &m));
   EXPECT_TRUE(!analyze::log_has_gpu_runtime_error("Example app listening on port 3000!", &m));
 }
+
+// $KUBECONFIG with several files, merged like client-go's clientcmd loading rules.
+TEST(kubeconfig_multi_file_merge_and_save) {
+  std::string d = fs::make_temp_dir("kcmerge-");
+  fs::mkdirs(fs::join(d, "one"));
+  fs::mkdirs(fs::join(d, "two/certs"));
+  std::string f1 = fs::join(d, "one/config"), f2 = fs::join(d, "two/config");
+  fs::write_file(f1,
+                 "apiVersion: v1\nkind: Config\ncurrent-context: a\n"
+                 "clusters:\n- name: c1\n  cluster: {server: 'https://one:6443'}\n"
+                 "contexts:\n- name: a\n  context: {cluster: c1, user: u1, namespace: ns-a}\n"
+                 "users:\n- name: u1\n  user: {token: first}\n");
+  fs::write_file(fs::join(d, "two/certs/ca.crt"), "CA-PEM");
+  fs::write_file(f2,
+                 "apiVersion: v1\nkind: Config\ncurrent-context: b\n"
+                 "clusters:\n- name: c2\n  cluster: {server: 'https://two:6443', certificate-authority: certs/ca.crt}\n"
+                 "contexts:\n- name: a\n  context: {cluster: c2, user: u2}\n"
+                 "- name: b\n  context: {cluster: c2, user: u1}\n"
+                 "users:\n- name: u1\n  user: {token: shadowed}\n- name: u2\n  user: {token: second}\n");
+  setenv("KUBECONFIG", (f1 + ":" + f2 + ":" + f1).c_str(), 1);
+  kube::KubeConfig kc = kube::KubeConfig::load();
+  EXPECT_EQ(kc.files.size(), (size_t)2);
+  EXPECT_EQ(kc.current_context(), std::string("a"));  // first file that sets it
+  auto a = kc.resolve("a");
+  EXPECT_EQ(a.server, std::string("https://one:6443"));  // first definition of "a" wins
+  EXPECT_EQ(a.token, std::string("first"));
+  auto b = kc.resolve("b");
+  EXPECT_EQ(b.server, std::string("https://two:6443"));
+  EXPECT_EQ(b.ca_pem, std::string("CA-PEM"));  // relative to the file that defines c2
+  EXPECT_EQ(b.token, std::string("first"));    // u1 from the first file
+  // edits go back where each entry lives; the current context to the file that set it
+  kc.set_current_context("b");
+  kc.set_context_namespace("b", "ns-b");
+  kc.set_context("new", "c1", "u1", "");
+  kc.save();
+  Value v1 = yaml_load_file(f1), v2 = yaml_load_file(f2);
+  EXPECT_EQ(v1.get("current-context").as_string(), std::string("b"));
+  EXPECT_EQ(v2.get("current-context").as_string(), std::string("b"));  // untouched (was b)
+  EXPECT_EQ(v1.get("contexts").size(), (size_t)2);                      // a + new
+  bool b_ns = false, shadow_kept = false;
+  for (auto& c : v2.get("contexts").items()) {
+    if (c.get("name").as_string() == "b") b_ns = c.at_path("context.namespace").as_string() == "ns-b";
+    if (c.get("name").as_string() == "a") shadow_kept = c.at_path("context.cluster").as_string() == "c2";
+  }
+  EXPECT_TRUE(b_ns);
+  EXPECT_TRUE(shadow_kept);
+  unsetenv("KUBECONFIG");
+  fs::remove_all(d);
+}
+
+TEST(no_proxy_matching) {
+  using net::no_proxy_matches;
+  EXPECT_TRUE(no_proxy_matches("*", "api.example.com", 443));
+  EXPECT_TRUE(no_proxy_matches("example.com", "api.example.com", 443));
+  EXPECT_TRUE(no_proxy_matches(".example.com", "api.example.com", 443));
+  EXPECT_TRUE(no_proxy_matches("example.com", "example.com", 443));
+  EXPECT_TRUE(!no_proxy_matches("example.com", "badexample.com", 443));
+  EXPECT_TRUE(no_proxy_matches("10.0.0.0/8, localhost", "10.96.0.1", 443));
+  EXPECT_TRUE(!no_proxy_matches("10.0.0.0/8", "11.0.0.1", 443));
+  EXPECT_TRUE(no_proxy_matches("kube.local:6443", "kube.local", 6443));
+  EXPECT_TRUE(!no_proxy_matches("kube.local:6443", "kube.local", 443));
+  EXPECT_TRUE(no_proxy_matches("127.0.0.1", "127.0.0.1", 8443));
+  net::ProxyConfig p;
+  p.https_proxy = "http://proxy:3128";
+  p.no_proxy = "localhost";
+  EXPECT_EQ(p.proxy_for("https", "api", 443), std::string("http://proxy:3128"));
+  EXPECT_EQ(p.proxy_for("https", "localhost", 443), std::string(""));
+  EXPECT_EQ(p.proxy_for("http", "api", 80), std::string(""));
+}
+
+TEST(websocket_accept_rfc6455_example) {
+  // RFC 6455 §1.3 worked example
+  EXPECT_EQ(net::websocket_accept("dGhlIHNhbXBsZSBub25jZQ=="), std::string("s3pPLMBiTxaQ9kYGzzhZRbK+xOo="));
+}
