@@ -219,14 +219,14 @@ int run_dev(cli::Command& c, const std::vector<std::string>& args) {
         rc = services::start_terminal(s.cfg(), s.kube, c.get_str("selector"), c.get_str("container"),
                                       c.get_str("label-selector"), c.get_str("namespace"), false, args, stop_now);
       } else {
+        log::done("Services started (Press Ctrl+C to abort port-forwarding and sync)");
         log::info("Will now try to print the logs of a running pod...");
         try {
           services::start_attach(s.cfg(), s.kube, c.get_str("selector"), c.get_str("container"),
-                                 c.get_str("label-selector"), c.get_str("namespace"), stop_now);
+                                 c.get_str("label-selector"), c.get_str("namespace"), stop_now, true);
         } catch (const std::exception& e) {
           log::info(std::string("Couldn't print logs of running pod: ") + e.what());
         }
-        if (!stop_now()) log::done("Services started (Press Ctrl+C to abort port-forwarding and sync)");
         while (!stop_now()) std::this_thread::sleep_for(std::chrono::milliseconds(100));
       }
     } catch (const std::exception& e) {

@@ -10,6 +10,7 @@
 #include <termios.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <cstring>
 
 #include "core/fs.h"
@@ -144,8 +145,11 @@ std::vector<std::unique_ptr<sync::Session>> start_sync(const Value& cfg, std::sh
 // ---------------------------------------------------------------- port forwarding
 
 PortForwarder::PortForwarder(std::shared_ptr<kube::Client> k, Value pod, std::vector<std::pair<int, int>> ports,
-                             std::vector<std::string> addresses)
-    : k_(std::move(k)), pod_(std::move(pod)), ports_(std::move(ports)), addrs_(std::move(addresses)) {}
+                             std::vector<std::string> addresses, std::string label_selector)
+    : k_(std::move(k)), pod_(std::move(pod)), selector_(std::move(label_selector)), ports_(std::move(ports)),
+      addrs_(std::move(addresses)) {
+  ns_ = pod_.at_path("metadata.namespace").as_string();
+}
 
 PortForwarder::~PortForwarder() { close(); }
 
@@ -153,6 +157,18 @@ std::string PortForwarder::describe() const {
   std::vector<std::string> p;
   for (auto& pr : ports_) p.push_back(std::to_string(pr.first) + ":" + std::to_string(pr.second));
   return join(p, ", ");
+}
+
+std::string PortForwarder::pod_name() {
+  std::lock_guard<std::mutex> g(pod_mu_);
+  return pod_.at_path("metadata.name").as_string();
+}
+
+size_t PortForwarder::active_connections() {
+  std::lock_guard<std::mutex> g(conns_mu_);
+  size_t n = 0;
+  for (auto& c : conns_) n += !c->done;
+  return n;
 }
 
 void PortForwarder::start() {
@@ -185,27 +201,82 @@ void PortForwarder::start() {
   }
 }
 
+void PortForwarder::reap(bool all) {
+  std::vector<std::unique_ptr<Conn>> finished;
+  {
+    std::lock_guard<std::mutex> g(conns_mu_);
+    for (auto it = conns_.begin(); it != conns_.end();) {
+      if (all || (*it)->done) {
+        finished.push_back(std::move(*it));
+        it = conns_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  for (auto& c : finished)
+    if (c->t.joinable()) c->t.join();
+}
+
 void PortForwarder::accept_loop(int lfd, int remote_port) {
   while (!stop_) {
+    reap(false);
     struct pollfd pf{lfd, POLLIN, 0};
     if (::poll(&pf, 1, 200) <= 0) continue;
-    int c = ::accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
-    if (c < 0) continue;
-    std::thread([this, c, remote_port] { handle(c, remote_port); }).detach();
+    int cfd = ::accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
+    if (cfd < 0) continue;
+    auto c = std::make_unique<Conn>();
+    c->fd = cfd;
+    Conn* raw = c.get();
+    std::lock_guard<std::mutex> g(conns_mu_);
+    if (stop_) {
+      ::close(cfd);
+      break;
+    }
+    conns_.push_back(std::move(c));
+    raw->t = std::thread([this, raw, remote_port] { handle(raw, remote_port); });
   }
 }
 
-void PortForwarder::handle(int cfd, int remote_port) {
+std::unique_ptr<net::WebSocket> PortForwarder::open_stream(int remote_port) {
+  Value pod;
+  {
+    std::lock_guard<std::mutex> g(pod_mu_);
+    pod = pod_;
+  }
+  std::string name = pod.at_path("metadata.name").as_string();
+  try {
+    return k_->portforward(ns_, name, remote_port);
+  } catch (const std::exception& e) {
+    if (selector_.empty() || stop_) throw;
+    // the pod is gone or not running any more: follow the selector to its newest pod
+    Value fresh = k_->newest_running_pod(ns_, selector_, 60000);
+    std::string fresh_name = fresh.at_path("metadata.name").as_string();
+    if (fresh_name == name) throw;
+    {
+      std::lock_guard<std::mutex> g(pod_mu_);
+      pod_ = fresh;
+    }
+    reselections_++;
+    log::file_logger("portforwarding")->emit("info", "Pod " + name + " is gone (" + e.what() +
+                                             "), forwarding to " + fresh_name, {});
+    log::info("Port forwarding " + describe() + " now targets pod " + fresh_name);
+    return k_->portforward(ns_, fresh_name, remote_port);
+  }
+}
+
+void PortForwarder::handle(Conn* conn, int remote_port) {
+  int cfd = conn->fd;
   std::unique_ptr<net::WebSocket> ws;
   try {
-    ws = k_->portforward(pod_.at_path("metadata.namespace").as_string(), pod_.at_path("metadata.name").as_string(),
-                         remote_port);
+    ws = open_stream(remote_port);
   } catch (const std::exception& e) {
     log::file_logger("portforwarding")->emit("error", std::string("Error forwarding ports: ") + e.what(), {});
     ::close(cfd);
+    conn->done = true;
     return;
   }
-  std::atomic<bool> done{false};
+  std::atomic<bool> down_done{false};
   std::thread down([&] {
     std::string msg;
     bool first_data = true, first_err = true;
@@ -228,12 +299,12 @@ void PortForwarder::handle(int cfd, int remote_port) {
         log::file_logger("portforwarding")->emit("error", data, {});
       }
     }
-    done = true;
+    down_done = true;
     ::shutdown(cfd, SHUT_RDWR);
   });
   char buf[65536];
   buf[0] = 0;
-  while (!done && !stop_) {
+  while (!down_done && !stop_) {
     struct pollfd pf{cfd, POLLIN, 0};
     int r = ::poll(&pf, 1, 200);
     if (r == 0) continue;
@@ -244,6 +315,7 @@ void PortForwarder::handle(int cfd, int remote_port) {
   ws->close();
   down.join();
   ::close(cfd);
+  conn->done = true;
 }
 
 void PortForwarder::close() {
@@ -252,6 +324,7 @@ void PortForwarder::close() {
     if (t.joinable()) t.join();
   for (int fd : listeners_) ::close(fd);
   listeners_.clear();
+  reap(true);  // every connection thread ends within one poll interval once stop_ is set
 }
 
 std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& cfg, std::shared_ptr<kube::Client> k,
@@ -274,7 +347,7 @@ std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& c
       ports.emplace_back((int)m.get("localPort").as_int(), (int)m.get("remotePort").as_int());
       addrs.push_back(m.get("bindAddress").as_string("127.0.0.1"));
     }
-    auto fwd = std::make_unique<PortForwarder>(k, pod, ports, addrs);
+    auto fwd = std::make_unique<PortForwarder>(k, pod, ports, addrs, ref.labels.to_query());
     fwd->start();
     log::done("Port forwarding started on " + fwd->describe());
     out.push_back(std::move(fwd));
@@ -367,49 +440,84 @@ Value find_pod(const Value& cfg, kube::Client& k, const Target& t, bool pick, in
 
 }  // namespace
 
+// True when `pod` is deleted, terminating or not running any more (its streams ended
+// because of the pod, not because the remote command finished).
+static bool pod_gone(kube::Client& k, const Value& pod) {
+  try {
+    auto cur = k.try_get("/api/v1/namespaces/" + pod.at_path("metadata.namespace").as_string() + "/pods/" +
+                         pod.at_path("metadata.name").as_string());
+    if (!cur) return true;
+    if (cur->at_path("metadata.uid").as_string() != pod.at_path("metadata.uid").as_string()) return true;
+    return kube::pod_status(*cur) != "Running";
+  } catch (const std::exception&) {
+    return false;  // API unreachable: do not guess
+  }
+}
+
 int start_terminal(const Value& cfg, std::shared_ptr<kube::Client> k, const std::string& selector,
                    const std::string& container, const std::string& label_selector, const std::string& ns, bool pick,
                    std::vector<std::string> cmd, const std::function<bool()>& interrupt) {
   Target t = resolve_target(cfg, selector, label_selector, ns, container);
-  log::start_wait("Terminal: Waiting for pods...");
-  Value pod;
-  try {
-    pod = find_pod(cfg, *k, t, pick, 5000);
-  } catch (...) {
-    log::stop_wait();
-    throw;
-  }
-  log::stop_wait();
-  std::string c = select_container(pod, t.container);
   if (cmd.empty()) {
     for (auto& s : cfg.at_path("dev.terminal.command").items()) cmd.push_back(s.as_string());
   }
   if (cmd.empty()) cmd = {"sh", "-c", "command -v bash >/dev/null 2>&1 && exec bash || exec sh"};
   bool tty = ::isatty(0) && ::isatty(1);
-  auto s = k->exec(pod.at_path("metadata.namespace").as_string(), pod.at_path("metadata.name").as_string(), c, cmd,
-                   tty, true);
-  {
-    RawTty raw;
-    pump_session(*s, tty, true, interrupt);
+  for (int attempt = 0;; ++attempt) {
+    log::start_wait("Terminal: Waiting for pods...");
+    Value pod;
+    try {
+      pod = find_pod(cfg, *k, t, pick && attempt == 0, attempt == 0 ? 5000 : 120000);
+    } catch (...) {
+      log::stop_wait();
+      throw;
+    }
+    log::stop_wait();
+    std::string c = select_container(pod, t.container);
+    auto s = k->exec(pod.at_path("metadata.namespace").as_string(), pod.at_path("metadata.name").as_string(), c, cmd,
+                     tty, true);
+    {
+      RawTty raw;
+      pump_session(*s, tty, true, interrupt);
+    }
+    int code = s->wait(2000);
+    s->close();
+    // An interactive session whose pod went away (restart, rollout: the shell was killed with
+    // the container) reconnects to the newest pod of the selector; the reference exits
+    // (terminal.go:104). Non-interactive commands are never re-run.
+    bool interrupted = interrupt && interrupt();
+    if (!tty || interrupted || attempt >= 4 || !pod_gone(*k, pod))
+      return code < 0 ? 0 : code;  // CodeExitError is not a devspace failure (terminal.go:104)
+    log::info("Pod " + pod.at_path("metadata.name").as_string() +
+              " went away, reconnecting the terminal to the newest running pod...");
   }
-  int code = s->wait(2000);
-  s->close();
-  return code < 0 ? 0 : code;  // CodeExitError is not a devspace failure (terminal.go:104)
 }
 
 int start_attach(const Value& cfg, std::shared_ptr<kube::Client> k, const std::string& selector,
                  const std::string& container, const std::string& label_selector, const std::string& ns,
-                 const std::function<bool()>& interrupt) {
+                 const std::function<bool()>& interrupt, bool follow_restarts) {
   Target t = resolve_target(cfg, selector, label_selector, ns, container);
-  Value pod = find_pod(cfg, *k, t, false, 5000);
-  std::string c = select_container(pod, t.container);
-  auto s = k->attach(pod.at_path("metadata.namespace").as_string(), pod.at_path("metadata.name").as_string(), c, true,
-                     false);
-  log::info("Attached to container " + c + " of pod " + pod.at_path("metadata.name").as_string());
-  pump_session(*s, false, false, interrupt);
-  int code = s->wait(2000);
-  s->close();
-  return code;
+  int backoff_ms = 200;
+  while (true) {
+    Value pod = find_pod(cfg, *k, t, false, follow_restarts ? 120000 : 5000);
+    std::string c = select_container(pod, t.container);
+    auto s = k->attach(pod.at_path("metadata.namespace").as_string(), pod.at_path("metadata.name").as_string(), c,
+                       true, false);
+    log::info("Attached to container " + c + " of pod " + pod.at_path("metadata.name").as_string());
+    auto t0 = std::chrono::steady_clock::now();
+    pump_session(*s, false, false, interrupt);
+    int code = s->wait(2000);
+    s->close();
+    if (!follow_restarts || (interrupt && interrupt())) return code;
+    // the container restarted or the pod was replaced: attach to whatever runs now
+    auto lived = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+    backoff_ms = lived > 10000 ? 200 : std::min(backoff_ms * 2, 5000);
+    log::info("Attach stream of pod " + pod.at_path("metadata.name").as_string() + " ended, re-attaching...");
+    for (int waited = 0; waited < backoff_ms; waited += 50) {
+      if (interrupt && interrupt()) return code;
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+  }
 }
 
 int start_logs(const Value& cfg, std::shared_ptr<kube::Client> k, const std::string& selector,

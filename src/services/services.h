@@ -5,6 +5,7 @@
 #include <atomic>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -39,26 +40,46 @@ struct SyncOptions {
 std::vector<std::unique_ptr<sync::Session>> start_sync(const Value& cfg, std::shared_ptr<kube::Client> k,
                                                         const SyncOptions& o);
 
+// Local listeners forwarding to a pod port over the portforward.k8s.io WebSocket protocol
+// (services/port_forwarding.go:18, kubectl/client.go:356). Every accepted connection gets its
+// own stream and thread; the forwarder owns those threads and joins them in close(). When the
+// pod goes away (restart, rollout) new connections re-select the newest running pod of the
+// selector instead of failing forever (the reference keeps forwarding to the dead pod).
 class PortForwarder {
  public:
   PortForwarder(std::shared_ptr<kube::Client> k, Value pod, std::vector<std::pair<int, int>> ports,
-                std::vector<std::string> addresses);
+                std::vector<std::string> addresses, std::string label_selector = "");
   ~PortForwarder();
   // Binds all listeners; throws on failure.
   void start();
   void close();
   std::string describe() const;
+  std::string pod_name();
+  int reselections() const { return reselections_; }
+  size_t active_connections();
 
  private:
+  struct Conn {
+    std::thread t;
+    int fd = -1;
+    std::atomic<bool> done{false};
+  };
   void accept_loop(int lfd, int remote_port);
-  void handle(int cfd, int remote_port);
+  void handle(Conn* c, int remote_port);
+  void reap(bool all);
+  std::unique_ptr<net::WebSocket> open_stream(int remote_port);
   std::shared_ptr<kube::Client> k_;
+  std::mutex pod_mu_;
   Value pod_;
+  std::string ns_, selector_;
   std::vector<std::pair<int, int>> ports_;
   std::vector<std::string> addrs_;
   std::vector<int> listeners_;
   std::vector<std::thread> threads_;
+  std::mutex conns_mu_;
+  std::vector<std::unique_ptr<Conn>> conns_;
   std::atomic<bool> stop_{false};
+  std::atomic<int> reselections_{0};
 };
 
 std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& cfg, std::shared_ptr<kube::Client> k,
@@ -70,10 +91,12 @@ int start_terminal(const Value& cfg, std::shared_ptr<kube::Client> k, const std:
                    const std::string& container, const std::string& label_selector, const std::string& ns, bool pick,
                    std::vector<std::string> cmd, const std::function<bool()>& interrupt);
 
-// Attach to the container output (services/attach.go:18).
+// Attach to the container output (services/attach.go:18). With follow_restarts (dev) a
+// stream that ends because the container restarted or the pod was replaced re-attaches to the
+// newest running pod until `interrupt` fires.
 int start_attach(const Value& cfg, std::shared_ptr<kube::Client> k, const std::string& selector,
                  const std::string& container, const std::string& label_selector, const std::string& ns,
-                 const std::function<bool()>& interrupt);
+                 const std::function<bool()>& interrupt, bool follow_restarts = false);
 
 // Print last N lines, optionally follow (services/logs.go:17).
 int start_logs(const Value& cfg, std::shared_ptr<kube::Client> k, const std::string& selector,
