@@ -41,15 +41,19 @@ def _phases(trace_path):
     """Per-phase milliseconds of one CLI run from .devspace/logs/trace.jsonl."""
     import json
 
-    out = {}
+    out, net = {}, {}
     try:
         with open(trace_path) as f:
             for line in f:
                 s = json.loads(line)
+                if s["span"] == "net":  # transport counters of one CLI run (src/main.cc)
+                    for k in ("tcp_dials", "tls_handshakes", "requests", "reused"):
+                        net[k] = net.get(k, 0) + int(s.get(k, 0))
+                    continue
                 out[s["span"]] = round(out.get(s["span"], 0.0) + s["dur_us"] / 1000.0, 2)
     except OSError:
         pass
-    return out
+    return out, net
 
 
 def _prewarm_runtime():
@@ -69,22 +73,23 @@ def _prewarm_runtime():
     return done
 
 
-def bench_deploy(workdir, example="quickstart"):
+def bench_deploy(workdir, example="quickstart", tls=False):
     base = os.path.join(workdir, "deploy-bench")
     os.makedirs(base, exist_ok=True)
     proj = os.path.join(base, example)
     shutil.copytree(os.path.join(ROOT, "examples", example), proj, symlinks=True)
     prewarmed = _prewarm_runtime()
-    cluster = LocalCluster(os.path.join(base, "cluster"), gpus=0).start()
+    cluster = LocalCluster(os.path.join(base, "cluster"), gpus=0, tls=tls).start()
     try:
         env = devspace_env(cluster, base)
         trace = os.path.join(proj, ".devspace", "logs", "trace.jsonl")
         cold, out = run_devspace(["deploy"], proj, env)
         if "Successfully deployed!" not in out:
             raise RuntimeError(out)
-        phases = _phases(trace)
+        phases, net = _phases(trace)
         warm, _ = run_devspace(["deploy", "-d"], proj, env)
         run_devspace(["purge"], proj, env)
-        return {"cold_s": cold, "warm_s": warm, "cold_phases_ms": phases, "host_runtime_prewarmed": prewarmed}
+        return {"cold_s": cold, "warm_s": warm, "cold_phases_ms": phases, "net": net,
+                "host_runtime_prewarmed": prewarmed}
     finally:
         cluster.stop()

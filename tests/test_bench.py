@@ -18,12 +18,21 @@ def _run(args, timeout):
 
 
 def test_bench_cpu_tiny():
-    d = _run(["--steps", "3", "--warmup", "1", "--ref-steps", "1", "--tiny"], 600)
+    d = _run(["--steps", "3", "--warmup", "1", "--ref-steps", "1", "--qs-steps", "3", "--tiny"], 600)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "config"):
         assert k in d
     assert d["higher_is_better"] is False
     assert d["value"] > 0
-    assert d["reference_equivalent_p50_ms"] > d["value"]
+    # the config names what was measured: app, transport, builder fidelity
+    assert d["config"]["app"] == "examples/rocm-pytorch"
+    assert d["config"]["transport"].startswith("https + wss")
+    assert "RUN steps not executed" in d["config"]["builder"]
+    assert d["deploy"]["control_plane_only"] is True
+    assert d["deploy"]["net"]["tls_handshakes"] >= 1
+    assert d["reference_equivalent"]["p50_ms"] > d["value"]
+    # Node.js quickstart loop through sync + port-forward, and the sync-protocol comparison
+    assert d["quickstart"]["n"] == 3 and d["quickstart"]["reload_p50_ms"] > d["quickstart"]["sync_p50_ms"] > 0
+    assert d["tool_attributable"]["reference_protocol_sync_p50_ms"] > d["tool_attributable"]["sync_p50_ms"]
 
 
 def test_bench_torchrun_two_ranks_cpu():
@@ -31,7 +40,7 @@ def test_bench_torchrun_two_ranks_cpu():
     drives the dev loop, rank 1 joins the timing barriers; exactly one JSON line."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", "29655", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
-           "--warmup", "1", "--tiny", "--ref-steps", "0", "--no-deploy-bench"]
+           "--warmup", "1", "--tiny", "--ref-steps", "0", "--qs-steps", "0", "--no-deploy-bench"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
