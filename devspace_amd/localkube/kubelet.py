@@ -259,6 +259,60 @@ class Kubelet:
         if obj.get("status") != status:
             self.store.update_status(group, resource, ns, md["name"], status)
 
+    def reconcile_jobs(self):
+        """Job controller (batch/v1): one pod at a time from the template; a succeeded pod
+        completes the Job (condition Complete), failed pods are replaced until
+        spec.backoffLimit (default 6) is exceeded (condition Failed). Helm hooks wait on this."""
+        for job in self.store.list("batch", "jobs"):
+            md, spec = job["metadata"], job.get("spec", {})
+            st = job.get("status") or {}
+            if md.get("deletionTimestamp") or any(c.get("status") == "True" and c.get("type") in ("Complete", "Failed")
+                                                  for c in st.get("conditions", [])):
+                continue
+            ns = md["namespace"]
+            pods = [o for (k, o) in self.store.owned_by(md["uid"]) if k[1] == "pods"]
+            succeeded = sum(1 for p in pods if (p.get("status") or {}).get("phase") == "Succeeded")
+            failed = sum(1 for p in pods if (p.get("status") or {}).get("phase") == "Failed")
+            active = [p for p in pods if (p.get("status") or {}).get("phase") not in ("Succeeded", "Failed")
+                      and not p["metadata"].get("deletionTimestamp")]
+            now = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+            status = {"active": len(active), "succeeded": succeeded, "failed": failed,
+                      "startTime": st.get("startTime") or now}
+            if succeeded >= int(spec.get("completions") or 1):
+                status["conditions"] = [{"type": "Complete", "status": "True", "lastTransitionTime": now}]
+                status["completionTime"] = now
+                status["active"] = 0
+                self.event(job, "Completed", "Job completed")
+            elif failed > int(spec.get("backoffLimit", 6)):
+                status["conditions"] = [{"type": "Failed", "status": "True", "reason": "BackoffLimitExceeded",
+                                         "message": "Job has reached the specified backoff limit",
+                                         "lastTransitionTime": now}]
+                status["active"] = 0
+                self.event(job, "BackoffLimitExceeded", "Job has reached the specified backoff limit", "Warning")
+            elif not active:
+                template = spec.get("template") or {}
+                pmd = dict(template.get("metadata") or {})
+                labels = dict(pmd.get("labels") or {})
+                labels.setdefault("job-name", md["name"])
+                labels.setdefault("controller-uid", md["uid"])
+                name = f"{md['name']}-{os.urandom(3).hex()[:5]}"
+                pspec = json.loads(json.dumps(template.get("spec") or {}))
+                pspec.setdefault("restartPolicy", "Never")
+                pod = {"apiVersion": "v1", "kind": "Pod",
+                       "metadata": {"name": name, "namespace": ns, "labels": labels,
+                                    "annotations": dict(pmd.get("annotations") or {}),
+                                    "ownerReferences": [{"apiVersion": "batch/v1", "kind": "Job", "name": md["name"],
+                                                         "uid": md["uid"], "controller": True}]},
+                       "spec": pspec, "status": {"phase": "Pending"}}
+                try:
+                    self.store.create("", "pods", ns, pod, "v1")
+                    self.event(job, "SuccessfulCreate", f"Created pod: {name}")
+                    status["active"] = 1
+                except ApiError:
+                    pass
+            if {k: v for k, v in st.items()} != status:
+                self.store.update_status("batch", "jobs", ns, md["name"], status)
+
     def reconcile_pvcs(self):
         """PV binder + pvc-protection: bind new claims to a local volume (the binder writes
         spec.volumeName, as on a real cluster), release a deleted claim once no pod uses it."""
@@ -614,9 +668,11 @@ class Kubelet:
                 wake.clear()
                 try:
                     self.reconcile_workloads()
+                    self.reconcile_jobs()
                     self.reconcile_pvcs()
                     if await self.reconcile_pods():
                         self.reconcile_workloads()
+                        self.reconcile_jobs()
                 except Exception as e:  # keep the node alive; surface in the log
                     print(f"[localkube] reconcile error: {e!r}", flush=True)
                 try:

@@ -8,7 +8,11 @@
 #include <sstream>
 #include <vector>
 
+#include <openssl/evp.h>
+#include <zlib.h>
+
 #include "core/codec.h"
+#include "core/match.h"
 #include "core/strutil.h"
 
 namespace ds {
@@ -315,6 +319,355 @@ std::vector<Segment> split_segments(const std::string& src) {
 
 }  // namespace
 
+
+// ============================================================== Helm objects with methods
+
+namespace {
+
+const char* const kObjTag = "\x01obj";
+const char* const kObjData = "\x01data";
+
+bool is_obj(const Value& v, const char* kind) {
+  if (!v.is_map()) return false;
+  const Value* t = v.find(kObjTag);
+  return t && t->str() == kind;
+}
+
+std::string base_name(const std::string& p) {
+  size_t s = p.rfind('/');
+  return s == std::string::npos ? p : p.substr(s + 1);
+}
+
+// toYAML of a map[string]string (Files.AsConfig / AsSecrets): keys sorted like yaml.Marshal.
+std::string yaml_string_map(std::vector<std::pair<std::string, std::string>> kv) {
+  std::sort(kv.begin(), kv.end());
+  Value m = Value::map();
+  for (auto& e : kv) {
+    Value v(e.second);
+    v.set_quoted(true);
+    m[e.first] = v;
+  }
+  if (kv.empty()) return "{}";
+  std::string y = yaml_dump(m);
+  if (ends_with(y, "\n")) y.pop_back();
+  return y;
+}
+
+// Method call on a Helm object; *found=false when `recv` has no such method.
+Value call_method(const Value& recv, const std::string& name, const std::vector<Value>& args, bool* found) {
+  *found = true;
+  auto need = [&](size_t n) {
+    if (args.size() != n)
+      throw TemplateError("wrong number of args for " + name + ": want " + std::to_string(n) + " got " +
+                          std::to_string(args.size()));
+  };
+  if (is_obj(recv, "files")) {
+    const Value& data = recv.get(kObjData);
+    if (name == "Get" || name == "GetBytes") {
+      need(1);
+      return Value(data.get(args[0].as_string()).as_string());
+    }
+    if (name == "Lines") {
+      need(1);
+      const Value* f = data.find(args[0].as_string());
+      if (!f || f->str().empty()) return Value::seq();
+      std::string t = f->str();
+      if (t.back() == '\n') t.pop_back();
+      return Value::strings(split(t, "\n"));
+    }
+    if (name == "Glob") {
+      need(1);
+      std::vector<std::pair<std::string, std::string>> sel;
+      for (auto& e : data.entries())
+        if (glob_match(args[0].as_string(), e.first)) sel.emplace_back(e.first, e.second.str());
+      return make_files_object(sel);
+    }
+    if (name == "AsConfig" || name == "AsSecrets") {
+      need(0);
+      std::vector<std::pair<std::string, std::string>> kv;
+      for (auto& e : data.entries())
+        kv.emplace_back(base_name(e.first), name == "AsConfig" ? e.second.str() : base64_encode(e.second.str()));
+      return Value(yaml_string_map(std::move(kv)));
+    }
+  } else if (is_obj(recv, "apiversions")) {
+    if (name == "Has") {
+      need(1);
+      for (auto& v : recv.get(kObjData).items())
+        if (v.str() == args[0].as_string()) return Value(true);
+      return Value(false);
+    }
+  }
+  *found = false;
+  return Value();
+}
+
+// "v1.2.3-rc.1+meta" -> (1, 2, 3, "rc.1"); missing / x components are 0
+struct Semver {
+  int64_t major = 0, minor = 0, patch = 0;
+  std::string pre;
+  bool ok = false;
+};
+
+Semver parse_semver(std::string v) {
+  Semver s;
+  v = trim(v);
+  if (!v.empty() && (v[0] == 'v' || v[0] == 'V')) v.erase(0, 1);
+  size_t plus = v.find('+');
+  if (plus != std::string::npos) v = v.substr(0, plus);
+  size_t dash = v.find('-');
+  if (dash != std::string::npos) {
+    s.pre = v.substr(dash + 1);
+    v = v.substr(0, dash);
+  }
+  auto parts = split(v, ".");
+  if (parts.empty() || parts.size() > 3) return s;
+  int64_t* dst[3] = {&s.major, &s.minor, &s.patch};
+  for (size_t i = 0; i < parts.size(); ++i) {
+    if (parts[i] == "x" || parts[i] == "X" || parts[i] == "*") continue;
+    if (!parse_int64(parts[i], dst[i])) return s;
+  }
+  s.ok = true;
+  return s;
+}
+
+int semver_cmp(const Semver& a, const Semver& b) {
+  if (a.major != b.major) return a.major < b.major ? -1 : 1;
+  if (a.minor != b.minor) return a.minor < b.minor ? -1 : 1;
+  if (a.patch != b.patch) return a.patch < b.patch ? -1 : 1;
+  if (a.pre == b.pre) return 0;
+  if (a.pre.empty()) return 1;  // 1.0.0 > 1.0.0-rc
+  if (b.pre.empty()) return -1;
+  return a.pre < b.pre ? -1 : 1;
+}
+
+// Masterminds/semver constraint check: comma (AND) and "||" (OR) lists of
+// =, !=, >, <, >=, <=, ~ (patch-level), ^ (major-level), x-ranges and "a - b" ranges.
+// As Helm does for Capabilities checks, a prerelease version satisfies only constraints
+// that name a prerelease — except that the "-0" idiom (">=1.19-0") admits all prereleases.
+bool semver_satisfies(const std::string& constraint, const std::string& version) {
+  Semver v = parse_semver(version);
+  if (!v.ok) throw TemplateError("invalid semantic version: " + version);
+  for (auto& alt : split(constraint, "||")) {
+    bool all = true;
+    std::string a = trim(alt);
+    // hyphen range "1.2 - 1.4.5"
+    size_t hy = a.find(" - ");
+    std::vector<std::string> terms;
+    if (hy != std::string::npos) {
+      terms.push_back(">=" + trim(a.substr(0, hy)));
+      terms.push_back("<=" + trim(a.substr(hy + 3)));
+    } else {
+      for (auto& t : split(a, ",")) {
+        // space-separated terms are ANDed too (">= 1.2 < 2")
+        std::string cur;
+        std::string tt = trim(t);
+        for (size_t i = 0; i < tt.size(); ++i) {
+          char c = tt[i];
+          if (c == ' ' && !cur.empty() && !std::strchr("<>=!~^", cur.back())) {
+            terms.push_back(cur);
+            cur.clear();
+          } else if (c != ' ') {
+            cur.push_back(c);
+          }
+        }
+        if (!cur.empty()) terms.push_back(cur);
+      }
+    }
+    for (auto& term : terms) {
+      std::string op;
+      std::string t = term;
+      while (!t.empty() && std::strchr("<>=!~^", t[0])) op.push_back(t[0]), t.erase(0, 1);
+      Semver c = parse_semver(t);
+      if (!c.ok) throw TemplateError("improper constraint: " + term);
+      std::string tv = trim(t);
+      if (!tv.empty() && (tv[0] == 'v' || tv[0] == 'V')) tv.erase(0, 1);
+      int given = 0;  // how many components were spelled (x-ranges count as not given)
+      for (auto& p : split(tv.substr(0, tv.find_first_of("-+")), ".")) {
+        if (p == "x" || p == "X" || p == "*") break;
+        ++given;
+      }
+      if (!v.pre.empty() && c.pre.empty()) {
+        all = false;  // prerelease versions only match prerelease constraints
+        break;
+      }
+      int r = semver_cmp(v, c);
+      bool ok;
+      if (op.empty() || op == "=" || op == "==") {
+        if (given >= 3) ok = r == 0;
+        else if (given == 2) ok = v.major == c.major && v.minor == c.minor;
+        else if (given == 1) ok = v.major == c.major;
+        else ok = true;
+      } else if (op == "!=") ok = r != 0;
+      else if (op == ">") {
+        if (given == 2) ok = v.major > c.major || (v.major == c.major && v.minor > c.minor);
+        else if (given == 1) ok = v.major > c.major;
+        else ok = r > 0;
+      } else if (op == ">=" || op == "=>") ok = r >= 0;
+      else if (op == "<") ok = r < 0;
+      else if (op == "<=" || op == "=<") {
+        if (given == 2) ok = v.major < c.major || (v.major == c.major && v.minor <= c.minor);
+        else if (given == 1) ok = v.major <= c.major;
+        else ok = r <= 0;
+      } else if (op == "~" || op == "~>") {
+        ok = r >= 0 && v.major == c.major && (given <= 1 || v.minor == c.minor);
+      } else if (op == "^") {
+        if (c.major > 0) ok = r >= 0 && v.major == c.major;
+        else if (c.minor > 0 || given < 3) ok = r >= 0 && v.major == 0 && (given < 2 || v.minor == c.minor);
+        else ok = r >= 0 && v.major == 0 && v.minor == 0 && v.patch == c.patch;
+      } else {
+        throw TemplateError("improper constraint: " + term);
+      }
+      if (!ok) {
+        all = false;
+        break;
+      }
+    }
+    if (all) return true;
+  }
+  return false;
+}
+
+std::string digest_hex(const EVP_MD* md, const std::string& data) {
+  unsigned char out[EVP_MAX_MD_SIZE];
+  unsigned int n = 0;
+  EVP_Digest(data.data(), data.size(), out, &n, md, nullptr);
+  return hex_encode(std::string((const char*)out, n));
+}
+
+std::string b32_encode(const std::string& in) {
+  static const char* A = "ABCDEFGHIJKLMNOPQRSTUVWXYZ234567";
+  std::string out;
+  size_t i = 0;
+  while (i < in.size()) {
+    unsigned char b[5] = {0, 0, 0, 0, 0};
+    size_t n = std::min<size_t>(5, in.size() - i);
+    for (size_t k = 0; k < n; ++k) b[k] = (unsigned char)in[i + k];
+    uint64_t x = 0;
+    for (int k = 0; k < 5; ++k) x = (x << 8) | b[k];
+    static const size_t chars_for[6] = {0, 2, 4, 5, 7, 8};
+    for (size_t k = 0; k < 8; ++k) out.push_back(k < chars_for[n] ? A[(x >> (35 - 5 * k)) & 31] : '=');
+    i += n;
+  }
+  return out;
+}
+
+std::string b32_decode(const std::string& in) {
+  std::string out;
+  uint64_t buf = 0;
+  int bits = 0;
+  for (char c : in) {
+    int v;
+    if (c >= 'A' && c <= 'Z') v = c - 'A';
+    else if (c >= '2' && c <= '7') v = c - '2' + 26;
+    else if (c == '=') break;
+    else throw TemplateError("illegal base32 data");
+    buf = (buf << 5) | (uint64_t)v;
+    bits += 5;
+    if (bits >= 8) {
+      bits -= 8;
+      out.push_back((char)((buf >> bits) & 0xff));
+    }
+  }
+  return out;
+}
+
+// Sprig's word splitting for camelcase/snakecase/kebabcase.
+std::vector<std::string> words_of(const std::string& s) {
+  std::vector<std::string> w;
+  std::string cur;
+  for (size_t i = 0; i < s.size(); ++i) {
+    char c = s[i];
+    if (c == '_' || c == '-' || c == ' ' || c == '.') {
+      if (!cur.empty()) w.push_back(cur), cur.clear();
+      continue;
+    }
+    if (std::isupper((unsigned char)c) && !cur.empty() &&
+        (std::islower((unsigned char)cur.back()) ||
+         (i + 1 < s.size() && std::islower((unsigned char)s[i + 1]) && std::isupper((unsigned char)cur.back()))))
+      w.push_back(cur), cur.clear();
+    cur.push_back(c);
+  }
+  if (!cur.empty()) w.push_back(cur);
+  return w;
+}
+
+std::string path_clean(const std::string& p) {
+  if (p.empty()) return ".";
+  bool abs = p[0] == '/';
+  std::vector<std::string> out;
+  for (auto& seg : split(p, "/")) {
+    if (seg.empty() || seg == ".") continue;
+    if (seg == "..") {
+      if (!out.empty() && out.back() != "..") out.pop_back();
+      else if (!abs) out.push_back("..");
+      continue;
+    }
+    out.push_back(seg);
+  }
+  std::string r = (abs ? "/" : "") + join(out, "/");
+  return r.empty() ? "." : r;
+}
+
+std::string toml_scalar(const Value& v) {
+  if (v.is_string()) {
+    std::string o = "\"";
+    for (char c : v.str()) {
+      if (c == '"' || c == '\\') o.push_back('\\');
+      if (c == '\n') {
+        o += "\\n";
+        continue;
+      }
+      o.push_back(c);
+    }
+    return o + "\"";
+  }
+  if (v.is_seq()) {
+    std::vector<std::string> parts;
+    for (auto& it : v.items()) parts.push_back(toml_scalar(it));
+    return "[" + join(parts, ", ") + "]";
+  }
+  return v.as_string();
+}
+
+void toml_table(const Value& m, const std::string& prefix, std::string& out) {
+  std::vector<std::string> subs;
+  for (auto& e : m.entries()) {
+    if (e.second.is_map()) {
+      subs.push_back(e.first);
+      continue;
+    }
+    if (e.second.is_null()) continue;
+    out += e.first + " = " + toml_scalar(e.second) + "\n";
+  }
+  for (auto& k : subs) {
+    std::string name = prefix.empty() ? k : prefix + "." + k;
+    out += "\n[" + name + "]\n";
+    toml_table(m.get(k), name, out);
+  }
+}
+
+}  // namespace
+
+bool semver_match(const std::string& constraint, const std::string& version) {
+  return semver_satisfies(constraint, version);
+}
+
+Value make_files_object(const std::vector<std::pair<std::string, std::string>>& files) {
+  Value o = Value::map();
+  o[kObjTag] = "files";
+  Value d = Value::map();
+  for (auto& f : files) d[f.first] = f.second;
+  o[kObjData] = d;
+  return o;
+}
+
+Value make_api_versions_object(const std::vector<std::string>& versions) {
+  Value o = Value::map();
+  o[kObjTag] = "apiversions";
+  o[kObjData] = Value::strings(versions);
+  return o;
+}
+
 // ============================================================== engine
 
 struct Engine::Impl {
@@ -480,12 +833,47 @@ struct Engine::Impl {
       if (part.empty()) continue;
       if (cur.is_map()) {
         const Value* n = cur.find(part);
+        if (!n && cur.has(kObjTag)) {  // niladic method: (.Files.Glob "x").AsConfig
+          bool found = false;
+          Value r = call_method(cur, part, {}, &found);
+          if (found) {
+            cur = r;
+            continue;
+          }
+        }
         cur = n ? *n : Value();
       } else {
         return Value();  // missingkey=zero semantics (Helm)
       }
     }
     return cur;
+  }
+
+  // `.Files.Get "x"` / `$.Capabilities.APIVersions.Has "v"`: the command's first word is a
+  // field chain ending in a method of a Helm object. Returns false if it is not a method call.
+  bool try_method_call(Scope& sc, const Arg& first, std::vector<Value>& args, Value* out) {
+    std::string chain;
+    Value base;
+    if (first.kind == Arg::Field) {
+      chain = first.name;
+      base = sc.dot;
+    } else if (first.kind == Arg::Var) {
+      size_t d = first.name.find('.');
+      if (d == std::string::npos) return false;
+      base = lookup_var(sc, first.name.substr(0, d));
+      chain = first.name.substr(d);
+    } else if (first.kind == Arg::Sub && !first.chain.empty()) {
+      base = eval_pipeline(sc, *first.sub, false);
+      chain = first.chain;
+    } else {
+      return false;
+    }
+    size_t last = chain.rfind('.');
+    Value recv = field_chain(base, chain.substr(0, last));
+    if (!recv.has(kObjTag)) return false;
+    bool found = false;
+    *out = call_method(recv, chain.substr(last + 1), args, &found);
+    return found;
   }
 
   Value lookup_var(const Scope& sc, const std::string& ref) {
@@ -522,9 +910,15 @@ struct Engine::Impl {
         std::vector<Value> args;
         for (size_t i = 1; i < c.args.size(); ++i) args.push_back(eval_arg(sc, c.args[i]));
         last = call(sc, first.name, std::move(args), have_last ? &last : nullptr);
+      } else if (c.args.size() > 1 || have_last) {
+        std::vector<Value> args;
+        for (size_t i = 1; i < c.args.size(); ++i) args.push_back(eval_arg(sc, c.args[i]));
+        if (have_last) args.push_back(last);
+        if (!try_method_call(sc, first, args, &last)) {
+          if (c.args.size() > 1) throw TemplateError("can't give argument to non-function");
+          throw TemplateError("can't pipe into non-function");
+        }
       } else {
-        if (c.args.size() > 1) throw TemplateError("can't give argument to non-function");
-        if (have_last) throw TemplateError("can't pipe into non-function");
         last = eval_arg(sc, first);
       }
       have_last = true;
@@ -684,7 +1078,7 @@ struct Engine::Impl {
     if (fn == "not") { need(1); return Value(!truth(args[0])); }
     if (fn == "len") {
       need(1);
-      const Value& v = args[0];
+      const Value& v = is_obj(args[0], "files") ? args[0].get(kObjData) : args[0];
       return Value((int64_t)(v.is_string() ? v.str().size() : v.size()));
     }
     if (fn == "index") {
@@ -922,29 +1316,21 @@ struct Engine::Impl {
       need(3);
       return S(std::regex_replace(strval(args[1]), std::regex(args[0].as_string()), args[2].as_string()));
     }
-    if (fn == "semverCompare") {
+    if (fn == "semverCompare" || fn == "mustSemverCompare") {
       need(2);
-      // supports ">=1.2.3", "<1.x" style with numeric major/minor/patch
-      std::string c = trim(args[0].as_string());
-      std::string op;
-      while (!c.empty() && std::strchr("<>=!~^", c[0])) op.push_back(c[0]), c.erase(0, 1);
-      auto parse = [](std::string v) {
-        if (!v.empty() && v[0] == 'v') v.erase(0, 1);
-        auto p = split(v.substr(0, v.find_first_of("-+")), ".");
-        std::vector<int64_t> n;
-        for (auto& x : p) n.push_back(std::atoll(x.c_str()));
-        while (n.size() < 3) n.push_back(0);
-        return n;
-      };
-      auto a = parse(args[1].as_string()), b = parse(c);
-      int r = a < b ? -1 : a > b ? 1 : 0;
-      if (op.empty() || op == "=") return Value(r == 0);
-      if (op == ">=") return Value(r >= 0);
-      if (op == ">") return Value(r > 0);
-      if (op == "<=") return Value(r <= 0);
-      if (op == "<") return Value(r < 0);
-      if (op == "!=") return Value(r != 0);
-      return Value(r >= 0);
+      return Value(semver_satisfies(args[0].as_string(), args[1].as_string()));
+    }
+    if (fn == "semver") {
+      need(1);
+      Semver v = parse_semver(args[0].as_string());
+      if (!v.ok) throw TemplateError("invalid semantic version: " + args[0].as_string());
+      Value m = Value::map();
+      m["Major"] = v.major;
+      m["Minor"] = v.minor;
+      m["Patch"] = v.patch;
+      m["Prerelease"] = v.pre;
+      m["Original"] = args[0].as_string();
+      return m;
     }
     if (fn == "include") { need(2); return S(include(args[0].as_string(), args[1])); }
     if (fn == "tpl") {
@@ -971,6 +1357,398 @@ struct Engine::Impl {
       return S(h.substr(0, 8) + "-" + h.substr(8, 4) + "-4" + h.substr(13, 3) + "-a" + h.substr(17, 3) + "-" + h.substr(20, 12));
     }
     if (fn == "randAlphaNum" || fn == "randAlpha") { need(1); return S(random_string((size_t)args[0].as_int())); }
+    // ---- wider Sprig set (strings)
+    if (fn == "sha1sum") { need(1); return S(digest_hex(EVP_sha1(), strval(args[0]))); }
+    if (fn == "adler32sum") {
+      need(1);
+      std::string d = strval(args[0]);
+      return S(std::to_string(::adler32(::adler32(0L, Z_NULL, 0), (const Bytef*)d.data(), (uInt)d.size())));
+    }
+    if (fn == "b32enc") { need(1); return S(b32_encode(strval(args[0]))); }
+    if (fn == "b32dec") { need(1); return S(b32_decode(strval(args[0]))); }
+    if (fn == "abbrev") {
+      need(2);
+      std::string str = strval(args[1]);
+      int64_t w = args[0].as_int();
+      if (w < 4 || (int64_t)str.size() <= w) return S(str);
+      return S(str.substr(0, (size_t)w - 3) + "...");
+    }
+    if (fn == "abbrevboth") {
+      need(3);
+      std::string str = strval(args[2]);
+      int64_t l = args[0].as_int(), w = args[1].as_int();
+      if ((int64_t)str.size() <= w) return S(str);
+      if (l > 4) str = "..." + str.substr((size_t)std::min<int64_t>(l, (int64_t)str.size()));
+      if ((int64_t)str.size() > w) str = str.substr(0, (size_t)std::max<int64_t>(0, w - 3)) + "...";
+      return S(str);
+    }
+    if (fn == "camelcase") {
+      need(1);
+      std::string o;
+      for (auto& w : words_of(strval(args[0]))) {
+        std::string x = to_lower(w);
+        x[0] = (char)std::toupper((unsigned char)x[0]);
+        o += x;
+      }
+      return S(o);
+    }
+    if (fn == "snakecase" || fn == "kebabcase") {
+      need(1);
+      std::vector<std::string> ws;
+      for (auto& w : words_of(strval(args[0]))) ws.push_back(to_lower(w));
+      return S(join(ws, fn == "snakecase" ? "_" : "-"));
+    }
+    if (fn == "swapcase") {
+      need(1);
+      std::string o = strval(args[0]);
+      for (auto& c : o)
+        c = std::isupper((unsigned char)c) ? (char)std::tolower((unsigned char)c) : (char)std::toupper((unsigned char)c);
+      return S(o);
+    }
+    if (fn == "untitle") {
+      need(1);
+      std::string o = strval(args[0]);
+      bool start = true;
+      for (auto& c : o) {
+        if (start && std::isalpha((unsigned char)c)) c = (char)std::tolower((unsigned char)c);
+        start = std::isspace((unsigned char)c);
+      }
+      return S(o);
+    }
+    if (fn == "initials") {
+      need(1);
+      std::string o;
+      for (auto& w : split(strval(args[0]), " "))
+        if (!w.empty()) o.push_back(w[0]);
+      return S(o);
+    }
+    if (fn == "nospace") {
+      need(1);
+      std::string o;
+      for (char c : strval(args[0]))
+        if (!std::isspace((unsigned char)c)) o.push_back(c);
+      return S(o);
+    }
+    if (fn == "substr") {
+      need(3);
+      std::string str = strval(args[2]);
+      int64_t a = args[0].as_int(), b = args[1].as_int();
+      if (a < 0) return S(str.substr(0, (size_t)std::min<int64_t>(b, (int64_t)str.size())));
+      if (b < 0 || b > (int64_t)str.size()) return S(a < (int64_t)str.size() ? str.substr((size_t)a) : "");
+      return S(a < b ? str.substr((size_t)a, (size_t)(b - a)) : "");
+    }
+    if (fn == "wrap" || fn == "wrapWith") {
+      need(fn == "wrap" ? 2 : 3);
+      size_t width = (size_t)args[0].as_int();
+      std::string nl = fn == "wrap" ? "\n" : args[1].as_string();
+      std::string out, line;
+      for (auto& w : split(strval(args.back()), " ")) {
+        if (w.empty()) continue;
+        if (!line.empty() && line.size() + 1 + w.size() > width) {
+          out += line + nl;
+          line.clear();
+        }
+        line += (line.empty() ? "" : " ") + w;
+      }
+      return S(out + line);
+    }
+    if (fn == "cat") {
+      std::vector<std::string> parts;
+      for (auto& a : args)
+        if (!a.is_null()) parts.push_back(strval(a));
+      return S(join(parts, " "));
+    }
+    if (fn == "plural") { need(3); return S(args[2].as_int() == 1 ? args[0].as_string() : args[1].as_string()); }
+    if (fn == "randNumeric" || fn == "randAscii") {
+      need(1);
+      std::string r = random_string((size_t)args[0].as_int());
+      if (fn == "randNumeric")
+        for (auto& c : r) c = (char)('0' + ((unsigned char)c % 10));
+      return S(r);
+    }
+    if (fn == "trimall") { need(2); return S(trim(strval(args[1]), args[0].as_string())); }
+    // ---- lists
+    if (fn == "append" || fn == "push") { need(2); Value l = args[0].is_null() ? Value::seq() : args[0]; l.push(args[1]); return l; }
+    if (fn == "prepend") {
+      need(2);
+      Value l = Value::seq();
+      l.push(args[1]);
+      for (auto& it : args[0].items()) l.push(it);
+      return l;
+    }
+    if (fn == "concat") {
+      Value l = Value::seq();
+      for (auto& a : args)
+        for (auto& it : a.items()) l.push(it);
+      return l;
+    }
+    if (fn == "uniq") {
+      need(1);
+      Value l = Value::seq();
+      for (auto& it : args[0].items()) {
+        bool dup = false;
+        for (auto& x : l.items()) dup |= cmp_eq(x, it);
+        if (!dup) l.push(it);
+      }
+      return l;
+    }
+    if (fn == "compact") {
+      need(1);
+      Value l = Value::seq();
+      for (auto& it : args[0].items())
+        if (truth(it)) l.push(it);
+      return l;
+    }
+    if (fn == "without") {
+      need(1);
+      Value l = Value::seq();
+      for (auto& it : args[0].items()) {
+        bool drop = false;
+        for (size_t i = 1; i < args.size(); ++i) drop |= cmp_eq(args[i], it);
+        if (!drop) l.push(it);
+      }
+      return l;
+    }
+    if (fn == "rest" || fn == "initial" || fn == "reverse") {
+      need(1);
+      Value l = Value::seq();
+      const auto& its = args[0].items();
+      if (fn == "rest")
+        for (size_t i = 1; i < its.size(); ++i) l.push(its[i]);
+      else if (fn == "initial")
+        for (size_t i = 0; i + 1 < its.size(); ++i) l.push(its[i]);
+      else
+        for (auto it = its.rbegin(); it != its.rend(); ++it) l.push(*it);
+      return l;
+    }
+    if (fn == "sortAlpha") {
+      need(1);
+      std::vector<std::string> v;
+      for (auto& it : args[0].items()) v.push_back(strval(it));
+      std::sort(v.begin(), v.end());
+      return Value::strings(v);
+    }
+    if (fn == "slice") {
+      need(1);
+      if (args[0].is_string()) {
+        const std::string& str = args[0].str();
+        size_t a = args.size() > 1 ? (size_t)args[1].as_int() : 0, b = args.size() > 2 ? (size_t)args[2].as_int() : str.size();
+        if (a > b || b > str.size()) throw TemplateError("slice: index out of range");
+        return S(str.substr(a, b - a));
+      }
+      const auto& its = args[0].items();
+      size_t a = args.size() > 1 ? (size_t)args[1].as_int() : 0, b = args.size() > 2 ? (size_t)args[2].as_int() : its.size();
+      if (a > b || b > its.size()) throw TemplateError("slice: index out of range");
+      Value l = Value::seq();
+      for (size_t i = a; i < b; ++i) l.push(its[i]);
+      return l;
+    }
+    if (fn == "untilStep") {
+      need(3);
+      Value l = Value::seq();
+      int64_t a = args[0].as_int(), b = args[1].as_int(), st = args[2].as_int();
+      if (st == 0) return l;
+      for (int64_t i = a; st > 0 ? i < b : i > b; i += st) l.push(Value(i));
+      return l;
+    }
+    if (fn == "seq") {
+      need(1);
+      int64_t a = 1, b = args.back().as_int(), st = 1;
+      if (args.size() == 2) a = args[0].as_int(), b = args[1].as_int();
+      if (args.size() >= 3) a = args[0].as_int(), st = args[1].as_int(), b = args[2].as_int();
+      if (args.size() >= 2 && args.size() < 3 && a > b) st = -1;
+      std::vector<std::string> o;
+      if (st != 0)
+        for (int64_t i = a; st > 0 ? i <= b : i >= b; i += st) o.push_back(std::to_string(i));
+      return S(join(o, " "));
+    }
+    if (fn == "all") {
+      for (auto& a : args)
+        if (!truth(a)) return Value(false);
+      return Value(true);
+    }
+    if (fn == "any") {
+      for (auto& a : args)
+        if (truth(a)) return Value(true);
+      return Value(false);
+    }
+    // ---- dicts
+    if (fn == "pick" || fn == "omit") {
+      need(1);
+      Value m = Value::map();
+      for (auto& e : args[0].entries()) {
+        bool listed = false;
+        for (size_t i = 1; i < args.size(); ++i) listed |= args[i].as_string() == e.first;
+        if (listed == (fn == "pick")) m[e.first] = e.second;
+      }
+      return m;
+    }
+    if (fn == "pluck") {
+      need(1);
+      Value l = Value::seq();
+      for (size_t i = 1; i < args.size(); ++i)
+        if (args[i].has(args[0].as_string())) l.push(args[i].get(args[0].as_string()));
+      return l;
+    }
+    if (fn == "dig") {
+      need(3);
+      Value cur = args.back();
+      for (size_t i = 0; i + 2 < args.size(); ++i) {
+        const Value* n = cur.is_map() ? cur.find(args[i].as_string()) : nullptr;
+        if (!n) return args[args.size() - 2];
+        cur = *n;
+      }
+      return cur;
+    }
+    if (fn == "deepCopy") { need(1); return args[0]; }
+    if (fn == "deepEqual") { need(2); return Value(args[0] == args[1]); }
+    if (fn == "kindOf") {
+      need(1);
+      const Value& v = args[0];
+      return S(v.is_map() ? "map" : v.is_seq() ? "slice" : v.is_string() ? "string" : v.is_int() ? "int64"
+               : v.is_float() ? "float64" : v.is_bool() ? "bool" : "invalid");
+    }
+    if (fn == "typeIs" || fn == "typeIsLike") {
+      need(2);
+      const Value& v = args[1];
+      std::string t = v.is_map() ? "map[string]interface {}" : v.is_seq() ? "[]interface {}" : v.is_string() ? "string"
+                      : v.is_int() ? "int64" : v.is_float() ? "float64" : v.is_bool() ? "bool" : "<nil>";
+      std::string want = args[0].as_string();
+      if (fn == "typeIsLike" && starts_with(want, "*")) want = want.substr(1);
+      return Value(t == want || (want == "int" && t == "int64"));
+    }
+    // ---- regex / paths / math / encodings
+    if (fn == "regexFind") {
+      need(2);
+      std::smatch m;
+      std::string str = strval(args[1]);
+      return S(std::regex_search(str, m, std::regex(args[0].as_string())) ? m.str(0) : "");
+    }
+    if (fn == "regexFindAll" || fn == "regexSplit") {
+      need(3);
+      std::string str = strval(args[1]);
+      std::regex re(args[0].as_string());
+      int64_t n = args[2].as_int();
+      std::vector<std::string> out;
+      if (fn == "regexFindAll") {
+        for (auto it = std::sregex_iterator(str.begin(), str.end(), re); it != std::sregex_iterator(); ++it) {
+          if (n >= 0 && (int64_t)out.size() >= n) break;
+          out.push_back(it->str(0));
+        }
+      } else {
+        size_t pos = 0;
+        for (auto it = std::sregex_iterator(str.begin(), str.end(), re); it != std::sregex_iterator(); ++it) {
+          if (n > 0 && (int64_t)out.size() >= n - 1) break;
+          out.push_back(str.substr(pos, (size_t)it->position(0) - pos));
+          pos = (size_t)(it->position(0) + it->length(0));
+        }
+        out.push_back(str.substr(pos));
+      }
+      return Value::strings(out);
+    }
+    if (fn == "regexReplaceAllLiteral") {
+      need(3);
+      return S(std::regex_replace(strval(args[1]), std::regex(args[0].as_string()), args[2].as_string(),
+                                  std::regex_constants::format_sed));
+    }
+    if (fn == "regexQuoteMeta") {
+      need(1);
+      std::string o;
+      for (char c : strval(args[0])) {
+        if (std::strchr("\\.+*?()|[]{}^$", c)) o.push_back('\\');
+        o.push_back(c);
+      }
+      return S(o);
+    }
+    if (fn == "base") { need(1); std::string p = path_clean(strval(args[0])); return S(p == "/" ? "/" : base_name(p)); }
+    if (fn == "dir") {
+      need(1);
+      std::string p = path_clean(strval(args[0]));
+      size_t k = p.rfind('/');
+      return S(k == std::string::npos ? "." : k == 0 ? "/" : p.substr(0, k));
+    }
+    if (fn == "ext") {
+      need(1);
+      std::string b = base_name(strval(args[0]));
+      size_t k = b.rfind('.');
+      return S(k == std::string::npos ? "" : b.substr(k));
+    }
+    if (fn == "clean") { need(1); return S(path_clean(strval(args[0]))); }
+    if (fn == "isAbs") { need(1); return Value(!strval(args[0]).empty() && strval(args[0])[0] == '/'); }
+    if (fn == "floor") { need(1); return Value(std::floor(args[0].as_double())); }
+    if (fn == "ceil") { need(1); return Value(std::ceil(args[0].as_double())); }
+    if (fn == "round") {
+      need(2);
+      double p = std::pow(10.0, (double)args[1].as_int());
+      return Value(std::round(args[0].as_double() * p) / p);
+    }
+    if (fn == "add1") { need(1); return Value(args[0].as_int() + 1); }
+    if (fn == "addf" || fn == "subf" || fn == "mulf" || fn == "divf" || fn == "maxf" || fn == "minf") {
+      need(1);
+      double r = args[0].as_double();
+      for (size_t i = 1; i < args.size(); ++i) {
+        double x = args[i].as_double();
+        if (fn == "addf") r += x;
+        else if (fn == "subf") r -= x;
+        else if (fn == "mulf") r *= x;
+        else if (fn == "divf") r /= x;
+        else if (fn == "maxf") r = std::max(r, x);
+        else r = std::min(r, x);
+      }
+      return Value(r);
+    }
+    if (fn == "toDecimal") { need(1); return Value((int64_t)std::strtoll(strval(args[0]).c_str(), nullptr, 8)); }
+    if (fn == "toToml") {
+      need(1);
+      std::string o;
+      if (args[0].is_map()) toml_table(args[0], "", o);
+      return S(o);
+    }
+    if (fn == "fromYamlArray" || fn == "fromJsonArray") {
+      need(1);
+      Value v = fn == "fromYamlArray" ? yaml_parse(args[0].as_string()) : json_parse(args[0].as_string());
+      return v.is_seq() ? v : Value::seq();
+    }
+    if (fn == "urlquery") {
+      std::string o;
+      for (auto& a : args) o += strval(a);
+      std::string r;
+      for (unsigned char c : o) {
+        if (std::isalnum(c) || c == '-' || c == '_' || c == '.' || c == '~') r.push_back((char)c);
+        else if (c == ' ') r.push_back('+');
+        else r += strfmt("%%%02X", c);
+      }
+      return S(r);
+    }
+    if (fn == "html" || fn == "js") {
+      std::string o;
+      for (auto& a : args) o += strval(a);
+      std::string r;
+      for (char c : o) {
+        if (fn == "html") {
+          if (c == '<') r += "&lt;"; else if (c == '>') r += "&gt;"; else if (c == '&') r += "&amp;";
+          else if (c == '"') r += "&#34;"; else if (c == '\'') r += "&#39;"; else r.push_back(c);
+        } else {
+          if (c == '\\' || c == '\'' || c == '"') r += std::string("\\") + c;
+          else if (c == '<') r += "\\u003C"; else if (c == '>') r += "\\u003E"; else if (c == '&') r += "\\u0026";
+          else if (c == '=') r += "\\u003D"; else if (c == '\n') r += "\\n"; else r.push_back(c);
+        }
+      }
+      return S(r);
+    }
+    if (fn == "unixEpoch") return S(std::to_string((long long)std::time(nullptr)));
+    if (fn == "dateInZone" || fn == "htmlDate") {
+      std::time_t t = std::time(nullptr);
+      char buf[64];
+      std::strftime(buf, sizeof(buf), "%Y-%m-%d", std::gmtime(&t));
+      return S(buf);
+    }
+    // mustX is X that returns its error instead of panicking; errors already throw here
+    if (starts_with(fn, "must") && fn.size() > 4 && std::isupper((unsigned char)fn[4])) {
+      std::string base(1, (char)std::tolower((unsigned char)fn[4]));
+      base += fn.substr(5);
+      return call(sc, base, std::move(args), nullptr);
+    }
     throw TemplateError("function \"" + fn + "\" not defined");
   }
 
@@ -1011,6 +1789,7 @@ struct Engine::Impl {
         std::vector<std::string> decl = p.decl;
         p.decl.clear();
         Value v = eval_pipeline(sc, p, false);
+        if (is_obj(v, "files")) v = v.get(kObjData);  // range over .Files: path -> bytes
         std::vector<std::pair<Value, Value>> items;
         if (v.is_seq()) {
           for (size_t i = 0; i < v.size(); ++i) items.emplace_back(Value((int64_t)i), v[i]);

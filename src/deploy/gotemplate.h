@@ -9,7 +9,12 @@
 // trimSuffix upper lower title replace contains hasPrefix hasSuffix trunc repeat join split
 // splitList list dict get set unset hasKey keys values merge int int64 float64 toString atoi
 // add sub mul div mod max min until b64enc b64dec sha256sum kindIs typeOf regexMatch
-// regexReplaceAll semverCompare tpl lookup (nil) now date uuidv4 randAlphaNum.
+// regexReplaceAll semverCompare tpl lookup (nil) now date uuidv4 randAlphaNum, plus the wider
+// Sprig set stable charts use (string case/abbrev/wrap/substr, list append/prepend/concat/uniq/
+// without/rest/initial/reverse/sortAlpha/compact/slice, dict pick/omit/pluck/dig/deepCopy,
+// regexFind(All)/regexSplit, path base/dir/ext/clean, math floor/ceil/round, sha1/adler32,
+// b32enc/dec, semver, toToml, fromYamlArray/fromJsonArray, urlquery, and the must* variants),
+// and method calls on Helm's Files / APIVersions objects (see below).
 #pragma once
 
 #include <functional>
@@ -17,6 +22,8 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "core/value.h"
 
@@ -46,6 +53,18 @@ class Engine {
  private:
   std::unique_ptr<Impl> impl_;
 };
+
+// Helm's built-in objects with methods. Go templates call methods on values
+// (`.Files.Get "x"`, `(.Files.Glob "conf/*").AsConfig`, `.Capabilities.APIVersions.Has "apps/v1"`);
+// these are maps tagged with a reserved key that the engine dispatches method calls on.
+//   Files:       Get GetBytes Glob Lines AsConfig AsSecrets   (helm pkg/engine/files.go)
+//   APIVersions: Has
+Value make_files_object(const std::vector<std::pair<std::string, std::string>>& files);
+Value make_api_versions_object(const std::vector<std::string>& versions);
+
+// Masterminds/semver constraint check (semverCompare, requirements version ranges):
+// "^1.2", "~1.2.3", ">=1.19-0", "1.x", "1.2 - 1.4", "a || b", "a, b". Throws on a bad version.
+bool semver_match(const std::string& constraint, const std::string& version);
 
 }  // namespace tmpl
 }  // namespace ds

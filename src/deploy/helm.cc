@@ -2,6 +2,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <ctime>
+#include <map>
 #include <set>
 #include <thread>
 
@@ -11,6 +13,7 @@
 #include "core/log.h"
 #include "core/strutil.h"
 #include "core/trace.h"
+#include "core/match.h"
 #include "deploy/gotemplate.h"
 
 namespace ds {
@@ -31,26 +34,75 @@ int kind_order(const std::string& kind) {
 
 void merge_values(Value& base, const Value& over) { merge_into(base, over); }
 
+// ============================================================== chart loading
+
+// Helm 3 loader: these names are chart structure, everything else is a `.Files` entry.
+static bool special_chart_file(const std::string& rel) {
+  return rel == "Chart.yaml" || rel == "values.yaml" || rel == "values.schema.json" || rel == "requirements.yaml" ||
+         rel == "requirements.lock" || rel == "Chart.lock" || rel == ".helmignore" || starts_with(rel, "templates/") ||
+         starts_with(rel, "charts/");
+}
+
+static std::vector<Dependency> parse_requirements(const Value& list) {
+  std::vector<Dependency> out;
+  for (auto& d : list.items()) {
+    Dependency r;
+    r.name = d.get("name").as_string();
+    r.version = d.get("version").as_string();
+    r.repository = d.get("repository").as_string();
+    r.condition = d.get("condition").as_string();
+    r.alias = d.get("alias").as_string();
+    for (auto& t : d.get("tags").items()) r.tags.push_back(t.as_string());
+    r.import_values = d.get("import-values").is_seq() ? d.get("import-values") : Value::seq();
+    out.push_back(std::move(r));
+  }
+  return out;
+}
+
 Chart load_chart(const std::string& dir) {
   Chart c;
   c.dir = dir;
   std::string cy = fs::join(dir, "Chart.yaml");
   if (!fs::exists(cy)) throw std::runtime_error("Chart.yaml file is missing in " + dir);
   c.metadata = yaml_load_file(cy);
+  if (!c.metadata.is_map()) throw std::runtime_error("Chart.yaml in " + dir + " is not a map");
   std::string vy = fs::join(dir, "values.yaml");
-  if (fs::exists(vy)) c.values = yaml_load_file(vy);
-  if (!c.values.is_map()) c.values = Value::map();
-  std::string tdir = fs::join(dir, "templates");
-  if (fs::is_dir(tdir)) {
-    fs::walk(tdir, [&](const std::string& p, const fs::StatInfo& st) {
-      if (!st.is_dir) c.templates.emplace_back(fs::relative(dir, p), fs::read_file(p));
-      return true;
-    });
-    std::sort(c.templates.begin(), c.templates.end());
+  if (fs::exists(vy)) {
+    c.values_raw = fs::read_file(vy);
+    c.values = yaml_parse(c.values_raw);
   }
+  if (!c.values.is_map()) c.values = Value::map();
+  if (fs::exists(fs::join(dir, "values.schema.json"))) c.schema = fs::read_file(fs::join(dir, "values.schema.json"));
+  // dependencies: Chart.yaml (apiVersion v2) or requirements.yaml (v1)
+  if (c.metadata.get("dependencies").is_seq()) {
+    c.requirements = parse_requirements(c.metadata.get("dependencies"));
+  } else if (fs::exists(fs::join(dir, "requirements.yaml"))) {
+    c.requirements = parse_requirements(yaml_load_file(fs::join(dir, "requirements.yaml")).get("dependencies"));
+  }
+  GitIgnore ignore;
+  std::string hi = fs::join(dir, ".helmignore");
+  if (fs::exists(hi)) ignore.add_lines(split(fs::read_file(hi), "\n"));
+  fs::walk(dir, [&](const std::string& p, const fs::StatInfo& st) {
+    if (p == dir) return true;
+    std::string rel = fs::relative(dir, p);
+    if (rel == "charts") return false;  // subcharts are loaded below
+    if (!ignore.empty() && ignore.matches("/" + rel + (st.is_dir ? "/" : ""))) return false;
+    if (st.is_dir) return true;
+    if (starts_with(rel, "templates/")) {
+      // the loader skips hidden files in templates/ (rules.AddDefaults)
+      if (!starts_with(fs::basename(rel), ".")) c.templates.emplace_back(rel, fs::read_file(p));
+    } else if (!special_chart_file(rel)) {
+      c.files.emplace_back(rel, fs::read_file(p));
+    }
+    return true;
+  });
+  std::sort(c.templates.begin(), c.templates.end());
+  std::sort(c.files.begin(), c.files.end());
   std::string cdir = fs::join(dir, "charts");
   if (fs::is_dir(cdir)) {
-    for (auto& e : fs::list_dir(cdir)) {
+    auto entries = fs::list_dir(cdir);
+    std::sort(entries.begin(), entries.end(), [](const fs::DirEntry& a, const fs::DirEntry& b) { return a.name < b.name; });
+    for (auto& e : entries) {
       std::string sub = fs::join(cdir, e.name);
       if (e.is_dir && fs::exists(fs::join(sub, "Chart.yaml"))) {
         c.dependencies.push_back(load_chart(sub));
@@ -75,13 +127,210 @@ Chart load_chart(const std::string& dir) {
   return c;
 }
 
+// ============================================================== values + dependencies
+
+// Helm's coalesce: `over` wins, maps merge recursively, a null in `over` deletes the key.
+static void coalesce_into(Value& base, const Value& over) {
+  if (!over.is_map()) return;
+  if (!base.is_map()) base = Value::map();
+  for (auto& e : over.entries()) {
+    if (e.second.is_null()) {
+      base.erase(e.first);
+      continue;
+    }
+    Value* cur = base.find(e.first);
+    if (cur && cur->is_map() && e.second.is_map())
+      coalesce_into(*cur, e.second);
+    else
+      base[e.first] = e.second;
+  }
+}
+
+// CoalesceTables(dst, src): keys missing in dst are filled from src; dst wins.
+static void fill_missing(Value& dst, const Value& src) {
+  if (!src.is_map()) return;
+  if (!dst.is_map()) dst = Value::map();
+  for (auto& e : src.entries()) {
+    Value* cur = dst.find(e.first);
+    if (!cur)
+      dst[e.first] = e.second;
+    else if (cur->is_map() && e.second.is_map())
+      fill_missing(*cur, e.second);
+  }
+}
+
+Value coalesce_values(const Chart& c, const Value& user_values) {
+  Value v = c.values.is_map() ? c.values : Value::map();
+  coalesce_into(v, user_values);
+  for (auto& d : c.dependencies) {
+    Value sub = coalesce_values(d, v.get(d.name()));
+    const Value& g = v.get("global");
+    if (g.is_map()) {  // the parent's globals reach every subchart and win over the subchart's own
+      Value sg = sub.get("global").is_map() ? sub.get("global") : Value::map();
+      coalesce_into(sg, g);
+      sub["global"] = sg;
+    }
+    v[d.name()] = sub;
+  }
+  return v;
+}
+
+static bool version_compatible(const std::string& constraint, const std::string& version) {
+  if (constraint.empty() || version.empty()) return true;
+  try {
+    return tmpl::semver_match(constraint, version);
+  } catch (const std::exception&) {
+    return constraint == version;
+  }
+}
+
+// processDependencyEnabled: alias copies, then tags and conditions against the coalesced
+// values of the whole tree (`top`), with `path` the chart's position in it ("" or "sub.").
+static void dependency_enabled(Chart& c, const Value& top, const std::string& path) {
+  if (c.requirements.empty()) return;
+  std::vector<Chart> deps;
+  for (auto& ex : c.dependencies) {
+    bool listed = false;
+    for (auto& r : c.requirements) listed |= ex.name() == r.name && version_compatible(r.version, ex.version());
+    if (!listed) deps.push_back(ex);  // charts/ entries no requirement names stay enabled
+  }
+  for (auto& r : c.requirements) {
+    for (auto& ex : c.dependencies) {
+      if (ex.name() != r.name || !version_compatible(r.version, ex.version())) continue;
+      Chart copy = ex;
+      if (!r.alias.empty()) copy.metadata["name"] = r.alias;
+      deps.push_back(std::move(copy));
+      break;
+    }
+    if (!r.alias.empty()) r.name = r.alias;
+    r.enabled = true;
+  }
+  c.dependencies = std::move(deps);
+  const Value& tags = top.get("tags");
+  for (auto& r : c.requirements) {
+    bool has_true = false, has_false = false;
+    for (auto& t : r.tags) {
+      const Value* b = tags.is_map() ? tags.find(t) : nullptr;
+      if (b && b->is_bool()) (b->as_bool() ? has_true : has_false) = true;
+    }
+    if (!has_true && has_false) r.enabled = false;
+    for (auto& cond : split(r.condition, ",")) {
+      std::string k = trim(cond);
+      if (k.empty()) continue;
+      const Value& v = top.at_path(path + k);
+      if (v.is_bool()) {
+        r.enabled = v.as_bool();
+        break;
+      }
+    }
+  }
+  std::set<std::string> off;
+  for (auto& r : c.requirements)
+    if (!r.enabled) off.insert(r.name);
+  std::vector<Chart> keep;
+  for (auto& d : c.dependencies)
+    if (!off.count(d.name())) keep.push_back(std::move(d));
+  c.dependencies = std::move(keep);
+  for (auto& d : c.dependencies) dependency_enabled(d, top, path + d.name() + ".");
+}
+
+static Value path_to_map(const std::string& path, const Value& data) {
+  if (path.empty() || path == ".") return data;
+  Value out = Value::map();
+  Value* cur = &out;
+  auto parts = split(path, ".");
+  for (size_t i = 0; i < parts.size(); ++i) {
+    if (parts[i].empty()) continue;
+    if (i + 1 == parts.size())
+      (*cur)[parts[i]] = data;
+    else
+      cur = &(*cur)[parts[i]];
+  }
+  return out;
+}
+
+// processImportValues (bottom-up): child values copied into the parent's values; the
+// parent's own values take precedence over imported ones.
+static void import_values(Chart& c) {
+  for (auto& d : c.dependencies) import_values(d);
+  bool any = false;
+  for (auto& r : c.requirements) any |= r.import_values.size() > 0;
+  if (!any) return;
+  Value cvals = coalesce_values(c, Value::map());
+  Value b = Value::map();
+  for (auto& r : c.requirements) {
+    if (!r.enabled) continue;
+    for (auto& iv : r.import_values.items()) {
+      if (iv.is_map()) {
+        const Value& vv = cvals.at_path(r.name + "." + iv.get("child").as_string());
+        if (vv.is_map()) fill_missing(b, path_to_map(iv.get("parent").as_string(), vv));
+      } else if (iv.is_string()) {
+        const Value& vm = cvals.at_path(r.name + ".exports." + iv.as_string());
+        if (vm.is_map()) fill_missing(b, vm);
+      }
+    }
+  }
+  Value nv = c.values;
+  fill_missing(nv, b);
+  c.values = nv;
+}
+
+void process_dependencies(Chart& c, const Value& user_values) {
+  dependency_enabled(c, coalesce_values(c, user_values), "");
+  import_values(c);
+}
+
+// ============================================================== rendering
+
+static bool mentions_capabilities(const Chart& c) {
+  for (auto& t : c.templates)
+    if (t.second.find("Capabilities") != std::string::npos) return true;
+  for (auto& d : c.dependencies)
+    if (mentions_capabilities(d)) return true;
+  return false;
+}
+
+static const char* kHelmVersion = "v3.14.0";
+
+static Value capabilities_value(const Value& in) {
+  Value caps = Value::map();
+  const Value& kv = in.get("KubeVersion");
+  std::string git = kv.get("GitVersion").as_string("v1.29.0");
+  caps["KubeVersion"]["Major"] = kv.get("Major").as_string("1");
+  caps["KubeVersion"]["Minor"] = kv.get("Minor").as_string("29");
+  caps["KubeVersion"]["GitVersion"] = git;
+  caps["KubeVersion"]["Version"] = git;
+  std::vector<std::string> apis;
+  for (auto& a : in.get("APIVersions").items()) apis.push_back(a.as_string());
+  if (apis.empty())
+    apis = {"v1", "apps/v1", "batch/v1", "rbac.authorization.k8s.io/v1", "autoscaling/v1", "autoscaling/v2",
+            "networking.k8s.io/v1", "policy/v1", "storage.k8s.io/v1", "apiextensions.k8s.io/v1"};
+  caps["APIVersions"] = tmpl::make_api_versions_object(apis);
+  caps["HelmVersion"]["Version"] = kHelmVersion;
+  caps["HelmVersion"]["GitCommit"] = "";
+  caps["HelmVersion"]["GoVersion"] = "";
+  return caps;
+}
+
 static void add_templates(tmpl::Engine& eng, const Chart& c, const std::string& prefix) {
   for (auto& t : c.templates) eng.add(prefix + t.first, t.second);
   for (auto& d : c.dependencies) add_templates(eng, d, prefix + "charts/" + d.name() + "/");
 }
 
+static Value chart_object(const Chart& c) {
+  Value chart = Value::map();
+  for (auto& e : c.metadata.entries()) {
+    std::string k = e.first;
+    if (k == "apiVersion") k = "APIVersion";
+    if (!k.empty()) k[0] = (char)std::toupper((unsigned char)k[0]);
+    chart[k] = e.second;
+  }
+  return chart;
+}
+
 static void render_chart(tmpl::Engine& eng, const Chart& c, const Value& values, const RenderOptions& o,
-                         const std::string& prefix, std::vector<std::pair<std::string, std::string>>* out) {
+                         const Value& caps, const std::string& prefix, bool top,
+                         std::vector<std::pair<std::string, std::string>>* out) {
   Value dot = Value::map();
   dot["Values"] = values;
   Value rel = Value::map();
@@ -93,50 +342,72 @@ static void render_chart(tmpl::Engine& eng, const Chart& c, const Value& values,
   rel["Revision"] = o.revision;
   rel["Time"] = log::rfc3339_now();
   dot["Release"] = rel;
-  Value chart = Value::map();
-  for (auto& e : c.metadata.entries()) {
-    std::string k = e.first;
-    if (!k.empty()) k[0] = (char)std::toupper((unsigned char)k[0]);
-    chart[k] = e.second;
-  }
-  dot["Chart"] = chart;
-  Value caps = Value::map();
-  caps["KubeVersion"]["Major"] = "1";
-  caps["KubeVersion"]["Minor"] = "29";
-  caps["KubeVersion"]["GitVersion"] = "v1.29.0";
-  caps["KubeVersion"]["Version"] = "v1.29.0";
-  caps["APIVersions"] = Value::strings({"v1", "apps/v1", "batch/v1", "rbac.authorization.k8s.io/v1",
-                                        "autoscaling/v2", "autoscaling/v2beta1", "networking.k8s.io/v1"});
+  dot["Chart"] = chart_object(c);
   dot["Capabilities"] = caps;
-  for (auto& t : c.templates) {
-    std::string base = fs::basename(t.first);
-    if (starts_with(base, "_")) continue;  // partials
-    if (!ends_with(base, ".yaml") && !ends_with(base, ".yml") && !ends_with(base, ".tpl") && !ends_with(base, ".json"))
-      continue;
-    if (ends_with(base, ".tpl")) continue;
-    Value d = dot;
-    d["Template"]["Name"] = c.name() + "/" + t.first;
-    d["Template"]["BasePath"] = c.name() + "/templates";
-    out->emplace_back(prefix + t.first, eng.execute(prefix + t.first, d));
+  dot["Files"] = tmpl::make_files_object(c.files);
+  if (!c.is_library()) {  // library charts only contribute their defines
+    for (auto& t : c.templates) {
+      std::string base = fs::basename(t.first);
+      bool notes = top && t.first == "templates/NOTES.txt";
+      if (starts_with(base, "_")) continue;  // partials
+      if (!notes && !ends_with(base, ".yaml") && !ends_with(base, ".yml") && !ends_with(base, ".json")) continue;
+      Value d = dot;
+      d["Template"]["Name"] = c.name() + "/" + t.first;
+      d["Template"]["BasePath"] = c.name() + "/templates";
+      out->emplace_back(prefix + t.first, eng.execute(prefix + t.first, d));
+    }
   }
   for (auto& dep : c.dependencies) {
-    Value sub = dep.values;
-    merge_into(sub, values.get(dep.name()));
-    if (values.get("global").is_map()) merge_into(sub["global"], values.get("global"));
-    render_chart(eng, dep, sub, o, prefix + "charts/" + dep.name() + "/", out);
+    // idempotent on already-coalesced values; also accepts plain user values
+    Value sub = coalesce_values(dep, values.get(dep.name()));
+    if (values.get("global").is_map()) {
+      Value sg = sub.get("global").is_map() ? sub.get("global") : Value::map();
+      coalesce_into(sg, values.get("global"));
+      sub["global"] = sg;
+    }
+    render_chart(eng, dep, sub, o, caps, prefix + "charts/" + dep.name() + "/", false, out);
   }
 }
 
-std::string render_to_string(const Chart& chart, const Value& values, const RenderOptions& o) {
+std::vector<std::pair<std::string, std::string>> render_files(const Chart& chart, const Value& values,
+                                                              const RenderOptions& o) {
   tmpl::Engine eng;
   add_templates(eng, chart, "");
   std::vector<std::pair<std::string, std::string>> out;
-  render_chart(eng, chart, values, o, "", &out);
+  render_chart(eng, chart, values, o, capabilities_value(o.capabilities), "", true, &out);
+  for (auto& kv : out) kv.first = chart.name() + "/" + kv.first;
+  return out;
+}
+
+// SplitManifests: documents of one rendered file, separated by "---" lines.
+static std::vector<std::string> split_documents(const std::string& text) {
+  std::vector<std::string> docs;
+  std::string cur;
+  for (auto& line : split(text, "\n")) {
+    if (starts_with(line, "---") && trim(line.substr(3)).empty()) {
+      docs.push_back(cur);
+      cur.clear();
+      continue;
+    }
+    cur += line + "\n";
+  }
+  docs.push_back(cur);
+  std::vector<std::string> out;
+  for (auto& d : docs) {
+    std::string t = trim(d);
+    bool only_comments = true;
+    for (auto& l : split(t, "\n"))
+      if (!trim(l).empty() && !starts_with(trim(l), "#")) only_comments = false;
+    if (!only_comments) out.push_back(trim_right(d, " \t\r\n"));
+  }
+  return out;
+}
+
+std::string render_to_string(const Chart& chart, const Value& values, const RenderOptions& o) {
   std::string all;
-  for (auto& kv : out) {
-    std::string body = trim(kv.second);
-    if (body.empty()) continue;
-    all += "---\n# Source: " + chart.name() + "/" + kv.first + "\n" + kv.second + "\n";
+  for (auto& kv : render_files(chart, values, o)) {
+    if (ends_with(kv.first, "/NOTES.txt")) continue;
+    for (auto& doc : split_documents(kv.second)) all += "---\n# Source: " + kv.first + "\n" + doc + "\n";
   }
   return all;
 }
@@ -154,39 +425,116 @@ std::vector<Value> render(const Chart& chart, const Value& values, const RenderO
   return objs;
 }
 
-// ============================================================== release storage
+// ============================================================== release storage (Helm 3)
 
 static std::string secret_name(const std::string& name, int v) {
   return "sh.helm.release.v1." + name + ".v" + std::to_string(v);
 }
 
-static Release decode_release(const Value& secret) {
+static Value file_list(const std::vector<std::pair<std::string, std::string>>& files) {
+  Value l = Value::seq();
+  for (auto& f : files) {
+    Value e = Value::map();
+    e["name"] = f.first;
+    e["data"] = base64_encode(f.second);  // []byte marshals as base64
+    l.push(e);
+  }
+  return l;
+}
+
+static Value chart_record(const Chart& c) {
+  Value ch = Value::map();
+  ch["metadata"] = c.metadata;
+  ch["lock"] = Value();
+  ch["templates"] = file_list(c.templates);
+  ch["values"] = c.values;
+  ch["schema"] = c.schema.empty() ? Value() : Value(base64_encode(c.schema));
+  ch["files"] = file_list(c.files);
+  return ch;
+}
+
+Value release_to_json(const Release& r) {
+  Value v = Value::map();
+  v["name"] = r.name;
+  Value info = Value::map();
+  info["first_deployed"] = r.first_deployed.empty() ? r.last_deployed : r.first_deployed;
+  info["last_deployed"] = r.last_deployed;
+  info["deleted"] = r.status == "uninstalled" ? Value(log::rfc3339_now()) : Value("0001-01-01T00:00:00Z");
+  if (!r.description.empty()) info["description"] = r.description;
+  info["status"] = r.status;
+  if (!r.notes.empty()) info["notes"] = r.notes;
+  v["info"] = info;
+  Value ch = r.chart_json;
+  if (!ch.is_map()) {
+    ch = Value::map();
+    ch["metadata"]["name"] = r.chart;
+    ch["metadata"]["version"] = r.chart_version;
+    ch["lock"] = Value();
+    ch["templates"] = Value::seq();
+    ch["values"] = Value::map();
+    ch["schema"] = Value();
+    ch["files"] = Value::seq();
+  }
+  v["chart"] = ch;
+  if (r.config.is_map() && r.config.size()) v["config"] = r.config;
+  if (!r.manifest.empty()) v["manifest"] = r.manifest;
+  if (!r.hooks.empty()) {
+    Value hs = Value::seq();
+    for (auto& h : r.hooks) {
+      Value e = Value::map();
+      e["name"] = h.name;
+      e["kind"] = h.kind;
+      e["path"] = h.path;
+      e["manifest"] = h.manifest;
+      e["events"] = Value::strings(h.events);
+      e["last_run"] = h.last_run.is_map() ? h.last_run : Value::map();
+      if (h.weight) e["weight"] = h.weight;
+      if (!h.delete_policies.empty()) e["delete_policies"] = Value::strings(h.delete_policies);
+      hs.push(e);
+    }
+    v["hooks"] = hs;
+  }
+  v["version"] = r.version;
+  v["namespace"] = r.namespace_;
+  return v;
+}
+
+Release release_from_json(const Value& v) {
   Release r;
-  std::string data = secret.at_path("data.release").as_string();
-  Value v = json_parse(gzip_decompress(base64_decode(base64_decode(data))));
   r.name = v.get("name").as_string();
   r.namespace_ = v.get("namespace").as_string();
   r.version = (int)v.get("version").as_int();
   r.status = v.at_path("info.status").as_string();
+  r.first_deployed = v.at_path("info.first_deployed").as_string();
   r.last_deployed = v.at_path("info.last_deployed").as_string();
+  r.description = v.at_path("info.description").as_string();
+  r.notes = v.at_path("info.notes").as_string();
   r.chart = v.at_path("chart.metadata.name").as_string();
   r.chart_version = v.at_path("chart.metadata.version").as_string();
-  r.config = v.get("config");
+  r.chart_json = v.get("chart");
+  r.config = v.get("config").is_map() ? v.get("config") : Value::map();
   r.manifest = v.get("manifest").as_string();
+  for (auto& h : v.get("hooks").items()) {
+    Hook k;
+    k.name = h.get("name").as_string();
+    k.kind = h.get("kind").as_string();
+    k.path = h.get("path").as_string();
+    k.manifest = h.get("manifest").as_string();
+    for (auto& e : h.get("events").items()) k.events.push_back(e.as_string());
+    for (auto& e : h.get("delete_policies").items()) k.delete_policies.push_back(e.as_string());
+    k.weight = (int)h.get("weight").as_int(0);
+    k.last_run = h.get("last_run");
+    r.hooks.push_back(std::move(k));
+  }
   return r;
 }
 
+static Release decode_release(const Value& secret) {
+  std::string data = secret.at_path("data.release").as_string();
+  return release_from_json(json_parse(gzip_decompress(base64_decode(base64_decode(data)))));
+}
+
 void Client::store(const Release& r) {
-  Value v = Value::map();
-  v["name"] = r.name;
-  v["namespace"] = r.namespace_;
-  v["version"] = r.version;
-  v["info"]["status"] = r.status;
-  v["info"]["last_deployed"] = r.last_deployed;
-  v["chart"]["metadata"]["name"] = r.chart;
-  v["chart"]["metadata"]["version"] = r.chart_version;
-  v["config"] = r.config;
-  v["manifest"] = r.manifest;
   Value s = Value::map();
   s["apiVersion"] = "v1";
   s["kind"] = "Secret";
@@ -197,8 +545,9 @@ void Client::store(const Release& r) {
   s["metadata"]["labels"]["name"] = r.name;
   s["metadata"]["labels"]["status"] = r.status;
   s["metadata"]["labels"]["version"] = std::to_string(r.version);
+  s["metadata"]["labels"]["modifiedAt"] = std::to_string((long long)time(nullptr));
   // Helm 3 stores base64(gzip(json)) inside Secret data (itself base64 on the wire)
-  s["data"]["release"] = base64_encode(base64_encode(gzip_compress(json_dump(v))));
+  s["data"]["release"] = base64_encode(base64_encode(gzip_compress(json_dump(release_to_json(r)))));
   k_->apply(s, r.namespace_);
 }
 
@@ -235,6 +584,33 @@ std::vector<Release> Client::list(const std::string& ns) {
   std::vector<Release> out;
   for (auto& kv : latest) out.push_back(kv.second);
   return out;
+}
+
+Value Client::capabilities() {
+  if (caps_.is_map()) return caps_;
+  Value c = Value::map();
+  try {
+    Value ver = k_->get("/version");
+    std::string minor = ver.get("minor").as_string();
+    while (!minor.empty() && !std::isdigit((unsigned char)minor.back())) minor.pop_back();  // "29+" (GKE/EKS)
+    c["KubeVersion"]["Major"] = ver.get("major").as_string();
+    c["KubeVersion"]["Minor"] = minor;
+    c["KubeVersion"]["GitVersion"] = ver.get("gitVersion").as_string();
+  } catch (const std::exception& e) {
+    log::debug(std::string("capabilities: /version: ") + e.what());
+  }
+  std::vector<std::string> apis;
+  try {
+    Value core = k_->get("/api"), groups = k_->get("/apis");  // keep the documents alive while iterating
+    for (auto& v : core.get("versions").items()) apis.push_back(v.as_string());
+    for (auto& g : groups.get("groups").items())
+      for (auto& gv : g.get("versions").items()) apis.push_back(gv.get("groupVersion").as_string());
+  } catch (const std::exception& e) {
+    log::debug(std::string("capabilities: discovery: ") + e.what());
+  }
+  c["APIVersions"] = Value::strings(apis);
+  caps_ = c;
+  return caps_;
 }
 
 static std::string object_key(const Value& o) {
@@ -289,10 +665,136 @@ std::string Client::wait_ready(const std::vector<Value>& objs, const std::string
   return "";
 }
 
+// ============================================================== hooks
+
+static const char* kHookAnno = "helm.sh/hook";
+
+static bool hook_has_event(const Hook& h, const std::string& ev) {
+  for (auto& e : h.events)
+    if (e == ev || (ev == "pre-install" && e == "crd-install")) return true;
+  return false;
+}
+
+static bool has_policy(const Hook& h, const std::string& p) {
+  if (h.delete_policies.empty()) return p == "before-hook-creation";  // Helm 3 default
+  return std::find(h.delete_policies.begin(), h.delete_policies.end(), p) != h.delete_policies.end();
+}
+
+// Completion of a hook object: "" = still running, "Succeeded" or "Failed: <why>".
+static std::string hook_phase(const std::string& kind, const std::optional<Value>& cur) {
+  if (!cur) return "";
+  if (kind == "Job") {
+    for (auto& c : cur->at_path("status.conditions").items()) {
+      if (c.get("status").as_string() != "True") continue;
+      if (c.get("type").as_string() == "Complete") return "Succeeded";
+      if (c.get("type").as_string() == "Failed") return "Failed: " + c.get("message").as_string(c.get("reason").as_string());
+    }
+    if (cur->at_path("status.succeeded").as_int(0) >= cur->at_path("spec.completions").as_int(1)) return "Succeeded";
+    return "";
+  }
+  if (kind == "Pod") {
+    std::string ph = cur->at_path("status.phase").as_string();
+    if (ph == "Succeeded") return "Succeeded";
+    if (ph == "Failed") return "Failed: pod " + cur->at_path("metadata.name").as_string() + " failed";
+    return "";
+  }
+  return "Succeeded";  // other kinds are done once created
+}
+
+void Client::run_hooks(std::vector<Hook>& hooks, const std::string& event, const std::string& ns, int timeout_s) {
+  std::vector<Hook*> sel;
+  for (auto& h : hooks)
+    if (hook_has_event(h, event)) sel.push_back(&h);
+  std::stable_sort(sel.begin(), sel.end(), [](const Hook* a, const Hook* b) {
+    if (a->weight != b->weight) return a->weight < b->weight;
+    int ka = kind_order(a->kind), kb = kind_order(b->kind);
+    if (ka != kb) return ka < kb;
+    return a->name < b->name;
+  });
+  for (Hook* h : sel) {
+    trace::Span span("deploy.helm_hook", {{"event", event}, {"hook", h->kind + "/" + h->name}});
+    Value obj = yaml_parse(h->manifest);
+    if (obj.at_path("metadata.namespace").is_null() && !kube::is_cluster_scoped(h->kind)) obj["metadata"]["namespace"] = ns;
+    std::string path = kube::resource_path(obj.get("apiVersion").as_string(), h->kind,
+                                           obj.at_path("metadata.namespace").as_string(ns), h->name);
+    int wait_ms = (timeout_s > 0 ? timeout_s : 300) * 1000;
+    if (has_policy(*h, "before-hook-creation") && k_->delete_object(obj, ns))
+      k_->wait_object(path, wait_ms, [](const std::optional<Value>& o) { return !o.has_value(); });
+    h->last_run = Value::map();
+    h->last_run["started_at"] = log::rfc3339_now();
+    h->last_run["phase"] = "Running";
+    log::info("Running " + event + " hook " + h->kind + "/" + h->name);
+    k_->apply(obj, ns);
+    std::string phase;
+    bool done = k_->wait_object(path, wait_ms, [&](const std::optional<Value>& cur) {
+      phase = hook_phase(h->kind, cur);
+      return !phase.empty();
+    });
+    if (!done) phase = "Failed: timed out waiting for the condition";
+    h->last_run["completed_at"] = log::rfc3339_now();
+    h->last_run["phase"] = phase == "Succeeded" ? "Succeeded" : "Failed";
+    if (phase != "Succeeded") {
+      if (has_policy(*h, "hook-failed")) k_->delete_object(obj, ns);
+      throw std::runtime_error(event + " hook " + h->kind + "/" + h->name + " failed: " + phase.substr(phase.find(':') + 2));
+    }
+    if (has_policy(*h, "hook-succeeded")) k_->delete_object(obj, ns);
+  }
+}
+
+// Rendered release: manifest text (hooks excluded), hook records, notes.
+struct Rendered {
+  std::string manifest, notes;
+  std::vector<Hook> hooks;
+  std::vector<Value> objs;
+};
+
+static Rendered render_release(const Chart& chart, const Value& values, const RenderOptions& ro) {
+  Rendered out;
+  for (auto& kv : render_files(chart, values, ro)) {
+    if (ends_with(kv.first, "/NOTES.txt")) {
+      if (kv.first == chart.name() + "/templates/NOTES.txt") out.notes = kv.second;
+      continue;
+    }
+    for (auto& doc : split_documents(kv.second)) {
+      Value d = yaml_parse(doc);
+      if (!d.is_map() || d.get("kind").is_null()) continue;
+      const Value& anno = d.at_path("metadata.annotations").get(kHookAnno);
+      if (!anno.is_null()) {
+        Hook h;
+        h.name = d.at_path("metadata.name").as_string();
+        h.kind = d.get("kind").as_string();
+        h.path = kv.first;
+        h.manifest = doc;
+        for (auto& e : split(anno.as_string(), ",")) {
+          std::string t = trim(e);
+          if (!t.empty()) h.events.push_back(t);
+        }
+        h.weight = (int)d.at_path("metadata.annotations").get("helm.sh/hook-weight").as_int(0);
+        for (auto& p : split(d.at_path("metadata.annotations").get("helm.sh/hook-delete-policy").as_string(), ",")) {
+          std::string t = trim(p);
+          if (!t.empty()) h.delete_policies.push_back(t);
+        }
+        out.hooks.push_back(std::move(h));
+        continue;
+      }
+      out.manifest += "---\n# Source: " + kv.first + "\n" + doc + "\n";
+      out.objs.push_back(d);
+    }
+  }
+  std::stable_sort(out.objs.begin(), out.objs.end(), [](const Value& a, const Value& b) {
+    return kind_order(a.get("kind").as_string()) < kind_order(b.get("kind").as_string());
+  });
+  return out;
+}
+
+// ============================================================== install / upgrade / rollback / delete
+
 Release Client::install_or_upgrade(const std::string& name, const std::string& ns_in, const std::string& chart_path,
                                    const Value& values, bool wait, int timeout_s) {
   std::string ns = ns_in.empty() ? k_->default_namespace() : ns_in;
   Chart chart = load_chart(chart_path);
+  if (chart.is_library()) throw std::runtime_error("library charts are not installable: " + chart.name());
+  process_dependencies(chart, values);
   auto hist = history(ns, name);
   const Release* last_deployed = nullptr;
   for (auto& h : hist)
@@ -303,15 +805,10 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
   ro.namespace_ = ns;
   ro.revision = rev;
   ro.is_install = last_deployed == nullptr;
-  Value merged = chart.values;
-  merge_values(merged, values);
-  std::string manifest = render_to_string(chart, merged, ro);
-  std::vector<Value> objs;
-  for (auto& d : yaml_parse_all(manifest))
-    if (d.is_map() && !d.get("kind").is_null()) objs.push_back(d);
-  std::stable_sort(objs.begin(), objs.end(), [](const Value& a, const Value& b) {
-    return kind_order(a.get("kind").as_string()) < kind_order(b.get("kind").as_string());
-  });
+  if (mentions_capabilities(chart)) ro.capabilities = capabilities();
+  Value merged = coalesce_values(chart, values);
+  Rendered rd = render_release(chart, merged, ro);
+  std::vector<Value>& objs = rd.objs;
   k_->check_gpu_requests(objs);
   for (auto& o : objs) {
     o["metadata"]["labels"]["app.kubernetes.io/managed-by"] = o.at_path("metadata.labels").get("app.kubernetes.io/managed-by").is_null()
@@ -328,11 +825,16 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
   r.version = rev;
   r.chart = chart.name();
   r.chart_version = chart.version();
-  r.config = values;
-  r.manifest = manifest;
+  r.chart_json = chart_record(chart);
+  r.config = values.is_map() ? values : Value::map();
+  r.manifest = rd.manifest;
+  r.notes = rd.notes;
+  r.hooks = rd.hooks;
   r.last_deployed = log::rfc3339_now();
+  r.first_deployed = hist.empty() ? r.last_deployed : hist.front().first_deployed;
   std::string err;
   try {
+    run_hooks(r.hooks, ro.is_install ? "pre-install" : "pre-upgrade", ns, timeout_s);
     for (auto& o : objs) k_->apply(o, ns);
     // objects that disappeared since the previous deployed revision
     if (last_deployed) {
@@ -361,11 +863,13 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
         log::warn(std::string("Error creating analyze report: ") + e.what());
       }
     }
+    if (err.empty()) run_hooks(r.hooks, ro.is_install ? "post-install" : "post-upgrade", ns, timeout_s);
   } catch (const std::exception& e) {
     err = e.what();
   }
   if (!err.empty()) {
     r.status = "failed";
+    r.description = "Release \"" + name + "\" failed: " + err;
     store(r);
     if (last_deployed) {
       log::warn("Upgrade failed (" + err + "), rolling back to revision " + std::to_string(last_deployed->version));
@@ -389,6 +893,7 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
       store(old);
     }
   r.status = "deployed";
+  r.description = ro.is_install ? "Install complete" : "Upgrade complete";
   store(r);
   return r;
 }
@@ -396,15 +901,36 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
 void Client::rollback(const std::string& ns, const std::string& name, int to_version) {
   auto hist = history(ns, name);
   const Release* target = nullptr;
-  for (auto& h : hist)
+  const Release* current = nullptr;
+  for (auto& h : hist) {
     if (h.version == to_version) target = &h;
+    if (h.status == "deployed") current = &h;
+  }
   if (!target) throw std::runtime_error("release " + name + " has no revision " + std::to_string(to_version));
-  for (auto& d : yaml_parse_all(target->manifest))
-    if (d.is_map() && !d.get("kind").is_null()) k_->apply(d, ns);
   Release r = *target;
   r.version = hist.back().version + 1;
   r.status = "deployed";
+  r.description = "Rollback to " + std::to_string(to_version);
   r.last_deployed = log::rfc3339_now();
+  r.first_deployed = hist.front().first_deployed.empty() ? hist.front().last_deployed : hist.front().first_deployed;
+  run_hooks(r.hooks, "pre-rollback", ns, 300);
+  std::set<std::string> keep;
+  for (auto& d : yaml_parse_all(target->manifest)) {
+    if (!d.is_map() || d.get("kind").is_null()) continue;
+    if (d.at_path("metadata.namespace").is_null() && !kube::is_cluster_scoped(d.get("kind").as_string()))
+      d["metadata"]["namespace"] = ns;
+    keep.insert(object_key(d));
+    k_->apply(d, ns);
+  }
+  if (current) {  // objects the rolled-back-from revision added
+    for (auto& d : yaml_parse_all(current->manifest)) {
+      if (!d.is_map() || d.get("kind").is_null()) continue;
+      if (d.at_path("metadata.namespace").is_null() && !kube::is_cluster_scoped(d.get("kind").as_string()))
+        d["metadata"]["namespace"] = ns;
+      if (!keep.count(object_key(d))) k_->delete_object(d, ns);
+    }
+  }
+  run_hooks(r.hooks, "post-rollback", ns, 300);
   for (auto& h : hist)
     if (h.status == "deployed") {
       Release old = h;
@@ -417,11 +943,21 @@ void Client::rollback(const std::string& ns, const std::string& name, int to_ver
 void Client::delete_release(const std::string& ns, const std::string& name, bool purge) {
   auto hist = history(ns, name);
   if (hist.empty()) throw std::runtime_error("release: \"" + name + "\" not found");
-  const Release& last = hist.back();
+  Release last = hist.back();
+  try {
+    run_hooks(last.hooks, "pre-delete", ns, 300);
+  } catch (const std::exception& e) {
+    log::warn(e.what());
+  }
   auto docs = yaml_parse_all(last.manifest);
   std::reverse(docs.begin(), docs.end());
   for (auto& d : docs)
     if (d.is_map() && !d.get("kind").is_null()) k_->delete_object(d, ns);
+  try {
+    run_hooks(last.hooks, "post-delete", ns, 300);
+  } catch (const std::exception& e) {
+    log::warn(e.what());
+  }
   if (purge) {
     for (auto& h : hist) {
       try {
@@ -430,9 +966,9 @@ void Client::delete_release(const std::string& ns, const std::string& name, bool
       }
     }
   } else {
-    Release r = last;
-    r.status = "uninstalled";
-    store(r);
+    last.status = "uninstalled";
+    last.description = "Uninstallation complete";
+    store(last);
   }
 }
 

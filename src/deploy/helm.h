@@ -1,7 +1,18 @@
 // Native Helm: chart loading + rendering (gotemplate), releases stored as Secrets
-// (`sh.helm.release.v1.<name>.v<rev>`, Helm-3 layout), install / upgrade (with rollback on
-// failure) / delete / status / history, and --wait readiness. Replaces the reference's Helm v2
-// + Tiller stack (helm/client.go, helm/install.go, helm/tiller.go) — Tiller is obsolete.
+// (`sh.helm.release.v1.<name>.v<rev>`, the Helm 3 storage layout, readable by `helm list /
+// history / rollback`), install / upgrade (with rollback on failure) / delete / status /
+// history, lifecycle hooks, and --wait readiness. Replaces the reference's Helm v2 + Tiller
+// stack (helm/client.go, helm/install.go:54-166, helm/tiller.go) — Tiller is obsolete.
+//
+// Chart semantics follow Helm 3's loader and engine:
+//  * `.Files` — every non-special chart file (not Chart.yaml / values.yaml / requirements.* /
+//    templates/ / charts/, minus .helmignore), with Get/GetBytes/Glob/Lines/AsConfig/AsSecrets;
+//  * dependencies from requirements.yaml (apiVersion v1) or Chart.yaml `dependencies` (v2):
+//    `alias`, `condition` (first resolvable bool wins), `tags`, `import-values` (exports and
+//    child/parent forms; the parent's own values take precedence), nested charts;
+//  * library charts (type: library) contribute their defines only;
+//  * `.Capabilities` from the API server's /version and /api(s) discovery;
+//  * NOTES.txt of the top chart rendered into the release's info.notes.
 #pragma once
 
 #include <memory>
@@ -14,36 +25,74 @@
 namespace ds {
 namespace helm {
 
+struct Dependency {
+  std::string name, version, repository, condition, alias;
+  std::vector<std::string> tags;
+  Value import_values;  // seq of strings / {child, parent} maps
+  bool enabled = true;
+};
+
 struct Chart {
   std::string dir;
   Value metadata;  // Chart.yaml
   Value values;    // values.yaml
+  std::string values_raw, schema;
   std::vector<std::pair<std::string, std::string>> templates;  // (relative name, text)
+  std::vector<std::pair<std::string, std::string>> files;      // .Files (relative name, bytes)
+  std::vector<Dependency> requirements;                        // requirements.yaml / Chart.yaml v2
   std::vector<Chart> dependencies;                             // charts/<sub>
   std::string name() const { return metadata.get("name").as_string(); }
   std::string version() const { return metadata.get("version").as_string(); }
+  bool is_library() const { return metadata.get("type").as_string() == "library"; }
 };
 
 Chart load_chart(const std::string& dir);
+
+// Helm's ProcessDependencies: drops disabled subcharts (condition/tags, against the chart
+// defaults coalesced with `user_values`), applies aliases and import-values. Mutates `c`.
+void process_dependencies(Chart& c, const Value& user_values);
+
+// CoalesceValues: chart defaults (recursively, each subchart under its name) under the user's
+// values, with `global` propagated into every subchart.
+Value coalesce_values(const Chart& c, const Value& user_values);
 
 struct RenderOptions {
   std::string release_name, namespace_;
   int revision = 1;
   bool is_install = true;
+  // {KubeVersion: {Major, Minor, GitVersion, Version}, APIVersions: [..]}; null = defaults
+  Value capabilities;
 };
 
 // Renders all templates into manifests (parsed YAML docs, empty docs dropped, sorted in
-// Helm's install order).
+// Helm's install order). `values` are the coalesced values (see coalesce_values).
 std::vector<Value> render(const Chart& chart, const Value& values, const RenderOptions& o);
 std::string render_to_string(const Chart& chart, const Value& values, const RenderOptions& o);
+// Rendered templates by path ("<chart>/templates/x.yaml" -> text), NOTES.txt included.
+std::vector<std::pair<std::string, std::string>> render_files(const Chart& chart, const Value& values,
+                                                              const RenderOptions& o);
+
+// A hook object (`helm.sh/hook` annotation) of a release.
+struct Hook {
+  std::string name, kind, path, manifest;
+  std::vector<std::string> events, delete_policies;
+  int weight = 0;
+  Value last_run;  // {started_at, completed_at, phase}
+};
 
 struct Release {
-  std::string name, namespace_, status;  // deployed | failed | superseded | uninstalled
+  std::string name, namespace_, status;  // deployed | failed | superseded | uninstalled | pending-*
   int version = 0;
-  std::string chart, chart_version, last_deployed;
-  Value config;
+  std::string chart, chart_version, first_deployed, last_deployed, description, notes;
+  Value config;      // user-supplied values
+  Value chart_json;  // Helm 3 chart record: metadata, templates, values, files, schema, lock
   std::string manifest;
+  std::vector<Hook> hooks;
 };
+
+// Helm 3 release JSON (pkg/release/release.go) <-> Release.
+Value release_to_json(const Release& r);
+Release release_from_json(const Value& v);
 
 class Client {
  public:
@@ -59,10 +108,15 @@ class Client {
   void delete_release(const std::string& ns, const std::string& name, bool purge = true);
   // Waits for every workload in the manifest to be ready; returns "" or a failure summary.
   std::string wait_ready(const std::vector<Value>& objs, const std::string& ns, int timeout_s);
+  // .Capabilities from the API server (cached per client).
+  Value capabilities();
 
  private:
   void store(const Release& r);
+  // Runs the hooks of one lifecycle event in weight order; throws on a failed hook.
+  void run_hooks(std::vector<Hook>& hooks, const std::string& event, const std::string& ns, int timeout_s);
   std::shared_ptr<kube::Client> k_;
+  Value caps_;
 };
 
 // Values.MergeInto (deploy/helm/merge.go:8): deep merge, `over` wins.
