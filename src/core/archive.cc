@@ -4,7 +4,9 @@
 #include <unistd.h>
 #include <zlib.h>
 
+#include <cmath>
 #include <cstring>
+#include <vector>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -132,6 +134,69 @@ std::string gzip_compress(const std::string& data, int level) {
   GzipWriter w(string_sink(&out), level);
   w.write(data);
   w.finish();
+  return out;
+}
+
+// Order-0 entropy of a sample in bits/byte: already-compressed or random payloads (model
+// weights, images, archives) sit near 8 and gain nothing from deflate except its cost.
+static double sample_entropy(const unsigned char* p, size_t n) {
+  if (n == 0) return 0;
+  uint32_t hist[256] = {0};
+  for (size_t i = 0; i < n; ++i) hist[p[i]]++;
+  double h = 0;
+  for (uint32_t c : hist) {
+    if (!c) continue;
+    double q = (double)c / (double)n;
+    h -= q * std::log2(q);
+  }
+  return h;
+}
+
+std::string gzip_compress_adaptive(const std::string& data, int level) {
+  // One gzip member (any `tar xz` / gunzip reads it), compressed in 1 MiB chunks whose level
+  // follows their sampled entropy: stored blocks (level 0) for incompressible chunks, `level`
+  // otherwise. deflate at level 1 runs ~20 MB/s on random bytes; stored blocks run at memcpy +
+  // CRC speed, so a tree of model checkpoints is no longer compression-bound.
+  std::string out;
+  out.reserve(data.size() / 2 + 1024);
+  z_stream z;
+  std::memset(&z, 0, sizeof(z));
+  if (deflateInit2(&z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK)
+    throw std::runtime_error("deflateInit2 failed");
+  std::vector<char> buf(1 << 17);
+  auto drain = [&](int flush) {
+    int r;
+    do {
+      z.next_out = (Bytef*)buf.data();
+      z.avail_out = (uInt)buf.size();
+      r = deflate(&z, flush);
+      out.append(buf.data(), buf.size() - z.avail_out);
+    } while (z.avail_out == 0 || (flush == Z_FINISH && r != Z_STREAM_END));
+  };
+  const size_t kChunk = 1 << 20, kSample = 1 << 16;
+  int cur = level;
+  for (size_t off = 0; off < data.size(); off += kChunk) {
+    size_t n = std::min(kChunk, data.size() - off);
+    const unsigned char* p = (const unsigned char*)data.data() + off;
+    int want = sample_entropy(p, std::min(n, kSample)) > 7.5 ? 0 : level;
+    if (want != cur) {
+      int r;
+      do {
+        z.next_out = (Bytef*)buf.data();
+        z.avail_out = (uInt)buf.size();
+        r = deflateParams(&z, want, Z_DEFAULT_STRATEGY);
+        out.append(buf.data(), buf.size() - z.avail_out);
+      } while (r == Z_BUF_ERROR);
+      cur = want;
+    }
+    z.next_in = (Bytef*)p;
+    z.avail_in = (uInt)n;
+    drain(Z_NO_FLUSH);
+  }
+  z.next_in = nullptr;
+  z.avail_in = 0;
+  drain(Z_FINISH);
+  deflateEnd(&z);
   return out;
 }
 

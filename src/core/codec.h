@@ -72,6 +72,9 @@ class GzipReader {
 };
 
 std::string gzip_compress(const std::string& data, int level = 6);
+// gzip whose deflate level adapts per 1 MiB chunk: stored blocks where the data is already
+// incompressible (sampled entropy), `level` elsewhere. Output is a standard gzip member.
+std::string gzip_compress_adaptive(const std::string& data, int level = 1);
 std::string gzip_decompress(const std::string& data);
 
 struct TarEntry {

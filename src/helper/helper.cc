@@ -22,9 +22,11 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <climits>
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <set>
 #include <string>
 #include <thread>
@@ -38,12 +40,57 @@
 using namespace ds;
 
 static std::string g_dest;
-static std::atomic<long> g_suppress_until_us{0};
 
 static long now_us() {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return ts.tv_sec * 1000000L + ts.tv_nsec / 1000;
+}
+
+// Paths this helper itself wrote or removed (upstream ops), so their inotify echo does not
+// trigger a downstream scan, while changes the pod makes to any other path — even during an
+// upload — still do. Entries live while an op runs and for kOwnEchoUs after it finished.
+static std::mutex g_own_mu;
+static std::set<std::string> g_own, g_own_trees;
+static long g_own_until = 0;  // monotonic us; LONG_MAX while an op runs
+static const long kOwnEchoUs = 2000000;
+
+static void own_begin() {
+  std::lock_guard<std::mutex> g(g_own_mu);
+  g_own_until = LONG_MAX;
+}
+
+static void own_end() {
+  std::lock_guard<std::mutex> g(g_own_mu);
+  g_own_until = now_us() + kOwnEchoUs;
+}
+
+static void own_path(const std::string& p) {
+  std::lock_guard<std::mutex> g(g_own_mu);
+  if (!starts_with(p, g_dest)) return;
+  for (std::string q = p;; q = fs::dirname(q)) {
+    if (!g_own.insert(q).second) break;  // ancestors already recorded
+    if (q.size() <= g_dest.size()) break;  // dest itself (its own IN_ATTRIB echo) included
+  }
+}
+
+static void own_subtree(const std::string& p) {
+  own_path(p);
+  std::lock_guard<std::mutex> g(g_own_mu);
+  g_own_trees.insert(p);
+}
+
+static bool is_own(const std::string& p) {
+  std::lock_guard<std::mutex> g(g_own_mu);
+  if (now_us() > g_own_until) {
+    g_own.clear();
+    g_own_trees.clear();
+    return false;
+  }
+  if (g_own.count(p)) return true;
+  for (std::string q = p; q.size() > g_dest.size(); q = fs::dirname(q))
+    if (g_own_trees.count(q)) return true;
+  return false;
 }
 
 static bool reply(const std::string& s) { return write_all(1, s); }
@@ -66,6 +113,7 @@ static std::string op_extract(const std::string& payload) {
   try {
     while (tr.next(&e)) {
       std::string out = safe_join(e.name);
+      own_path(out);
       if (e.type == '5') {
         fs::mkdirs(out, 0755);
         ::chmod(out.c_str(), e.mode & 07777);
@@ -153,14 +201,14 @@ static void op_remove(const std::string& payload) {
     if (rel.empty()) continue;
     std::string p = safe_join(rel);
     if (p == g_dest) continue;
+    own_subtree(p);
     fs::remove_all(p);
   }
 }
 
 static std::string op_download(const std::string& payload) {
-  std::string out;
-  GzipWriter gz(string_sink(&out), 1);
-  TarWriter tw([&](const char* d, size_t n) { return gz.write(d, n); });
+  std::string raw;
+  TarWriter tw(string_sink(&raw));
   for (auto& rel : split(payload, "\n")) {
     if (rel.empty()) continue;
     std::string p = safe_join(rel);
@@ -176,8 +224,9 @@ static std::string op_download(const std::string& payload) {
     tw.add_file_from_path(e, p);
   }
   tw.finish();
-  gz.finish();
-  return out;
+  // checkpoints and other binaries written in the pod are incompressible: stored blocks for
+  // those chunks instead of deflate at ~20 MB/s
+  return gzip_compress_adaptive(raw, 1);
 }
 
 static void add_watch_rec(int fd, const std::string& dir, std::map<int, std::string>& wds, int depth) {
@@ -203,39 +252,40 @@ static void watch_loop() {
       if (errno == EINTR) continue;
       break;
     }
-    bool changed = false;
-    for (char* p = buf; p < buf + n;) {
-      auto* ev = (struct inotify_event*)p;
-      p += sizeof(struct inotify_event) + ev->len;
-      std::string name = ev->len ? std::string(ev->name) : "";
-      if (ends_with(name, ".devspace-tmp")) continue;
-      if ((ev->mask & IN_ISDIR) && (ev->mask & (IN_CREATE | IN_MOVED_TO))) {
+    // true if the batch holds a change the pod made (not the echo of our own writes)
+    auto process = [&](ssize_t len) {
+      bool foreign = false;
+      for (char* p = buf; p < buf + len;) {
+        auto* ev = (struct inotify_event*)p;
+        p += sizeof(struct inotify_event) + ev->len;
+        if (ev->mask & IN_Q_OVERFLOW) {  // events were lost: rescan
+          foreign = true;
+          continue;
+        }
+        std::string name = ev->len ? std::string(ev->name) : "";
         auto it = wds.find(ev->wd);
-        if (it != wds.end()) add_watch_rec(fd, it->second + "/" + name, wds, 0);
+        if (ev->mask & IN_IGNORED) {
+          wds.erase(ev->wd);
+          continue;
+        }
+        if (it == wds.end()) continue;
+        std::string path = name.empty() ? it->second : it->second + "/" + name;
+        if ((ev->mask & IN_ISDIR) && (ev->mask & (IN_CREATE | IN_MOVED_TO))) add_watch_rec(fd, path, wds, 0);
+        if (ends_with(name, ".devspace-tmp") || is_own(path)) continue;
+        foreign = true;
       }
-      if (ev->mask & IN_IGNORED) {
-        wds.erase(ev->wd);
-        continue;
-      }
-      changed = true;
-    }
-    if (!changed) continue;
+      return foreign;
+    };
+    bool changed = process(n);
     // settle: wait until no events for 20 ms, then notify once
     while (true) {
       struct pollfd pf{fd, POLLIN, 0};
       if (::poll(&pf, 1, 20) <= 0) break;
       ssize_t m = ::read(fd, buf, sizeof(buf));
       if (m <= 0) break;
-      for (char* p = buf; p < buf + m;) {
-        auto* ev = (struct inotify_event*)p;
-        p += sizeof(struct inotify_event) + ev->len;
-        if ((ev->mask & IN_ISDIR) && (ev->mask & (IN_CREATE | IN_MOVED_TO))) {
-          auto it = wds.find(ev->wd);
-          if (it != wds.end()) add_watch_rec(fd, it->second + "/" + std::string(ev->name), wds, 0);
-        }
-      }
+      changed |= process(m);
     }
-    if (now_us() < g_suppress_until_us.load()) continue;  // our own writes
+    if (!changed) continue;
     write_all(2, "E\n");
   }
 }
@@ -258,16 +308,16 @@ int main(int argc, char** argv) {
     if (len && !read_exact(0, &payload[0], len)) break;
     switch (hdr[0]) {
       case 'U': {
-        g_suppress_until_us = now_us() + 60000000L;
+        own_begin();
         std::string r = op_extract(payload);
-        g_suppress_until_us = now_us() + 40000;  // ignore the echo of our own extraction
+        own_end();  // the echo of our own extraction is ignored for a short while
         reply(r + "\n");
         break;
       }
       case 'R':
-        g_suppress_until_us = now_us() + 60000000L;
+        own_begin();
         op_remove(payload);
-        g_suppress_until_us = now_us() + 40000;
+        own_end();
         reply("OK\n");
         break;
       case 'S': reply(op_scan()); break;

@@ -143,7 +143,110 @@ class PySync {
     d["last_upload_ms"] = st.last_upload_ms;
     d["bytes_up"] = st.bytes_up;
     d["bytes_down"] = st.bytes_down;
+    d["full_scans"] = st.full_scans;
+    d["probes"] = st.probes;
+    d["probe_hits"] = st.probe_hits;
+    d["scan_bytes"] = st.scan_bytes;
     return d;
+  }
+
+ private:
+  std::unique_ptr<sync::Session> s_;
+};
+
+// The sync decision rules on an unstarted session, for property tests:
+// the caller sets up the index and asks shouldUpload / shouldDownload / shouldRemove*.
+class PyRules {
+ public:
+  PyRules(const std::string& watch_path, const std::string& mode, std::vector<std::string> exclude,
+          std::vector<std::string> download_exclude, std::vector<std::string> upload_exclude) {
+    sync::Options o;
+    o.watch_path = watch_path;
+    o.dest_path = "/app";
+    o.mode = sync::parse_mode(mode);
+    o.exclude_paths = std::move(exclude);
+    o.download_exclude_paths = std::move(download_exclude);
+    o.upload_exclude_paths = std::move(upload_exclude);
+    o.silent = true;
+    s_ = std::make_unique<sync::Session>(o, std::make_shared<sync::LocalShellTransport>());
+    s_->setup();
+  }
+  void put(const std::string& name, int64_t size, int64_t mtime, bool is_dir, bool is_symlink, int64_t local_mtime_ns) {
+    sync::FileInfo f;
+    f.name = name;
+    f.size = size;
+    f.mtime = mtime;
+    f.is_dir = is_dir;
+    f.is_symlink = is_symlink;
+    f.local_mtime_ns = local_mtime_ns;
+    std::lock_guard<std::mutex> g(s_->index().mu);
+    s_->index().files[name] = f;
+  }
+  void create_dir(const std::string& d) {
+    std::lock_guard<std::mutex> g(s_->index().mu);
+    s_->index().create_dir(d);
+  }
+  void remove_dir(const std::string& d) {
+    std::lock_guard<std::mutex> g(s_->index().mu);
+    s_->index().remove_dir(d);
+  }
+  py::object get(const std::string& name) {
+    std::lock_guard<std::mutex> g(s_->index().mu);
+    sync::FileInfo* f = s_->index().find(name);
+    if (!f) return py::none();
+    py::dict d;
+    d["size"] = f->size;
+    d["mtime"] = f->mtime;
+    d["is_dir"] = f->is_dir;
+    d["is_symlink"] = f->is_symlink;
+    return d;
+  }
+  std::vector<std::string> names() {
+    std::lock_guard<std::mutex> g(s_->index().mu);
+    std::vector<std::string> out;
+    for (auto& kv : s_->index().files) out.push_back(kv.first);
+    return out;
+  }
+  bool should_upload(const std::string& rel, bool exists, bool is_dir, bool is_symlink, int64_t mtime_sec,
+                     int64_t mtime_nsec, int64_t size, bool initial) {
+    fs::StatInfo st;
+    st.exists = exists;
+    st.is_dir = is_dir;
+    st.is_reg = exists && !is_dir && !is_symlink;
+    st.is_symlink = is_symlink;
+    st.mtime_sec = mtime_sec;
+    st.mtime_nsec = mtime_nsec;
+    st.size = size;
+    std::lock_guard<std::mutex> g(s_->index().mu);
+    return s_->should_upload(rel, st, initial);
+  }
+  bool should_download(const std::string& name, int64_t size, int64_t mtime, bool is_dir, bool is_symlink) {
+    sync::FileInfo f;
+    f.name = name;
+    f.size = size;
+    f.mtime = mtime;
+    f.is_dir = is_dir;
+    f.is_symlink = is_symlink;
+    std::lock_guard<std::mutex> g(s_->index().mu);
+    return s_->should_download(f);
+  }
+  bool should_remove_remote(const std::string& rel) {
+    std::lock_guard<std::mutex> g(s_->index().mu);
+    return s_->should_remove_remote(rel);
+  }
+  bool should_remove_local(const std::string& abs, const std::string& name, int64_t size, int64_t mtime, bool is_dir) {
+    sync::FileInfo f;
+    f.name = name;
+    f.size = size;
+    f.mtime = mtime;
+    f.is_dir = is_dir;
+    std::lock_guard<std::mutex> g(s_->index().mu);
+    return s_->should_remove_local(abs, f);
+  }
+  void apply_archive(py::bytes data) {
+    std::string a(data);
+    py::gil_scoped_release nogil;
+    s_->apply_downstream_archive(a);
   }
 
  private:
@@ -198,4 +301,24 @@ PYBIND11_MODULE(_native, m) {
       .def("error", &PySync::error)
       .def("mode", &PySync::mode)
       .def("stats", &PySync::stats);
+  py::class_<PyRules>(m, "SyncRules")
+      .def(py::init<const std::string&, const std::string&, std::vector<std::string>, std::vector<std::string>,
+                    std::vector<std::string>>(),
+           py::arg("watch_path"), py::arg("mode") = "fast", py::arg("exclude") = std::vector<std::string>{},
+           py::arg("download_exclude") = std::vector<std::string>{},
+           py::arg("upload_exclude") = std::vector<std::string>{})
+      .def("put", &PyRules::put, py::arg("name"), py::arg("size") = 0, py::arg("mtime") = 0, py::arg("is_dir") = false,
+           py::arg("is_symlink") = false, py::arg("local_mtime_ns") = 0)
+      .def("create_dir", &PyRules::create_dir)
+      .def("remove_dir", &PyRules::remove_dir)
+      .def("get", &PyRules::get)
+      .def("names", &PyRules::names)
+      .def("should_upload", &PyRules::should_upload, py::arg("rel"), py::arg("exists"), py::arg("is_dir"),
+           py::arg("is_symlink"), py::arg("mtime_sec"), py::arg("mtime_nsec"), py::arg("size"), py::arg("initial"))
+      .def("should_download", &PyRules::should_download, py::arg("name"), py::arg("size"), py::arg("mtime"),
+           py::arg("is_dir") = false, py::arg("is_symlink") = false)
+      .def("should_remove_remote", &PyRules::should_remove_remote)
+      .def("should_remove_local", &PyRules::should_remove_local, py::arg("abs"), py::arg("name"), py::arg("size"),
+           py::arg("mtime"), py::arg("is_dir") = false)
+      .def("apply_archive", &PyRules::apply_archive);
 }

@@ -174,7 +174,9 @@ void Session::setup() {
       break;
     case Mode::Helper:
       window_ms_ = 10;
-      poll_ms_ = 2000;  // fallback poll; events normally drive downstream
+      // fallback listing only: the helper's inotify events (its own writes filtered out by
+      // path, queue overflows reported) drive downstream
+      poll_ms_ = 10000;
       break;
   }
   if (o_.upstream_window_ms >= 0) window_ms_ = o_.upstream_window_ms;
@@ -493,7 +495,18 @@ void Session::upstream_loop() {
       std::unique_lock<std::mutex> lk(q_mu_);
       q_cv_.wait_for(lk, std::chrono::milliseconds(200), [this] { return !queue_.empty() || stopping_ || failed_; });
       if (queue_.empty()) continue;
+      up_busy_ = true;  // a batch is being gathered / uploaded (see wait_upstream_idle)
     }
+    struct Idle {  // cleared on every way out of this iteration
+      Session* s;
+      ~Idle() {
+        {
+          std::lock_guard<std::mutex> g(s->q_mu_);
+          s->up_busy_ = false;
+        }
+        s->q_cv_.notify_all();
+      }
+    } idle{this};
     std::vector<FileInfo> changes;
     std::map<std::string, size_t> pos;
     long first_us = 0;
@@ -706,7 +719,7 @@ std::string Session::build_archive(const std::vector<FileInfo>& files, std::map<
   // The reference always gzips (sync/tar.go:146). Small edits are latency-bound, not
   // bandwidth-bound: fast modes ship them as plain tar (no gzip process on either side).
   if (mode_ != Mode::Compat && raw.size() <= 256 * 1024) return raw;
-  return gzip_compress(raw, mode_ == Mode::Compat ? 6 : 1);
+  return mode_ == Mode::Compat ? gzip_compress(raw, 6) : gzip_compress_adaptive(raw, 1);
 }
 
 static bool is_gzip(const std::string& a) { return a.size() >= 2 && (unsigned char)a[0] == 0x1f && (unsigned char)a[1] == 0x8b; }
@@ -946,6 +959,14 @@ void Session::initial_sync() {
     std::map<std::string, FileInfo> none;
     apply_downstream(dl, none);
   }
+  // "initial sync done" means the container has the files, not that they are queued
+  wait_upstream_idle();
+}
+
+void Session::wait_upstream_idle() {
+  std::unique_lock<std::mutex> lk(q_mu_);
+  while (!stopping_ && !failed_ && (up_busy_ || !queue_.empty()))
+    q_cv_.wait_for(lk, std::chrono::milliseconds(50));
 }
 
 // ============================================================ downstream
@@ -971,6 +992,16 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
   RateLimiter rl(o_.downstream_limit);
   long deadline = mono_us() + 300000000L;
   bool partial_ok = mode_ == Mode::Compat && !down_helper_;
+  uint64_t scan_bytes = 0;
+  struct Count {  // recorded on every exit path
+    Session* s;
+    uint64_t* bytes;
+    ~Count() {
+      std::lock_guard<std::mutex> g(s->stats_mu_);
+      s->stats_.full_scans++;
+      s->stats_.scan_bytes += *bytes;
+    }
+  } count{this, &scan_bytes};
   while (true) {
     std::string line;
     if (!down_out_.read_line(&line, 200)) {
@@ -1009,6 +1040,7 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
       }
     }
     if (o_.downstream_limit > 0) rl.take(line.size() + 1);
+    scan_bytes += line.size() + 1;
     if (line == kDone) break;
     if (line == kError) {
       sleep_ms(4000);
@@ -1040,6 +1072,43 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
   }
   if (!dest_found) throw SyncError("DestPath not found, find command did not execute correctly");
   return creates;
+}
+
+// Fast mode: instead of listing the whole tree every poll, ask the container whether anything
+// under the destination changed since the stamp touched two probes ago (`find -cnewer`, at
+// most one line back). Comparing against the stamp from two probes back (not the last one) keeps
+// files written in the same coarse timestamp tick as a stamp touch from being missed. No
+// stamp support (read-only /tmp, no touch) reports a change, i.e. falls back to full scans.
+bool Session::probe_changes() {
+  std::lock_guard<std::mutex> sg(down_shell_mu_);
+  if (probe_id_.empty()) probe_id_ = hex_encode(random_string(6));
+  std::string st = "/tmp/.devspace-sync-" + probe_id_;
+  // -cnewer (inode change time, which every write and chmod bumps and no tool can preserve)
+  // where find has it (GNU); busybox find falls back to -newer (mtime)
+  std::string qd = shell_quote(dest_);
+  std::string cmd = "if touch " + st + ".c 2>/dev/null; then if [ -e " + st + ".a ]; then { find -L " + qd +
+                    " -cnewer " + st + ".a 2>/dev/null || find -L " + qd + " -newer " + st +
+                    ".a 2>/dev/null; } | head -n 1; else echo FIRST; fi; [ -e " +
+                    st + ".b ] && mv -f " + st + ".b " + st + ".a; mv -f " + st + ".c " + st +
+                    ".b; else echo NOSTAMP; fi; echo " + kDone + "\n";
+  if (!write_all(down_shell_->in(), cmd)) throw SyncError("downstream: write failed");
+  long deadline = mono_us() + 60000000L;
+  bool hit = false;
+  while (true) {
+    std::string line;
+    if (!down_out_.read_line(&line, 200)) {
+      if (down_out_.eof()) throw SyncError("\n[Downstream] Stream closed unexpectedly");
+      if (stopping_) throw SyncError("sync stopped");
+      if (mono_us() > deadline) throw SyncError("downstream: probe timeout");
+      continue;
+    }
+    if (line == kDone) break;
+    if (!line.empty()) hit = true;
+  }
+  std::lock_guard<std::mutex> g(stats_mu_);
+  stats_.probes++;
+  if (hit) stats_.probe_hits++;
+  return hit;
 }
 
 std::string Session::download_files(const std::vector<FileInfo>& files) {
@@ -1303,11 +1372,22 @@ void Session::apply_downstream(const std::vector<FileInfo>& creates, std::map<st
 
 void Session::downstream_loop() {
   size_t last_amount = 0;
+  // fast mode without the helper: cheap change probes while idle, full listings only after a
+  // probe saw a change and until the stability rule has applied it
+  bool probing = mode_ == Mode::Fast && !down_helper_ && o_.downstream_probe;
+  bool scanned = false;
   while (!stopping_ && !failed_) {
-    auto removes = clone_index();
-    std::vector<FileInfo> creates;
+    bool skip = false;
     try {
-      creates = collect_changes(&removes);
+      if (probing && scanned && last_amount == 0) skip = !probe_changes();
+    } catch (const std::exception& e) {
+      fail(e.what());
+      return;
+    }
+    if (!skip) try {
+      auto removes = clone_index();
+      std::vector<FileInfo> creates = collect_changes(&removes);
+      scanned = true;
       size_t amount = creates.size() + removes.size();
       bool apply;
       if (down_helper_)

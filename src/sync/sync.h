@@ -86,6 +86,8 @@ struct Options {
   // Timing knobs (defaults depend on mode; <0 = mode default)
   int upstream_window_ms = -1;
   int downstream_poll_ms = -1;
+  // Fast mode: probe for changes (`find -newer`) between full listings (false = always list)
+  bool downstream_probe = true;
   // Reconnect: when set, a dead stream triggers a transport refresh (e.g. pick the newest
   // running pod again) instead of a fatal stop (the reference log.Fatalf's, sync_config.go:481).
   std::function<std::shared_ptr<Transport>()> reconnect;
@@ -101,6 +103,9 @@ struct Stats {
   uint64_t reconnects = 0;
   double last_upload_ms = 0;  // first event -> remote ack
   uint64_t bytes_up = 0, bytes_down = 0;
+  // downstream scanning (non-helper modes): full `find | stat` listings, cheap change probes
+  // (fast mode: `find -newer stamp`, one line at most) and the listing bytes read
+  uint64_t full_scans = 0, probes = 0, probe_hits = 0, scan_bytes = 0;
 };
 
 class Session {
@@ -118,6 +123,13 @@ class Session {
   const Options& options() const { return o_; }
   std::string pod_name();  // current pod (changes when a reconnect picks a new one)
   Mode effective_mode() const { return mode_; }
+
+  // Decision rules (sync/evaluater.go) — index lock held by the caller.
+  // Public so the property tests (tests/test_sync_rules_fuzz.py) can drive them directly.
+  bool should_remove_remote(const std::string& rel);
+  bool should_upload(const std::string& rel, const fs::StatInfo& st, bool initial);
+  bool should_download(const FileInfo& f);
+  bool should_remove_local(const std::string& abs, const FileInfo& f);
 
   // --- pieces exposed for tests (the reference tests drive setup/initialSync directly)
   void setup();
@@ -147,11 +159,6 @@ class Session {
   void logf(const std::string& msg);
   void log_error(const std::string& msg);
 
-  // rules (sync/evaluater.go) — index lock held
-  bool should_remove_remote(const std::string& rel);
-  bool should_upload(const std::string& rel, const fs::StatInfo& st, bool initial);
-  bool should_download(const FileInfo& f);
-  bool should_remove_local(const std::string& abs, const FileInfo& f);
 
   // upstream
   void push_event(UpEvent e);
@@ -173,6 +180,8 @@ class Session {
   // downstream
   void downstream_loop();
   std::vector<FileInfo> collect_changes(std::map<std::string, FileInfo>* removes);
+  bool probe_changes();  // fast mode: did anything under dest change since the last probes?
+  std::string probe_id_;
   void apply_downstream(const std::vector<FileInfo>& creates, std::map<std::string, FileInfo>& removes);
   std::string download_files(const std::vector<FileInfo>& files);
   void untar_all(const std::string& archive);
@@ -216,6 +225,8 @@ class Session {
   std::mutex q_mu_;
   std::condition_variable q_cv_;
   std::deque<UpEvent> queue_;
+  bool up_busy_ = false;  // guarded by q_mu_
+  void wait_upstream_idle();
 
   std::thread up_thread_, down_thread_, supervisor_;
   std::atomic<bool> running_{false}, stopping_{false};

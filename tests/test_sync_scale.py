@@ -1,0 +1,206 @@
+"""Sync at scale: a 10,000-file / ~200 MB tree through the native engine in all three
+protocols, and through `devspace dev` over the exec WebSocket (TLS) in the default protocol.
+
+Checks the initial sync is complete and byte-exact, that an idle fast-mode session costs change
+probes (one `find -cnewer` line) instead of full tree listings, that container-side edits and
+deletes still come back, and records timings to $SYNC_SCALE_OUT when set
+(scripts/bench_sync_scale.sh writes profiles/r2_sync_scale.json)."""
+
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import tempfile
+import time
+
+import pytest
+
+from conftest import ROOT
+
+_native = pytest.importorskip("devspace_amd._native")
+
+N_DIRS, N_PER_DIR, SMALL = 100, 100, 1024  # 10,000 files, ~10 MB
+BIG = [("big/model-0.bin", 48 << 20), ("big/model-1.bin", 48 << 20), ("big/data.bin", 48 << 20),
+       ("big/cache.bin", 46 << 20)]  # ~190 MB
+HELPER = os.path.join(ROOT, "bin", "devspace-helper")
+RESULTS = {}
+
+
+def _record(key, value):
+    RESULTS[key] = value
+    out = os.environ.get("SYNC_SCALE_OUT")
+    if out:
+        with open(out, "w") as f:
+            json.dump(RESULTS, f, indent=1, sort_keys=True)
+
+
+@pytest.fixture(scope="module")
+def tree(tmp_path_factory):
+    root = str(tmp_path_factory.mktemp("scale-src"))
+    payload = os.urandom(SMALL)
+    for d in range(N_DIRS):
+        dd = os.path.join(root, "src", f"pkg{d:03d}")
+        os.makedirs(dd)
+        for i in range(N_PER_DIR):
+            with open(os.path.join(dd, f"m{i:03d}.py"), "wb") as f:
+                f.write(payload[: (i * 7) % SMALL] + f"{d}/{i}".encode())
+    digests = {}
+    for rel, size in BIG:
+        p = os.path.join(root, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        h = hashlib.sha256()
+        with open(p, "wb") as f:
+            left = size
+            while left:
+                chunk = os.urandom(min(left, 4 << 20))
+                f.write(chunk)
+                h.update(chunk)
+                left -= len(chunk)
+        digests[rel] = h.hexdigest()
+    yield root, digests
+    shutil.rmtree(root, ignore_errors=True)
+
+
+def _count_files(root):
+    n = 0
+    for _, _, files in os.walk(root):
+        n += len(files)
+    return n
+
+
+def _sha(p):
+    h = hashlib.sha256()
+    with open(p, "rb") as f:
+        for chunk in iter(lambda: f.read(4 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def _verify(src, dst, digests):
+    assert _count_files(dst) == N_DIRS * N_PER_DIR + len(BIG)
+    for rel, d in digests.items():
+        assert _sha(os.path.join(dst, rel)) == d, rel
+    for d, i in ((0, 0), (57, 33), (99, 99)):
+        rel = os.path.join("src", f"pkg{d:03d}", f"m{i:03d}.py")
+        assert open(os.path.join(src, rel), "rb").read() == open(os.path.join(dst, rel), "rb").read()
+
+
+def _wait(pred, timeout, what):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        if pred():
+            return
+        time.sleep(0.02)
+    raise AssertionError(f"timed out: {what}")
+
+
+@pytest.mark.parametrize("mode", ["helper", "fast", "compat"])
+def test_initial_sync_10k_files_200mb(tree, mode, tmp_path):
+    src, digests = tree
+    dst = str(tmp_path / "pod" / "app")
+    os.makedirs(dst)
+    sess = _native.SyncSession(src, dst, mode=mode, helper_path=HELPER if mode == "helper" else "",
+                               log_dir=str(tmp_path / "logs"), pod_name=f"scale-{mode}")
+    t0 = time.perf_counter()
+    sess.start()
+    try:
+        assert sess.wait_initial_sync(300000), sess.error()
+        initial_s = time.perf_counter() - t0
+        _verify(src, dst, digests)
+        time.sleep(1.5)  # start-up listings (fast mode: first scan + two stamp-less probes)
+        st0 = sess.stats()
+        time.sleep(3.0)  # idle: what does watching a 10k-file tree cost?
+        st1 = sess.stats()
+        idle = {k: st1[k] - st0[k] for k in ("full_scans", "probes", "scan_bytes")}
+        if mode == "fast":
+            # one-line change probes while idle, no full tree listing
+            assert idle["probes"] >= 8, idle
+            assert idle["full_scans"] == 0 and idle["scan_bytes"] == 0, idle
+        elif mode == "helper":
+            assert idle["full_scans"] == 0, idle  # event-driven (inotify in the container)
+        else:
+            assert idle["full_scans"] >= 1, idle  # the reference protocol lists the tree every 1.3 s
+        # container-side create + delete still come back (probe hit -> full listing)
+        t1 = time.perf_counter()
+        with open(os.path.join(dst, "src", "pkg010", "from_pod.txt"), "w") as f:
+            f.write("pod edit")
+        os.remove(os.path.join(dst, "src", "pkg011", "m005.py"))
+        _wait(lambda: os.path.exists(os.path.join(src, "src", "pkg010", "from_pod.txt")) and
+              not os.path.exists(os.path.join(src, "src", "pkg011", "m005.py")), 60, "downstream create+delete")
+        down_s = time.perf_counter() - t1
+        # a checkpoint written in the pod (incompressible, 32 MiB) comes back intact
+        ckpt = os.urandom(32 << 20)
+        t2 = time.perf_counter()
+        with open(os.path.join(dst, "big", "ckpt.pt.tmp"), "wb") as f:
+            f.write(ckpt)
+        os.rename(os.path.join(dst, "big", "ckpt.pt.tmp"), os.path.join(dst, "big", "ckpt.pt"))
+        local_ckpt = os.path.join(src, "big", "ckpt.pt")
+        _wait(lambda: os.path.exists(local_ckpt) and os.path.getsize(local_ckpt) == len(ckpt), 120, "checkpoint down")
+        ckpt_s = time.perf_counter() - t2
+        assert open(local_ckpt, "rb").read() == ckpt
+        os.remove(local_ckpt)
+        _record(f"native_{mode}", {"initial_sync_s": round(initial_s, 3), "idle_3s": idle,
+                                   "downstream_create_delete_s": round(down_s, 3),
+                                   "downstream_32mib_checkpoint_s": round(ckpt_s, 3)})
+    finally:
+        sess.stop()
+        # restore the shared source tree for the next mode
+        os.remove(os.path.join(src, "src", "pkg010", "from_pod.txt")) if os.path.exists(
+            os.path.join(src, "src", "pkg010", "from_pod.txt")) else None
+        p = os.path.join(src, "src", "pkg011", "m005.py")
+        if not os.path.exists(p):
+            with open(os.path.join(src, "src", "pkg011", "m004.py"), "rb") as f:
+                data = f.read()
+            with open(p, "wb") as f:
+                f.write(os.urandom(SMALL)[: (5 * 7) % SMALL] + b"11/5")
+            del data
+
+
+def test_dev_sync_10k_files_over_wss(tree, tmp_path):
+    """`devspace dev` (helper protocol) of the 10k-file tree into a pod over the TLS exec WebSocket."""
+    from devspace_amd.localkube import LocalCluster
+    from test_e2e_cli import container_root, running, wait_for
+
+    from conftest import DevspaceEnv
+
+    src, digests = tree
+    base = str(tmp_path)
+    cluster = LocalCluster(os.path.join(base, "state"), gpus=0, tls=True).start()
+    dev = None
+    try:
+        lk = DevspaceEnv(cluster, base)
+        proj = lk.project("quickstart", "qs-scale")
+        os.symlink  # the tree is copied in, not linked: sync must see real files
+        shutil.copytree(os.path.join(src, "src"), os.path.join(proj, "src"))
+        shutil.copytree(os.path.join(src, "big"), os.path.join(proj, "big"))
+        t0 = time.perf_counter()
+        dev = subprocess.Popen([lk.bin, "dev", "--terminal=false", "--portforwarding=false"], cwd=proj, env=lk.env,
+                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, text=True,
+                               start_new_session=True)
+        pods = wait_for(lambda: running(lk.pods("quickstart")), timeout=120, what="dev pod")
+        root = os.path.join(container_root(lk, pods[0]), "app")
+        _wait(lambda: os.path.exists(os.path.join(root, "big", "cache.bin")) and
+              os.path.getsize(os.path.join(root, "big", "cache.bin")) == BIG[-1][1] and
+              _count_files(os.path.join(root, "src")) == N_DIRS * N_PER_DIR, 300, "initial sync over wss")
+        initial_s = time.perf_counter() - t0
+        for rel, d in digests.items():
+            assert _sha(os.path.join(root, rel)) == d, rel
+        # one edit after the big initial sync arrives promptly
+        t1 = time.perf_counter()
+        with open(os.path.join(proj, "src", "pkg042", "m042.py"), "a") as f:
+            f.write("# edit\n")
+        _wait(lambda: open(os.path.join(root, "src", "pkg042", "m042.py"), "rb").read().endswith(b"# edit\n"), 30,
+              "edit after initial sync")
+        _record("dev_helper_wss", {"initial_sync_incl_deploy_s": round(initial_s, 3),
+                                   "edit_after_initial_s": round(time.perf_counter() - t1, 4)})
+    finally:
+        if dev is not None and dev.poll() is None:
+            os.killpg(dev.pid, 2)
+            try:
+                dev.wait(20)
+            except subprocess.TimeoutExpired:
+                os.killpg(dev.pid, 9)
+                dev.wait()
+        cluster.stop()
+        tempfile.gettempdir()
