@@ -325,7 +325,7 @@ std::vector<Segment> split_segments(const std::string& src) {
 namespace {
 
 const char* const kObjTag = "\x01obj";
-const char* const kObjData = "\x01data";
+const char* const kObjData = "\x01" "data";
 
 bool is_obj(const Value& v, const char* kind) {
   if (!v.is_map()) return false;

@@ -253,7 +253,18 @@ bool Client::refresh_after_unauthorized() {
   return false;
 }
 
-bool Client::is_local_cluster() const { return contains(cfg_.context, "devspace-local") || contains(cfg_.server, "127.0.0.1"); }
+bool Client::is_local_cluster() {
+  // A loopback API server alone is not enough (kind, minikube's docker driver and k3d all
+  // listen on 127.0.0.1): the bundled cluster identifies itself in /version.
+  if (local_cluster_ < 0) {
+    local_cluster_ = 0;
+    try {
+      local_cluster_ = contains(get("/version").get("gitVersion").as_string(), "devspace-local") ? 1 : 0;
+    } catch (const std::exception&) {
+    }
+  }
+  return local_cluster_ == 1;
+}
 
 std::shared_ptr<Client> Client::from_devspace_config(const Value& cfg, bool switch_context) {
   const Value& cl = cfg.get("cluster");

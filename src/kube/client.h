@@ -68,7 +68,7 @@ class Client {
 
   const RestConfig& rest() const { return cfg_; }
   std::string default_namespace() const { return cfg_.namespace_.empty() ? "default" : cfg_.namespace_; }
-  bool is_local_cluster() const;  // devspace local cluster (process pods)
+  bool is_local_cluster();  // the bundled local cluster (process pods on the host network)
   bool is_minikube() const { return cfg_.context == "minikube"; }
 
   // REST (JSON bodies). Throw ApiError on non-2xx.
@@ -144,6 +144,7 @@ class Client {
   void apply_auth_locked();
   std::unique_ptr<net::WebSocket> ws_connect(const std::string& path, const std::vector<std::string>& protocols);
   RestConfig cfg_;
+  int local_cluster_ = -1;  // is_local_cluster() cache
   net::HttpClient http_;
   ApplyOptions apply_opts_;
   std::mutex auth_mu_;

@@ -223,10 +223,9 @@ bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out) {
     if (!write_all(sh->in(), bin)) return false;
     if (!out.wait_for(kDone, 30000)) return false;
   }
-  std::string exec = "exec " + name + " serve " + shell_quote(dest_) + " 2>&1 1>&3 3>&- || echo HELPERFAIL\n";
-  // keep stderr separate: exec with fds as-is
-  exec = "mkdir -p " + shell_quote(dest_) + " && exec " + name + " serve " + shell_quote(dest_) +
-         " || echo HELPERFAIL\n";
+  // stdout carries replies, stderr the change events: exec with the shell's fds as-is
+  std::string exec = "mkdir -p " + shell_quote(dest_) + " && exec " + name + " serve " + shell_quote(dest_) +
+                     " || echo HELPERFAIL\n";
   if (!write_all(sh->in(), exec)) return false;
   if (!out.read_line(&line, 15000)) return false;
   return line == "HELPER READY";
