@@ -245,10 +245,16 @@ void Session::open_up_shell() {
       up_out_.reset(up_shell_->out());
     }
   }
+  up_has_head_ = false;
   if (mode_ != Mode::Compat && !up_helper_) {
-    // create the destination once instead of per upload
-    write_all(up_shell_->in(), "mkdir -p " + shell_quote(dest_) + "; echo " + kDone + "\n");
-    wait_ack(up_out_, kDone, false, nullptr, 30000);
+    // create the destination once instead of per upload, and check for `head` (the streamed
+    // upload needs `head -c`; without it uploads use the reference's cat + stat protocol)
+    write_all(up_shell_->in(), "mkdir -p " + shell_quote(dest_) +
+                                   "; if command -v head >/dev/null 2>&1; then echo HAVEHEAD; fi; echo " + kDone + "\n");
+    std::string before;
+    wait_ack(up_out_, kDone, false, &before, 30000);
+    up_has_head_ = contains(before, "HAVEHEAD");
+    if (!up_has_head_) logf("[Sync] `head` not found in the container: uploads use the POSIX cat/stat protocol");
   }
 }
 
@@ -758,8 +764,9 @@ void Session::upload_archive(const std::string& archive) {
     return;
   }
   std::string qdest = shell_quote(dest_);
-  if (mode_ == Mode::Compat) {
-    // byte-for-byte reference protocol (sync/upstream.go:387-411)
+  if (mode_ == Mode::Compat || !up_has_head_) {
+    // the reference protocol (sync/upstream.go:387-411); compat archives are always gzip, the
+    // fast mode's cat/stat fallback may ship a small edit as plain tar
     std::string cmd = "fileSize=" + size + R"(;
 					tmpFile="/tmp/devspace-upstream";
 					mkdir -p /tmp;
@@ -782,7 +789,7 @@ void Session::upload_archive(const std::string& archive) {
 							sleep 0.1;
 					done;
 
-					tar xzpf "$tmpFile" -C ')" + dest_ + R"(/.' 2>/tmp/devspace-upstream-error;
+					tar )" + std::string(is_gzip(archive) ? "xzpf" : "xpf") + R"( "$tmpFile" -C ')" + dest_ + R"(/.' 2>/tmp/devspace-upstream-error;
 					echo "DONE";
 		)";
     if (!write_all(fd, cmd)) throw SyncError("upstream: write failed");
@@ -1074,22 +1081,25 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
 }
 
 // Fast mode: instead of listing the whole tree every poll, ask the container whether anything
-// under the destination changed since the stamp touched two probes ago (`find -cnewer`, at
-// most one line back). Comparing against the stamp from two probes back (not the last one) keeps
-// files written in the same coarse timestamp tick as a stamp touch from being missed. No
-// stamp support (read-only /tmp, no touch) reports a change, i.e. falls back to full scans.
+// under the destination changed since the stamp written two probes ago (`find -cnewer`, one
+// word back). Comparing against the stamp from two probes back (not the last one) keeps files
+// written in the same coarse timestamp tick as a stamp from being missed. Only tools of the
+// reference's POSIX set are used (sh builtins, find, rm): stamps are created with a shell
+// redirect and numbered instead of renamed, and the first match is taken with `read`. No
+// writable /tmp reports a change, i.e. falls back to full listings.
 bool Session::probe_changes() {
   std::lock_guard<std::mutex> sg(down_shell_mu_);
   if (probe_id_.empty()) probe_id_ = hex_encode(random_string(6));
-  std::string st = "/tmp/.devspace-sync-" + probe_id_;
-  // -cnewer (inode change time, which every write and chmod bumps and no tool can preserve)
-  // where find has it (GNU); busybox find falls back to -newer (mtime)
+  std::string st = "/tmp/.devspace-sync-" + probe_id_ + ".";
+  long k = probe_seq_++;
   std::string qd = shell_quote(dest_);
-  std::string cmd = "if touch " + st + ".c 2>/dev/null; then if [ -e " + st + ".a ]; then { find -L " + qd +
-                    " -cnewer " + st + ".a 2>/dev/null || find -L " + qd + " -newer " + st +
-                    ".a 2>/dev/null; } | head -n 1; else echo FIRST; fi; [ -e " +
-                    st + ".b ] && mv -f " + st + ".b " + st + ".a; mv -f " + st + ".c " + st +
-                    ".b; else echo NOSTAMP; fi; echo " + kDone + "\n";
+  std::string cur = st + std::to_string(k), old = st + std::to_string(k - 2);
+  // -cnewer (inode change time: every write and chmod bumps it, no tool can preserve it) where
+  // find has it (GNU); busybox find falls back to -newer (mtime)
+  std::string cmd = ": > " + cur + " 2>/dev/null || echo NOSTAMP; if [ -e " + old + " ]; then { find -L " + qd +
+                    " -cnewer " + old + " 2>/dev/null || find -L " + qd + " -newer " + old +
+                    " 2>/dev/null; } | { IFS= read -r l && echo CHANGED; }; else echo FIRST; fi; rm -f " + st +
+                    std::to_string(k - 3) + "; echo " + kDone + "\n";
   if (!write_all(down_shell_->in(), cmd)) throw SyncError("downstream: write failed");
   long deadline = mono_us() + 60000000L;
   bool hit = false;

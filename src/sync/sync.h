@@ -182,6 +182,8 @@ class Session {
   std::vector<FileInfo> collect_changes(std::map<std::string, FileInfo>* removes);
   bool probe_changes();  // fast mode: did anything under dest change since the last probes?
   std::string probe_id_;
+  bool up_has_head_ = true;  // fast mode: container has `head -c` for streamed uploads
+  long probe_seq_ = 0;
   void apply_downstream(const std::vector<FileInfo>& creates, std::map<std::string, FileInfo>& removes);
   std::string download_files(const std::vector<FileInfo>& files);
   void untar_all(const std::string& archive);

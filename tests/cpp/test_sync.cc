@@ -345,7 +345,7 @@ TEST(sync_reconnect_after_stream_drop) {
   Dirs d;
   Options o = base_options(d, Mode::Fast);
   FaultPlan plan;
-  plan.kill_after_stdin_bytes = 64;  // first upstream shell dies mid-command
+  plan.kill_after_stdin_bytes = 400;  // first upstream shell dies mid-upload (after its setup command)
   plan.only_shell = 1;
   auto faulty = std::make_shared<FaultInjectingTransport>(std::make_shared<LocalShellTransport>(), plan);
   o.reconnect = [] { return std::make_shared<LocalShellTransport>(); };
