@@ -579,6 +579,23 @@ std::string context_tar(const std::string& context_dir, const std::vector<std::s
   return out;
 }
 
+std::vector<int> dockerfile_ports(const std::string& content) {
+  std::string d = replace_all(replace_all(content, "\r\n", "\n"), "\r", "\n");
+  std::vector<int> ports;
+  for (auto& line : split(d, "\n")) {
+    // ^EXPOSE\s(.*)$ — case-sensitive, at line start, like the reference's regex
+    if (line.size() < 7 || line.compare(0, 6, "EXPOSE") != 0 || !std::isspace((unsigned char)line[6])) continue;
+    for (auto& tok : split(line.substr(7), " ")) {
+      if (tok.empty()) continue;
+      std::string num = tok.substr(0, tok.find('/'));
+      int64_t p;
+      if (!parse_int64(num, &p)) throw std::runtime_error("strconv.Atoi: parsing \"" + num + "\": invalid syntax");
+      if (std::find(ports.begin(), ports.end(), (int)p) == ports.end()) ports.push_back((int)p);
+    }
+  }
+  return ports;
+}
+
 std::string dockerfile_with_entrypoint(const std::string& content, const std::vector<std::string>& entrypoint) {
   if (entrypoint.empty()) throw std::runtime_error("Entrypoint is empty");
   auto q = [](const std::string& s) { return json_escape(s); };

@@ -133,6 +133,11 @@ std::string context_tar(const std::string& context_dir, const std::vector<std::s
 // builder/util.go:43: Dockerfile content + ENTRYPOINT/CMD override (dev.overrideImages).
 std::string dockerfile_with_entrypoint(const std::string& dockerfile_content, const std::vector<std::string>& entrypoint);
 
+// util/dockerfile.GetPorts (pkg/util/dockerfile/get.go:14): the ports a Dockerfile EXPOSEs, in
+// order, deduplicated ("8080/tcp" -> 8080; CRLF / CR newlines normalised). Throws on a
+// non-numeric port, as the reference does. `devspace init` offers the first one as the default.
+std::vector<int> dockerfile_ports(const std::string& dockerfile_content);
+
 // ---------------------------------------------------------------- hashes
 
 // util/hash/hash.go:20 — sha256 over "path;size;mtimeNs" of every walked entry (chart skip cache).

@@ -60,11 +60,21 @@ void add_default_selector(Value& cfg) {
 }
 
 void add_default_ports(Value& cfg, InitState& st) {
+  // an existing Dockerfile's first EXPOSEd port is the default (util/dockerfile.GetPorts)
+  std::string def = "3000";
+  try {
+    std::string df;
+    if (fs::read_file("Dockerfile", &df)) {
+      auto ports = build::dockerfile_ports(df);
+      if (!ports.empty()) def = std::to_string(ports[0]);
+    }
+  } catch (const std::exception&) {
+  }
   prompt::Params p;
-  p.question = "Which port is the app listening on? (Default: 3000)";
+  p.question = "Which port is the app listening on? (Default: " + def + ")";
   p.default_value = "";
   std::string port = prompt::ask(p);
-  if (port.empty()) port = "3000";
+  if (port.empty()) port = def;
   Value pms = Value::seq();
   int64_t n;
   if (parse_int64(port, &n)) {

@@ -4,10 +4,14 @@
 //
 // Reference: cmd/install.go:40 (add executable dir to PATH), cmd/upgrade.go:39 +
 // pkg/devspace/upgrade/upgrade.go:67 (self-update), cmd/login.go:48 (cloud.ReLogin).
+#include <fcntl.h>
 #include <limits.h>
 #include <signal.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
+
+#include <ctime>
 
 #include <chrono>
 #include <thread>
@@ -19,6 +23,7 @@
 #include "core/proc.h"
 #include "core/strutil.h"
 #include "deploy/helmrepo.h"
+#include "upgrade/upgrade.h"
 #include "services/services.h"
 #include "sync/sync.h"
 
@@ -69,48 +74,117 @@ int compare_release(const std::string& a, const std::string& b) {
   return pa == pb ? 0 : (pa ? -1 : 1);
 }
 
-// Self-update from a release source: a local binary (--from) or a URL serving
-// "<url>/latest" (version text) and "<url>/devspace-linux-amd64" (DEVSPACE_RELEASE_URL).
+// Self-update (upgrade.go:69 Upgrade): from a local binary (--from), a plain mirror
+// (DEVSPACE_RELEASE_URL serving "<url>/latest" and "<url>/devspace-linux-amd64"), or by default
+// the newest GitHub release of devspace-cloud/devspace with a linux/amd64 asset.
 int run_upgrade(cli::Command& c, const Args&) {
   log::start_file_logging();
   std::string from = c.get_str("from");
   std::string url = getenv("DEVSPACE_RELEASE_URL") ? getenv("DEVSPACE_RELEASE_URL") : "";
-  std::string tmp;
-  std::string newest;
+  std::string exe = self_exe();
   try {
-    if (!from.empty()) {
-      RunResult r = run({from, "version"}, "", {}, 20000);
-      if (r.code != 0) throw std::runtime_error(from + " is not a devspace binary");
-      newest = trim(r.out);
-      auto sp = newest.rfind(' ');
-      if (sp != std::string::npos) newest = newest.substr(sp + 1);
-      tmp = from;
-    } else if (!url.empty()) {
-      newest = trim(helmrepo::fetch(trim_right(url, "/") + "/latest"));
-    } else {
-      throw std::runtime_error(
-          "no release source configured (use --from <binary> or set DEVSPACE_RELEASE_URL); this build has no "
-          "network access to a release server");
+    if (!from.empty() || !url.empty()) {
+      std::string newest;
+      if (!from.empty()) {
+        RunResult r = run({from, "version"}, "", {}, 20000);
+        if (r.code != 0) throw std::runtime_error(from + " is not a devspace binary");
+        newest = trim(r.out);
+        auto sp = newest.rfind(' ');
+        if (sp != std::string::npos) newest = newest.substr(sp + 1);
+      } else {
+        newest = trim(helmrepo::fetch(trim_right(url, "/") + "/latest"));
+      }
+      if (compare_release(newest, kVersion) <= 0) {
+        log::info(std::string("Current binary is the latest version: ") + kVersion);
+        return 0;
+      }
+      log::info("Downloading newest version...");
+      std::string staged = exe + ".new";
+      if (!from.empty())
+        fs::copy(from, staged, true);
+      else
+        fs::write_file(staged, helmrepo::fetch(trim_right(url, "/") + "/devspace-linux-amd64"), 0755);
+      chmod(staged.c_str(), 0755);
+      if (!fs::rename(staged, exe)) throw std::runtime_error("cannot replace " + exe);
+      log::info("Successfully updated to version " + newest);
+      return 0;
     }
-    if (compare_release(newest, kVersion) <= 0) {
+    auto latest = upgrade::detect_latest();
+    if (!latest || upgrade::compare_versions(latest->version, kVersion) <= 0) {
       log::info(std::string("Current binary is the latest version: ") + kVersion);
       return 0;
     }
     log::info("Downloading newest version...");
-    std::string exe = self_exe();
-    std::string staged = exe + ".new";
-    if (!from.empty())
-      fs::copy(tmp, staged, true);
-    else
-      fs::write_file(staged, helmrepo::fetch(trim_right(url, "/") + "/devspace-linux-amd64"), 0755);
-    chmod(staged.c_str(), 0755);
-    if (!fs::rename(staged, exe)) throw std::runtime_error("cannot replace " + exe);
-    log::info("Successfully updated to version " + newest);
+    upgrade::install_release(*latest, exe);
+    log::info("Successfully updated to version " + latest->version);
+    if (!latest->notes.empty()) log::info("Release note:\n" + latest->notes);
   } catch (const std::exception& e) {
     log::fatal(std::string("Couldn't upgrade: ") + e.what());
   }
   return 0;
 }
+
+// ~/.devspace/upgrade-check.json: {"checked": unix seconds, "latest": "x.y.z" | ""}
+std::string update_cache_path() { return fs::join(fs::home_dir(), ".devspace", "upgrade-check.json"); }
+
+// Hidden: refresh the cache (started detached by notify_newer_version, at most once a day).
+int run_upgrade_check(cli::Command&, const Args&) {
+  Value v = Value::map();
+  v["checked"] = (int64_t)time(nullptr);
+  try {
+    v["latest"] = upgrade::check_for_newer_version(kVersion);
+  } catch (const std::exception& e) {
+    v["latest"] = "";
+    v["error"] = e.what();
+  }
+  try {
+    fs::write_file_atomic(update_cache_path(), json_dump(v));
+  } catch (...) {
+  }
+  return 0;
+}
+
+}  // namespace
+
+// root.go:38: tell the user about a newer release. The reference asks GitHub synchronously on
+// every command; here the answer comes from a daily cache refreshed by a detached child, so no
+// command waits on the network. Only for interactive terminals, never under
+// DEVSPACE_NONINTERACTIVE / DEVSPACE_SKIP_UPDATE_CHECK, never for -alpha/-beta builds.
+void notify_newer_version(const std::vector<std::string>& args) {
+  if (getenv("DEVSPACE_SKIP_UPDATE_CHECK") || getenv("DEVSPACE_NONINTERACTIVE")) return;
+  if (!isatty(0) || !isatty(1)) return;
+  if (contains(kVersion, "-alpha") || contains(kVersion, "-beta")) return;
+  if (!args.empty() && (args[0] == "upgrade" || args[0] == "upgrade-check")) return;
+  Value cache;
+  try {
+    cache = json_parse(fs::read_file(update_cache_path()));
+  } catch (...) {
+  }
+  std::string latest = cache.get("latest").as_string();
+  if (!latest.empty() && compare_release(latest, kVersion) > 0)
+    log::warn("There is a newer version of DevSpace v" + latest +
+              ". Run `devspace upgrade` to upgrade to the newest version.\n");
+  if ((int64_t)time(nullptr) - cache.get("checked").as_int(0) < 24 * 3600) return;
+  std::string exe = self_exe();
+  if (exe.empty()) return;
+  pid_t pid = fork();
+  if (pid == 0) {
+    // detached grandchild: never holds the terminal or the caller's pipes
+    if (fork() != 0) _exit(0);
+    setsid();
+    int null = open("/dev/null", O_RDWR);
+    if (null >= 0) {
+      dup2(null, 0);
+      dup2(null, 1);
+      dup2(null, 2);
+    }
+    execl(exe.c_str(), exe.c_str(), "upgrade-check", (char*)nullptr);
+    _exit(0);
+  }
+  if (pid > 0) waitpid(pid, nullptr, 0);
+}
+
+namespace {
 
 int run_login(cli::Command& c, const Args&) {
   std::string name = c.get_str("provider");
@@ -211,6 +285,13 @@ void register_misc(cli::Command& root) {
     c->max_args = 0;
     c->str("from", "", "", "Path of a newer devspace binary to install");
     c->run = run_upgrade;
+    root.add(std::move(c));
+  }
+  {
+    auto c = std::make_unique<cli::Command>("upgrade-check", "Refreshes the cached newest-release check");
+    c->hidden = true;
+    c->max_args = 0;
+    c->run = run_upgrade_check;
     root.add(std::move(c));
   }
   {

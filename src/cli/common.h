@@ -44,6 +44,8 @@ void register_core(cli::Command& root);     // deploy dev up enter logs analyze 
 void register_init(cli::Command& root);     // init
 void register_config(cli::Command& root);   // add list remove status update use create
 void register_misc(cli::Command& root);     // install upgrade login version sync
+// Prints the cached "newer version" notice and refreshes the cache in the background (root.go:38).
+void notify_newer_version(const std::vector<std::string>& args);
 
 std::unique_ptr<cli::Command> make_root();
 

@@ -30,6 +30,7 @@ int main(int argc, char** argv) {
   std::vector<std::string> args(argv + 1, argv + argc);
   if (args.size() == 1 && (args[0] == "--version" || args[0] == "-v")) args[0] = "version";
   auto root = ds::cmd::make_root();
+  ds::cmd::notify_newer_version(args);
   try {
     return root->execute(args);
   } catch (const ds::log::FatalError& e) {

@@ -1,0 +1,179 @@
+#include "upgrade/upgrade.h"
+
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdlib>
+#include <regex>
+#include <stdexcept>
+
+#include "core/codec.h"
+#include "core/fs.h"
+#include "core/net.h"
+#include "core/strutil.h"
+#include "core/value.h"
+
+namespace ds {
+namespace upgrade {
+
+const char* const kGithubSlug = "devspace-cloud/devspace";
+
+std::string erase_version_prefix(const std::string& version) {
+  static const std::regex re(R"(\d+\.\d+\.\d+)");
+  std::smatch m;
+  if (!std::regex_search(version, m, re)) throw std::runtime_error("Version not adopting semver: " + version);
+  return version.substr((size_t)m.position(0));
+}
+
+int compare_versions(const std::string& a_in, const std::string& b_in) {
+  auto parse = [](const std::string& v) {
+    std::string s = erase_version_prefix(v);
+    std::string core = s.substr(0, s.find_first_of("-+"));
+    std::string pre;
+    size_t dash = s.find('-');
+    if (dash != std::string::npos) pre = s.substr(dash + 1, s.find('+') == std::string::npos ? std::string::npos
+                                                                                           : s.find('+') - dash - 1);
+    std::vector<long long> n;
+    for (auto& p : split(core, ".")) n.push_back(std::atoll(p.c_str()));
+    while (n.size() < 3) n.push_back(0);
+    return std::make_pair(n, pre);
+  };
+  auto a = parse(a_in), b = parse(b_in);
+  if (a.first != b.first) return a.first < b.first ? -1 : 1;
+  if (a.second == b.second) return 0;
+  if (a.second.empty()) return 1;
+  if (b.second.empty()) return -1;
+  return a.second < b.second ? -1 : 1;
+}
+
+std::vector<std::string> asset_suffixes() {
+  std::vector<std::string> out;
+  for (const char* sep : {"_", "-"})
+    for (const char* ext : {"", ".gz", ".tar.gz", ".tgz"}) out.push_back(std::string("linux") + sep + "amd64" + ext);
+  return out;
+}
+
+namespace {
+
+std::string api_base() {
+  const char* e = getenv("DEVSPACE_GITHUB_API");
+  return trim_right(e && *e ? e : "https://api.github.com", "/");
+}
+
+// GET with redirects (release assets redirect to object storage), proxy from the environment,
+// GitHub's required User-Agent, and the token when one is set.
+std::string http_get(const std::string& url_in, const std::string& accept) {
+  std::string cur = url_in;
+  for (int hop = 0; hop < 8; ++hop) {
+    net::Url u = net::Url::parse(cur);
+    std::string origin = u.scheme + "://" + u.host + (u.port ? ":" + std::to_string(u.port) : "");
+    net::HttpClient c(origin);
+    c.set_proxy(net::ProxyConfig::from_env());
+    c.set_header("User-Agent", "devspace-selfupdate");
+    c.set_header("Accept", accept);
+    const char* tok = getenv("GITHUB_TOKEN");
+    if (tok && *tok && hop == 0) c.set_header("Authorization", std::string("token ") + tok);
+    net::Request rq;
+    rq.path = u.path.empty() ? "/" : u.path;
+    rq.timeout_ms = 120000;
+    net::Response r = c.request(rq);
+    if (r.status >= 300 && r.status < 400 && !r.header("location").empty()) {
+      std::string loc = r.header("location");
+      cur = loc[0] == '/' ? origin + loc : loc;
+      continue;
+    }
+    if (r.status != 200) throw std::runtime_error("GET " + cur + ": HTTP " + std::to_string(r.status));
+    return r.body;
+  }
+  throw std::runtime_error("too many redirects fetching " + url_in);
+}
+
+bool has_suffix_match(const std::string& name) {
+  for (auto& s : asset_suffixes())
+    if (ends_with(name, s)) return true;
+  return false;
+}
+
+}  // namespace
+
+std::optional<Release> detect_latest(const std::string& slug) {
+  Value rels = json_parse(http_get(api_base() + "/repos/" + slug + "/releases?per_page=100",
+                                   "application/vnd.github+json"));
+  std::optional<Release> best;
+  for (auto& rel : rels.items()) {
+    if (rel.get("draft").as_bool() || rel.get("prerelease").as_bool()) continue;
+    std::string tag = rel.get("tag_name").as_string();
+    std::string ver;
+    try {
+      ver = erase_version_prefix(tag);
+    } catch (const std::exception&) {
+      continue;  // not a semver tag
+    }
+    for (auto& a : rel.get("assets").items()) {
+      std::string name = a.get("name").as_string();
+      if (!has_suffix_match(name)) continue;
+      if (!best || compare_versions(ver, best->version) > 0) {
+        Release r;
+        r.version = ver;
+        r.tag = tag;
+        r.name = rel.get("name").as_string();
+        r.notes = rel.get("body").as_string();
+        r.asset_name = name;
+        r.asset_url = a.get("browser_download_url").as_string();
+        best = r;
+      }
+      break;
+    }
+  }
+  return best;
+}
+
+std::string check_for_newer_version(const std::string& current) {
+  auto latest = detect_latest();
+  if (!latest || compare_versions(latest->version, current) <= 0) return "";
+  return latest->version;
+}
+
+std::string extract_binary(const std::string& asset_name, const std::string& data) {
+  if (ends_with(asset_name, ".tar.gz") || ends_with(asset_name, ".tgz")) {
+    std::string copy = data;
+    GzipReader gz(string_source(&copy));
+    TarReader tr([&](char* b, size_t n) { return gz.read(b, n); });
+    TarEntry e;
+    while (tr.next(&e)) {
+      std::string base = fs::basename(e.name);
+      if ((e.type == '0' || e.type == '7') && (base == "devspace" || starts_with(base, "devspace-linux") ||
+                                               starts_with(base, "devspace_linux")))
+        return tr.read_all();
+      tr.skip();
+    }
+    throw std::runtime_error("no devspace binary inside " + asset_name);
+  }
+  if (ends_with(asset_name, ".gz")) return gzip_decompress(data);
+  return data;
+}
+
+void install_release(const Release& r, const std::string& exe) {
+  std::string bin = extract_binary(r.asset_name, http_get(r.asset_url, "application/octet-stream"));
+  if (bin.size() < 4 || bin.compare(0, 4, "\x7f" "ELF") != 0)
+    throw std::runtime_error("downloaded asset " + r.asset_name + " is not an executable");
+  // go-github-selfupdate's update.Apply: new file next to the target, old one kept until the
+  // swap succeeded, then removed
+  std::string staged = exe + ".new", old = exe + ".old";
+  fs::write_file(staged, bin, 0755);
+  ::chmod(staged.c_str(), 0755);
+  fs::remove(old);
+  if (!fs::rename(exe, old)) {
+    fs::remove(staged);
+    throw std::runtime_error("cannot move " + exe + " aside");
+  }
+  if (!fs::rename(staged, exe)) {
+    fs::rename(old, exe);  // roll back
+    fs::remove(staged);
+    throw std::runtime_error("cannot replace " + exe);
+  }
+  fs::remove(old);
+}
+
+}  // namespace upgrade
+}  // namespace ds

@@ -49,3 +49,14 @@ TEST(image_name_helpers) {
   EXPECT_EQ(build::split_image_tag("reg:5000/a/b").second, std::string(""));
   EXPECT_EQ(build::pull_secret_name("my.Reg:5000"), std::string("devspace-auth-my-reg-5000"));
 }
+
+// util/dockerfile/get.go:14 GetPorts
+TEST(dockerfile_ports_like_get_ports) {
+  EXPECT_TRUE(build::dockerfile_ports("FROM node\nRUN x\n").empty());
+  auto p = build::dockerfile_ports("FROM node\r\nEXPOSE 3000 8080/tcp\rEXPOSE 3000\nEXPOSE  9229/udp\n  EXPOSE 1\nexpose 2\n");
+  EXPECT_EQ(p.size(), (size_t)3);
+  EXPECT_EQ(p[0], 3000);
+  EXPECT_EQ(p[1], 8080);
+  EXPECT_EQ(p[2], 9229);
+  EXPECT_THROWS(build::dockerfile_ports("EXPOSE $PORT\n"));
+}

@@ -10,6 +10,7 @@ cmd/update/update.go:20, cmd/use/use.go:20-23. Config files: config/configs/sche
 config/configutil/get.go:193-221, config/configutil/load.go:23-72.
 """
 
+import json
 import os
 import re
 import shutil
@@ -214,7 +215,162 @@ def test_upgrade_from_local_release(tmp_path):
     assert "Successfully updated to version v99.0.0" in p.stdout + p.stderr
     assert "v99.0.0" in subprocess.run([str(exe)], capture_output=True, text=True).stdout
     assert ver
+    # no reachable release server: a clear error, not a hang
     no_src = subprocess.run([BIN, "upgrade"], capture_output=True, text=True,
-                            env={k: v for k, v in dict(os.environ, HOME=home).items() if k != "DEVSPACE_RELEASE_URL"},
+                            env={**{k: v for k, v in os.environ.items() if k != "DEVSPACE_RELEASE_URL"}, "HOME": home,
+                                 "DEVSPACE_GITHUB_API": "http://127.0.0.1:9"},
                             timeout=60, cwd=tmp_path)
-    assert no_src.returncode != 0 and "no release source" in no_src.stdout + no_src.stderr
+    assert no_src.returncode != 0 and "Couldn't upgrade" in no_src.stdout + no_src.stderr
+
+
+class _FakeGithub:
+    """GitHub releases API + asset downloads (redirected, as GitHub does to object storage)."""
+
+    def __init__(self, releases, files):
+        import http.server
+        import threading
+
+        outer = self
+        self.releases, self.files, self.hits = releases, files, []
+
+        class H(http.server.BaseHTTPRequestHandler):
+            def log_message(self, *a):
+                pass
+
+            def do_GET(self):
+                outer.hits.append((self.path, self.headers.get("User-Agent"), self.headers.get("Authorization")))
+                if self.path.startswith("/repos/devspace-cloud/devspace/releases"):
+                    body = json.dumps(outer.releases).encode()
+                    self.send_response(200)
+                    self.send_header("Content-Type", "application/json")
+                elif self.path.startswith("/dl/"):
+                    self.send_response(302)
+                    self.send_header("Location", "/blob/" + self.path[4:])
+                    self.send_header("Content-Length", "0")
+                    self.end_headers()
+                    return
+                elif self.path.startswith("/blob/") and self.path[6:] in outer.files:
+                    body = outer.files[self.path[6:]]
+                    self.send_response(200)
+                else:
+                    body = b"not found"
+                    self.send_response(404)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+        self.srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+        self.url = f"http://127.0.0.1:{self.srv.server_address[1]}"
+        threading.Thread(target=self.srv.serve_forever, daemon=True).start()
+
+    def close(self):
+        self.srv.shutdown()
+
+
+def _release(tag, assets, base, draft=False, prerelease=False):
+    return {"tag_name": tag, "name": tag, "body": f"notes for {tag}", "draft": draft, "prerelease": prerelease,
+            "assets": [{"name": a, "browser_download_url": f"{base}/dl/{a}"} for a in assets]}
+
+
+def test_upgrade_from_github_releases(tmp_path):
+    """Default `upgrade`: newest non-draft, non-prerelease release with a linux/amd64 asset
+    (go-github-selfupdate rules), tarball extracted, running binary swapped atomically."""
+    import io
+    import tarfile
+
+    home = str(tmp_path / "home")
+    os.makedirs(home)
+    exe = tmp_path / "devspace"
+    shutil.copy2(BIN, exe)
+    new_bin = open(BIN, "rb").read() + b"\n# release v2.5.0\n"  # still a runnable ELF
+    tgz = io.BytesIO()
+    with tarfile.open(fileobj=tgz, mode="w:gz") as tf:
+        ti = tarfile.TarInfo("devspace-v2.5.0/devspace")
+        ti.size, ti.mode = len(new_bin), 0o755
+        tf.addfile(ti, io.BytesIO(new_bin))
+    gh = _FakeGithub([], {"devspace_linux_amd64.tar.gz": tgz.getvalue(), "devspace-darwin-amd64": b"x"})
+    gh.releases = [
+        _release("v9.0.0-rc1", ["devspace-linux-amd64"], gh.url, prerelease=True),  # prerelease: skipped
+        _release("v8.0.0", ["devspace-linux-amd64"], gh.url, draft=True),  # draft: skipped
+        _release("v3.0.0", ["devspace-darwin-amd64"], gh.url),  # no asset for this platform
+        _release("v2.5.0", ["devspace_linux_amd64.tar.gz", "checksums.txt"], gh.url),
+        _release("v1.0.0", ["devspace-linux-amd64"], gh.url),
+        _release("nightly", ["devspace-linux-amd64"], gh.url),  # not semver
+    ]
+    env = {**os.environ, "HOME": home, "DEVSPACE_GITHUB_API": gh.url, "GITHUB_TOKEN": "t0k"}
+    env.pop("DEVSPACE_RELEASE_URL", None)
+    try:
+        p = subprocess.run([str(exe), "upgrade"], capture_output=True, text=True, env=env, timeout=60, cwd=tmp_path)
+        out = p.stdout + p.stderr
+        assert p.returncode == 0, out
+        assert "Successfully updated to version 2.5.0" in out and "notes for v2.5.0" in out, out
+        assert open(exe, "rb").read() == new_bin
+        assert os.access(exe, os.X_OK) and not os.path.exists(str(exe) + ".old")
+        assert subprocess.run([str(exe), "version"], capture_output=True, text=True).returncode == 0
+        api = [h for h in gh.hits if h[0].startswith("/repos/")]
+        assert api and api[0][1] and api[0][2] == "token t0k"  # User-Agent + token sent to the API
+        # already newest: nothing downloaded
+        gh.releases = [_release("v0.0.1", ["devspace-linux-amd64"], gh.url)]
+        n = len(gh.hits)
+        p = subprocess.run([str(exe), "upgrade"], capture_output=True, text=True, env=env, timeout=60, cwd=tmp_path)
+        assert p.returncode == 0 and "latest version" in p.stdout + p.stderr
+        assert not any(h[0].startswith("/dl/") for h in gh.hits[n:])
+        # a non-executable asset is refused and the binary is left in place
+        gh.releases = [_release("v7.0.0", ["devspace-linux-amd64"], gh.url)]
+        gh.files["devspace-linux-amd64"] = b"<html>oops</html>"
+        p = subprocess.run([str(exe), "upgrade"], capture_output=True, text=True, env=env, timeout=60, cwd=tmp_path)
+        assert p.returncode != 0 and "not an executable" in p.stdout + p.stderr
+        assert open(exe, "rb").read() == new_bin
+    finally:
+        gh.close()
+
+
+def test_newer_version_notice_from_daily_cache(tmp_path):
+    """root.go:38: interactive runs print a "newer version" notice. Here it comes from a daily
+    cache that a detached `devspace upgrade-check` refreshes, so no command waits on GitHub."""
+    import pty
+    import time
+
+    home = tmp_path / "home"
+    (home / ".devspace").mkdir(parents=True)
+    gh = _FakeGithub([], {})
+    gh.releases = [_release("v42.0.0", ["devspace-linux-amd64"], gh.url)]
+    env = {k: v for k, v in os.environ.items() if k not in ("DEVSPACE_NONINTERACTIVE", "DEVSPACE_SKIP_UPDATE_CHECK")}
+    env.update(HOME=str(home), DEVSPACE_GITHUB_API=gh.url)
+
+    def run_tty():
+        master, slave = pty.openpty()
+        p = subprocess.run([BIN, "version"], stdin=slave, stdout=slave, stderr=slave, env=env, timeout=30)
+        os.close(slave)
+        out = b""
+        while True:
+            try:
+                chunk = os.read(master, 65536)
+            except OSError:
+                break
+            if not chunk:
+                break
+            out += chunk
+        os.close(master)
+        return p.returncode, out.decode(errors="replace")
+
+    try:
+        cache = home / ".devspace" / "upgrade-check.json"
+        # no cache yet: nothing printed, a background check fills the cache
+        rc, out = run_tty()
+        assert rc == 0 and "newer version" not in out, out
+        deadline = time.time() + 20
+        while time.time() < deadline and not cache.exists():
+            time.sleep(0.1)
+        assert json.loads(cache.read_text())["latest"] == "42.0.0"
+        # next interactive run tells the user, without asking GitHub again (cache is fresh)
+        n = len(gh.hits)
+        rc, out = run_tty()
+        assert rc == 0 and "There is a newer version of DevSpace v42.0.0" in out, out
+        time.sleep(0.5)
+        assert len(gh.hits) == n
+        # non-interactive (CI) runs stay silent
+        p = subprocess.run([BIN, "version"], capture_output=True, text=True, env=env, timeout=30)
+        assert "newer version" not in p.stdout + p.stderr
+    finally:
+        gh.close()
