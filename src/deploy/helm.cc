@@ -120,7 +120,13 @@ Chart load_chart(const std::string& dir) {
           fs::write_file(out, tr.read_all());
           if (top.empty()) top = split(te.name, "/")[0];
         }
-        if (!top.empty()) c.dependencies.push_back(load_chart(fs::join(tmp, top)));
+        if (!top.empty()) {
+          // everything the renderer needs is read into memory: the extraction can go
+          Chart sub_chart = load_chart(fs::join(tmp, top));
+          sub_chart.dir = sub;
+          c.dependencies.push_back(std::move(sub_chart));
+        }
+        fs::remove_all(tmp);
       }
     }
   }

@@ -9,6 +9,7 @@
 //   'R' payload=rel\n...        -> rm -rf <dest><rel>                          reply "OK\n"
 //   'S' (empty)                 -> "<abs>///size,mtime,hexmode,perm,uid,gid\n"... then "DONE\n"
 //   'D' payload=rel\n...        -> "SIZE n\n" + n bytes tar.gz (relative member names)
+//   'H' payload=rel\n...        -> one crc32 hex (or "-") per path, then "DONE\n"
 //   'W' (empty)                 -> start watching; "E\n" on stderr after changes settle
 //   'Q'                          -> exit
 //
@@ -20,6 +21,7 @@
 #include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
+#include <zlib.h>
 
 #include <atomic>
 #include <climits>
@@ -229,6 +231,27 @@ static std::string op_download(const std::string& payload) {
   return gzip_compress_adaptive(raw, 1);
 }
 
+// 'H': CRC-32 of files (initial sync: tells identical copies from changed files when mtimes
+// differ only by the sub-second part a seconds-resolution tar dropped). "-" = unreadable.
+static std::string op_hash(const std::string& payload) {
+  std::string out;
+  std::vector<char> buf(1 << 20);
+  for (auto& rel : split(payload, "\n")) {
+    if (rel.empty()) continue;
+    int fd = ::open(safe_join(rel).c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+      out += "-\n";
+      continue;
+    }
+    uLong crc = crc32(0L, Z_NULL, 0);
+    ssize_t n;
+    while ((n = ::read(fd, buf.data(), buf.size())) > 0) crc = crc32(crc, (const Bytef*)buf.data(), (uInt)n);
+    ::close(fd);
+    out += n < 0 ? "-\n" : strfmt("%08lx\n", (unsigned long)crc);
+  }
+  return out + "DONE\n";
+}
+
 static void add_watch_rec(int fd, const std::string& dir, std::map<int, std::string>& wds, int depth) {
   int wd = inotify_add_watch(fd, dir.c_str(),
                              IN_CREATE | IN_DELETE | IN_CLOSE_WRITE | IN_MOVED_FROM | IN_MOVED_TO | IN_ATTRIB);
@@ -321,6 +344,7 @@ int main(int argc, char** argv) {
         reply("OK\n");
         break;
       case 'S': reply(op_scan()); break;
+      case 'H': reply(op_hash(payload)); break;
       case 'D': {
         std::string a = op_download(payload);
         reply("SIZE " + std::to_string(a.size()) + "\n");

@@ -958,6 +958,7 @@ void Session::initial_sync() {
   std::vector<FileInfo> local_changes;
   auto remote_only = clone_index();
   diff_server_client(o_.watch_path, &local_changes, &remote_only, false);
+  if (down_helper_ && mode_ != Mode::Compat && !local_changes.empty()) drop_identical_copies(local_changes);
   if (!local_changes.empty()) send_changes_to_upstream(std::move(local_changes));
   if (!remote_only.empty()) {
     std::vector<FileInfo> dl;
@@ -967,6 +968,74 @@ void Session::initial_sync() {
   }
   // "initial sync done" means the container has the files, not that they are queued
   wait_upstream_idle();
+}
+
+// Initial sync against a pod whose image already holds the project (`COPY . .`): the copies
+// carry whole-second mtimes (tar), so a local file whose mtime has a sub-second part >= 0.5
+// rounds past its remote copy and the reference re-uploads it (roundMtime vs %Y). Files whose
+// remote mtime is the local mtime truncated and whose size matches are compared by CRC-32 in
+// the container (helper 'H') instead; identical ones are recorded as synced, not re-sent.
+void Session::drop_identical_copies(std::vector<FileInfo>& changes) {
+  std::vector<size_t> cand;
+  {
+    std::lock_guard<std::mutex> g(index_.mu);
+    for (size_t i = 0; i < changes.size(); ++i) {
+      const FileInfo& c = changes[i];
+      if (c.is_dir) continue;
+      FileInfo* f = index_.find(c.name);
+      if (!f || f->is_dir || f->is_symlink || f->size != c.size || f->mtime != c.mtime - 1) continue;
+      cand.push_back(i);
+    }
+  }
+  if (cand.empty()) return;
+  std::vector<bool> same(changes.size(), false);
+  size_t dropped = 0;
+  for (size_t b = 0; b < cand.size(); b += 2000) {
+    size_t e = std::min(cand.size(), b + 2000);
+    std::string list;
+    for (size_t k = b; k < e; ++k) list += changes[cand[k]].name + "\n";
+    std::vector<std::string> remote;
+    {
+      std::lock_guard<std::mutex> sg(down_shell_mu_);
+      if (!write_all(down_shell_->in(), frame('H', list))) throw SyncError("downstream: write failed");
+      long deadline = mono_us() + 300000000L;
+      while (true) {
+        std::string line;
+        if (!down_out_.read_line(&line, 200)) {
+          if (down_out_.eof()) throw SyncError("\n[Downstream] Stream closed unexpectedly");
+          if (stopping_) throw SyncError("sync stopped");
+          if (mono_us() > deadline) throw SyncError("downstream: hash timeout");
+          continue;
+        }
+        if (line == kDone) break;
+        remote.push_back(line);
+      }
+    }
+    if (remote.size() != e - b) throw SyncError("downstream: hash reply size mismatch");
+    for (size_t k = b; k < e; ++k) {
+      const FileInfo& c = changes[cand[k]];
+      std::string abs = o_.watch_path + c.name;
+      fs::StatInfo st = fs::stat(abs);
+      if (!st.exists || st.size != c.size) continue;
+      if (remote[k - b] != "-" && remote[k - b] == crc32_file_hex(abs)) {
+        same[cand[k]] = true;
+        ++dropped;
+        std::lock_guard<std::mutex> g(index_.mu);
+        FileInfo* f = index_.find(c.name);
+        if (f) {
+          f->mtime = st.mtime_rounded();
+          f->local_mtime_ns = st.mtime_sec * 1000000000LL + st.mtime_nsec;
+        }
+      }
+    }
+  }
+  if (!dropped) return;
+  std::vector<FileInfo> keep;
+  keep.reserve(changes.size() - dropped);
+  for (size_t i = 0; i < changes.size(); ++i)
+    if (!same[i]) keep.push_back(std::move(changes[i]));
+  changes.swap(keep);
+  logf(strfmt("[Sync] %zu file(s) already identical in the container (CRC-32), not re-uploaded", dropped));
 }
 
 void Session::wait_upstream_idle() {

@@ -229,6 +229,7 @@ class Session {
   std::deque<UpEvent> queue_;
   bool up_busy_ = false;  // guarded by q_mu_
   void wait_upstream_idle();
+  void drop_identical_copies(std::vector<FileInfo>& changes);
 
   std::thread up_thread_, down_thread_, supervisor_;
   std::atomic<bool> running_{false}, stopping_{false};

@@ -178,12 +178,22 @@ def test_dev_sync_10k_files_over_wss(tree, tmp_path):
         dev = subprocess.Popen([lk.bin, "dev", "--terminal=false", "--portforwarding=false"], cwd=proj, env=lk.env,
                                stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, text=True,
                                start_new_session=True)
+        # the image already carries the tree (COPY . .); "Sync started" is printed once the
+        # initial sync has reconciled the pod with the local folder
+        deadline = time.monotonic() + 300
+        out = []
+        while time.monotonic() < deadline:
+            line = dev.stdout.readline()
+            if not line:
+                break
+            out.append(line)
+            if "Sync started" in line:
+                break
+        assert any("Sync started" in l for l in out), "".join(out)
+        initial_s = time.perf_counter() - t0
         pods = wait_for(lambda: running(lk.pods("quickstart")), timeout=120, what="dev pod")
         root = os.path.join(container_root(lk, pods[0]), "app")
-        _wait(lambda: os.path.exists(os.path.join(root, "big", "cache.bin")) and
-              os.path.getsize(os.path.join(root, "big", "cache.bin")) == BIG[-1][1] and
-              _count_files(os.path.join(root, "src")) == N_DIRS * N_PER_DIR, 300, "initial sync over wss")
-        initial_s = time.perf_counter() - t0
+        assert _count_files(os.path.join(root, "src")) == N_DIRS * N_PER_DIR
         for rel, d in digests.items():
             assert _sha(os.path.join(root, rel)) == d, rel
         # one edit after the big initial sync arrives promptly
@@ -204,3 +214,38 @@ def test_dev_sync_10k_files_over_wss(tree, tmp_path):
                 dev.wait()
         cluster.stop()
         tempfile.gettempdir()
+
+
+def test_initial_sync_skips_identical_image_copies(tmp_path):
+    """A pod whose image already holds the project (`COPY . .`, whole-second mtimes from tar):
+    files whose local mtime only differs by the dropped sub-second part are compared by CRC-32
+    in the container and not re-uploaded; a same-size, same-second file with other content is."""
+    src, dst = tmp_path / "src", tmp_path / "pod" / "app"
+    src.mkdir()
+    dst.mkdir(parents=True)
+    base = int(time.time()) - 100
+    names = [f"f{i:03d}.txt" for i in range(200)]
+    for i, n in enumerate(names):
+        data = f"content {i}\n".encode() * 10
+        (src / n).write_bytes(data)
+        (dst / n).write_bytes(data if n != "f007.txt" else data.upper())  # f007: same size, different bytes
+        os.utime(src / n, ns=(base * 10**9 + 700_000_000, base * 10**9 + 700_000_000))  # rounds up
+        os.utime(dst / n, (base, base))  # what a seconds-resolution tar leaves
+    sess = _native.SyncSession(str(src), str(dst), mode="helper", helper_path=HELPER, log_dir=str(tmp_path / "logs"),
+                               pod_name="image-copies")
+    sess.start()
+    try:
+        assert sess.wait_initial_sync(60000), sess.error()
+        st = sess.stats()
+        assert st["upstream_changes"] == 1, st  # only the file whose bytes differ
+        assert (dst / "f007.txt").read_bytes() == (src / "f007.txt").read_bytes()
+        log = (tmp_path / "logs" / "sync.log").read_text()
+        assert "199 file(s) already identical in the container" in log, log[-1500:]
+        # and they stay in sync: an edit afterwards is uploaded, nothing comes back down
+        (src / "f001.txt").write_text("edited\n")
+        _wait(lambda: (dst / "f001.txt").read_text() == "edited\n", 30, "edit after initial")
+        time.sleep(0.5)
+        assert (src / "f002.txt").read_bytes() == (dst / "f002.txt").read_bytes()
+        assert sess.stats()["downstream_changes"] == 0
+    finally:
+        sess.stop()
