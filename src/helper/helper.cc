@@ -67,6 +67,11 @@ static void own_end() {
   g_own_until = now_us() + kOwnEchoUs;
 }
 
+struct OwnOp {  // own_begin/own_end around one upstream op, exceptions included
+  OwnOp() { own_begin(); }
+  ~OwnOp() { own_end(); }
+};
+
 static void own_path(const std::string& p) {
   std::lock_guard<std::mutex> g(g_own_mu);
   if (!starts_with(p, g_dest)) return;
@@ -331,18 +336,27 @@ int main(int argc, char** argv) {
     if (len && !read_exact(0, &payload[0], len)) break;
     switch (hdr[0]) {
       case 'U': {
-        own_begin();
-        std::string r = op_extract(payload);
-        own_end();  // the echo of our own extraction is ignored for a short while
+        std::string r;
+        {
+          OwnOp op;  // the echo of our own extraction is ignored while it runs and shortly after
+          r = op_extract(payload);
+        }
         reply(r + "\n");
         break;
       }
-      case 'R':
-        own_begin();
-        op_remove(payload);
-        own_end();
+      case 'R': {
+        {
+          OwnOp op;
+          try {
+            op_remove(payload);
+          } catch (const std::exception&) {
+            // like the shell protocols' `rm -R ... || true`: a path that cannot be removed does
+            // not stop the sync
+          }
+        }
         reply("OK\n");
         break;
+      }
       case 'S': reply(op_scan()); break;
       case 'H': reply(op_hash(payload)); break;
       case 'D': {
