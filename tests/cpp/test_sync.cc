@@ -1,6 +1,7 @@
 // Sync engine behaviour matrix — port of sync/sync_config_test.go (TestInitialSync,
 // TestNormalSync incl. remove/rename matrix) and sync/util_test.go (TestCopyToContainerTestable),
-// run over the local-shell transport in every protocol mode.
+// run over the local-shell transport in every protocol mode, and over the Kubernetes exec
+// WebSocket transport (kube::ExecTransport) when tests/test_sync_matrix_kube.py points it at a pod.
 #include <unistd.h>
 
 #include <algorithm>
@@ -11,6 +12,7 @@
 #include "core/fs.h"
 #include "core/log.h"
 #include "core/strutil.h"
+#include "kube/client.h"
 #include "sync/sync.h"
 #include "testing.h"
 
@@ -29,10 +31,37 @@ struct Case {
 using Cases = std::vector<Case>;
 const char* kContents = "TestContents";
 
+// Over the kube exec transport (DS_SYNC_KUBE_POD set by tests/test_sync_matrix_kube.py, which
+// runs a pod on the bundled cluster): `remote` is the host directory behind the container path
+// `dest` (the local kubelet's container root), so the matrix checks both sides directly.
+struct KubeTarget {
+  std::string ns, pod, container, root;  // root: host dir of the container's "/"
+  bool enabled() const { return !pod.empty(); }
+};
+
+KubeTarget kube_target() {
+  KubeTarget t;
+  auto env = [](const char* k) { return std::string(getenv(k) ? getenv(k) : ""); };
+  t.ns = env("DS_SYNC_KUBE_NS");
+  t.pod = env("DS_SYNC_KUBE_POD");
+  t.container = env("DS_SYNC_KUBE_CONTAINER");
+  t.root = env("DS_SYNC_KUBE_ROOT");
+  return t;
+}
+
 struct Dirs {
   std::string remote, local, outside;
+  std::string dest;  // container path (== remote for the local-shell transport)
   Dirs() {
-    remote = fs::realpath(fs::make_temp_dir("remote-"));
+    KubeTarget k = kube_target();
+    if (k.enabled()) {
+      dest = "/matrix/" + fs::basename(fs::make_temp_dir("remote-"));
+      remote = k.root + dest;
+      fs::mkdirs(remote);
+    } else {
+      remote = fs::realpath(fs::make_temp_dir("remote-"));
+      dest = remote;
+    }
     local = fs::realpath(fs::make_temp_dir("local-"));
     outside = fs::realpath(fs::make_temp_dir("outside-"));
   }
@@ -214,12 +243,20 @@ void check_eventually(const Dirs& d, const Cases& files, const Cases& folders, i
 Options base_options(const Dirs& d, Mode m) {
   Options o;
   o.watch_path = d.local;
-  o.dest_path = d.remote;
+  o.dest_path = d.dest;
   o.verbose = true;
   o.mode = m;
   o.helper_path = fs::join(fs::dirname(fs::realpath("/proc/self/exe")), "devspace-helper");
   o.sync_log_name = "sync-test";
   return o;
+}
+
+std::shared_ptr<Transport> matrix_transport() {
+  KubeTarget k = kube_target();
+  if (!k.enabled()) return std::make_shared<LocalShellTransport>();
+  auto client = kube::Client::from_devspace_config(Value::map(), false);
+  Value pod = client->get("/api/v1/namespaces/" + k.ns + "/pods/" + k.pod);
+  return std::make_shared<kube::ExecTransport>(client, pod, k.container);
 }
 
 void run_initial(Mode m) {
@@ -231,7 +268,7 @@ void run_initial(Mode m) {
   Cases all = files;
   all.insert(all.end(), folders.begin(), folders.end());
   set_excludes(&o, all);
-  Session s(o, std::make_shared<LocalShellTransport>());
+  Session s(o, matrix_transport());
   s.setup();
   s.open_shells();
   create_all(d, files, folders);
@@ -254,7 +291,7 @@ void run_normal(Mode m) {
   Cases all = files;
   all.insert(all.end(), folders.begin(), folders.end());
   set_excludes(&o, all);
-  Session s(o, std::make_shared<LocalShellTransport>());
+  Session s(o, matrix_transport());
   s.start();
   EXPECT_TRUE(s.wait_initial_sync(15000));
   create_all(d, files, folders);
