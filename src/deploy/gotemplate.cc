@@ -157,7 +157,7 @@ struct Pipeline {
 };
 
 struct Node {
-  enum Kind { Text, Action, If, Range, With, Template, List } kind;
+  enum Kind { Text, Action, If, Range, With, Template, List, Break, Continue } kind;
   std::string text;
   std::shared_ptr<Pipeline> pipe;
   std::vector<std::shared_ptr<Node>> body, else_body;
@@ -670,6 +670,9 @@ Value make_api_versions_object(const std::vector<std::string>& versions) {
 
 // ============================================================== engine
 
+struct LoopBreak {};
+struct LoopContinue {};
+
 struct Engine::Impl {
   std::map<std::string, std::vector<NodeP>> templates;
   Engine* owner = nullptr;
@@ -705,6 +708,12 @@ struct Engine::Impl {
       if (kw == "end" || kw == "else") {
         *stop = a;
         return out;
+      }
+      if (a == "break" || a == "continue") {  // Go 1.18: only valid inside {{range}}
+        auto n = std::make_shared<Node>();
+        n->kind = a == "break" ? Node::Break : Node::Continue;
+        out.push_back(n);
+        continue;
       }
       if (kw == "if" || kw == "with" || kw == "range") {
         out.push_back(parse_control(tname, kw, a.substr(kw.size()), segs, pos));
@@ -906,6 +915,24 @@ struct Engine::Impl {
     bool have_last = false;
     for (auto& c : p.cmds) {
       const Arg& first = c.args[0];
+      if (first.kind == Arg::Ident && (first.name == "and" || first.name == "or") && c.args.size() > 1) {
+        // Go 1.18+: and/or evaluate their arguments lazily and stop at the first deciding one,
+        // so `and (hasKey . "x") (gt .x 1)` never compares a missing value
+        bool is_and = first.name == "and";
+        Value v;
+        bool decided = false;
+        for (size_t i = 1; i < c.args.size(); ++i) {
+          v = eval_arg(sc, c.args[i]);
+          if (truth(v) != is_and) {
+            decided = true;
+            break;
+          }
+        }
+        if (!decided && have_last) v = last;  // a piped value is the final argument
+        last = v;
+        have_last = true;
+        continue;
+      }
       if (first.kind == Arg::Ident) {
         std::vector<Value> args;
         for (size_t i = 1; i < c.args.size(); ++i) args.push_back(eval_arg(sc, c.args[i]));
@@ -1042,7 +1069,13 @@ struct Engine::Impl {
     Scope sc;
     sc.dot = dot;
     sc.vars.emplace_back("$", dot);
-    return render_nodes(sc, it->second);
+    try {
+      return render_nodes(sc, it->second);
+    } catch (const LoopBreak&) {
+      throw TemplateError("{{break}} outside {{range}}");
+    } catch (const LoopContinue&) {
+      throw TemplateError("{{continue}} outside {{range}}");
+    }
   }
 
   Value call(Scope& sc, const std::string& fn, std::vector<Value> args, const Value* piped) {
@@ -1763,25 +1796,32 @@ struct Engine::Impl {
       case Node::If: {
         size_t mark = sc.vars.size();
         Value v = eval_pipeline(sc, *n.pipe, true);
-        if (truth(v))
-          out += render_nodes(sc, n.body);
-        else
-          out += render_nodes(sc, n.else_body);
-        sc.vars.resize(mark);
+        struct Restore {  // loop control may unwind through this scope
+          Scope& sc;
+          size_t mark;
+          ~Restore() { sc.vars.resize(mark); }
+        } restore{sc, mark};
+        for (auto& child : (truth(v) ? n.body : n.else_body)) exec_node(sc, *child, out);
         return;
       }
       case Node::With: {
         size_t mark = sc.vars.size();
         Value v = eval_pipeline(sc, *n.pipe, true);
+        struct Restore {  // loop control may unwind through this scope
+          Scope& sc;
+          size_t mark;
+          Value dot;
+          ~Restore() {
+            sc.vars.resize(mark);
+            sc.dot = dot;
+          }
+        } restore{sc, mark, sc.dot};
         if (truth(v)) {
-          Value saved = sc.dot;
           sc.dot = v;
-          out += render_nodes(sc, n.body);
-          sc.dot = saved;
+          for (auto& child : n.body) exec_node(sc, *child, out);
         } else {
-          out += render_nodes(sc, n.else_body);
+          for (auto& child : n.else_body) exec_node(sc, *child, out);
         }
-        sc.vars.resize(mark);
         return;
       }
       case Node::Range: {
@@ -1813,9 +1853,16 @@ struct Engine::Impl {
             sc.vars.emplace_back(decl[1], kv.second);
           }
           sc.dot = kv.second;
-          out += render_nodes(sc, n.body);
+          bool brk = false;
+          try {
+            for (auto& child : n.body) exec_node(sc, *child, out);
+          } catch (const LoopContinue&) {
+          } catch (const LoopBreak&) {
+            brk = true;
+          }
           // assignments with "=" to outer vars must survive: only drop the loop's own vars
           sc.vars.resize(mark);
+          if (brk) break;
         }
         sc.dot = saved;
         return;
@@ -1826,6 +1873,8 @@ struct Engine::Impl {
         return;
       }
       case Node::List: out += render_nodes(sc, n.body); return;
+      case Node::Break: throw LoopBreak{};
+      case Node::Continue: throw LoopContinue{};
     }
   }
 };

@@ -260,3 +260,22 @@ TEST(semver_constraints) {
   EXPECT_TRUE(tmpl::semver_match("0.10.2", "0.10.2"));
   EXPECT_THROWS(tmpl::semver_match(">=1", "not-a-version"));
 }
+
+TEST(gotemplate_go118_control_flow) {
+  auto R = [](const std::string& src, const std::string& data = "{}") {
+    tmpl::Engine e;
+    e.add("t", src);
+    return e.execute("t", yaml_parse(data));
+  };
+  // {{break}} / {{continue}} inside range (also from inside if/with bodies)
+  EXPECT_EQ(R("{{ range $i, $v := .l }}{{ if eq $v 3 }}{{ break }}{{ end }}{{ $v }},{{ end }}", "l: [1, 2, 3, 4]"),
+            std::string("1,2,"));
+  EXPECT_EQ(R("{{ range .l }}{{ with . }}{{ if eq . 2 }}{{ continue }}{{ end }}{{ . }}{{ end }};{{ end }}",
+              "l: [1, 2, 3]"),
+            std::string("1;3;"));
+  EXPECT_THROWS(R("{{ break }}"));
+  // and/or stop at the first deciding argument: the comparison with a missing value never runs
+  EXPECT_EQ(R("{{ if and (hasKey . \"x\") (gt .x 1) }}big{{ else }}none{{ end }}"), std::string("none"));
+  EXPECT_EQ(R("{{ if or (not (hasKey . \"x\")) (gt .x 1) }}ok{{ end }}"), std::string("ok"));
+  EXPECT_EQ(R("{{ and 1 0 2 }}|{{ or 0 \"\" 3 }}|{{ 5 | and 1 }}|{{ 0 | or \"\" }}"), std::string("0|3|5|0"));
+}
