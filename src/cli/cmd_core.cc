@@ -181,19 +181,31 @@ int run_dev(cli::Command& c, const std::vector<std::string>& args) {
     }
     if (c.get_bool("exit-after-deploy")) return 0;
 
-    // dev.go:249 startServices
+    // dev.go:249 startServices — port-forwarding and sync each look up their pods and open
+    // their streams; on a real cluster that is a few API round trips apiece, so both start
+    // concurrently instead of one after the other as in the reference.
     std::vector<std::unique_ptr<services::PortForwarder>> forwards;
     std::vector<std::unique_ptr<sync::Session>> syncs;
-    try {
-      if (c.get_bool("portforwarding")) forwards = services::start_port_forwarding(s.cfg(), s.kube);
-    } catch (const std::exception& e) {
-      log::fatal(std::string("Unable to start portforwarding: ") + e.what());
+    std::string pf_err, sync_err;
+    {
+      bool want_pf = c.get_bool("portforwarding"), want_sync = c.get_bool("sync");
+      auto opts = dev_sync_options(c.get_bool("verbose-sync"));
+      std::thread pf_thread([&] {
+        try {
+          if (want_pf) forwards = services::start_port_forwarding(s.cfg(), s.kube);
+        } catch (const std::exception& e) {
+          pf_err = e.what();
+        }
+      });
+      try {
+        if (want_sync) syncs = services::start_sync(s.cfg(), s.kube, opts);
+      } catch (const std::exception& e) {
+        sync_err = e.what();
+      }
+      pf_thread.join();
     }
-    try {
-      if (c.get_bool("sync")) syncs = services::start_sync(s.cfg(), s.kube, dev_sync_options(c.get_bool("verbose-sync")));
-    } catch (const std::exception& e) {
-      log::fatal(std::string("Unable to start sync: ") + e.what());
-    }
+    if (!pf_err.empty()) log::fatal("Unable to start portforwarding: " + pf_err);
+    if (!sync_err.empty()) log::fatal("Unable to start sync: " + sync_err);
     print_space_domain(s);
 
     std::atomic<bool> reload{false};
