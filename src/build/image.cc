@@ -3,6 +3,7 @@
 #include <poll.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <chrono>
 #include <mutex>
 #include <regex>
@@ -437,6 +438,12 @@ std::unique_ptr<Builder> create_builder(const Value& cfg, const Value& ic, const
 
 // ------------------------------------------------------------------------------ orchestration
 
+// Guards the shared generated.yaml cache when several images build at once.
+static std::mutex& gen_mu() {
+  static std::mutex m;
+  return m;
+}
+
 static std::string context_cache_path(const std::string& abs_ctx) {
   return fs::join(".devspace", "cache", "context-" + sha256_hex(abs_ctx).substr(0, 16) + ".json");
 }
@@ -455,6 +462,7 @@ bool should_rebuild(config::Generated& gen, const Value& ic, const std::string& 
     trace::Span span("image.context_hash", {{"context", context_path}});
     hash = hash_directory_excludes(abs_ctx, excludes, context_cache_path(abs_ctx));
   }
+  std::lock_guard<std::mutex> g(gen_mu());  // images build concurrently (build_all)
   Value& cache = gen.cache(is_dev);
   bool must = true;
   if (!force)
@@ -488,7 +496,10 @@ bool build_image(const Value& cfg, config::Generated& gen, const std::string& na
   ImageBuildSettings s;
   s.image = image;
   s.tag = ic.get("tag").as_string().empty() ? random_string(7) : ic.get("tag").as_string();
-  s.last_tag = gen.cache(o.is_dev).get("imageTags").get(image).as_string();
+  {
+    std::lock_guard<std::mutex> g(gen_mu());
+    s.last_tag = gen.cache(o.is_dev).get("imageTags").get(image).as_string();
+  }
   for (auto& kv : ic.at_path("build.options.buildArgs").entries()) s.build_args[kv.first] = kv.second.as_string();
   s.target = ic.at_path("build.options.target").as_string();
   if (!o.docker_target.empty()) s.target = o.docker_target;
@@ -540,21 +551,49 @@ bool build_image(const Value& cfg, config::Generated& gen, const std::string& na
   } else {
     log::info("Skip image push for " + image);
   }
-  gen.cache(o.is_dev)["imageTags"][image] = s.tag;
+  {
+    std::lock_guard<std::mutex> g(gen_mu());
+    gen.cache(o.is_dev)["imageTags"][image] = s.tag;
+  }
   log::done("Done processing image '" + image + "'");
   return true;
 }
 
 bool build_all(const Value& cfg, config::Generated& gen, std::shared_ptr<kube::Client> kube, const BuildOptions& o) {
-  bool rebuilt = false;
+  std::vector<const std::pair<std::string, Value>*> todo;
   for (auto& e : cfg.get("images").entries()) {
     if (e.second.at_path("build.disabled").as_bool(false)) {
       log::info("Skipping building image " + e.first);
       continue;
     }
-    if (build_image(cfg, gen, e.first, e.second, kube, o)) rebuilt = true;
+    todo.push_back(&e);
   }
-  return rebuilt;
+  const char* par = getenv("DEVSPACE_BUILD_PARALLEL");
+  if (todo.size() <= 1 || (par && std::string(par) == "0")) {
+    bool rebuilt = false;
+    for (auto* e : todo)
+      if (build_image(cfg, gen, e->first, e->second, kube, o)) rebuilt = true;
+    return rebuilt;
+  }
+  // The reference builds images one after another (image/build.go); independent images build
+  // and push concurrently here, so a multi-service project waits for its slowest image, not the
+  // sum. The first failure is reported after every build has finished.
+  std::vector<std::thread> threads;
+  std::vector<std::string> errors(todo.size());
+  std::atomic<bool> rebuilt{false};
+  for (size_t i = 0; i < todo.size(); ++i) {
+    threads.emplace_back([&, i] {
+      try {
+        if (build_image(cfg, gen, todo[i]->first, todo[i]->second, kube, o)) rebuilt = true;
+      } catch (const std::exception& e) {
+        errors[i] = e.what();
+      }
+    });
+  }
+  for (auto& t : threads) t.join();
+  for (auto& e : errors)
+    if (!e.empty()) throw std::runtime_error(e);
+  return rebuilt.load();
 }
 
 }  // namespace build
