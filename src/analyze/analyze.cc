@@ -5,6 +5,7 @@
 #include <chrono>
 #include <map>
 #include <regex>
+#include <set>
 #include <thread>
 
 #include "core/log.h"
@@ -55,7 +56,8 @@ bool log_has_gpu_runtime_error(const std::string& text, std::string* match) {
       "No HIP GPUs are available|RuntimeError: No CUDA GPUs are available|"
       "rccl.*(error|failed)|NCCL error|ncclSystemError|ncclInternalError|ncclUnhandledCudaError|"
       "amdgpu.ids: No such file|Unable to open /dev/kfd|/dev/kfd: (Permission denied|No such file)|"
-      "torch.OutOfMemoryError|HIP out of memory)",
+      "torch.OutOfMemoryError|HIP out of memory|"
+      "Bus error|unable to (write to|allocate) .*shared memory|shared memory segment|/dev/shm.*No space left)",
       std::regex::icase);
   std::smatch m;
   if (std::regex_search(text, m, re)) {
@@ -65,6 +67,28 @@ bool log_has_gpu_runtime_error(const std::string& text, std::string* match) {
     return true;
   }
   return false;
+}
+
+// RCCL between the GPUs of one pod (one process per GPU) and PyTorch's worker processes use
+// /dev/shm; container runtimes give 64 MiB unless a memory-backed emptyDir is mounted there.
+// Returns "" when a multi-GPU pod has one, else the problem.
+std::string shm_problem(const Value& pod, int64_t gpus) {
+  if (gpus < 2) return "";
+  std::set<std::string> mem_volumes;
+  for (auto& v : pod.at_path("spec.volumes").items())
+    if (v.at_path("emptyDir.medium").as_string() == "Memory") mem_volumes.insert(v.get("name").as_string());
+  for (auto& c : pod.at_path("spec.containers").items()) {
+    const Value& lim = c.at_path("resources.limits").get("amd.com/gpu");
+    if (lim.as_int(0) == 0 && c.at_path("resources.requests").get("amd.com/gpu").as_int(0) == 0) continue;
+    bool ok = false;
+    for (auto& m : c.get("volumeMounts").items())
+      if (m.get("mountPath").as_string() == "/dev/shm" && mem_volumes.count(m.get("name").as_string())) ok = true;
+    if (!ok)
+      return "container " + c.get("name").as_string() + " uses " + std::to_string(gpus) +
+             " GPUs but has no memory-backed /dev/shm (RCCL intra-node transport; the runtime default is 64 MiB) — "
+             "mount an emptyDir{medium: Memory} at /dev/shm";
+  }
+  return "";
 }
 
 static int64_t gpu_request(const Value& pod) {
@@ -191,6 +215,8 @@ std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, co
       out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + " requests amd.com/gpu: " +
                     std::to_string(want) + " but the largest node has " + std::to_string(max_alloc) +
                     " (MI355X nodes expose 8 GPUs; HBM is not a schedulable resource)\n");
+    std::string shm = shm_problem(p, want);
+    if (!shm.empty()) out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + shm + "\n");
     for (auto& c : p.at_path("status.containerStatuses").items()) {
       bool crashed = c.get("restartCount").as_int() > 0 || !c.at_path("state.terminated").is_null();
       if (!crashed) continue;

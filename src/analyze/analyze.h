@@ -34,6 +34,8 @@ std::string analyze(kube::Client& k, const std::string& ns, const Options& o);
 std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, const std::vector<Value>& pods,
                                       const Options& o);
 bool log_has_gpu_runtime_error(const std::string& log, std::string* match);
+// Multi-GPU pod without a memory-backed /dev/shm (RCCL): the problem text, or "".
+std::string shm_problem(const Value& pod, int64_t gpus);
 // Runs the shell-only GPU probe in a container; returns the problems it found (empty = fine).
 // Works in images without devspace_amd (torch check) and without python3 (device nodes only,
 // reported as "probe unavailable").

@@ -3,6 +3,7 @@
 #include "analyze/analyze.h"
 #include "core/codec.h"
 #include "core/fs.h"
+#include "core/strutil.h"
 #include "kube/client.h"
 #include "kube/kubeconfig.h"
 #include "testing.h"
@@ -84,6 +85,16 @@ TEST(analyze_gpu_runtime_log_matcher) {
   EXPECT_TRUE(analyze::log_has_gpu_runtime_error("NCCL WARN NET/Socket : no socket found\nncclSystemError", &m));
   EXPECT_TRUE(analyze::log_has_gpu_runtime_error("hipErrorNoDevice", &m));
   EXPECT_TRUE(!analyze::log_has_gpu_runtime_error("Example app listening on port 3000!", &m));
+  EXPECT_TRUE(analyze::log_has_gpu_runtime_error("ERROR: Unexpected bus error encountered in worker. Bus error", &m));
+  // multi-GPU pods need a memory-backed /dev/shm (RCCL); the devspace chart mounts one
+  Value pod = yaml_parse(
+      "spec:\n  containers:\n  - name: train\n    resources: {limits: {amd.com/gpu: 8}}\n    volumeMounts: []\n");
+  EXPECT_TRUE(contains(analyze::shm_problem(pod, 8), "no memory-backed /dev/shm"));
+  EXPECT_EQ(analyze::shm_problem(pod, 1), std::string(""));
+  Value ok = yaml_parse(
+      "spec:\n  volumes: [{name: shm, emptyDir: {medium: Memory, sizeLimit: 64Gi}}]\n  containers:\n  - name: train\n"
+      "    resources: {limits: {amd.com/gpu: 8}}\n    volumeMounts: [{name: shm, mountPath: /dev/shm}]\n");
+  EXPECT_EQ(analyze::shm_problem(ok, 8), std::string(""));
 }
 
 // $KUBECONFIG with several files, merged like client-go's clientcmd loading rules.
