@@ -619,6 +619,12 @@ Value Client::capabilities() {
   return caps_;
 }
 
+// helm.sh/resource-policy: keep — Helm never deletes such an object on uninstall or when an
+// upgrade drops it from the chart (typically PersistentVolumeClaims holding data).
+static bool keep_on_delete(const Value& o) {
+  return o.at_path("metadata.annotations").get("helm.sh/resource-policy").as_string() == "keep";
+}
+
 static std::string object_key(const Value& o) {
   return o.get("apiVersion").as_string() + "/" + o.get("kind").as_string() + "/" +
          o.at_path("metadata.namespace").as_string() + "/" + o.at_path("metadata.name").as_string();
@@ -850,7 +856,7 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
         if (!d.is_map() || d.get("kind").is_null()) continue;
         if (d.at_path("metadata.namespace").is_null() && !kube::is_cluster_scoped(d.get("kind").as_string()))
           d["metadata"]["namespace"] = ns;
-        if (!keep.count(object_key(d))) k_->delete_object(d, ns);
+        if (!keep.count(object_key(d)) && !keep_on_delete(d)) k_->delete_object(d, ns);
       }
     }
     if (wait) {
@@ -933,7 +939,7 @@ void Client::rollback(const std::string& ns, const std::string& name, int to_ver
       if (!d.is_map() || d.get("kind").is_null()) continue;
       if (d.at_path("metadata.namespace").is_null() && !kube::is_cluster_scoped(d.get("kind").as_string()))
         d["metadata"]["namespace"] = ns;
-      if (!keep.count(object_key(d))) k_->delete_object(d, ns);
+      if (!keep.count(object_key(d)) && !keep_on_delete(d)) k_->delete_object(d, ns);
     }
   }
   run_hooks(r.hooks, "post-rollback", ns, 300);
@@ -957,8 +963,15 @@ void Client::delete_release(const std::string& ns, const std::string& name, bool
   }
   auto docs = yaml_parse_all(last.manifest);
   std::reverse(docs.begin(), docs.end());
-  for (auto& d : docs)
-    if (d.is_map() && !d.get("kind").is_null()) k_->delete_object(d, ns);
+  for (auto& d : docs) {
+    if (!d.is_map() || d.get("kind").is_null()) continue;
+    if (keep_on_delete(d)) {
+      log::info("Keeping " + d.get("kind").as_string() + " " + d.at_path("metadata.name").as_string() +
+                " (helm.sh/resource-policy: keep)");
+      continue;
+    }
+    k_->delete_object(d, ns);
+  }
   try {
     run_hooks(last.hooks, "post-delete", ns, 300);
   } catch (const std::exception& e) {

@@ -80,8 +80,8 @@ def test_hooks_run_in_order_and_release_is_helm3(localkube):
     assert set(chart) >= {"metadata", "lock", "templates", "values", "schema", "files"}
     assert chart["metadata"]["name"] == "hooks-chart" and chart["metadata"]["apiVersion"] == "v2"
     names = sorted(t["name"] for t in chart["templates"])
-    assert names == ["templates/app.yaml", "templates/migrate-job.yaml", "templates/post-hook.yaml",
-                     "templates/test-pod.yaml"], names
+    assert names == ["templates/app.yaml", "templates/data-pvc.yaml", "templates/migrate-job.yaml",
+                     "templates/post-hook.yaml", "templates/test-pod.yaml"], names
     src = {t["name"]: base64.b64decode(t["data"]).decode() for t in chart["templates"]}
     assert "helm.sh/hook" in src["templates/migrate-job.yaml"]
     assert chart["values"] == {"migrate": {"exitCode": 0}}
@@ -106,9 +106,14 @@ def test_hooks_run_in_order_and_release_is_helm3(localkube):
     job2 = lk.cluster.store.get("batch", "jobs", ns, "rel-migrate")
     assert job2["metadata"]["uid"] != job["metadata"]["uid"]
 
-    lk.run(["purge"], proj)
+    pvc = lk.cluster.store.get("", "persistentvolumeclaims", ns, "rel-data")
+    out = lk.run(["purge"], proj).stdout
     wait_for(lambda: not _releases(lk, ns), timeout=30, what="release secrets purged")
     assert _cm(lk, ns, "rel-app") is None
+    # helm.sh/resource-policy: keep survives the uninstall (same object, not recreated)
+    kept = lk.cluster.store.try_get("", "persistentvolumeclaims", ns, "rel-data")
+    assert kept and kept["metadata"]["uid"] == pvc["metadata"]["uid"], out
+    assert "resource-policy: keep" in out, out
 
 
 def test_failed_pre_upgrade_hook_rolls_back(localkube):
