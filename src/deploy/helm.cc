@@ -378,6 +378,7 @@ static void render_chart(tmpl::Engine& eng, const Chart& c, const Value& values,
 std::vector<std::pair<std::string, std::string>> render_files(const Chart& chart, const Value& values,
                                                               const RenderOptions& o) {
   tmpl::Engine eng;
+  if (o.lookup) eng.lookup = o.lookup;
   add_templates(eng, chart, "");
   std::vector<std::pair<std::string, std::string>> out;
   render_chart(eng, chart, values, o, capabilities_value(o.capabilities), "", true, &out);
@@ -818,6 +819,22 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
   ro.revision = rev;
   ro.is_install = last_deployed == nullptr;
   if (mentions_capabilities(chart)) ro.capabilities = capabilities();
+  // Helm 3 `lookup`: live objects (a single object by name, or a List when name is empty); a
+  // missing object or a forbidden read renders as an empty map, as Helm does
+  ro.lookup = [this](const std::string& av, const std::string& kind, const std::string& lns,
+                     const std::string& lname) -> Value {
+    try {
+      if (!lname.empty()) {
+        auto o = k_->try_get(kube::resource_path(av, kind, lns, lname));
+        return o ? *o : Value::map();
+      }
+      Value list = k_->get(kube::resource_path(av, kind, lns, ""));
+      list["kind"] = kind + "List";
+      return list;
+    } catch (const std::exception&) {
+      return Value::map();
+    }
+  };
   Value merged = coalesce_values(chart, values);
   Rendered rd = render_release(chart, merged, ro);
   std::vector<Value>& objs = rd.objs;

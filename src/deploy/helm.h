@@ -15,6 +15,7 @@
 //  * NOTES.txt of the top chart rendered into the release's info.notes.
 #pragma once
 
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -62,6 +63,10 @@ struct RenderOptions {
   bool is_install = true;
   // {KubeVersion: {Major, Minor, GitVersion, Version}, APIVersions: [..]}; null = defaults
   Value capabilities;
+  // `lookup` against the live cluster (install/upgrade); unset = {} as in `helm template`
+  std::function<Value(const std::string& api_version, const std::string& kind, const std::string& ns,
+                      const std::string& name)>
+      lookup;
 };
 
 // Renders all templates into manifests (parsed YAML docs, empty docs dropped, sorted in

@@ -162,3 +162,19 @@ def test_dependencies_files_and_capabilities_on_cluster(localkube):
     files = sorted(f["name"] for f in rel["chart"]["files"])
     assert files == ["README.md", "conf/a.conf", "conf/b.conf", "data/lines.txt", "data/token.txt"], files
     lk.run(["purge"], proj)
+
+
+def test_lookup_keeps_generated_secret_across_upgrades(localkube):
+    """Helm 3 `lookup` reads the live cluster during install/upgrade: the chart reuses the
+    password it generated on the first install instead of rotating it on every deploy."""
+    lk = localkube
+    ns = "helm-lookup"
+    proj = _helm_project(lk, "lookup-chart", "helm-lookup", ns)
+    lk.run(["deploy"], proj)
+    pw1 = lk.cluster.store.get("", "secrets", ns, "rel-auth")["data"]["password"]
+    assert _cm(lk, ns, "rel-lookup")["data"]["found-before"] == "no"
+    lk.run(["deploy", "-d"], proj)
+    assert lk.cluster.store.get("", "secrets", ns, "rel-auth")["data"]["password"] == pw1
+    cm = _cm(lk, ns, "rel-lookup")["data"]
+    assert cm["found-before"] == "yes" and int(cm["configmaps-seen"]) >= 1, cm
+    lk.run(["purge"], proj)
