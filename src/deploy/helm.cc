@@ -2,8 +2,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <ctime>
 #include <map>
+#include <regex>
 #include <set>
 #include <thread>
 
@@ -284,6 +286,188 @@ static void import_values(Chart& c) {
 void process_dependencies(Chart& c, const Value& user_values) {
   dependency_enabled(c, coalesce_values(c, user_values), "");
   import_values(c);
+}
+
+// ============================================================== values.schema.json
+
+namespace {
+
+std::string json_type_of(const Value& v) {
+  switch (v.type()) {
+    case Value::Type::Null: return "null";
+    case Value::Type::Bool: return "boolean";
+    case Value::Type::Int: return "integer";
+    case Value::Type::Float: return v.as_double() == std::floor(v.as_double()) ? "integer" : "number";
+    case Value::Type::String: return "string";
+    case Value::Type::Seq: return "array";
+    case Value::Type::Map: return "object";
+  }
+  return "null";
+}
+
+bool type_matches(const Value& v, const std::string& t) {
+  std::string vt = json_type_of(v);
+  return vt == t || (t == "number" && vt == "integer");
+}
+
+// JSON Schema (draft-07 subset Helm charts use): type, enum, const, required, properties,
+// additionalProperties, patternProperties, items, min/maxItems, uniqueItems, minimum/maximum
+// (+exclusive), multipleOf, min/maxLength, pattern, allOf/anyOf/oneOf/not, $ref into
+// #/definitions or #/$defs. Errors are "path: message" lines like Helm's gojsonschema output.
+void validate_schema(const Value& v, const Value& schema, const Value& root, const std::string& path,
+                     std::vector<std::string>* errs, int depth = 0) {
+  if (!schema.is_map() || depth > 64) return;
+  auto err = [&](const std::string& m) { errs->push_back((path.empty() ? "(root)" : path) + ": " + m); };
+  if (schema.has("$ref")) {
+    std::string ref = schema.get("$ref").as_string();
+    if (starts_with(ref, "#/")) {
+      const Value* cur = &root;
+      for (auto& part : split(ref.substr(2), "/")) {
+        cur = cur->is_map() ? cur->find(part) : nullptr;
+        if (!cur) break;
+      }
+      if (cur) validate_schema(v, *cur, root, path, errs, depth + 1);
+    }
+  }
+  const Value& type = schema.get("type");
+  if (!type.is_null()) {
+    bool ok = false;
+    if (type.is_seq()) {
+      for (auto& t : type.items()) ok |= type_matches(v, t.as_string());
+    } else {
+      ok = type_matches(v, type.as_string());
+    }
+    if (!ok) {
+      err("Invalid type. Expected: " + (type.is_seq() ? json_dump(type) : type.as_string()) + ", given: " +
+          json_type_of(v));
+      return;
+    }
+  }
+  if (schema.get("enum").is_seq()) {
+    bool ok = false;
+    for (auto& e : schema.get("enum").items()) ok |= e == v || (e.is_number() && v.is_number() && e.as_double() == v.as_double());
+    if (!ok) err("must be one of the following: " + json_dump(schema.get("enum")));
+  }
+  if (schema.has("const") && !(schema.get("const") == v)) err("does not match: " + json_dump(schema.get("const")));
+  if (v.is_map()) {
+    for (auto& r : schema.get("required").items())
+      if (!v.has(r.as_string())) err(r.as_string() + " is required");
+    const Value& props = schema.get("properties");
+    const Value& pprops = schema.get("patternProperties");
+    for (auto& e : v.entries()) {
+      std::string sub = path.empty() ? e.first : path + "." + e.first;
+      bool known = false;
+      if (const Value* ps = props.is_map() ? props.find(e.first) : nullptr) {
+        known = true;
+        validate_schema(e.second, *ps, root, sub, errs, depth + 1);
+      }
+      for (auto& pp : pprops.entries()) {
+        try {
+          if (std::regex_search(e.first, std::regex(pp.first))) {
+            known = true;
+            validate_schema(e.second, pp.second, root, sub, errs, depth + 1);
+          }
+        } catch (const std::regex_error&) {
+        }
+      }
+      if (known) continue;
+      const Value& ap = schema.get("additionalProperties");
+      if (ap.is_bool() && !ap.as_bool())
+        err("Additional property " + e.first + " is not allowed");
+      else if (ap.is_map())
+        validate_schema(e.second, ap, root, sub, errs, depth + 1);
+    }
+    if (schema.has("minProperties") && (int64_t)v.size() < schema.get("minProperties").as_int())
+      err("must have at least " + schema.get("minProperties").as_string() + " properties");
+  }
+  if (v.is_seq()) {
+    if (schema.has("minItems") && (int64_t)v.size() < schema.get("minItems").as_int())
+      err("Array must have at least " + schema.get("minItems").as_string() + " items");
+    if (schema.has("maxItems") && (int64_t)v.size() > schema.get("maxItems").as_int())
+      err("Array must have at most " + schema.get("maxItems").as_string() + " items");
+    if (schema.get("uniqueItems").as_bool(false))
+      for (size_t i = 0; i < v.size(); ++i)
+        for (size_t j = i + 1; j < v.size(); ++j)
+          if (v[i] == v[j]) err("array items[" + std::to_string(i) + "," + std::to_string(j) + "] must be unique");
+    if (schema.get("items").is_map())
+      for (size_t i = 0; i < v.size(); ++i)
+        validate_schema(v[i], schema.get("items"), root, path + "." + std::to_string(i), errs, depth + 1);
+  }
+  if (v.is_number()) {
+    double x = v.as_double();
+    if (schema.has("minimum") && x < schema.get("minimum").as_double())
+      err("Must be greater than or equal to " + schema.get("minimum").as_string());
+    if (schema.has("maximum") && x > schema.get("maximum").as_double())
+      err("Must be less than or equal to " + schema.get("maximum").as_string());
+    if (schema.get("exclusiveMinimum").is_number() && x <= schema.get("exclusiveMinimum").as_double())
+      err("Must be greater than " + schema.get("exclusiveMinimum").as_string());
+    if (schema.get("exclusiveMaximum").is_number() && x >= schema.get("exclusiveMaximum").as_double())
+      err("Must be less than " + schema.get("exclusiveMaximum").as_string());
+    if (schema.has("multipleOf") && schema.get("multipleOf").as_double() > 0) {
+      double q = x / schema.get("multipleOf").as_double();
+      if (std::fabs(q - std::round(q)) > 1e-9) err("Must be a multiple of " + schema.get("multipleOf").as_string());
+    }
+  }
+  if (v.is_string()) {
+    size_t n = 0;
+    for (unsigned char c : v.str()) n += (c & 0xC0) != 0x80;  // code points
+    if (schema.has("minLength") && (int64_t)n < schema.get("minLength").as_int())
+      err("String length must be greater than or equal to " + schema.get("minLength").as_string());
+    if (schema.has("maxLength") && (int64_t)n > schema.get("maxLength").as_int())
+      err("String length must be less than or equal to " + schema.get("maxLength").as_string());
+    if (schema.has("pattern")) {
+      try {
+        if (!std::regex_search(v.str(), std::regex(schema.get("pattern").as_string(), std::regex::ECMAScript)))
+          err("Does not match pattern '" + schema.get("pattern").as_string() + "'");
+      } catch (const std::regex_error&) {
+      }
+    }
+  }
+  for (auto& s : schema.get("allOf").items()) validate_schema(v, s, root, path, errs, depth + 1);
+  auto passes = [&](const Value& s) {
+    std::vector<std::string> e;
+    validate_schema(v, s, root, path, &e, depth + 1);
+    return e.empty();
+  };
+  if (schema.get("anyOf").is_seq()) {
+    bool any = false;
+    for (auto& s : schema.get("anyOf").items()) any |= passes(s);
+    if (!any) err("Must validate at least one schema (anyOf)");
+  }
+  if (schema.get("oneOf").is_seq()) {
+    int n = 0;
+    for (auto& s : schema.get("oneOf").items()) n += passes(s);
+    if (n != 1) err("Must validate one and only one schema (oneOf)");
+  }
+  if (schema.get("not").is_map() && passes(schema.get("not"))) err("Must not validate the schema (not)");
+}
+
+void validate_chart_values(const Chart& c, const Value& values, std::string* report) {
+  if (!c.schema.empty()) {
+    Value schema;
+    try {
+      schema = json_parse(c.schema);
+    } catch (const std::exception& e) {
+      *report += c.name() + ":\n- values.schema.json: " + e.what() + "\n";
+    }
+    std::vector<std::string> errs;
+    validate_schema(values, schema, schema, "", &errs);
+    if (!errs.empty()) {
+      *report += c.name() + ":\n";
+      for (auto& e : errs) *report += "- " + e + "\n";
+    }
+  }
+  for (auto& d : c.dependencies) validate_chart_values(d, values.get(d.name()), report);
+}
+
+}  // namespace
+
+void validate_values(const Chart& chart, const Value& coalesced_values) {
+  std::string report;
+  validate_chart_values(chart, coalesced_values, &report);
+  if (!report.empty())
+    throw std::runtime_error("values don't meet the specifications of the schema(s) in the following chart(s):\n" +
+                             report);
 }
 
 // ============================================================== rendering
@@ -836,6 +1020,7 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
     }
   };
   Value merged = coalesce_values(chart, values);
+  validate_values(chart, merged);  // values.schema.json, as `helm install` does before rendering
   Rendered rd = render_release(chart, merged, ro);
   std::vector<Value>& objs = rd.objs;
   k_->check_gpu_requests(objs);

@@ -12,7 +12,9 @@
 //    child/parent forms; the parent's own values take precedence), nested charts;
 //  * library charts (type: library) contribute their defines only;
 //  * `.Capabilities` from the API server's /version and /api(s) discovery;
-//  * NOTES.txt of the top chart rendered into the release's info.notes.
+//  * NOTES.txt of the top chart rendered into the release's info.notes;
+//  * values.schema.json validation (JSON Schema subset) before rendering;
+//  * `lookup` against the live cluster, `helm.sh/resource-policy: keep`.
 #pragma once
 
 #include <functional>
@@ -52,6 +54,10 @@ Chart load_chart(const std::string& dir);
 // Helm's ProcessDependencies: drops disabled subcharts (condition/tags, against the chart
 // defaults coalesced with `user_values`), applies aliases and import-values. Mutates `c`.
 void process_dependencies(Chart& c, const Value& user_values);
+
+// values.schema.json of the chart and of every subchart (against its part of the values), as
+// Helm 3 does before rendering; throws with Helm's report format when any value is invalid.
+void validate_values(const Chart& chart, const Value& coalesced_values);
 
 // CoalesceValues: chart defaults (recursively, each subchart under its name) under the user's
 // values, with `global` propagated into every subchart.

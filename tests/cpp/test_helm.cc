@@ -279,3 +279,41 @@ TEST(gotemplate_go118_control_flow) {
   EXPECT_EQ(R("{{ if or (not (hasKey . \"x\")) (gt .x 1) }}ok{{ end }}"), std::string("ok"));
   EXPECT_EQ(R("{{ and 1 0 2 }}|{{ or 0 \"\" 3 }}|{{ 5 | and 1 }}|{{ 0 | or \"\" }}"), std::string("0|3|5|0"));
 }
+
+TEST(helm_values_schema_validation) {
+  helm::Chart c = helm::load_chart(kCharts + "schema-chart");
+  EXPECT_TRUE(!c.schema.empty());
+  helm::validate_values(c, helm::coalesce_values(c, Value::map()));  // defaults are valid
+  Value bad = yaml_parse(
+      "replicas: 40\ngpus: 3\nimage: {repository: 'Bad Repo', pullPolicy: Sometimes, extra: 1}\nsub: {mode: turbo}\n");
+  std::string msg;
+  try {
+    helm::validate_values(c, helm::coalesce_values(c, bad));
+  } catch (const std::exception& e) {
+    msg = e.what();
+  }
+  EXPECT_TRUE(starts_with(msg, "values don't meet the specifications of the schema(s) in the following chart(s):"));
+  EXPECT_TRUE(contains(msg, "schema-chart:\n"));
+  EXPECT_TRUE(contains(msg, "- replicas: Must be less than or equal to 16"));
+  EXPECT_TRUE(contains(msg, "- gpus: must be one of the following: [0,1,2,4,8]"));
+  EXPECT_TRUE(contains(msg, "- image.repository: Does not match pattern"));
+  EXPECT_TRUE(contains(msg, "- image.pullPolicy: must be one of the following"));  // via $ref
+  EXPECT_TRUE(contains(msg, "- image: Additional property extra is not allowed"));
+  EXPECT_TRUE(contains(msg, "sub:\n- mode: must be one of the following"));  // subchart schema
+  Value wrong_type = yaml_parse("replicas: 'two'\n");
+  msg.clear();
+  try {
+    helm::validate_values(c, helm::coalesce_values(c, wrong_type));
+  } catch (const std::exception& e) {
+    msg = e.what();
+  }
+  EXPECT_TRUE(contains(msg, "- replicas: Invalid type. Expected: integer, given: string"));
+  Value missing = yaml_parse("image: null\n");  // a null user value deletes the default
+  msg.clear();
+  try {
+    helm::validate_values(c, helm::coalesce_values(c, missing));
+  } catch (const std::exception& e) {
+    msg = e.what();
+  }
+  EXPECT_TRUE(contains(msg, "- (root): image is required"));
+}

@@ -178,3 +178,21 @@ def test_lookup_keeps_generated_secret_across_upgrades(localkube):
     cm = _cm(lk, ns, "rel-lookup")["data"]
     assert cm["found-before"] == "yes" and int(cm["configmaps-seen"]) >= 1, cm
     lk.run(["purge"], proj)
+
+
+def test_values_schema_rejects_invalid_values_before_anything_is_applied(localkube):
+    lk = localkube
+    ns = "helm-schema"
+    proj = _helm_project(lk, "schema-chart", "helm-schema", ns, values={"replicas": 99})
+    p = lk.run(["deploy"], proj, check=False)
+    out = p.stdout + p.stderr
+    assert p.returncode != 0 and "values don't meet the specifications of the schema(s)" in out, out
+    assert "replicas: Must be less than or equal to 16" in out, out
+    assert _cm(lk, ns, "rel-schema") is None and not _releases(lk, ns)
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    cfg["deployments"][0]["helm"]["overrideValues"] = {"replicas": 2}
+    open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    lk.run(["deploy"], proj)
+    assert _cm(lk, ns, "rel-schema")["data"]["replicas"] == "2"
+    lk.run(["purge"], proj)
