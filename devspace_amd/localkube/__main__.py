@@ -1,4 +1,4 @@
-"""python -m devspace_amd.localkube up --state DIR [--port P] [--gpus N] [--kubeconfig PATH]"""
+"""python -m devspace_amd.localkube up --state DIR [--port P] [--gpus N] [--kubeconfig PATH] [--context NAME] [--tls]"""
 import argparse
 import os
 import signal
@@ -17,8 +17,10 @@ def main(argv=None):
     up.add_argument("--gpus", type=int, default=None)
     up.add_argument("--kubeconfig", default="")
     up.add_argument("--namespace", default="default")
+    up.add_argument("--context", default="devspace-local", help="kube context name (e.g. minikube)")
+    up.add_argument("--tls", action="store_true", help="https + wss with client certificates")
     args = ap.parse_args(argv)
-    c = LocalCluster(args.state, port=args.port, gpus=args.gpus).start()
+    c = LocalCluster(args.state, port=args.port, gpus=args.gpus, context=args.context, tls=args.tls).start()
     kc = args.kubeconfig or os.path.join(args.state, "kubeconfig")
     c.write_kubeconfig(kc, args.namespace)
     print(f"ready server={c.server} kubeconfig={kc} docker=unix://{c.docker_sock} gpus={c.gpus}", flush=True)

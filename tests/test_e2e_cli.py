@@ -339,3 +339,34 @@ def test_add_list_remove_package_from_chart_repo(localkube):
         lk.run(["purge"], proj)
     finally:
         lk.env.pop("DEVSPACE_HELM_HOME", None)
+
+
+def test_minikube_example_builds_in_minikube_daemon(tmp_path):
+    """examples/minikube: kube context `minikube` -> the image is built by minikube's Docker
+    daemon (`minikube docker-env`, builder/docker/client.go) and not pushed (skipPush)."""
+    from devspace_amd.localkube import LocalCluster
+
+    from conftest import DevspaceEnv
+
+    base = str(tmp_path)
+    cluster = LocalCluster(os.path.join(base, "state"), gpus=0, context="minikube").start()
+    try:
+        lk = DevspaceEnv(cluster, base)
+        shim = tmp_path / "shim"
+        shim.mkdir()
+        (shim / "minikube").write_text(
+            "#!/bin/sh\n[ \"$1\" = docker-env ] || exit 1\n"
+            f"echo DOCKER_HOST=unix://{cluster.docker_sock}\necho MINIKUBE_ACTIVE_DOCKERD=minikube\n")
+        (shim / "minikube").chmod(0o755)
+        lk.env.pop("DOCKER_HOST")  # only `minikube docker-env` knows where the daemon is
+        lk.env["PATH"] = f"{shim}:{lk.env['PATH']}"
+        proj = lk.project("minikube")
+        out = lk.run(["deploy"], proj, timeout=120).stdout
+        assert "Skip image push for devspace" in out, out
+        pods = wait_for(lambda: running(lk.pods("devspace")), what="minikube example pod")
+        assert pods[0]["spec"]["containers"][0]["image"].startswith("devspace:"), pods[0]["spec"]
+        # never pushed: the registry side of the image store stays empty
+        assert not cluster.images.resolve("registry.invalid/devspace")
+        lk.run(["purge"], proj)
+    finally:
+        cluster.stop()
