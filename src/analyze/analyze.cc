@@ -151,7 +151,7 @@ fi
 )SH";
 
 std::vector<std::string> probe_pod_gpus(kube::Client& k, const std::string& ns, const std::string& pod,
-                                        const std::string& container) {
+                                        const std::string& container, std::string* summary) {
   auto s = k.exec(ns, pod, container, {"sh", "-c", kGpuProbeScript}, false, false);
   s->close_stdin_if_any();
   std::string outp = read_all(s->out());
@@ -176,6 +176,20 @@ std::vector<std::string> probe_pod_gpus(kube::Client& k, const std::string& ns, 
   if (!json_text.empty()) {
     Value rep = json_parse(json_text);
     for (auto& pr : rep.get("problems").items()) problems.push_back(pr.as_string());
+    // what the probe verified, so a clean report still says that the devices were exercised
+    std::vector<std::string> devs;
+    for (auto& d : rep.get("devices").items()) {
+      std::string arch = d.get("arch").as_string();
+      std::string dev = "gpu" + std::to_string(d.get("index").as_int()) + " " + (arch.empty() ? "?" : arch);
+      if (!d.get("mfma_selftest_max_abs_err").is_null())
+        dev += " MFMA self-test err " + json_dump(d.get("mfma_selftest_max_abs_err"));
+      else if (!d.get("matmul_rel_err").is_null())
+        dev += " bf16 matmul rel err " + json_dump(d.get("matmul_rel_err"));
+      devs.push_back(dev);
+    }
+    if (summary)
+      *summary = std::to_string(devs.size()) + " device(s) checked by the " + kv["PROBE"] + " probe" +
+                 (devs.empty() ? "" : ": " + join(devs, ", "));
   } else if (kv["PROBE"] == "unavailable" || kv.count("PROBE_FAILED") || kv["PROBE"].empty()) {
     problems.push_back("GPU probe unavailable (no python3 in the image): only device nodes were checked");
   }
@@ -234,8 +248,10 @@ std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, co
     if (o.gpu_probe && kube::pod_status(p) == "Running") {
       std::string c = p.at_path("spec.containers")[0].get("name").as_string();
       try {
-        for (auto& line : probe_pod_gpus(k, ns, name, c))
+        std::string summary;
+        for (auto& line : probe_pod_gpus(k, ns, name, c, &summary))
           out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + line + "\n");
+        if (!summary.empty()) log::infof("GPU probe of pod %s: %s", name.c_str(), summary.c_str());
       } catch (const std::exception& e) {
         out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": GPU probe unavailable (" + e.what() +
                       ")\n");

@@ -38,9 +38,10 @@ bool log_has_gpu_runtime_error(const std::string& log, std::string* match);
 std::string shm_problem(const Value& pod, int64_t gpus);
 // Runs the shell-only GPU probe in a container; returns the problems it found (empty = fine).
 // Works in images without devspace_amd (torch check) and without python3 (device nodes only,
-// reported as "probe unavailable").
+// reported as "probe unavailable"). `summary` (optional) receives what was verified, e.g.
+// "1 device(s) checked by the devspace probe: gpu0 gfx950 MFMA self-test err 0".
 std::vector<std::string> probe_pod_gpus(kube::Client& k, const std::string& ns, const std::string& pod,
-                                        const std::string& container);
+                                        const std::string& container, std::string* summary = nullptr);
 
 }  // namespace analyze
 }  // namespace ds

@@ -4,6 +4,7 @@ runs the gfx950 probe kernels inside the pod."""
 
 import json
 import os
+import re
 import time
 
 import pytest
@@ -43,8 +44,17 @@ def test_rocm_pytorch_pod_trains_on_gpu(tmp_path):
                     if "started gen=" in (open(root + ".log").read() if os.path.exists(root + ".log") else "")
                     else None, 300, "runner start")
         assert "device=cuda:0" in log, log
-        report = lk.run(["analyze", "--wait=false", "--gpu-probe", "-n", "rocm-pytorch"], proj, timeout=300).stdout
-        assert "GPU" not in report or "No problems found" in report, report
+        r = lk.run(["analyze", "--wait=false", "--gpu-probe", "-n", "rocm-pytorch"], proj, timeout=300)
+        report = r.stdout + r.stderr
+        # the probe ran inside the pod and exercised every granted device (MFMA self-test)
+        assert "No problems found" in report, report
+        m = re.search(r"GPU probe of pod \S+: (\d+) device\(s\) checked by the (\w+) probe: (.*)", report)
+        assert m, report
+        granted = int(pod["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"])
+        assert int(m.group(1)) == granted and m.group(2) in ("devspace", "torch"), report
+        assert "gfx950" in m.group(3), report
+        if m.group(2) == "devspace":
+            assert re.search(r"MFMA self-test err 0(\.0)?(,|$)", m.group(3)), report
         lk.run(["purge"], proj, timeout=120)
     finally:
         cluster.stop()
