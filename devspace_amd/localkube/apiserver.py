@@ -21,6 +21,7 @@ import time
 import yaml
 from aiohttp import WSMsgType, web
 
+from .kubelet import close_proc
 from .store import CLUSTER_SCOPED, ApiError, labels_match, parse_selector
 
 GROUP_KINDS = {
@@ -492,33 +493,42 @@ class ApiServer:
                     pass
 
         reader = asyncio.create_task(read_ws())
-        code = await proc.wait()
-        c.exec_procs.discard(proc)
-        if tty:
-            try:
-                await asyncio.sleep(0.05)
-                loop.remove_reader(master)
-            except Exception:
-                pass
-            try:
-                while True:
-                    rest = os.read(master, 65536)
-                    if not rest:
-                        break
-                    await ws.send_bytes(b"\x01" + rest)
-            except OSError:
-                pass
-            q.put_nowait(b"")
-        await asyncio.gather(*tasks, return_exceptions=True)
-        if not ws.closed:
-            await ws.send_bytes(b"\x03" + json.dumps(_exit_status(code)).encode())
-            await ws.close()
-        reader.cancel()
-        if master is not None:
-            try:
-                os.close(master)
-            except OSError:
-                pass
+        try:
+            code = await proc.wait()
+            c.exec_procs.discard(proc)
+            if tty:
+                try:
+                    await asyncio.sleep(0.05)
+                    loop.remove_reader(master)
+                except Exception:
+                    pass
+                try:
+                    while True:
+                        rest = os.read(master, 65536)
+                        if not rest:
+                            break
+                        await ws.send_bytes(b"\x01" + rest)
+                except OSError:
+                    pass
+                q.put_nowait(b"")
+            await asyncio.gather(*tasks, return_exceptions=True)
+            if not ws.closed:
+                await ws.send_bytes(b"\x03" + json.dumps(_exit_status(code)).encode())
+                await ws.close()
+            reader.cancel()
+            if master is not None:
+                try:
+                    os.close(master)
+                except OSError:
+                    pass
+        finally:
+            # also when the handler is cancelled (cluster shutdown): the subprocess transport is
+            # closed while the loop still runs, never by the GC after the loop has closed
+            c.exec_procs.discard(proc)
+            reader.cancel()
+            for t in tasks:
+                t.cancel()
+            close_proc(proc)
         return ws
 
     async def _attach(self, ws, c):

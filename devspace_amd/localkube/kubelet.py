@@ -29,6 +29,14 @@ GPU_RESOURCE = "amd.com/gpu"
 HOST_IMAGES = ("rocm/pytorch", "rocm/dev", "python", "node", "ubuntu", "debian", "busybox", "alpine",
                "devspace-local/runtime", "gcr.io/kaniko-project/executor")
 
+def close_proc(proc):
+    """Close an asyncio subprocess's transport (its pipes) from the running loop. Left to the
+    GC, the transport closes after the loop did and raises 'Event loop is closed'."""
+    t = getattr(proc, "_transport", None) if proc is not None else None
+    if t is not None and not t.is_closing():
+        t.close()
+
+
 HOST_ONLY_ENV = {"RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
                  "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT", "KUBECONFIG",
                  "DOCKER_HOST", "DOCKER_CERT_PATH", "DOCKER_TLS_VERIFY", "HIP_VISIBLE_DEVICES",
@@ -620,6 +628,7 @@ class Kubelet:
                     await asyncio.wait_for(asyncio.shield(c.pump), timeout=0.5)
                 except (asyncio.TimeoutError, asyncio.CancelledError):
                     c.pump.cancel()
+            close_proc(c.proc)
         self.gpus_free.extend(rt.gpus)
         self.gpus_free.sort()
         rt.gpus = []

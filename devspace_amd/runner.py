@@ -311,7 +311,10 @@ def worker_main(args) -> int:
         # 1. pick up local change notifications (non-blocking while training; blocking when idle)
         timeout = 0 if (not script_mode and args.train) else 0.05
         n_changes, t_first = feed.take(timeout)
-        if n_changes:
+        # Rank 0's feed alone advances the generation: every rank watches the same synced
+        # directory, but their feeds post the edit microseconds apart, and a rank that saw it one
+        # step late would otherwise bump the group to a second generation (a spurious reload).
+        if n_changes and (ctl is None or rank == 0):
             pending_gen += 1
             if reload_t0 is None:
                 reload_t0 = t_first

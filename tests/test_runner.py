@@ -53,7 +53,10 @@ def _run_reload(tmp_path, extra_env=None, nproc=1):
             lines.append(line)
             if "reload failed" in line:
                 break
-        assert any("reload failed" in l for l in lines)
+        failed = [l for l in lines if "reload failed" in l]
+        assert failed
+        # one generation per edit on every rank count (no second, spurious reload of the first edit)
+        assert "gen=3" in failed[0], "".join(lines[-20:])
         assert proc.poll() is None
         return reload_line[0] + "".join(l for l in lines if "started gen=1" in l)
     finally:
