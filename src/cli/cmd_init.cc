@@ -73,6 +73,7 @@ void add_default_ports(Value& cfg, InitState& st) {
   prompt::Params p;
   p.question = "Which port is the app listening on? (Default: " + def + ")";
   p.default_value = "";
+  p.optional = true;  // the default is applied below
   std::string port = prompt::ask(p);
   if (port.empty()) port = def;
   Value pms = Value::seq();

@@ -99,6 +99,7 @@ std::string ask(const Params& p) {
     std::string line;
     if (!read_line(&line, p.is_password)) {
       if (!p.default_value.empty()) return p.default_value;
+      if (p.optional) return "";
       throw PromptError("cannot prompt for \"" + q +
                         "\" in non-interactive mode (set a default, an env var, or run interactively)");
     }

@@ -17,6 +17,7 @@ struct Params {
   std::string validation_regex;  // anchored implicitly like the reference (^...$)
   bool is_password = false;
   std::vector<std::string> options;  // select prompt when non-empty
+  bool optional = false;  // no answer available (non-interactive, stdin at EOF) = "" instead of an error
 };
 
 struct PromptError : std::runtime_error {

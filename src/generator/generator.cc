@@ -126,13 +126,34 @@ std::string ChartGenerator::detect_language() const {
   return best;
 }
 
+// The python/ruby templates start `main.<ext>`; a project whose entry file has another
+// conventional name (app.py, server.py, ...) or that has a single top-level source file gets
+// that file in the generated Dockerfile's CMD instead of a CMD that crashes on start.
+static std::string entry_file(const std::string& project, const std::string& ext) {
+  if (fs::exists(fs::join(project, "main" + ext))) return "main" + ext;
+  for (const char* base : {"app", "server", "run", "wsgi", "__main__"})
+    if (fs::exists(fs::join(project, base + ext))) return base + ext;
+  std::vector<std::string> top;
+  for (auto& e : fs::list_dir(project))
+    if (!e.is_dir && ends_with(e.name, ext)) top.push_back(e.name);
+  return top.size() == 1 ? top[0] : "main" + ext;
+}
+
 void ChartGenerator::create_chart(const std::string& language, bool overwrite) const {
   if (!is_supported(language)) throw std::runtime_error("Language Template not found");
   for (const std::string& dir : {std::string("_base"), language}) {
     for (auto& kv : files(dir)) {
       std::string dst = fs::join(project_, kv.first);
       if (!overwrite && fs::exists(dst)) continue;
-      fs::write_file(dst, kv.second, ends_with(kv.first, ".sh") ? 0755 : 0644);
+      std::string content = kv.second;
+      if (kv.first == "Dockerfile") {
+        for (const char* ext : {".py", ".rb"}) {
+          std::string tmpl = std::string("\"main") + ext + "\"";
+          size_t at = content.find(tmpl);
+          if (at != std::string::npos) content.replace(at, tmpl.size(), "\"" + entry_file(project_, ext) + "\"");
+        }
+      }
+      fs::write_file(dst, content, ends_with(kv.first, ".sh") ? 0755 : 0644);
     }
   }
 }

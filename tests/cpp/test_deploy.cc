@@ -153,6 +153,21 @@ TEST(generator_detects_languages) {
   fs::remove_all(d);
 }
 
+TEST(generator_dockerfile_cmd_uses_the_entry_file) {
+  auto cmd_of = [](const std::vector<std::string>& files) {
+    std::string d = fs::make_temp_dir("gen-");
+    for (auto& f : files) fs::write_file(fs::join(d, f), "print(1)\n");
+    generator::ChartGenerator(d).create_chart("python", false);
+    std::string df = fs::read_file(fs::join(d, "Dockerfile"));
+    fs::remove_all(d);
+    return df.substr(df.find("CMD"));
+  };
+  EXPECT_EQ(cmd_of({"main.py", "app.py"}), std::string("CMD [\"python\", \"main.py\"]\n"));
+  EXPECT_EQ(cmd_of({"util.py", "app.py"}), std::string("CMD [\"python\", \"app.py\"]\n"));
+  EXPECT_EQ(cmd_of({"hello.py"}), std::string("CMD [\"python\", \"hello.py\"]\n"));
+  EXPECT_EQ(cmd_of({"a.py", "b.py"}), std::string("CMD [\"python\", \"main.py\"]\n"));
+}
+
 TEST(configure_mutations) {
   std::string d = fs::make_temp_dir("cfg-");
   std::string old = fs::cwd();
