@@ -194,7 +194,11 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         _log(f"dev: pod {pod_name} synced after {deploy_s:.2f}s")
         _, _, idx = tail.wait_for(r"Attached to container", start_index=idx, timeout=120)
         _wait_file_contains(root + ".log", "[devspace-runner] started gen=", timeout=900, interval=0.05)
-        _log("runner up")
+        m = re.search(r"\[devspace-runner\] started gen=\d+ .*?world=(\d+) device=(\S+)", open(root + ".log").read())
+        pod_world = int(m.group(1)) if m else 0
+        _log(f"runner up: {pod_world} rank(s), rank 0 on {m.group(2) if m else '?'}")
+        if pod_world != nproc:
+            raise RuntimeError(f"the pod runs {pod_world} training rank(s), expected {nproc}")
         mode = os.environ.get("DEVSPACE_SYNC_MODE") or (
             "helper" if os.path.exists(os.path.join(ROOT, "bin", "devspace-helper")) else "fast")
         pod_file = os.path.join(root, "app", "train.py")
@@ -454,7 +458,8 @@ def main():
     nproc = max(args.gpus, world)
     gpus = nproc if cuda else 0
     if not cuda:
-        nproc = 1
+        # CPU rehearsal of the N>1 shape: the pod runs one gloo rank per bench rank
+        nproc = world
     workdir = tempfile.mkdtemp(prefix="devspace-bench-")
     tls = args.transport == "tls"
     result, ref, deploy, qs, qs_compat = {}, None, None, None, None

@@ -253,9 +253,6 @@ def worker_main(args) -> int:
         import torch.distributed as dist  # noqa: WPS433
 
         backend = "nccl" if device.type == "cuda" else "gloo"  # nccl == RCCL on ROCm
-        # DEVSPACE_DIST_BACKEND=gloo: rehearse the N-rank pod on fewer GPUs than ranks (RCCL
-        # refuses two ranks on one device); the collectives then stage through host memory.
-        backend = os.environ.get("DEVSPACE_DIST_BACKEND") or backend
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     if device.type == "cuda" and args.gemm_tuning != "off":
         try:

@@ -52,6 +52,8 @@ def test_bench_torchrun_two_ranks_cpu():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["steps"] == 2 and d["value"] > 0
+    # the pod ran one training rank per bench rank (the runner's N-rank generation agreement)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
 
 
 @pytest.mark.gpu
