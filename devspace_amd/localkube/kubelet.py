@@ -134,6 +134,7 @@ class Kubelet:
         self.pods_dir = os.path.join(state_dir, "pods")
         os.makedirs(self.pods_dir, exist_ok=True)
         self._stop = False
+        self._event_names = {}  # (ns, uid, reason, message, type) -> Event name, for aggregation
 
     # ------------------------------------------------------------ node
 
@@ -177,7 +178,19 @@ class Kubelet:
     def event(self, obj, reason, message, etype="Normal"):
         md = obj["metadata"]
         ns = md.get("namespace", "default")
+        # Repeats of one event (same object, reason, message, type) bump count/lastTimestamp of
+        # the existing Event, as client-go's EventCorrelator does, instead of adding objects.
+        key = (ns, md.get("uid") or md["name"], reason, message, etype)
+        seen = self._event_names.get(key)
+        if seen is not None:
+            def bump(ev):
+                ev["count"] = int(ev.get("count") or 1) + 1
+                ev["lastTimestamp"] = now_rfc3339()
+
+            if self.store.mutate("", "events", ns, seen, bump) is not None:
+                return
         name = f"{md['name']}.{int(time.time() * 1e6):x}"
+        self._event_names[key] = name
         ev = {
             "apiVersion": "v1",
             "kind": "Event",
@@ -382,7 +395,7 @@ class Kubelet:
         want = sum(_gpu_request(c) for c in containers)
         if want > len(self.gpus_free):
             st = pod.get("status") or {}
-            if st.get("reason") != "Unschedulable":
+            if not any(c.get("reason") == "Unschedulable" for c in st.get("conditions") or []):
                 msg = f"0/1 nodes are available: 1 Insufficient {GPU_RESOURCE}."
                 self.store.update_status("", "pods", md["namespace"], md["name"], {
                     "phase": "Pending", "conditions": [{"type": "PodScheduled", "status": "False",

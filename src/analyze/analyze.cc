@@ -33,19 +33,40 @@ static std::string human_age(int64_t secs) {
 static bool is_okay(const std::string& s) { return s == "Completed" || s == "Running"; }
 
 std::vector<std::string> events_problems(kube::Client& k, const std::string& ns) {
-  std::vector<std::string> out;
+  // events.go:20-55: every non-Normal event whose involved object still exists. One GET per
+  // involved object (not per event), and events repeating the same message for the same
+  // object are reported once with their counts summed (a correlator that did not aggregate
+  // them would otherwise flood the report).
   Value evs = k.get("/api/v1/namespaces/" + ns + "/events");
+  std::map<std::string, bool> exists;
+  std::vector<std::pair<std::string, int64_t>> order;  // (header + message) -> count
+  std::map<std::string, size_t> index;
   for (auto& e : evs.get("items").items()) {
     if (e.get("type").as_string() == "Normal") continue;
     const Value& io = e.get("involvedObject");
     std::string av = io.get("apiVersion").as_string("v1");
     std::string path = kube::resource_path(av, io.get("kind").as_string(), ns, io.get("name").as_string());
-    if (!k.try_get(path)) continue;  // only objects that still exist
+    auto it = exists.find(path);
+    if (it == exists.end()) it = exists.emplace(path, (bool)k.try_get(path)).first;
+    if (!it->second) continue;  // only objects that still exist
     std::string header = log::color(e.get("type").as_string() + " - " + io.get("kind").as_string() + " " +
                                         io.get("name").as_string() + ": ",
                                     "202+b");
-    out.push_back(kPad + header + "\n" + kPad + std::to_string(e.get("count").as_int(1)) + "x " +
-                  e.get("message").as_string() + " \n");
+    std::string key = header + "\n" + e.get("message").as_string();
+    int64_t n = e.get("count").as_int(1);
+    auto at = index.find(key);
+    if (at != index.end()) {
+      order[at->second].second += n;
+      continue;
+    }
+    index[key] = order.size();
+    order.push_back({key, n});
+  }
+  std::vector<std::string> out;
+  for (auto& kv : order) {
+    size_t nl = kv.first.find('\n');
+    out.push_back(kPad + kv.first.substr(0, nl) + "\n" + kPad + std::to_string(kv.second) + "x " +
+                  kv.first.substr(nl + 1) + " \n");
   }
   return out;
 }

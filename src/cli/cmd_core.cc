@@ -87,7 +87,12 @@ void pipeline(Session& s, bool is_dev, bool force_build, bool force_deploy, cons
   bo.force_rebuild = force_build;
   bo.docker_target = docker_target;
   bo.interrupted = [] { return interrupted().load(); };
+  // a kaniko build polls the flag and deletes its build pod when interrupted
+  std::unique_ptr<GracefulInterrupt> kaniko_cleanup;
+  for (auto& kv : s.cfg().get("images").entries())
+    if (!kv.second.at_path("build.kaniko").is_null()) kaniko_cleanup.reset(new GracefulInterrupt());
   bool rebuilt = build::build_all(s.cfg(), gen, s.kube, bo);
+  kaniko_cleanup.reset();
   if (rebuilt) s.ctx.save_generated();
   if (s.cfg().get("deployments").size() > 0 || !is_dev) {
     deploy::deploy_all(s.cfg(), gen, s.kube, is_dev, rebuilt || force_deploy);
@@ -158,6 +163,7 @@ services::SyncOptions dev_sync_options(bool verbose) {
 }
 
 int run_dev(cli::Command& c, const std::vector<std::string>& args) {
+  GracefulInterrupt graceful;
   Session s;
   open_project(s, c);
   cloud_configure(s.ctx);
@@ -254,6 +260,7 @@ int run_dev(cli::Command& c, const std::vector<std::string>& args) {
 }
 
 int run_enter(cli::Command& c, const std::vector<std::string>& args) {
+  GracefulInterrupt graceful;
   Session s;
   open_project(s, c);
   cloud_configure(s.ctx);
@@ -268,6 +275,7 @@ int run_enter(cli::Command& c, const std::vector<std::string>& args) {
 }
 
 int run_logs(cli::Command& c, const std::vector<std::string>&) {
+  GracefulInterrupt graceful;
   Session s;
   apply_config_flag(s.ctx, c);
   if (!config::set_devspace_root()) log::fatal("Couldn't find any devspace configuration. Please run `devspace init`");

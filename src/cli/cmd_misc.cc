@@ -200,6 +200,7 @@ int run_login(cli::Command& c, const Args&) {
 // Standalone sync (hidden): local dir <-> container path of one pod (or the newest running
 // pod of a label selector). Runs until interrupted or --once finishes the initial sync.
 int run_sync(cli::Command& c, const Args&) {
+  GracefulInterrupt graceful;
   Session s;
   bool have_root = config::set_devspace_root();
   Value cfg = Value::map();
@@ -253,6 +254,7 @@ int run_sync(cli::Command& c, const Args&) {
 
 // Starts the bundled local cluster in the foreground (python3 -m devspace_amd.localkube up).
 int run_local_cluster(cli::Command& c, const Args&) {
+  GracefulInterrupt graceful;
   std::string root = fs::dirname(fs::dirname(self_exe()));  // <repo>/bin/devspace -> <repo>
   std::vector<std::string> argv = {"python3", "-m", "devspace_amd.localkube", "up", "--state", c.get_str("state")};
   if (c.get_int("port")) argv.insert(argv.end(), {"--port", std::to_string(c.get_int("port"))});

@@ -18,10 +18,23 @@ std::atomic<bool>& interrupted() {
   return f;
 }
 
+static std::atomic<int> g_graceful{0};
+
+GracefulInterrupt::GracefulInterrupt() { g_graceful.fetch_add(1); }
+GracefulInterrupt::~GracefulInterrupt() { g_graceful.fetch_sub(1); }
+
 void install_signal_handlers() {
   signal(SIGPIPE, SIG_IGN);
   struct sigaction sa{};
-  sa.sa_handler = [](int) { interrupted() = true; };
+  sa.sa_handler = [](int sig) {
+    // async-signal-safe: atomics, write(2), _exit(2)
+    bool again = interrupted().exchange(true);
+    if (g_graceful.load() == 0 || again) {
+      const char nl = '\n';
+      (void)!::write(2, &nl, 1);
+      ::_exit(128 + sig);
+    }
+  };
   sigemptyset(&sa.sa_mask);
   sigaction(SIGINT, &sa, nullptr);
   sigaction(SIGTERM, &sa, nullptr);

@@ -16,9 +16,18 @@ namespace cmd {
 
 extern const char* const kVersion;
 
-// Process-wide interrupt flag (Ctrl-C / SIGTERM).
+// Process-wide interrupt flag (Ctrl-C / SIGTERM). Outside a GracefulInterrupt scope a signal
+// ends the process right away (exit 128+signal), like a Go binary without a handler; inside
+// one (dev loop, logs -f, enter, sync, kaniko build wait) the first signal only sets the flag
+// so the command can clean up, and a second one ends the process.
 std::atomic<bool>& interrupted();
 void install_signal_handlers();
+struct GracefulInterrupt {
+  GracefulInterrupt();
+  ~GracefulInterrupt();
+  GracefulInterrupt(const GracefulInterrupt&) = delete;
+  GracefulInterrupt& operator=(const GracefulInterrupt&) = delete;
+};
 
 // Finds the project root (SetDevSpaceRoot) or fails with the reference's message.
 void require_devspace_root();

@@ -139,7 +139,7 @@ class HelmDeployer : public Deployer {
     log::start_wait("Deploying helm chart");
     Value values = helm_values(cfg_, d_, gen, is_dev);
     bool wait = d_.at_path("helm.wait").as_bool(true);
-    int timeout = (int)d_.at_path("helm.timeout").as_int(180);
+    int timeout = (int)d_.at_path("helm.timeout").as_int(0);  // 0: helm::Client's default
     helm::Release r;
     try {
       r = hc.install_or_upgrade(name, ns, chart, values, wait, timeout);

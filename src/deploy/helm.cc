@@ -1023,7 +1023,7 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
   validate_values(chart, merged);  // values.schema.json, as `helm install` does before rendering
   Rendered rd = render_release(chart, merged, ro);
   std::vector<Value>& objs = rd.objs;
-  k_->check_gpu_requests(objs);
+  std::string gpu_issue = k_->check_gpu_requests(objs);
   for (auto& o : objs) {
     o["metadata"]["labels"]["app.kubernetes.io/managed-by"] = o.at_path("metadata.labels").get("app.kubernetes.io/managed-by").is_null()
                                                                   ? Value("Helm")
@@ -1063,7 +1063,12 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
     }
     if (wait) {
       trace::Span wspan("deploy.helm_wait", {{"release", name}});
-      err = wait_ready(objs, ns, timeout_s > 0 ? timeout_s : 40);
+      // install.go:28 DeploymentTimeout (40 s) unless the chart sets one; GPU workloads get
+      // 300 s (rocm/pytorch images are tens of GB to pull). A GPU request that no node can
+      // satisfy (check_gpu_requests) is not waited out: the analyze report follows at once.
+      int wait_s = timeout_s > 0 ? timeout_s : (kube::Client::max_gpu_request(objs) > 0 ? 300 : 40);
+      if (!gpu_issue.empty()) wait_s = std::min(wait_s, 5);
+      err = wait_ready(objs, ns, wait_s);
     }
     // install.go:181 analyzeError: a wait timeout is explained by an analyze report of the
     // namespace; no problems found means the release is fine (just slow).

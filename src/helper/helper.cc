@@ -327,7 +327,7 @@ int main(int argc, char** argv) {
   g_dest = fs::clean(argv[2]);
   fs::mkdirs(g_dest);
   reply("HELPER READY\n");
-  std::thread watcher;
+  bool watching = false;
   while (true) {
     unsigned char hdr[5];
     if (!read_exact(0, hdr, 5)) break;
@@ -366,9 +366,11 @@ int main(int argc, char** argv) {
         break;
       }
       case 'W':
-        if (!watcher.joinable()) {
-          watcher = std::thread(watch_loop);
-          watcher.detach();
+        // one watch loop per helper process (a detached thread is never joinable again, so
+        // joinable() cannot be the guard); it ends with the process
+        if (!watching) {
+          watching = true;
+          std::thread(watch_loop).detach();
         }
         break;
       case 'Q': return 0;

@@ -581,6 +581,15 @@ static int64_t pod_gpu_request(const Value& pod_spec) {
   return n;
 }
 
+int64_t Client::max_gpu_request(const std::vector<Value>& objs) {
+  int64_t want = 0;
+  for (auto& o : objs) {
+    const Value& spec = o.get("kind").as_string() == "Pod" ? o.get("spec") : o.at_path("spec.template.spec");
+    if (spec.is_map()) want = std::max(want, pod_gpu_request(spec));
+  }
+  return want;
+}
+
 std::string Client::check_gpu_requests(const std::vector<Value>& objs) {
   int64_t want = 0;
   std::string who;

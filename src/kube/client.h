@@ -113,6 +113,8 @@ class Client {
   // allocatable (AMD device plugin); warns before deploying something unschedulable.
   // Returns the warning text ("" when fine).
   std::string check_gpu_requests(const std::vector<Value>& objs);
+  // Largest per-pod amd.com/gpu request among workload manifests (0 = no GPU workload).
+  static int64_t max_gpu_request(const std::vector<Value>& objs);
 
   // Server-side apply (PATCH application/apply-patch+yaml, fieldManager=devspace, force):
   // fields set by other managers (the PV binder's spec.volumeName, a Service's clusterIP,
