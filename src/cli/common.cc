@@ -7,6 +7,7 @@
 #include "cloud/cloud.h"
 #include "core/fs.h"
 #include "core/log.h"
+#include "core/prompt.h"
 
 namespace ds {
 namespace cmd {
@@ -30,6 +31,7 @@ void install_signal_handlers() {
     // async-signal-safe: atomics, write(2), _exit(2)
     bool again = interrupted().exchange(true);
     if (g_graceful.load() == 0 || again) {
+      prompt::restore_cooked_tty_from_signal();
       const char nl = '\n';
       (void)!::write(2, &nl, 1);
       ::_exit(128 + sig);

@@ -4,6 +4,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <atomic>
 #include <deque>
 #include <iostream>
 #include <mutex>
@@ -142,6 +143,20 @@ std::string select(const std::string& question, const std::vector<std::string>& 
   p.options = options;
   p.default_value = def;
   return ask(p);
+}
+
+static struct termios g_cooked{};
+static std::atomic<bool> g_cooked_set{false};
+
+void remember_cooked_tty(const struct termios& saved) {
+  g_cooked = saved;
+  g_cooked_set = true;
+}
+
+void forget_cooked_tty() { g_cooked_set = false; }
+
+void restore_cooked_tty_from_signal() {
+  if (g_cooked_set.load()) tcsetattr(0, TCSANOW, &g_cooked);
 }
 
 }  // namespace prompt

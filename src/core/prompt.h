@@ -3,6 +3,8 @@
 // answer, or the next line from stdin when one is piped in; a prompt with neither fails.
 #pragma once
 
+#include <termios.h>
+
 #include <functional>
 #include <stdexcept>
 #include <string>
@@ -33,6 +35,12 @@ std::string select(const std::string& question, const std::vector<std::string>& 
 bool interactive();
 // Test hook: answers consumed in order instead of reading stdin.
 void set_scripted_answers(const std::vector<std::string>& answers);
+
+// Terminal mode saved by whoever puts stdin into raw mode, so a signal handler that ends the
+// process can put the user's terminal back (tcsetattr is async-signal-safe).
+void remember_cooked_tty(const struct termios& saved);
+void forget_cooked_tty();
+void restore_cooked_tty_from_signal();
 
 }  // namespace prompt
 }  // namespace ds

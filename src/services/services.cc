@@ -367,11 +367,14 @@ struct RawTty {
     if (tcgetattr(0, &saved) != 0) return;
     struct termios raw = saved;
     cfmakeraw(&raw);
+    prompt::remember_cooked_tty(saved);
     tcsetattr(0, TCSANOW, &raw);
     active = true;
   }
   ~RawTty() {
-    if (active) tcsetattr(0, TCSANOW, &saved);
+    if (!active) return;
+    tcsetattr(0, TCSANOW, &saved);
+    prompt::forget_cooked_tty();
   }
 };
 

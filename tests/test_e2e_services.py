@@ -113,6 +113,38 @@ def test_enter_interactive_pty(localkube):
     lk.run(["purge"], proj)
 
 
+def test_enter_restores_terminal_when_signalled(localkube):
+    """Two SIGTERMs end `enter` at once (the second one exits from the signal handler): the
+    terminal it had put into raw mode is cooked again either way."""
+    import termios
+
+    lk = localkube
+    proj = lk.project("quickstart", "quickstart-tty-sig")
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    cfg["cluster"]["namespace"] = "tty-sig"
+    open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    lk.run(["deploy"], proj)
+    wait_for(lambda: running(lk.pods("tty-sig")), what="pod")
+    master, slave = pty.openpty()
+    assert termios.tcgetattr(slave)[3] & termios.ICANON
+    p = subprocess.Popen([lk.bin, "enter"], cwd=proj, env=lk.env, stdin=slave, stdout=slave, stderr=slave,
+                         start_new_session=True)
+    try:
+        wait_for(lambda: not (termios.tcgetattr(slave)[3] & termios.ICANON), what="raw mode")
+        os.kill(p.pid, signal.SIGTERM)
+        os.kill(p.pid, signal.SIGTERM)
+        p.wait(10)
+        lflag = termios.tcgetattr(slave)[3]
+        assert lflag & termios.ICANON and lflag & termios.ECHO, lflag
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGKILL)
+        os.close(master)
+        os.close(slave)
+    lk.run(["purge"], proj)
+
+
 def test_logs_follow_streams_new_lines(localkube):
     lk = localkube
     proj = lk.project("quickstart", "quickstart-logs")
