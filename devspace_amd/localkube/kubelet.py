@@ -135,6 +135,7 @@ class Kubelet:
         os.makedirs(self.pods_dir, exist_ok=True)
         self._stop = False
         self._event_names = {}  # (ns, uid, reason, message, type) -> Event name, for aggregation
+        self._exited_procs = []
 
     # ------------------------------------------------------------ node
 
@@ -560,6 +561,10 @@ class Kubelet:
                 code = c.proc.returncode
                 c.last_state = {"terminated": {"exitCode": code, "reason": "Completed" if code == 0 else "Error",
                                                "startedAt": c.started_at, "finishedAt": now_rfc3339()}}
+                # its pipes may outlive it (grandchildren keep them open): closed at shutdown
+                self._exited_procs = [p for p in self._exited_procs
+                                      if getattr(p, "_transport", None) and not p._transport.is_closing()]
+                self._exited_procs.append(c.proc)
                 c.proc = None
                 policy = pod.get("spec", {}).get("restartPolicy", "Always")
                 if policy == "Never" or (policy == "OnFailure" and code == 0):
@@ -708,3 +713,6 @@ class Kubelet:
         self._stop = True
         for key in list(self.pods):
             await self._kill_pod(self.pods.pop(key), 1)
+        for proc in self._exited_procs:
+            close_proc(proc)
+        self._exited_procs.clear()
