@@ -152,6 +152,60 @@ class Context:
             time.sleep(0)  # releases the GIL: the change feed thread can post the edit
 
 
+def _user_modules(watch_dir: str) -> dict:
+    """{module name: (source path, mtime_ns)} of the modules imported from the synced tree
+    (helpers the entry file imports); packages installed in the image, compiled extensions and
+    this runner itself are not included."""
+    root = os.path.realpath(watch_dir) + os.sep
+    me = os.path.realpath(__file__)
+    out = {}
+    for name, m in list(sys.modules.items()):
+        f = getattr(m, "__file__", None)
+        if not f or name == "__main__" or not f.endswith(".py"):
+            continue
+        rf = os.path.realpath(f)
+        if not rf.startswith(root) or rf == me or os.sep + "site-packages" + os.sep in rf:
+            continue
+        try:
+            out[name] = (rf, os.stat(rf).st_mtime_ns)
+        except OSError:
+            out[name] = (rf, None)
+    return out
+
+
+class ModuleTracker:
+    """Makes edits of imported helper modules take effect at a reload: when any module imported
+    from the synced tree changed on disk since it was imported, all of them are dropped from
+    sys.modules (a module that did `from helper import f` must re-import too), so the next exec
+    of the entry file imports the edited code. Unchanged helpers stay cached (no re-import cost
+    when only the entry file was edited)."""
+
+    def __init__(self, watch_dir: str):
+        self.watch_dir = watch_dir
+        self.seen = _user_modules(watch_dir)
+
+    def refresh(self) -> list:
+        cur = _user_modules(self.watch_dir)
+        changed = False
+        for name, (path, _) in cur.items():
+            try:
+                now = os.stat(path).st_mtime_ns
+            except OSError:
+                now = None
+            if self.seen.get(name, (path, now))[1] != now:
+                changed = True
+                break
+        if not changed:
+            return []
+        for name in cur:
+            sys.modules.pop(name, None)
+        importlib.invalidate_caches()
+        return sorted(cur)
+
+    def snapshot(self):
+        self.seen = _user_modules(self.watch_dir)
+
+
 def load_module(path: str, generation: int, feed=None) -> types.ModuleType:
     """Compile the user file into a fresh module object (no import cache involved). When the
     change feed already compiled exactly these bytes in the background, that code is used."""
@@ -266,12 +320,15 @@ def worker_main(args) -> int:
     ctx = Context(rank, world, local_rank, device)
     entry = os.path.abspath(args.entry)
     watch_dir = os.path.abspath(args.watch or os.path.dirname(entry))
+    if os.path.dirname(entry) not in sys.path:  # `import helper` next to the entry file, as `python train.py`
+        sys.path.insert(0, os.path.dirname(entry))
     watcher = make_watcher(watch_dir)
     feed = ChangeFeed(watcher, entry)
 
     gen = 1
     t_start = time.perf_counter()
     mod = load_module(entry, gen)
+    tracker = ModuleTracker(watch_dir)
     ctx.generation = gen
     state = mod.setup(ctx) if hasattr(mod, "setup") else None
     setup_version = getattr(mod, "SETUP_VERSION", None)
@@ -329,7 +386,9 @@ def worker_main(args) -> int:
             t_reload = time.perf_counter()
             wait_ms = (t_reload - reload_t0) * 1000.0 if reload_t0 else 0.0
             try:
+                tracker.refresh()
                 new_mod = load_module(entry, target, feed)
+                tracker.snapshot()
                 new_setup_version = getattr(new_mod, "SETUP_VERSION", None)
                 if hasattr(new_mod, "setup") and (state is None or new_setup_version != setup_version):
                     state = new_mod.setup(ctx)

@@ -268,3 +268,59 @@ def test_vendored_runner_copies_match_the_package():
     for copy in (os.path.join(ROOT, "templates", "rocm-pytorch", "devspace_runner.py"),
                  os.path.join(ROOT, "examples", "rocm-pytorch", "devspace_runner.py")):
         assert open(copy).read() == src, f"{copy} is out of date: cp devspace_amd/runner.py {copy}"
+
+
+HELPER_ENTRY = '''
+import helper_mod
+MARKER = helper_mod.MARKER
+
+
+def setup(ctx):
+    return {}
+
+
+def step(ctx, state):
+    import time
+    time.sleep(0.01)
+    return {"loss": helper_mod.value()}
+'''
+
+
+def test_runner_reloads_edited_helper_module(tmp_path):
+    """An edit of a module the entry file imports (not only of the entry file) takes effect at
+    the next reload: the runner drops the synced tree's modules from the import cache."""
+    (tmp_path / "helper_mod.py").write_text('MARKER = "v0"\n\n\ndef value():\n    return 1\n')
+    entry = tmp_path / "train.py"
+    entry.write_text(HELPER_ENTRY)
+    env = dict(os.environ, PYTHONPATH=ROOT, HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1")
+    proc = subprocess.Popen([sys.executable, "-u", "-m", "devspace_amd.runner", "--watch", str(tmp_path), str(entry)],
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, text=True, cwd=str(tmp_path))
+    import queue
+    import threading
+
+    lines, q = [], queue.Queue()
+    threading.Thread(target=lambda: [q.put(l) for l in proc.stdout], daemon=True).start()
+
+    def until(pat, timeout=60):
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            try:
+                line = q.get(timeout=max(0.01, deadline - time.time()))
+            except queue.Empty:
+                break
+            lines.append(line)
+            if re.search(pat, line):
+                return line
+        raise AssertionError(f"no line matching {pat!r}:\n" + "".join(lines[-20:]))
+
+    try:
+        until(r"started gen=1 marker=v0")
+        (tmp_path / "helper_mod.py").write_text('MARKER = "v1"\n\n\ndef value():\n    return 2\n')
+        line = until(r"reloaded gen=\d+ marker=v1")
+        assert "loss=2" in line, line
+        # an edit of the entry file alone keeps the (unchanged) helper cached and still reloads
+        entry.write_text(HELPER_ENTRY.replace("MARKER = helper_mod.MARKER", 'MARKER = "entry-" + helper_mod.MARKER'))
+        until(r"reloaded gen=\d+ marker=entry-v1")
+    finally:
+        proc.terminate()
+        proc.wait(10)
