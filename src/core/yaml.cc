@@ -873,7 +873,9 @@ void emit(const Value& v, int indent, std::string& out) {
 }  // namespace
 
 std::vector<Value> yaml_parse_all(const std::string& text) {
-  Parser p(text);
+  // a UTF-8 byte order mark (Windows editors) is not content, as in go-yaml's reader
+  static const std::string kBom = "\xEF\xBB\xBF";
+  Parser p(text.compare(0, kBom.size(), kBom) == 0 ? text.substr(kBom.size()) : text);
   return p.parse_all();
 }
 

@@ -40,6 +40,12 @@ TEST(yaml_basic_map_and_seq) {
   EXPECT_TRUE(pm.get("localPort").is_int());
 }
 
+TEST(yaml_bom_and_crlf) {
+  Value v = yaml_parse("\xEF\xBB\xBFversion: v1alpha2\r\nimages:\r\n  default:\r\n    image: x\r\n");
+  EXPECT_EQ(v.get("version").as_string(), std::string("v1alpha2"));
+  EXPECT_EQ(v.at_path("images.default.image").as_string(), std::string("x"));
+}
+
 TEST(yaml_scalars_and_quotes) {
   Value v = yaml_parse(
       "a: \"123\"\n"
