@@ -263,6 +263,16 @@ class Parser {
       return parse_inline(acc, parent_indent);
     }
     Value v = parse_inline(t, parent_indent);
+    if (v.is_string() && !v.quoted() && c0 != '|' && c0 != '>' && c0 != '&' && c0 != '*' && c0 != '!') {
+      // "key: a: b" — a plain scalar cannot hold ": " (or end in ':'); go-yaml reports it
+      // rather than reading a typo as a string
+      std::string body = strip_comment(t);
+      if (body.find(": ") != std::string::npos || body.find(":\t") != std::string::npos ||
+          (!body.empty() && body.back() == ':')) {
+        int ln = pos_ > 0 && pos_ - 1 < lines_.size() ? lines_[pos_ - 1].lineno : (int)lines_.size();
+        throw ParseError("yaml: line " + std::to_string(ln) + ": mapping values are not allowed in this context");
+      }
+    }
     if (v.is_string() && !v.quoted() && c0 != '|' && c0 != '>') {
       // plain multi-line continuation
       std::string acc = v.str();

@@ -46,6 +46,22 @@ TEST(yaml_bom_and_crlf) {
   EXPECT_EQ(v.at_path("images.default.image").as_string(), std::string("x"));
 }
 
+TEST(yaml_colon_space_in_plain_value_is_an_error) {
+  for (const char* bad : {"a: b: c\n", "a: b:\n", "- a: b\n- c: d: e\n"}) {
+    bool threw = false;
+    try {
+      yaml_parse(bad);
+    } catch (const std::exception& e) {
+      threw = contains(e.what(), "mapping values are not allowed");
+    }
+    EXPECT_TRUE(threw);
+  }
+  EXPECT_EQ(yaml_parse("a: http://x:80/y\n").get("a").as_string(), std::string("http://x:80/y"));
+  EXPECT_EQ(yaml_parse("a: b # c: d\n").get("a").as_string(), std::string("b"));
+  EXPECT_EQ(yaml_parse("a: \"b: c\"\n").get("a").as_string(), std::string("b: c"));
+  EXPECT_EQ(yaml_parse("a: b:c\n").get("a").as_string(), std::string("b:c"));
+}
+
 TEST(yaml_scalars_and_quotes) {
   Value v = yaml_parse(
       "a: \"123\"\n"
