@@ -315,3 +315,53 @@ TEST(fs_paths) {
   EXPECT_EQ(fs::relative("/a/b", "/a/b/c/d"), std::string("c/d"));
   EXPECT_EQ(fs::join("a/", "/b"), std::string("a/b"));
 }
+
+// Mutation fuzz of the YAML reader/writer: every mutated document parses or throws a
+// std::exception, and what parses dumps to YAML that reads back to the same value.
+TEST(yaml_mutation_fuzz_roundtrip) {
+  const std::vector<std::string> seeds = {
+      "version: v1alpha2\nimages:\n  default:\n    image: reg/app\n    build:\n      kaniko:\n        cache: true\n"
+      "dev:\n  sync:\n  - containerPath: /app\n    excludePaths: [node_modules/, '*.pyc']\n  ports:\n"
+      "  - portMappings:\n    - {localPort: 3000, remotePort: 3000}\n",
+      "a: |\n  line one\n  line two\nb: >-\n  folded\n  text\nc: &anc {x: 1, y: [1, 2]}\nd: *anc\ne: \"q\\\"s\"\n"
+      "f: 'it''s'\ng: ~\nh: 0x1F\ni: -1.5e3\n---\n- x\n- - nested\n  - seq\n- k: v\n  k2: v2\n"};
+  const std::string alphabet = " \n\t:-[]{},#&*!|>'\"%@?ab01.";
+  uint64_t rng = 0xD1B54A32D192ED03ull;
+  auto next = [&rng] {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return rng;
+  };
+  int ok = 0;
+  for (int it = 0; it < 20000; ++it) {
+    std::string t = seeds[next() % seeds.size()];
+    int nmut = 1 + (int)(next() % 4);
+    for (int m = 0; m < nmut && !t.empty(); ++m) {
+      size_t i = next() % t.size();
+      switch (next() % 3) {
+        case 0: t[i] = alphabet[next() % alphabet.size()]; break;
+        case 1: t.erase(i, 1 + next() % 6); break;
+        default: t.insert(i, 1, alphabet[next() % alphabet.size()]);
+      }
+    }
+    std::vector<Value> docs;
+    try {
+      docs = yaml_parse_all(t);
+    } catch (const std::exception&) {
+      continue;
+    }
+    ++ok;
+    for (auto& d : docs) {
+      std::string out = yaml_dump(d);
+      Value back = yaml_parse(out);
+      if (!(back == d)) {
+        std::fprintf(stderr, "roundtrip mismatch for:\n%s\n--- dumped:\n%s\n", t.c_str(), out.c_str());
+        EXPECT_TRUE(false);
+        return;
+      }
+    }
+  }
+  EXPECT_TRUE(ok > 1000);
+}
+

@@ -244,3 +244,53 @@ TEST(helmrepo_versions_and_search) {
   fs::remove_all(home);
   fs::remove_all(repo);
 }
+
+// Mutation fuzz of the template engine over the embedded component chart: every mutated
+// template either renders or throws a std::exception (parse/exec error) — no crash, hang or
+// other exception type. Under scripts/sanitize.sh this also checks memory safety.
+TEST(gotemplate_mutation_fuzz_never_crashes) {
+  const auto& emb = generator::embedded_templates();
+  std::string helpers = emb.at("_base/chart/templates/_helpers.tpl");
+  Value values = yaml_parse(emb.at("_base/chart/values.yaml"));
+  Value data = Value::map();
+  data["Values"] = values;
+  data["Release"]["Name"] = "rel";
+  data["Release"]["Namespace"] = "ns";
+  data["Chart"]["Name"] = "chart";
+  std::vector<std::string> seeds;
+  for (auto& kv : emb)
+    if (starts_with(kv.first, "_base/chart/templates/") && ends_with(kv.first, ".yaml")) seeds.push_back(kv.second);
+  EXPECT_TRUE(seeds.size() >= 3);
+  const std::string alphabet = "{}|$.()\"- :=,_abeinrtV0123\n";
+  uint64_t rng = 0x9E3779B97F4A7C15ull;
+  auto next = [&rng] {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return rng;
+  };
+  int rendered = 0, errors = 0;
+  for (int it = 0; it < 4000; ++it) {
+    std::string t = seeds[next() % seeds.size()];
+    int nmut = 1 + (int)(next() % 3);
+    for (int m = 0; m < nmut && !t.empty(); ++m) {
+      size_t i = next() % t.size();
+      switch (next() % 3) {
+        case 0: t[i] = alphabet[next() % alphabet.size()]; break;
+        case 1: t.erase(i, 1 + next() % 4); break;
+        default: t.insert(i, 1, alphabet[next() % alphabet.size()]);
+      }
+    }
+    try {
+      tmpl::Engine e;
+      e.add("_helpers.tpl", helpers);
+      e.add("t", t);
+      e.execute("t", data);
+      ++rendered;
+    } catch (const std::exception&) {
+      ++errors;
+    }
+  }
+  EXPECT_TRUE(rendered > 100 && errors > 100);
+}
+
