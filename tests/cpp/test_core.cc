@@ -365,3 +365,68 @@ TEST(yaml_mutation_fuzz_roundtrip) {
   EXPECT_TRUE(ok > 1000);
 }
 
+// Archives and JSON arrive from containers and API servers: corrupted tar, gzip and JSON input
+// is rejected with an exception or read partially, never a crash or an unbounded allocation.
+TEST(untrusted_tar_gzip_json_mutation_fuzz) {
+  std::string tar;
+  {
+    TarWriter tw(string_sink(&tar));
+    TarEntry e;
+    e.name = "dir/file.txt";
+    tw.add_file(e, std::string(3000, 'x'));
+    e.name = std::string(150, 'n') + "/long-name-needs-pax.txt";
+    tw.add_file(e, "hello");
+    TarEntry d;
+    d.name = "dir/sub";
+    d.type = '5';
+    tw.add_dir(d);
+    tw.finish();
+  }
+  std::string gz = gzip_compress(tar);
+  std::string js = "{\"kind\":\"Pod\",\"metadata\":{\"name\":\"p\",\"labels\":{\"a\":\"b\"}},"
+                   "\"items\":[1,2.5,-3e2,true,null,\"\\u00e9\\n\"],\"s\":\"x\"}";
+  uint64_t rng = 0x2545F4914F6CDD1Dull;
+  auto next = [&rng] {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return rng;
+  };
+  auto mutate = [&](std::string t) {
+    int n = 1 + (int)(next() % 4);
+    for (int m = 0; m < n && !t.empty(); ++m) {
+      size_t i = next() % t.size();
+      switch (next() % 3) {
+        case 0: t[i] = (char)(next() & 0xff); break;
+        case 1: t.erase(i, 1 + next() % 8); break;
+        default: t.insert(i, 1, (char)(next() & 0xff));
+      }
+    }
+    return t;
+  };
+  for (int it = 0; it < 3000; ++it) {
+    std::string t = mutate(tar);
+    try {
+      TarReader r(string_source(&t));
+      TarEntry e;
+      int entries = 0;
+      while (r.next(&e) && entries++ < 100) {
+        std::string body = r.read_all();
+        EXPECT_TRUE((int64_t)body.size() <= (int64_t)t.size());
+      }
+    } catch (const std::exception&) {
+    }
+    std::string g = mutate(gz);
+    try {
+      std::string out = gzip_decompress(g);
+      EXPECT_TRUE(out.size() <= (size_t)64 << 20);
+    } catch (const std::exception&) {
+    }
+    std::string j = mutate(js);
+    try {
+      json_parse(j);
+    } catch (const std::exception&) {
+    }
+  }
+}
+
