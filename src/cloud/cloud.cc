@@ -15,6 +15,7 @@
 #include "core/log.h"
 #include "core/net.h"
 #include "core/proc.h"
+#include "core/prompt.h"
 #include "core/strutil.h"
 #include "kube/kubeconfig.h"
 
@@ -235,7 +236,8 @@ std::string Client::login_via_browser(int timeout_s) {
     int c = ::accept(fd, nullptr, nullptr);
     if (c < 0) continue;
     char buf[8192];
-    ssize_t n = ::recv(c, buf, sizeof(buf) - 1, 0);
+    struct pollfd cp{c, POLLIN, 0};
+    ssize_t n = ::poll(&cp, 1, 2000) > 0 ? ::recv(c, buf, sizeof(buf) - 1, 0) : 0;  // a silent client cannot stall login
     std::string req(buf, n > 0 ? (size_t)n : 0);
     size_t p = req.find("/token?token=");
     if (p != std::string::npos) {
@@ -271,6 +273,11 @@ Provider login(const std::string& name, const std::string& token) {
   auto ps = load_providers();
   auto it = ps.find(name);
   if (it == ps.end()) throw std::runtime_error("Cloud provider " + name + " not found");
+  if (token.empty() && !prompt::interactive())
+    // the browser flow waits for a callback on localhost:25853: nothing will ever call it in
+    // a CI job or a piped session (the reference waits forever there)
+    throw std::runtime_error("Not logged in to " + name + " and this session is not interactive: run `devspace login --provider " +
+                             name + " --token <token>` first");
   it->second.token = token.empty() ? Client(it->second).login_via_browser() : token;
   save_providers(ps);
   // cloud/registry.go:27 LoginIntoRegistries: docker credentials for every provider registry
