@@ -152,58 +152,26 @@ class Context:
             time.sleep(0)  # releases the GIL: the change feed thread can post the edit
 
 
-def _user_modules(watch_dir: str) -> dict:
-    """{module name: (source path, mtime_ns)} of the modules imported from the synced tree
-    (helpers the entry file imports); packages installed in the image, compiled extensions and
-    this runner itself are not included."""
+def purge_user_modules(watch_dir: str) -> list:
+    """Drops the modules imported from the synced tree (helpers the entry file imports) from
+    sys.modules, so the next exec of the entry file imports their edited versions; packages
+    installed in the image, compiled extensions and this runner itself stay. Called only when a
+    helper .py file changed: a plain prefix test first, realpath only for the candidates (the
+    import cache of a torch process holds thousands of modules)."""
+    prefixes = tuple({os.path.abspath(watch_dir) + os.sep, os.path.realpath(watch_dir) + os.sep})
     root = os.path.realpath(watch_dir) + os.sep
     me = os.path.realpath(__file__)
-    out = {}
+    gone = []
     for name, m in list(sys.modules.items()):
         f = getattr(m, "__file__", None)
-        if not f or name == "__main__" or not f.endswith(".py"):
+        if not f or name == "__main__" or not f.endswith(".py") or not f.startswith(prefixes):
             continue
         rf = os.path.realpath(f)
-        if not rf.startswith(root) or rf == me or os.sep + "site-packages" + os.sep in rf:
-            continue
-        try:
-            out[name] = (rf, os.stat(rf).st_mtime_ns)
-        except OSError:
-            out[name] = (rf, None)
-    return out
-
-
-class ModuleTracker:
-    """Makes edits of imported helper modules take effect at a reload: when any module imported
-    from the synced tree changed on disk since it was imported, all of them are dropped from
-    sys.modules (a module that did `from helper import f` must re-import too), so the next exec
-    of the entry file imports the edited code. Unchanged helpers stay cached (no re-import cost
-    when only the entry file was edited)."""
-
-    def __init__(self, watch_dir: str):
-        self.watch_dir = watch_dir
-        self.seen = _user_modules(watch_dir)
-
-    def refresh(self) -> list:
-        cur = _user_modules(self.watch_dir)
-        changed = False
-        for name, (path, _) in cur.items():
-            try:
-                now = os.stat(path).st_mtime_ns
-            except OSError:
-                now = None
-            if self.seen.get(name, (path, now))[1] != now:
-                changed = True
-                break
-        if not changed:
-            return []
-        for name in cur:
-            sys.modules.pop(name, None)
-        importlib.invalidate_caches()
-        return sorted(cur)
-
-    def snapshot(self):
-        self.seen = _user_modules(self.watch_dir)
+        if rf.startswith(root) and rf != me and os.sep + "site-packages" + os.sep not in rf:
+            del sys.modules[name]
+            gone.append(name)
+    importlib.invalidate_caches()
+    return gone
 
 
 def load_module(path: str, generation: int, feed=None) -> types.ModuleType:
@@ -235,6 +203,8 @@ class ChangeFeed:
         self.first_t = None
         self.prepared = None
         self.compiling = None  # source bytes whose background compile is running
+        self.entry_real = os.path.realpath(entry)
+        self.helper_changed = False  # a .py file other than the entry changed since the last take
         self.stop = False
         self.thread = threading.Thread(target=self._run, name="devspace-change-feed", daemon=True)
         self.thread.start()
@@ -252,18 +222,19 @@ class ChangeFeed:
             if not changed:
                 continue
             t = time.perf_counter()
+            helper = any(p.endswith(".py") and os.path.realpath(p) != self.entry_real for p in changed)
             try:
                 with open(self.entry, "rb") as f:
                     src = f.read()
             except OSError:
                 src = None
             if compile_first:
-                self._post(t, src, self._compile(src))
+                self._post(t, src, self._compile(src), helper=helper)
                 continue
             # Post the change first, then compile: a step boundary reached while the compile
             # runs already sees the change (and waits for this compile in prepared_for) instead
             # of starting one more step with the old code.
-            self._post(t, src, None, compiling=src is not None)
+            self._post(t, src, None, compiling=src is not None, helper=helper)
             if src is not None:
                 code = self._compile(src)
                 with self.cv:
@@ -280,9 +251,10 @@ class ChangeFeed:
         except Exception:  # syntax errors surface (with traceback) at the reload itself
             return None
 
-    def _post(self, t, src, code, compiling=False):
+    def _post(self, t, src, code, compiling=False, helper=False):
         with self.cv:
             self.count += 1
+            self.helper_changed = self.helper_changed or helper
             if self.first_t is None:
                 self.first_t = t
             self.prepared = (src, code) if code is not None else None
@@ -294,13 +266,14 @@ class ChangeFeed:
         return self.count > 0
 
     def take(self, timeout_s=0.0):
-        """(number of change batches since the last call, perf_counter of the first one)."""
+        """(number of change batches since the last call, perf_counter of the first one,
+        whether a .py file other than the entry file changed in them)."""
         with self.cv:
             if self.count == 0 and timeout_s > 0:
                 self.cv.wait(timeout_s)
-            n, t = self.count, self.first_t
-            self.count, self.first_t = 0, None
-            return n, t
+            n, t, helper = self.count, self.first_t, self.helper_changed
+            self.count, self.first_t, self.helper_changed = 0, None, False
+            return n, t, helper
 
     def prepared_for(self, src, wait_s=0.05):
         """Code object compiled in the background for exactly these bytes; waits (bounded)
@@ -360,11 +333,12 @@ def worker_main(args) -> int:
     gen = 1
     t_start = time.perf_counter()
     mod = load_module(entry, gen)
-    tracker = ModuleTracker(watch_dir)
     ctx.generation = gen
     state = mod.setup(ctx) if hasattr(mod, "setup") else None
     setup_version = getattr(mod, "SETUP_VERSION", None)
-    ctl = torch.zeros(1, dtype=torch.int64, device=device) if world > 1 else None
+    # [newest generation, helper modules changed]: all-reduced (MAX) every step
+    ctl = torch.zeros(2, dtype=torch.int64, device=device) if world > 1 else None
+    helper_pending = False
     first = {}
     if hasattr(mod, "step"):
         first = mod.step(ctx, state) or {}
@@ -399,28 +373,33 @@ def worker_main(args) -> int:
     while not stop:
         # 1. pick up local change notifications (non-blocking while training; blocking when idle)
         timeout = 0 if (not script_mode and args.train) else 0.05
-        n_changes, t_first = feed.take(timeout)
+        n_changes, t_first, helper_changed = feed.take(timeout)
         # Rank 0's feed alone advances the generation: every rank watches the same synced
         # directory, but their feeds post the edit microseconds apart, and a rank that saw it one
         # step late would otherwise bump the group to a second generation (a spurious reload).
         if n_changes and (ctl is None or rank == 0):
             pending_gen += 1
+            helper_pending = helper_pending or helper_changed
             if reload_t0 is None:
                 reload_t0 = t_first
-        # 2. ranks agree on the newest generation (keeps collectives in `step` matched)
+        # 2. ranks agree on the newest generation (keeps collectives in `step` matched) and on
+        #    whether helper modules must be re-imported (rank 0's view, like the generation)
         target = pending_gen
         if ctl is not None:
-            ctl.fill_(pending_gen)
+            ctl[0] = pending_gen
+            ctl[1] = int(helper_pending)
             dist.all_reduce(ctl, op=dist.ReduceOp.MAX)
-            target = int(ctl.item())
+            target, agreed_helper = (int(v) for v in ctl.tolist())
             pending_gen = max(pending_gen, target)
+            helper_pending = helper_pending or bool(agreed_helper)
         if target > gen:
             t_reload = time.perf_counter()
             wait_ms = (t_reload - reload_t0) * 1000.0 if reload_t0 else 0.0
             try:
-                tracker.refresh()
+                if helper_pending:
+                    purge_user_modules(watch_dir)
+                    helper_pending = False
                 new_mod = load_module(entry, target, feed)
-                tracker.snapshot()
                 new_setup_version = getattr(new_mod, "SETUP_VERSION", None)
                 if hasattr(new_mod, "setup") and (state is None or new_setup_version != setup_version):
                     state = new_mod.setup(ctx)

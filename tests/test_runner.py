@@ -75,6 +75,9 @@ def _run_reload(tmp_path, extra_env=None, nproc=1):
 def test_runner_hot_reload_cpu(tmp_path):
     line = _run_reload(tmp_path, {"HIP_VISIBLE_DEVICES": "-1", "CUDA_VISIBLE_DEVICES": "-1"})
     assert "gen=2" in line
+    # the code swap stays cheap with torch's thousands of modules imported (a per-reload scan of
+    # sys.modules with realpath() once cost ~50 ms here)
+    assert float(re.search(r"reload_ms=([\d.]+)", line).group(1)) < 15, line
 
 
 def test_runner_hot_reload_two_ranks_cpu(tmp_path):
