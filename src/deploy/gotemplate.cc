@@ -14,6 +14,7 @@
 #include "core/codec.h"
 #include "core/match.h"
 #include "core/strutil.h"
+#include "deploy/sprig_crypto.h"
 
 namespace ds {
 namespace tmpl {
@@ -1007,6 +1008,23 @@ struct Engine::Impl {
   }
 
   static std::string strval(const Value& v) { return v.is_null() ? "" : print_value(v); }
+  // "2006-01-02T15:04:05Z07:00" (fractional seconds ignored) -> unix seconds; 0 if unparsable
+  static int64_t parse_rfc3339(const std::string& t) {
+    struct tm tm{};
+    int off_h = 0, off_m = 0;
+    char sign = 0;
+    if (std::sscanf(t.c_str(), "%d-%d-%dT%d:%d:%d", &tm.tm_year, &tm.tm_mon, &tm.tm_mday, &tm.tm_hour, &tm.tm_min,
+                    &tm.tm_sec) != 6)
+      return 0;
+    tm.tm_year -= 1900;
+    tm.tm_mon -= 1;
+    size_t z = t.find_first_of("+-Z", 19);
+    if (z != std::string::npos && t[z] != 'Z' && std::sscanf(t.c_str() + z, "%c%d:%d", &sign, &off_h, &off_m) == 3) {
+      int64_t off = off_h * 3600 + off_m * 60;
+      return (int64_t)timegm(&tm) - (sign == '-' ? -off : off);
+    }
+    return (int64_t)timegm(&tm);
+  }
 
   static std::string indent_str(int n, const std::string& s) {
     std::string pad(n, ' ');
@@ -1390,6 +1408,47 @@ struct Engine::Impl {
       return S(h.substr(0, 8) + "-" + h.substr(8, 4) + "-4" + h.substr(13, 3) + "-a" + h.substr(17, 3) + "-" + h.substr(20, 12));
     }
     if (fn == "randAlphaNum" || fn == "randAlpha") { need(1); return S(random_string((size_t)args[0].as_int())); }
+    // ---- certificates and encryption (sprig crypto.go)
+    auto strings_of = [](const Value& l) {
+      std::vector<std::string> out;
+      for (auto& it : l.items()) out.push_back(strval(it));
+      return out;
+    };
+    if (fn == "genPrivateKey") { need(1); return S(sprig::gen_private_key(args[0].as_string())); }
+    if (fn == "genCA") { need(2); return sprig::gen_ca(strval(args[0]), (int)args[1].as_int()); }
+    if (fn == "genSelfSignedCert") {
+      need(4);
+      return sprig::gen_self_signed_cert(strval(args[0]), strings_of(args[1]), strings_of(args[2]), (int)args[3].as_int());
+    }
+    if (fn == "genSignedCert") {
+      need(5);
+      return sprig::gen_signed_cert(strval(args[0]), strings_of(args[1]), strings_of(args[2]), (int)args[3].as_int(),
+                                    args[4]);
+    }
+    if (fn == "encryptAES") { need(2); return S(sprig::encrypt_aes(strval(args[0]), strval(args[1]))); }
+    if (fn == "decryptAES") { need(2); return S(sprig::decrypt_aes(strval(args[0]), strval(args[1]))); }
+    // ---- durations (sprig date.go): Go's time.Duration.String() of whole seconds
+    auto go_duration = [](int64_t sec) {
+      if (sec == 0) return std::string("0s");
+      std::string sign = sec < 0 ? "-" : "";
+      uint64_t a = (uint64_t)(sec < 0 ? -sec : sec);
+      uint64_t h = a / 3600, m = a % 3600 / 60, x = a % 60;
+      if (h) return sign + std::to_string(h) + "h" + std::to_string(m) + "m" + std::to_string(x) + "s";
+      if (m) return sign + std::to_string(m) + "m" + std::to_string(x) + "s";
+      return sign + std::to_string(x) + "s";
+    };
+    if (fn == "duration") {
+      need(1);
+      int64_t sec = 0;
+      parse_int64(strval(args[0]), &sec);
+      return S(go_duration(sec));
+    }
+    if (fn == "ago") {
+      need(1);
+      int64_t t = 0;
+      if (!parse_int64(strval(args[0]), &t)) t = parse_rfc3339(strval(args[0]));
+      return S(go_duration((int64_t)std::time(nullptr) - t));
+    }
     // ---- wider Sprig set (strings)
     if (fn == "sha1sum") { need(1); return S(digest_hex(EVP_sha1(), strval(args[0]))); }
     if (fn == "adler32sum") {

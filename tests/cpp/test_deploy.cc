@@ -2,6 +2,10 @@
 // detection and config mutations (configure/*).
 #include <algorithm>
 
+#include <openssl/pem.h>
+#include <openssl/x509.h>
+#include <openssl/x509v3.h>
+
 #include "config/config.h"
 #include "configure/configure.h"
 #include "core/fs.h"
@@ -292,5 +296,41 @@ TEST(gotemplate_mutation_fuzz_never_crashes) {
     }
   }
   EXPECT_TRUE(rendered > 100 && errors > 100);
+}
+
+TEST(sprig_certificates_encryption_durations) {
+  Value d = Value::map();
+  std::string out = render_tmpl(
+      "{{ $ca := genCA \"my-ca\" 365 }}{{ $c := genSignedCert \"svc\" (list \"10.0.0.1\") (list \"svc.ns.svc\") 30 $ca }}"
+      "{{ $ca.Cert }}|{{ $c.Cert }}|{{ $c.Key }}|{{ (genSelfSignedCert \"self\" nil (list \"a.b\") 1).Cert }}",
+      d);
+  auto parts = split(out, "|");
+  EXPECT_EQ(parts.size(), (size_t)4);
+  auto read_cert = [](const std::string& pem) {
+    BIO* b = BIO_new_mem_buf(pem.data(), (int)pem.size());
+    X509* x = PEM_read_bio_X509(b, nullptr, nullptr, nullptr);
+    BIO_free(b);
+    return x;
+  };
+  X509* ca = read_cert(parts[0]);
+  X509* leaf = read_cert(parts[1]);
+  X509* self = read_cert(parts[3]);
+  EXPECT_TRUE(ca && leaf && self);
+  EXPECT_EQ(X509_check_ca(ca), 1);
+  EVP_PKEY* ca_pub = X509_get_pubkey(ca);
+  EXPECT_EQ(X509_verify(leaf, ca_pub), 1);  // signed by the CA
+  EXPECT_EQ(X509_check_host(leaf, "svc.ns.svc", 0, 0, nullptr), 1);
+  EXPECT_EQ(X509_check_ip_asc(leaf, "10.0.0.1", 0), 1);
+  EXPECT_EQ(X509_check_host(self, "a.b", 0, 0, nullptr), 1);
+  EXPECT_TRUE(contains(parts[2], "BEGIN RSA PRIVATE KEY"));
+  EVP_PKEY_free(ca_pub);
+  X509_free(ca);
+  X509_free(leaf);
+  X509_free(self);
+  for (const char* t : {"rsa", "ecdsa", "ed25519"})
+    EXPECT_TRUE(contains(render_tmpl(std::string("{{ genPrivateKey \"") + t + "\" }}", d), "PRIVATE KEY-----"));
+  EXPECT_EQ(render_tmpl("{{ encryptAES \"secretkey\" \"plaintext\" | decryptAES \"secretkey\" }}", d),
+            std::string("plaintext"));
+  EXPECT_EQ(render_tmpl("{{ duration 3725 }} {{ duration \"95\" }} {{ duration 0 }}", d), std::string("1h2m5s 1m35s 0s"));
 }
 
