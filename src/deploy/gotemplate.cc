@@ -1427,6 +1427,7 @@ struct Engine::Impl {
     }
     if (fn == "encryptAES") { need(2); return S(sprig::encrypt_aes(strval(args[0]), strval(args[1]))); }
     if (fn == "decryptAES") { need(2); return S(sprig::decrypt_aes(strval(args[0]), strval(args[1]))); }
+    if (fn == "htpasswd") { need(2); return S(sprig::htpasswd(strval(args[0]), strval(args[1]))); }
     // ---- durations (sprig date.go): Go's time.Duration.String() of whole seconds
     auto go_duration = [](int64_t sec) {
       if (sec == 0) return std::string("0s");

@@ -1,5 +1,6 @@
 #include "deploy/sprig_crypto.h"
 
+#include <crypt.h>
 #include <openssl/bn.h>
 #include <openssl/ec.h>
 #include <openssl/evp.h>
@@ -191,6 +192,21 @@ std::string decrypt_aes(const std::string& password, const std::string& b64) {
   if (!ok) fail("decryptAES: bad key or corrupt ciphertext");
   out.resize((size_t)n1 + (size_t)n2);
   return out;
+}
+
+std::string htpasswd(const std::string& user, const std::string& password) {
+  if (user.find(':') != std::string::npos) return "invalid username: " + user;  // sprig's text
+  unsigned char rnd[16];
+  RAND_bytes(rnd, sizeof(rnd));
+  char setting[CRYPT_GENSALT_OUTPUT_SIZE];
+  // bcrypt with Go's bcrypt.DefaultCost (10) and its "$2a$" prefix, via libxcrypt
+  if (!crypt_gensalt_rn("$2a$", 10, (const char*)rnd, (int)sizeof(rnd), setting, (int)sizeof(setting)))
+    fail("htpasswd: bcrypt salt generation failed");
+  struct crypt_data data;
+  std::memset(&data, 0, sizeof(data));
+  const char* h = crypt_r(password.c_str(), setting, &data);
+  if (!h || h[0] == '*') fail("htpasswd: bcrypt failed");
+  return user + ":" + h;
 }
 
 }  // namespace sprig

@@ -25,6 +25,8 @@ Value gen_signed_cert(const std::string& cn, const std::vector<std::string>& ips
 // base64(iv || ciphertext) — Sprig's format, so values round-trip with charts rendered by Helm.
 std::string encrypt_aes(const std::string& password, const std::string& plaintext);
 std::string decrypt_aes(const std::string& password, const std::string& b64);
+// "user:$2a$10$..." (bcrypt, cost 10), the htpasswd line docker-registry style charts render.
+std::string htpasswd(const std::string& user, const std::string& password);
 
 }  // namespace sprig
 }  // namespace ds

@@ -1,7 +1,9 @@
 // Go-template engine, Helm chart rendering (the embedded component chart), generator language
 // detection and config mutations (configure/*).
 #include <algorithm>
+#include <cstring>
 
+#include <crypt.h>
 #include <openssl/pem.h>
 #include <openssl/x509.h>
 #include <openssl/x509v3.h>
@@ -332,5 +334,11 @@ TEST(sprig_certificates_encryption_durations) {
   EXPECT_EQ(render_tmpl("{{ encryptAES \"secretkey\" \"plaintext\" | decryptAES \"secretkey\" }}", d),
             std::string("plaintext"));
   EXPECT_EQ(render_tmpl("{{ duration 3725 }} {{ duration \"95\" }} {{ duration 0 }}", d), std::string("1h2m5s 1m35s 0s"));
+  std::string line = render_tmpl("{{ htpasswd \"admin\" \"s3cret\" }}", d);
+  EXPECT_TRUE(starts_with(line, "admin:$2a$10$") && line.size() == 6 + 60);
+  struct crypt_data cd;
+  std::memset(&cd, 0, sizeof(cd));
+  std::string hash = line.substr(6);
+  EXPECT_EQ(std::string(crypt_r("s3cret", hash.c_str(), &cd)), hash);  // verifies as bcrypt
 }
 
