@@ -1,6 +1,10 @@
 #include "deploy/gotemplate.h"
 
+#include <arpa/inet.h>
+#include <netdb.h>
+
 #include <algorithm>
+#include <map>
 #include <cmath>
 #include <cstring>
 #include <ctime>
@@ -1835,6 +1839,108 @@ struct Engine::Impl {
       char buf[64];
       std::strftime(buf, sizeof(buf), "%Y-%m-%d", std::gmtime(&t));
       return S(buf);
+    }
+    // ---- remaining Sprig functions: os* aliases, biggest, sha512sum, shuffle, chunk, URLs, DNS
+    static const std::map<std::string, std::string> kAliases = {
+        {"osBase", "base"}, {"osDir", "dir"}, {"osClean", "clean"}, {"osExt", "ext"}, {"osIsAbs", "isAbs"},
+        {"biggest", "max"}};
+    auto al = kAliases.find(fn);
+    if (al != kAliases.end()) return call(sc, al->second, std::move(args), nullptr);
+    if (fn == "sha512sum") { need(1); return S(digest_hex(EVP_sha512(), strval(args[0]))); }
+    if (fn == "shuffle") {
+      need(1);
+      std::string t = strval(args[0]);
+      std::string r = random_string(t.size() * 4 + 4);
+      for (size_t i = t.size(); i > 1; --i) std::swap(t[i - 1], t[(unsigned char)r[i] * 131u % i]);
+      return S(t);
+    }
+    if (fn == "chunk") {
+      need(2);
+      int64_t n = args[0].as_int();
+      if (n <= 0) throw TemplateError("chunk: size must be positive");
+      Value out = Value::seq(), cur = Value::seq();
+      for (auto& it : args[1].items()) {
+        cur.push(it);
+        if ((int64_t)cur.size() == n) {
+          out.push(cur);
+          cur = Value::seq();
+        }
+      }
+      if (cur.size()) out.push(cur);
+      return out;
+    }
+    if (fn == "urlParse") {
+      need(1);
+      std::string u = strval(args[0]);
+      Value m = Value::map();
+      std::string rest = u, frag, query;
+      size_t h = rest.find('#');
+      if (h != std::string::npos) frag = rest.substr(h + 1), rest = rest.substr(0, h);
+      size_t q = rest.find('?');
+      if (q != std::string::npos) query = rest.substr(q + 1), rest = rest.substr(0, q);
+      std::string scheme, host, userinfo, path = rest, opaque;
+      size_t c = rest.find(':');
+      if (c != std::string::npos && c > 0 && rest.find('/') > c) {
+        scheme = rest.substr(0, c);
+        rest = rest.substr(c + 1);
+        if (starts_with(rest, "//")) {
+          rest = rest.substr(2);
+          size_t sl = rest.find('/');
+          std::string auth = rest.substr(0, sl);
+          path = sl == std::string::npos ? "" : rest.substr(sl);
+          size_t at = auth.rfind('@');
+          if (at != std::string::npos) userinfo = auth.substr(0, at), auth = auth.substr(at + 1);
+          host = auth;
+        } else {
+          opaque = rest;
+          path = "";
+        }
+      }
+      std::string hostname = host;
+      if (!hostname.empty() && hostname[0] == '[') hostname = hostname.substr(1, hostname.find(']') - 1);
+      else if (hostname.find(':') != std::string::npos) hostname = hostname.substr(0, hostname.find(':'));
+      m["scheme"] = scheme;
+      m["host"] = host;
+      m["hostname"] = hostname;
+      m["path"] = path;
+      m["query"] = query;
+      m["opaque"] = opaque;
+      m["fragment"] = frag;
+      m["userinfo"] = userinfo;
+      return m;
+    }
+    if (fn == "urlJoin") {
+      need(1);
+      const Value& m = args[0];
+      std::string out;
+      if (!m.get("scheme").as_string().empty()) out += m.get("scheme").as_string() + ":";
+      if (!m.get("opaque").as_string().empty()) {
+        out += m.get("opaque").as_string();
+      } else {
+        if (!m.get("host").as_string().empty() || !m.get("userinfo").as_string().empty()) {
+          out += "//";
+          if (!m.get("userinfo").as_string().empty()) out += m.get("userinfo").as_string() + "@";
+          out += m.get("host").as_string();
+        }
+        out += m.get("path").as_string();
+      }
+      if (!m.get("query").as_string().empty()) out += "?" + m.get("query").as_string();
+      if (!m.get("fragment").as_string().empty()) out += "#" + m.get("fragment").as_string();
+      return S(out);
+    }
+    if (fn == "getHostByName") {
+      need(1);
+      struct addrinfo hints{}, *res = nullptr;
+      hints.ai_family = AF_UNSPEC;
+      std::string ip;
+      if (::getaddrinfo(strval(args[0]).c_str(), nullptr, &hints, &res) == 0 && res) {
+        char buf[INET6_ADDRSTRLEN] = {0};
+        void* a = res->ai_family == AF_INET ? (void*)&((struct sockaddr_in*)res->ai_addr)->sin_addr
+                                             : (void*)&((struct sockaddr_in6*)res->ai_addr)->sin6_addr;
+        if (::inet_ntop(res->ai_family, a, buf, sizeof(buf))) ip = buf;
+        ::freeaddrinfo(res);
+      }
+      return S(ip);
     }
     // mustX is X that returns its error instead of panicking; errors already throw here
     if (starts_with(fn, "must") && fn.size() > 4 && std::isupper((unsigned char)fn[4])) {

@@ -342,3 +342,22 @@ TEST(sprig_certificates_encryption_durations) {
   EXPECT_EQ(std::string(crypt_r("s3cret", hash.c_str(), &cd)), hash);  // verifies as bcrypt
 }
 
+TEST(sprig_remaining_functions) {
+  Value d = Value::map();
+  EXPECT_EQ(render_tmpl("{{ osBase \"/a/b.txt\" }} {{ osExt \"x.tar.gz\" }} {{ biggest 1 7 3 }}", d), std::string("b.txt .gz 7"));
+  EXPECT_EQ(render_tmpl("{{ sha512sum \"abc\" | trunc 16 }}", d), std::string("ddaf35a193617aba"));
+  EXPECT_EQ(render_tmpl("{{ chunk 2 (list 1 2 3 4 5) | toJson }}", d), std::string("[[1,2],[3,4],[5]]"));
+  std::string sh = render_tmpl("{{ shuffle \"abcdef\" }}", d);
+  std::string sorted = sh;
+  std::sort(sorted.begin(), sorted.end());
+  EXPECT_EQ(sorted, std::string("abcdef"));
+  EXPECT_EQ(render_tmpl("{{ $u := urlParse \"https://me:pw@example.com:8443/p/q?x=1#frag\" }}"
+                        "{{ $u.scheme }}|{{ $u.host }}|{{ $u.hostname }}|{{ $u.path }}|{{ $u.query }}|{{ $u.fragment }}|{{ $u.userinfo }}",
+                        d),
+            std::string("https|example.com:8443|example.com|/p/q|x=1|frag|me:pw"));
+  EXPECT_EQ(render_tmpl("{{ urlJoin (dict \"scheme\" \"http\" \"host\" \"h:80\" \"path\" \"/x\" \"query\" \"a=b\") }}", d),
+            std::string("http://h:80/x?a=b"));
+  EXPECT_EQ(render_tmpl("{{ getHostByName \"localhost\" | empty | not }}", d), std::string("true"));
+  EXPECT_EQ(render_tmpl("{{ mustMerge (dict \"a\" 1) (dict \"a\" 2 \"b\" 3) | toJson }}", d), std::string("{\"a\":1,\"b\":3}"));
+}
+
