@@ -1012,6 +1012,36 @@ struct Engine::Impl {
   }
 
   static std::string strval(const Value& v) { return v.is_null() ? "" : print_value(v); }
+  // Go marshals map[string]interface{} with sorted keys (yaml and json alike): values that
+  // went through toYaml/toJson render byte-identical to Helm's output (and to its checksums).
+  static Value sorted_maps(const Value& v) {
+    if (v.is_map()) {
+      Value out = Value::map();
+      std::vector<const std::pair<std::string, Value>*> es;
+      for (auto& e : v.entries()) es.push_back(&e);
+      std::sort(es.begin(), es.end(), [](auto* a, auto* b) { return a->first < b->first; });
+      for (auto* e : es) out.entries().emplace_back(e->first, sorted_maps(e->second));
+      return out;
+    }
+    if (v.is_seq()) {
+      Value out = Value::seq();
+      for (auto& it : v.items()) out.push(sorted_maps(it));
+      return out;
+    }
+    return v;
+  }
+  // json.Marshal's HTML escaping of <, > and & (sprig toJson; toRawJson keeps them)
+  static std::string html_escape_json(const std::string& j) {
+    std::string o;
+    o.reserve(j.size());
+    for (char c : j) {
+      if (c == '<') o += "\\u003c";
+      else if (c == '>') o += "\\u003e";
+      else if (c == '&') o += "\\u0026";
+      else o.push_back(c);
+    }
+    return o;
+  }
   // "2006-01-02T15:04:05Z07:00" (fractional seconds ignored) -> unix seconds; 0 if unparsable
   static int64_t parse_rfc3339(const std::string& t) {
     struct tm tm{};
@@ -1195,12 +1225,13 @@ struct Engine::Impl {
     if (fn == "toYaml") {
       need(1);
       if (args[0].is_null()) return S("null");
-      std::string y = yaml_dump(args[0]);
+      std::string y = yaml_dump(sorted_maps(args[0]));
       if (ends_with(y, "\n")) y.pop_back();
       return S(y);
     }
-    if (fn == "toJson" || fn == "toRawJson" || fn == "mustToJson") { need(1); return S(json_dump(args[0])); }
-    if (fn == "toPrettyJson") { need(1); return S(json_dump(args[0], 2)); }
+    if (fn == "toJson" || fn == "mustToJson") { need(1); return S(html_escape_json(json_dump(sorted_maps(args[0])))); }
+    if (fn == "toRawJson") { need(1); return S(json_dump(sorted_maps(args[0]))); }
+    if (fn == "toPrettyJson") { need(1); return S(html_escape_json(json_dump(sorted_maps(args[0]), 2))); }
     if (fn == "fromYaml") { need(1); return yaml_parse(args[0].as_string()); }
     if (fn == "fromJson") { need(1); return json_parse(args[0].as_string()); }
     if (fn == "indent") { need(2); return S(indent_str((int)args[0].as_int(), strval(args[1]))); }
@@ -1798,7 +1829,7 @@ struct Engine::Impl {
     if (fn == "toToml") {
       need(1);
       std::string o;
-      if (args[0].is_map()) toml_table(args[0], "", o);
+      if (args[0].is_map()) toml_table(sorted_maps(args[0]), "", o);
       return S(o);
     }
     if (fn == "fromYamlArray" || fn == "fromJsonArray") {

@@ -361,3 +361,47 @@ TEST(sprig_remaining_functions) {
   EXPECT_EQ(render_tmpl("{{ mustMerge (dict \"a\" 1) (dict \"a\" 2 \"b\" 3) | toJson }}", d), std::string("{\"a\":1,\"b\":3}"));
 }
 
+// Behaviours of Go's text/template + Sprig that charts rely on (checked against Go semantics).
+TEST(gotemplate_go_semantics_corner_cases) {
+  Value d = yaml_parse("list: [1, 2]\nm: {b: 1, a: 2}\nzero: 0\nf: 1.5\n");
+  struct Case {
+    const char* tmpl;
+    const char* want;
+  } cases[] = {
+      {"{{ and 1 0 2 }}", "0"},
+      {"{{ or 0 \"\" \"x\" }}", "x"},
+      {"{{ range $k, $v := .m }}{{ $k }}{{ end }}", "ab"},
+      {"{{ with .missing }}x{{ else }}y{{ end }}", "y"},
+      {"{{ \"a\" | printf \"%s-%s\" \"b\" }}", "b-a"},
+      {"{{ 3 | add 1 }}", "4"},
+      {"{{ printf \"%v\" .list }}", "[1 2]"},
+      {"{{ .f }} {{ 1e3 }}", "1.5 1000"},
+      {"{{ default 5 .zero }}", "5"},
+      {"{{ empty (list) }}", "true"},
+      {"{{ ternary \"a\" \"b\" true }}", "a"},
+      {"[{{ quote .missing }}]", "[]"},
+      {"{{ quote 1 \"x\" }}", "\"1\" \"x\""},
+      {"{{ eq 1 2 1 }}", "true"},
+      {"{{ len .m }}", "2"},
+      {"{{ index .list 1 }}", "2"},
+      {"{{- \"x\" -}}  {{- \"y\" }}", "xy"},
+      {"{{ toYaml .m | trim }}", "a: 2\nb: 1"},
+      {"{{ $x := 1 }}{{ if true }}{{ $x = 2 }}{{ end }}{{ $x }}", "2"},
+      {"{{ range $i, $e := until 3 }}{{ $i }}{{ end }}", "012"},
+      {"{{ int \"12\" | add 1 }} {{ atoi \"7\" }}", "13 7"},
+      {"{{ not 0 }} {{ not 1 }}", "true false"},
+      {"{{ lt 1 2 }} {{ ge 2 2 }}", "true true"},
+      {"{{ print 1 2 \"a\" \"b\" 3 }}", "1 2ab3"},  // fmt.Sprint: spaces only between two non-strings
+  };
+  for (auto& c : cases) {
+    std::string got;
+    try {
+      got = render_tmpl(c.tmpl, d);
+    } catch (const std::exception& e) {
+      got = std::string("ERROR: ") + e.what();
+    }
+    if (got != c.want) std::fprintf(stderr, "  %s -> [%s], want [%s]\n", c.tmpl, got.c_str(), c.want);
+    EXPECT_EQ(got, std::string(c.want));
+  }
+}
+
