@@ -1115,9 +1115,24 @@ struct Engine::Impl {
     return out;
   }
 
+  int depth = 0;  // nested template/include calls
+
   std::string include(const std::string& name, const Value& dot) {
     auto it = templates.find(name);
     if (it == templates.end()) throw TemplateError("template: no template \"" + name + "\" associated");
+    // Go's text/template stops runaway recursion with an error (maxExecDepth); here the
+    // native stack is the limit, so stop well before it (100 levels fit an 8 MB stack even in
+    // the ASan build, whose frames are several times larger; real charts nest ~10 deep)
+    struct DepthGuard {
+      int& d;
+      explicit DepthGuard(int& x) : d(x) {
+        if (++d > 100) {
+          --d;
+          throw TemplateError("template: exceeded maximum template depth (100)");
+        }
+      }
+      ~DepthGuard() { --d; }
+    } guard(depth);
     Scope sc;
     sc.dot = dot;
     sc.vars.emplace_back("$", dot);

@@ -363,7 +363,7 @@ TEST(sprig_remaining_functions) {
 
 // Behaviours of Go's text/template + Sprig that charts rely on (checked against Go semantics).
 TEST(gotemplate_go_semantics_corner_cases) {
-  Value d = yaml_parse("list: [1, 2]\nm: {b: 1, a: 2}\nzero: 0\nf: 1.5\n");
+  Value d = yaml_parse("list: [1, 2]\nm: {b: 1, a: 2}\nzero: 0\nf: 1.5\nbig: 1000000\ntwo: 2.0\nhuge: 1.0e+21\nsmall: 1.0e-7\n");
   struct Case {
     const char* tmpl;
     const char* want;
@@ -392,6 +392,17 @@ TEST(gotemplate_go_semantics_corner_cases) {
       {"{{ not 0 }} {{ not 1 }}", "true false"},
       {"{{ lt 1 2 }} {{ ge 2 2 }}", "true true"},
       {"{{ print 1 2 \"a\" \"b\" 3 }}", "1 2ab3"},  // fmt.Sprint: spaces only between two non-strings
+      {"{{ .big }} {{ .two }} {{ .huge }} {{ .small }}", "1000000 2 1e+21 1e-07"},
+      {"a{{/* c */}}b{{- /* c2 */ -}} c", "abc"},
+      {"{{ define \"tt\" }}<{{ . }}>{{ end }}{{ template \"tt\" 5 }}", "<5>"},
+      {"{{ define \"rec\" }}{{ include \"rec\" . }}{{ end }}{{ include \"rec\" 1 }}",
+       "ERROR: render error in t: template: exceeded maximum template depth (100)"},
+      {"{{ block \"blk\" . }}dflt{{ end }}", "dflt"},
+      {"{{ range .list }}{{ $.f }}{{ end }}", "1.51.5"},
+      {"{{ .missing | default \"a\" | upper }}", "A"},
+      {"{{ if eq .missing nil }}nil{{ end }}", "nil"},
+      {"{{ (index .m \"a\") }} {{ .m.b }}", "2 1"},
+      {"{{ printf \"%d %s %q %5.2f\" 3 \"x\" \"y\" 3.14159 }}", "3 x \"y\"  3.14"},
   };
   for (auto& c : cases) {
     std::string got;
