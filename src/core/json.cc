@@ -12,6 +12,8 @@ namespace {
 struct JParser {
   const std::string& s;
   size_t p = 0;
+  int depth = 0;  // nesting of objects/arrays: bounded like Go's encoding/json (10000) but
+                  // sized for the native stack (API responses are untrusted input)
 
   [[noreturn]] void fail(const std::string& m) {
     throw ParseError("json: " + m + " at offset " + std::to_string(p));
@@ -80,6 +82,13 @@ struct JParser {
   Value val() {
     ws();
     if (p >= s.size()) fail("unexpected end");
+    struct Nest {
+      JParser& j;
+      explicit Nest(JParser& x) : j(x) {
+        if (++j.depth > 1000) j.fail("exceeded max depth (1000)");
+      }
+      ~Nest() { --j.depth; }
+    } nest(*this);
     char c = s[p];
     if (c == '{') {
       ++p;

@@ -226,6 +226,7 @@ class Parser {
   }
 
   Value parse_block(int indent) {
+    Nest nest(nest_);
     skip_blank();
     if (pos_ >= lines_.size()) return Value();
     Line& l = lines_[pos_];
@@ -621,7 +622,20 @@ class Parser {
     while (*p < s.size() && (s[*p] == ' ' || s[*p] == '\t' || s[*p] == '\n')) ++*p;
   }
 
+  struct Nest {
+    int& d;
+    explicit Nest(int& x) : d(x) {
+      if (++d > 1000) {
+        --d;
+        throw ParseError("yaml: exceeded max depth (1000)");
+      }
+    }
+    ~Nest() { --d; }
+  };
+  int nest_ = 0;  // collection nesting (flow and block): untrusted documents cannot exhaust the stack
+
   Value parse_flow_value(const std::string& s, size_t* p, bool in_flow) {
+    Nest nest(nest_);
     skip_ws(s, p);
     if (*p >= s.size()) return Value();
     char c = s[*p];

@@ -430,3 +430,18 @@ TEST(untrusted_tar_gzip_json_mutation_fuzz) {
   }
 }
 
+TEST(parsers_bound_nesting_depth) {
+  auto nested = [](size_t n) { return std::string(n, '[') + std::string(n, ']'); };
+  EXPECT_TRUE(json_parse(nested(500)).is_seq());
+  EXPECT_TRUE(yaml_parse(nested(500)).is_seq());
+  for (auto* parse : {+[](const std::string& t) { json_parse(t); }, +[](const std::string& t) { yaml_parse(t); }}) {
+    bool threw = false;
+    try {
+      parse(nested(200000));  // would overflow the stack without the bound
+    } catch (const std::exception& e) {
+      threw = contains(e.what(), "max depth");
+    }
+    EXPECT_TRUE(threw);
+  }
+}
+
