@@ -1,12 +1,35 @@
 #include "core/match.h"
 
 #include <algorithm>
+#include <cstdint>
 #include <functional>
+#include <vector>
 
 #include "core/fs.h"
 #include "core/strutil.h"
 
 namespace ds {
+
+namespace {
+// Failure memo for the backtracking matchers below: their result depends only on (pattern
+// position, subject position), so a state that failed once fails again. This bounds every
+// match to O(pattern x subject) states; without it patterns such as "**/**/**/**/x" or
+// "*a*a*a*a*a*c" take exponential time (a `.dockerignore` line could hang a build).
+struct FailMemo {
+  std::vector<uint8_t> bits;
+  size_t width = 0;
+  void reset(size_t p, size_t s) {
+    width = s + 1;
+    bits.assign((p + 1) * width, 0);
+  }
+  bool failed(size_t pi, size_t si) const { return bits[pi * width + si] != 0; }
+  bool fail(size_t pi, size_t si) {
+    bits[pi * width + si] = 1;
+    return false;
+  }
+};
+thread_local FailMemo g_gi_memo, g_pm_memo, g_dk_memo, g_ds_memo;
+}  // namespace
 
 // ---------------------------------------------------------------- gitignore
 
@@ -76,7 +99,13 @@ void GitIgnore::add_line(const std::string& raw) {
   pats_.push_back(std::move(p));
 }
 
+static bool gi_match_(const std::vector<GitIgnore::Tok>& t, size_t ti, const std::string& s, size_t si);
 static bool gi_match(const std::vector<GitIgnore::Tok>& t, size_t ti, const std::string& s, size_t si) {
+  if (g_gi_memo.failed(ti, si)) return false;
+  return gi_match_(t, ti, s, si) || g_gi_memo.fail(ti, si);
+}
+
+static bool gi_match_(const std::vector<GitIgnore::Tok>& t, size_t ti, const std::string& s, size_t si) {
   using Tok = GitIgnore::Tok;
   if (ti == t.size()) return si == s.size();
   const Tok& k = t[ti];
@@ -128,6 +157,7 @@ static bool gi_match(const std::vector<GitIgnore::Tok>& t, size_t ti, const std:
 bool GitIgnore::matches(const std::string& path) const {
   bool m = false;
   for (auto& p : pats_) {
+    g_gi_memo.reset(p.toks.size(), path.size());
     if (gi_match(p.toks, 0, path, 0)) {
       if (!p.negate)
         m = true;
@@ -175,7 +205,13 @@ static bool match_class(const std::string& pat, size_t* pi, char c, bool* ok) {
   return matched != neg;
 }
 
+static bool pm_rec_(const std::string& p, size_t pi, const std::string& s, size_t si);
 static bool pm_rec(const std::string& p, size_t pi, const std::string& s, size_t si) {
+  if (g_pm_memo.failed(pi, si)) return false;
+  return pm_rec_(p, pi, s, si) || g_pm_memo.fail(pi, si);
+}
+
+static bool pm_rec_(const std::string& p, size_t pi, const std::string& s, size_t si) {
   while (pi < p.size()) {
     char c = p[pi];
     if (c == '*') {
@@ -212,12 +248,26 @@ static bool pm_rec(const std::string& p, size_t pi, const std::string& s, size_t
   return si == s.size();
 }
 
-bool path_match(const std::string& pattern, const std::string& name) { return pm_rec(pattern, 0, name, 0); }
+bool path_match(const std::string& pattern, const std::string& name) {
+  g_pm_memo.reset(pattern.size(), name.size());
+  return pm_rec(pattern, 0, name, 0);
+}
 
 // ---------------------------------------------------------------- docker ignore
 
 // Docker's pattern regex: "**" matches across separators, "*" doesn't, "?" single non-sep.
+static bool docker_rec_(const std::string& p, size_t pi, const std::string& s, size_t si);
 static bool docker_rec(const std::string& p, size_t pi, const std::string& s, size_t si) {
+  if (g_dk_memo.failed(pi, si)) return false;
+  return docker_rec_(p, pi, s, si) || g_dk_memo.fail(pi, si);
+}
+
+static bool docker_match(const std::string& p, const std::string& s) {
+  g_dk_memo.reset(p.size(), s.size());
+  return docker_rec(p, 0, s, 0);
+}
+
+static bool docker_rec_(const std::string& p, size_t pi, const std::string& s, size_t si) {
   while (pi < p.size()) {
     char c = p[pi];
     if (c == '*') {
@@ -292,11 +342,11 @@ bool DockerIgnore::matches(const std::string& rel_in) const {
   bool matched = false;
   for (auto& p : pats_) {
     if (p.exclusion != matched) continue;  // only patterns that can flip the state matter
-    bool m = docker_rec(p.pat, 0, rel, 0);
+    bool m = docker_match(p.pat, rel);
     if (!m && !parent_is_root) {
       if (p.dirs.size() <= parent_dirs.size()) {
         std::vector<std::string> sub(parent_dirs.begin(), parent_dirs.begin() + p.dirs.size());
-        m = docker_rec(p.pat, 0, join(sub, "/"), 0);
+        m = docker_match(p.pat, join(sub, "/"));
       }
     }
     if (m) matched = !p.exclusion;
@@ -336,7 +386,13 @@ static bool brace_expand_match(const std::string& pattern, const std::string& pa
 
 static bool seg_match(const std::string& pat, const std::string& seg) { return path_match(pat, seg); }
 
+static bool ds_rec_(const std::vector<std::string>& p, size_t pi, const std::vector<std::string>& s, size_t si);
 static bool ds_rec(const std::vector<std::string>& p, size_t pi, const std::vector<std::string>& s, size_t si) {
+  if (g_ds_memo.failed(pi, si)) return false;
+  return ds_rec_(p, pi, s, si) || g_ds_memo.fail(pi, si);
+}
+
+static bool ds_rec_(const std::vector<std::string>& p, size_t pi, const std::vector<std::string>& s, size_t si) {
   if (pi == p.size()) return si == s.size();
   if (p[pi] == "**") {
     for (size_t j = si; j <= s.size(); ++j)
@@ -385,6 +441,7 @@ static bool brace_expand_match(const std::string& pattern, const std::string& pa
     if (abs != starts_with(path, "/")) continue;
     auto ps = split_nonempty(pat, '/');
     auto ss = split_nonempty(path, '/');
+    g_ds_memo.reset(ps.size(), ss.size());
     if (ds_rec(ps, 0, ss, 0)) return true;
   }
   return false;

@@ -1,6 +1,8 @@
 // Core library tests: YAML/JSON, matchers, tar/gzip, hashing, CLI parser.
 #include <unistd.h>
 
+#include <chrono>
+
 #include "core/cli.h"
 #include "core/codec.h"
 #include "core/fs.h"
@@ -443,5 +445,32 @@ TEST(parsers_bound_nesting_depth) {
     }
     EXPECT_TRUE(threw);
   }
+}
+
+// Patterns that make a plain backtracking matcher exponential finish at once (failure memo).
+TEST(matchers_pathological_patterns_are_fast) {
+  std::string deep;
+  for (int i = 0; i < 40; ++i) deep += "a/";
+  deep += "b";
+  std::string stars;
+  for (int i = 0; i < 25; ++i) stars += "*a";
+  stars += "c";
+  std::string dstars;
+  for (int i = 0; i < 10; ++i) dstars += "**/";
+  dstars += "c";
+  auto t0 = std::chrono::steady_clock::now();
+  EXPECT_TRUE(!glob_match(dstars, deep));
+  EXPECT_TRUE(!path_match(stars, std::string(60, 'a')));
+  GitIgnore gi;
+  gi.add_line(dstars);
+  gi.add_line(stars);
+  EXPECT_TRUE(!gi.matches(deep) && !gi.matches(std::string(60, 'a')));
+  DockerIgnore di({dstars, stars});
+  EXPECT_TRUE(!di.matches(deep) && !di.matches(std::string(60, 'a')));
+  // and they still match what they should
+  EXPECT_TRUE(glob_match(dstars, deep.substr(0, deep.size() - 1) + "c"));
+  EXPECT_TRUE(path_match(stars, std::string(59, 'a') + "c"));
+  auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+  EXPECT_TRUE(ms < 500);
 }
 
