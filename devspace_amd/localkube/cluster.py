@@ -202,6 +202,16 @@ class LocalCluster:
                 t.cancel()
             if rest:  # bounded: a handler that swallows one cancellation must not hang stop()
                 await asyncio.wait(rest, timeout=2.0)
+            # catch-all: any subprocess transport of this loop still open (a process whose
+            # handle was dropped without close) is closed now, while the loop can still run
+            # its callbacks, not later by the GC on a closed loop
+            import gc
+            from asyncio.base_subprocess import BaseSubprocessTransport
+
+            loop = asyncio.get_running_loop()
+            for o in gc.get_objects():
+                if isinstance(o, BaseSubprocessTransport) and getattr(o, "_loop", None) is loop and not o.is_closing():
+                    o.close()
             await asyncio.sleep(0)  # let subprocess transports deliver their connection_lost
 
         fut = asyncio.run_coroutine_threadsafe(shutdown(), self.loop)
