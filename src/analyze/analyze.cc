@@ -9,6 +9,7 @@
 #include <thread>
 
 #include "core/log.h"
+#include "core/safe_regex.h"
 #include "core/strutil.h"
 
 namespace ds {
@@ -80,11 +81,15 @@ bool log_has_gpu_runtime_error(const std::string& text, std::string* match) {
       "torch.OutOfMemoryError|HIP out of memory|"
       "Bus error|unable to (write to|allocate) .*shared memory|shared memory segment|/dev/shm.*No space left)",
       std::regex::icase);
-  std::smatch m;
-  if (std::regex_search(text, m, re)) {
-    if (match) *match = m.str(0);
+  // line by line (the patterns never span lines), each line capped: container logs can hold
+  // megabyte-long lines (progress bars, JSON dumps) that std::regex cannot scan in one piece
+  for (auto& full : split(text, "\n")) {
+    std::string line = full.size() > 16384 ? full.substr(0, 16384) : full;
+    std::smatch m;
+    if (!safe_regex_search(line, &m, re)) continue;
     // amdgpu.ids is a benign warning on most images
-    if (contains(m.str(0), "amdgpu.ids")) return false;
+    if (contains(m.str(0), "amdgpu.ids")) continue;
+    if (match) *match = m.str(0);
     return true;
   }
   return false;

@@ -15,6 +15,7 @@
 #include "core/log.h"
 #include "core/match.h"
 #include "core/proc.h"
+#include "core/safe_regex.h"
 #include "core/strutil.h"
 #include "core/trace.h"
 #include "sync/sync.h"
@@ -130,17 +131,17 @@ std::pair<std::string, std::string> format_kaniko_line(const std::string& line) 
   std::smatch m;
   std::string msg;
   bool is_log = false;
-  if (std::regex_match(line, m, logrus)) {
+  if (safe_regex_match(line, &m, logrus)) {
     msg = m[3];
     is_log = true;
-  } else if (std::regex_match(line, m, klog)) {
+  } else if (safe_regex_match(line, &m, klog)) {
     msg = m[2];
     is_log = true;
   } else {
     msg = line;
   }
   for (auto& f : formats) {
-    if (std::regex_match(msg, f.first)) return {"done", std::regex_replace(msg, f.first, f.second)};
+    if (safe_regex_match(msg, f.first)) return {"done", safe_regex_replace(msg, f.first, f.second)};
   }
   if (!is_log) return {"info", ">> " + line};
   return {"", msg};

@@ -12,6 +12,7 @@
 #include "core/fs.h"
 #include "core/log.h"
 #include "core/prompt.h"
+#include "core/safe_regex.h"
 #include "core/strutil.h"
 #include "deploy/deploy.h"
 #include "deploy/helmrepo.h"
@@ -586,15 +587,15 @@ std::unique_ptr<cli::Command> make_status() {
           s.status = "Error";
           s.error = msg;
           s.last_time = time;
-        } else if (std::regex_match(msg, sm, down)) {
+        } else if (safe_regex_match(msg, &sm, down)) {
           s.last = "Downloaded " + sm[1].str() + " changes";
           s.last_time = time;
           s.total += std::stoll(sm[1].str());
-        } else if (std::regex_match(msg, sm, up)) {
+        } else if (safe_regex_match(msg, &sm, up)) {
           s.last = "Uploaded " + sm[1].str() + " changes";
           s.last_time = time;
           s.total += std::stoll(sm[1].str());
-        } else if (std::regex_match(msg, stopped)) {
+        } else if (safe_regex_match(msg, stopped)) {
           s.status = "Stopped";
           s.last = "Sync stopped";
           s.last_time = time;

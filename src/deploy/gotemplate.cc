@@ -17,6 +17,7 @@
 
 #include "core/codec.h"
 #include "core/match.h"
+#include "core/safe_regex.h"
 #include "core/strutil.h"
 #include "deploy/sprig_crypto.h"
 
@@ -1412,10 +1413,10 @@ struct Engine::Impl {
       return S(v.is_map() ? "map[string]interface {}" : v.is_seq() ? "[]interface {}" : v.is_string() ? "string"
                : v.is_int() ? "int64" : v.is_float() ? "float64" : v.is_bool() ? "bool" : "<nil>");
     }
-    if (fn == "regexMatch") { need(2); return Value(std::regex_search(strval(args[1]), std::regex(args[0].as_string()))); }
+    if (fn == "regexMatch") { need(2); return Value(safe_regex_search(strval(args[1]), std::regex(args[0].as_string()))); }
     if (fn == "regexReplaceAll") {
       need(3);
-      return S(std::regex_replace(strval(args[1]), std::regex(args[0].as_string()), args[2].as_string()));
+      return S(safe_regex_replace(strval(args[1]), std::regex(args[0].as_string()), args[2].as_string()));
     }
     if (fn == "semverCompare" || fn == "mustSemverCompare") {
       need(2);
@@ -1765,7 +1766,7 @@ struct Engine::Impl {
       need(2);
       std::smatch m;
       std::string str = strval(args[1]);
-      return S(std::regex_search(str, m, std::regex(args[0].as_string())) ? m.str(0) : "");
+      return S(safe_regex_search(str, &m, std::regex(args[0].as_string())) ? m.str(0) : "");
     }
     if (fn == "regexFindAll" || fn == "regexSplit") {
       need(3);
@@ -1773,6 +1774,7 @@ struct Engine::Impl {
       std::regex re(args[0].as_string());
       int64_t n = args[2].as_int();
       std::vector<std::string> out;
+      safe_regex_run(str.size(), [&] {
       if (fn == "regexFindAll") {
         for (auto it = std::sregex_iterator(str.begin(), str.end(), re); it != std::sregex_iterator(); ++it) {
           if (n >= 0 && (int64_t)out.size() >= n) break;
@@ -1787,12 +1789,15 @@ struct Engine::Impl {
         }
         out.push_back(str.substr(pos));
       }
+      });
       return Value::strings(out);
     }
     if (fn == "regexReplaceAllLiteral") {
       need(3);
-      return S(std::regex_replace(strval(args[1]), std::regex(args[0].as_string()), args[2].as_string(),
-                                  std::regex_constants::format_sed));
+      std::string str = strval(args[1]), out;
+      std::regex re(args[0].as_string());
+      safe_regex_run(str.size(), [&] { out = std::regex_replace(str, re, args[2].as_string(), std::regex_constants::format_sed); });
+      return S(out);
     }
     if (fn == "regexQuoteMeta") {
       need(1);

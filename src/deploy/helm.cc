@@ -13,6 +13,7 @@
 #include "core/codec.h"
 #include "core/fs.h"
 #include "core/log.h"
+#include "core/safe_regex.h"
 #include "core/strutil.h"
 #include "core/trace.h"
 #include "core/match.h"
@@ -363,7 +364,7 @@ void validate_schema(const Value& v, const Value& schema, const Value& root, con
       }
       for (auto& pp : pprops.entries()) {
         try {
-          if (std::regex_search(e.first, std::regex(pp.first))) {
+          if (safe_regex_search(e.first, std::regex(pp.first))) {
             known = true;
             validate_schema(e.second, pp.second, root, sub, errs, depth + 1);
           }
@@ -417,7 +418,7 @@ void validate_schema(const Value& v, const Value& schema, const Value& root, con
       err("String length must be less than or equal to " + schema.get("maxLength").as_string());
     if (schema.has("pattern")) {
       try {
-        if (!std::regex_search(v.str(), std::regex(schema.get("pattern").as_string(), std::regex::ECMAScript)))
+        if (!safe_regex_search(v.str(), std::regex(schema.get("pattern").as_string(), std::regex::ECMAScript)))
           err("Does not match pattern '" + schema.get("pattern").as_string() + "'");
       } catch (const std::regex_error&) {
       }

@@ -8,6 +8,7 @@
 #include <openssl/x509.h>
 #include <openssl/x509v3.h>
 
+#include "analyze/analyze.h"
 #include "config/config.h"
 #include "configure/configure.h"
 #include "core/fs.h"
@@ -414,5 +415,22 @@ TEST(gotemplate_go_semantics_corner_cases) {
     if (got != c.want) std::fprintf(stderr, "  %s -> [%s], want [%s]\n", c.tmpl, got.c_str(), c.want);
     EXPECT_EQ(got, std::string(c.want));
   }
+}
+
+// std::regex recurses per input character; long inputs used to overflow the stack (a 100 kB
+// container log line crashed `devspace analyze`).
+TEST(regex_on_long_inputs_does_not_crash) {
+  std::string big = "rccl " + std::string(300000, 'x') + " failed\n";
+  std::string m;
+  EXPECT_TRUE(analyze::log_has_gpu_runtime_error(std::string(200000, 'y') + "\nNCCL error: boom\n", &m));
+  EXPECT_EQ(m, std::string("NCCL error"));
+  EXPECT_TRUE(!analyze::log_has_gpu_runtime_error(std::string(500000, 'z'), &m));
+  Value d = Value::map();
+  d["s"] = std::string(200000, 'a') + "b";
+  EXPECT_EQ(render_tmpl("{{ regexFind \"a*b\" .s | len }}", d), std::string("200001"));
+  EXPECT_EQ(render_tmpl("{{ regexMatch \"^a+b$\" .s }}", d), std::string("true"));
+  EXPECT_EQ(render_tmpl("{{ regexReplaceAll \"a+\" .s \"x\" }}", d), std::string("xb"));
+  EXPECT_EQ(render_tmpl("{{ regexFindAll \"a+b\" .s -1 | len }}", d), std::string("1"));
+  (void)big;
 }
 
