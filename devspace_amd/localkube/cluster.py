@@ -210,7 +210,9 @@ class LocalCluster:
 
             loop = asyncio.get_running_loop()
             for o in gc.get_objects():
-                if isinstance(o, BaseSubprocessTransport) and getattr(o, "_loop", None) is loop and not o.is_closing():
+                # type(), not isinstance(): the latter reads __class__, which some proxy objects
+                # in the heap (torch's deprecated reduce_op) answer with a warning
+                if issubclass(type(o), BaseSubprocessTransport) and o._loop is loop and not o.is_closing():
                     o.close()
             await asyncio.sleep(0)  # let subprocess transports deliver their connection_lost
 
