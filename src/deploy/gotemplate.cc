@@ -1013,6 +1013,14 @@ struct Engine::Impl {
   }
 
   static std::string strval(const Value& v) { return v.is_null() ? "" : print_value(v); }
+  // Generated sizes (until/untilStep/seq elements, repeat output) are bounded: a chart typo
+  // such as `until 1000000000` must fail the render, not take the host's memory.
+  static constexpr int64_t kMaxGenerated = 10000000;
+  static void check_generated(int64_t n, const char* fn) {
+    if (n > kMaxGenerated)
+      throw TemplateError(std::string(fn) + ": " + std::to_string(n) + " elements exceed the limit of " +
+                          std::to_string(kMaxGenerated));
+  }
   // Go marshals map[string]interface{} with sorted keys (yaml and json alike): values that
   // went through toYaml/toJson render byte-identical to Helm's output (and to its checksums).
   static Value sorted_maps(const Value& v) {
@@ -1290,8 +1298,10 @@ struct Engine::Impl {
     }
     if (fn == "repeat") {
       need(2);
-      std::string o;
-      for (int64_t i = 0; i < args[0].as_int(); ++i) o += strval(args[1]);
+      std::string o, unit = strval(args[1]);
+      int64_t n = args[0].as_int();
+      check_generated(n * (int64_t)std::max<size_t>(1, unit.size()), "repeat");
+      for (int64_t i = 0; i < n; ++i) o += unit;
       return S(o);
     }
     if (fn == "join") {
@@ -1393,6 +1403,7 @@ struct Engine::Impl {
     if (fn == "until") {
       need(1);
       Value l = Value::seq();
+      check_generated(args[0].as_int(), "until");
       for (int64_t i = 0; i < args[0].as_int(); ++i) l.push(Value(i));
       return l;
     }
@@ -1692,6 +1703,7 @@ struct Engine::Impl {
       Value l = Value::seq();
       int64_t a = args[0].as_int(), b = args[1].as_int(), st = args[2].as_int();
       if (st == 0) return l;
+      check_generated((b - a) / st, "untilStep");
       for (int64_t i = a; st > 0 ? i < b : i > b; i += st) l.push(Value(i));
       return l;
     }
@@ -1702,6 +1714,7 @@ struct Engine::Impl {
       if (args.size() >= 3) a = args[0].as_int(), st = args[1].as_int(), b = args[2].as_int();
       if (args.size() >= 2 && args.size() < 3 && a > b) st = -1;
       std::vector<std::string> o;
+      if (st != 0) check_generated((b - a) / st, "seq");
       if (st != 0)
         for (int64_t i = a; st > 0 ? i <= b : i >= b; i += st) o.push_back(std::to_string(i));
       return S(join(o, " "));

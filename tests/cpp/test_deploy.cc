@@ -404,6 +404,9 @@ TEST(gotemplate_go_semantics_corner_cases) {
       {"{{ if eq .missing nil }}nil{{ end }}", "nil"},
       {"{{ (index .m \"a\") }} {{ .m.b }}", "2 1"},
       {"{{ printf \"%d %s %q %5.2f\" 3 \"x\" \"y\" 3.14159 }}", "3 x \"y\"  3.14"},
+      {"{{ until 1000000000 | len }}",
+       "ERROR: render error in t: until: 1000000000 elements exceed the limit of 10000000"},
+      {"{{ repeat 3 \"ab\" }} {{ seq 3 }} {{ untilStep 0 6 2 | len }}", "ababab 1 2 3 3"},
   };
   for (auto& c : cases) {
     std::string got;
