@@ -1,4 +1,5 @@
 #include "analyze/analyze.h"
+#include "gpu/sizing.h"
 
 #include <time.h>
 
@@ -257,6 +258,8 @@ std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, co
                     " (MI355X nodes expose 8 GPUs; HBM is not a schedulable resource)\n");
     std::string shm = shm_problem(p, want);
     if (!shm.empty()) out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + shm + "\n");
+    for (auto& prob : gpu::pod_sizing_problems(p.get("spec")))
+      out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + prob + "\n");
     for (auto& c : p.at_path("status.containerStatuses").items()) {
       bool crashed = c.get("restartCount").as_int() > 0 || !c.at_path("state.terminated").is_null();
       if (!crashed) continue;

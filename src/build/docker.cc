@@ -3,6 +3,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <regex>
 #include <cstdlib>
 #include <set>
 #include <stdexcept>
@@ -44,6 +45,39 @@ std::pair<std::string, std::string> split_image_tag(const std::string& ref) {
   if (colon != std::string::npos && (slash == std::string::npos || colon > slash))
     return {name.substr(0, colon) + (at == std::string::npos ? "" : ref.substr(at)), name.substr(colon + 1)};
   return {ref, ""};
+}
+
+std::string image_reference_problem(const std::string& ref) {
+  static const std::regex kComponent("[a-z0-9]+((\\.|_|__|-+)[a-z0-9]+)*");
+  static const std::regex kDomain("([a-zA-Z0-9]|[a-zA-Z0-9][a-zA-Z0-9-]*[a-zA-Z0-9])(\\.([a-zA-Z0-9]|[a-zA-Z0-9][a-zA-Z0-9-]*"
+                                  "[a-zA-Z0-9]))*(:[0-9]+)?");
+  static const std::regex kTag("[\\w][\\w.-]{0,127}");
+  static const std::regex kDigest("[A-Za-z][A-Za-z0-9]*([-_+.][A-Za-z][A-Za-z0-9]*)*:[0-9a-fA-F]{32,}");
+  if (ref.empty()) return "the image name is empty";
+  if (ref.size() > 255 + 128 + 80) return "the image reference is too long";
+  std::string rest = ref;
+  size_t at = rest.find('@');
+  if (at != std::string::npos) {
+    if (!std::regex_match(rest.substr(at + 1), kDigest)) return "invalid digest \"" + rest.substr(at + 1) + "\"";
+    rest = rest.substr(0, at);
+  }
+  auto nt = split_image_tag(rest);
+  if (!nt.second.empty() && !std::regex_match(nt.second, kTag)) return "invalid tag \"" + nt.second + "\"";
+  if (rest.size() > 0 && rest.back() == ':') return "empty tag";
+  std::vector<std::string> parts = split(nt.first, "/");
+  size_t first = 0;
+  if (parts.size() > 1 && (contains(parts[0], ".") || contains(parts[0], ":") || parts[0] == "localhost")) {
+    if (!std::regex_match(parts[0], kDomain)) return "invalid registry host \"" + parts[0] + "\"";
+    first = 1;
+  }
+  if (first >= parts.size()) return "no repository name after the registry";
+  for (size_t i = first; i < parts.size(); ++i) {
+    if (parts[i].empty()) return "empty path component in \"" + nt.first + "\" (leading, trailing or double '/')";
+    if (!std::regex_match(parts[i], kComponent))
+      return "invalid path component \"" + parts[i] + "\" (lower-case letters, digits and . _ __ - separators only)";
+  }
+  if (nt.first.size() > 255) return "the repository name is longer than 255 characters";
+  return "";
 }
 
 std::string pull_secret_name(const std::string& registry) {

@@ -36,6 +36,10 @@ extern const char* const kDefaultIndexServer;  // "https://index.docker.io/v1/"
 std::string registry_from_image(const std::string& image);
 // Splits "reg:5000/a/b:tag" into ("reg:5000/a/b", "tag"); digests are kept with the name.
 std::pair<std::string, std::string> split_image_tag(const std::string& ref);
+// Checks an image reference against the distribution reference grammar
+// ([domain[:port]/]component(/component)*[:tag][@digest]; components lower-case alphanumerics
+// joined by '.', '_', '__' or '-'s). Returns "" when valid, else why not.
+std::string image_reference_problem(const std::string& ref);
 // "devspace-auth-" + registry lower-cased with [^a-z0-9-] -> '-' ("docker" for Docker Hub).
 std::string pull_secret_name(const std::string& registry);
 // Hostname form used as credential key for non-default registries (registry.ConvertToHostname).

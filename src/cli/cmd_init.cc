@@ -3,6 +3,8 @@
 // cluster (kube context + namespace, or cloud provider), selector/port/sync defaults, image
 // name + registry. MI355X additions: a `rocm-pytorch` template (GPU training pod running the
 // hot-reload runner) and a GPU-count question that fills amd.com/gpu limits in the chart.
+#include <set>
+
 #include "build/docker.h"
 #include "cli/common.h"
 #include "cloud/cloud.h"
@@ -13,6 +15,8 @@
 #include "core/prompt.h"
 #include "core/strutil.h"
 #include "generator/generator.h"
+#include "gpu/sizing.h"
+#include "kube/client.h"
 #include "kube/kubeconfig.h"
 
 namespace ds {
@@ -34,7 +38,32 @@ struct InitState {
   std::string port;
   std::string gpus = "0";
   std::string language;
+  gpu::PodSizing sizing;
 };
+
+// Default base image of the rocm-pytorch template. A concrete, immutable tag: `latest` moves
+// under the developer (and GPU nodes are often air-gapped, with images pre-pulled by tag).
+const char* kDefaultRocmImage = "rocm/pytorch:rocm7.0_ubuntu24.04_py3.12_pytorch_release_2.8.0";
+
+// Per-GPU CPU/memory from the cluster's GPU nodes when they can be listed (3 s budget; init
+// also works offline), otherwise the per-GPU defaults.
+gpu::PodSizing discover_sizing(int gpus) {
+  std::vector<gpu::GpuNode> nodes;
+  if (gpus > 0 && !getenv("DEVSPACE_INIT_NO_NODE_DISCOVERY")) {
+    try {
+      auto k = kube::Client::from_devspace_config(Value::map(), false);
+      net::Response r = k->raw("GET", "/api/v1/nodes", "", "application/json", 3000);
+      if (r.status == 200) nodes = gpu::gpu_nodes(json_parse(r.body));
+    } catch (const std::exception&) {
+      // no cluster configured / reachable, or nodes not listable for this user
+    }
+  }
+  gpu::PodSizing s = gpu::size_pod(gpus, nodes);
+  if (gpus > 0)
+    log::infof("Sizing the pod for %d GPU(s) (%s): %d CPUs, %d Gi memory incl. %d Gi /dev/shm", gpus, s.basis.c_str(),
+               s.cpu(), s.memory_gi(), s.shm_gi());
+  return s;
+}
 
 void configure_cluster_local(Value& cfg) {
   std::string current;
@@ -91,16 +120,30 @@ void add_default_ports(Value& cfg, InitState& st) {
   st.port = port;
 }
 
-void add_default_sync(Value& cfg) {
+// Machine-learning projects: byte-code caches, notebook checkpoints, model checkpoints, run
+// logs and datasets are per-side artefacts (multi-GB on MI355X nodes), never synced.
+const char* kMlSyncExcludes[] = {"__pycache__/", "*.pyc", ".ipynb_checkpoints/", "checkpoints/", "*.pt",
+                                 "*.pth", "*.safetensors", "wandb/", "data/"};
+
+void add_default_sync(Value& cfg, const std::string& language) {
   Value& sync = cfg.ensure_path("dev.sync");
   if (!sync.is_seq()) sync = Value::seq();
   for (auto& s : sync.items())
     if (s.get("localSubPath").as_string() == "./" || s.get("containerPath").as_string() == "/app") return;
   Value ex = Value::seq();
+  std::set<std::string> seen;
+  auto add = [&](const std::string& r) {
+    if (!r.empty() && seen.insert(r).second) ex.push(Value(r));
+  };
   std::string di;
   if (fs::read_file(".dockerignore", &di))
-    for (auto& r : split(di, "\n"))
-      if (!r.empty()) ex.push(Value(r));
+    for (auto& r : split(di, "\n")) add(trim(r));
+  if (language == "rocm-pytorch") {
+    for (const char* r : kMlSyncExcludes) add(r);
+  } else if (language == "python") {
+    add("__pycache__/");
+    add("*.pyc");
+  }
   Value s = Value::map();
   s["selector"] = "default";
   s["containerPath"] = "/app";
@@ -167,12 +210,19 @@ void replace_placeholders(Value& cfg, InitState& st) {
   data = replace_all(data, "#image#", image);
   data = replace_all(data, "#port#", st.port);
   data = replace_all(data, "#gpus#", st.gpus);
+  data = replace_all(data, "#resources#", gpu::resources_yaml(st.sizing));
+  std::string settings = gpu::gpu_settings_yaml(st.sizing);
+  data = replace_all(data, settings.empty() ? "#gpu-settings#\n" : "#gpu-settings#", settings);
   fs::write_file("chart/values.yaml", data);
-  // ROCm base image pin (the box may have no network: pick a tag that is pre-pulled)
+  // ROCm base image pin (GPU nodes are often air-gapped: a tag that is pre-pulled there)
   std::string df;
   if (fs::read_file("Dockerfile", &df) && contains(df, "#rocm-image#")) {
-    const char* img = getenv("DEVSPACE_ROCM_IMAGE");
-    fs::write_file("Dockerfile", replace_all(df, "#rocm-image#", img && *img ? img : "rocm/pytorch:latest"));
+    const char* env = getenv("DEVSPACE_ROCM_IMAGE");
+    std::string img = env && *env ? env : kDefaultRocmImage;
+    std::string tag = build::split_image_tag(img).second;
+    if (tag.empty() || tag == "latest")
+      log::fatal("DEVSPACE_ROCM_IMAGE=" + img + " has no concrete tag: pin one, e.g. " + kDefaultRocmImage);
+    fs::write_file("Dockerfile", replace_all(df, "#rocm-image#", img));
   }
 }
 
@@ -239,6 +289,7 @@ int run_init(cli::Command& c, const std::vector<std::string>&) {
       g.default_value = "1";
       g.validation_regex = "[1-8]";
       st.gpus = prompt::ask(g);
+      st.sizing = discover_sizing(std::atoi(st.gpus.c_str()));
     }
   }
   // Dev-mode entrypoint override: keep the container idle for sync + terminal, except for
@@ -274,7 +325,7 @@ int run_init(cli::Command& c, const std::vector<std::string>&) {
     }
     add_default_selector(cfg);
     add_default_ports(cfg, st);
-    add_default_sync(cfg);
+    add_default_sync(cfg, st.language);
     configure_image(ctx, use_cloud);
     try {
       ctx.save_base();

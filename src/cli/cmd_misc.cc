@@ -198,40 +198,70 @@ int run_login(cli::Command& c, const Args&) {
 }
 
 // Standalone sync (hidden): local dir <-> container path of one pod (or the newest running
-// pod of a label selector). Runs until interrupted or --once finishes the initial sync.
+// pod of a label selector), or — with --local-root — of a local "pod" directory driven through
+// local shells (the reference's own test seam, sync/upstream.go:67-95; used by the large-file
+// and fault tests and the bench). Runs until interrupted or --once finishes the initial sync.
+// --fault-* wrap the first connection in a FaultInjectingTransport (test hook): the killed
+// stream must be followed by a reconnect and a complete sync.
 int run_sync(cli::Command& c, const Args&) {
   GracefulInterrupt graceful;
-  Session s;
-  bool have_root = config::set_devspace_root();
-  Value cfg = Value::map();
-  try {
-    if (have_root) cfg = s.ctx.get();
-    s.kube = kube::Client::from_devspace_config(cfg, false);
-  } catch (const std::exception& e) {
-    log::fatal(e.what());
-  }
-  std::string ns = c.get_str("namespace").empty() ? config::default_namespace(cfg) : c.get_str("namespace");
-  Value pod;
-  try {
-    if (!c.get_str("pod").empty())
-      pod = s.kube->get("/api/v1/namespaces/" + ns + "/pods/" + c.get_str("pod"));
-    else
-      pod = s.kube->newest_running_pod(ns, c.get_str("label-selector"), 120000);
-  } catch (const std::exception& e) {
-    log::fatal(std::string("Unable to find pod: ") + e.what());
-  }
-  std::string container = c.get_str("container-name");
-  if (container.empty()) container = pod.at_path("spec.containers")[0].get("name").as_string();
   sync::Options o;
   o.watch_path = fs::abs_path(c.get_str("local"));
   o.dest_path = c.get_str("container");
-  o.pod_name = pod.at_path("metadata.name").as_string();
   o.exclude_paths = c.get_slice("exclude");
   o.verbose = c.get_bool("verbose");
   o.helper_path = helper_path();
   o.mode = sync::parse_mode(c.get_str("mode").empty() ? (fs::is_file(o.helper_path) ? "helper" : "fast")
                                                       : c.get_str("mode"));
-  auto transport = std::make_shared<kube::ExecTransport>(s.kube, pod, container);
+  if (c.get_int("idle-timeout")) o.idle_timeout_ms = (int)c.get_int("idle-timeout") * 1000;
+  std::shared_ptr<sync::Transport> transport;
+  std::string root = c.get_str("local-root");
+  if (!root.empty()) {
+    root = fs::abs_path(root);
+    fs::mkdirs(root);
+    o.pod_name = "local";
+    transport = std::make_shared<sync::LocalShellTransport>("", root);
+    o.reconnect = [root]() -> std::shared_ptr<sync::Transport> {
+      return std::make_shared<sync::LocalShellTransport>("", root);
+    };
+  } else {
+    Session s;
+    bool have_root = config::set_devspace_root();
+    Value cfg = Value::map();
+    try {
+      if (have_root) cfg = s.ctx.get();
+      s.kube = kube::Client::from_devspace_config(cfg, false);
+    } catch (const std::exception& e) {
+      log::fatal(e.what());
+    }
+    std::string ns = c.get_str("namespace").empty() ? config::default_namespace(cfg) : c.get_str("namespace");
+    std::string pod_name = c.get_str("pod"), sel = c.get_str("label-selector");
+    auto k = s.kube;
+    auto find_pod = [k, ns, pod_name, sel]() {
+      if (!pod_name.empty()) return k->get("/api/v1/namespaces/" + ns + "/pods/" + pod_name);
+      return k->newest_running_pod(ns, sel, 120000);
+    };
+    Value pod;
+    try {
+      pod = find_pod();
+    } catch (const std::exception& e) {
+      log::fatal(std::string("Unable to find pod: ") + e.what());
+    }
+    std::string container = c.get_str("container-name");
+    if (container.empty()) container = pod.at_path("spec.containers")[0].get("name").as_string();
+    o.pod_name = pod.at_path("metadata.name").as_string();
+    transport = std::make_shared<kube::ExecTransport>(k, pod, container);
+    o.reconnect = [k, find_pod, container]() -> std::shared_ptr<sync::Transport> {
+      return std::make_shared<kube::ExecTransport>(k, find_pod(), container);
+    };
+  }
+  if (c.get_int("fault-stdin-bytes") || c.get_int("fault-stdout-bytes")) {
+    sync::FaultPlan plan;
+    plan.kill_after_stdin_bytes = (size_t)c.get_int("fault-stdin-bytes");
+    plan.kill_after_stdout_bytes = (size_t)c.get_int("fault-stdout-bytes");
+    plan.only_shell = (int)c.get_int("fault-shell");
+    transport = std::make_shared<sync::FaultInjectingTransport>(transport, plan);
+  }
   sync::Session session(o, transport);
   try {
     session.start();
@@ -239,7 +269,7 @@ int run_sync(cli::Command& c, const Args&) {
   } catch (const std::exception& e) {
     log::fatal(std::string("Sync error: ") + e.what());
   }
-  log::done("Sync started on " + o.watch_path + " <-> " + o.dest_path + " (pod " + o.pod_name + ", mode " +
+  log::done("Sync started on " + o.watch_path + " <-> " + o.dest_path + " (pod " + session.pod_name() + ", mode " +
             sync::mode_name(session.effective_mode()) + ")");
   if (c.get_bool("once")) {
     session.stop();
@@ -329,7 +359,12 @@ void register_misc(cli::Command& root) {
         .str("mode", "", "", "Sync protocol: compat | fast | helper")
         .slice("exclude", "e", "Exclude paths (gitignore syntax)")
         .boolean("verbose", "", false, "Log every change")
-        .boolean("once", "", false, "Exit after the initial sync");
+        .boolean("once", "", false, "Exit after the initial sync")
+        .str("local-root", "", "", "Sync into a local directory that stands for the container's root (no cluster)")
+        .integer("idle-timeout", "", 0, "Seconds without data after which a stream counts as dead (default 120)")
+        .integer("fault-stdin-bytes", "", 0, "Test hook: kill the stream after this many bytes sent")
+        .integer("fault-stdout-bytes", "", 0, "Test hook: kill the stream after this many bytes received")
+        .integer("fault-shell", "", 1, "Test hook: which opened shell (1-based) gets the fault, 0 = all");
     c->run = run_sync;
     root.add(std::move(c));
   }

@@ -573,7 +573,14 @@ void init_image(config::Context& ctx, const std::string& docker_username_in, boo
       log::warn("No dockerhub credentials were found in the credentials store");
       log::warn("Please make sure you have a https://hub.docker.com account");
       log::warn("Installing docker is NOT required\n");
-      username = prompt::ask("What is your docker hub username?", "");
+      // a Docker Hub image needs an account namespace (the reference loops on docker login,
+      // configure/init_image.go:63-90): never fall through to an image named "/devspace"
+      for (int attempt = 0; attempt < 3 && username.empty(); ++attempt)
+        username = trim(prompt::ask("What is your docker hub username?", ""));
+      if (username.empty())
+        throw std::runtime_error(
+            "a Docker Hub username is required to push to Docker Hub (or answer the registry question with "
+            "another registry, e.g. a local one)");
       prompt::Params pw;
       pw.question = "What is your docker hub password?";
       pw.is_password = true;
@@ -619,6 +626,8 @@ void init_image(config::Context& ctx, const std::string& docker_username_in, boo
     q.validation_regex = "(yes|no)";
     pull_secret = prompt::ask(q) == "yes";
   }
+  std::string why = build::image_reference_problem(image);
+  if (!why.empty()) throw std::runtime_error("invalid image name \"" + image + "\": " + why);
   cfg["images"]["default"]["image"] = image;
   if (pull_secret) cfg["images"]["default"]["createPullSecret"] = true;
 }

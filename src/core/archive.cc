@@ -1,6 +1,7 @@
 // gzip + tar streams (sync/tar.go, util/tar/tar.go). Kept free of OpenSSL so the static
 // in-container helper (src/helper/helper.cc) can link it with only zlib.
 #include <fcntl.h>
+#include <stdlib.h>
 #include <unistd.h>
 #include <zlib.h>
 
@@ -86,47 +87,54 @@ GzipReader::~GzipReader() {
 }
 
 ssize_t GzipReader::read(char* out, size_t n) {
+  if (n == 0) return 0;
   z_stream* z = (z_stream*)z_;
+  if (single_ && stream_end_) return 0;
   z->next_out = (Bytef*)out;
   z->avail_out = (uInt)n;
   while (z->avail_out == n) {
+    if (stream_end_) {
+      // multi-member mode: another member may follow the one that just ended
+      if (z->avail_in == 0) {
+        if (eof_) return 0;
+        ssize_t r = src_(in_.data(), in_.size());
+        if (r < 0) return -1;
+        if (r == 0) {
+          eof_ = true;
+          return 0;
+        }
+        z->next_in = (Bytef*)in_.data();
+        z->avail_in = (uInt)r;
+      }
+      inflateReset(z);
+      stream_end_ = false;
+    }
     if (z->avail_in == 0) {
-      if (eof_) return stream_end_ ? 0 : -1;
+      if (eof_) return -1;  // the member is truncated
       ssize_t r = src_(in_.data(), in_.size());
       if (r < 0) return -1;
       if (r == 0) {
         eof_ = true;
-        if (stream_end_) return 0;
-        // try to flush what we have
+        return -1;
       }
       z->next_in = (Bytef*)in_.data();
-      z->avail_in = (uInt)(r > 0 ? r : 0);
-      if (r == 0 && !stream_end_) {
-        int rr = inflate(z, Z_SYNC_FLUSH);
-        if (rr == Z_STREAM_END) stream_end_ = true;
-        size_t got = n - z->avail_out;
-        return got > 0 ? (ssize_t)got : (stream_end_ ? 0 : -1);
-      }
-    }
-    if (stream_end_) {
-      // concatenated member?
-      if (z->avail_in > 0) {
-        inflateReset(z);
-        stream_end_ = false;
-      } else {
-        continue;
-      }
+      z->avail_in = (uInt)r;
     }
     int r = inflate(z, Z_NO_FLUSH);
     if (r == Z_STREAM_END) {
       stream_end_ = true;
-      if (n - z->avail_out > 0) break;
-      if (z->avail_in == 0 && eof_) return 0;
+      if (single_) break;  // never pull the source past the member
       continue;
     }
     if (r != Z_OK && r != Z_BUF_ERROR) return -1;
   }
   return (ssize_t)(n - z->avail_out);
+}
+
+std::string GzipReader::leftover() const {
+  z_stream* z = (z_stream*)z_;
+  if (!stream_end_ || z->avail_in == 0) return "";
+  return std::string((const char*)z->next_in, z->avail_in);
 }
 
 std::string gzip_compress(const std::string& data, int level) {
@@ -152,51 +160,102 @@ static double sample_entropy(const unsigned char* p, size_t n) {
   return h;
 }
 
+// deflate at level 1 runs ~20 MB/s on random bytes; stored blocks run at memcpy + CRC speed,
+// so a tree of model checkpoints is no longer compression-bound.
+static const size_t kAdaptiveChunk = 1 << 20, kEntropySample = 1 << 16;
+static const uint64_t kMaxMemberInput = 1ull << 30;
+
+AdaptiveGzipWriter::AdaptiveGzipWriter(Sink sink, int level)
+    : sink_(std::move(sink)), level_(level), cur_(level), out_(1 << 17) {
+  z_stream* z = new z_stream();
+  std::memset(z, 0, sizeof(*z));
+  if (deflateInit2(z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+    delete z;
+    throw std::runtime_error("deflateInit2 failed");
+  }
+  z_ = z;
+  buf_.reserve(kAdaptiveChunk);
+}
+
+AdaptiveGzipWriter::~AdaptiveGzipWriter() {
+  z_stream* z = (z_stream*)z_;
+  deflateEnd(z);
+  delete z;
+}
+
+bool AdaptiveGzipWriter::drain(int flush) {
+  z_stream* z = (z_stream*)z_;
+  int r;
+  do {
+    z->next_out = (Bytef*)out_.data();
+    z->avail_out = (uInt)out_.size();
+    r = deflate(z, flush);
+    if (r == Z_STREAM_ERROR) return false;
+    size_t have = out_.size() - z->avail_out;
+    if (have && !sink_(out_.data(), have)) return false;
+  } while (z->avail_out == 0 || (flush == Z_FINISH && r != Z_STREAM_END));
+  return true;
+}
+
+// Ends the current gzip member and starts a fresh deflate stream at `level`. Levels are never
+// switched inside one stream (deflateParams after >2 GiB of stored blocks crashes zlib 1.2.11),
+// and no member holds more than 1 GiB of input: the output is a series of gzip members, which
+// gunzip, `tar xz` (GNU and busybox) and GzipReader all read as one stream.
+bool AdaptiveGzipWriter::new_member(int level) {
+  z_stream* z = (z_stream*)z_;
+  if (member_in_ > 0) {
+    z->next_in = nullptr;
+    z->avail_in = 0;
+    if (!drain(Z_FINISH)) return false;
+  }
+  deflateEnd(z);
+  std::memset(z, 0, sizeof(*z));
+  if (deflateInit2(z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+  cur_ = level;
+  member_in_ = 0;
+  return true;
+}
+
+bool AdaptiveGzipWriter::deflate_chunk(bool last) {
+  z_stream* z = (z_stream*)z_;
+  if (!buf_.empty()) {
+    const unsigned char* p = (const unsigned char*)buf_.data();
+    int want = sample_entropy(p, std::min(buf_.size(), kEntropySample)) > 7.5 ? 0 : level_;
+    if ((want != cur_ || member_in_ >= kMaxMemberInput) && !new_member(want)) return false;
+  }
+  z->next_in = (Bytef*)buf_.data();
+  z->avail_in = (uInt)buf_.size();
+  member_in_ += buf_.size();
+  if (!drain(last ? Z_FINISH : Z_NO_FLUSH)) return false;
+  buf_.clear();
+  return true;
+}
+
+bool AdaptiveGzipWriter::write(const char* d, size_t n) {
+  if (finished_) return false;
+  while (n > 0) {
+    size_t take = std::min(n, kAdaptiveChunk - buf_.size());
+    buf_.append(d, take);
+    d += take;
+    n -= take;
+    if (buf_.size() == kAdaptiveChunk && !deflate_chunk(false)) return false;
+  }
+  return true;
+}
+
+bool AdaptiveGzipWriter::finish() {
+  if (finished_) return true;
+  finished_ = true;
+  return deflate_chunk(true);
+}
+
 std::string gzip_compress_adaptive(const std::string& data, int level) {
-  // One gzip member (any `tar xz` / gunzip reads it), compressed in 1 MiB chunks whose level
-  // follows their sampled entropy: stored blocks (level 0) for incompressible chunks, `level`
-  // otherwise. deflate at level 1 runs ~20 MB/s on random bytes; stored blocks run at memcpy +
-  // CRC speed, so a tree of model checkpoints is no longer compression-bound.
+  // one gzip member (any `tar xz` / gunzip reads it) whose level follows each chunk's entropy
   std::string out;
   out.reserve(data.size() / 2 + 1024);
-  z_stream z;
-  std::memset(&z, 0, sizeof(z));
-  if (deflateInit2(&z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK)
-    throw std::runtime_error("deflateInit2 failed");
-  std::vector<char> buf(1 << 17);
-  auto drain = [&](int flush) {
-    int r;
-    do {
-      z.next_out = (Bytef*)buf.data();
-      z.avail_out = (uInt)buf.size();
-      r = deflate(&z, flush);
-      out.append(buf.data(), buf.size() - z.avail_out);
-    } while (z.avail_out == 0 || (flush == Z_FINISH && r != Z_STREAM_END));
-  };
-  const size_t kChunk = 1 << 20, kSample = 1 << 16;
-  int cur = level;
-  for (size_t off = 0; off < data.size(); off += kChunk) {
-    size_t n = std::min(kChunk, data.size() - off);
-    const unsigned char* p = (const unsigned char*)data.data() + off;
-    int want = sample_entropy(p, std::min(n, kSample)) > 7.5 ? 0 : level;
-    if (want != cur) {
-      int r;
-      do {
-        z.next_out = (Bytef*)buf.data();
-        z.avail_out = (uInt)buf.size();
-        r = deflateParams(&z, want, Z_DEFAULT_STRATEGY);
-        out.append(buf.data(), buf.size() - z.avail_out);
-      } while (r == Z_BUF_ERROR);
-      cur = want;
-    }
-    z.next_in = (Bytef*)p;
-    z.avail_in = (uInt)n;
-    drain(Z_NO_FLUSH);
-  }
-  z.next_in = nullptr;
-  z.avail_in = 0;
-  drain(Z_FINISH);
-  deflateEnd(&z);
+  AdaptiveGzipWriter w(string_sink(&out), level);
+  w.write(data);
+  w.finish();
   return out;
 }
 
@@ -236,6 +295,103 @@ Source string_source(const std::string* in) {
     *pos += c;
     return (ssize_t)c;
   };
+}
+
+Source prefixed_source(std::string prefix, Source rest) {
+  auto pre = std::make_shared<std::string>(std::move(prefix));
+  auto pos = std::make_shared<size_t>(0);
+  return [pre, pos, rest](char* b, size_t n) -> ssize_t {
+    if (*pos < pre->size()) {
+      size_t c = std::min(n, pre->size() - *pos);
+      std::memcpy(b, pre->data() + *pos, c);
+      *pos += c;
+      return (ssize_t)c;
+    }
+    return rest(b, n);
+  };
+}
+
+Source limited_source(Source inner, uint64_t n) {
+  auto left = std::make_shared<uint64_t>(n);
+  return [inner, left](char* b, size_t k) -> ssize_t {
+    if (*left == 0) return 0;
+    ssize_t r = inner(b, (size_t)std::min<uint64_t>(k, *left));
+    if (r > 0) *left -= (uint64_t)r;
+    if (r == 0) return -1;  // the stream ended before the announced length
+    return r;
+  };
+}
+
+// ------------------------------------------------------------------ spill buffer
+
+SpillBuffer::SpillBuffer(size_t mem_limit, std::string dir) : limit_(mem_limit), dir_(std::move(dir)) {
+  if (dir_.empty()) {
+    const char* t = getenv("TMPDIR");
+    dir_ = t && *t ? t : "/tmp";
+  }
+}
+
+SpillBuffer::~SpillBuffer() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+bool SpillBuffer::flush_stage() {
+  if (stage_.empty()) return true;
+  if (!write_all(fd_, stage_.data(), stage_.size())) return false;
+  stage_.clear();
+  if (stage_.capacity() > (2u << 20)) std::string().swap(stage_);
+  return true;
+}
+
+bool SpillBuffer::append(const char* d, size_t n) {
+  size_ += n;
+  if (fd_ < 0) {
+    if (mem_.size() + n <= limit_) {
+      mem_.append(d, n);
+      return true;
+    }
+    // unlinked from the start: nothing is left behind whatever way the process ends
+    fd_ = ::open(dir_.c_str(), O_TMPFILE | O_RDWR | O_CLOEXEC, 0600);
+    if (fd_ < 0) {
+      std::string tmpl = dir_ + "/devspace-spill-XXXXXX";
+      fd_ = ::mkstemp(&tmpl[0]);
+      if (fd_ < 0) return false;
+      ::unlink(tmpl.c_str());
+    }
+    stage_.swap(mem_);
+    std::string().swap(mem_);
+  }
+  stage_.append(d, n);
+  if (stage_.size() >= (1u << 20)) return flush_stage();
+  return true;
+}
+
+bool SpillBuffer::replay(const Sink& out) {
+  const size_t kBlock = 1 << 20;
+  if (fd_ < 0) {
+    for (size_t off = 0; off < mem_.size(); off += kBlock)
+      if (!out(mem_.data() + off, std::min(kBlock, mem_.size() - off))) return false;
+    return true;
+  }
+  if (!flush_stage()) return false;
+  std::vector<char> buf(kBlock);
+  uint64_t off = 0;
+  while (off < size_) {
+    ssize_t r = ::pread(fd_, buf.data(), (size_t)std::min<uint64_t>(kBlock, size_ - off), (off_t)off);
+    if (r <= 0) return false;
+    if (!out(buf.data(), (size_t)r)) return false;
+    off += (uint64_t)r;
+  }
+  return true;
+}
+
+std::string SpillBuffer::head(size_t n) {
+  if (fd_ < 0) return mem_.substr(0, n);
+  if (!flush_stage()) return "";
+  std::string out(std::min<uint64_t>(n, size_), '\0');
+  ssize_t r = ::pread(fd_, &out[0], out.size(), 0);
+  out.resize(r > 0 ? (size_t)r : 0);
+  return out;
 }
 
 // ------------------------------------------------------------------ tar
@@ -446,6 +602,17 @@ bool TarReader::next(TarEntry* e) {
       // end-of-archive marker; drain the second block if present
       return false;
     }
+    // header checksum (unsigned, or signed as some old tars wrote it): garbage is an error,
+    // never a bogus entry
+    unsigned sum_u = 0;
+    int sum_s = 0;
+    for (int i = 0; i < 512; ++i) {
+      char c = (i >= 148 && i < 156) ? ' ' : h[i];
+      sum_u += (unsigned char)c;
+      sum_s += (signed char)c;
+    }
+    uint64_t stored = get_octal(h + 148, 8);
+    if (stored != sum_u && (int64_t)stored != (int64_t)sum_s) throw std::runtime_error("tar: invalid header checksum");
     TarEntry t;
     std::string name(h, strnlen(h, 100));
     std::string prefix;

@@ -56,12 +56,44 @@ class GzipWriter {
   bool finished_ = false;
 };
 
+// Streaming gzip whose deflate level adapts per 1 MiB chunk (sampled order-0 entropy): stored
+// blocks for incompressible chunks (checkpoints, archives, images), `level` elsewhere. A
+// standard gzip stream (a new member at each level change and every 1 GiB); memory is bounded
+// by the chunk buffer whatever the stream length.
+class AdaptiveGzipWriter {
+ public:
+  explicit AdaptiveGzipWriter(Sink sink, int level = 1);
+  ~AdaptiveGzipWriter();
+  AdaptiveGzipWriter(const AdaptiveGzipWriter&) = delete;
+  bool write(const char* d, size_t n);
+  bool write(const std::string& s) { return write(s.data(), s.size()); }
+  bool finish();
+
+ private:
+  bool deflate_chunk(bool last);
+  bool drain(int flush);
+  bool new_member(int level);
+  Sink sink_;
+  void* z_;
+  int level_, cur_;
+  uint64_t member_in_ = 0;
+  std::string buf_;
+  std::vector<char> out_;
+  bool finished_ = false;
+};
+
 // Streaming gzip decompressor pulling from a source (handles concatenated members).
 class GzipReader {
  public:
   explicit GzipReader(Source src);
   ~GzipReader();
   ssize_t read(char* out, size_t n);
+  // Single-member mode: stop at the end of the first gzip member and never read the source
+  // past it; bytes already pulled beyond the member are available from leftover(). Used when
+  // the member is followed by other protocol data on the same stream.
+  void set_single_member(bool on) { single_ = on; }
+  bool at_end() const { return stream_end_; }
+  std::string leftover() const;
 
  private:
   Source src_;
@@ -69,11 +101,47 @@ class GzipReader {
   std::vector<char> in_;
   bool eof_ = false;
   bool stream_end_ = false;
+  bool single_ = false;
 };
+
+// Byte buffer that stays in memory up to `mem_limit` and spills to an unlinked temp file
+// beyond it (sync/tar.go:146 writes every archive to a temp file; here only big ones are).
+// Lets protocols that must announce a length first (`head -c N`, the reference's fileSize=N
+// script) send multi-GB archives with bounded memory.
+class SpillBuffer {
+ public:
+  explicit SpillBuffer(size_t mem_limit = 8u << 20, std::string dir = "");
+  ~SpillBuffer();
+  SpillBuffer(const SpillBuffer&) = delete;
+  bool append(const char* d, size_t n);
+  Sink sink() {
+    return [this](const char* d, size_t n) { return append(d, n); };
+  }
+  uint64_t size() const { return size_; }
+  bool spilled() const { return fd_ >= 0; }
+  // Streams the whole content, from the start, to `out` in blocks of at most 1 MiB.
+  bool replay(const Sink& out);
+  // First bytes (for format sniffing); up to n.
+  std::string head(size_t n);
+
+ private:
+  bool flush_stage();
+  size_t limit_;
+  std::string dir_;
+  std::string mem_;    // content while not spilled
+  std::string stage_;  // write-behind buffer once spilled
+  int fd_ = -1;
+  uint64_t size_ = 0;
+};
+
+// Source that first returns `prefix`, then reads from `rest` (format sniffing without loss).
+Source prefixed_source(std::string prefix, Source rest);
+// Source limited to exactly `n` bytes of `inner` (returns 0 after that).
+Source limited_source(Source inner, uint64_t n);
 
 std::string gzip_compress(const std::string& data, int level = 6);
 // gzip whose deflate level adapts per 1 MiB chunk: stored blocks where the data is already
-// incompressible (sampled entropy), `level` elsewhere. Output is a standard gzip member.
+// incompressible (sampled entropy), `level` elsewhere (see AdaptiveGzipWriter).
 std::string gzip_compress_adaptive(const std::string& data, int level = 1);
 std::string gzip_decompress(const std::string& data);
 
@@ -108,7 +176,8 @@ class TarWriter {
 class TarReader {
  public:
   explicit TarReader(Source src) : src_(std::move(src)) {}
-  // Returns false at end of archive; throws on corrupt input.
+  // Returns false at end of archive; throws on corrupt input (bad header checksum, EOF inside
+  // an entry).
   bool next(TarEntry* e);
   // Read file data of the current entry; returns 0 when exhausted.
   ssize_t read(char* out, size_t n);

@@ -2,18 +2,23 @@
 //
 // Replaces the reference's per-operation shell scripts (sync/upstream.go:387, downstream.go:373)
 // and the 1.3 s full `find` poll with a persistent process speaking a framed protocol on
-// stdin/stdout and pushing inotify change notifications on stderr:
+// stdin/stdout and pushing inotify change notifications on stderr (framing: src/sync/frame.h):
 //
-//   request  := op:u8  len:u32be  payload[len]
-//   'U' payload=tar.gz          -> extract under <dest> (tar xzpf semantics)   reply "OK\n" | "ERR msg\n"
+//   request := op:u8 len:u64be payload[len]
+//   'U' (len 0) + chunk stream of a tar (or tar.gz) -> extract under <dest>   reply "OK\n" | "ERR msg\n"
 //   'R' payload=rel\n...        -> rm -rf <dest><rel>                          reply "OK\n"
 //   'S' (empty)                 -> "<abs>///size,mtime,hexmode,perm,uid,gid\n"... then "DONE\n"
-//   'D' payload=rel\n...        -> "SIZE n\n" + n bytes tar.gz (relative member names)
+//   'D' payload=rel\n...        -> "STREAM\n" + chunk stream of a tar (relative member names)
+//                                  + "OK\n"
 //   'H' payload=rel\n...        -> one crc32 hex (or "-") per path, then "DONE\n"
-//   'W' (empty)                 -> start watching; "E\n" on stderr after changes settle
+//   'W' (empty)                 -> start watching; "E\n" on stderr after foreign changes settle
 //   'Q'                          -> exit
 //
-// Built with -static so it runs in any x86_64 container image (no libc/zlib dependency).
+// Archives are streamed through fixed-size buffers in both directions, so memory stays bounded
+// for files of any size (a multi-GB checkpoint written in a training pod is read and sent in
+// 1 MiB pieces; the helper shares the pod's memory cgroup). Extraction writes each file to a
+// temp name and renames it into place, so an interrupted transfer never leaves a truncated
+// file at the real path. Built with -static so it runs in any x86_64 container image.
 #include <fcntl.h>
 #include <poll.h>
 #include <signal.h>
@@ -38,10 +43,13 @@
 #include "core/fs.h"
 #include "core/proc.h"
 #include "core/strutil.h"
+#include "sync/frame.h"
 
 using namespace ds;
+namespace frame = ds::sync::frame;
 
 static std::string g_dest;
+static const char* kTmpSuffix = ".devspace-tmp";
 
 static long now_us() {
   struct timespec ts;
@@ -49,11 +57,20 @@ static long now_us() {
   return ts.tv_sec * 1000000L + ts.tv_nsec / 1000;
 }
 
-// Paths this helper itself wrote or removed (upstream ops), so their inotify echo does not
-// trigger a downstream scan, while changes the pod makes to any other path — even during an
-// upload — still do. Entries live while an op runs and for kOwnEchoUs after it finished.
+// What this helper itself wrote or removed (upstream ops), so the inotify echo of its own
+// writes does not trigger a downstream scan. An event counts as our own only while the path
+// still holds exactly what we left there (same kind, size and mtime for files; absent for
+// removals): a pod process that rewrites a file it just received — a formatter, a code
+// generator — changes size or mtime and is reported at once. Records live while an op runs
+// and for kOwnEchoUs after it finished (the echo of a write arrives within milliseconds).
+struct OwnRecord {
+  enum Kind { File, Dir, Link, Gone } kind = File;
+  int64_t size = 0;
+  int64_t mtime = 0;  // seconds; written files carry nsec 0 (tar resolution)
+};
 static std::mutex g_own_mu;
-static std::set<std::string> g_own, g_own_trees;
+static std::map<std::string, OwnRecord> g_own;
+static std::set<std::string> g_gone_trees;  // removed subtrees: anything absent below is ours
 static long g_own_until = 0;  // monotonic us; LONG_MAX while an op runs
 static const long kOwnEchoUs = 2000000;
 
@@ -72,31 +89,57 @@ struct OwnOp {  // own_begin/own_end around one upstream op, exceptions included
   ~OwnOp() { own_end(); }
 };
 
-static void own_path(const std::string& p) {
+static void own_record(const std::string& p, OwnRecord r) {
   std::lock_guard<std::mutex> g(g_own_mu);
   if (!starts_with(p, g_dest)) return;
-  for (std::string q = p;; q = fs::dirname(q)) {
-    if (!g_own.insert(q).second) break;  // ancestors already recorded
-    if (q.size() <= g_dest.size()) break;  // dest itself (its own IN_ATTRIB echo) included
+  g_own[p] = r;
+  // ancestors get IN_ATTRIB / IN_CREATE echoes while we write below them
+  for (std::string q = fs::dirname(p); q.size() >= g_dest.size() && starts_with(q, g_dest); q = fs::dirname(q)) {
+    auto it = g_own.find(q);
+    if (it != g_own.end() && it->second.kind == OwnRecord::Dir) break;
+    OwnRecord d;
+    d.kind = OwnRecord::Dir;
+    g_own[q] = d;
+    if (q.size() == g_dest.size()) break;
   }
 }
 
-static void own_subtree(const std::string& p) {
-  own_path(p);
+static void own_gone_tree(const std::string& p) {
+  OwnRecord r;
+  r.kind = OwnRecord::Gone;
+  own_record(p, r);
   std::lock_guard<std::mutex> g(g_own_mu);
-  g_own_trees.insert(p);
+  g_gone_trees.insert(p);
+}
+
+static bool matches(const OwnRecord& r, const std::string& p) {
+  struct stat st;
+  bool exists = ::lstat(p.c_str(), &st) == 0;
+  switch (r.kind) {
+    case OwnRecord::Gone: return !exists;
+    case OwnRecord::Dir: return exists && S_ISDIR(st.st_mode);
+    case OwnRecord::Link: return exists && S_ISLNK(st.st_mode);
+    case OwnRecord::File:
+      return exists && S_ISREG(st.st_mode) && st.st_size == r.size && st.st_mtim.tv_sec == r.mtime &&
+             st.st_mtim.tv_nsec == 0;
+  }
+  return false;
 }
 
 static bool is_own(const std::string& p) {
   std::lock_guard<std::mutex> g(g_own_mu);
   if (now_us() > g_own_until) {
     g_own.clear();
-    g_own_trees.clear();
+    g_gone_trees.clear();
     return false;
   }
-  if (g_own.count(p)) return true;
+  auto it = g_own.find(p);
+  if (it != g_own.end()) return matches(it->second, p);
   for (std::string q = p; q.size() > g_dest.size(); q = fs::dirname(q))
-    if (g_own_trees.count(q)) return true;
+    if (g_gone_trees.count(q)) {
+      struct stat st;
+      return ::lstat(p.c_str(), &st) != 0;
+    }
   return false;
 }
 
@@ -109,18 +152,28 @@ static std::string safe_join(const std::string& rel_in) {
   return c == "/" ? g_dest : g_dest + c;
 }
 
-static std::string op_extract(const std::string& payload) {
-  // gzip or plain tar (small edits are shipped uncompressed)
-  bool gzipped = payload.size() >= 2 && (unsigned char)payload[0] == 0x1f && (unsigned char)payload[1] == 0x8b;
-  GzipReader gz(string_source(&payload));
-  Source raw = string_source(&payload);
+// Extracts a (gzip-or-plain) tar stream under g_dest with `tar xpf` semantics.
+static std::string op_extract(Source src) {
+  // sniff gzip vs plain tar (small edits are shipped uncompressed)
+  std::string magic;
+  char m[2];
+  while (magic.size() < 2) {
+    ssize_t n = src(m, 2 - magic.size());
+    if (n <= 0) break;
+    magic.append(m, (size_t)n);
+  }
+  if (magic.empty()) return "OK";
+  bool gzipped = magic.size() == 2 && (unsigned char)magic[0] == 0x1f && (unsigned char)magic[1] == 0x8b;
+  Source raw = prefixed_source(magic, src);
+  GzipReader gz(raw);
   TarReader tr([&](char* b, size_t n) { return gzipped ? gz.read(b, n) : raw(b, n); });
   TarEntry e;
   bool root = ::geteuid() == 0;
+  std::string tmp;
+  std::vector<char> buf(1 << 20);
   try {
     while (tr.next(&e)) {
       std::string out = safe_join(e.name);
-      own_path(out);
       if (e.type == '5') {
         fs::mkdirs(out, 0755);
         ::chmod(out.c_str(), e.mode & 07777);
@@ -129,6 +182,9 @@ static std::string op_extract(const std::string& payload) {
           (void)ignored;
         }
         fs::set_mtime(out, e.mtime);
+        OwnRecord r;
+        r.kind = OwnRecord::Dir;
+        own_record(out, r);
         continue;
       }
       if (e.type == '2') {
@@ -136,6 +192,9 @@ static std::string op_extract(const std::string& payload) {
         ::unlink(out.c_str());
         int ignored = ::symlink(e.linkname.c_str(), out.c_str());
         (void)ignored;
+        OwnRecord r;
+        r.kind = OwnRecord::Link;
+        own_record(out, r);
         continue;
       }
       if (e.type != '0' && e.type != '7') {
@@ -143,16 +202,21 @@ static std::string op_extract(const std::string& payload) {
         continue;
       }
       fs::mkdirs(fs::dirname(out));
-      std::string tmp = out + ".devspace-tmp";
+      tmp = out + kTmpSuffix;
       int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0600);
-      if (fd < 0) return std::string("ERR open ") + out + ": " + std::strerror(errno);
-      char buf[1 << 16];
+      if (fd < 0) {
+        std::string err = std::string("ERR open ") + out + ": " + std::strerror(errno);
+        tmp.clear();
+        return err;
+      }
       while (true) {
-        ssize_t n = tr.read(buf, sizeof(buf));
+        ssize_t n = tr.read(buf.data(), buf.size());
         if (n <= 0) break;
-        if (!write_all(fd, buf, (size_t)n)) {
+        if (!write_all(fd, buf.data(), (size_t)n)) {
+          std::string err = std::string("ERR write ") + out + ": " + std::strerror(errno);
           ::close(fd);
-          return "ERR write " + out;
+          ::unlink(tmp.c_str());
+          return err;
         }
       }
       ::fchmod(fd, e.mode & 07777);
@@ -162,30 +226,60 @@ static std::string op_extract(const std::string& payload) {
       }
       ::close(fd);
       fs::set_mtime(tmp, e.mtime);
+      OwnRecord r;
+      r.size = e.size;
+      r.mtime = e.mtime;
+      own_record(out, r);  // before the rename: its IN_MOVED_TO echo must find the record
       if (::rename(tmp.c_str(), out.c_str()) != 0) {
         // target may be a directory being replaced by a file
         fs::remove_all(out);
-        if (::rename(tmp.c_str(), out.c_str()) != 0) return "ERR rename " + out;
+        if (::rename(tmp.c_str(), out.c_str()) != 0) {
+          ::unlink(tmp.c_str());
+          return "ERR rename " + out;
+        }
       }
+      tmp.clear();
     }
   } catch (const std::exception& ex) {
+    if (!tmp.empty()) ::unlink(tmp.c_str());  // never leave a partial file behind
     return std::string("ERR ") + ex.what();
   }
   return "OK";
 }
 
-static void scan_rec(const std::string& p, std::string& out, std::set<std::pair<uint64_t, uint64_t>>& seen,
-                     int depth) {
+// Buffered stdout writer for listings of any size.
+struct OutBuf {
+  std::string b;
+  bool ok = true;
+  void put(const std::string& s) {
+    b += s;
+    if (b.size() >= (256u << 10)) flush();
+  }
+  void flush() {
+    if (ok && !b.empty()) ok = write_all(1, b);
+    b.clear();
+  }
+};
+
+static void scan_rec(const std::string& p, OutBuf& out, std::set<std::pair<uint64_t, uint64_t>>& seen, int depth) {
   struct stat lst;
   if (::lstat(p.c_str(), &lst) != 0) return;
+  if (ends_with(p, kTmpSuffix)) {
+    // a transfer in progress (its ctime moves with every write) or one cut off when a helper
+    // was killed mid-upload: the latter is removed once it has been still for two minutes
+    struct timespec now;
+    clock_gettime(CLOCK_REALTIME, &now);
+    if (S_ISREG(lst.st_mode) && now.tv_sec - lst.st_ctim.tv_sec > 120) ::unlink(p.c_str());
+    return;
+  }
   struct stat st = lst;
   if (S_ISLNK(lst.st_mode)) {
     if (::stat(p.c_str(), &st) != 0) st = lst;
   }
   // like `find -L ... -exec stat -c` : stat of the path itself (links reported as links)
-  out += p + "///" + std::to_string((long long)lst.st_size) + "," + std::to_string((long long)lst.st_mtim.tv_sec) +
-         "," + strfmt("%x", (unsigned)lst.st_mode) + "," + strfmt("%o", (unsigned)(lst.st_mode & 07777)) + "," +
-         std::to_string(lst.st_uid) + "," + std::to_string(lst.st_gid) + "\n";
+  out.put(p + "///" + std::to_string((long long)lst.st_size) + "," + std::to_string((long long)lst.st_mtim.tv_sec) +
+          "," + strfmt("%x", (unsigned)lst.st_mode) + "," + strfmt("%o", (unsigned)(lst.st_mode & 07777)) + "," +
+          std::to_string(lst.st_uid) + "," + std::to_string(lst.st_gid) + "\n");
   if (S_ISDIR(st.st_mode) && depth < 128) {
     auto key = std::make_pair((uint64_t)st.st_dev, (uint64_t)st.st_ino);
     if (seen.count(key)) return;
@@ -194,13 +288,13 @@ static void scan_rec(const std::string& p, std::string& out, std::set<std::pair<
   }
 }
 
-static std::string op_scan() {
+static void op_scan() {
   fs::mkdirs(g_dest);
-  std::string out;
+  OutBuf out;
   std::set<std::pair<uint64_t, uint64_t>> seen;
   scan_rec(g_dest, out, seen, 0);
-  out += "DONE\n";
-  return out;
+  out.put("DONE\n");
+  out.flush();
 }
 
 static void op_remove(const std::string& payload) {
@@ -208,16 +302,21 @@ static void op_remove(const std::string& payload) {
     if (rel.empty()) continue;
     std::string p = safe_join(rel);
     if (p == g_dest) continue;
-    own_subtree(p);
+    own_gone_tree(p);
     fs::remove_all(p);
   }
 }
 
-static std::string op_download(const std::string& payload) {
-  std::string raw;
-  TarWriter tw(string_sink(&raw));
+// 'D': streams the requested files as one tar.gz, chunk-framed, while reading them.
+static void op_download(const std::string& payload) {
+  if (!reply("STREAM\n")) return;
+  // checkpoints and other binaries written in the pod are incompressible: those chunks go out
+  // as they are, text chunks raw-deflated (frame::ChunkWriter), no gzip CRC pass
+  frame::ChunkWriter cw(fd_sink(1), frame::kMaxChunk, 1);
+  TarWriter tw(cw.sink());
+  bool ok = true;
   for (auto& rel : split(payload, "\n")) {
-    if (rel.empty()) continue;
+    if (rel.empty() || !ok) continue;
     std::string p = safe_join(rel);
     fs::StatInfo st = fs::stat(p);
     if (!st.exists || st.is_dir) continue;
@@ -228,12 +327,14 @@ static std::string op_download(const std::string& payload) {
     e.gid = st.gid;
     e.size = st.size;
     e.mtime = st.mtime_sec;
-    tw.add_file_from_path(e, p);
+    if (!tw.add_file_from_path(e, p)) {
+      // unreadable or vanished before open: skip it (the header may already be out, padded
+      // with zeros by add_file_from_path when the file shrank)
+      continue;
+    }
   }
-  tw.finish();
-  // checkpoints and other binaries written in the pod are incompressible: stored blocks for
-  // those chunks instead of deflate at ~20 MB/s
-  return gzip_compress_adaptive(raw, 1);
+  ok = tw.finish() && cw.finish();
+  if (ok) reply("OK\n");
 }
 
 // 'H': CRC-32 of files (initial sync: tells identical copies from changed files when mtimes
@@ -299,7 +400,7 @@ static void watch_loop() {
         if (it == wds.end()) continue;
         std::string path = name.empty() ? it->second : it->second + "/" + name;
         if ((ev->mask & IN_ISDIR) && (ev->mask & (IN_CREATE | IN_MOVED_TO))) add_watch_rec(fd, path, wds, 0);
-        if (ends_with(name, ".devspace-tmp") || is_own(path)) continue;
+        if (ends_with(name, kTmpSuffix) || is_own(path)) continue;
         foreign = true;
       }
       return foreign;
@@ -328,25 +429,38 @@ int main(int argc, char** argv) {
   fs::mkdirs(g_dest);
   reply("HELPER READY\n");
   bool watching = false;
+  Source in = fd_source(0);
   while (true) {
-    unsigned char hdr[5];
-    if (!read_exact(0, hdr, 5)) break;
-    uint32_t len = ((uint32_t)hdr[1] << 24) | ((uint32_t)hdr[2] << 16) | ((uint32_t)hdr[3] << 8) | hdr[4];
-    std::string payload(len, '\0');
-    if (len && !read_exact(0, &payload[0], len)) break;
-    switch (hdr[0]) {
-      case 'U': {
-        std::string r;
-        {
-          OwnOp op;  // the echo of our own extraction is ignored while it runs and shortly after
-          r = op_extract(payload);
+    unsigned char hdr[frame::kHeaderSize];
+    if (!read_exact(0, hdr, sizeof(hdr))) break;
+    char op;
+    uint64_t len;
+    frame::parse_header(hdr, &op, &len);
+    if (op == 'U') {
+      std::string r;
+      {
+        OwnOp own;  // the echo of our own extraction is ignored while it runs and shortly after
+        frame::ChunkReader cr(in);
+        try {
+          r = op_extract(cr.source());
+          cr.drain();  // an early error still consumes the whole stream: framing stays in step
+        } catch (const std::exception& ex) {
+          return 1;  // the stream itself is broken (sender gone): nothing left to reply to
         }
-        reply(r + "\n");
-        break;
       }
+      reply(r + "\n");
+      continue;
+    }
+    if (len > frame::kMaxListPayload) {
+      std::fprintf(stderr, "devspace-helper: request payload of %llu bytes refused\n", (unsigned long long)len);
+      return 1;
+    }
+    std::string payload((size_t)len, '\0');
+    if (len && !read_exact(0, &payload[0], (size_t)len)) break;
+    switch (op) {
       case 'R': {
         {
-          OwnOp op;
+          OwnOp own;
           try {
             op_remove(payload);
           } catch (const std::exception&) {
@@ -357,14 +471,9 @@ int main(int argc, char** argv) {
         reply("OK\n");
         break;
       }
-      case 'S': reply(op_scan()); break;
+      case 'S': op_scan(); break;
       case 'H': reply(op_hash(payload)); break;
-      case 'D': {
-        std::string a = op_download(payload);
-        reply("SIZE " + std::to_string(a.size()) + "\n");
-        write_all(1, a);
-        break;
-      }
+      case 'D': op_download(payload); break;
       case 'W':
         // one watch loop per helper process (a detached thread is never joinable again, so
         // joinable() cannot be the guard); it ends with the process

@@ -786,6 +786,7 @@ void ExecSession::pump_in() {
     }
     if (!ws_->send(std::string(buf, (size_t)n + 1))) break;
   }
+  in_r_.reset();  // the stream is gone: writers get EPIPE instead of blocking on a full pipe
 }
 
 void ExecSession::pump_out() {

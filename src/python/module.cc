@@ -16,6 +16,7 @@
 #include "core/match.h"
 #include "core/value.h"
 #include "core/watch.h"
+#include "sync/frame.h"
 #include "sync/sync.h"
 
 namespace py = pybind11;
@@ -272,6 +273,17 @@ PYBIND11_MODULE(_native, m) {
     return DockerIgnore(pats).matches(path);
   });
   m.def("glob_match", &glob_match);
+  m.def("frame_header", [](const std::string& op, uint64_t len) {
+    return py::bytes(sync::frame::header(op.empty() ? '\0' : op[0], len));
+  });
+  m.def("frame_parse", [](py::bytes b) {
+    std::string h(b);
+    if (h.size() != sync::frame::kHeaderSize) throw std::invalid_argument("frame header must be 9 bytes");
+    char op;
+    uint64_t len;
+    sync::frame::parse_header((const unsigned char*)h.data(), &op, &len);
+    return py::make_tuple(std::string(1, op), len);
+  });
   m.def("parse_config", [](py::object data) { return to_py(config::parse_versioned(from_py(data))); });
   m.def("copy_to_container",
         [](const std::string& local, const std::string& container, std::vector<std::string> excludes,

@@ -1,16 +1,21 @@
 #include "sync/sync.h"
 
+#include <fcntl.h>
+#include <poll.h>
 #include <signal.h>
+#include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
 
 #include "core/strutil.h"
 #include "core/trace.h"
+#include "sync/frame.h"
 
 namespace ds {
 namespace sync {
@@ -18,6 +23,7 @@ namespace sync {
 static const char* kStart = "START";
 static const char* kDone = "DONE";
 static const char* kError = "ERROR";
+static const char* kTmpSuffix = ".devspace-tmp";  // in-flight files (helper and local untar)
 static const size_t kInitialUpstreamBatch = 1000;  // sync_config.go:20
 
 static long mono_us() {
@@ -179,6 +185,11 @@ void Session::setup() {
       poll_ms_ = 10000;
       break;
   }
+  if (o_.large_file_warn_bytes >= 0) {
+    large_warn_bytes_ = o_.large_file_warn_bytes;
+  } else if (const char* mb = getenv("DEVSPACE_SYNC_WARN_FILE_MB")) {
+    large_warn_bytes_ = std::atoll(mb) << 20;
+  }
   if (o_.upstream_window_ms >= 0) window_ms_ = o_.upstream_window_ms;
   if (o_.downstream_poll_ms >= 0) poll_ms_ = o_.downstream_poll_ms;
   dest_ = remote(o_.dest_path);
@@ -186,21 +197,110 @@ void Session::setup() {
 
 // ============================================================ helper bootstrap
 
-static void put_u32(std::string& s, uint32_t v) {
-  s.push_back((char)(v >> 24));
-  s.push_back((char)(v >> 16));
-  s.push_back((char)(v >> 8));
-  s.push_back((char)v);
+using frame::request;
+
+// Sniffs gzip (0x1f 0x8b) vs plain tar.
+static bool is_gzip_magic(const std::string& m) {
+  return m.size() >= 2 && (unsigned char)m[0] == 0x1f && (unsigned char)m[1] == 0x8b;
 }
 
-static std::string frame(char op, const std::string& payload) {
-  std::string f;
-  f.reserve(payload.size() + 5);
-  f.push_back(op);
-  put_u32(f, (uint32_t)payload.size());
-  f += payload;
-  return f;
+// tar bytes -> wire bytes for the shell protocols (`tar x` / `tar xz` in the container): plain
+// tar while the archive is small (latency-bound edits: no gzip on either side) or when its
+// first MiB is incompressible (checkpoints: gzip would only add CRC + framing work on both
+// ends), gzip otherwise — adaptive, so incompressible chunks later in the stream go out as
+// stored blocks. plain_limit 0 = always gzip (the reference's protocol).
+class ArchiveEncoder {
+ public:
+  ArchiveEncoder(Sink out, size_t plain_limit, int level) : out_(std::move(out)), limit_(plain_limit), level_(level) {}
+  bool write(const char* d, size_t n) {
+    if (gz_) return gz_->write(d, n);
+    if (plain_) return out_(d, n);
+    pending_.append(d, n);
+    if (limit_ == 0 || pending_.size() >= kDecideBytes) return decide();
+    return true;
+  }
+  Sink sink() {
+    return [this](const char* d, size_t n) { return write(d, n); };
+  }
+  bool finish() {
+    if (!gz_ && !plain_) {
+      if (limit_ > 0 && pending_.size() <= limit_) {
+        plain_ = true;
+        return pending_.empty() || out_(pending_.data(), pending_.size());
+      }
+      if (!decide()) return false;
+    }
+    return gz_ ? gz_->finish() : true;
+  }
+  bool gzipped() const { return gz_ != nullptr; }
+
+ private:
+  static const size_t kDecideBytes = 1 << 20;
+  bool decide() {
+    if (limit_ > 0 && entropy(pending_) > 7.2) {
+      plain_ = true;
+    } else {
+      gz_ = std::make_unique<AdaptiveGzipWriter>(out_, level_);
+    }
+    bool ok = gz_ ? gz_->write(pending_) : out_(pending_.data(), pending_.size());
+    std::string().swap(pending_);
+    return ok;
+  }
+  static double entropy(const std::string& d) {
+    uint32_t hist[256] = {0};
+    for (unsigned char c : d) hist[c]++;
+    double h = 0;
+    for (uint32_t c : hist)
+      if (c) h -= (double)c / (double)d.size() * std::log2((double)c / (double)d.size());
+    return h;
+  }
+  Sink out_;
+  size_t limit_;
+  int level_;
+  bool plain_ = false;
+  std::string pending_;
+  std::unique_ptr<AdaptiveGzipWriter> gz_;
+};
+
+static const size_t kPlainTarLimit = 256 * 1024;
+static const uint64_t kProgressMin = 64ull << 20;
+
+static std::string human_bytes(uint64_t b) {
+  if (b >= (1ull << 30)) return strfmt("%.2f GiB", (double)b / (double)(1ull << 30));
+  if (b >= (1ull << 20)) return strfmt("%.1f MiB", (double)b / (double)(1ull << 20));
+  if (b >= 1024) return strfmt("%.1f KiB", (double)b / 1024.0);
+  return strfmt("%llu B", (unsigned long long)b);
 }
+
+// Progress lines in sync.log for big transfers (every 5 s, and a summary at the end).
+struct Session::Progress {
+  Session* s;
+  std::string what;
+  uint64_t total;  // 0 = unknown
+  uint64_t done = 0;
+  long start_us, last_us;
+  Progress(Session* sess, std::string w, uint64_t t) : s(sess), what(std::move(w)), total(t) {
+    start_us = last_us = mono_us();
+  }
+  void add(size_t n) {
+    done += n;
+    long now = mono_us();
+    if (now - last_us < 5000000 || done < kProgressMin) return;
+    last_us = now;
+    double mbps = (double)done / 1e6 / ((double)(now - start_us) / 1e6);
+    if (total)
+      s->logf(strfmt("%s: %s / %s (%.0f%%, %.0f MB/s)", what.c_str(), human_bytes(done).c_str(),
+                     human_bytes(total).c_str(), 100.0 * (double)done / (double)total, mbps));
+    else
+      s->logf(strfmt("%s: %s (%.0f MB/s)", what.c_str(), human_bytes(done).c_str(), mbps));
+  }
+  void finish() {
+    if (done < kProgressMin) return;
+    double secs = (double)(mono_us() - start_us) / 1e6;
+    s->logf(strfmt("%s: %s in %.1f s (%.0f MB/s)", what.c_str(), human_bytes(done).c_str(), secs,
+                   (double)done / 1e6 / std::max(secs, 1e-6)));
+  }
+};
 
 bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out) {
   // Probe architecture + writable /tmp, upload the static helper once (content-addressed),
@@ -246,6 +346,7 @@ void Session::open_up_shell() {
     }
   }
   up_has_head_ = false;
+  set_nonblocking(up_shell_->in(), true);
   if (mode_ != Mode::Compat && !up_helper_) {
     // create the destination once instead of per upload, and check for `head` (the streamed
     // upload needs `head -c`; without it uploads use the reference's cat + stat protocol)
@@ -273,7 +374,7 @@ void Session::open_down_shell() {
       down_err_.reset(down_shell_->err());
     } else {
       // subscribe to container-side change events (pushed on stderr)
-      write_all(down_shell_->in(), frame('W', ""));
+      write_all(down_shell_->in(), request('W', ""));
     }
   }
 }
@@ -439,6 +540,7 @@ void Session::start_watcher() {
 }
 
 std::optional<FileInfo> Session::evaluate_change(const std::string& rel, const std::string& abs) {
+  if (ends_with(rel, kTmpSuffix)) return std::nullopt;  // a download in progress
   fs::StatInfo st = fs::stat(abs);
   if (st.exists) {
     if (has_upload_ignore_ && upload_ignore_.matches(rel)) {
@@ -602,13 +704,74 @@ void Session::apply_upstream(std::vector<FileInfo>& changes, long first_event_us
 
 bool Session::wait_ack(LineReader& r, const std::string& keyword, bool partial, std::string* before,
                        int timeout_ms) {
-  long deadline = mono_us() + (long)timeout_ms * 1000;
+  // idle timeout: any byte received (e.g. listing lines before the keyword) restarts it
+  long start = mono_us();
   while (!stopping_) {
     if (r.wait_for(keyword, 200, before, partial)) return true;
     if (r.eof()) throw SyncError("stream closed unexpectedly while waiting for " + keyword);
-    if (mono_us() > deadline) throw SyncError("timeout waiting for " + keyword);
+    if (mono_us() - std::max(start, r.last_activity_us()) > (long)timeout_ms * 1000)
+      throw SyncError(strfmt("no data for %d s while waiting for %s", timeout_ms / 1000, keyword.c_str()));
   }
   throw SyncError("sync stopped");
+}
+
+void Session::send(int fd, const char* d, size_t n) {
+  // the shell's stdin is non-blocking on our side (open_*_shell): a container that stops
+  // reading is detected after the idle timeout instead of blocking this thread for ever
+  long last = mono_us();
+  while (n > 0) {
+    ssize_t w = ::write(fd, d, n);
+    if (w > 0) {
+      d += w;
+      n -= (size_t)w;
+      last = mono_us();
+      continue;
+    }
+    if (w < 0 && errno == EINTR) continue;
+    if (w < 0 && errno != EAGAIN) throw SyncError(std::string("stream closed while sending: ") + std::strerror(errno));
+    if (stopping_) throw SyncError("sync stopped");
+    if (mono_us() - last > (long)o_.idle_timeout_ms * 1000)
+      throw SyncError(strfmt("the container accepted no data for %d s", o_.idle_timeout_ms / 1000));
+    struct pollfd pf{fd, POLLOUT, 0};
+    ::poll(&pf, 1, 200);
+  }
+}
+
+std::string Session::read_line_idle(LineReader& r, int idle_ms, const char* what) {
+  long start = mono_us();
+  std::string line;
+  while (true) {
+    if (r.read_line(&line, 200)) return line;
+    if (r.eof()) throw SyncError(std::string(what) + ": stream closed");
+    if (stopping_) throw SyncError("sync stopped");
+    if (mono_us() - std::max(start, r.last_activity_us()) > (long)idle_ms * 1000)
+      throw SyncError(strfmt("%s: no data for %d s", what, idle_ms / 1000));
+  }
+}
+
+Source Session::reader_source(LineReader& r, int idle_ms, const char* what) {
+  std::string w = what;
+  return [this, &r, idle_ms, w](char* b, size_t n) -> ssize_t {
+    long start = mono_us();
+    while (true) {
+      ssize_t got = r.read_some(b, n, 200);
+      if (got > 0) return got;
+      if (got == 0 || got == -1) throw SyncError(w + ": stream closed");
+      if (stopping_) throw SyncError("sync stopped");
+      if (mono_us() - std::max(start, r.last_activity_us()) > (long)idle_ms * 1000)
+        throw SyncError(strfmt("%s: no data for %d s", w.c_str(), idle_ms / 1000));
+    }
+  };
+}
+
+void Session::warn_large(const std::string& rel, int64_t size) {
+  if (large_warn_bytes_ <= 0 || size < large_warn_bytes_ || !warned_large_.insert(rel).second) return;
+  std::string msg = strfmt(
+      "[Sync] Large file %s (%s) is being synced; if it should stay on one side, add it to excludePaths "
+      "(or uploadExcludePaths / downloadExcludePaths) of this sync path",
+      rel.c_str(), human_bytes((uint64_t)size).c_str());
+  logf(msg);
+  if (!o_.silent) log::warn(msg);
 }
 
 void Session::apply_removes(const std::vector<FileInfo>& files) {
@@ -632,7 +795,7 @@ void Session::apply_removes(const std::vector<FileInfo>& files) {
     }
     if (args.empty()) continue;
     if (up_helper_) {
-      if (!write_all(up_shell_->in(), frame('R', helper_payload))) throw SyncError("upstream: write failed");
+      if (!write_all(up_shell_->in(), request('R', helper_payload))) throw SyncError("upstream: write failed");
       wait_ack(up_out_, "OK", false);
     } else if (mode_ == Mode::Compat) {
       std::string cmd = "rm -R " + join(args, " ") + "  >/dev/null 2>/dev/null && printf \"" + kDone +
@@ -649,14 +812,11 @@ void Session::apply_removes(const std::vector<FileInfo>& files) {
 
 void Session::recursive_tar(const std::string& rel, std::map<std::string, FileInfo>* written, TarWriter* tw,
                             int depth) {
+  // index lock held by the caller (stream_upload)
   if (depth > 64 || written->count(rel)) return;
-  bool excluded = false;
-  {
-    std::lock_guard<std::mutex> g(index_.mu);
-    if (has_ignore_ && ignore_.matches(rel)) excluded = true;
-    if (has_upload_ignore_ && upload_ignore_.matches(rel)) excluded = true;
-  }
-  if (excluded) return;
+  if (has_ignore_ && ignore_.matches(rel)) return;
+  if (has_upload_ignore_ && upload_ignore_.matches(rel)) return;
+  if (ends_with(rel, kTmpSuffix)) return;
   std::string abs = o_.watch_path + rel;
   fs::StatInfo st = fs::stat(abs);  // follows symlinks like the reference (os.Stat)
   if (!st.exists) {
@@ -671,18 +831,15 @@ void Session::recursive_tar(const std::string& rel, std::map<std::string, FileIn
   if (mode_ != Mode::Compat) fi.local_mtime_ns = st.mtime_sec * 1000000000LL + st.mtime_nsec;
   uint32_t mode = st.mode & 07777;
   uint32_t uid = st.uid, gid = st.gid;
-  {
-    std::lock_guard<std::mutex> g(index_.mu);
-    if (FileInfo* known = index_.find(rel)) {
-      fi.remote_mode = known->remote_mode;
-      fi.remote_uid = known->remote_uid;
-      fi.remote_gid = known->remote_gid;
-      fi.has_remote_attrs = known->has_remote_attrs;
-      if (known->has_remote_attrs) {
-        mode = (uint32_t)known->remote_mode;
-        uid = (uint32_t)known->remote_uid;
-        gid = (uint32_t)known->remote_gid;
-      }
+  if (FileInfo* known = index_.find(rel)) {
+    fi.remote_mode = known->remote_mode;
+    fi.remote_uid = known->remote_uid;
+    fi.remote_gid = known->remote_gid;
+    fi.has_remote_attrs = known->has_remote_attrs;
+    if (known->has_remote_attrs) {
+      mode = (uint32_t)known->remote_mode;
+      uid = (uint32_t)known->remote_uid;
+      gid = (uint32_t)known->remote_gid;
     }
   }
   std::string name = rel.empty() ? "" : rel.substr(1);
@@ -708,6 +865,7 @@ void Session::recursive_tar(const std::string& rel, std::map<std::string, FileIn
   e.gid = gid;
   e.size = st.size;
   e.mtime = st.mtime_sec;
+  warn_large(rel, st.size);
   if (!tw->add_file_from_path(e, abs)) {
     logf("[Upstream] Couldn't read file " + abs);
     return;
@@ -715,55 +873,50 @@ void Session::recursive_tar(const std::string& rel, std::map<std::string, FileIn
   (*written)[rel] = fi;
 }
 
-std::string Session::build_archive(const std::vector<FileInfo>& files, std::map<std::string, FileInfo>* written) {
-  std::string raw;
-  TarWriter tw(string_sink(&raw));
-  for (auto& f : files)
-    if (!written->count(f.name)) recursive_tar(f.name, written, &tw, 0);
-  tw.finish();
-  // The reference always gzips (sync/tar.go:146). Small edits are latency-bound, not
-  // bandwidth-bound: fast modes ship them as plain tar (no gzip process on either side).
-  if (mode_ != Mode::Compat && raw.size() <= 256 * 1024) return raw;
-  return mode_ == Mode::Compat ? gzip_compress(raw, 6) : gzip_compress_adaptive(raw, 1);
-}
-
-static bool is_gzip(const std::string& a) { return a.size() >= 2 && (unsigned char)a[0] == 0x1f && (unsigned char)a[1] == 0x8b; }
-
-void Session::upload_archive(const std::string& archive) {
-  const std::string size = std::to_string(archive.size());
+uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std::string, FileInfo>* written) {
   int fd = up_shell_->in();
-  auto send_payload = [&]() {
-    if (o_.upstream_limit > 0) {
-      RateLimiter rl(o_.upstream_limit);
-      for (size_t off = 0; off < archive.size(); off += 16384) {
-        size_t n = std::min<size_t>(16384, archive.size() - off);
-        rl.take(n);
-        if (!write_all(fd, archive.data() + off, n)) throw SyncError("upstream: write failed");
-      }
-    } else if (!write_all(fd, archive)) {
-      throw SyncError("upstream: write failed");
-    }
+  RateLimiter rl(o_.upstream_limit);
+  Progress prog(this, "[Upstream] Upload", 0);
+  Sink to_shell = [&](const char* d, size_t n) {
+    if (o_.upstream_limit > 0) rl.take(n);
+    prog.add(n);
+    send(fd, d, n);
+    return true;
+  };
+  auto tar_all = [&](TarWriter& tw) {
+    for (auto& f : files)
+      if (!written->count(f.name)) recursive_tar(f.name, written, &tw, 0);
+    return tw.finish();
   };
   if (up_helper_) {
-    if (o_.upstream_limit > 0) {
-      std::string hdr = frame('U', "");
-      hdr.resize(1);
-      put_u32(hdr, (uint32_t)archive.size());
-      if (!write_all(fd, hdr)) throw SyncError("upstream: write failed");
-      send_payload();
-    } else if (!write_all(fd, frame('U', archive))) {
-      throw SyncError("upstream: write failed");
-    }
-    std::string line;
-    long deadline = mono_us() + 120000000L;
-    while (!up_out_.read_line(&line, 200)) {
-      if (up_out_.eof() || stopping_) throw SyncError("upstream: helper stream closed");
-      if (mono_us() > deadline) throw SyncError("upstream: helper timeout");
-    }
+    // chunk-framed stream: tar -> (plain | adaptive gzip) -> chunks -> exec stdin, no length
+    // announced, nothing staged (the container extracts while we read the files)
+    if (!write_all(fd, frame::header('U', 0))) throw SyncError("upstream: write failed");
+    frame::ChunkWriter cw(to_shell, frame::kMaxChunk, 1);  // per-chunk deflate where it pays
+    TarWriter tw(cw.sink());
+    if (!tar_all(tw) || !cw.finish()) throw SyncError("upstream: write failed");
+    std::string line = read_line_idle(up_out_, o_.idle_timeout_ms, "upstream: helper reply");
     if (line != "OK") throw SyncError("upstream: helper error: " + line);
-    return;
+    prog.finish();
+    return prog.done;
   }
-  std::string qdest = shell_quote(dest_);
+  // The shell protocols announce the length first (`head -c N`, the reference's fileSize=N
+  // script): the archive is staged in a SpillBuffer — memory up to 8 MiB, an unlinked temp
+  // file beyond — instead of a string (the reference always used a temp file, tar.go:146).
+  // The reference always gzips; fast modes ship small edits as plain tar.
+  SpillBuffer spill;
+  ArchiveEncoder enc(spill.sink(), mode_ == Mode::Compat ? 0 : kPlainTarLimit, mode_ == Mode::Compat ? 6 : 1);
+  TarWriter tw(enc.sink());
+  if (!tar_all(tw) || !enc.finish()) throw SyncError("upstream: cannot stage the archive (temp space?)");
+  if (written->empty()) return 0;
+  const std::string size = std::to_string(spill.size());
+  const char* xflags = enc.gzipped() ? "xzpf" : "xpf";
+  // the container cannot start extracting before the whole archive arrived (compat) or after
+  // the last byte only finishes the last file (fast); allow for it beyond the idle timeout
+  int done_ms = o_.idle_timeout_ms + (int)std::min<uint64_t>(spill.size() / 20000, 3600000);
+  auto send_payload = [&] {
+    if (!spill.replay(to_shell)) throw SyncError("upstream: write failed");
+  };
   if (mode_ == Mode::Compat || !up_has_head_) {
     // the reference protocol (sync/upstream.go:387-411); compat archives are always gzip, the
     // fast mode's cat/stat fallback may ship a small edit as plain tar
@@ -789,38 +942,47 @@ void Session::upload_archive(const std::string& archive) {
 							sleep 0.1;
 					done;
 
-					tar )" + std::string(is_gzip(archive) ? "xzpf" : "xpf") + R"( "$tmpFile" -C ')" + dest_ + R"(/.' 2>/tmp/devspace-upstream-error;
+					tar )" + std::string(xflags) + R"( "$tmpFile" -C ')" + dest_ + R"(/.' 2>/tmp/devspace-upstream-error;
 					echo "DONE";
 		)";
     if (!write_all(fd, cmd)) throw SyncError("upstream: write failed");
-    wait_ack(up_out_, kStart, false);
+    wait_ack(up_out_, kStart, false, nullptr, o_.idle_timeout_ms);
     send_payload();
-    wait_ack(up_out_, kDone, false);
-    return;
+    wait_ack(up_out_, kDone, false, nullptr, done_ms);
+    prog.finish();
+    return spill.size();
   }
-  (void)qdest;  // dest is created once when the shell opens
-  std::string cmd = "echo " + std::string(kStart) + " && head -c " + size + " | tar " +
-                    (is_gzip(archive) ? "xzpf" : "xpf") + " - -C " + shell_quote(dest_ + "/.") +
-                    " 2>/tmp/devspace-upstream-error; echo " + kDone + "\n";
+  // dest is created once when the shell opens; `head -c N | tar x` streams (no temp file, no
+  // polling in the container)
+  std::string cmd = "echo " + std::string(kStart) + " && head -c " + size + " | tar " + xflags + " - -C " +
+                    shell_quote(dest_ + "/.") + " 2>/tmp/devspace-upstream-error; echo " + kDone + "\n";
   if (!write_all(fd, cmd)) throw SyncError("upstream: write failed");
-  wait_ack(up_out_, kStart, false);
+  wait_ack(up_out_, kStart, false, nullptr, o_.idle_timeout_ms);
   send_payload();
-  wait_ack(up_out_, kDone, false);
+  wait_ack(up_out_, kDone, false, nullptr, done_ms);
+  prog.finish();
+  return spill.size();
 }
 
 void Session::apply_creates(const std::vector<FileInfo>& files) {
   std::map<std::string, FileInfo> written;
-  std::string archive = build_archive(files, &written);
+  std::lock_guard<std::mutex> ig(index_.mu);
+  uint64_t sent = 0;
+  try {
+    std::lock_guard<std::mutex> sg(up_shell_mu_);
+    sent = stream_upload(files, &written);
+  } catch (...) {
+    // whatever was in flight may sit half-written in the container with a fresh mtime; the
+    // initial sync after the reconnect must send it again instead of trusting that mtime
+    for (auto& kv : written) force_up_.insert(kv.first);
+    for (auto& f : files) force_up_.insert(f.name);
+    throw;
+  }
   if (written.empty()) return;
   if (o_.verbose || written.size() <= 3) {
     for (auto& kv : written) logf((kv.second.is_dir ? "[Upstream] Create Folder " : "[Upstream] Create File ") + kv.first);
   }
-  std::lock_guard<std::mutex> ig(index_.mu);
-  logf(strfmt("[Upstream] Upload %zu create changes (size %zu)", written.size(), archive.size()));
-  {
-    std::lock_guard<std::mutex> sg(up_shell_mu_);
-    upload_archive(archive);
-  }
+  logf(strfmt("[Upstream] Upload %zu create changes (size %llu)", written.size(), (unsigned long long)sent));
   for (auto& kv : written) {
     index_.create_dir(fs::dirname(kv.first));
     FileInfo f = kv.second;
@@ -835,7 +997,7 @@ void Session::apply_creates(const std::vector<FileInfo>& files) {
     index_.files[kv.first] = f;
   }
   std::lock_guard<std::mutex> g(stats_mu_);
-  stats_.bytes_up += archive.size();
+  stats_.bytes_up += sent;
 }
 
 void Session::send_changes_to_upstream(std::vector<FileInfo> changes) {
@@ -870,6 +1032,7 @@ void Session::send_changes_to_upstream(std::vector<FileInfo> changes) {
 void Session::diff_server_client(const std::string& abs, std::vector<FileInfo>* send,
                                  std::map<std::string, FileInfo>* download, bool dont_send) {
   std::string rel = abs.substr(o_.watch_path.size());
+  if (ends_with(rel, kTmpSuffix)) return;
   fs::StatInfo st = fs::stat(abs);
   if (!st.exists) return;
   download->erase(rel);
@@ -954,10 +1117,20 @@ void Session::initial_sync() {
     std::lock_guard<std::mutex> g(index_.mu);
     for (auto& f : creates)
       if (!index_.files.count(f.name)) index_.files[f.name] = f;
+    // uploads cut off by a broken stream: whatever the container holds there now (a partial
+    // file with a fresh mtime in the shell protocols) must not win the mtime comparison
+    for (auto& p : force_up_) {
+      FileInfo* f = index_.find(p);
+      if (f && !f->is_dir) index_.files.erase(p);
+    }
   }
   std::vector<FileInfo> local_changes;
   auto remote_only = clone_index();
   diff_server_client(o_.watch_path, &local_changes, &remote_only, false);
+  {
+    std::lock_guard<std::mutex> g(index_.mu);
+    force_up_.clear();
+  }
   if (down_helper_ && mode_ != Mode::Compat && !local_changes.empty()) drop_identical_copies(local_changes);
   if (!local_changes.empty()) send_changes_to_upstream(std::move(local_changes));
   if (!remote_only.empty()) {
@@ -997,7 +1170,7 @@ void Session::drop_identical_copies(std::vector<FileInfo>& changes) {
     std::vector<std::string> remote;
     {
       std::lock_guard<std::mutex> sg(down_shell_mu_);
-      if (!write_all(down_shell_->in(), frame('H', list))) throw SyncError("downstream: write failed");
+      if (!write_all(down_shell_->in(), request('H', list))) throw SyncError("downstream: write failed");
       long deadline = mono_us() + 300000000L;
       while (true) {
         std::string line;
@@ -1052,7 +1225,7 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
   std::lock_guard<std::mutex> sg(down_shell_mu_);
   std::string qd = shell_quote(dest_);
   if (down_helper_) {
-    if (!write_all(down_shell_->in(), frame('S', ""))) throw SyncError("downstream: write failed");
+    if (!write_all(down_shell_->in(), request('S', ""))) throw SyncError("downstream: write failed");
   } else if (mode_ == Mode::Compat) {
     std::string cmd = "mkdir -p '" + dest_ + "' && find -L '" + dest_ +
                       "' -exec stat -c \"%n///%s,%Y,%f,%a,%u,%g\" {} + 2>/dev/null && echo -n \"" + kDone +
@@ -1134,6 +1307,7 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
       dest_found = true;
       continue;
     }
+    if (ends_with(fi->name, kTmpSuffix)) continue;
     std::lock_guard<std::mutex> ig(index_.mu);
     if (removes) removes->erase(fi->name);
     if (FileInfo* known = index_.find(fi->name)) {
@@ -1189,34 +1363,57 @@ bool Session::probe_changes() {
   return hit;
 }
 
-std::string Session::download_files(const std::vector<FileInfo>& files) {
-  int64_t total = 0;
-  for (auto& f : files) total += f.size;
-  if (files.size() > 3) logf(strfmt("[Downstream] Download %zu files (size: %lld)", files.size(), (long long)total));
-  std::string list;
-  for (auto& f : files) {
-    if (files.size() <= 3 || o_.verbose)
-      logf(strfmt("[Downstream] Download file %s, size: %lld", f.name.c_str(), (long long)f.size));
-    list += dest_ + f.name + "\n";
+void Session::download_and_apply(const std::vector<FileInfo>& files) {
+  uint64_t total = 0;
+  for (auto& f : files) total += (uint64_t)std::max<int64_t>(0, f.size);
+  if (files.size() > 3) logf(strfmt("[Downstream] Download %zu files (size: %llu)", files.size(), (unsigned long long)total));
+  {
+    std::lock_guard<std::mutex> ig(index_.mu);
+    for (auto& f : files) {
+      if (files.size() <= 3 || o_.verbose)
+        logf(strfmt("[Downstream] Download file %s, size: %lld", f.name.c_str(), (long long)f.size));
+      warn_large(f.name, f.size);
+    }
   }
-  std::string archive;
   std::lock_guard<std::mutex> sg(down_shell_mu_);
   int fd = down_shell_->in();
+  const int idle = o_.idle_timeout_ms;
+  Progress prog(this, "[Downstream] Download", total);
+  RateLimiter rl(o_.downstream_limit);
+  auto counted = [&](Source inner) -> Source {
+    return [&, inner](char* b, size_t n) -> ssize_t {
+      ssize_t r = inner(b, n);
+      if (r > 0) {
+        if (o_.downstream_limit > 0) rl.take((size_t)r);
+        prog.add((size_t)r);
+      }
+      return r;
+    };
+  };
+  struct Count {  // wire bytes, recorded however the transfer ends
+    Session* s;
+    Progress* p;
+    ~Count() {
+      std::lock_guard<std::mutex> g(s->stats_mu_);
+      s->stats_.bytes_down += p->done;
+    }
+  } count{this, &prog};
   if (down_helper_) {
     std::string rels;
     for (auto& f : files) rels += f.name + "\n";
-    if (!write_all(fd, frame('D', rels))) throw SyncError("downstream: write failed");
-    std::string line;
-    long deadline = mono_us() + 120000000L;
-    while (!down_out_.read_line(&line, 200)) {
-      if (down_out_.eof() || stopping_) throw SyncError("downstream: helper stream closed");
-      if (mono_us() > deadline) throw SyncError("downstream: helper timeout");
-    }
-    if (!starts_with(line, "SIZE ")) throw SyncError("downstream: helper error: " + line);
-    int64_t n = std::atoll(line.substr(5).c_str());
-    if (!down_out_.read_exact(&archive, (size_t)n, 120000)) throw SyncError("downstream: short read");
-    return archive;
+    if (!write_all(fd, request('D', rels))) throw SyncError("downstream: write failed");
+    std::string line = read_line_idle(down_out_, idle, "downstream: helper reply");
+    if (line != "STREAM") throw SyncError("downstream: helper error: " + line);
+    frame::ChunkReader cr(counted(reader_source(down_out_, idle, "downstream: helper stream")));
+    untar_stream(cr.source(), nullptr);
+    cr.drain();
+    line = read_line_idle(down_out_, idle, "downstream: helper reply");
+    if (line != "OK") throw SyncError("downstream: helper error: " + line);
+    prog.finish();
+    return;
   }
+  std::string list;
+  for (auto& f : files) list += dest_ + f.name + "\n";
   if (mode_ == Mode::Compat) {
     std::string cmd = "fileSize=" + std::to_string(list.size()) + R"(;
 					tmpFileInput="/tmp/devspace-downstream-input";
@@ -1246,48 +1443,63 @@ std::string Session::download_files(const std::vector<FileInfo>& files) {
 					cat "$tmpFileOutput";
 		)";
     if (!write_all(fd, cmd)) throw SyncError("downstream: write failed");
-    wait_ack(down_out_, kStart, false);
+    wait_ack(down_out_, kStart, false, nullptr, idle);
     if (!write_all(fd, list)) throw SyncError("downstream: write failed");
+    // the container gzips everything into its temp file before the size line: silent for a
+    // while on big files (gzip -6 runs ~20 MB/s on incompressible data)
     std::string before;
-    wait_ack(down_err_, kDone, false, &before);
+    wait_ack(down_err_, kDone, false, &before, idle + (int)std::min<uint64_t>(total / 5000, 3600000));
     auto lines = split(trim(before), "\n");
     if (lines.empty()) throw SyncError("[Downstream] Cannot find size");
     int64_t n = std::atoll(lines.back().c_str());
     if (n == 0) throw SyncError("[Downstream] Empty tar");
-    if (!down_out_.read_to(
-            (size_t)n,
-            [&](const char* d, size_t k) {
-              archive.append(d, k);
-              return true;
-            },
-            120000, o_.downstream_limit))
-      throw SyncError("[Downstream] Downloaded tar has wrong filesize");
-    return archive;
+    Source body = limited_source(counted(reader_source(down_out_, idle, "[Downstream] tar stream")), (uint64_t)n);
+    untar_stream(body, nullptr);
+    char sink[1 << 15];
+    while (true) {  // the rest of the announced bytes (tar padding)
+      ssize_t r = body(sink, sizeof(sink));
+      if (r == 0) break;
+      if (r < 0) throw SyncError("[Downstream] Downloaded tar has wrong filesize");
+    }
+    prog.finish();
+    return;
   }
-  // fast POSIX: relative member names via -C, size line then payload on stdout
+  // fast POSIX: the container streams `tar -c` straight to stdout between two marker lines (no
+  // temp file in the pod, no size needed up front). Small sets are gzipped; big ones go as
+  // plain tar, which is link-bound instead of gzip-bound (~20 MB/s on checkpoints).
+  bool gz = total <= (8ull << 20);
   std::vector<std::string> args;
   for (auto& f : files) args.push_back(shell_quote("." + f.name));
-  std::string cmd = "f=/tmp/devspace-downstream-$$; tar -czf \"$f\" -C " + shell_quote(dest_) + " -- " +
-                    join(args, " ") + " 2>/tmp/devspace-downstream-error; echo \"SIZE $(stat -c %s \"$f\" 2>/dev/null || echo 0)\"; cat \"$f\"; rm -f \"$f\"\n";
+  std::string cmd = std::string("echo DSSTART; tar -c") + (gz ? "z" : "") + "f - -C " + shell_quote(dest_) + " -- " +
+                    join(args, " ") + " 2>/tmp/devspace-downstream-error; echo; echo \"DSEND $?\"\n";
   if (!write_all(fd, cmd)) throw SyncError("downstream: write failed");
-  std::string line;
-  long deadline = mono_us() + 120000000L;
-  while (!down_out_.read_line(&line, 200)) {
-    if (down_out_.eof() || stopping_) throw SyncError("downstream: stream closed");
-    if (mono_us() > deadline) throw SyncError("downstream: timeout");
+  while (read_line_idle(down_out_, idle, "downstream") != "DSSTART") {
   }
-  if (!starts_with(line, "SIZE ")) throw SyncError("downstream: unexpected reply: " + line);
-  int64_t n = std::atoll(line.substr(5).c_str());
-  if (n == 0) throw SyncError("[Downstream] Empty tar");
-  if (!down_out_.read_to(
-          (size_t)n,
-          [&](const char* d, size_t k) {
-            archive.append(d, k);
-            return true;
-          },
-          120000, o_.downstream_limit))
-    throw SyncError("[Downstream] Downloaded tar has wrong filesize");
-  return archive;
+  std::string leftover;
+  untar_stream(counted(reader_source(down_out_, idle, "downstream: tar stream")), &leftover);
+  down_out_.unread(leftover);
+  // plain tar: zero blocks up to the end of tar's last record, then the marker line
+  char zb[4096];
+  while (true) {
+    ssize_t r = down_out_.read_some(zb, sizeof(zb), 200);
+    if (r == -2) {
+      if (stopping_) throw SyncError("sync stopped");
+      if (mono_us() - down_out_.last_activity_us() > (long)idle * 1000) throw SyncError("downstream: no end marker");
+      continue;
+    }
+    if (r <= 0) throw SyncError("downstream: stream closed");
+    ssize_t i = 0;
+    while (i < r && zb[i] == 0) ++i;
+    if (i < r) {
+      down_out_.unread(std::string(zb + i, (size_t)(r - i)));
+      break;
+    }
+  }
+  while (true) {
+    std::string line = read_line_idle(down_out_, idle, "downstream");
+    if (starts_with(line, "DSEND")) break;
+  }
+  prog.finish();
 }
 
 bool has_dotdot_segment(const std::string& rel) {
@@ -1296,14 +1508,38 @@ bool has_dotdot_segment(const std::string& rel) {
   return false;
 }
 
-void Session::untar_all(const std::string& archive) {
-  GzipReader gz(string_source(&archive));
-  TarReader tr([&](char* b, size_t n) { return gz.read(b, n); });
+void Session::untar_stream(Source raw, std::string* leftover) {
+  std::string magic;
+  {
+    char m[2];
+    while (magic.size() < 2) {
+      ssize_t n = raw(m, 2 - magic.size());
+      if (n <= 0) break;
+      magic.append(m, (size_t)n);
+    }
+  }
+  if (magic.empty()) return;
+  if (leftover && magic[0] == '\n') {  // fast protocol: tar wrote nothing, the end marker follows
+    *leftover = magic;
+    return;
+  }
+  bool gz = is_gzip_magic(magic);
+  Source src = prefixed_source(magic, raw);
+  std::unique_ptr<GzipReader> gzr;
+  if (gz) {
+    gzr = std::make_unique<GzipReader>(src);
+    gzr->set_single_member(leftover != nullptr);
+  }
+  TarReader tr([&](char* b, size_t n) -> ssize_t {
+    if (!gzr) return src(b, n);
+    ssize_t r = gzr->read(b, n);
+    if (r < 0) throw SyncError("[Downstream] corrupt gzip stream");
+    return r;
+  });
   TarEntry e;
   int count = 0;
-  while (true) {
-    std::lock_guard<std::mutex> ig(index_.mu);
-    if (!tr.next(&e)) break;
+  std::vector<char> buf(1 << 20);
+  while (tr.next(&e)) {
     std::string name = e.name;
     if (starts_with(name, "./")) name = name.substr(1);
     if (!starts_with(name, "/")) name = "/" + name;
@@ -1319,45 +1555,91 @@ void Session::untar_all(const std::string& archive) {
       continue;
     }
     std::string out = o_.watch_path + rel;
-    fs::StatInfo st = fs::stat(out);
-    if (st.exists && st.mtime_rounded() > e.mtime) {
-      FileInfo f;
-      f.name = rel;
-      f.mtime = st.mtime_rounded();
-      f.size = st.size;
-      f.is_dir = st.is_dir;
-      index_.files[rel] = f;
-      logf("[Downstream] Don't override " + rel + " because file has newer mTime timestamp");
+    fs::StatInfo before;
+    {
+      std::lock_guard<std::mutex> ig(index_.mu);
+      before = fs::stat(out);
+      if (before.exists && before.mtime_rounded() > e.mtime) {
+        FileInfo f;
+        f.name = rel;
+        f.mtime = before.mtime_rounded();
+        f.size = before.size;
+        f.is_dir = before.is_dir;
+        index_.files[rel] = f;
+        logf("[Downstream] Don't override " + rel + " because file has newer mTime timestamp");
+        tr.skip();
+        continue;
+      }
+      fs::mkdirs(fs::dirname(out));
+      if (e.type == '5') {
+        fs::mkdirs(out);
+        index_.create_dir(rel);
+        continue;
+      }
+      if (e.type != '0' && e.type != '7') {
+        tr.skip();
+        continue;
+      }
+    }
+    // stream the contents to a temp name next to the target (the upstream watcher ignores the
+    // suffix) without holding the index: a big file must not stall local edits meanwhile
+    std::string tmp = out + kTmpSuffix;
+    int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0600);
+    if (fd < 0) {
+      sleep_ms(mode_ == Mode::Compat ? 5000 : 200);  // retry once (tar.go:97)
+      fs::mkdirs(fs::dirname(out));
+      fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0600);
+    }
+    if (fd < 0) {
+      logf("[Downstream] Cannot create " + out + ": " + std::strerror(errno));
       tr.skip();
       continue;
     }
-    fs::mkdirs(fs::dirname(out));
-    if (e.type == '5') {
-      fs::mkdirs(out);
-      index_.create_dir(rel);
+    int64_t written = 0;
+    try {
+      while (true) {
+        ssize_t n = tr.read(buf.data(), buf.size());
+        if (n <= 0) break;
+        if (!write_all(fd, buf.data(), (size_t)n)) throw SyncError("[Downstream] write " + out + ": " + std::strerror(errno));
+        written += n;
+      }
+    } catch (...) {
+      ::close(fd);
+      ::unlink(tmp.c_str());  // an interrupted transfer leaves no partial file behind
+      throw;
+    }
+    ::fchmod(fd, (mode_t)(before.exists ? (before.mode & 07777) : (e.mode & 07777 ? e.mode & 07777 : 0644)));
+    ::close(fd);
+    fs::set_mtime(tmp, e.mtime, 0);
+    std::lock_guard<std::mutex> ig(index_.mu);
+    fs::StatInfo now = fs::stat(out);
+    if (now.exists != before.exists ||
+        (now.exists && (now.mtime_sec != before.mtime_sec || now.mtime_nsec != before.mtime_nsec ||
+                        now.size != before.size || now.ino != before.ino))) {
+      // edited locally while it was downloading: the local edit wins (it is uploaded next)
+      ::unlink(tmp.c_str());
+      logf("[Downstream] Don't override " + rel + " because it changed locally during the download");
       continue;
     }
-    if (e.type != '0' && e.type != '7') {
-      tr.skip();
+    if (::rename(tmp.c_str(), out.c_str()) != 0) {
+      ::unlink(tmp.c_str());
+      logf("[Downstream] Cannot write " + out + ": " + std::strerror(errno));
       continue;
     }
     index_.create_dir(fs::dirname(rel));
-    std::string data = tr.read_all();
-    try {
-      fs::write_file(out, data, (int)(e.mode & 07777 ? e.mode & 07777 : 0644));
-    } catch (...) {
-      sleep_ms(mode_ == Mode::Compat ? 5000 : 200);  // retry once (tar.go:97)
-      fs::write_file(out, data, 0644);
-    }
-    if (st.exists) ::chmod(out.c_str(), st.mode & 07777);
-    fs::set_mtime(out, e.mtime, 0);
     FileInfo f;
     f.name = rel;
     f.mtime = e.mtime;
-    f.size = (int64_t)data.size();
+    f.size = written;
     if (mode_ != Mode::Compat) f.local_mtime_ns = e.mtime * 1000000000LL;
     index_.files[rel] = f;
     if (++count % 500 == 0) logf(strfmt("[Downstream] Untared %d files...", count));
+  }
+  if (gzr && leftover) {
+    // the rest of the member (tar's zero records), then whatever followed it on the stream
+    while (gzr->read(buf.data(), buf.size()) > 0) {
+    }
+    *leftover = gzr->leftover();
   }
 }
 
@@ -1420,27 +1702,15 @@ void Session::apply_downstream(const std::vector<FileInfo>& creates, std::map<st
                    {{"changes", std::to_string(creates.size() + removes.size())}, {"dest", o_.dest_path}});
   std::vector<FileInfo> files, dirs;
   for (auto& c : creates) (c.is_dir ? dirs : files).push_back(c);
-  std::string archive;
-  if (!files.empty()) {
-    // batch very long lists (argv limits in fast mode)
-    if (mode_ != Mode::Compat && !down_helper_ && files.size() > 500) {
-      for (size_t i = 0; i < files.size(); i += 500) {
-        std::vector<FileInfo> part(files.begin() + i, files.begin() + std::min(files.size(), i + 500));
-        std::string a = download_files(part);
-        untar_all(a);
-        std::lock_guard<std::mutex> g(stats_mu_);
-        stats_.bytes_down += a.size();
-      }
-    } else {
-      archive = download_files(files);
-    }
-  }
   remove_files_and_folders(removes);
   create_folders(dirs);
-  if (!archive.empty()) {
-    untar_all(archive);
-    std::lock_guard<std::mutex> g(stats_mu_);
-    stats_.bytes_down += archive.size();
+  if (!files.empty()) {
+    // batch very long lists (argv limits in fast mode); every batch streams into the tree
+    size_t step = mode_ != Mode::Compat && !down_helper_ ? 500 : files.size();
+    for (size_t i = 0; i < files.size(); i += step) {
+      std::vector<FileInfo> part(files.begin() + i, files.begin() + std::min(files.size(), i + step));
+      download_and_apply(part);
+    }
   }
   logf(strfmt("[Downstream] Successfully processed %zu change(s)", creates.size() + removes.size()));
   std::lock_guard<std::mutex> g(stats_mu_);
@@ -1620,9 +1890,12 @@ void Session::start() {
 
 bool Session::wait_initial_sync(int timeout_ms) {
   std::unique_lock<std::mutex> lk(state_mu_);
-  return state_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms),
-                            [this] { return initial_done_ || !error_.empty(); }) &&
-         initial_done_;
+  auto ready = [this] { return initial_done_ || !error_.empty() || stopping_; };
+  if (timeout_ms < 0)
+    state_cv_.wait(lk, ready);
+  else if (!state_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready))
+    return false;
+  return initial_done_;
 }
 
 std::string Session::error() {

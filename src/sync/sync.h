@@ -20,6 +20,7 @@
 #include <memory>
 #include <mutex>
 #include <optional>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -92,6 +93,12 @@ struct Options {
   // running pod again) instead of a fatal stop (the reference log.Fatalf's, sync_config.go:481).
   std::function<std::shared_ptr<Transport>()> reconnect;
   int max_reconnects = 10;
+  // A stream that delivers no byte for this long is dead (replaces fixed per-transfer
+  // deadlines: a multi-GB transfer may take minutes, a stalled one is cut after this).
+  int idle_timeout_ms = 120000;
+  // Files at least this big get a one-time warning suggesting an exclude (<0: the default,
+  // 1 GiB, or $DEVSPACE_SYNC_WARN_FILE_MB).
+  int64_t large_file_warn_bytes = -1;
   std::function<void(const std::string&)> on_error;
   std::function<void()> on_initial_sync_done;
   std::string sync_log_name = "sync";
@@ -139,7 +146,7 @@ class Session {
   void start_loops(bool upstream, bool downstream);
   FileIndex& index() { return index_; }
   // Extracts a downstream tar.gz (as received from the container) into the local folder.
-  void apply_downstream_archive(const std::string& archive) { untar_all(archive); }
+  void apply_downstream_archive(const std::string& archive) { untar_stream(string_source(&archive), nullptr); }
 
   // One-shot upload of a local folder/file (sync/util.go:21 CopyToContainer).
   static void copy_to_container(std::shared_ptr<Transport> t, const std::string& local_path,
@@ -167,12 +174,20 @@ class Session {
   void apply_upstream(std::vector<FileInfo>& changes, long first_event_us);
   void apply_removes(const std::vector<FileInfo>& removes);
   void apply_creates(const std::vector<FileInfo>& creates);
-  std::string build_archive(const std::vector<FileInfo>& files, std::map<std::string, FileInfo>* written);
+  // Streams a tar of `files` (recursively) to the container; index lock held by the caller.
+  // Returns the wire bytes sent; throws on a broken stream.
+  uint64_t stream_upload(const std::vector<FileInfo>& files, std::map<std::string, FileInfo>* written);
   void recursive_tar(const std::string& rel, std::map<std::string, FileInfo>* written, TarWriter* tw, int depth);
   bool wait_ack(LineReader& r, const std::string& keyword, bool partial, std::string* before = nullptr,
                 int timeout_ms = 120000);
   void stop_loops();
-  void upload_archive(const std::string& archive);
+  // Bulk write to a shell's stdin with an idle timeout (SyncError when stuck or closed).
+  void send(int fd, const char* d, size_t n);
+  // Blocking reads with an idle timeout (no byte for idle_ms -> SyncError), honouring stop().
+  std::string read_line_idle(LineReader& r, int idle_ms, const char* what);
+  Source reader_source(LineReader& r, int idle_ms, const char* what);
+  void warn_large(const std::string& rel, int64_t size);  // index lock held
+  struct Progress;
   void send_changes_to_upstream(std::vector<FileInfo> changes);
   void diff_server_client(const std::string& abs, std::vector<FileInfo>* send,
                           std::map<std::string, FileInfo>* download, bool dont_send);
@@ -185,8 +200,12 @@ class Session {
   bool up_has_head_ = true;  // fast mode: container has `head -c` for streamed uploads
   long probe_seq_ = 0;
   void apply_downstream(const std::vector<FileInfo>& creates, std::map<std::string, FileInfo>& removes);
-  std::string download_files(const std::vector<FileInfo>& files);
-  void untar_all(const std::string& archive);
+  // Streams the files from the container straight into the local tree (no archive in memory).
+  void download_and_apply(const std::vector<FileInfo>& files);
+  // Extracts a tar / tar.gz stream into the local folder, each file through a temp name and a
+  // rename. leftover != nullptr: the stream continues after the archive (fast protocol) — a gzip
+  // member is read exactly to its end and any bytes pulled past it are returned there.
+  void untar_stream(Source raw, std::string* leftover);
   void remove_files_and_folders(std::map<std::string, FileInfo>& removes);
   void delete_safe_recursive(const std::string& rel, std::map<std::string, FileInfo>& removes);
   void create_folders(const std::vector<FileInfo>& dirs);
@@ -241,6 +260,11 @@ class Session {
   std::string error_;
   Stats stats_;
   std::mutex stats_mu_;
+  // Paths whose upload was cut off by a broken stream (index lock): re-sent after a reconnect
+  // even though the container may now hold a newer-looking partial copy.
+  std::set<std::string> force_up_;
+  std::set<std::string> warned_large_;  // index lock
+  int64_t large_warn_bytes_ = 1ll << 30;
   std::string pending_failure_;
   int reconnects_ = 0;
 };

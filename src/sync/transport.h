@@ -60,6 +60,8 @@ class LocalShellTransport : public Transport {
 struct FaultPlan {
   // Kill the shell once this many bytes were written to its stdin (0 = never).
   size_t kill_after_stdin_bytes = 0;
+  // Kill the shell once this many bytes were read from its stdout (0 = never).
+  size_t kill_after_stdout_bytes = 0;
   // Delay every chunk read from remote stdout by this many ms.
   int stall_stdout_ms = 0;
   // Replace the first occurrence of `corrupt_from` in stdout with `corrupt_to`.
@@ -88,11 +90,7 @@ class FaultInjectingTransport : public Transport {
 class LineReader {
  public:
   explicit LineReader(int fd = -1) : fd_(fd) {}
-  void reset(int fd) {
-    fd_ = fd;
-    buf_.clear();
-    eof_ = false;
-  }
+  void reset(int fd);
   // Reads one '\n'-terminated line (without it). false on EOF/timeout/error.
   bool read_line(std::string* line, int timeout_ms = -1);
   // Waits for a line equal to keyword, or (partial=true) a trailing unterminated chunk equal to
@@ -103,8 +101,15 @@ class LineReader {
   // Streams exactly n bytes to a sink.
   bool read_to(size_t n, const std::function<bool(const char*, size_t)>& sink, int timeout_ms = -1,
                int64_t rate_limit = 0);
+  // Up to n bytes (buffered read-ahead first). Returns bytes, 0 on EOF, -1 on error, -2 on
+  // timeout.
+  ssize_t read_some(char* out, size_t n, int timeout_ms = -1);
+  // Puts bytes back in front of the read-ahead (a parser that pulled past its own data).
+  void unread(const std::string& data) { buf_.insert(0, data); }
   int fd() const { return fd_; }
   bool eof() const { return eof_; }
+  // Monotonic time (us) of the last byte received; the reset time before any.
+  long last_activity_us() const { return last_us_; }
   std::string take_buffer() {
     std::string b;
     b.swap(buf_);
@@ -116,6 +121,7 @@ class LineReader {
   int fd_;
   std::string buf_;
   bool eof_ = false;
+  long last_us_ = 0;
 };
 
 // Token-bucket rate limiter (juju/ratelimit in the reference; bytes/second).

@@ -16,7 +16,9 @@
 #include "deploy/gotemplate.h"
 #include "deploy/helm.h"
 #include "deploy/helmrepo.h"
+#include "build/docker.h"
 #include "generator/generator.h"
+#include "gpu/sizing.h"
 #include "testing.h"
 
 using namespace ds;
@@ -449,3 +451,129 @@ TEST(regex_on_long_inputs_does_not_crash) {
   EXPECT_EQ(render_tmpl("{{ regexFindAll \"a+b\" .s -1 | len }}", d), std::string("1"));
 }
 
+
+// ---------------------------------------------------------------- MI355X pod sizing
+
+static Value init_values(int gpus, const std::vector<gpu::GpuNode>& nodes = {}) {
+  // what `devspace init` writes into the base chart's values.yaml for a rocm-pytorch project
+  std::string v = fs::read_file(std::string(DEVSPACE_SOURCE_DIR) + "/templates/_base/chart/values.yaml");
+  gpu::PodSizing s = gpu::size_pod(gpus, nodes);
+  v = replace_all(v, "#image#", "reg/train:tag");
+  v = replace_all(v, "#port#", "29500");
+  v = replace_all(v, "#resources#", gpu::resources_yaml(s));
+  std::string settings = gpu::gpu_settings_yaml(s);
+  v = replace_all(v, settings.empty() ? "#gpu-settings#\n" : "#gpu-settings#", settings);
+  return yaml_parse(v);
+}
+
+static void check_gpu_pod_invariants(const Value& spec, int gpus) {
+  const Value& ct = spec.get("containers")[0];
+  const Value& lim = ct.at_path("resources.limits");
+  const Value& req = ct.at_path("resources.requests");
+  EXPECT_EQ(lim.get("amd.com/gpu").as_int(), (int64_t)gpus);
+  double cpu = gpu::parse_cpu(lim.get("cpu").as_string());
+  int64_t mem = gpu::parse_memory_bytes(lim.get("memory").as_string());
+  EXPECT_TRUE(cpu >= gpus);  // at least one core per rank
+  EXPECT_EQ(req.get("cpu").as_string(), lim.get("cpu").as_string());
+  EXPECT_EQ(req.get("memory").as_string(), lim.get("memory").as_string());
+  int64_t shm = -1;
+  for (auto& v : spec.get("volumes").items())
+    if (v.get("name").as_string() == "dshm") shm = gpu::parse_memory_bytes(v.at_path("emptyDir.sizeLimit").as_string());
+  EXPECT_TRUE(shm > 0);
+  // tmpfs pages are charged to the container: memory covers shm plus a host budget per rank
+  EXPECT_TRUE(mem >= shm + (int64_t)gpus * (8ll << 30));
+  bool tol = false;
+  for (auto& t : spec.get("tolerations").items())
+    if (t.get("key").as_string() == "amd.com/gpu" && t.get("effect").as_string() == "NoSchedule") tol = true;
+  EXPECT_TRUE(tol);
+  EXPECT_TRUE(gpu::pod_sizing_problems(spec).empty());
+}
+
+TEST(component_chart_gpu_sizing_1_2_4_8) {
+  helm::Chart c = helm::load_chart(std::string(DEVSPACE_SOURCE_DIR) + "/templates/_base/chart");
+  helm::RenderOptions o;
+  o.release_name = "train";
+  for (int g : {1, 2, 4, 8}) {
+    auto objs = helm::render(c, init_values(g), o);
+    const Value* d = find_kind(objs, "Deployment");
+    EXPECT_TRUE(d != nullptr);
+    const Value& spec = d->at_path("spec.template.spec");
+    check_gpu_pod_invariants(spec, g);
+    // defaults: 12 CPUs and 80 Gi (16 Gi shm + 64 Gi) per GPU
+    const Value& lim = spec.get("containers")[0].at_path("resources.limits");
+    EXPECT_EQ(lim.get("cpu").as_string(), std::to_string(12 * g));
+    EXPECT_EQ(lim.get("memory").as_string(), std::to_string(80 * g) + "Gi");
+    EXPECT_TRUE(spec.find("nodeSelector") == nullptr);
+  }
+}
+
+TEST(component_chart_gpu_sizing_from_node_allocatable) {
+  // an 8x MI355X node with 256 CPUs and 3 TiB allocatable, labelled by the GPU operator
+  Value nodes = yaml_parse(
+      "items:\n"
+      "- metadata: {name: mi355x-0, labels: {amd.com/gpu.product-name: AMD_Instinct_MI355X}}\n"
+      "  status: {allocatable: {cpu: '256', memory: 3221225472Ki, amd.com/gpu: '8'}}\n"
+      "- metadata: {name: cpu-0}\n"
+      "  status: {allocatable: {cpu: '64', memory: 256Gi}}\n");
+  auto gn = gpu::gpu_nodes(nodes);
+  EXPECT_EQ(gn.size(), (size_t)1);
+  EXPECT_EQ(gn[0].memory, (int64_t)3221225472ll * 1024);
+  gpu::PodSizing s = gpu::size_pod(4, gn);
+  EXPECT_EQ(s.cpu_per_gpu, 28);  // floor(256 * 0.9 / 8)
+  EXPECT_EQ(s.shm_per_gpu_gi + s.host_per_gpu_gi, 345);  // floor(3072 GiB * 0.9 / 8)
+  EXPECT_EQ(s.product, std::string("AMD_Instinct_MI355X"));
+  helm::Chart c = helm::load_chart(std::string(DEVSPACE_SOURCE_DIR) + "/templates/_base/chart");
+  helm::RenderOptions o;
+  o.release_name = "train";
+  auto objs = helm::render(c, init_values(4, gn), o);
+  const Value& spec = find_kind(objs, "Deployment")->at_path("spec.template.spec");
+  check_gpu_pod_invariants(spec, 4);
+  EXPECT_EQ(spec.at_path("nodeSelector").get("amd.com/gpu.product-name").as_string(),
+            std::string("AMD_Instinct_MI355X"));
+  EXPECT_EQ(spec.get("containers")[0].at_path("resources.limits.cpu").as_string(), std::string("112"));
+}
+
+TEST(component_chart_cpu_only_has_no_gpu_scheduling) {
+  helm::Chart c = helm::load_chart(std::string(DEVSPACE_SOURCE_DIR) + "/templates/_base/chart");
+  helm::RenderOptions o;
+  o.release_name = "web";
+  auto objs = helm::render(c, init_values(0), o);
+  const Value& spec = find_kind(objs, "Deployment")->at_path("spec.template.spec");
+  EXPECT_TRUE(spec.find("tolerations") == nullptr);
+  const Value& ct = spec.get("containers")[0];
+  EXPECT_EQ(ct.at_path("resources.limits.cpu").as_string(), std::string("2"));
+  EXPECT_TRUE(ct.at_path("resources").find("requests") == nullptr);
+  EXPECT_TRUE(ct.at_path("resources.limits").find("amd.com/gpu") == nullptr);
+}
+
+TEST(gpu_sizing_problems_flag_undersized_pods) {
+  // the round-2 chart for 8 GPUs: 2 CPUs, 4 Gi memory, 128 Gi memory-backed shm
+  Value spec = yaml_parse(
+      "containers:\n"
+      "- name: train\n"
+      "  resources: {limits: {cpu: '2', memory: 4Gi, amd.com/gpu: 8}}\n"
+      "  volumeMounts: [{name: dshm, mountPath: /dev/shm}]\n"
+      "volumes: [{name: dshm, emptyDir: {medium: Memory, sizeLimit: 128Gi}}]\n");
+  auto probs = gpu::pod_sizing_problems(spec);
+  EXPECT_EQ(probs.size(), (size_t)2);
+  EXPECT_TRUE(contains(probs[0], "/dev/shm") && contains(probs[0], "OOM"));
+  EXPECT_TRUE(contains(probs[1], "2 CPU(s) for 8 GPU rank(s)"));
+  Value nolimit = yaml_parse("containers:\n- name: t\n  resources: {limits: {amd.com/gpu: 1}}\n");
+  EXPECT_EQ(gpu::pod_sizing_problems(nolimit).size(), (size_t)1);
+  EXPECT_EQ(gpu::parse_memory_bytes("1.5Gi"), (int64_t)1610612736);
+  EXPECT_EQ(gpu::parse_memory_bytes("500M"), (int64_t)500000000);
+  EXPECT_EQ(gpu::parse_memory_bytes("1e3"), (int64_t)1000);
+  EXPECT_EQ(gpu::parse_memory_bytes("12Qi"), (int64_t)-1);
+  EXPECT_TRUE(gpu::parse_cpu("500m") == 0.5);
+}
+
+TEST(image_reference_validation) {
+  for (const char* ok : {"devspace", "user/devspace", "local.registry/init-node", "localhost:5000/a/b:v1",
+                         "rocm/pytorch:rocm7.0_ubuntu24.04_py3.12_pytorch_release_2.8.0", "gcr.io/p/img@sha256:"
+                         "0123456789abcdef0123456789abcdef0123456789abcdef0123456789abcdef",
+                         "my-reg.example.com:443/team/app__x.y-z:1.0"})
+    EXPECT_EQ(build::image_reference_problem(ok), std::string(""));
+  for (const char* bad : {"", "/devspace", "user//app", "user/", "User/App", "reg.io/", "app:", "app:-bad",
+                          "a b", "user/app@sha256:xyz"})
+    EXPECT_TRUE(!build::image_reference_problem(bad).empty());
+}

@@ -5,6 +5,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstring>
 #include <chrono>
 #include <regex>
 #include <thread>
@@ -13,6 +14,7 @@
 #include "core/log.h"
 #include "core/strutil.h"
 #include "kube/client.h"
+#include "sync/frame.h"
 #include "sync/sync.h"
 #include "testing.h"
 
@@ -452,4 +454,171 @@ TEST(sync_downstream_archive_rejects_parent_segments) {
   EXPECT_TRUE(!fs::exists(fs::join(fs::dirname(d.local), "escaped2.txt")));
   EXPECT_TRUE(has_dotdot_segment("/a/../b"));
   EXPECT_TRUE(!has_dotdot_segment("/a/..b/c.."));
+}
+
+// ---------------------------------------------------------------- streaming (bounded memory)
+
+TEST(sync_frame_header_is_64_bit) {
+  for (uint64_t n : {0ull, 1ull, 0xffffffffull, 0x100000000ull, (5ull << 30) + 7, (1ull << 63) + 3}) {
+    std::string h = sync::frame::header('D', n);
+    EXPECT_EQ(h.size(), sync::frame::kHeaderSize);
+    char op = 0;
+    uint64_t len = 0;
+    sync::frame::parse_header((const unsigned char*)h.data(), &op, &len);
+    EXPECT_EQ(op, 'D');
+    EXPECT_EQ(len, n);
+  }
+}
+
+// 4.5 GiB of generated data through ChunkWriter -> pipe of chunks -> ChunkReader, never held in
+// memory: the archive stream of the helper protocol has no 32-bit limit anywhere.
+TEST(sync_chunk_stream_over_4gib) {
+  const uint64_t total = (9ull << 29) + 12345;  // 4.5 GiB + change
+  auto gen = [](uint64_t off) { return (char)((off >> 16) * 2654435761ull >> 7); };  // per 64 KiB block
+  // the writer's output is consumed by the reader through a bounded ring (no real pipe needed)
+  std::string ring;
+  size_t ring_pos = 0;
+  uint64_t produced = 0;
+  sync::frame::ChunkWriter cw([&](const char* d, size_t n) {
+    ring.append(d, n);
+    return true;
+  });
+  Source raw = [&](char* b, size_t n) -> ssize_t {
+    while (ring_pos >= ring.size()) {
+      ring.clear();
+      ring_pos = 0;
+      if (produced == total) {
+        if (!cw.finish()) return -1;
+        if (ring.empty()) return 0;
+        break;
+      }
+      char buf[1 << 16];
+      size_t k = (size_t)std::min<uint64_t>(sizeof(buf), total - produced);
+      std::memset(buf, gen(produced), k);  // produced is 64 KiB-aligned here
+      produced += k;
+      if (!cw.write(buf, k)) return -1;
+    }
+    size_t c = std::min(n, ring.size() - ring_pos);
+    std::memcpy(b, ring.data() + ring_pos, c);
+    ring_pos += c;
+    return (ssize_t)c;
+  };
+  sync::frame::ChunkReader cr(raw);
+  uint64_t got = 0;
+  bool ok = true;
+  char buf[1 << 16];
+  while (true) {
+    ssize_t r = cr.read(buf, sizeof(buf));
+    if (r == 0) break;
+    for (ssize_t i = 0; i < r; i += 4093) ok = ok && buf[i] == gen(got + (uint64_t)i);
+    got += (uint64_t)r;
+  }
+  EXPECT_TRUE(ok);
+  EXPECT_EQ(got, total);
+  EXPECT_EQ(cr.bytes(), total);
+  EXPECT_TRUE(ring.size() < (4u << 20));  // bounded buffering
+}
+
+TEST(sync_chunk_reader_rejects_truncation) {
+  std::string wire;
+  sync::frame::ChunkWriter cw(string_sink(&wire), 1000);
+  std::string data(2500, 'x');
+  cw.write(data.data(), data.size());
+  cw.finish();
+  std::string cut = wire.substr(0, wire.size() - 600);  // inside the last chunk, no end marker
+  sync::frame::ChunkReader cr(string_source(&cut));
+  EXPECT_THROWS(cr.drain());
+}
+
+TEST(sync_adaptive_gzip_stream_matches_oneshot) {
+  std::string data;
+  for (int i = 0; i < 3000000; ++i) data.push_back((char)(i % 7 == 0 ? (i * 131) : 'a' + i % 13));
+  std::string rnd = random_string(3 << 20);
+  data += rnd;
+  std::string out;
+  AdaptiveGzipWriter w(string_sink(&out), 1);
+  for (size_t off = 0; off < data.size(); off += 77777) w.write(data.data() + off, std::min<size_t>(77777, data.size() - off));
+  EXPECT_TRUE(w.finish());
+  EXPECT_EQ(gzip_decompress(out), data);
+  EXPECT_EQ(gzip_decompress(gzip_compress_adaptive(data, 1)), data);
+}
+
+TEST(sync_gzip_single_member_returns_leftover) {
+  std::string member = gzip_compress(std::string(100000, 'q'));
+  std::string wire = member + "\nDSEND 0\n";
+  GzipReader gz(string_source(&wire));
+  gz.set_single_member(true);
+  std::string out;
+  char buf[4096];
+  while (true) {
+    ssize_t n = gz.read(buf, sizeof(buf));
+    EXPECT_TRUE(n >= 0);
+    if (n == 0) break;
+    out.append(buf, (size_t)n);
+  }
+  EXPECT_EQ(out.size(), (size_t)100000);
+  EXPECT_EQ(gz.leftover(), std::string("\nDSEND 0\n"));
+}
+
+TEST(sync_spill_buffer_spills_and_replays) {
+  SpillBuffer sb(1000);
+  std::string want;
+  for (int i = 0; i < 5000; ++i) {
+    std::string piece = std::to_string(i) + ",";
+    want += piece;
+    EXPECT_TRUE(sb.append(piece.data(), piece.size()));
+  }
+  EXPECT_TRUE(sb.spilled());
+  EXPECT_EQ(sb.size(), (uint64_t)want.size());
+  std::string got;
+  EXPECT_TRUE(sb.replay(string_sink(&got)));
+  EXPECT_EQ(got, want);
+  EXPECT_EQ(sb.head(6), want.substr(0, 6));
+  SpillBuffer small(1000);
+  small.append("abc", 3);
+  EXPECT_TRUE(!small.spilled());
+  got.clear();
+  EXPECT_TRUE(small.replay(string_sink(&got)));
+  EXPECT_EQ(got, std::string("abc"));
+}
+
+TEST(sync_tar_reader_rejects_bad_checksum) {
+  std::string raw;
+  TarWriter tw(string_sink(&raw));
+  TarEntry e;
+  e.name = "a.txt";
+  tw.add_file(e, "hello");
+  tw.finish();
+  raw[10] ^= 0x5a;  // corrupt the name: the header checksum no longer matches
+  TarReader tr(string_source(&raw));
+  TarEntry got;
+  EXPECT_THROWS(tr.next(&got));
+}
+
+TEST(sync_chunk_stream_codes_chunks_by_entropy) {
+  std::string text, rnd = random_string(1);
+  for (int i = 0; i < 200000; ++i) text += "line " + std::to_string(i % 977) + " of a log\n";
+  std::string noise;
+  for (int i = 0; i < (3 << 20); ++i) noise.push_back((char)(std::rand() & 0xff));
+  std::string data = text + noise + text;
+  std::string wire;
+  sync::frame::ChunkWriter cw(string_sink(&wire), sync::frame::kMaxChunk, 1);
+  for (size_t off = 0; off < data.size(); off += 100000) cw.write(data.data() + off, std::min<size_t>(100000, data.size() - off));
+  EXPECT_TRUE(cw.finish());
+  EXPECT_TRUE(cw.deflated_chunks() >= 4);                 // the text chunks
+  EXPECT_TRUE(wire.size() < noise.size() + text.size());  // text compressed, noise stored as-is
+  sync::frame::ChunkReader cr(string_source(&wire));
+  std::string back;
+  char buf[70000];
+  while (true) {
+    ssize_t r = cr.read(buf, sizeof(buf));
+    if (r == 0) break;
+    back.append(buf, (size_t)r);
+  }
+  EXPECT_EQ(back.size(), data.size());
+  EXPECT_TRUE(back == data);
+  std::string bad = wire;
+  bad[10] ^= 0x55;  // inside the first (deflated) chunk
+  sync::frame::ChunkReader cr2(string_source(&bad));
+  EXPECT_THROWS(cr2.drain());
 }

@@ -191,6 +191,71 @@ def test_init_detects_rocm_pytorch_and_requests_gpus(localkube):
     lk.run(["purge"], proj)
 
 
+def test_init_8_gpus_sizes_pod_and_analyze_flags_undersized(localkube):
+    """`devspace init` of a rocm-pytorch project for 8 GPUs: CPU and memory sized
+    per GPU with requests = limits, memory >= memory-backed shm + a host budget per rank, the
+    amd.com/gpu NoSchedule toleration, ML sync excludes and a pinned base image tag. Then the
+    round-2 sizing (2 CPUs / 4 Gi for 8 GPUs with 128 Gi shm) is flagged by `analyze`."""
+    import yaml
+
+    lk = localkube
+    proj = os.path.join(lk.base, "init-torch8")
+    os.makedirs(proj, exist_ok=True)
+    with open(os.path.join(proj, "train.py"), "w") as f:
+        f.write("import torch\nprint(torch.__version__)\n")
+    answers = "\n8\ntorch8-ns\n\nlocal.registry\nlocal.registry/torch8\nno\n"
+    out = lk.run(["init"], proj, input=answers).stdout
+    assert "Project successfully initialized" in out
+    assert "Sizing the pod for 8 GPU(s)" in out, out
+    values = yaml.safe_load(open(os.path.join(proj, "chart", "values.yaml")))
+    comp = values["components"][0]
+    res = comp["containers"][0]["resources"]
+    assert res["limits"] == {"gpu": 8, "cpu": "96", "memory": "640Gi"}, res
+    assert res["requests"] == {"cpu": "96", "memory": "640Gi"}, res
+    assert comp["shmPerGPU"] == 16 and comp["hostMemoryPerGPU"] == 64
+    df = open(os.path.join(proj, "Dockerfile")).read()
+    assert re.search(r"^FROM rocm/pytorch:rocm[\w.]+_pytorch_release_[\d.]+$", df, re.M), df
+    cfg = yaml.safe_load(open(os.path.join(proj, ".devspace", "config.yaml")))
+    excludes = cfg["dev"]["sync"][0]["excludePaths"]
+    for e in ("__pycache__/", "*.pyc", ".ipynb_checkpoints/", "checkpoints/", "*.pt", "*.safetensors", "wandb/", "data/"):
+        assert e in excludes, excludes
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    raw = open(cfg_path).read().replace("chartPath: ./chart", "chartPath: ./chart\n    wait: false")
+    open(cfg_path, "w").write(raw)
+    lk.run(["deploy"], proj, timeout=120)
+    pods = wait_for(lambda: lk.pods("torch8-ns"), what="gpu pod object")
+    spec = pods[0]["spec"]
+    c = spec["containers"][0]
+    assert c["resources"]["limits"]["cpu"] == "96" and c["resources"]["requests"]["memory"] == "640Gi"
+    assert {"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"} in spec["tolerations"]
+    shm = [v for v in spec["volumes"] if v["name"] == "dshm"][0]["emptyDir"]["sizeLimit"]
+    assert shm == "128Gi"
+    report = lk.run(["analyze", "--wait=false", "-n", "torch8-ns"], proj, check=False).stdout
+    assert "OOM" not in report and "CPU(s) for" not in report, report
+    # the round-2 defaults: 2 CPUs and 4 Gi for 8 ranks sharing a 128 Gi memory-backed /dev/shm
+    values["components"][0]["containers"][0]["resources"] = {"limits": {"gpu": 8, "cpu": "2", "memory": "4Gi"},
+                                                            "requests": {"cpu": "2", "memory": "4Gi"}}
+    open(os.path.join(proj, "chart", "values.yaml"), "w").write(yaml.safe_dump(values))
+    lk.run(["deploy", "-d"], proj, timeout=120)
+    wait_for(lambda: [p for p in lk.pods("torch8-ns")
+                      if p["spec"]["containers"][0]["resources"]["limits"]["memory"] == "4Gi"], what="resized pod")
+    report = lk.run(["analyze", "--wait=false", "-n", "torch8-ns"], proj, check=False).stdout
+    assert "OOM-killed" in report and "2 CPU(s) for 8 GPU rank(s)" in report, report
+    lk.run(["purge"], proj)
+
+
+def test_init_rejects_invalid_image_name(localkube):
+    lk = localkube
+    proj = os.path.join(lk.base, "init-badimg")
+    os.makedirs(proj, exist_ok=True)
+    with open(os.path.join(proj, "index.js"), "w") as f:
+        f.write("console.log(1)\n")
+    answers = "\nbad-ns\n3000\nlocal.registry\nlocal.registry//Bad\nno\n"
+    p = lk.run(["init"], proj, input=answers, check=False)
+    assert p.returncode != 0
+    assert "invalid image name" in p.stdout + p.stderr, p.stdout + p.stderr
+
+
 def test_add_list_remove_config_commands(localkube):
     lk = localkube
     proj = lk.project("quickstart", "quickstart-cfg")
