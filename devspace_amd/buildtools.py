@@ -41,14 +41,27 @@ def build_hip(verbose=False):
     return ops_build.build(verbose=verbose)
 
 
+def write_example_kit(verbose=False):
+    """examples/rocm-pytorch carries the workload kit like a `devspace init`'d project does
+    (devspace_amd/kit.py; not tracked in git), with the in-tree gfx950 build in place of the
+    image build's cached one."""
+    from devspace_amd import kit
+
+    written = kit.write_kit(os.path.join(ROOT, "examples", "rocm-pytorch"), prebuilt=True)
+    if verbose and written:
+        print("+ workload kit -> examples/rocm-pytorch/devspace_amd: " + ", ".join(written), flush=True)
+
+
 def build_all(verbose=False):
     build_cpp(verbose=verbose)
     try:
         build_hip(verbose=verbose)
     except FileNotFoundError as e:  # hipcc missing: CPU-only environments still get the tool
         print(f"skipping HIP build: {e}", flush=True)
+    write_example_kit(verbose=verbose)
 
 
 def ensure_built():
     if not native_ready():
         build_cpp(verbose=False)
+    write_example_kit()

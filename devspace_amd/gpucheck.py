@@ -29,7 +29,7 @@ class Probe:
 
         path = path or ops_build.lib_path()
         if not os.path.exists(path):
-            ops_build.build()
+            ops_build.build_probe()
         self.lib = ctypes.CDLL(path)
         self.lib.gp_device_count.restype = ctypes.c_int
         self.lib.gp_device_info.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]

@@ -40,7 +40,10 @@ def close_proc(proc):
 HOST_ONLY_ENV = {"RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
                  "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT", "KUBECONFIG",
                  "DOCKER_HOST", "DOCKER_CERT_PATH", "DOCKER_TLS_VERIFY", "HIP_VISIBLE_DEVICES",
-                 "CUDA_VISIBLE_DEVICES", "DEVSPACE_NONINTERACTIVE"}
+                 "CUDA_VISIBLE_DEVICES", "DEVSPACE_NONINTERACTIVE",
+                 # a container sees its image's Python path, not the developer's checkout: a pod
+                 # imports devspace_amd only when its project vendors it (rocm-pytorch kit)
+                 "PYTHONPATH"}
 HOST_ONLY_ENV_PREFIXES = ("TORCHELASTIC_", "TORCH_ELASTIC_", "PET_")
 
 # Binaries of tool images that exist on the host under another name / as an emulation.
@@ -496,6 +499,9 @@ class Kubelet:
         for e in c.spec.get("env") or []:
             if "value" in e:
                 env[e["name"]] = str(e["value"])
+        if self._argv(c)[:3] == [sys.executable, "-m", "devspace_amd.localkube.kaniko"]:
+            # the kaniko emulation is part of this cluster, not of the image
+            env["PYTHONPATH"] = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["HOSTNAME"] = rt.name
         env["DEVSPACE_CONTAINER_ROOT"] = c.root
         env["DEVSPACE_LOCAL_IMAGES"] = self.images.root  # used by the kaniko emulation

@@ -48,11 +48,43 @@ def build_probe(verbose=False, force=False):
     return out
 
 
-def build_fused(verbose=False, force=False):
+def _fused_tag():
+    """Cache key of a fused-ops build: source bytes, torch build, target arch, Python ABI."""
+    import hashlib
+
+    import torch
+
+    h = hashlib.sha256(open(os.path.join(HERE, "fused_ops.hip"), "rb").read())
+    h.update(f"{torch.__version__}|{torch.version.hip}|{ARCH}|{sysconfig.get_config_var('EXT_SUFFIX')}".encode())
+    return h.hexdigest()[:16]
+
+
+def fused_cache_path():
+    """Where a vendored copy (a project made by `devspace init`, running in its pod) keeps the
+    extension it compiled: $DEVSPACE_OPS_CACHE or ~/.cache/devspace_amd, keyed by _fused_tag()."""
+    base = os.environ.get("DEVSPACE_OPS_CACHE") or os.path.join(os.path.expanduser("~"), ".cache", "devspace_amd")
+    return os.path.join(base, "fused-" + _fused_tag(), "_fused_ops" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def ensure_fused_cached(verbose=True):
+    """Compiles the extension into the cache unless it is there (minutes: done at image build by
+    the rocm-pytorch Dockerfile, else once on the first pod start). Returns its path."""
+    out = fused_cache_path()
+    if not os.path.exists(out):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        tmp = out + f".tmp{os.getpid()}"
+        if verbose:
+            print(f"[devspace_amd] compiling the fused gfx950 ops ({ARCH}) into {out} ...", flush=True)
+        build_fused(verbose=False, force=True, out=tmp)
+        os.replace(tmp, out)  # concurrent ranks: whoever finishes first wins, the rest overwrite
+    return out
+
+
+def build_fused(verbose=False, force=False, out=None):
     import torch  # headers + libraries of the torch this extension is loaded into
 
     src = os.path.join(HERE, "fused_ops.hip")
-    out = fused_path()
+    out = out or fused_path()
     if not (force or _stale(out, src)):
         return out
     troot = os.path.dirname(torch.__file__)
@@ -73,3 +105,23 @@ def build(verbose=False, force=False):
     out = build_probe(verbose=verbose, force=force)
     build_fused(verbose=verbose, force=force)
     return out
+
+
+def main(argv=None):
+    import argparse
+
+    p = argparse.ArgumentParser(prog="devspace_amd.ops.build", description=__doc__.split("\n")[0])
+    p.add_argument("--fused", action="store_true", help="the fused training ops")
+    p.add_argument("--probe", action="store_true", help="the GPU probe library")
+    p.add_argument("--cache", action="store_true",
+                   help="build the fused ops into the cache (image build of a vendored copy) instead of in place")
+    a = p.parse_args(argv)
+    if a.probe:
+        print(build_probe(verbose=True))
+    if a.fused:
+        print(ensure_fused_cached() if a.cache else build_fused(verbose=True))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -21,20 +21,50 @@ _ext = None
 _ext_error = None
 
 
+def _load_cached():
+    """A copy of this package vendored into a project (`devspace init`, rocm-pytorch) has no
+    in-tree build: compile into the cache (done at image build by the template's Dockerfile,
+    else once on the first pod start) and load it from there."""
+    import importlib.util
+
+    from . import build
+
+    path = build.ensure_fused_cached()
+    spec = importlib.util.spec_from_file_location(f"{__package__}._fused_ops", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def ext():
     """The compiled extension module (raises with the build error on a GPU box)."""
     global _ext, _ext_error
     if _ext is None and _ext_error is None:
         try:
-            from devspace_amd.ops import _fused_ops  # noqa: WPS433
+            from . import _fused_ops  # noqa: WPS433 - the in-tree (or image-built) extension
 
             _ext = _fused_ops
         except ImportError as e:  # pragma: no cover - depends on the build
-            _ext_error = e
+            try:
+                _ext = _load_cached()
+            except Exception as e2:  # no hipcc / ROCm headers in the image, build error
+                _ext_error = f"{e}; building it failed: {e2}"
     if _ext is None:
         raise RuntimeError(f"devspace_amd fused HIP ops are not built ({_ext_error}); run "
-                           "`python -c 'import __graft_entry__ as g; g.build()'`")
+                           "`python -m devspace_amd.ops.build --fused`")
     return _ext
+
+
+def backend() -> str:
+    """"hip" when the gfx950 kernels are loaded (loading or compiling them now), else
+    "eager (<why>)". For the training script's start-up line: never a silent fallback."""
+    if not torch.cuda.is_available():
+        return "eager (no GPU)"
+    try:
+        ext()
+        return "hip"
+    except RuntimeError as e:
+        return f"eager ({e})"
 
 
 def _use_hip(t: torch.Tensor) -> bool:

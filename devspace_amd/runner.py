@@ -16,7 +16,8 @@ communicators) and swaps only the *code* at a step boundary:
 
 On every source change each rank recompiles the module from disk; the ranks agree on the
 code generation with one tiny MAX all-reduce per step (so collectives inside `step` stay
-matched), and rank 0 prints
+matched) over a separate gloo (CPU) group: the control plane never enqueues work on a GPU
+stream nor waits for one, so the host keeps running ahead of the GPUs. Rank 0 prints
 
     [devspace-runner] reloaded gen=3 marker=v1 step=120 loss=... step_ms=... reload_ms=...
 
@@ -24,8 +25,10 @@ A module without `step()` is treated as a plain script and re-executed in the wa
 interpreter on each change. Exceptions in new code keep the previous version running.
 
 Preemptible steps: a step may call `ctx.preempt_point()` between its phases (e.g. between
-forward and backward). On a single GPU the point abandons the rest of the step when a newer
-version of the code is waiting — before the optimizer touched any state. For long steps
+forward and backward). The point abandons the rest of the step when a newer version of the
+code is waiting — before the optimizer touched any state. With several ranks the decision is
+collective (rank 0's view, agreed over the gloo group at the point), so every rank leaves the
+step at the same point and the collectives of the next step stay matched. For long steps
 (loop period >= --preempt-drain-ms, default 20 ms) the point also drains the GPU work queued
 so far while watching the change feed, so an edit waits only for the phase in flight instead
 of the whole queued step (the host otherwise runs a full step ahead of the GPU and blocks in
@@ -91,14 +94,100 @@ class _PollWatcher:
         pass
 
 
+class _InotifyWatcher:
+    """inotify through ctypes: what the runner uses inside a pod, where the native module
+    (built for the developer machine's Python) is not importable. Recursive, settled events
+    only (close-after-write, renames, deletes), so a file still being written triggers nothing."""
+
+    _IN_CLOSE_WRITE, _IN_MOVED_FROM, _IN_MOVED_TO = 0x008, 0x040, 0x080
+    _IN_CREATE, _IN_DELETE, _IN_DELETE_SELF, _IN_Q_OVERFLOW = 0x100, 0x200, 0x400, 0x4000
+    _IN_ISDIR, _IN_IGNORED, _IN_NONBLOCK, _IN_CLOEXEC = 0x40000000, 0x8000, 0o4000, 0o2000000
+
+    def __init__(self, path: str):
+        import ctypes
+        import ctypes.util
+
+        self._libc = ctypes.CDLL(ctypes.util.find_library("c") or "libc.so.6", use_errno=True)
+        self.fd = self._libc.inotify_init1(self._IN_NONBLOCK | self._IN_CLOEXEC)
+        if self.fd < 0:
+            raise OSError(ctypes.get_errno(), "inotify_init1 failed")
+        self.mask = (self._IN_CLOSE_WRITE | self._IN_MOVED_FROM | self._IN_MOVED_TO | self._IN_CREATE |
+                     self._IN_DELETE | self._IN_DELETE_SELF)
+        self.wds = {}
+        self._add_tree(path)
+
+    def _add(self, d: str) -> None:
+        wd = self._libc.inotify_add_watch(self.fd, os.fsencode(d), self.mask)
+        if wd >= 0:
+            self.wds[wd] = d
+
+    def _add_tree(self, root: str) -> None:
+        for d, dirs, _ in os.walk(root):
+            dirs[:] = [x for x in dirs if x not in ("__pycache__", ".git")]
+            self._add(d)
+
+    def poll(self, timeout_ms: int = 0):
+        import select
+        import struct
+
+        out = []
+        r, _, _ = select.select([self.fd], [], [], max(0, timeout_ms) / 1000.0)
+        if not r:
+            return out
+        while True:
+            try:
+                buf = os.read(self.fd, 1 << 16)
+            except BlockingIOError:
+                break
+            off = 0
+            while off + 16 <= len(buf):
+                wd, mask, _cookie, n = struct.unpack_from("iIII", buf, off)
+                name = buf[off + 16:off + 16 + n].split(b"\0", 1)[0].decode(errors="replace")
+                off += 16 + n
+                if mask & self._IN_IGNORED:
+                    self.wds.pop(wd, None)
+                    continue
+                if mask & self._IN_Q_OVERFLOW:
+                    out.append(next(iter(self.wds.values()), ""))  # events were lost: reload
+                    continue
+                base = self.wds.get(wd)
+                if base is None:
+                    continue
+                p = os.path.join(base, name) if name else base
+                if mask & self._IN_ISDIR:
+                    if mask & (self._IN_CREATE | self._IN_MOVED_TO):
+                        self._add_tree(p)
+                    continue
+                if mask & self._IN_CREATE:
+                    continue  # wait for its close-after-write
+                out.append(p)
+            # a burst (an editor's write + rename) arrives within microseconds: take it whole
+            r, _, _ = select.select([self.fd], [], [], 0.002)
+            if not r:
+                break
+        return out
+
+    def close(self):
+        if self.fd >= 0:
+            os.close(self.fd)
+            self.fd = -1
+
+
 def make_watcher(path: str):
+    settled = os.environ.get("DEVSPACE_WATCH_SETTLED", "1") != "0"
     try:
         from devspace_amd import _native  # noqa: WPS433
 
         # settled events only: a file still being written must not trigger (or preempt) a reload
-        return _native.Watcher(path, settled_only=os.environ.get("DEVSPACE_WATCH_SETTLED", "1") != "0")
-    except Exception:  # pragma: no cover - native module missing
-        return _PollWatcher(path)
+        return _native.Watcher(path, settled_only=settled)
+    except Exception:  # native module missing: a vendored runner inside a pod
+        pass
+    if settled and sys.platform.startswith("linux"):
+        try:
+            return _InotifyWatcher(path)
+        except OSError:
+            pass
+    return _PollWatcher(path)
 
 
 class Preempted(BaseException):
@@ -106,6 +195,36 @@ class Preempted(BaseException):
     step is skipped and the runner swaps the code right away. A BaseException (like
     KeyboardInterrupt) so a user step's generic `except Exception` cannot swallow it and carry
     on into the optimizer update."""
+
+
+class Agreement:
+    """Control plane of a multi-rank group: the code generation at each step boundary and the
+    preemption decision at each `preempt_point()`, agreed with MAX all-reduces of CPU tensors
+    over a dedicated gloo process group. Nothing here touches a GPU stream or reads a device
+    tensor (no `.item()` / `.tolist()` on the device: those would stall the host on every
+    step). Every rank must make the same sequence of calls."""
+
+    def __init__(self, dist, group=None):
+        import torch
+
+        self.dist = dist
+        self.group = group if group is not None else dist.new_group(backend="gloo")
+        self.ctl = torch.zeros(2, dtype=torch.int64)  # [newest generation, helper modules changed]
+        self.flag = torch.zeros(1, dtype=torch.int64)
+        self.calls = 0
+
+    def boundary(self, pending_gen: int, helper_pending: bool):
+        self.ctl[0] = pending_gen
+        self.ctl[1] = int(helper_pending)
+        self.dist.all_reduce(self.ctl, op=self.dist.ReduceOp.MAX, group=self.group)
+        self.calls += 1
+        return int(self.ctl[0]), bool(self.ctl[1])
+
+    def preempt(self, pending: bool) -> bool:
+        self.flag[0] = int(pending)
+        self.dist.all_reduce(self.flag, op=self.dist.ReduceOp.MAX, group=self.group)
+        self.calls += 1
+        return bool(self.flag[0])
 
 
 class Context:
@@ -123,6 +242,7 @@ class Context:
         self._event = None  # one reusable HIP event for the drain
         self._period_ms = 0.0  # steady-state loop period (set by the runner)
         self._drain_min_ms = 20.0  # drain at preemption points only for steps at least this long
+        self._agree = None  # Agreement when world > 1
 
     def log(self, msg: str) -> None:
         if self.rank == 0:
@@ -131,15 +251,26 @@ class Context:
     def preempt_point(self) -> None:
         """Cooperative reload point inside `step()`: raises Preempted if a newer version of the
         code is waiting. For long steps it first drains the GPU work queued so far while polling
-        the change feed. No-op when distributed (every rank must issue the same collectives, and
-        the ranks only agree on the generation at the step boundary) or when preemption is off."""
+        the change feed. With several ranks the ranks decide together (rank 0's change feed,
+        one gloo all-reduce of a CPU flag) so they all leave the step at the same point; the
+        drain then runs to completion before the decision (a decision polled during the drain
+        would differ between ranks). No-op when preemption is off."""
         feed = self._feed
         if feed is None:
             return
+        long_step = self.device.type == "cuda" and self._period_ms >= self._drain_min_ms
+        if self._agree is not None:
+            if long_step:
+                self._drain(None)
+            if self._agree.preempt(self.rank == 0 and feed.pending()):
+                raise Preempted()
+            return
         if feed.pending():
             raise Preempted()
-        if self.device.type != "cuda" or self._period_ms < self._drain_min_ms:
-            return
+        if long_step:
+            self._drain(feed)
+
+    def _drain(self, feed) -> None:
         import torch
 
         if self._event is None:
@@ -147,7 +278,7 @@ class Context:
         ev = self._event
         ev.record()
         while not ev.query():
-            if feed.pending():
+            if feed is not None and feed.pending():
                 raise Preempted()
             time.sleep(0)  # releases the GIL: the change feed thread can post the edit
 
@@ -307,8 +438,8 @@ def worker_main(args) -> int:
     ctx.generation = gen
     state = mod.setup(ctx) if hasattr(mod, "setup") else None
     setup_version = getattr(mod, "SETUP_VERSION", None)
-    # [newest generation, helper modules changed]: all-reduced (MAX) every step
-    ctl = torch.zeros(2, dtype=torch.int64, device=device) if world > 1 else None
+    # control plane of the group (gloo, CPU tensors): generation + preemption agreement
+    agree = Agreement(dist) if world > 1 else None
     helper_pending = False
     first = {}
     if hasattr(mod, "step"):
@@ -319,13 +450,15 @@ def worker_main(args) -> int:
     # Preemption only from here on: an edit that lands during setup() or the first step stays
     # pending in the feed and is picked up by the main loop's first check (a Preempted raised
     # there would have had no handler).
-    if args.preempt and world == 1:
+    if args.preempt:
         ctx._feed = feed
+        ctx._agree = agree
         ctx._drain_min_ms = args.preempt_drain_ms
     ctx.log(
         f"started gen={gen} marker={getattr(mod, 'MARKER', '')} digest={mod.__devspace_digest__} "
         f"world={world} device={device} loss={first.get('loss') if isinstance(first, dict) else None} "
-        f"startup_ms={(time.perf_counter() - t_start) * 1000.0:.1f}"
+        f"startup_ms={(time.perf_counter() - t_start) * 1000.0:.1f} "
+        f"kit={os.path.dirname(os.path.dirname(os.path.abspath(__file__)))}"
     )
     pending_gen = gen
     reload_t0 = None
@@ -348,7 +481,7 @@ def worker_main(args) -> int:
         # Rank 0's feed alone advances the generation: every rank watches the same synced
         # directory, but their feeds post the edit microseconds apart, and a rank that saw it one
         # step late would otherwise bump the group to a second generation (a spurious reload).
-        if n_changes and (ctl is None or rank == 0):
+        if n_changes and (agree is None or rank == 0):
             pending_gen += 1
             helper_pending = helper_pending or helper_changed
             if reload_t0 is None:
@@ -356,13 +489,10 @@ def worker_main(args) -> int:
         # 2. ranks agree on the newest generation (keeps collectives in `step` matched) and on
         #    whether helper modules must be re-imported (rank 0's view, like the generation)
         target = pending_gen
-        if ctl is not None:
-            ctl[0] = pending_gen
-            ctl[1] = int(helper_pending)
-            dist.all_reduce(ctl, op=dist.ReduceOp.MAX)
-            target, agreed_helper = (int(v) for v in ctl.tolist())
+        if agree is not None:
+            target, agreed_helper = agree.boundary(pending_gen, helper_pending)
             pending_gen = max(pending_gen, target)
-            helper_pending = helper_pending or bool(agreed_helper)
+            helper_pending = helper_pending or agreed_helper
         if target > gen:
             t_reload = time.perf_counter()
             wait_ms = (t_reload - reload_t0) * 1000.0 if reload_t0 else 0.0

@@ -9,27 +9,43 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-try:  # gfx950 HIP kernels shipped with devspace_amd (attention, RMSNorm, SwiGLU, CE, AdamW)
-    from devspace_amd.ops.fused import AdamW, RMSNorm, add_rms_norm, attention, cross_entropy, swiglu
-except ImportError:  # plain PyTorch when the package is not in the image
-    RMSNorm = nn.RMSNorm
-    AdamW = None
 
-    def add_rms_norm(x, delta, weight, eps=None):
-        s = x + delta
-        return s, F.rms_norm(s, (s.shape[-1],), weight, eps)
+def _eager_add_rms_norm(x, delta, weight, eps=None):
+    s = x + delta
+    return s, F.rms_norm(s, (s.shape[-1],), weight, eps)
 
-    def attention(qkv, causal=True):
-        q, k, v = qkv.unbind(2)
-        o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=causal)
-        return o.transpose(1, 2)
 
-    def swiglu(h):
-        g, u = h.chunk(2, dim=-1)
-        return F.silu(g) * u
+def _eager_attention(qkv, causal=True):
+    q, k, v = qkv.unbind(2)
+    o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=causal)
+    return o.transpose(1, 2)
 
-    def cross_entropy(logits, target):
-        return F.cross_entropy(logits.float(), target)
+
+def _eager_swiglu(h):
+    g, u = h.chunk(2, dim=-1)
+    return F.silu(g) * u
+
+
+def _eager_cross_entropy(logits, target):
+    return F.cross_entropy(logits.float(), target)
+
+
+# gfx950 HIP kernels (attention, RMSNorm, SwiGLU, cross-entropy, AdamW) from devspace_amd.ops,
+# which `devspace init` vendors into the project next to this file (built at image build, or
+# compiled once on the first pod start). FUSED says which path runs; setup() prints it.
+try:
+    from devspace_amd.ops import fused as _fused
+
+    FUSED = _fused.backend()
+except ImportError as e:  # the kit is not in the image
+    _fused, FUSED = None, f"eager (devspace_amd.ops not importable: {e})"
+if FUSED == "hip" or (_fused is not None and not torch.cuda.is_available()):
+    # (without a GPU the fused module runs its PyTorch formulation: CPU smoke runs and tests)
+    AdamW, RMSNorm = _fused.AdamW, _fused.RMSNorm
+    add_rms_norm, attention, cross_entropy, swiglu = _fused.add_rms_norm, _fused.attention, _fused.cross_entropy, _fused.swiglu
+else:
+    AdamW, RMSNorm = None, nn.RMSNorm
+    add_rms_norm, attention, cross_entropy, swiglu = _eager_add_rms_norm, _eager_attention, _eager_cross_entropy, _eager_swiglu
 
 MARKER = "v0"
 SETUP_VERSION = 1  # bump to rebuild model/optimizer on the next reload
@@ -84,6 +100,7 @@ class TinyLM(nn.Module):
 
 
 def setup(ctx):
+    ctx.log(f"fused={FUSED}")
     torch.manual_seed(1234 + ctx.rank)
     model = TinyLM().to(device=ctx.device, dtype=torch.bfloat16)
     if ctx.distributed:

@@ -156,7 +156,9 @@ TEST(generator_detects_languages) {
   EXPECT_TRUE(fs::exists(fs::join(d, "chart/Chart.yaml")));
   EXPECT_TRUE(fs::exists(fs::join(d, "chart/templates/deployments.yaml")));
   EXPECT_TRUE(contains(fs::read_file(fs::join(d, "Dockerfile")), "rocm/pytorch"));
-  EXPECT_TRUE(contains(fs::read_file(fs::join(d, "devspace_runner.py")), "Hot-reload runner"));
+  EXPECT_TRUE(contains(fs::read_file(fs::join(d, "devspace_amd/runner.py")), "Hot-reload runner"));
+  EXPECT_TRUE(contains(fs::read_file(fs::join(d, "devspace_amd/ops/fused_ops.hip")), "gfx950"));
+  EXPECT_TRUE(fs::exists(fs::join(d, "devspace_amd/ops/build.py")));
   // no overwrite of user files
   EXPECT_TRUE(contains(fs::read_file(fs::join(d, "train.py")), "import torch"));
   fs::remove_all(d);

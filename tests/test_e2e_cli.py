@@ -12,6 +12,8 @@ import time
 
 import pytest
 
+from conftest import ROOT
+
 
 def wait_for(fn, timeout=30.0, interval=0.05, what="condition"):
     deadline = time.time() + timeout
@@ -162,7 +164,13 @@ def test_init_detects_rocm_pytorch_and_requests_gpus(localkube):
     out = lk.run(["init"], proj, input=answers).stdout
     assert "Project successfully initialized" in out
     assert "FROM rocm/pytorch" in open(os.path.join(proj, "Dockerfile")).read()
-    assert os.path.exists(os.path.join(proj, "devspace_runner.py"))
+    # the workload kit (runner + fused gfx950 ops) is vendored from the package, byte for byte
+    for rel in ("runner.py", "ops/fused.py", "ops/fused_ops.hip", "ops/build.py"):
+        assert open(os.path.join(proj, "devspace_amd", rel), "rb").read() == \
+            open(os.path.join(ROOT, "devspace_amd", rel), "rb").read(), rel
+    assert open(os.path.join(proj, "train.py")).read() == open(os.path.join(ROOT, "examples", "rocm-pytorch",
+                                                                            "train.py")).read()
+    assert 'CMD ["python", "-m", "devspace_amd.runner"' in open(os.path.join(proj, "Dockerfile")).read()
     values = open(os.path.join(proj, "chart", "values.yaml")).read()
     assert re.search(r"gpu: 2\b", values)
     cfg = open(os.path.join(proj, ".devspace", "config.yaml")).read()

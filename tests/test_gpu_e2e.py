@@ -44,6 +44,10 @@ def test_rocm_pytorch_pod_trains_on_gpu(tmp_path):
                     if "started gen=" in (open(root + ".log").read() if os.path.exists(root + ".log") else "")
                     else None, 300, "runner start")
         assert "device=cuda:0" in log, log
+        # the pod runs the workload kit vendored into the project (no devspace checkout on its
+        # Python path, as in a real image) and the gfx950 kernels, not an eager fallback
+        assert re.search(r"kit=" + re.escape(root), log), log
+        assert "[devspace-runner] fused=hip" in log, log
         r = lk.run(["analyze", "--wait=false", "--gpu-probe", "-n", "rocm-pytorch"], proj, timeout=300)
         report = r.stdout + r.stderr
         # the probe ran inside the pod and exercised every granted device (MFMA self-test)

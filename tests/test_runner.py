@@ -137,13 +137,13 @@ def step(ctx, state):
 '''
 
 
-def _pickup_ms(tmp_path, preempt, src=SLOW_STEP, gpu=False):
+def _pickup_ms(tmp_path, preempt, src=SLOW_STEP, gpu=False, nproc=1):
     p = tmp_path / "slow.py"
     p.write_text(src)
     env = dict(os.environ, PYTHONPATH=ROOT)
     if not gpu:
         env.update(HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1")
-    cmd = [sys.executable, "-u", "-m", "devspace_amd.runner", "--watch", str(tmp_path), str(p)]
+    cmd = [sys.executable, "-u", "-m", "devspace_amd.runner", "--nproc", str(nproc), "--watch", str(tmp_path), str(p)]
     if not preempt:
         cmd.insert(-1, "--no-preempt")
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, text=True)
@@ -184,6 +184,59 @@ def test_preempt_point_cuts_inflight_wait(tmp_path):
     inflight_np, updates_np = _pickup_ms(tmp_path, preempt=False)
     assert inflight_np > 250, inflight_np
     assert updates_np == 3
+
+
+def test_preempt_point_four_ranks_cpu(tmp_path):
+    """world > 1 preempts too: the ranks decide together at the point (rank 0's
+    change feed, one gloo all-reduce of a CPU flag), so an edit landing mid-step is picked up
+    within a fraction of the 0.8 s step on 4 gloo ranks, as with one rank, and every rank skips
+    the rest of the old step (its state update) at the same point."""
+    inflight, updates = _pickup_ms(tmp_path, preempt=True, nproc=4)
+    assert inflight < 200, inflight
+    assert updates == 2, updates
+    inflight_np, updates_np = _pickup_ms(tmp_path, preempt=False, nproc=4)
+    assert inflight_np > 250, inflight_np
+    assert updates_np == 3
+
+
+def test_control_plane_never_touches_the_device():
+    """The multi-rank control plane (generation + preemption agreement) runs on CPU tensors over
+    its own gloo group, and the steady-state training loop holds no device sync (`.item()`,
+    `.tolist()`, `torch.cuda.synchronize()`): the host keeps running ahead of the GPUs."""
+    import ast
+    import types
+
+    import torch
+
+    from devspace_amd import runner
+
+    calls = []
+
+    def all_reduce(t, op=None, group=None):
+        calls.append((t.device.type, group, op))
+        t.mul_(1)  # a single-rank MAX is the identity
+
+    fake = types.SimpleNamespace(all_reduce=all_reduce, ReduceOp=types.SimpleNamespace(MAX="max"),
+                                 new_group=lambda backend: f"group:{backend}")
+    a = runner.Agreement(fake)
+    assert a.group == "group:gloo"
+    assert a.boundary(7, True) == (7, True)
+    assert a.preempt(True) is True and a.preempt(False) is False
+    assert calls and all(c == ("cpu", "group:gloo", "max") for c in calls), calls
+
+    tree = ast.parse(open(runner.__file__).read())
+    worker = next(n for n in ast.walk(tree) if isinstance(n, ast.FunctionDef) and n.name == "worker_main")
+    loop = next(n for n in ast.walk(worker) if isinstance(n, ast.While))
+    reload_branch = next(n for n in loop.body if isinstance(n, ast.If) and "target > gen" in ast.unparse(n.test))
+    steady = [n for n in loop.body if n is not reload_branch]
+    syncing = []
+    for stmt in steady:
+        for n in ast.walk(stmt):
+            if isinstance(n, ast.Call) and isinstance(n.func, ast.Attribute) and n.func.attr in (
+                    "item", "tolist", "synchronize", "cpu"):
+                syncing.append(ast.unparse(n))
+    assert not syncing, syncing
+    assert not [n for n in ast.walk(worker) if isinstance(n, ast.Attribute) and n.attr == "tolist"]
 
 
 @pytest.mark.gpu
@@ -264,13 +317,54 @@ def test_preempted_is_not_swallowed_by_generic_handlers():
             pass
 
 
-def test_vendored_runner_copies_match_the_package():
-    """`devspace init` (templates/rocm-pytorch) and examples/rocm-pytorch ship the runner as a
-    single file next to train.py, so the image does not need devspace_amd installed."""
-    src = open(os.path.join(ROOT, "devspace_amd", "runner.py")).read()
-    for copy in (os.path.join(ROOT, "templates", "rocm-pytorch", "devspace_runner.py"),
-                 os.path.join(ROOT, "examples", "rocm-pytorch", "devspace_runner.py")):
-        assert open(copy).read() == src, f"{copy} is out of date: cp devspace_amd/runner.py {copy}"
+def test_workload_kit_is_the_package(tmp_path):
+    """The workload kit (runner + gfx950 fused ops) that `devspace init` vendors into rocm-pytorch
+    projects and the build writes into examples/rocm-pytorch is the package itself: one source
+    (devspace_amd/KIT), byte-identical copies, no tracked duplicate in git."""
+    from devspace_amd import kit
+
+    names = kit.files()
+    assert {"runner.py", "ops/fused.py", "ops/fused_ops.hip", "ops/build.py"} <= set(names)
+    kit.write_kit(str(tmp_path))
+    for rel in names:
+        assert (tmp_path / "devspace_amd" / rel).read_bytes() == open(os.path.join(ROOT, "devspace_amd", rel), "rb").read()
+    tracked = subprocess.run(["git", "ls-files", "examples/rocm-pytorch", "templates/rocm-pytorch"], cwd=ROOT,
+                             capture_output=True, text=True).stdout.split()
+    assert not [t for t in tracked if "devspace_amd/" in t or t.endswith("devspace_runner.py")], tracked
+    # the example carries the kit after a build (the test session's ensure_built)
+    for rel in names:
+        assert open(os.path.join(ROOT, "examples", "rocm-pytorch", "devspace_amd", rel), "rb").read() == \
+            open(os.path.join(ROOT, "devspace_amd", rel), "rb").read(), rel
+
+
+def test_vendored_runner_runs_without_the_checkout(tmp_path):
+    """A project with the kit and no devspace_amd on the Python path (a pod): the runner and the
+    fused ops import from the project, the file watcher is the ctypes inotify one, and train.py
+    says which op path runs (fused=... line; eager on this CPU-only machine)."""
+    from devspace_amd import kit
+
+    proj = tmp_path / "proj"
+    proj.mkdir()
+    kit.write_kit(str(proj))
+    src = open(TRAIN).read()
+    for k, v in (("VOCAB", 128), ("DIM", 64), ("HEADS", 4), ("LAYERS", 1), ("SEQ", 16), ("BATCH", 2)):
+        src = re.sub(rf"^{k} = \d+$", f"{k} = {v}", src, flags=re.M)
+    (proj / "train.py").write_text(src)
+    env = {k: v for k, v in os.environ.items() if k != "PYTHONPATH"}
+    env.update(HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1")
+    probe = subprocess.run([sys.executable, "-c", "import devspace_amd, devspace_amd.runner as r; "
+                            "print(devspace_amd.__file__); print(type(r.make_watcher('.')).__name__)"],
+                           cwd=str(proj), env=env, capture_output=True, text=True)
+    assert probe.returncode == 0, probe.stderr
+    where, watcher = probe.stdout.split()
+    assert where.startswith(str(proj)), where
+    assert watcher == "_InotifyWatcher", watcher
+    proc = subprocess.Popen([sys.executable, "-u", "-m", "devspace_amd.runner", "--max-steps", "3", "--watch",
+                             str(proj), "train.py"], cwd=str(proj), env=env, stdout=subprocess.PIPE,
+                            stderr=subprocess.STDOUT, text=True)
+    out, _ = proc.communicate(timeout=180)
+    assert proc.returncode == 0, out
+    assert "fused=eager (no GPU)" in out and "started gen=1" in out, out
 
 
 HELPER_ENTRY = '''
