@@ -576,18 +576,24 @@ class ApiServer:
             return ws
 
         async def up():
-            while True:
-                data = await reader.read(65536)
-                if not data:
-                    break
-                await ws.send_bytes(b"\x00" + data)
+            try:
+                while True:
+                    data = await reader.read(65536)
+                    if not data:
+                        break
+                    await ws.send_bytes(b"\x00" + data)
+            except (ConnectionError, asyncio.CancelledError):  # either side went away
+                pass
             await ws.close()
 
         t = asyncio.create_task(up())
-        async for msg in ws:
-            if msg.type == WSMsgType.BINARY and msg.data and msg.data[0] == 0:
-                writer.write(msg.data[1:])
-                await writer.drain()
+        try:
+            async for msg in ws:
+                if msg.type == WSMsgType.BINARY and msg.data and msg.data[0] == 0:
+                    writer.write(msg.data[1:])
+                    await writer.drain()
+        except ConnectionError:  # the pod's server closed the connection (e.g. a restart)
+            pass
         writer.close()
         t.cancel()
         return ws

@@ -73,8 +73,10 @@ def _prewarm_runtime():
     return done
 
 
-def bench_deploy(workdir, example="quickstart", tls=False):
-    base = os.path.join(workdir, "deploy-bench")
+def bench_deploy(workdir, example="quickstart", tls=False, reference=False):
+    """reference=True: the reference's waits (DEVSPACE_REFERENCE_TIMING: 1 s pod sleeps, 5 s
+    rollout polls, no kept-alive connections) and sync protocol, on the same cluster code."""
+    base = os.path.join(workdir, "deploy-bench" + ("-ref" if reference else ""))
     os.makedirs(base, exist_ok=True)
     proj = os.path.join(base, example)
     shutil.copytree(os.path.join(ROOT, "examples", example), proj, symlinks=True)
@@ -82,6 +84,8 @@ def bench_deploy(workdir, example="quickstart", tls=False):
     cluster = LocalCluster(os.path.join(base, "cluster"), gpus=0, tls=tls).start()
     try:
         env = devspace_env(cluster, base)
+        if reference:
+            env.update(DEVSPACE_REFERENCE_TIMING="1", DEVSPACE_SYNC_MODE="compat")
         trace = os.path.join(proj, ".devspace", "logs", "trace.jsonl")
         cold, out = run_devspace(["deploy"], proj, env)
         if "Successfully deployed!" not in out:

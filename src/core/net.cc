@@ -1,5 +1,7 @@
 #include "core/net.h"
 
+#include "core/compat.h"
+
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netdb.h>
@@ -588,7 +590,7 @@ struct HttpClient::State {
   mutable std::mutex mu;
   std::map<std::string, std::string> headers;
   std::vector<std::unique_ptr<Conn>> idle;
-  bool keepalive = true;
+  bool keepalive = !reference_timing();  // the reference-equivalent column dials per request
   size_t max_idle = 8;
   ProxyConfig proxy = ProxyConfig::from_env();
 };

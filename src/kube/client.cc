@@ -1,5 +1,7 @@
 #include "kube/client.h"
 
+#include "core/compat.h"
+
 #include <time.h>
 #include <unistd.h>
 
@@ -486,6 +488,17 @@ bool Client::wait_object(const std::string& object_path, int timeout_ms,
   size_t slash = object_path.rfind('/');
   std::string collection = object_path.substr(0, slash);
   std::string name = object_path.substr(slash + 1);
+  if (reference_timing()) {
+    // the reference polls readiness every 5 s (tiller / kaniko waits), the first check after
+    // one interval (wait.Poll semantics)
+    auto t0 = std::chrono::steady_clock::now();
+    while (true) {
+      auto el = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+      if (el + 5000 > timeout_ms) return pred(try_get(object_path));
+      sleep_ms(5000);
+      if (pred(try_get(object_path))) return true;
+    }
+  }
   return list_watch(collection, "fieldSelector=" + net::url_encode("metadata.name=" + name), timeout_ms,
                     [&](const std::vector<Value>& objs) {
                       for (auto& o : objs)
@@ -507,6 +520,7 @@ static const Value* newest_of(const std::vector<Value>& pods) {
 }
 
 Value Client::newest_running_pod(const std::string& ns, const std::string& sel, int max_wait_ms, int poll_ms) {
+  if (reference_timing()) poll_ms = std::max(poll_ms, 1000);
   auto timeout_error = [&] {
     return std::runtime_error("Waiting for pod with selector " + sel + " in namespace " + ns + " timed out");
   };

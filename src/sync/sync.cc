@@ -350,7 +350,7 @@ void Session::open_up_shell() {
   if (mode_ != Mode::Compat && !up_helper_) {
     // create the destination once instead of per upload, and check for `head` (the streamed
     // upload needs `head -c`; without it uploads use the reference's cat + stat protocol)
-    write_all(up_shell_->in(), "mkdir -p " + shell_quote(dest_) +
+    write_all(up_shell_->in(), "mkdir -p " + shell_quote(dest_) + " " + shell_quote(remote("/tmp")) +
                                    "; if command -v head >/dev/null 2>&1; then echo HAVEHEAD; fi; echo " + kDone + "\n");
     std::string before;
     wait_ack(up_out_, kDone, false, &before, 30000);
@@ -919,10 +919,12 @@ uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std
   };
   if (mode_ == Mode::Compat || !up_has_head_) {
     // the reference protocol (sync/upstream.go:387-411); compat archives are always gzip, the
-    // fast mode's cat/stat fallback may ship a small edit as plain tar
+    // fast mode's cat/stat fallback may ship a small edit as plain tar. Its fixed temp file
+    // lives in the container's /tmp (remote(): under the pod root for local-pod backends, whose
+    // pods share the host's /tmp).
     std::string cmd = "fileSize=" + size + R"(;
-					tmpFile="/tmp/devspace-upstream";
-					mkdir -p /tmp;
+					tmpFile=")" + remote("/tmp/devspace-upstream") + R"(";
+					mkdir -p )" + remote("/tmp") + R"(;
 					mkdir -p ')" + dest_ + R"(';
 
 					pid=$$;
@@ -942,7 +944,7 @@ uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std
 							sleep 0.1;
 					done;
 
-					tar )" + std::string(xflags) + R"( "$tmpFile" -C ')" + dest_ + R"(/.' 2>/tmp/devspace-upstream-error;
+					tar )" + std::string(xflags) + R"( "$tmpFile" -C ')" + dest_ + R"(/.' 2>)" + remote("/tmp/devspace-upstream-error") + R"(;
 					echo "DONE";
 		)";
     if (!write_all(fd, cmd)) throw SyncError("upstream: write failed");
@@ -955,7 +957,7 @@ uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std
   // dest is created once when the shell opens; `head -c N | tar x` streams (no temp file, no
   // polling in the container)
   std::string cmd = "echo " + std::string(kStart) + " && head -c " + size + " | tar " + xflags + " - -C " +
-                    shell_quote(dest_ + "/.") + " 2>/tmp/devspace-upstream-error; echo " + kDone + "\n";
+                    shell_quote(dest_ + "/.") + " 2>" + remote("/tmp/devspace-upstream-error") + "; echo " + kDone + "\n";
   if (!write_all(fd, cmd)) throw SyncError("upstream: write failed");
   wait_ack(up_out_, kStart, false, nullptr, o_.idle_timeout_ms);
   send_payload();
@@ -1416,9 +1418,9 @@ void Session::download_and_apply(const std::vector<FileInfo>& files) {
   for (auto& f : files) list += dest_ + f.name + "\n";
   if (mode_ == Mode::Compat) {
     std::string cmd = "fileSize=" + std::to_string(list.size()) + R"(;
-					tmpFileInput="/tmp/devspace-downstream-input";
-					tmpFileOutput="/tmp/devspace-downstream-output";
-					mkdir -p /tmp;
+					tmpFileInput=")" + remote("/tmp/devspace-downstream-input") + R"(";
+					tmpFileOutput=")" + remote("/tmp/devspace-downstream-output") + R"(";
+					mkdir -p )" + remote("/tmp") + R"(;
 
 					pid=$$;
 					cat </proc/$pid/fd/0 >"$tmpFileInput" &
@@ -1436,7 +1438,7 @@ void Session::download_and_apply(const std::vector<FileInfo>& files) {
 
 							sleep 0.1;
 					done;
-					tar -czf "$tmpFileOutput" -T "$tmpFileInput" 2>/tmp/devspace-downstream-error;
+					tar -czf "$tmpFileOutput" -T "$tmpFileInput" 2>)" + remote("/tmp/devspace-downstream-error") + R"(;
 					(>&2 echo "START");
 					(>&2 echo $(stat -c "%s" "$tmpFileOutput"));
 					(>&2 echo "DONE");
@@ -1470,8 +1472,9 @@ void Session::download_and_apply(const std::vector<FileInfo>& files) {
   bool gz = total <= (8ull << 20);
   std::vector<std::string> args;
   for (auto& f : files) args.push_back(shell_quote("." + f.name));
-  std::string cmd = std::string("echo DSSTART; tar -c") + (gz ? "z" : "") + "f - -C " + shell_quote(dest_) + " -- " +
-                    join(args, " ") + " 2>/tmp/devspace-downstream-error; echo; echo \"DSEND $?\"\n";
+  std::string cmd = "mkdir -p " + shell_quote(remote("/tmp")) + " 2>/dev/null; echo DSSTART; tar -c" +
+                    std::string(gz ? "z" : "") + "f - -C " + shell_quote(dest_) + " -- " +
+                    join(args, " ") + " 2>" + remote("/tmp/devspace-downstream-error") + "; echo; echo \"DSEND $?\"\n";
   if (!write_all(fd, cmd)) throw SyncError("downstream: write failed");
   while (read_line_idle(down_out_, idle, "downstream") != "DSSTART") {
   }

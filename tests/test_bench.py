@@ -18,42 +18,56 @@ def _run(args, timeout):
 
 
 def test_bench_cpu_tiny():
+    """The full contract on CPU: the headline is the quickstart loop (BASELINE configs[0], the
+    metric's named config) with its same-box reference-equivalent column; extras cover the
+    deploy (both columns), the GPU-pod loop and BASELINE configs[1-3] (both columns)."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--ref-steps",
-                        "1", "--qs-steps", "3", "--tiny"], capture_output=True, text=True, timeout=600, cwd=ROOT)
+                        "1", "--gpu-steps", "2", "--example-steps", "2", "--tiny"], capture_output=True, text=True,
+                       timeout=900, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    # the extras are best-effort inside bench.py (logged, not fatal): show why one is missing
-    assert "quickstart" in d and "tool_attributable" in d, r.stderr[-3000:]
-    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "config"):
-        assert k in d
-    assert d["higher_is_better"] is False
-    assert d["value"] > 0
-    # the config names what was measured: app, transport, builder fidelity
-    assert d["config"]["app"] == "examples/rocm-pytorch"
-    assert d["config"]["transport"].startswith("https + wss")
-    assert "RUN steps not executed" in d["config"]["builder"]
-    assert d["deploy"]["control_plane_only"] is True
-    assert d["deploy"]["net"]["tls_handshakes"] >= 1
-    assert d["reference_equivalent"]["p50_ms"] > d["value"]
-    # Node.js quickstart loop through sync + port-forward, and the sync-protocol comparison
-    assert d["quickstart"]["n"] == 3 and d["quickstart"]["reload_p50_ms"] > d["quickstart"]["sync_p50_ms"] > 0
-    assert d["tool_attributable"]["reference_protocol_sync_p50_ms"] > d["tool_attributable"]["sync_p50_ms"]
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["metric"].endswith("quickstart") and d["higher_is_better"] is False
+    assert d["value"] > 0 and d["steps"] == 3 and d["value"] == d["p50_ms"]
+    cfg = d["config"]
+    assert cfg["app"] == "examples/quickstart"
+    assert cfg["transport"].startswith("https + wss") and "RUN steps not executed" in cfg["builder"]
+    # same-box reference column of the headline (compat protocol + reference waits)
+    assert d["reference_equivalent"]["p50_ms"] > d["value"], r.stderr[-3000:]
+    assert d["reference_equivalent"]["sync_p50_ms"] > d["sync_p50_ms"]
+    dep = d["deploy"]
+    assert dep["control_plane_only"] is True and dep["net"]["tls_handshakes"] >= 1
+    # reference timing: no kept-alive connections, 5 s rollout polls
+    assert dep["reference_equivalent"]["wall_clock_s"] > dep["wall_clock_s"], dep
+    assert dep["reference_equivalent"]["net"]["reused"] == 0, dep
+    g = d["gpu_pod"]
+    assert g["n"] == 2 and g["reload_p50_ms"] > 0 and g["fused_ops"].startswith("eager (no GPU)"), g
+    assert g["reference_equivalent"]["p50_ms"] > g["reload_p50_ms"]
+    for key in ("php_mysql", "microservices", "kaniko"):
+        e = d[key]
+        assert "error" not in e, (key, e, r.stderr[-3000:])
+        assert e["n"] == 2 and e["edit_to_pod_p50_ms"] > 0 and e["deploy_cold_s"] > 0, (key, e)
+        assert e["reference_equivalent"]["edit_to_pod_p50_ms"] > e["edit_to_pod_p50_ms"], (key, e)
+    assert d["microservices"]["sync_paths"] == 2 and d["microservices"]["port_forwards"] == 2
 
 
 def test_bench_torchrun_two_ranks_cpu():
     """The driver's N>1 launch shape (torchrun, one rank per GPU) on CPU with gloo: rank 0
-    drives the dev loop, rank 1 joins the timing barriers; exactly one JSON line."""
+    drives the CLI, rank 1 joins the timing barriers; exactly one JSON line, and the GPU-pod
+    extra ran one training rank per bench rank."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", "29655", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
-           "--warmup", "1", "--tiny", "--ref-steps", "0", "--qs-steps", "0", "--no-deploy-bench"]
+           "--warmup", "1", "--tiny", "--ref-steps", "0", "--gpu-steps", "2", "--example-steps", "0",
+           "--no-deploy-bench"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["steps"] == 2 and d["value"] > 0
-    # the pod ran one training rank per bench rank (the runner's N-rank generation agreement)
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["n_gpus"] == 2 and d["gpu_pod"]["parallelism"] == "dp2", d
 
 
 @pytest.mark.gpu
