@@ -262,10 +262,15 @@ def make_app(store: ImageStore):
         dockerfile = q.get("dockerfile", "Dockerfile")
         buildargs = json.loads(q.get("buildargs", "{}") or "{}")
         target = q.get("target") or None
-        body = await request.read()
-        if body[:2] == b"\x1f\x8b":
-            body = gzip.decompress(body)
+        # the context streams in (chunked or sized) to a temp file, as dockerd spools it: a
+        # multi-GB context never sits in memory on either side
         ctx = tempfile.mkdtemp(prefix="lk-ctx-")
+        spool = tempfile.NamedTemporaryFile(prefix="lk-ctx-", suffix=".tar", delete=False)
+        try:
+            async for chunk in request.content.iter_chunked(1 << 20):
+                spool.write(chunk)
+        finally:
+            spool.close()
         resp = web.StreamResponse(headers={"Content-Type": "application/json"})
         await resp.prepare(request)
 
@@ -273,7 +278,7 @@ def make_app(store: ImageStore):
             await resp.write((json.dumps(obj) + "\r\n").encode())
 
         try:
-            with tarfile.open(fileobj=io.BytesIO(body)) as tf:
+            with tarfile.open(spool.name, "r:*") as tf:  # plain or gzip
                 tf.extractall(ctx, filter="fully_trusted") if hasattr(tarfile, "data_filter") else tf.extractall(ctx)
             logs = []
             image_id = build_image(store, ctx, dockerfile, tag, buildargs, target, log=logs.append)
@@ -286,6 +291,7 @@ def make_app(store: ImageStore):
             await emit({"errorDetail": {"message": str(e)}, "error": str(e)})
         finally:
             shutil.rmtree(ctx, ignore_errors=True)
+            os.unlink(spool.name)
         await resp.write_eof()
         return resp
 

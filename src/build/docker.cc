@@ -3,6 +3,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <regex>
 #include <cstdlib>
 #include <set>
@@ -442,6 +443,11 @@ class JsonMessageStream {
 
 std::string DockerClient::build(const std::string& context_tar, const BuildRequest& req,
                                 const std::function<void(const std::string&)>& out) {
+  return build_stream([&](const Sink& sink) { return sink(context_tar.data(), context_tar.size()); }, req, out);
+}
+
+std::string DockerClient::build_stream(const std::function<bool(const Sink&)>& write_context, const BuildRequest& req,
+                                       const std::function<void(const std::string&)>& out) {
   std::string q = "/build?t=" + net::url_encode(req.tag) + "&dockerfile=" + net::url_encode(req.dockerfile) + "&rm=1";
   if (!req.build_args.empty()) {
     Value ba = Value::map();
@@ -459,9 +465,21 @@ std::string DockerClient::build(const std::string& context_tar, const BuildReque
     for (auto& kv : req.auth_configs) ac[kv.first] = kv.second.to_json();
     r.headers.push_back({"X-Registry-Config", base64_encode(json_dump(ac), true)});
   }
-  r.body = context_tar;
   r.timeout_ms = 3600 * 1000;
-  out(strfmt("Sending build context to Docker daemon  %.2fkB\n", (double)context_tar.size() / 1000.0));
+  uint64_t sent = 0;
+  auto t0 = std::chrono::steady_clock::now(), last = t0;
+  r.body_writer = [&](const std::function<bool(const char*, size_t)>& to_daemon) {
+    return write_context([&](const char* d, size_t n) {
+      sent += n;
+      auto now = std::chrono::steady_clock::now();
+      if (now - last > std::chrono::seconds(5)) {  // big contexts: show that it moves
+        last = now;
+        out(strfmt("Sending build context to Docker daemon  %.2fMB\n", (double)sent / 1e6));
+      }
+      return to_daemon(d, n);
+    });
+  };
+  out("Sending build context to Docker daemon\n");
   std::string image_id, err;
   JsonMessageStream js([&](const Value& m) {
     if (!err.empty()) return;
@@ -480,6 +498,8 @@ std::string DockerClient::build(const std::string& context_tar, const BuildReque
     return true;
   });
   js.finish();
+  out(strfmt("Sent build context: %.2fkB in %.2fs\n", (double)sent / 1000.0,
+             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count()));
   if (resp.status != 200) {
     std::string msg = body;
     try {
@@ -569,7 +589,15 @@ static void walk_context(const std::string& root, const DockerIgnore& m,
 std::string context_tar(const std::string& context_dir, const std::vector<std::string>& excludes,
                         const std::string& rel_dockerfile, const std::optional<std::string>& dockerfile_override) {
   std::string out;
-  TarWriter tw(string_sink(&out));
+  write_context_tar(string_sink(&out), context_dir, excludes, rel_dockerfile, dockerfile_override);
+  return out;
+}
+
+bool write_context_tar(const Sink& out, const std::string& context_dir, const std::vector<std::string>& excludes,
+                       const std::string& rel_dockerfile, const std::optional<std::string>& dockerfile_override) {
+  bool ok = true;
+  Sink guarded = [&](const char* d, size_t n) { return ok = ok && out(d, n); };
+  TarWriter tw(guarded);
   DockerIgnore m(excludes);
   bool replaced = false;
   walk_context(context_dir, m, [&](const std::string& abs, const std::string& rel, const fs::StatInfo& st) {
@@ -610,7 +638,7 @@ std::string context_tar(const std::string& context_dir, const std::vector<std::s
     tw.add_file(e, *dockerfile_override);
   }
   tw.finish();
-  return out;
+  return ok;
 }
 
 std::vector<int> dockerfile_ports(const std::string& content) {

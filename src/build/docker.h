@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "core/net.h"
+#include "core/codec.h"
 #include "core/value.h"
 
 namespace ds {
@@ -104,6 +105,11 @@ class DockerClient {
   // daemon error message. Returns the image id when reported.
   std::string build(const std::string& context_tar, const BuildRequest& req,
                     const std::function<void(const std::string&)>& out);
+  // Same with a streamed context: `write_context` produces the tar into the sink while it is
+  // sent (chunked transfer encoding), so the context is never held in memory
+  // (builder/docker/docker.go:94-158 streams a tar reader the same way).
+  std::string build_stream(const std::function<bool(const Sink&)>& write_context, const BuildRequest& req,
+                           const std::function<void(const std::string&)>& out);
   // POST /images/{name}/push?tag=  (X-Registry-Auth: base64url(JSON)).
   void push(const std::string& image_with_tag, const AuthConfig& auth,
             const std::function<void(const std::string&)>& out);
@@ -133,6 +139,10 @@ std::vector<std::string> context_excludes(const std::string& context_dir, const 
 std::string context_tar(const std::string& context_dir, const std::vector<std::string>& excludes,
                         const std::string& rel_dockerfile = "",
                         const std::optional<std::string>& dockerfile_override = std::nullopt);
+// Streaming form: the tar goes to `out` while the context is walked. false when `out` failed.
+bool write_context_tar(const Sink& out, const std::string& context_dir, const std::vector<std::string>& excludes,
+                       const std::string& rel_dockerfile = "",
+                       const std::optional<std::string>& dockerfile_override = std::nullopt);
 
 // builder/util.go:43: Dockerfile content + ENTRYPOINT/CMD override (dev.overrideImages).
 std::string dockerfile_with_entrypoint(const std::string& dockerfile_content, const std::vector<std::string>& entrypoint);

@@ -174,7 +174,6 @@ class DockerBuilder : public Builder {
       rel = ".dockerfile." + hex_encode(random_string(10)).substr(0, 20);
       if (!override_df) override_df = fs::read_file(dockerfile);
     }
-    std::string tar = context_tar(ctx, excludes, rel, override_df);
     BuildRequest req;
     req.tag = url();
     req.dockerfile = rel;
@@ -185,7 +184,9 @@ class DockerBuilder : public Builder {
       req.auth_configs = DockerConfigFile::load().all();
     } catch (const std::exception&) {
     }
-    c_->build(tar, req, write_out);
+    // the context tar streams to the daemon while the tree is walked (bounded memory)
+    c_->build_stream([&](const Sink& sink) { return write_context_tar(sink, ctx, excludes, rel, override_df); }, req,
+                     write_out);
   }
 
   void push_image() override {

@@ -18,6 +18,7 @@
 
 #include "cli/common.h"
 #include "cloud/cloud.h"
+#include "core/codec.h"
 #include "core/fs.h"
 #include "core/log.h"
 #include "core/proc.h"
@@ -74,9 +75,23 @@ int compare_release(const std::string& a, const std::string& b) {
   return pa == pb ? 0 : (pa ? -1 : 1);
 }
 
+// `devspace version` output: "devspace version <v>" (what the reference prints) plus the
+// product id, which a self-update checks its candidate for.
+std::string version_line() { return std::string("devspace version ") + kVersion + " " + upgrade::kProductMarker; }
+
+// The version in a `devspace version` line ("" when it is not one).
+static std::string parse_version_line(const std::string& out) {
+  auto toks = split(trim(out), " ");
+  for (size_t i = 0; i + 1 < toks.size(); ++i)
+    if (toks[i] == "version") return toks[i + 1];
+  return "";
+}
+
 // Self-update (upgrade.go:69 Upgrade): from a local binary (--from), a plain mirror
-// (DEVSPACE_RELEASE_URL serving "<url>/latest" and "<url>/devspace-linux-amd64"), or by default
-// the newest GitHub release of devspace-cloud/devspace with a linux/amd64 asset.
+// (DEVSPACE_RELEASE_URL serving "<url>/latest", "<url>/devspace-linux-amd64" and its ".sha256"),
+// or the newest GitHub release of this product's release channel (DEVSPACE_RELEASE_REPO) with
+// a linux/amd64 asset. Every candidate must be this product; downloads must match a published
+// SHA-256.
 int run_upgrade(cli::Command& c, const Args&) {
   log::start_file_logging();
   std::string from = c.get_str("from");
@@ -86,11 +101,12 @@ int run_upgrade(cli::Command& c, const Args&) {
     if (!from.empty() || !url.empty()) {
       std::string newest;
       if (!from.empty()) {
+        std::string data;
+        if (!fs::read_file(from, &data) || !upgrade::is_this_product(data))
+          throw std::runtime_error(from + " is not a " + std::string(upgrade::kProductId) + " binary");
         RunResult r = run({from, "version"}, "", {}, 20000);
-        if (r.code != 0) throw std::runtime_error(from + " is not a devspace binary");
-        newest = trim(r.out);
-        auto sp = newest.rfind(' ');
-        if (sp != std::string::npos) newest = newest.substr(sp + 1);
+        newest = parse_version_line(r.out);
+        if (r.code != 0 || newest.empty()) throw std::runtime_error(from + " is not a devspace binary");
       } else {
         newest = trim(helmrepo::fetch(trim_right(url, "/") + "/latest"));
       }
@@ -100,15 +116,27 @@ int run_upgrade(cli::Command& c, const Args&) {
       }
       log::info("Downloading newest version...");
       std::string staged = exe + ".new";
-      if (!from.empty())
+      if (!from.empty()) {
         fs::copy(from, staged, true);
-      else
-        fs::write_file(staged, helmrepo::fetch(trim_right(url, "/") + "/devspace-linux-amd64"), 0755);
+      } else {
+        std::string base = trim_right(url, "/");
+        std::string bin = helmrepo::fetch(base + "/devspace-linux-amd64");
+        std::string want = upgrade::published_sha256(helmrepo::fetch(base + "/devspace-linux-amd64.sha256"),
+                                                     "devspace-linux-amd64");
+        if (want.empty() || sha256_hex(bin) != want)
+          throw std::runtime_error("devspace-linux-amd64 does not match its published SHA-256");
+        if (!upgrade::is_this_product(bin))
+          throw std::runtime_error("the mirror's binary is not a " + std::string(upgrade::kProductId) + " build");
+        fs::write_file(staged, bin, 0755);
+      }
       chmod(staged.c_str(), 0755);
       if (!fs::rename(staged, exe)) throw std::runtime_error("cannot replace " + exe);
       log::info("Successfully updated to version " + newest);
       return 0;
     }
+    if (upgrade::release_repo().empty())
+      throw std::runtime_error("this build has no release channel: set DEVSPACE_RELEASE_REPO=owner/repo (GitHub "
+                               "releases of this product), DEVSPACE_RELEASE_URL=<mirror>, or use --from <binary>");
     auto latest = upgrade::detect_latest();
     if (!latest || upgrade::compare_versions(latest->version, kVersion) <= 0) {
       log::info(std::string("Current binary is the latest version: ") + kVersion);
@@ -152,6 +180,7 @@ int run_upgrade_check(cli::Command&, const Args&) {
 // DEVSPACE_NONINTERACTIVE / DEVSPACE_SKIP_UPDATE_CHECK, never for -alpha/-beta builds.
 void notify_newer_version(const std::vector<std::string>& args) {
   if (getenv("DEVSPACE_SKIP_UPDATE_CHECK") || getenv("DEVSPACE_NONINTERACTIVE")) return;
+  if (upgrade::release_repo().empty()) return;  // no release channel of this product configured
   if (!isatty(0) || !isatty(1)) return;
   if (contains(kVersion, "-alpha") || contains(kVersion, "-beta")) return;
   if (!args.empty() && (args[0] == "upgrade" || args[0] == "upgrade-check")) return;
@@ -341,7 +370,7 @@ void register_misc(cli::Command& root) {
     auto c = std::make_unique<cli::Command>("version", "Prints the devspace version");
     c->max_args = 0;
     c->run = [](cli::Command&, const Args&) {
-      log::get().write(std::string("devspace version ") + kVersion + "\n");
+      log::get().write(version_line() + "\n");
       return 0;
     };
     root.add(std::move(c));

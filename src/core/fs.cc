@@ -3,7 +3,6 @@
 #include <dirent.h>
 #include <fcntl.h>
 #include <limits.h>
-#include <pwd.h>
 #include <stdlib.h>
 #include <sys/time.h>
 #include <unistd.h>
@@ -240,8 +239,25 @@ bool chdir(const std::string& path) { return ::chdir(path.c_str()) == 0; }
 std::string home_dir() {
   const char* h = getenv("HOME");
   if (h && *h) return h;
-  struct passwd* pw = getpwuid(getuid());
-  if (pw && pw->pw_dir) return pw->pw_dir;
+  // /etc/passwd directly instead of getpwuid (NSS is unavailable to the static binary)
+  std::string pw;
+  if (read_file("/etc/passwd", &pw)) {
+    std::string uid = std::to_string(getuid());
+    size_t pos = 0;
+    while (pos < pw.size()) {
+      size_t nl = pw.find('\n', pos);
+      std::string line = pw.substr(pos, nl == std::string::npos ? std::string::npos : nl - pos);
+      pos = nl == std::string::npos ? pw.size() : nl + 1;
+      std::vector<std::string> f;
+      size_t a = 0, b;
+      while ((b = line.find(':', a)) != std::string::npos) {
+        f.push_back(line.substr(a, b - a));
+        a = b + 1;
+      }
+      f.push_back(line.substr(a));
+      if (f.size() >= 6 && f[2] == uid && !f[5].empty()) return f[5];
+    }
+  }
   return "/";
 }
 

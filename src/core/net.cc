@@ -1,6 +1,7 @@
 #include "core/net.h"
 
 #include "core/compat.h"
+#include "core/resolve.h"
 
 #include <arpa/inet.h>
 #include <fcntl.h>
@@ -20,6 +21,7 @@
 
 #include <chrono>
 #include <climits>
+#include <cstdio>
 #include <cstring>
 
 #include "core/codec.h"
@@ -353,24 +355,37 @@ class TlsConn : public Conn {
   std::atomic<bool> shut_{false};
 };
 
-// TCP connect with timeout; returns a blocking fd with TCP_NODELAY.
+// TCP connect with timeout; returns a blocking fd with TCP_NODELAY. Names resolve through
+// core/resolve (no NSS: the release binary is static); getaddrinfo is the last resort.
 int dial_fd(const std::string& host, int port, int timeout_ms) {
-  struct addrinfo hints{};
-  hints.ai_family = AF_UNSPEC;
-  hints.ai_socktype = SOCK_STREAM;
-  struct addrinfo* res = nullptr;
-  std::string h = host;
-  if (h.size() > 2 && h.front() == '[' && h.back() == ']') h = h.substr(1, h.size() - 2);
-  int rc = getaddrinfo(h.c_str(), std::to_string(port).c_str(), &hints, &res);
-  if (rc != 0) throw NetError("dial tcp " + host + ":" + std::to_string(port) + ": " + gai_strerror(rc));
+  std::string rerr;
+  std::vector<Address> addrs = resolve(host, port, &rerr);
+  if (addrs.empty()) {
+    struct addrinfo hints{};
+    hints.ai_family = AF_UNSPEC;
+    hints.ai_socktype = SOCK_STREAM;
+    struct addrinfo* res = nullptr;
+    std::string h = host;
+    if (h.size() > 2 && h.front() == '[' && h.back() == ']') h = h.substr(1, h.size() - 2);
+    int rc = getaddrinfo(h.c_str(), std::to_string(port).c_str(), &hints, &res);
+    if (rc != 0) throw NetError("dial tcp " + host + ":" + std::to_string(port) + ": lookup " + h + ": " + rerr);
+    for (auto* ai = res; ai; ai = ai->ai_next) {
+      Address a;
+      a.family = ai->ai_family;
+      std::memcpy(&a.addr, ai->ai_addr, ai->ai_addrlen);
+      a.len = ai->ai_addrlen;
+      addrs.push_back(a);
+    }
+    freeaddrinfo(res);
+  }
   int fd = -1;
   std::string last_err = "no addresses";
-  for (auto* ai = res; ai; ai = ai->ai_next) {
-    fd = ::socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC, ai->ai_protocol);
+  for (auto& a : addrs) {
+    fd = ::socket(a.family, SOCK_STREAM | SOCK_CLOEXEC, 0);
     if (fd < 0) continue;
     int fl = fcntl(fd, F_GETFL);
     fcntl(fd, F_SETFL, fl | O_NONBLOCK);
-    int r = ::connect(fd, ai->ai_addr, ai->ai_addrlen);
+    int r = ::connect(fd, (struct sockaddr*)&a.addr, a.len);
     if (r != 0 && errno == EINPROGRESS) {
       if (wait_fd(fd, POLLOUT, timeout_ms) > 0) {
         int err = 0;
@@ -393,7 +408,6 @@ int dial_fd(const std::string& host, int port, int timeout_ms) {
     ::close(fd);
     fd = -1;
   }
-  freeaddrinfo(res);
   if (fd < 0) throw NetError("dial tcp " + host + ":" + std::to_string(port) + ": " + last_err);
   stats().tcp_dials++;
   return fd;
@@ -688,13 +702,14 @@ void HttpClient::put_conn(std::unique_ptr<Conn> c) {
 
 namespace {
 
-bool read_head(Conn& c, Response* r, std::string* rest, int timeout_ms, bool* got_any) {
+bool read_head(Conn& c, Response* r, std::string* rest, int timeout_ms, bool* got_any, bool* timed_out = nullptr) {
   std::string buf = *rest;
   rest->clear();
   size_t end;
   while ((end = buf.find("\r\n\r\n")) == std::string::npos) {
     char tmp[8192];
     ssize_t n = c.read(tmp, sizeof(tmp), timeout_ms);
+    if (n == -2 && timed_out) *timed_out = true;
     if (n <= 0) return false;
     if (got_any) *got_any = true;
     buf.append(tmp, (size_t)n);
@@ -736,8 +751,12 @@ std::string build_request(const Url& url, const std::map<std::string, std::strin
   std::map<std::string, std::string> hdrs = defaults;
   for (auto& kv : r.headers) hdrs[kv.first] = kv.second;
   for (auto& kv : hdrs) out += kv.first + ": " + kv.second + "\r\n";
-  if (!hdrs.count("Content-Length") && (!r.body.empty() || r.method == "POST" || r.method == "PUT" || r.method == "PATCH"))
+  if (r.body_writer) {
+    if (!hdrs.count("Transfer-Encoding")) out += "Transfer-Encoding: chunked\r\n";
+  } else if (!hdrs.count("Content-Length") &&
+             (!r.body.empty() || r.method == "POST" || r.method == "PUT" || r.method == "PATCH")) {
     out += "Content-Length: " + std::to_string(r.body.size()) + "\r\n";
+  }
   if (!hdrs.count("Connection") && !keepalive) out += "Connection: close\r\n";
   out += "\r\n";
   return out;
@@ -762,18 +781,36 @@ Response HttpClient::stream(Request r, const std::function<bool(const std::strin
   std::unique_ptr<Conn> c;
   Response resp;
   std::string rest;
+  const bool idempotent = r.method == "GET" || r.method == "HEAD" || r.method == "PUT" || r.method == "DELETE" ||
+                          r.method == "OPTIONS";
   for (int attempt = 0;; ++attempt) {
     bool reused = false;
     c = take_conn(&reused);
-    bool wrote = c->write_all(head) && (r.body.empty() || c->write_all(r.body));
-    bool got_any = false;
+    bool wrote = c->write_all(head);
+    if (wrote && r.body_writer) {
+      // chunked transfer encoding: the body is produced while it is sent (bounded memory)
+      Conn* cp = c.get();
+      char hex[32];
+      wrote = r.body_writer([&](const char* d, size_t n) {
+        if (n == 0) return true;
+        int k = std::snprintf(hex, sizeof(hex), "%zx\r\n", n);
+        return cp->write_all(std::string(hex, (size_t)k)) && cp->write_all(std::string(d, n)) && cp->write_all("\r\n");
+      }) && c->write_all("0\r\n\r\n");
+    } else if (wrote && !r.body.empty()) {
+      wrote = c->write_all(r.body);
+    }
+    bool got_any = false, timed_out = false;
     resp = Response();
     rest.clear();
-    if (wrote && read_head(*c, &resp, &rest, r.timeout_ms, &got_any)) break;
-    // a pooled connection the server closed while idle: retry once on a fresh one
-    if (reused && !got_any && attempt == 0) continue;
+    if (wrote && read_head(*c, &resp, &rest, r.timeout_ms, &got_any, &timed_out)) break;
+    // A pooled connection the server closed while it sat idle: retry once on a fresh one —
+    // only when the connection was found dead (EOF / reset, never a timeout: a slow server
+    // would get the request twice) and the request is safe to repeat or never went out.
+    // Streamed bodies cannot be replayed.
+    if (reused && !got_any && !timed_out && attempt == 0 && !r.body_writer && (idempotent || !wrote)) continue;
     if (!wrote) throw NetError("write request failed: " + r.method + " " + r.path);
-    throw NetError("read response failed: " + r.path);
+    throw NetError(timed_out ? "timeout waiting for the response: " + r.method + " " + r.path
+                             : "read response failed: " + r.path);
   }
   bool reusable = keepalive && resp.version == "HTTP/1.1" &&
                   to_lower(resp.header("connection")).find("close") == std::string::npos;

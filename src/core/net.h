@@ -96,6 +96,9 @@ struct Request {
   std::string path = "/";
   std::vector<std::pair<std::string, std::string>> headers;
   std::string body;
+  // Streamed body (instead of `body`): called once with a sink that sends what it is given as
+  // chunked transfer encoding; returns false to abort the request. Never retried.
+  std::function<bool(const std::function<bool(const char*, size_t)>&)> body_writer;
   int timeout_ms = 60000;
   // stream(): for status >= 400 collect the body into Response::body instead of on_data
   bool errors_to_body = false;

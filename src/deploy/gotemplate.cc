@@ -1,5 +1,7 @@
 #include "deploy/gotemplate.h"
 
+#include "core/resolve.h"
+
 #include <arpa/inet.h>
 #include <netdb.h>
 
@@ -1994,17 +1996,8 @@ struct Engine::Impl {
     }
     if (fn == "getHostByName") {
       need(1);
-      struct addrinfo hints{}, *res = nullptr;
-      hints.ai_family = AF_UNSPEC;
-      std::string ip;
-      if (::getaddrinfo(strval(args[0]).c_str(), nullptr, &hints, &res) == 0 && res) {
-        char buf[INET6_ADDRSTRLEN] = {0};
-        void* a = res->ai_family == AF_INET ? (void*)&((struct sockaddr_in*)res->ai_addr)->sin_addr
-                                             : (void*)&((struct sockaddr_in6*)res->ai_addr)->sin6_addr;
-        if (::inet_ntop(res->ai_family, a, buf, sizeof(buf))) ip = buf;
-        ::freeaddrinfo(res);
-      }
-      return S(ip);
+      auto addrs = net::resolve(strval(args[0]), 0);
+      return S(addrs.empty() ? "" : addrs[0].text);
     }
     // mustX is X that returns its error instead of panicking; errors already throw here
     if (starts_with(fn, "must") && fn.size() > 4 && std::isupper((unsigned char)fn[4])) {

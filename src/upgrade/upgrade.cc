@@ -16,7 +16,44 @@
 namespace ds {
 namespace upgrade {
 
-const char* const kGithubSlug = "devspace-cloud/devspace";
+const char* const kProductId = "devspace-mi355x";
+const char* const kProductMarker = "(devspace-mi355x)";  // a literal: present in the binary as is
+
+#ifndef DEVSPACE_RELEASE_REPO
+#define DEVSPACE_RELEASE_REPO ""
+#endif
+
+std::string release_repo() {
+  const char* e = getenv("DEVSPACE_RELEASE_REPO");
+  return e && *e ? e : DEVSPACE_RELEASE_REPO;
+}
+
+bool is_this_product(const std::string& binary) {
+  // the marker as the binary stores it (and a release script would print it)
+  return binary.find(kProductMarker) != std::string::npos;
+}
+
+std::string published_sha256(const std::string& file, const std::string& asset) {
+  static const std::regex hex("^[0-9a-fA-F]{64}$");
+  std::string lone;
+  int lines = 0;
+  for (auto& raw : split(file, "\n")) {
+    std::string line = trim(raw);
+    if (line.empty()) continue;
+    ++lines;
+    size_t sp = line.find_first_of(" \t");
+    std::string digest = line.substr(0, sp);
+    if (!std::regex_match(digest, hex)) continue;
+    if (sp == std::string::npos) {
+      lone = digest;
+      continue;
+    }
+    std::string name = trim(line.substr(sp));
+    if (!name.empty() && name[0] == '*') name = name.substr(1);  // sha256sum binary mode
+    if (name == asset || fs::basename(name) == asset) return to_lower(digest);
+  }
+  return lines == 1 ? to_lower(lone) : "";
+}
 
 std::string erase_version_prefix(const std::string& version) {
   static const std::regex re(R"(\d+\.\d+\.\d+)");
@@ -97,6 +134,7 @@ bool has_suffix_match(const std::string& name) {
 }  // namespace
 
 std::optional<Release> detect_latest(const std::string& slug) {
+  if (slug.empty()) throw std::runtime_error("no release channel configured (set DEVSPACE_RELEASE_REPO=owner/repo)");
   Value rels = json_parse(http_get(api_base() + "/repos/" + slug + "/releases?per_page=100",
                                    "application/vnd.github+json"));
   std::optional<Release> best;
@@ -120,6 +158,14 @@ std::optional<Release> detect_latest(const std::string& slug) {
         r.notes = rel.get("body").as_string();
         r.asset_name = name;
         r.asset_url = a.get("browser_download_url").as_string();
+        for (auto& c : rel.get("assets").items()) {
+          std::string cn = c.get("name").as_string();
+          if (cn == name + ".sha256" || (r.checksum_name.empty() && (ends_with(cn, "checksums.txt") ||
+                                                                    cn == "SHA256SUMS" || cn == "sha256sums.txt"))) {
+            r.checksum_name = cn;
+            r.checksum_url = c.get("browser_download_url").as_string();
+          }
+        }
         best = r;
       }
       break;
@@ -129,6 +175,7 @@ std::optional<Release> detect_latest(const std::string& slug) {
 }
 
 std::string check_for_newer_version(const std::string& current) {
+  if (release_repo().empty()) return "";
   auto latest = detect_latest();
   if (!latest || compare_versions(latest->version, current) <= 0) return "";
   return latest->version;
@@ -154,9 +201,21 @@ std::string extract_binary(const std::string& asset_name, const std::string& dat
 }
 
 void install_release(const Release& r, const std::string& exe) {
-  std::string bin = extract_binary(r.asset_name, http_get(r.asset_url, "application/octet-stream"));
+  if (r.checksum_url.empty())
+    throw std::runtime_error("release " + r.tag + " publishes no SHA-256 for " + r.asset_name +
+                             " (<asset>.sha256 or checksums.txt): refusing an unverifiable binary");
+  std::string want = published_sha256(http_get(r.checksum_url, "application/octet-stream"), r.asset_name);
+  if (want.empty()) throw std::runtime_error(r.checksum_name + " has no SHA-256 for " + r.asset_name);
+  std::string asset = http_get(r.asset_url, "application/octet-stream");
+  std::string got = sha256_hex(asset);
+  if (got != want)
+    throw std::runtime_error("checksum mismatch for " + r.asset_name + ": got " + got + ", published " + want);
+  std::string bin = extract_binary(r.asset_name, asset);
   if (bin.size() < 4 || bin.compare(0, 4, "\x7f" "ELF") != 0)
     throw std::runtime_error("downloaded asset " + r.asset_name + " is not an executable");
+  if (!is_this_product(bin))
+    throw std::runtime_error("release " + r.tag + " is not a " + std::string(kProductId) + " build (e.g. an upstream "
+                             "devspace binary): refusing to replace this one with it");
   // go-github-selfupdate's update.Apply: new file next to the target, old one kept until the
   // swap succeeded, then removed
   std::string staged = exe + ".new", old = exe + ".old";

@@ -201,11 +201,19 @@ def test_upgrade_from_local_release(tmp_path):
     os.makedirs(home)
     exe = tmp_path / "devspace"
     shutil.copy2(BIN, exe)
-    ver = subprocess.run([str(exe), "version"], capture_output=True, text=True).stdout.strip().split()[-1]
-    # a "newer release": a script that reports a higher version
+    ver = subprocess.run([str(exe), "version"], capture_output=True, text=True).stdout.split()
+    assert ver[:2] == ["devspace", "version"] and ver[-1] == "(devspace-mi355x)", ver
+    # a "newer release": a script that reports a higher version of this product
     newer = tmp_path / "devspace-next"
-    newer.write_text("#!/bin/sh\necho 'devspace version v99.0.0'\n")
+    newer.write_text("#!/bin/sh\necho 'devspace version v99.0.0 (devspace-mi355x)'\n")
     newer.chmod(0o755)
+    # another product's binary (an upstream devspace) is refused whatever its version
+    upstream = tmp_path / "devspace-upstream"
+    upstream.write_text("#!/bin/sh\necho 'devspace version v5.18.5'\n")
+    upstream.chmod(0o755)
+    p = subprocess.run([str(exe), "upgrade", "--from", str(upstream)], capture_output=True, text=True,
+                       env=dict(os.environ, HOME=home), timeout=60, cwd=tmp_path)
+    assert p.returncode != 0 and "is not a devspace-mi355x binary" in p.stdout + p.stderr, p.stdout + p.stderr
     same = subprocess.run([str(exe), "upgrade", "--from", str(exe)], capture_output=True, text=True,
                           env=dict(os.environ, HOME=home), timeout=60, cwd=tmp_path)
     assert same.returncode == 0 and "latest version" in same.stdout + same.stderr, same.stdout + same.stderr
@@ -215,9 +223,14 @@ def test_upgrade_from_local_release(tmp_path):
     assert "Successfully updated to version v99.0.0" in p.stdout + p.stderr
     assert "v99.0.0" in subprocess.run([str(exe)], capture_output=True, text=True).stdout
     assert ver
+    # no release channel configured: never the upstream repository, a clear error instead
+    clean = {k: v for k, v in os.environ.items() if k not in ("DEVSPACE_RELEASE_URL", "DEVSPACE_RELEASE_REPO")}
+    no_ch = subprocess.run([BIN, "upgrade"], capture_output=True, text=True, env={**clean, "HOME": home},
+                           timeout=60, cwd=tmp_path)
+    assert no_ch.returncode != 0 and "no release channel" in no_ch.stdout + no_ch.stderr, no_ch.stdout + no_ch.stderr
     # no reachable release server: a clear error, not a hang
     no_src = subprocess.run([BIN, "upgrade"], capture_output=True, text=True,
-                            env={**{k: v for k, v in os.environ.items() if k != "DEVSPACE_RELEASE_URL"}, "HOME": home,
+                            env={**clean, "HOME": home, "DEVSPACE_RELEASE_REPO": "acme/devspace-mi355x",
                                  "DEVSPACE_GITHUB_API": "http://127.0.0.1:9"},
                             timeout=60, cwd=tmp_path)
     assert no_src.returncode != 0 and "Couldn't upgrade" in no_src.stdout + no_src.stderr
@@ -239,7 +252,7 @@ class _FakeGithub:
 
             def do_GET(self):
                 outer.hits.append((self.path, self.headers.get("User-Agent"), self.headers.get("Authorization")))
-                if self.path.startswith("/repos/devspace-cloud/devspace/releases"):
+                if self.path.startswith("/repos/acme/devspace-mi355x/releases"):
                     body = json.dumps(outer.releases).encode()
                     self.send_response(200)
                     self.send_header("Content-Type", "application/json")
@@ -273,8 +286,11 @@ def _release(tag, assets, base, draft=False, prerelease=False):
 
 
 def test_upgrade_from_github_releases(tmp_path):
-    """Default `upgrade`: newest non-draft, non-prerelease release with a linux/amd64 asset
-    (go-github-selfupdate rules), tarball extracted, running binary swapped atomically."""
+    """`upgrade` from this product's release channel: newest non-draft, non-prerelease release
+    with a linux/amd64 asset (go-github-selfupdate rules) whose SHA-256 matches the published
+    checksums, tarball extracted, running binary swapped atomically; an upstream devspace
+    binary, a checksum mismatch or a release without checksums are refused."""
+    import hashlib
     import io
     import tarfile
 
@@ -288,7 +304,9 @@ def test_upgrade_from_github_releases(tmp_path):
         ti = tarfile.TarInfo("devspace-v2.5.0/devspace")
         ti.size, ti.mode = len(new_bin), 0o755
         tf.addfile(ti, io.BytesIO(new_bin))
-    gh = _FakeGithub([], {"devspace_linux_amd64.tar.gz": tgz.getvalue(), "devspace-darwin-amd64": b"x"})
+    sums = hashlib.sha256(tgz.getvalue()).hexdigest() + "  devspace_linux_amd64.tar.gz\n"
+    gh = _FakeGithub([], {"devspace_linux_amd64.tar.gz": tgz.getvalue(), "devspace-darwin-amd64": b"x",
+                          "checksums.txt": sums.encode()})
     gh.releases = [
         _release("v9.0.0-rc1", ["devspace-linux-amd64"], gh.url, prerelease=True),  # prerelease: skipped
         _release("v8.0.0", ["devspace-linux-amd64"], gh.url, draft=True),  # draft: skipped
@@ -297,7 +315,8 @@ def test_upgrade_from_github_releases(tmp_path):
         _release("v1.0.0", ["devspace-linux-amd64"], gh.url),
         _release("nightly", ["devspace-linux-amd64"], gh.url),  # not semver
     ]
-    env = {**os.environ, "HOME": home, "DEVSPACE_GITHUB_API": gh.url, "GITHUB_TOKEN": "t0k"}
+    env = {**os.environ, "HOME": home, "DEVSPACE_GITHUB_API": gh.url, "GITHUB_TOKEN": "t0k",
+           "DEVSPACE_RELEASE_REPO": "acme/devspace-mi355x"}
     env.pop("DEVSPACE_RELEASE_URL", None)
     try:
         p = subprocess.run([str(exe), "upgrade"], capture_output=True, text=True, env=env, timeout=60, cwd=tmp_path)
@@ -315,12 +334,34 @@ def test_upgrade_from_github_releases(tmp_path):
         p = subprocess.run([str(exe), "upgrade"], capture_output=True, text=True, env=env, timeout=60, cwd=tmp_path)
         assert p.returncode == 0 and "latest version" in p.stdout + p.stderr
         assert not any(h[0].startswith("/dl/") for h in gh.hits[n:])
+        def offer(tag, data, checksum):
+            gh.files["devspace-linux-amd64"] = data
+            assets = ["devspace-linux-amd64"]
+            if checksum is not None:
+                gh.files["devspace-linux-amd64.sha256"] = checksum.encode()
+                assets.append("devspace-linux-amd64.sha256")
+            gh.releases = [_release(tag, assets, gh.url)]
+            return subprocess.run([str(exe), "upgrade"], capture_output=True, text=True, env=env, timeout=60,
+                                  cwd=tmp_path)
+
         # a non-executable asset is refused and the binary is left in place
-        gh.releases = [_release("v7.0.0", ["devspace-linux-amd64"], gh.url)]
-        gh.files["devspace-linux-amd64"] = b"<html>oops</html>"
-        p = subprocess.run([str(exe), "upgrade"], capture_output=True, text=True, env=env, timeout=60, cwd=tmp_path)
-        assert p.returncode != 0 and "not an executable" in p.stdout + p.stderr
+        bad = b"<html>oops</html>"
+        p = offer("v7.0.0", bad, hashlib.sha256(bad).hexdigest())
+        assert p.returncode != 0 and "not an executable" in p.stdout + p.stderr, p.stdout + p.stderr
+        # an upstream devspace release (an ELF without this product's id) is refused
+        upstream = b"\x7fELF" + b"\0" * 4096 + b"devspace version v6.3.2"
+        p = offer("v7.1.0", upstream, hashlib.sha256(upstream).hexdigest())
+        assert p.returncode != 0 and "is not a devspace-mi355x build" in p.stdout + p.stderr, p.stdout + p.stderr
+        # a checksum mismatch, and a release without any checksum, are refused
+        good = open(BIN, "rb").read() + b"\n# release v7.2.0\n"
+        p = offer("v7.2.0", good, "0" * 64)
+        assert p.returncode != 0 and "checksum mismatch" in p.stdout + p.stderr, p.stdout + p.stderr
+        p = offer("v7.3.0", good, None)
+        assert p.returncode != 0 and "publishes no SHA-256" in p.stdout + p.stderr, p.stdout + p.stderr
         assert open(exe, "rb").read() == new_bin
+        # and a verified one goes in (a lone digest in <asset>.sha256)
+        p = offer("v7.4.0", good, hashlib.sha256(good).hexdigest() + "\n")
+        assert p.returncode == 0 and open(exe, "rb").read() == good, p.stdout + p.stderr
     finally:
         gh.close()
 
@@ -336,7 +377,7 @@ def test_newer_version_notice_from_daily_cache(tmp_path):
     gh = _FakeGithub([], {})
     gh.releases = [_release("v42.0.0", ["devspace-linux-amd64"], gh.url)]
     env = {k: v for k, v in os.environ.items() if k not in ("DEVSPACE_NONINTERACTIVE", "DEVSPACE_SKIP_UPDATE_CHECK")}
-    env.update(HOME=str(home), DEVSPACE_GITHUB_API=gh.url)
+    env.update(HOME=str(home), DEVSPACE_GITHUB_API=gh.url, DEVSPACE_RELEASE_REPO="acme/devspace-mi355x")
 
     def run_tty():
         master, slave = pty.openpty()

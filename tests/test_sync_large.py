@@ -16,6 +16,7 @@ Timings and peaks go to $SYNC_LARGE_OUT when set (profiles/r3_sync_large.json)."
 import hashlib
 import json
 import os
+import re
 import shutil
 import signal
 import subprocess
@@ -257,3 +258,45 @@ def test_helper_frame_lengths_are_64_bit():
         assert len(h) == 9 and h[0:1] == b"U"
         assert int.from_bytes(h[1:], "big") == n
         assert _native.frame_parse(h) == ("U", n)
+
+
+def test_multi_gb_build_context_streams_to_the_daemon(payloads, tmp_path):
+    """`devspace deploy` of a project whose Docker build context holds a > 2 GiB file (VERDICT r2
+    #5): the context tar streams to the Docker Engine API as a chunked POST /build body while the
+    tree is walked (the reference streams a tar reader, builder/docker/docker.go:94-158), so the
+    CLI's peak RSS stays under 64 MiB; the daemon receives every byte."""
+    from conftest import DevspaceEnv
+    from devspace_amd.localkube import LocalCluster
+
+    cluster = LocalCluster(str(tmp_path / "state"), gpus=0).start()
+    try:
+        lk = DevspaceEnv(cluster, str(tmp_path))
+        proj = lk.project("quickstart", "qs-bigctx")
+        up_path, up_sha = payloads["up"]
+        os.link(up_path, os.path.join(proj, "weights.bin"))
+        # the chart's pod would copy the image rootfs (2 GiB more disk): the build is the point
+        cfg = os.path.join(proj, ".devspace", "config.yaml")
+        text = open(cfg).read().replace("chartPath: ./chart", "chartPath: ./chart\n    wait: false")
+        with open(cfg, "w") as f:
+            f.write(text)
+        p = subprocess.Popen([lk.bin, "deploy"], cwd=proj, env=lk.env, stdout=subprocess.PIPE,
+                             stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, text=True)
+        mon = PeakRss(p.pid)
+        out, _ = p.communicate(timeout=900)
+        peaks = mon.stop()
+        assert p.returncode == 0, out[-3000:]
+        assert "Sending build context to Docker daemon" in out and "Sent build context" in out, out[-3000:]
+        sent_kb = float(re.search(r"Sent build context: ([\d.]+)kB", out).group(1))
+        assert sent_kb * 1000 > SIZE, out[-2000:]
+        # the image the daemon built holds the whole file, byte for byte
+        img_root = None
+        for d, _, files in os.walk(str(tmp_path / "state")):
+            if "weights.bin" in files and os.path.getsize(os.path.join(d, "weights.bin")) == SIZE:
+                img_root = d
+                break
+        assert img_root, "weights.bin not in any image rootfs"
+        assert _sha(os.path.join(img_root, "weights.bin")) == up_sha
+        _record("docker_build_context", {"bytes": SIZE, "devspace_peak_rss_MiB": round(peaks["devspace"] / 2**20, 1)})
+        assert peaks["devspace"] < RSS_CAP, peaks
+    finally:
+        cluster.stop()
