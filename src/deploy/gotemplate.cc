@@ -1018,6 +1018,13 @@ struct Engine::Impl {
   // Generated sizes (until/untilStep/seq elements, repeat output) are bounded: a chart typo
   // such as `until 1000000000` must fail the render, not take the host's memory.
   static constexpr int64_t kMaxGenerated = 10000000;
+  // |b - a| / |step| without overflow (a span beyond int64 is over any limit anyway)
+  static int64_t span_count(int64_t a, int64_t b, int64_t st, const char* fn) {
+    int64_t d;
+    if (__builtin_sub_overflow(b, a, &d) || (st == -1 && d == INT64_MIN))
+      throw TemplateError(std::string(fn) + ": the range exceeds the limit of " + std::to_string(kMaxGenerated));
+    return d / st;
+  }
   static void check_generated(int64_t n, const char* fn) {
     if (n > kMaxGenerated)
       throw TemplateError(std::string(fn) + ": " + std::to_string(n) + " elements exceed the limit of " +
@@ -1302,7 +1309,10 @@ struct Engine::Impl {
       need(2);
       std::string o, unit = strval(args[1]);
       int64_t n = args[0].as_int();
-      check_generated(n * (int64_t)std::max<size_t>(1, unit.size()), "repeat");
+      // n * size can overflow int64: compare by division instead
+      if (n > 0 && (n > kMaxGenerated || (int64_t)unit.size() > kMaxGenerated / n))
+        throw TemplateError("repeat: " + std::to_string(n) + " x " + std::to_string(unit.size()) +
+                            " bytes exceeds the limit of " + std::to_string(kMaxGenerated));
       for (int64_t i = 0; i < n; ++i) o += unit;
       return S(o);
     }
@@ -1705,8 +1715,11 @@ struct Engine::Impl {
       Value l = Value::seq();
       int64_t a = args[0].as_int(), b = args[1].as_int(), st = args[2].as_int();
       if (st == 0) return l;
-      check_generated((b - a) / st, "untilStep");
-      for (int64_t i = a; st > 0 ? i < b : i > b; i += st) l.push(Value(i));
+      check_generated(span_count(a, b, st, "untilStep"), "untilStep");
+      for (int64_t i = a; st > 0 ? i < b : i > b;) {
+        l.push(Value(i));
+        if (__builtin_add_overflow(i, st, &i)) break;  // the next value is past int64: done
+      }
       return l;
     }
     if (fn == "seq") {
@@ -1716,9 +1729,12 @@ struct Engine::Impl {
       if (args.size() >= 3) a = args[0].as_int(), st = args[1].as_int(), b = args[2].as_int();
       if (args.size() >= 2 && args.size() < 3 && a > b) st = -1;
       std::vector<std::string> o;
-      if (st != 0) check_generated((b - a) / st, "seq");
+      if (st != 0) check_generated(span_count(a, b, st, "seq"), "seq");
       if (st != 0)
-        for (int64_t i = a; st > 0 ? i <= b : i >= b; i += st) o.push_back(std::to_string(i));
+        for (int64_t i = a; st > 0 ? i <= b : i >= b;) {
+          o.push_back(std::to_string(i));
+          if (__builtin_add_overflow(i, st, &i)) break;
+        }
       return S(join(o, " "));
     }
     if (fn == "all") {

@@ -411,6 +411,17 @@ TEST(gotemplate_go_semantics_corner_cases) {
       {"{{ until 1000000000 | len }}",
        "ERROR: render error in t: until: 1000000000 elements exceed the limit of 10000000"},
       {"{{ repeat 3 \"ab\" }} {{ seq 3 }} {{ untilStep 0 6 2 | len }}", "ababab 1 2 3 3"},
+      // n * size wraps int64 for these: the guard must not be fooled
+      {"{{ repeat 4611686018427387904 \"ab\" }}",
+       "ERROR: render error in t: repeat: 4611686018427387904 x 2 bytes exceeds the limit of 10000000"},
+      {"{{ repeat 6000000 \"ab\" | len }}",
+       "ERROR: render error in t: repeat: 6000000 x 2 bytes exceeds the limit of 10000000"},
+      {"{{ untilStep -9223372036854775807 9223372036854775807 1 | len }}",
+       "ERROR: render error in t: untilStep: the range exceeds the limit of 10000000"},
+      {"{{ untilStep 9223372036854775806 9223372036854775807 5 | len }}", "1"},
+      {"{{ seq 9223372036854775806 5 9223372036854775807 }}", "9223372036854775806"},
+      {"{{ seq -9223372036854775807 2 9223372036854775807 | len }}",
+       "ERROR: render error in t: seq: the range exceeds the limit of 10000000"},
   };
   for (auto& c : cases) {
     std::string got;

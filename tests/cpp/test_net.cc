@@ -1,0 +1,239 @@
+// HTTP client behaviour against scripted local servers (keep-alive retry rules, chunked request
+// bodies) and the NSS-free resolver's pieces.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <functional>
+#include <thread>
+
+#include "core/net.h"
+#include "core/resolve.h"
+#include "core/strutil.h"
+#include "testing.h"
+
+using namespace ds;
+
+namespace {
+
+// One-thread TCP server: `serve` gets each accepted connection's fd in turn.
+struct ScriptedServer {
+  int lfd = -1, port = 0;
+  std::thread t;
+  std::atomic<bool> stop{false};
+  explicit ScriptedServer(std::function<void(int fd, int index)> serve) {
+    lfd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    int one = 1;
+    setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    ::bind(lfd, (sockaddr*)&a, sizeof(a));
+    socklen_t len = sizeof(a);
+    getsockname(lfd, (sockaddr*)&a, &len);
+    port = ntohs(a.sin_port);
+    ::listen(lfd, 8);
+    t = std::thread([this, serve] {
+      for (int i = 0; !stop; ++i) {
+        int fd = ::accept(lfd, nullptr, nullptr);
+        if (fd < 0) return;
+        serve(fd, i);
+        ::close(fd);
+      }
+    });
+  }
+  ~ScriptedServer() {
+    stop = true;
+    ::shutdown(lfd, SHUT_RDWR);
+    ::close(lfd);
+    if (t.joinable()) t.join();
+  }
+  std::string url() const { return "http://127.0.0.1:" + std::to_string(port); }
+};
+
+// Reads one request (head + Content-Length or chunked body); "" on EOF.
+std::string read_request(int fd, std::string* body) {
+  std::string buf;
+  char tmp[65536];
+  size_t end;
+  while ((end = buf.find("\r\n\r\n")) == std::string::npos) {
+    ssize_t n = ::read(fd, tmp, sizeof(tmp));
+    if (n <= 0) return "";
+    buf.append(tmp, (size_t)n);
+  }
+  std::string head = buf.substr(0, end);
+  std::string rest = buf.substr(end + 4);
+  auto more = [&](size_t want) {
+    while (rest.size() < want) {
+      ssize_t n = ::read(fd, tmp, sizeof(tmp));
+      if (n <= 0) return false;
+      rest.append(tmp, (size_t)n);
+    }
+    return true;
+  };
+  body->clear();
+  std::string low = to_lower(head);
+  size_t cl = low.find("content-length:");
+  if (low.find("transfer-encoding: chunked") != std::string::npos) {
+    while (true) {
+      size_t le;
+      while ((le = rest.find("\r\n")) == std::string::npos)
+        if (!more(rest.size() + 1)) return head;
+      size_t sz = std::strtoul(rest.substr(0, le).c_str(), nullptr, 16);
+      rest.erase(0, le + 2);
+      if (!more(sz + 2)) return head;
+      body->append(rest.substr(0, sz));
+      rest.erase(0, sz + 2);
+      if (sz == 0) break;
+    }
+  } else if (cl != std::string::npos) {
+    size_t n = (size_t)std::atoll(low.c_str() + cl + 15);
+    more(n);
+    *body = rest.substr(0, n);
+  }
+  return head;
+}
+
+void respond(int fd, const std::string& body) {
+  std::string r = "HTTP/1.1 200 OK\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n" + body;
+  ::write(fd, r.data(), r.size());
+}
+
+}  // namespace
+
+// a request that outlasts its timeout on a pooled connection must not be sent again
+// (a POST creating a pod would be created twice); a connection found dead is retried.
+TEST(http_pooled_timeout_is_not_retried) {
+  std::atomic<int> posts{0};
+  ScriptedServer srv([&](int fd, int) {
+    std::string body;
+    while (true) {
+      std::string head = read_request(fd, &body);
+      if (head.empty()) return;
+      if (starts_with(head, "POST")) {
+        posts++;
+        std::this_thread::sleep_for(std::chrono::milliseconds(900));  // slower than the client waits
+        return;
+      }
+      respond(fd, "ok");
+    }
+  });
+  net::HttpClient c(srv.url());
+  EXPECT_EQ(c.get("/warm").status, 200);  // leaves a pooled keep-alive connection
+  net::Request post;
+  post.method = "POST";
+  post.path = "/api/v1/namespaces/x/pods";
+  post.body = "{}";
+  post.timeout_ms = 300;
+  EXPECT_THROWS(c.request(post));
+  std::this_thread::sleep_for(std::chrono::milliseconds(1200));
+  EXPECT_EQ(posts.load(), 1);
+}
+
+TEST(http_dead_pooled_connection_is_retried_once) {
+  ScriptedServer srv([&](int fd, int) {
+    std::string body;
+    if (read_request(fd, &body).empty()) return;
+    respond(fd, "first");  // then close: the pooled connection is dead before the next use
+  });
+  net::HttpClient c(srv.url());
+  EXPECT_EQ(c.get("/a").body, std::string("first"));
+  std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  net::Response r = c.get("/b");  // written into a dead pooled connection, retried on a new one
+  EXPECT_EQ(r.status, 200);
+  EXPECT_EQ(r.body, std::string("first"));
+}
+
+TEST(http_streamed_request_body_is_chunked) {
+  ScriptedServer srv([&](int fd, int) {
+    std::string body;
+    std::string head = read_request(fd, &body);
+    if (head.empty()) return;
+    bool chunked = to_lower(head).find("transfer-encoding: chunked") != std::string::npos;
+    respond(fd, std::string(chunked ? "chunked:" : "sized:") + std::to_string(body.size()) + ":" +
+                    (body.size() > 3 ? body.substr(body.size() - 3) : body));
+  });
+  net::HttpClient c(srv.url());
+  net::Request r;
+  r.method = "POST";
+  r.path = "/build";
+  size_t produced = 0;
+  r.body_writer = [&](const std::function<bool(const char*, size_t)>& sink) {
+    std::string block(100000, 'x');
+    for (int i = 0; i < 50; ++i) {
+      if (i == 49) block.replace(block.size() - 3, 3, "end");
+      if (!sink(block.data(), block.size())) return false;
+      produced += block.size();
+    }
+    return true;
+  };
+  net::Response resp = c.request(r);
+  EXPECT_EQ(resp.status, 200);
+  EXPECT_EQ(resp.body, std::string("chunked:5000000:end"));
+  EXPECT_EQ(produced, (size_t)5000000);
+}
+
+TEST(resolver_hosts_resolvconf_and_candidates) {
+  std::string hosts = "127.0.0.1 localhost\n# comment\n10.1.2.3\tapi.internal  api # alias\n::1 ip6-localhost\n";
+  EXPECT_EQ(net::hosts_lookup(hosts, "API").size(), (size_t)1);
+  EXPECT_EQ(net::hosts_lookup(hosts, "api.internal.")[0], std::string("10.1.2.3"));
+  EXPECT_TRUE(net::hosts_lookup(hosts, "comment").empty());
+  net::ResolvConf rc = net::ResolvConf::parse(
+      "nameserver 10.96.0.10\nnameserver fe80::1%eth0\nsearch ns1.svc.cluster.local svc.cluster.local cluster.local\n"
+      "options ndots:5 timeout:1 attempts:3\n");
+  EXPECT_EQ(rc.nameservers.size(), (size_t)2);
+  EXPECT_EQ(rc.ndots, 5);
+  EXPECT_EQ(rc.timeout_s, 1);
+  EXPECT_EQ(rc.attempts, 3);
+  auto c = net::dns_candidates("kubernetes.default", rc);  // fewer dots than ndots: search first
+  EXPECT_EQ(c.front(), std::string("kubernetes.default.ns1.svc.cluster.local"));
+  EXPECT_EQ(c.back(), std::string("kubernetes.default"));
+  EXPECT_EQ(net::dns_candidates("example.com.", rc).size(), (size_t)1);
+  net::ResolvConf def = net::ResolvConf::parse("");
+  EXPECT_EQ(def.nameservers.size(), (size_t)2);
+  auto d = net::dns_candidates("a.b", def);  // ndots 1: absolute first
+  EXPECT_EQ(d.front(), std::string("a.b"));
+  auto lit = net::resolve("127.0.0.1", 80);
+  EXPECT_EQ(lit.size(), (size_t)1);
+  EXPECT_EQ(net::resolve("[::1]", 80).size(), (size_t)1);
+  EXPECT_TRUE(!net::resolve("localhost", 80).empty());
+}
+
+TEST(resolver_dns_packets) {
+  std::string q = net::dns_query_packet("api.example.com", 1, 0x1234);
+  EXPECT_EQ(q.size(), (size_t)(12 + 17 + 4));
+  // a response: the question, a CNAME, then two A records (compressed owner names)
+  std::string r = q;
+  r[2] = (char)0x81;
+  r[3] = (char)0x80;
+  r[7] = 3;  // ANCOUNT
+  auto rr = [&](uint16_t type, const std::string& rdata) {
+    std::string x = "\xc0\x0c";
+    x.push_back((char)(type >> 8));
+    x.push_back((char)type);
+    x += std::string("\x00\x01\x00\x00\x00\x3c", 6);
+    x.push_back((char)(rdata.size() >> 8));
+    x.push_back((char)rdata.size());
+    return x + rdata;
+  };
+  r += rr(5, std::string("\x03" "lb1\xc0\x10", 6));
+  r += rr(1, std::string("\x0a\x00\x00\x07", 4));
+  r += rr(1, std::string("\x0a\x00\x00\x08", 4));
+  std::vector<std::string> addrs;
+  bool tc = true;
+  EXPECT_TRUE(net::dns_parse_response(r, 0x1234, &addrs, &tc));
+  EXPECT_TRUE(!tc);
+  EXPECT_EQ(addrs.size(), (size_t)2);
+  EXPECT_EQ(addrs[0], std::string("10.0.0.7"));
+  std::vector<std::string> none;
+  EXPECT_TRUE(!net::dns_parse_response(r, 0x9999, &none, &tc));  // not our id
+  std::string nx = q;
+  nx[2] = (char)0x81;
+  nx[3] = (char)0x83;  // NXDOMAIN
+  EXPECT_TRUE(!net::dns_parse_response(nx, 0x1234, &none, &tc));
+  EXPECT_TRUE(!net::dns_parse_response(r.substr(0, r.size() - 2), 0x1234, &none, &tc));  // truncated record
+}
