@@ -78,6 +78,8 @@ SP build_latest() {
   auto helm = st("latest.HelmConfig", {{"chartPath", str()},
                                        {"wait", boolean()},
                                        {"timeout", integer()},
+                                       // revisions kept per release (helm --history-max; 0 = all)
+                                       {"maxHistory", integer()},
                                        {"tillerNamespace", str()},
                                        {"overrides", list(str())},
                                        {"overrideValues", any()}});

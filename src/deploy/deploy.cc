@@ -1,5 +1,6 @@
 #include "deploy/deploy.h"
 
+#include <cstdlib>
 #include <algorithm>
 
 #include "build/docker.h"
@@ -130,6 +131,8 @@ class HelmDeployer : public Deployer {
       if (dep["helmOverrideTimestamps"].get(ov.as_string()).as_int(-1) != st.mtime_sec) override_changed = true;
     }
     helm::Client hc(k_);
+    if (const char* mh = std::getenv("DEVSPACE_HELM_MAX_HISTORY")) hc.set_max_history(std::atoi(mh));
+    if (!d_.at_path("helm.maxHistory").is_null()) hc.set_max_history((int)d_.at_path("helm.maxHistory").as_int(10));
     bool redeploy = force || dep.get("helmChartHash").as_string() != hash || override_changed;
     if (!redeploy) redeploy = !hc.release_exists(ns, name);
     if (!redeploy) {

@@ -743,6 +743,31 @@ void Client::store(const Release& r) {
   k_->apply(s, r.namespace_);
 }
 
+// Helm 3 (pkg/action/upgrade.go + storage.removeLeastRecent): delete the oldest revisions
+// beyond max_history_, never the deployed one.
+void Client::prune_history(const std::string& ns, const std::string& name) {
+  if (max_history_ <= 0) return;
+  Value list = k_->get("/api/v1/namespaces/" + ns + "/secrets?labelSelector=" +
+                       net::url_encode("owner=helm,name=" + name));
+  std::vector<std::pair<int, std::pair<std::string, std::string>>> revs;  // version, (secret, status)
+  for (auto& s : list.get("items").items())
+    revs.push_back({(int)std::atoi(s.at_path("metadata.labels.version").as_string("0").c_str()),
+                    {s.at_path("metadata.name").as_string(), s.at_path("metadata.labels.status").as_string()}});
+  std::sort(revs.begin(), revs.end());
+  int excess = (int)revs.size() - max_history_;
+  for (auto& r : revs) {
+    if (excess <= 0) break;
+    if (r.second.second == "deployed") continue;
+    try {
+      k_->del("/api/v1/namespaces/" + ns + "/secrets/" + r.second.first);
+      --excess;
+    } catch (const std::exception& e) {
+      log::warn("Could not prune release revision " + r.second.first + ": " + e.what());
+      return;
+    }
+  }
+}
+
 std::vector<Release> Client::history(const std::string& ns, const std::string& name) {
   std::vector<Release> out;
   Value list = k_->get("/api/v1/namespaces/" + ns + "/secrets?labelSelector=" +
@@ -1115,6 +1140,7 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
   r.status = "deployed";
   r.description = ro.is_install ? "Install complete" : "Upgrade complete";
   store(r);
+  prune_history(ns, name);
   return r;
 }
 
@@ -1158,6 +1184,7 @@ void Client::rollback(const std::string& ns, const std::string& name, int to_ver
       store(old);
     }
   store(r);
+  prune_history(ns, name);
 }
 
 void Client::delete_release(const std::string& ns, const std::string& name, bool purge) {

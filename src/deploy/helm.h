@@ -116,6 +116,10 @@ class Client {
   Release install_or_upgrade(const std::string& name, const std::string& ns, const std::string& chart_path,
                              const Value& values, bool wait, int timeout_s);
   void rollback(const std::string& ns, const std::string& name, int to_version);
+  // Revisions kept per release after an install/upgrade/rollback (Helm 3's --history-max,
+  // default 10; 0 keeps all). Each revision is a Secret holding the gzipped chart, so a long
+  // `devspace dev` session with auto-reload would otherwise pile them up.
+  void set_max_history(int n) { max_history_ = n; }
   void delete_release(const std::string& ns, const std::string& name, bool purge = true);
   // Waits for every workload in the manifest to be ready; returns "" or a failure summary.
   std::string wait_ready(const std::vector<Value>& objs, const std::string& ns, int timeout_s);
@@ -124,6 +128,8 @@ class Client {
 
  private:
   void store(const Release& r);
+  void prune_history(const std::string& ns, const std::string& name);
+  int max_history_ = 10;
   // Runs the hooks of one lifecycle event in weight order; throws on a failed hook.
   void run_hooks(std::vector<Hook>& hooks, const std::string& event, const std::string& ns, int timeout_s);
   std::shared_ptr<kube::Client> k_;

@@ -196,3 +196,24 @@ def test_values_schema_rejects_invalid_values_before_anything_is_applied(localku
     lk.run(["deploy"], proj)
     assert _cm(lk, ns, "rel-schema")["data"]["replicas"] == "2"
     lk.run(["purge"], proj)
+
+
+def test_release_history_is_pruned(localkube):
+    """Helm 3's --history-max: each revision is a Secret with the gzipped chart; a dev session that
+    redeploys on every chart edit keeps only the newest `maxHistory` (default 10), never dropping
+    the deployed one."""
+    lk = localkube
+    ns = "helm-history"
+    proj = _helm_project(lk, "hooks-chart", "helm-history", ns)
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    cfg["deployments"][0]["helm"]["maxHistory"] = 3
+    with open(cfg_path, "w") as f:
+        yaml.safe_dump(cfg, f)
+    for _ in range(5):
+        lk.run(["deploy", "-d"], proj)
+    rels = _releases(lk, ns)
+    assert [r["version"] for _, r in rels] == [3, 4, 5], [r["version"] for _, r in rels]
+    assert rels[-1][1]["info"]["status"] == "deployed"
+    assert all(r["info"]["status"] == "superseded" for _, r in rels[:-1])
+    lk.run(["purge"], proj)

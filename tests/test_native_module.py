@@ -52,6 +52,7 @@ def test_sync_session_roundtrip(tmp_path, mode):
     assert wait(lambda: (local / "b.txt").exists())
     (local / "a.txt").write_text("two!")
     assert wait(lambda: (remote / "a.txt").read_text() == "two!")
-    st = s.stats()
-    assert st["upstream_changes"] >= 2 and st["downstream_changes"] >= 1
+    # the counters move after the remote ack (and its log line), i.e. just after the bytes
+    # landed: wait for them instead of reading them the moment the file changed
+    assert wait(lambda: s.stats()["upstream_changes"] >= 2 and s.stats()["downstream_changes"] >= 1), s.stats()
     s.stop()
