@@ -15,6 +15,7 @@
 
 #include "core/fs.h"
 #include "core/log.h"
+#include "core/resolve.h"
 #include "core/prompt.h"
 #include "core/strutil.h"
 
@@ -171,33 +172,85 @@ size_t PortForwarder::active_connections() {
   return n;
 }
 
+// Listen addresses for one mapping's bindAddress, as `kubectl port-forward --address` reads
+// them: "localhost" (the default) is 127.0.0.1 plus ::1, an IPv6 literal ("::1", "[::1]", "::")
+// binds an AF_INET6 socket, a host name goes through the resolver. Returns (family, address).
+std::vector<std::pair<int, std::string>> listen_addresses(const std::string& bind) {
+  std::string a = bind.empty() ? "localhost" : bind;
+  if (a.size() > 2 && a.front() == '[' && a.back() == ']') a = a.substr(1, a.size() - 2);
+  if (to_lower(a) == "localhost") return {{AF_INET, "127.0.0.1"}, {AF_INET6, "::1"}};
+  struct in_addr v4;
+  struct in6_addr v6;
+  if (inet_pton(AF_INET, a.c_str(), &v4) == 1) return {{AF_INET, a}};
+  if (inet_pton(AF_INET6, a.c_str(), &v6) == 1) return {{AF_INET6, a}};
+  std::vector<std::pair<int, std::string>> out;
+  for (auto& r : net::resolve(a, 0)) out.push_back({r.family, r.text});
+  if (out.empty()) throw std::runtime_error("Unable to resolve port-forward address \"" + bind + "\"");
+  return out;
+}
+
+// One listening socket or -errno. "::" is dual-stack (also takes IPv4), every other IPv6
+// address is v6-only so it can sit next to the IPv4 listener on the same port.
+static int listen_on(int family, const std::string& addr, int port) {
+  int fd = ::socket(family, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) return -errno;
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  struct sockaddr_storage ss{};
+  socklen_t len;
+  if (family == AF_INET6) {
+    auto* a6 = (struct sockaddr_in6*)&ss;
+    a6->sin6_family = AF_INET6;
+    a6->sin6_port = htons((uint16_t)port);
+    inet_pton(AF_INET6, addr.c_str(), &a6->sin6_addr);
+    int v6only = addr == "::" ? 0 : 1;
+    setsockopt(fd, IPPROTO_IPV6, IPV6_V6ONLY, &v6only, sizeof(v6only));
+    len = sizeof(*a6);
+  } else {
+    auto* a4 = (struct sockaddr_in*)&ss;
+    a4->sin_family = AF_INET;
+    a4->sin_port = htons((uint16_t)port);
+    inet_pton(AF_INET, addr.c_str(), &a4->sin_addr);
+    len = sizeof(*a4);
+  }
+  if (::bind(fd, (struct sockaddr*)&ss, len) != 0 || ::listen(fd, 64) != 0) {
+    int err = errno;
+    ::close(fd);
+    return -err;
+  }
+  return fd;
+}
+
 void PortForwarder::start() {
   for (size_t i = 0; i < ports_.size(); ++i) {
-    int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
-    int one = 1;
-    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-    struct sockaddr_in a{};
-    a.sin_family = AF_INET;
-    a.sin_port = htons((uint16_t)ports_[i].first);
-    std::string addr = i < addrs_.size() && !addrs_[i].empty() ? addrs_[i] : "127.0.0.1";
-    if (addr == "localhost") addr = "127.0.0.1";
-    if (inet_pton(AF_INET, addr.c_str(), &a.sin_addr) != 1) a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-    if (::bind(fd, (struct sockaddr*)&a, sizeof(a)) != 0 || ::listen(fd, 64) != 0) {
-      int err = errno;
-      std::string e = std::strerror(err);
-      ::close(fd);
-      // Pods of the bundled local cluster share the host network: a same-number mapping is
-      // already served by the container itself.
-      if (err == EADDRINUSE && k_->is_local_cluster() && ports_[i].first == ports_[i].second) {
-        log::info("Port " + std::to_string(ports_[i].first) +
-                  " is served directly by the pod (local cluster shares the host network)");
+    std::string bind = i < addrs_.size() ? addrs_[i] : "";
+    auto addrs = listen_addresses(bind);
+    bool is_default = addrs.size() == 2 && addrs[0].second == "127.0.0.1" && addrs[1].second == "::1";
+    int bound = 0;
+    int first_err = 0;
+    for (size_t k = 0; k < addrs.size(); ++k) {
+      int fd = listen_on(addrs[k].first, addrs[k].second, ports_[i].first);
+      if (fd < 0) {
+        // kubectl tolerates one of localhost's two families failing (a host without IPv6)
+        if (is_default && k == 1 && bound > 0) continue;
+        if (!first_err) first_err = -fd;
         continue;
       }
-      throw std::runtime_error("Unable to listen on port " + std::to_string(ports_[i].first) + ": " + e);
+      listeners_.push_back(fd);
+      ++bound;
+      int rp = ports_[i].second;
+      threads_.emplace_back([this, fd, rp] { accept_loop(fd, rp); });
     }
-    listeners_.push_back(fd);
-    int rp = ports_[i].second;
-    threads_.emplace_back([this, fd, rp] { accept_loop(fd, rp); });
+    if (bound == (int)addrs.size() || (is_default && bound > 0)) continue;
+    // Pods of the bundled local cluster share the host network: a same-number mapping is
+    // already served by the container itself.
+    if (bound == 0 && first_err == EADDRINUSE && k_->is_local_cluster() && ports_[i].first == ports_[i].second) {
+      log::info("Port " + std::to_string(ports_[i].first) +
+                " is served directly by the pod (local cluster shares the host network)");
+      continue;
+    }
+    throw std::runtime_error("Unable to listen on " + (bind.empty() ? std::string("localhost") : bind) + ":" +
+                             std::to_string(ports_[i].first) + ": " + std::strerror(first_err));
   }
 }
 
@@ -345,7 +398,7 @@ std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& c
     std::vector<std::string> addrs;
     for (auto& m : pf.get("portMappings").items()) {
       ports.emplace_back((int)m.get("localPort").as_int(), (int)m.get("remotePort").as_int());
-      addrs.push_back(m.get("bindAddress").as_string("127.0.0.1"));
+      addrs.push_back(m.get("bindAddress").as_string("localhost")  /* port_forwarding.go:64-67 */);
     }
     auto fwd = std::make_unique<PortForwarder>(k, pod, ports, addrs, ref.labels.to_query());
     fwd->start();

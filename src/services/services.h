@@ -40,6 +40,10 @@ struct SyncOptions {
 std::vector<std::unique_ptr<sync::Session>> start_sync(const Value& cfg, std::shared_ptr<kube::Client> k,
                                                         const SyncOptions& o);
 
+// Listen addresses (family, literal) for a port mapping's bindAddress ("" = localhost: both
+// 127.0.0.1 and ::1, like kubectl port-forward's default).
+std::vector<std::pair<int, std::string>> listen_addresses(const std::string& bind);
+
 // Local listeners forwarding to a pod port over the portforward.k8s.io WebSocket protocol
 // (services/port_forwarding.go:18, kubectl/client.go:356). Every accepted connection gets its
 // own stream and thread; the forwarder owns those threads and joins them in close(). When the

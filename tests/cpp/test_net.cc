@@ -14,6 +14,7 @@
 #include "core/net.h"
 #include "core/resolve.h"
 #include "core/strutil.h"
+#include "services/services.h"
 #include "testing.h"
 
 using namespace ds;
@@ -236,4 +237,16 @@ TEST(resolver_dns_packets) {
   nx[3] = (char)0x83;  // NXDOMAIN
   EXPECT_TRUE(!net::dns_parse_response(nx, 0x1234, &none, &tc));
   EXPECT_TRUE(!net::dns_parse_response(r.substr(0, r.size() - 2), 0x1234, &none, &tc));  // truncated record
+}
+
+// port-forward bindAddress "::1" / "::" must not silently become 127.0.0.1.
+TEST(port_forward_listen_addresses) {
+  auto d = services::listen_addresses("");
+  EXPECT_EQ(d.size(), (size_t)2);
+  EXPECT_EQ(d[0].second, std::string("127.0.0.1"));
+  EXPECT_EQ(d[1].first, AF_INET6);
+  EXPECT_EQ(services::listen_addresses("::1")[0].first, AF_INET6);
+  EXPECT_EQ(services::listen_addresses("[::]")[0].second, std::string("::"));
+  EXPECT_EQ(services::listen_addresses("0.0.0.0")[0].first, AF_INET);
+  EXPECT_EQ(services::listen_addresses("localhost").size(), (size_t)2);
 }

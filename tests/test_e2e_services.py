@@ -39,11 +39,13 @@ def test_dev_port_forwarding_reaches_app(localkube):
     proj = lk.project("quickstart", "quickstart-pf")
     remote = _free_port()  # pods share the host network here: use a free port for the app
     local = _free_port()
+    local6 = _free_port()
     cfg_path = os.path.join(proj, ".devspace", "config.yaml")
     cfg = yaml.safe_load(open(cfg_path))
     cfg["cluster"]["namespace"] = "pf"
     cfg["dev"].pop("overrideImages")  # run the app itself in dev mode
-    cfg["dev"]["ports"][0]["portMappings"] = [{"localPort": local, "remotePort": remote}]
+    cfg["dev"]["ports"][0]["portMappings"] = [{"localPort": local, "remotePort": remote},
+                                              {"localPort": local6, "remotePort": remote, "bindAddress": "::1"}]
     open(cfg_path, "w").write(yaml.safe_dump(cfg))
     values = os.path.join(proj, "chart", "values.yaml")
     v = yaml.safe_load(open(values))
@@ -53,9 +55,9 @@ def test_dev_port_forwarding_reaches_app(localkube):
     try:
         wait_for(lambda: running(lk.pods("pf")), timeout=60, what="pod")
 
-        def fetch():
+        def fetch(host="127.0.0.1", port=local):
             try:
-                return urllib.request.urlopen(f"http://127.0.0.1:{local}/", timeout=2).read().decode()
+                return urllib.request.urlopen(f"http://{host}:{port}/", timeout=2).read().decode()
             except Exception:
                 return None
 
@@ -64,6 +66,12 @@ def test_dev_port_forwarding_reaches_app(localkube):
         # many connections through the forwarder (one WebSocket stream each)
         for _ in range(20):
             assert fetch().startswith("Hello from")
+        # the default address is localhost: ::1 as well as 127.0.0.1 (kubectl port-forward)
+        assert fetch("[::1]").startswith("Hello from")
+        # an IPv6 bindAddress listens there, not on a silently substituted 127.0.0.1
+        assert fetch("[::1]", local6).startswith("Hello from")
+        with socket.socket() as s4:
+            assert s4.connect_ex(("127.0.0.1", local6)) != 0
     finally:
         out = _stop(dev)
     assert f"Port forwarding started on {local}:{remote}" in out, out
