@@ -147,6 +147,7 @@ class PySync {
     d["full_scans"] = st.full_scans;
     d["probes"] = st.probes;
     d["probe_hits"] = st.probe_hits;
+    d["probe_interval_ms"] = st.probe_interval_ms;
     d["scan_bytes"] = st.scan_bytes;
     return d;
   }

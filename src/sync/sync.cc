@@ -1727,10 +1727,19 @@ void Session::downstream_loop() {
   // probe saw a change and until the stability rule has applied it
   bool probing = mode_ == Mode::Fast && !down_helper_ && o_.downstream_probe;
   bool scanned = false;
+  // Adaptive probe interval (fast mode): every probe walks the remote tree (`find -cnewer`), so
+  // poll at poll_ms_ (250 ms) only while something moves — a probe hit, a pending change, an
+  // upload — and back off by doubling to the reference's 1.3 s walk rate when idle.
+  bool adaptive = probing && o_.downstream_poll_ms < 0;
+  const int idle_ms = std::max(poll_ms_, 1300);
+  int wait_ms = poll_ms_;
+  uint64_t seen_up = 0;
   while (!stopping_ && !failed_) {
     bool skip = false;
+    bool active = false;
     try {
       if (probing && scanned && last_amount == 0) skip = !probe_changes();
+      active = probing && scanned && !skip;
     } catch (const std::exception& e) {
       fail(e.what());
       return;
@@ -1747,12 +1756,24 @@ void Session::downstream_loop() {
         apply = last_amount > 0 && amount == last_amount;  // stability rule (downstream.go:117)
       if (apply) apply_downstream(creates, removes);
       last_amount = amount;
+      active = active || amount > 0;
     } catch (const std::exception& e) {
       fail(e.what());
       return;
     }
+    if (adaptive) {
+      {
+        std::lock_guard<std::mutex> g(stats_mu_);
+        if (stats_.upstream_batches != seen_up) active = true;
+        seen_up = stats_.upstream_batches;
+        wait_ms = active ? poll_ms_ : std::min(idle_ms, wait_ms * 2);
+        stats_.probe_interval_ms = wait_ms;
+      }
+    } else {
+      wait_ms = poll_ms_;
+    }
     // wait for the next poll (or a container-side event in helper mode)
-    long until = mono_us() + (long)poll_ms_ * 1000;
+    long until = mono_us() + (long)wait_ms * 1000;
     while (!stopping_ && !failed_ && mono_us() < until) {
       if (down_helper_) {
         std::string ev;
@@ -1768,7 +1789,7 @@ void Session::downstream_loop() {
           return;
         }
       } else {
-        sleep_ms(std::min<int>(50, poll_ms_));
+        sleep_ms(std::min<int>(50, wait_ms));
       }
     }
   }

@@ -6,10 +6,12 @@
 //                  (600 ms upload window, 1300 ms downstream poll + stability rule,
 //                  `sleep 0.1` receive polling). Used as the reference-equivalent baseline.
 //   Mode::Fast   — POSIX-only but streamed: inotify + ~15 ms coalescing, `head -c N | tar x`
-//                  (no temp files / polling), newline acks, 250 ms downstream poll.
+//                  (no temp files / polling), newline acks; downstream `find -cnewer` change
+//                  probes every 250 ms after activity, backing off to 1.3 s when idle.
 //   Mode::Helper — uploads a static helper (src/helper) into the container that speaks a
-//                  framed binary protocol and pushes inotify events for event-driven
-//                  downstream; falls back to Fast when it cannot run.
+//                  framed binary protocol (64-bit lengths, chunk-streamed archives) and pushes
+//                  inotify events for event-driven downstream; falls back to Fast when it
+//                  cannot run.
 #pragma once
 
 #include <atomic>
@@ -113,6 +115,7 @@ struct Stats {
   // downstream scanning (non-helper modes): full `find | stat` listings, cheap change probes
   // (fast mode: `find -newer stamp`, one line at most) and the listing bytes read
   uint64_t full_scans = 0, probes = 0, probe_hits = 0, scan_bytes = 0;
+  int probe_interval_ms = 0;  // fast mode: the adaptive interval last waited (250 .. 1300)
 };
 
 class Session {
