@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Renders the README benchmark table from a driver-written ``BENCH_rNN.json`` (never from the
+builder's own runs under ``profiles/``), so the README quotes exactly what the driver measured.
+
+    python scripts/bench_table.py BENCH_r02.json            # print the table
+    python scripts/bench_table.py BENCH_r03.json --update   # rewrite README.md's bench block
+
+The README block sits between ``<!-- bench-table source=FILE -->`` and ``<!-- /bench-table -->``;
+``tests/test_readme_bench.py`` checks that it equals what this script renders from FILE.
+Handles both bench.py line formats: round 2 (``value`` = rocm-pytorch pod reload, quickstart
+under ``quickstart``) and round 3+ (``value`` = quickstart reload, extras under ``gpu_pod``,
+``deploy``, ``php_mysql``, ``microservices``, ``kaniko``).
+"""
+
+import argparse
+import json
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BEGIN = re.compile(r"<!-- bench-table source=(\S+) -->\n")
+END = "<!-- /bench-table -->"
+
+
+def load_line(path):
+    """The bench.py JSON line out of a driver BENCH file (or a bare bench.py output file)."""
+    with open(path) as f:
+        doc = json.load(f)
+    if "metric" in doc:
+        return doc, {}
+    tail = doc.get("run", {}).get("stdout_tail", "")
+    for line in tail.splitlines():
+        line = line.strip()
+        if line.startswith('{"metric"'):
+            return json.loads(line), doc
+    raise ValueError(f"{path}: no bench.py JSON line in run.stdout_tail")
+
+
+def _ms(v):
+    return "—" if v is None else (f"{v:.2f} ms" if v < 100 else f"{v:.0f} ms")
+
+
+def _s(v):
+    return "—" if v is None else f"{v:.3f} s"
+
+
+def _x(a, b):
+    return f" (**{b / a:.1f}x**)" if a and b else ""
+
+
+def render(path):
+    b, doc = load_line(path)
+    name = os.path.basename(path)
+    rows = []
+    round3 = "gpu_pod" in b or "php_mysql" in b or b.get("config", {}).get("app") == "examples/quickstart"
+    if round3:
+        ref = b.get("reference_equivalent", {})
+        rows.append(("edit → new response p50, quickstart (headline `value`)",
+                     f"**{_ms(b['value'])}** (p90 {_ms(b.get('p90_ms'))}; sync {_ms(b.get('sync_p50_ms'))})",
+                     _ms(ref.get("p50_ms")) + _x(b["value"], ref.get("p50_ms"))))
+        rows.append(("sync p50, quickstart (edit → bytes in the pod)", f"**{_ms(b.get('sync_p50_ms'))}**",
+                     _ms(ref.get("sync_p50_ms")) + _x(b.get("sync_p50_ms"), ref.get("sync_p50_ms"))))
+        g = b.get("gpu_pod")
+        if isinstance(g, dict) and "reload_p50_ms" in g:
+            gr = g.get("reference_equivalent", {})
+            rows.append((f"edit → pod hot-reload p50, rocm-pytorch ({g.get('parallelism')}, fused={g.get('fused_ops')})",
+                         f"**{_ms(g['reload_p50_ms'])}** (sync {_ms(g.get('sync_p50_ms'))})",
+                         _ms(gr.get("p50_ms")) + " (compat sync + cold workload restart)" if gr else "—"))
+        for key, label in (("php_mysql", "php-mysql"), ("microservices", "microservices"), ("kaniko", "kaniko")):
+            e = b.get(key)
+            if isinstance(e, dict) and "edit_to_pod_p50_ms" in e:
+                er = e.get("reference_equivalent", {})
+                rows.append((f"{label}: edit → pod p50 / deploy cold",
+                             f"{_ms(e['edit_to_pod_p50_ms'])} / {_s(e.get('deploy_cold_s'))}",
+                             f"{_ms(er.get('edit_to_pod_p50_ms'))} / {_s(er.get('deploy_cold_s'))}" if er else "—"))
+            elif isinstance(e, dict) and "error" in e:
+                rows.append((f"{label}", f"failed: {e['error'][:60]}", "—"))
+    else:
+        qs = b.get("quickstart", {})
+        rows.append(("edit → pod hot-reload p50, rocm-pytorch (headline `value`)",
+                     f"**{_ms(b['value'])}** (p90 {_ms(b.get('p90_ms'))}; sync {_ms(b.get('sync_p50_ms'))})",
+                     _ms(b.get("reference_equivalent", {}).get("p50_ms")) + " (compat sync + cold workload restart)"))
+        rows.append(("edit → new response p50, quickstart", f"**{_ms(qs.get('reload_p50_ms'))}**",
+                     _ms(qs.get("compat_reload_p50_ms")) + _x(qs.get("reload_p50_ms"), qs.get("compat_reload_p50_ms"))))
+        rows.append(("sync p50, quickstart (edit → bytes in the pod)", f"**{_ms(qs.get('sync_p50_ms'))}**",
+                     _ms(qs.get("compat_sync_p50_ms")) + _x(qs.get("sync_p50_ms"), qs.get("compat_sync_p50_ms"))))
+    d = b.get("deploy")
+    if isinstance(d, dict) and "wall_clock_s" in d:
+        dr = d.get("reference_equivalent", {})
+        net = d.get("net") or {}
+        rows.append(("`devspace deploy` quickstart, cold / warm (control plane only)",
+                     f"{_s(d['wall_clock_s'])} / {_s(d.get('warm_wall_clock_s'))} "
+                     f"({net.get('tls_handshakes', '?')} TLS handshakes, {net.get('requests', '?')} requests)",
+                     f"{_s(dr.get('wall_clock_s'))} / {_s(dr.get('warm_wall_clock_s'))}" if dr else "—"))
+    where = doc.get("where", "bench.py output")
+    cmd = doc.get("cmd", "")
+    head = doc.get("head", "")
+    out = [f"Driver run `{name}`: `{cmd}` on {where}" + (f", commit `{head}`" if head else "") +
+           f"; {b.get('steps')} timed steps after {b.get('warmup')} warmup, `ms_per_step` {b.get('ms_per_step')}.",
+           "",
+           "| | this rebuild | reference-equivalent, same box |",
+           "|---|---|---|"]
+    out += [f"| {a} | {c} | {r} |" for a, c, r in rows]
+    return "\n".join(out) + "\n"
+
+
+def update_readme(path, readme=os.path.join(ROOT, "README.md")):
+    text = open(readme).read()
+    m = BEGIN.search(text)
+    if not m:
+        raise SystemExit("README.md has no <!-- bench-table source=... --> block")
+    end = text.index(END, m.end())
+    name = os.path.basename(path)
+    new = text[:m.start()] + f"<!-- bench-table source={name} -->\n" + render(path) + text[end:]
+    with open(readme, "w") as f:
+        f.write(new)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("bench_file")
+    ap.add_argument("--update", action="store_true", help="rewrite README.md's bench-table block")
+    a = ap.parse_args(argv)
+    if a.update:
+        update_readme(a.bench_file)
+    else:
+        sys.stdout.write(render(a.bench_file))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

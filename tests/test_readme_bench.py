@@ -1,0 +1,63 @@
+"""The README's benchmark numbers are the driver's, not the builder's: the block between
+``<!-- bench-table source=FILE -->`` and ``<!-- /bench-table -->`` must equal what
+``scripts/bench_table.py`` renders from that driver file (README quoted a best run)."""
+
+import importlib.util
+import json
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bt():
+    spec = importlib.util.spec_from_file_location("bench_table", os.path.join(ROOT, "scripts", "bench_table.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_readme_table_is_the_driver_bench_file():
+    bt = _bt()
+    text = open(os.path.join(ROOT, "README.md")).read()
+    m = bt.BEGIN.search(text)
+    assert m, "README.md lacks the bench-table block"
+    src = m.group(1)
+    assert re.fullmatch(r"BENCH_r\d\d\.json", src), src
+    block = text[m.end():text.index(bt.END, m.end())]
+    assert block == bt.render(os.path.join(ROOT, src))
+    # every number in the table's rows comes from the driver's line
+    line, _ = bt.load_line(os.path.join(ROOT, src))
+    assert f"**{line['value']:.2f} ms**" in block
+
+
+def test_round3_line_renders_all_extras(tmp_path):
+    bt = _bt()
+    line = {
+        "metric": "m", "value": 48.2, "steps": 20, "warmup": 5, "ms_per_step": 60.1, "p90_ms": 55.0,
+        "sync_p50_ms": 0.9, "config": {"app": "examples/quickstart"},
+        "reference_equivalent": {"p50_ms": 700.0, "sync_p50_ms": 610.0},
+        "deploy": {"wall_clock_s": 0.03, "warm_wall_clock_s": 0.02, "net": {"tls_handshakes": 2, "requests": 13},
+                   "reference_equivalent": {"wall_clock_s": 6.1, "warm_wall_clock_s": 5.9}},
+        "gpu_pod": {"reload_p50_ms": 6.0, "sync_p50_ms": 0.8, "parallelism": "dp1", "fused_ops": "hip",
+                    "reference_equivalent": {"p50_ms": 5000.0}},
+        "php_mysql": {"edit_to_pod_p50_ms": 3.0, "deploy_cold_s": 1.0,
+                      "reference_equivalent": {"edit_to_pod_p50_ms": 650.0, "deploy_cold_s": 7.0}},
+        "microservices": {"error": "boom"},
+    }
+    doc = {"cmd": "python3 bench.py", "where": "mi355x:1", "head": "abc",
+           "run": {"stdout_tail": json.dumps(line) + "\n\n---- stderr ----\nnoise\n"}}
+    p = tmp_path / "BENCH_r99.json"
+    p.write_text(json.dumps(doc))
+    out = bt.render(str(p))
+    assert "**48.20 ms**" in out and "700 ms (**14.5x**)" in out
+    assert "fused=hip" in out and "dp1" in out
+    assert "php-mysql" in out and "650 ms" in out
+    assert "microservices | failed: boom" in out
+    assert "6.100 s / 5.900 s" in out
+    readme = tmp_path / "README.md"
+    readme.write_text("x\n<!-- bench-table source=BENCH_r02.json -->\nSTALE-TABLE\n<!-- /bench-table -->\ny\n")
+    bt.update_readme(str(p), readme=str(readme))
+    r = readme.read_text()
+    assert r.startswith("x\n<!-- bench-table source=BENCH_r99.json -->\nDriver run") and r.endswith(
+        "<!-- /bench-table -->\ny\n") and "STALE-TABLE" not in r
