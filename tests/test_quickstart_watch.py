@@ -1,0 +1,85 @@
+"""examples/quickstart/watch.js — the restart-on-change runner of the headline benchmark's app.
+Each edit must restart the server as a fresh process running the new code as its main module
+(what nodemon does), whether the restart goes through the pre-booted standby or a cold spawn."""
+
+import os
+import shutil
+import signal
+import socket
+import subprocess
+import time
+import urllib.request
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = shutil.which("node")
+
+APP = """const http = require('http');
+const port = process.env.PORT;
+const main = require.main === module;
+const st = typeof process.send + '/' + typeof process.connected;  // the IPC channel of a standby must not leak into the app
+http.createServer((req, res) => {
+  res.end(JSON.stringify({tag: 'TAG', pid: process.pid, main, send: st, argv1: process.argv[1]}));
+}).listen(port);
+"""
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _get(port):
+    import json
+    try:
+        return json.loads(urllib.request.urlopen(f"http://127.0.0.1:{port}/", timeout=2).read())
+    except Exception:
+        return None
+
+
+def _wait(pred, timeout=30):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        v = pred()
+        if v:
+            return v
+        time.sleep(0.01)
+    raise AssertionError("timed out")
+
+
+@pytest.mark.skipif(NODE is None, reason="node not installed")
+@pytest.mark.parametrize("standby", ["1", "0"])
+def test_watch_restarts_fresh_main_module(tmp_path, standby):
+    shutil.copy(os.path.join(ROOT, "examples", "quickstart", "watch.js"), tmp_path / "watch.js")
+    app = tmp_path / "index.js"
+    app.write_text(APP.replace("TAG", "v0"))
+    port = _port()
+    p = subprocess.Popen([NODE, "watch.js", "index.js"], cwd=tmp_path, start_new_session=True,
+                         env=dict(os.environ, PORT=str(port), WATCH_STANDBY=standby),
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        first = _wait(lambda: _get(port))
+        pids = {first["pid"]}
+        for i in range(1, 4):
+            time.sleep(0.4)  # let the next standby boot
+            tmp = tmp_path / ".index.js.tmp"
+            tmp.write_text(APP.replace("TAG", f"v{i}"))
+            os.rename(tmp, app)  # how devspace sync lands a file
+            r = _wait(lambda: (lambda b: b if b and b["tag"] == f"v{i}" else None)(_get(port)))
+            assert r["main"] is True, r  # require.main === module, as under `node index.js`
+            assert r["send"] == "undefined/undefined", r
+            assert r["argv1"] == str(app), r
+            assert r["pid"] not in pids, r  # a fresh process per edit
+            pids.add(r["pid"])
+    finally:
+        os.killpg(p.pid, signal.SIGTERM)
+        out, _ = p.communicate(timeout=10)
+    assert "[watch] started gen=4" in out, out
+    # no process of the tree outlives the watcher (the standby exits with its parent channel)
+    time.sleep(0.5)
+    for pid in pids:
+        assert not os.path.exists(f"/proc/{pid}") or open(f"/proc/{pid}/stat").read().split()[2] == "Z"
