@@ -190,6 +190,9 @@ def test_tinylm_step_uses_fused_ops_and_trains():
         def preempt_point(self):  # runner.Context hook; nothing to preempt here
             pass
 
+        def log(self, msg):
+            print(msg)
+
     state = mod.setup(Ctx())
     losses = [mod.step(Ctx(), state)["loss"] for _ in range(8)]
     assert losses[-1] < losses[0], losses
