@@ -9,12 +9,13 @@
 // for it to exit so the port is free, and starts it again. Edits that land while a restart is
 // in progress coalesce into one more restart.
 //
-// Every restart is a fresh process, as with nodemon, but not a cold one: one standby node
-// process is kept booted (V8 + core modules initialised, nothing of the app loaded). A restart
-// hands the script to the standby, which loads it then — from disk, after the edit — as its
-// main module (`require.main === module` holds), and a new standby boots in the background.
-// That takes node's start-up (tens of ms) out of every edit -> response. Set
-// WATCH_STANDBY=0 for plain cold restarts.
+// Every restart is a fresh process, as with nodemon, but not a cold one: standby node
+// processes are kept booted (V8 + core modules initialised, nothing of the app loaded). A
+// restart hands the script to a booted standby, which loads it then — from disk, after the
+// edit — as its main module (`require.main === module` holds), and a replacement boots in the
+// background. That takes node's start-up (tens of ms) out of every edit -> response. Two
+// standbys by default, so back-to-back saves (format-on-save, quick fix-ups) still find one
+// booted; WATCH_STANDBY=N sets the count, 0 gives plain cold restarts.
 const {spawn} = require('child_process');
 const fs = require('fs');
 const path = require('path');
@@ -22,41 +23,50 @@ const path = require('path');
 const script = path.resolve(process.argv[2] || 'index.js');
 const dir = path.dirname(script);
 const ignored = /(^|\/)(node_modules|\.git|\.devspace)(\/|$)|\.sw.$|~$/;
-const useStandby = process.env.WATCH_STANDBY !== '0';
+const nStandby = Math.max(0, parseInt(process.env.WATCH_STANDBY || '2', 10) || 0);
 // The standby's whole program: load the core modules a server needs (node loads them lazily,
 // and they are shared, stateless code: nothing of the app), wait for the go message, drop the
 // IPC channel (the app must not see a parent channel) and run the script as the main module.
 const PRELOAD = ['http', 'https', 'net', 'url', 'querystring', 'stream', 'events', 'util', 'crypto',
                  'zlib', 'os', 'fs', 'path', 'buffer', 'string_decoder', 'timers', 'dns'];
 const BOOT = `for (const m of ${JSON.stringify(PRELOAD)}) { try { require(m); } catch (e) {} }\n` +
-    "process.once('message', (m) => { process.argv[1] = m.script; process.disconnect(); " +
+    "process.send('ready'); process.once('message', (m) => { " +
+    "process.argv[1] = m.script; process.disconnect(); " +
     "for (const k of ['send', 'disconnect', 'connected', 'channel']) { try { delete process[k]; } catch (e) {} } " +
     "require('module').runMain(); });";
 let child = null;
-let standby = null;
+let standbys = [];  // booting or booted, oldest first
 let pending = false;
 let restarting = false;
 let gen = 0;
 
-function bootStandby() {
-  if (!useStandby || standby) return;
-  standby = spawn(process.execPath, ['-e', BOOT], {stdio: ['inherit', 'inherit', 'inherit', 'ipc']});
-  const s = standby;
-  s.on('exit', () => {
-    if (standby === s) standby = null;
-  });
+function bootStandbys() {
+  while (standbys.length < nStandby) {
+    const s = spawn(process.execPath, ['-e', BOOT], {stdio: ['inherit', 'inherit', 'inherit', 'ipc']});
+    s.ready = false;
+    s.on('message', (m) => {
+      if (m === 'ready') s.ready = true;
+    });
+    s.on('exit', () => {
+      standbys = standbys.filter((x) => x !== s);
+    });
+    standbys.push(s);
+  }
 }
 
 function start() {
   gen++;
-  if (standby) {
-    child = standby;
-    standby = null;
+  // a booted standby if there is one, else the one that started booting first
+  const i = standbys.findIndex((s) => s.ready);
+  const s = standbys.splice(i >= 0 ? i : 0, 1)[0];
+  if (s) {
+    s.removeAllListeners('message');
+    child = s;
     child.send({script});
   } else {
     child = spawn(process.execPath, [script], {stdio: 'inherit'});
   }
-  console.log('[watch] started gen=' + gen + ' pid=' + child.pid);
+  console.log('[watch] started gen=' + gen + ' pid=' + child.pid + (s ? ' (standby' + (s.ready ? ')' : ', booting)') : ''));
   const me = child;
   me.on('exit', () => {
     if (child !== me) return;
@@ -67,8 +77,7 @@ function start() {
       if (pending) schedule();
     }
   });
-  // boot the next standby once this start is under way (it competes for the CPU otherwise)
-  setTimeout(bootStandby, 50);
+  setImmediate(bootStandbys);
 }
 
 function schedule() {
@@ -92,7 +101,7 @@ fs.watch(dir, {persistent: true}, (event, name) => {
 for (const sig of ['SIGINT', 'SIGTERM']) {
   process.on(sig, () => {
     restarting = false;
-    if (standby) standby.kill('SIGKILL');
+    for (const x of standbys) x.kill('SIGKILL');
     if (child) child.kill(sig);
     process.exit(0);
   });

@@ -52,7 +52,7 @@ def _wait(pred, timeout=30):
 
 
 @pytest.mark.skipif(NODE is None, reason="node not installed")
-@pytest.mark.parametrize("standby", ["1", "0"])
+@pytest.mark.parametrize("standby", ["2", "1", "0"])
 def test_watch_restarts_fresh_main_module(tmp_path, standby):
     shutil.copy(os.path.join(ROOT, "examples", "quickstart", "watch.js"), tmp_path / "watch.js")
     app = tmp_path / "index.js"
@@ -79,6 +79,10 @@ def test_watch_restarts_fresh_main_module(tmp_path, standby):
         os.killpg(p.pid, signal.SIGTERM)
         out, _ = p.communicate(timeout=10)
     assert "[watch] started gen=4" in out, out
+    if standby != "0":
+        assert "(standby)" in out, out  # restarts went through a booted standby
+    else:
+        assert "standby" not in out, out
     # no process of the tree outlives the watcher (the standby exits with its parent channel)
     time.sleep(0.5)
     for pid in pids:
