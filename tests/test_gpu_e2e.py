@@ -2,9 +2,12 @@
 examples/rocm-pytorch training pod through `devspace deploy`; `devspace analyze --gpu-probe`
 runs the gfx950 probe kernels inside the pod."""
 
+import glob
 import json
 import os
 import re
+import shutil
+import sys
 import time
 
 import pytest
@@ -32,6 +35,24 @@ def test_rocm_pytorch_pod_trains_on_gpu(tmp_path):
     try:
         lk = DevspaceEnv(cluster, str(tmp_path))
         proj = lk.project("rocm-pytorch")
+        prof = os.environ.get("DEVSPACE_E2E_POD_PROFILE")
+        if prof:
+            # profile the workload inside the pod, as one would on a real node: the container
+            # command runs the image's entrypoint under rocprofv3 (kernel trace, written when
+            # the runner exits on the pod's SIGTERM at purge)
+            import yaml
+
+            rocprof = shutil.which("rocprofv3")
+            assert rocprof, "rocprofv3 not on PATH"
+            prof = os.path.realpath(prof)
+            os.makedirs(prof, exist_ok=True)
+            vpath = os.path.join(proj, "chart", "values.yaml")
+            v = yaml.safe_load(open(vpath))
+            v["components"][0]["containers"][0]["command"] = [
+                rocprof, "--kernel-trace", "--stats", "-d", prof, "-o", "pod", "--",
+                sys.executable, "-m", "devspace_amd.runner", "--watch", "/app", "train.py"]
+            with open(vpath, "w") as f:
+                yaml.safe_dump(v, f, sort_keys=False)
         node = cluster.store.get("", "nodes", "", "devspace-local")
         assert node["status"]["allocatable"]["amd.com/gpu"] == str(gpus)
         out = lk.run(["deploy"], proj, timeout=600).stdout
@@ -60,5 +81,10 @@ def test_rocm_pytorch_pod_trains_on_gpu(tmp_path):
         if m.group(2) == "devspace":
             assert re.search(r"MFMA self-test err 0(\.0)?(,|$)", m.group(3)), report
         lk.run(["purge"], proj, timeout=120)
+        if prof:
+            dbs = _wait(lambda: glob.glob(os.path.join(prof, "**", "*.db"), recursive=True) or
+                        glob.glob(os.path.join(prof, "**", "*kernel_stats.csv"), recursive=True), 60,
+                        "the pod's rocprofv3 output")
+            print("pod profile:", dbs)
     finally:
         cluster.stop()
