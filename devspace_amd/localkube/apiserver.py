@@ -571,7 +571,11 @@ class ApiServer:
         try:
             reader, writer = await asyncio.open_connection("127.0.0.1", port)
         except OSError as e:
-            await ws.send_bytes(b"\x01" + f"error forwarding port {port} to pod {name}: {e}".encode())
+            # the kubelet's wording (CRI streaming server): clients key on "connection refused"
+            why = "connect: connection refused" if isinstance(e, ConnectionRefusedError) or "111" in str(e) else str(e)
+            await ws.send_bytes(b"\x01" + (f"error forwarding port {port} to pod {name}, uid : failed to connect to "
+                                            f"localhost:{port} inside namespace: dial tcp4 127.0.0.1:{port}: "
+                                            f"{why}").encode())
             await ws.close()
             return ws
 

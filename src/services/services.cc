@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cstring>
 
+#include "core/compat.h"
 #include "core/fs.h"
 #include "core/log.h"
 #include "core/resolve.h"
@@ -318,55 +319,116 @@ std::unique_ptr<net::WebSocket> PortForwarder::open_stream(int remote_port) {
   }
 }
 
+// True for the error-channel message of a stream whose pod-side connect failed (kubelet /
+// CRI: "... dial tcp4 127.0.0.1:8080: connect: connection refused"): nothing reached the
+// container, so the client's bytes can be replayed on a new stream.
+bool is_dial_refused(const std::string& err) { return contains(to_lower(err), "connection refused"); }
+
+static long mono_ms() {
+  return (long)std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+int port_forward_hold_ms() {
+  if (const char* v = std::getenv("DEVSPACE_PORTFORWARD_HOLD_MS")) return std::max(0, std::atoi(v));
+  return reference_timing() ? 0 : 3000;
+}
+
+// One accepted local connection. Restart-tolerant: while the app in the pod is restarting
+// (hot reload), its port refuses connections for a moment; kubectl then drops the client's
+// connection and a browser shows an error. Here, as long as nothing came back from the pod yet
+// and the pod-side connect was refused, the connection is held and its bytes replayed on a
+// new stream (backoff 2 -> 25 ms) for up to hold_ms_, so a request sent mid-restart is
+// answered by the new server as soon as it listens.
 void PortForwarder::handle(Conn* conn, int remote_port) {
   int cfd = conn->fd;
-  std::unique_ptr<net::WebSocket> ws;
-  try {
-    ws = open_stream(remote_port);
-  } catch (const std::exception& e) {
-    log::file_logger("portforwarding")->emit("error", std::string("Error forwarding ports: ") + e.what(), {});
-    ::close(cfd);
-    conn->done = true;
-    return;
-  }
-  std::atomic<bool> down_done{false};
-  std::thread down([&] {
-    std::string msg;
-    bool first_data = true, first_err = true;
-    while (ws->recv(&msg)) {
-      if (msg.empty()) continue;
-      unsigned char ch = (unsigned char)msg[0];
-      std::string data = msg.substr(1);
-      // each channel's first frame carries the port number (2 bytes LE)
-      if (ch == 0 && first_data) {
-        first_data = false;
-        if (data.size() == 2) continue;
+  const long hold_deadline = mono_ms() + hold_ms_;
+  std::string replay;           // client bytes of this connection, kept while no reply arrived
+  bool replayable = hold_ms_ > 0;
+  bool client_eof = false;
+  int backoff_ms = 2;
+  while (!stop_) {
+    std::unique_ptr<net::WebSocket> ws;
+    try {
+      ws = open_stream(remote_port);
+    } catch (const std::exception& e) {
+      log::file_logger("portforwarding")->emit("error", std::string("Error forwarding ports: ") + e.what(), {});
+      break;
+    }
+    if (!replay.empty() && !ws->send(std::string(1, '\0') + replay)) break;
+    int wake[2];
+    if (::pipe2(wake, O_CLOEXEC | O_NONBLOCK) != 0) break;
+    std::atomic<bool> down_done{false}, got_reply{false}, refused{false};
+    std::thread down([&] {
+      std::string msg;
+      bool first_data = true, first_err = true;
+      while (ws->recv(&msg)) {
+        if (msg.empty()) continue;
+        unsigned char ch = (unsigned char)msg[0];
+        std::string data = msg.substr(1);
+        // each channel's first frame carries the port number (2 bytes LE)
+        if (ch == 0 && first_data) {
+          first_data = false;
+          if (data.size() == 2) continue;
+        }
+        if (ch == 1 && first_err) {
+          first_err = false;
+          if (data.size() == 2) continue;
+        }
+        if (ch == 0) {
+          got_reply = true;
+          if (!write_all(cfd, data)) break;
+        } else if (ch == 1 && !data.empty()) {
+          if (!got_reply && is_dial_refused(data)) {
+            refused = true;
+            break;
+          }
+          log::file_logger("portforwarding")->emit("error", data, {});
+        }
       }
-      if (ch == 1 && first_err) {
-        first_err = false;
-        if (data.size() == 2) continue;
+      down_done = true;
+      ssize_t w = ::write(wake[1], "x", 1);
+      (void)w;
+    });
+    char buf[65536];
+    buf[0] = 0;
+    while (!down_done && !stop_ && !client_eof) {
+      struct pollfd pf[2] = {{cfd, POLLIN, 0}, {wake[0], POLLIN, 0}};
+      int r = ::poll(pf, 2, 200);
+      if (r <= 0 || !(pf[0].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+      ssize_t n = ::recv(cfd, buf + 1, sizeof(buf) - 1, 0);
+      if (n <= 0) {
+        client_eof = true;  // half-close: the request is complete, keep reading the reply
+        break;
       }
-      if (ch == 0) {
-        if (!write_all(cfd, data)) break;
-      } else if (ch == 1 && !data.empty()) {
-        log::file_logger("portforwarding")->emit("error", data, {});
+      if (replayable && !got_reply) {
+        replay.append(buf + 1, (size_t)n);
+        if (replay.size() > (4u << 20)) replayable = false;  // a large upload: do not buffer it
+      }
+      if (!ws->send(std::string(buf, (size_t)n + 1))) break;
+    }
+    if (client_eof && !down_done) {
+      // the client finished sending: wait for the reply (or the refusal) before closing
+      while (!down_done && !stop_) {
+        struct pollfd pw{wake[0], POLLIN, 0};
+        ::poll(&pw, 1, 200);
       }
     }
-    down_done = true;
-    ::shutdown(cfd, SHUT_RDWR);
-  });
-  char buf[65536];
-  buf[0] = 0;
-  while (!down_done && !stop_) {
-    struct pollfd pf{cfd, POLLIN, 0};
-    int r = ::poll(&pf, 1, 200);
-    if (r == 0) continue;
-    ssize_t n = ::recv(cfd, buf + 1, sizeof(buf) - 1, 0);
-    if (n <= 0) break;
-    if (!ws->send(std::string(buf, (size_t)n + 1))) break;
+    ws->close();
+    down.join();
+    ::close(wake[0]);
+    ::close(wake[1]);
+    if (refused && replayable && !stop_ && mono_ms() < hold_deadline) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(backoff_ms));
+      backoff_ms = std::min(25, backoff_ms * 2);
+      held_retries_++;
+      continue;
+    }
+    if (refused) log::file_logger("portforwarding")->emit("error", "connection refused by the pod", {});
+    break;
   }
-  ws->close();
-  down.join();
+  ::shutdown(cfd, SHUT_RDWR);
   ::close(cfd);
   conn->done = true;
 }

@@ -44,6 +44,11 @@ std::vector<std::unique_ptr<sync::Session>> start_sync(const Value& cfg, std::sh
 // 127.0.0.1 and ::1, like kubectl port-forward's default).
 std::vector<std::pair<int, std::string>> listen_addresses(const std::string& bind);
 
+// How long a local connection is held while the pod refuses it (app restarting):
+// DEVSPACE_PORTFORWARD_HOLD_MS, default 3000; 0 with DEVSPACE_REFERENCE_TIMING (kubectl drops it).
+int port_forward_hold_ms();
+bool is_dial_refused(const std::string& error_channel_message);
+
 // Local listeners forwarding to a pod port over the portforward.k8s.io WebSocket protocol
 // (services/port_forwarding.go:18, kubectl/client.go:356). Every accepted connection gets its
 // own stream and thread; the forwarder owns those threads and joins them in close(). When the
@@ -60,6 +65,8 @@ class PortForwarder {
   std::string describe() const;
   std::string pod_name();
   int reselections() const { return reselections_; }
+  // Connections replayed on a new stream because the pod refused them mid-restart.
+  int held_retries() const { return held_retries_; }
   size_t active_connections();
 
  private:
@@ -84,6 +91,8 @@ class PortForwarder {
   std::vector<std::unique_ptr<Conn>> conns_;
   std::atomic<bool> stop_{false};
   std::atomic<int> reselections_{0};
+  std::atomic<int> held_retries_{0};
+  int hold_ms_ = port_forward_hold_ms();
 };
 
 std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& cfg, std::shared_ptr<kube::Client> k,

@@ -52,10 +52,11 @@ class DevspaceEnv:
             raise AssertionError(f"devspace {' '.join(args)} failed rc={p.returncode}\n{p.stdout}\n{p.stderr}")
         return p
 
-    def popen(self, args, cwd):
+    def popen(self, args, cwd, env=None):
         import subprocess
 
-        return subprocess.Popen([self.bin] + list(args), cwd=cwd, env=self.env, stdout=subprocess.PIPE,
+        return subprocess.Popen([self.bin] + list(args), cwd=cwd, env=dict(self.env, **(env or {})),
+                                stdout=subprocess.PIPE,
                                 stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, text=True,
                                 start_new_session=True)
 

@@ -1,6 +1,7 @@
 """Dev services end to end: port-forwarding, interactive terminal (PTY), logs --follow, and the
 dev auto-reload loop (redeploy on change), against the local cluster."""
 
+import json
 import os
 import pty
 import re
@@ -11,6 +12,7 @@ import subprocess
 import time
 import urllib.request
 
+import pytest
 import yaml
 
 from test_e2e_cli import running, wait_for
@@ -203,4 +205,69 @@ def test_dev_auto_reload_redeploys_on_change(localkube):
         out = _stop(dev)
     assert "Change detected, will reload in 2 seconds" in out, out
     assert out.count("Building image") >= 2, out
+    lk.run(["purge"], proj)
+
+
+def _restart_project(lk, name, ns):
+    proj = lk.project("quickstart", name)
+    remote, local = _free_port(), _free_port()
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    cfg["cluster"]["namespace"] = ns
+    cfg["dev"]["overrideImages"][0]["entrypoint"] = ["node", "watch.js", "index.js"]
+    cfg["dev"]["ports"][0]["portMappings"] = [{"localPort": local, "remotePort": remote}]
+    open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    values = os.path.join(proj, "chart", "values.yaml")
+    v = yaml.safe_load(open(values))
+    # cold restarts: a wide window in which the pod refuses connections
+    v["components"][0]["containers"][0]["env"] = [{"name": "PORT", "value": str(remote)},
+                                                  {"name": "WATCH_STANDBY", "value": "0"}]
+    open(values, "w").write(yaml.safe_dump(v))
+    return proj, remote, local
+
+
+def _get(port, timeout=10):
+    try:
+        return urllib.request.urlopen(f"http://127.0.0.1:{port}/", timeout=timeout).read().decode()
+    except Exception as e:
+        return e
+
+
+def _refused(port):
+    with socket.socket() as s:
+        return s.connect_ex(("127.0.0.1", port)) != 0
+
+
+
+@pytest.mark.parametrize("hold", [True, False])
+def test_port_forward_holds_requests_across_app_restart(localkube, hold):
+    """A request sent while the app in the pod restarts (hot reload) is answered by the new
+    server instead of failing: the forwarder replays it on a new stream while the pod-side
+    connect is refused (DEVSPACE_PORTFORWARD_HOLD_MS=0 gives kubectl's drop)."""
+    lk = localkube
+    ns = "pf-hold" if hold else "pf-nohold"
+    proj, remote, local = _restart_project(lk, "quickstart-" + ns, ns)
+    env = {} if hold else {"DEVSPACE_PORTFORWARD_HOLD_MS": "0"}
+    dev = lk.popen(["dev", "--terminal=false"], proj, env=env)
+    try:
+        wait_for(lambda: isinstance(_get(local, 2), str) and _get(local, 2).startswith("Hello"), timeout=60,
+                 what="forwarded server")
+        root = json.loads(running(lk.pods(ns))[0]["metadata"]["annotations"]["devspace.sh/local-roots"])
+        pod_index = os.path.join(list(root.values())[0], "app", "index.js")
+        outcomes = []
+        for i in range(3):
+            src = open(os.path.join(proj, "index.js")).read()
+            with open(os.path.join(proj, "index.js"), "w") as f:
+                f.write(src.replace("'Hello from '", f"'[h{i}] Hello from '", 1) if i == 0 else
+                        src.replace(f"[h{i - 1}]", f"[h{i}]"))
+            wait_for(lambda: f"[h{i}]" in open(pod_index).read(), timeout=30, what="synced edit")
+            wait_for(lambda: _refused(remote), timeout=10, what="old server stopped")
+            outcomes.append(_get(local))  # sent while nothing listens in the pod
+            wait_for(lambda: not _refused(remote), timeout=30, what="new server")
+        if hold:
+            assert all(isinstance(o, str) and f"[h{i}]" in o for i, o in enumerate(outcomes)), outcomes
+        else:
+            assert all(not isinstance(o, str) for o in outcomes), outcomes
+    finally:
+        _stop(dev)
     lk.run(["purge"], proj)
