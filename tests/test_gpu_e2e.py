@@ -80,8 +80,23 @@ def test_rocm_pytorch_pod_trains_on_gpu(tmp_path):
         assert "gfx950" in m.group(3), report
         if m.group(2) == "devspace":
             assert re.search(r"MFMA self-test err 0(\.0)?(,|$)", m.group(3)), report
+        workload = []
+        if prof:
+            import psutil
+
+            for pr in psutil.process_iter(["cmdline"]):
+                try:
+                    if "devspace_amd.runner" in " ".join(pr.info["cmdline"] or []) and \
+                            pr.environ().get("DEVSPACE_CONTAINER_ROOT") == root:
+                        workload.append(pr)
+                except (psutil.Error, OSError):
+                    pass
+            assert workload, "profiled runner process not found"
         lk.run(["purge"], proj, timeout=120)
         if prof:
+            # the trace is written when the runner exits (SIGTERM from the pod deletion)
+            _, alive = psutil.wait_procs(workload, timeout=90)
+            assert not alive, alive
             dbs = _wait(lambda: glob.glob(os.path.join(prof, "**", "*.db"), recursive=True) or
                         glob.glob(os.path.join(prof, "**", "*kernel_stats.csv"), recursive=True), 60,
                         "the pod's rocprofv3 output")
