@@ -9,12 +9,16 @@ wss, client certificates) as every real cluster does (`--transport plain` for ws
 
   value (timed, K steps) — BASELINE configs[0], the metric's named config: examples/quickstart
      (Node.js) under `devspace dev`, its container running watch.js (restart on change, as
-     nodemon in the reference's quickstart). One step = edit index.js locally -> synced into the
-     pod -> node restarts -> an HTTP GET through devspace's port-forward returns the new text.
+     nodemon in the reference's quickstart: a fresh node process per edit, taken from a pool of
+     pre-booted standbys). One step = edit index.js locally -> synced into the pod -> node
+     restarts -> an HTTP GET through devspace's port-forward returns the new text (a request
+     sent while the app restarts is held by the port-forward and answered by the new server).
      Edits land after a random 0-10 ms think time.
-  reference_equivalent (same box): the same loop with the reference's sync protocol and waits
-     (compat shell scripts, 600 ms batching, 1.3 s poll; 1 s pod-discovery sleeps) — BASELINE.md
-     "How the rebuild will be compared" (the reference publishes no numbers: vs_baseline null).
+  reference_equivalent (same box): the same app and loop with the reference's behaviour: its
+     sync protocol and waits (compat shell scripts, 600 ms batching, 1.3 s poll; 1 s
+     pod-discovery sleeps), cold restarts as nodemon does (WATCH_STANDBY=0) and kubectl's
+     port-forward (connections refused mid-restart are dropped) — BASELINE.md "How the rebuild
+     will be compared" (the reference publishes no numbers: vs_baseline null).
   deploy: `devspace deploy` of the quickstart on a fresh cluster, cold and forced-warm, with phase
      times and TCP/TLS counts, and the same with reference timing (1 s pod sleeps, 5 s rollout
      polls, no kept-alive connections, compat sync). `control_plane_only`: the bundled Docker
@@ -312,6 +316,8 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
     values = os.path.join(proj, "chart", "values.yaml")
     v = yaml.safe_load(open(values))
     v["components"][0]["containers"][0]["env"] = [{"name": "PORT", "value": str(remote)}]
+    if reference:  # nodemon's cold restarts
+        v["components"][0]["containers"][0]["env"].append({"name": "WATCH_STANDBY", "value": "0"})
     open(values, "w").write(yaml.safe_dump(v))
 
     cluster = LocalCluster(os.path.join(base, "cluster"), gpus=0, tls=tls).start()
@@ -724,7 +730,8 @@ def report(args, nproc, tls, ms_total, qs, extras):
             "global_batch": None,  # a CLI benchmark: one edit per step, no batch
             "seq_len": None,
             "parallelism": f"none (CLI); GPU pod extra: dp{nproc}",
-            "sample": "edit index.js -> synced into the pod -> node restarts (watch.js, as nodemon) -> "
+            "sample": "edit index.js -> synced into the pod -> node restarts (watch.js: fresh process per edit "
+                      "from pre-booted standbys) -> "
                       "HTTP GET through devspace's port-forward returns the new text",
             "path": "devspace dev (exec-WebSocket sync + port-forward) on the bundled local cluster",
             "transport": "https + wss, mTLS" if tls else "plain http + ws",
@@ -738,8 +745,9 @@ def report(args, nproc, tls, ms_total, qs, extras):
     if _ok(ref):
         rp50 = _pct(ref["reload_ms"], 0.5)
         out["reference_equivalent"] = {
-            "what": "the same quickstart loop with the reference's sync protocol (compat shell scripts, 600 ms "
-                    "batching, 1.3 s poll) and waits (1 s pod-discovery sleeps): BASELINE.md's same-box column",
+            "what": "the same quickstart app and loop with the reference's sync protocol (compat shell scripts, "
+                    "600 ms batching, 1.3 s poll), waits (1 s pod-discovery sleeps), cold nodemon-style restarts "
+                    "and kubectl's port-forward (no hold): BASELINE.md's same-box column",
             "p50_ms": round(rp50, 2),
             "sync_p50_ms": round(_pct(ref["sync_ms"], 0.5), 2),
             "n": len(ref["reload_ms"]),
