@@ -20,6 +20,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <map>
 #include <climits>
 #include <cstdio>
 #include <cstring>
@@ -185,6 +186,68 @@ SSL_CTX* make_ctx(const TlsOptions& t) {
   return ctx;
 }
 
+// Client TLS contexts are shared per credential set (CA, client cert/key, verify mode): the
+// PEM parsing happens once, and the context carries a client session cache so a new
+// connection to the same API server resumes the last session (TLS 1.3 ticket / 1.2 session
+// id) instead of a full handshake with certificate verification on both sides — every
+// exec / attach / port-forward stream is a new connection. Off with DEVSPACE_REFERENCE_TIMING
+// (client-go configures no session cache).
+namespace {
+std::mutex g_tls_mu;
+std::map<std::string, SSL_CTX*> g_ctx_cache;          // credential digest -> ctx (one ref held)
+std::map<std::string, SSL_SESSION*> g_sessions;       // digest|peer -> latest resumable session
+
+int new_session_cb(SSL* ssl, SSL_SESSION* sess) {
+  auto* key = static_cast<const std::string*>(SSL_get_app_data(ssl));
+  if (!key || !SSL_SESSION_is_resumable(sess)) return 0;
+  std::lock_guard<std::mutex> g(g_tls_mu);
+  auto it = g_sessions.find(*key);
+  if (it != g_sessions.end()) SSL_SESSION_free(it->second);
+  g_sessions[*key] = sess;
+  return 1;  // we keep the reference
+}
+
+// A referenced context for these options (caller frees with SSL_CTX_free) and its cache key.
+SSL_CTX* shared_ctx(const TlsOptions& t, std::string* digest) {
+  std::string material = std::string(t.insecure ? "1" : "0") + "\n" + t.ca_pem + "\n" + t.cert_pem + "\n" + t.key_pem;
+  unsigned char md[SHA256_DIGEST_LENGTH];
+  SHA256((const unsigned char*)material.data(), material.size(), md);
+  *digest = std::string((const char*)md, sizeof(md));
+  std::lock_guard<std::mutex> g(g_tls_mu);
+  auto it = g_ctx_cache.find(*digest);
+  if (it == g_ctx_cache.end()) {
+    SSL_CTX* ctx = make_ctx(t);
+    SSL_CTX_set_session_cache_mode(ctx, SSL_SESS_CACHE_CLIENT | SSL_SESS_CACHE_NO_INTERNAL_STORE);
+    SSL_CTX_sess_set_new_cb(ctx, new_session_cb);
+    if (g_ctx_cache.size() >= 16) {  // bounded: credential sets rarely change within a process
+      for (auto& kv : g_ctx_cache) SSL_CTX_free(kv.second);
+      g_ctx_cache.clear();
+    }
+    it = g_ctx_cache.emplace(*digest, ctx).first;
+  }
+  SSL_CTX_up_ref(it->second);
+  return it->second;
+}
+
+std::string peer_key(int fd) {
+  sockaddr_storage ss{};
+  socklen_t len = sizeof(ss);
+  if (getpeername(fd, (sockaddr*)&ss, &len) != 0) return "";
+  char host[INET6_ADDRSTRLEN] = {0};
+  int port = 0;
+  if (ss.ss_family == AF_INET) {
+    inet_ntop(AF_INET, &((sockaddr_in*)&ss)->sin_addr, host, sizeof(host));
+    port = ntohs(((sockaddr_in*)&ss)->sin_port);
+  } else if (ss.ss_family == AF_INET6) {
+    inet_ntop(AF_INET6, &((sockaddr_in6*)&ss)->sin6_addr, host, sizeof(host));
+    port = ntohs(((sockaddr_in6*)&ss)->sin6_port);
+  } else {
+    return "unix";
+  }
+  return std::string(host) + ":" + std::to_string(port);
+}
+}  // namespace
+
 // TLS over a non-blocking socket. SSL_read/SSL_write run under ssl_mu_ only for the duration
 // of the call; waiting (poll) happens with no lock held, so a reader blocked on an idle
 // stream never holds up a concurrent writer. A writer that makes OpenSSL buffer incoming
@@ -197,9 +260,18 @@ class TlsConn : public Conn {
       int fl = fcntl(fd_, F_GETFL);
       fcntl(fd_, F_SETFL, fl | O_NONBLOCK);
       wake_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
-      ctx_ = make_ctx(t);
+      bool resume = !reference_timing();
+      std::string digest;
+      ctx_ = resume ? shared_ctx(t, &digest) : make_ctx(t);
       ssl_ = SSL_new(ctx_);
       if (!ssl_) throw NetError("SSL_new failed");
+      if (resume) {
+        session_key_ = digest + "|" + t.server_name + "|" + peer_key(fd_);
+        SSL_set_app_data(ssl_, &session_key_);
+        std::lock_guard<std::mutex> g(g_tls_mu);
+        auto it = g_sessions.find(session_key_);
+        if (it != g_sessions.end()) SSL_set_session(ssl_, it->second);
+      }
       SSL_set_mode(ssl_, SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
       SSL_set_fd(ssl_, fd_);
       if (!t.server_name.empty()) {
@@ -234,6 +306,7 @@ class TlsConn : public Conn {
         if (left == 0 || wait_fd(fd_, ev, left) == 0) throw NetError("tls handshake timed out");
       }
       stats().tls_handshakes++;
+      if (SSL_session_reused(ssl_)) stats().tls_resumed++;
     } catch (...) {
       cleanup();
       throw;
@@ -349,6 +422,7 @@ class TlsConn : public Conn {
   }
   int fd_;
   int wake_ = -1;
+  std::string session_key_;  // SSL app data: where new_session_cb files this peer's tickets
   SSL_CTX* ctx_ = nullptr;
   SSL* ssl_ = nullptr;
   std::mutex rmu_, wmu_, ssl_mu_;
@@ -921,8 +995,9 @@ std::string websocket_accept(const std::string& key) {
 }
 
 std::unique_ptr<WebSocket> WebSocket::connect(HttpClient& http, const std::string& path,
-                                              const std::vector<std::string>& protocols, int timeout_ms) {
-  auto c = http.connect();
+                                              const std::vector<std::string>& protocols, int timeout_ms,
+                                              std::unique_ptr<Conn> conn) {
+  auto c = conn && !conn->stale() ? std::move(conn) : http.connect();
   std::string key = base64_encode(random_string(16));
   Request r;
   r.method = "GET";

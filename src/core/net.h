@@ -42,6 +42,7 @@ struct TlsOptions {
 struct Stats {
   std::atomic<int64_t> tcp_dials{0};
   std::atomic<int64_t> tls_handshakes{0};
+  std::atomic<int64_t> tls_resumed{0};  // of those, abbreviated (session resumption)
   std::atomic<int64_t> requests{0};
   std::atomic<int64_t> reused{0};
   std::atomic<int64_t> proxied{0};
@@ -150,9 +151,11 @@ class WebSocket {
  public:
   static constexpr uint64_t kMaxFrame = 64ull << 20;  // refuse larger peer frames
   // Performs the client handshake on `path` with the given subprotocols; throws on failure.
+  // `conn`: an already dialed (TLS-established) connection to the endpoint to upgrade instead of
+  // dialing a new one; ignored when stale.
   static std::unique_ptr<WebSocket> connect(HttpClient& http, const std::string& path,
                                             const std::vector<std::string>& protocols,
-                                            int timeout_ms = 30000);
+                                            int timeout_ms = 30000, std::unique_ptr<Conn> conn = nullptr);
   explicit WebSocket(std::unique_ptr<Conn> c, std::string leftover = "");
   ~WebSocket();
   enum Op { Cont = 0, Text = 1, Binary = 2, Close = 8, Ping = 9, Pong = 10 };

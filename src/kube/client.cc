@@ -760,15 +760,17 @@ std::unique_ptr<ExecSession> Client::attach(const std::string& ns, const std::st
   return std::make_unique<ExecSession>(std::move(ws), tty);
 }
 
-std::unique_ptr<net::WebSocket> Client::portforward(const std::string& ns, const std::string& pod, int port) {
+std::unique_ptr<net::WebSocket> Client::portforward(const std::string& ns, const std::string& pod, int port,
+                                                    std::unique_ptr<net::Conn> spare) {
   std::string path = "/api/v1/namespaces/" + ns + "/pods/" + pod + "/portforward?ports=" + std::to_string(port);
-  return ws_connect(path, {"v4.channel.k8s.io", "portforward.k8s.io"});
+  return ws_connect(path, {"v4.channel.k8s.io", "portforward.k8s.io"}, std::move(spare));
 }
 
-std::unique_ptr<net::WebSocket> Client::ws_connect(const std::string& path, const std::vector<std::string>& protocols) {
+std::unique_ptr<net::WebSocket> Client::ws_connect(const std::string& path, const std::vector<std::string>& protocols,
+                                                   std::unique_ptr<net::Conn> spare) {
   ensure_fresh_credentials();
   try {
-    return net::WebSocket::connect(http_, path, protocols);
+    return net::WebSocket::connect(http_, path, protocols, 30000, std::move(spare));
   } catch (const net::UpgradeError& e) {
     if (e.status != 401 || !refresh_after_unauthorized()) throw;
   }

@@ -132,7 +132,9 @@ class Client {
                                     const std::vector<std::string>& cmd, bool tty, bool stdin = true);
   std::unique_ptr<ExecSession> attach(const std::string& ns, const std::string& pod, const std::string& container,
                                       bool tty, bool stdin = false);
-  std::unique_ptr<net::WebSocket> portforward(const std::string& ns, const std::string& pod, int port);
+  // `spare`: a pre-dialed connection to the API server to upgrade (saves the TLS handshake).
+  std::unique_ptr<net::WebSocket> portforward(const std::string& ns, const std::string& pod, int port,
+                                              std::unique_ptr<net::Conn> spare = nullptr);
 
   net::HttpClient& http() { return http_; }
 
@@ -144,7 +146,8 @@ class Client {
  private:
   void refresh_exec_credentials();
   void apply_auth_locked();
-  std::unique_ptr<net::WebSocket> ws_connect(const std::string& path, const std::vector<std::string>& protocols);
+  std::unique_ptr<net::WebSocket> ws_connect(const std::string& path, const std::vector<std::string>& protocols,
+                                             std::unique_ptr<net::Conn> spare = nullptr);
   RestConfig cfg_;
   int local_cluster_ = -1;  // is_local_cluster() cache
   net::HttpClient http_;

@@ -17,6 +17,7 @@ static void emit_net_stats() {
   ds::trace::emit("net", ds::trace::now_us(), 0,
                   {{"tcp_dials", std::to_string(s.tcp_dials.load())},
                    {"tls_handshakes", std::to_string(s.tls_handshakes.load())},
+                   {"tls_resumed", std::to_string(s.tls_resumed.load())},
                    {"requests", std::to_string(s.requests.load())},
                    {"reused", std::to_string(s.reused.load())},
                    {"proxied", std::to_string(s.proxied.load())}});

@@ -23,6 +23,13 @@
 namespace ds {
 namespace services {
 
+static long mono_ms() {
+  return (long)std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+
 // ---------------------------------------------------------------- selection
 
 Target resolve_target(const Value& cfg, const std::string& selector_flag, const std::string& label_selector_flag,
@@ -222,7 +229,54 @@ static int listen_on(int family, const std::string& addr, int port) {
   return fd;
 }
 
+void PortForwarder::spare_loop() {
+  const long kMaxAgeMs = 30000;  // below API-server idle timeouts; re-dialed after that
+  std::unique_lock<std::mutex> lk(spare_mu_);
+  while (!stop_) {
+    while (!spares_.empty() && mono_ms() - spares_.front().first > kMaxAgeMs) spares_.pop_front();
+    if ((int)spares_.size() < want_spares_) {
+      lk.unlock();
+      std::unique_ptr<net::Conn> c;
+      try {
+        c = k_->http().connect();
+      } catch (const std::exception&) {
+      }
+      lk.lock();
+      if (c) {
+        spares_.emplace_back(mono_ms(), std::move(c));
+      } else {
+        spare_cv_.wait_for(lk, std::chrono::seconds(1), [this] { return stop_.load(); });
+      }
+      continue;
+    }
+    spare_cv_.wait_for(lk, std::chrono::seconds(5),
+                       [this] { return stop_.load() || (int)spares_.size() < want_spares_; });
+  }
+  spares_.clear();
+}
+
+std::unique_ptr<net::Conn> PortForwarder::take_spare() {
+  std::unique_ptr<net::Conn> c;
+  {
+    std::lock_guard<std::mutex> g(spare_mu_);
+    while (!spares_.empty() && !c) {
+      c = std::move(spares_.front().second);
+      spares_.pop_front();
+      if (c->stale()) c.reset();
+    }
+  }
+  spare_cv_.notify_one();
+  if (c) spares_used_++;
+  return c;
+}
+
 void PortForwarder::start() {
+  if (const char* v = std::getenv("DEVSPACE_PORTFORWARD_SPARES")) {
+    want_spares_ = std::max(0, std::min(8, std::atoi(v)));
+  } else {
+    want_spares_ = reference_timing() ? 0 : 2;  // the reference dials every stream
+  }
+  if (want_spares_ > 0) spare_thread_ = std::thread([this] { spare_loop(); });
   for (size_t i = 0; i < ports_.size(); ++i) {
     std::string bind = i < addrs_.size() ? addrs_[i] : "";
     auto addrs = listen_addresses(bind);
@@ -300,7 +354,7 @@ std::unique_ptr<net::WebSocket> PortForwarder::open_stream(int remote_port) {
   }
   std::string name = pod.at_path("metadata.name").as_string();
   try {
-    return k_->portforward(ns_, name, remote_port);
+    return k_->portforward(ns_, name, remote_port, take_spare());
   } catch (const std::exception& e) {
     if (selector_.empty() || stop_) throw;
     // the pod is gone or not running any more: follow the selector to its newest pod
@@ -324,12 +378,6 @@ std::unique_ptr<net::WebSocket> PortForwarder::open_stream(int remote_port) {
 // container, so the client's bytes can be replayed on a new stream.
 bool is_dial_refused(const std::string& err) { return contains(to_lower(err), "connection refused"); }
 
-static long mono_ms() {
-  return (long)std::chrono::duration_cast<std::chrono::milliseconds>(
-             std::chrono::steady_clock::now().time_since_epoch())
-      .count();
-}
-
 int port_forward_hold_ms() {
   if (const char* v = std::getenv("DEVSPACE_PORTFORWARD_HOLD_MS")) return std::max(0, std::atoi(v));
   return reference_timing() ? 0 : 3000;
@@ -339,15 +387,14 @@ int port_forward_hold_ms() {
 // (hot reload), its port refuses connections for a moment; kubectl then drops the client's
 // connection and a browser shows an error. Here, as long as nothing came back from the pod yet
 // and the pod-side connect was refused, the connection is held and its bytes replayed on a
-// new stream (backoff 2 -> 25 ms) for up to hold_ms_, so a request sent mid-restart is
-// answered by the new server as soon as it listens.
+// new stream (every ms for the first 100 ms, then backing off to 25 ms) for up to hold_ms_, so
+// a request sent mid-restart is answered by the new server as soon as it listens.
 void PortForwarder::handle(Conn* conn, int remote_port) {
   int cfd = conn->fd;
   const long hold_deadline = mono_ms() + hold_ms_;
   std::string replay;           // client bytes of this connection, kept while no reply arrived
   bool replayable = hold_ms_ > 0;
   bool client_eof = false;
-  int backoff_ms = 2;
   while (!stop_) {
     std::unique_ptr<net::WebSocket> ws;
     try {
@@ -420,8 +467,11 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
     ::close(wake[0]);
     ::close(wake[1]);
     if (refused && replayable && !stop_ && mono_ms() < hold_deadline) {
-      std::this_thread::sleep_for(std::chrono::milliseconds(backoff_ms));
-      backoff_ms = std::min(25, backoff_ms * 2);
+      // a hot-reloading app is back within tens of ms: retry at once for the first 100 ms
+      // (each attempt is a stream open, itself ~a ms), then back off to 25 ms
+      long held = mono_ms() - (hold_deadline - hold_ms_);
+      int delay = held < 100 ? 1 : held < 1000 ? 5 : 25;
+      std::this_thread::sleep_for(std::chrono::milliseconds(delay));
       held_retries_++;
       continue;
     }
@@ -435,6 +485,11 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
 
 void PortForwarder::close() {
   if (stop_.exchange(true)) return;
+  {
+    std::lock_guard<std::mutex> g(spare_mu_);  // no lost wake-up between its check and wait
+  }
+  spare_cv_.notify_all();
+  if (spare_thread_.joinable()) spare_thread_.join();
   for (auto& t : threads_)
     if (t.joinable()) t.join();
   for (int fd : listeners_) ::close(fd);

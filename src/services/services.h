@@ -3,6 +3,8 @@
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -67,6 +69,8 @@ class PortForwarder {
   int reselections() const { return reselections_; }
   // Connections replayed on a new stream because the pod refused them mid-restart.
   int held_retries() const { return held_retries_; }
+  // Streams opened on a pre-dialed connection.
+  int spares_used() const { return spares_used_; }
   size_t active_connections();
 
  private:
@@ -76,6 +80,11 @@ class PortForwarder {
     std::atomic<bool> done{false};
   };
   void accept_loop(int lfd, int remote_port);
+  // Pre-dialed API-server connections (TCP + TLS done): a new local connection only pays the
+  // WebSocket upgrade round trip, not a handshake — kubectl gets the same by multiplexing
+  // its streams over one SPDY connection.
+  void spare_loop();
+  std::unique_ptr<net::Conn> take_spare();
   void handle(Conn* c, int remote_port);
   void reap(bool all);
   std::unique_ptr<net::WebSocket> open_stream(int remote_port);
@@ -92,6 +101,12 @@ class PortForwarder {
   std::atomic<bool> stop_{false};
   std::atomic<int> reselections_{0};
   std::atomic<int> held_retries_{0};
+  std::mutex spare_mu_;
+  std::condition_variable spare_cv_;
+  std::deque<std::pair<long, std::unique_ptr<net::Conn>>> spares_;  // (dialed at ms, conn)
+  std::thread spare_thread_;
+  int want_spares_ = 0;
+  std::atomic<int> spares_used_{0};
   int hold_ms_ = port_forward_hold_ms();
 };
 

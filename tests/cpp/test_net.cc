@@ -1,6 +1,9 @@
 // HTTP client behaviour against scripted local servers (keep-alive retry rules, chunked request
 // bodies) and the NSS-free resolver's pieces.
 #include <arpa/inet.h>
+#include <openssl/err.h>
+#include <openssl/pem.h>
+#include <openssl/ssl.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -14,6 +17,7 @@
 #include "core/net.h"
 #include "core/resolve.h"
 #include "core/strutil.h"
+#include "deploy/sprig_crypto.h"
 #include "services/services.h"
 #include "testing.h"
 
@@ -249,4 +253,50 @@ TEST(port_forward_listen_addresses) {
   EXPECT_EQ(services::listen_addresses("[::]")[0].second, std::string("::"));
   EXPECT_EQ(services::listen_addresses("0.0.0.0")[0].first, AF_INET);
   EXPECT_EQ(services::listen_addresses("localhost").size(), (size_t)2);
+}
+
+// A new connection to the same server resumes the previous TLS session (every exec / attach /
+// port-forward stream is a new connection); the handshake count stays, resumed ones are
+// counted apart.
+TEST(tls_client_resumes_sessions) {
+  Value cert = sprig::gen_self_signed_cert("127.0.0.1", {"127.0.0.1"}, {}, 1);
+  SSL_CTX* sctx = SSL_CTX_new(TLS_server_method());
+  const std::string cert_pem = cert.get("Cert").as_string(), key_pem = cert.get("Key").as_string();
+  BIO* cb = BIO_new_mem_buf(cert_pem.data(), (int)cert_pem.size());
+  X509* x = PEM_read_bio_X509(cb, nullptr, nullptr, nullptr);
+  BIO* kb = BIO_new_mem_buf(key_pem.data(), (int)key_pem.size());
+  EVP_PKEY* k = PEM_read_bio_PrivateKey(kb, nullptr, nullptr, nullptr);
+  EXPECT_TRUE(SSL_CTX_use_certificate(sctx, x) == 1 && SSL_CTX_use_PrivateKey(sctx, k) == 1);
+  ScriptedServer srv([&](int fd, int) {
+    SSL* ssl = SSL_new(sctx);
+    SSL_set_fd(ssl, fd);
+    if (SSL_accept(ssl) == 1) {
+      std::string buf;
+      char tmp[4096];
+      while (buf.find("\r\n\r\n") == std::string::npos) {
+        int n = SSL_read(ssl, tmp, sizeof(tmp));
+        if (n <= 0) break;
+        buf.append(tmp, (size_t)n);
+      }
+      std::string r = "HTTP/1.1 200 OK\r\nContent-Length: 2\r\nConnection: close\r\n\r\nok";
+      SSL_write(ssl, r.data(), (int)r.size());
+      SSL_shutdown(ssl);
+    }
+    SSL_free(ssl);
+  });
+  net::TlsOptions t;
+  t.ca_pem = cert_pem;
+  t.server_name = "127.0.0.1";
+  net::HttpClient c("https://127.0.0.1:" + std::to_string(srv.port), t);
+  c.set_keepalive(false);  // a new connection per request
+  int64_t hs0 = net::stats().tls_handshakes.load(), res0 = net::stats().tls_resumed.load();
+  for (int i = 0; i < 3; ++i) EXPECT_EQ(c.get("/x").body, std::string("ok"));
+  EXPECT_EQ(net::stats().tls_handshakes.load() - hs0, 3);
+  EXPECT_EQ(net::stats().tls_resumed.load() - res0, 2);  // all but the first
+  X509_free(x);
+  EVP_PKEY_free(k);
+  BIO_free(cb);
+  BIO_free(kb);
+  srv.stop = true;
+  SSL_CTX_free(sctx);
 }
