@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Where the quickstart edit -> response time goes (the bench headline's loop, instrumented).
+
+Runs bench.quickstart_loop with timestamped copies of the example's watch.js / index.js and
+prints per-edit phases on one clock (ms): edit -> synced into the pod, -> watcher saw the
+change, -> old server killed, -> new process handed the script (old one exited), -> new
+server listening, -> response through the port-forward.
+
+    python scripts/qs_breakdown.py [--steps 20] [--warmup 3]
+"""
+import argparse
+import json
+import os
+import shutil
+import statistics
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    trace = tempfile.mktemp(prefix="qs-trace-")
+    real_copytree = shutil.copytree
+
+    def copytree(src, dst, *args, **kw):
+        r = real_copytree(src, dst, *args, **kw)
+        if str(getattr(src, "path", src)).endswith(os.path.join("examples", "quickstart")):
+            t = "const T = (m) => require('fs').appendFileSync(%s, m + ' ' + Date.now() + '\\n');\n" % json.dumps(trace)
+            w = os.path.join(dst, "watch.js")
+            s = open(w).read()
+            s = s.replace("const {spawn} = require('child_process');", "const {spawn} = require('child_process');\n" + t)
+            s = s.replace("  restarting = true;\n  child.kill('SIGTERM');", "  restarting = true;\n  T('kill');\n  child.kill('SIGTERM');")
+            s = s.replace("    child.send({script});", "    T('handoff');\n    child.send({script});")
+            s = s.replace("  if (!name || ignored.test(name)", "  T('event');\n  if (!name || ignored.test(name)")
+            open(w, "w").write(s)
+            i = os.path.join(dst, "index.js")
+            s = open(i).read()
+            s = s.replace("}).listen(port, () => console.log(",
+                          "}).listen(port, () => require('fs').appendFileSync(%s, 'listening ' + Date.now() + '\\n') || "
+                          "console.log(" % json.dumps(trace))
+            open(i, "w").write(s)
+        return r
+
+    shutil.copytree = copytree
+    marks = []
+    orig_edit, orig_wait, orig_get = bench._qs_edit, bench._wait_file_contains, bench._http_get
+
+    def edit(path, marker):
+        marks.append({"edit": time.time() * 1000})
+        return orig_edit(path, marker)
+
+    def wait(*args, **kw):
+        r = orig_wait(*args, **kw)
+        marks[-1]["synced"] = time.time() * 1000
+        return r
+
+    def get(port, timeout=2.0):
+        body = orig_get(port, timeout)
+        if marks and body and "got" not in marks[-1] and "[q" in body:
+            m = body.split("[", 1)[1].split("]", 1)[0]
+            if m == f"q{len(marks) - 1}" + ("_" * ((len(marks) - 1) % 2)):
+                marks[-1]["got"] = time.time() * 1000
+        return body
+
+    bench._qs_edit, bench._wait_file_contains, bench._http_get = edit, wait, get
+    with tempfile.TemporaryDirectory() as d:
+        r = bench.quickstart_loop(d, a.steps, a.warmup)
+    events = []
+    for line in open(trace):
+        k, v = line.split()
+        events.append((float(v), k))
+    rows = []
+    for m in marks[a.warmup:]:
+        after = [(t, k) for t, k in events if t >= m["edit"] - 1]
+        first = {}
+        for t, k in after:
+            first.setdefault(k, t)
+        row = {"sync": m.get("synced", 0) - m["edit"]}
+        for k in ("event", "kill", "handoff", "listening"):
+            if k in first:
+                row[k] = first[k] - m["edit"]
+        if "got" in m:
+            row["response"] = m["got"] - m["edit"]
+        rows.append(row)
+    keys = ["sync", "event", "kill", "handoff", "listening", "response"]
+    print("ms after the edit (p50 over %d edits): " % len(rows) +
+          ", ".join("%s %.2f" % (k, statistics.median([x[k] for x in rows if k in x])) for k in keys
+                    if any(k in x for x in rows)))
+    print("bench p50 %.2f ms" % statistics.median(r["reload_ms"]))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"rows": rows, "reload_ms": r["reload_ms"]}, f, indent=1)
+    os.unlink(trace)
+
+
+if __name__ == "__main__":
+    main()
