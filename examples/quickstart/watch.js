@@ -13,9 +13,11 @@
 // processes are kept booted (V8 + core modules initialised, nothing of the app loaded). A
 // restart hands the script to a booted standby, which loads it then — from disk, after the
 // edit — as its main module (`require.main === module` holds), and a replacement boots in the
-// background. That takes node's start-up (tens of ms) out of every edit -> response. Two
+// background. That takes node's start-up (tens of ms) out of every edit -> response. Four
 // standbys by default, so back-to-back saves (format-on-save, quick fix-ups) still find one
-// booted; WATCH_STANDBY=N sets the count, 0 gives plain cold restarts.
+// that finished booting a while ago (a just-booted one measured ~10 ms slower to listen with
+// two standbys: profiles/r3_qs_standby_probe.txt); WATCH_STANDBY=N sets the count, 0 gives
+// plain cold restarts.
 const {spawn} = require('child_process');
 const fs = require('fs');
 const path = require('path');
@@ -23,14 +25,27 @@ const path = require('path');
 const script = path.resolve(process.argv[2] || 'index.js');
 const dir = path.dirname(script);
 const ignored = /(^|\/)(node_modules|\.git|\.devspace)(\/|$)|\.sw.$|~$/;
-const nStandby = Math.max(0, parseInt(process.env.WATCH_STANDBY || '2', 10) || 0);
+const nStandby = Math.max(0, parseInt(process.env.WATCH_STANDBY || '4', 10) || 0);
 // The standby's whole program: load the core modules a server needs (node loads them lazily,
 // and they are shared, stateless code: nothing of the app), wait for the go message, drop the
 // IPC channel (the app must not see a parent channel) and run the script as the main module.
+// `cluster` and `child_process` are in the list because net's listen() loads them on first
+// use. The boot also warms the runtime paths every server takes once: it compiles a module
+// from a string (the CommonJS wrapper/compiler), and it listens on an ephemeral loopback port
+// and closes it again (libuv's TCP setup and net's listen path). Measured with node 12, the
+// first listen() of a booted process took 6-9 ms to reach its callback, and 0.4 ms after this
+// warm-up (scripts/node_boot_probe.py). Nothing of the app runs before the go message.
 const PRELOAD = ['http', 'https', 'net', 'url', 'querystring', 'stream', 'events', 'util', 'crypto',
-                 'zlib', 'os', 'fs', 'path', 'buffer', 'string_decoder', 'timers', 'dns'];
+                 'zlib', 'os', 'fs', 'path', 'buffer', 'string_decoder', 'timers', 'dns', 'cluster',
+                 'child_process'];
+const WARM = "const M = require('module'); const w = new M('/.watch-warm.js'); " +
+    "w.filename = '/.watch-warm.js'; w.paths = []; w._compile('module.exports = 0;', '/.watch-warm.js'); " +
+    "const srv = require('net').createServer(); srv.on('error', ready); " +
+    "srv.listen(0, () => srv.close(ready));\n";
 const BOOT = `for (const m of ${JSON.stringify(PRELOAD)}) { try { require(m); } catch (e) {} }\n` +
-    "process.send('ready'); process.once('message', (m) => { " +
+    "let sent = false; function ready() { if (!sent) { sent = true; process.send('ready'); } }\n" +
+    `try { ${WARM} } catch (e) { ready(); }\n` +
+    "process.once('message', (m) => { " +
     "process.argv[1] = m.script; process.disconnect(); " +
     "for (const k of ['send', 'disconnect', 'connected', 'channel']) { try { delete process[k]; } catch (e) {} } " +
     "require('module').runMain(); });";

@@ -25,6 +25,10 @@ def main():
     print("node -e 0: p50 %.1f ms" % statistics.median(t))
     src = open(os.path.join(ROOT, "examples", "quickstart", "watch.js")).read()
     preload = re.search(r"const PRELOAD = (\[[^\]]*\]);", src, re.S).group(1)
+    # the boot's warm-up statement (a JS string expression in watch.js), evaluated by node
+    warm_expr = re.search(r"const WARM = (.*?);\n", src, re.S).group(1)
+    warm = subprocess.run([NODE, "-e", "process.stdout.write(%s)" % warm_expr], capture_output=True,
+                          text=True).stdout.replace("ready", "go")
     for label, mods in (("full preload", preload), ("no preload", "[]")):
         boot = ("const T0 = Date.now(); for (const m of %s) { try { require(m); } catch (e) {} }\n"
                 "process.stdout.write('ready ' + (Date.now() - T0) + '\\n');" % mods)
@@ -41,15 +45,17 @@ def main():
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    for label, mods in (("full preload", preload), ("no preload", "[]")):
+    for label, mods, warmup in (("full preload + warm-up", preload, warm), ("full preload", preload, ""),
+                                ("no preload", "[]", "")):
         t = []
         for _ in range(10):
             code = ("for (const m of %s) { try { require(m); } catch (e) {} }\n"
+                    "function go() {}\n" % mods) + warmup + (
                     "process.stdin.once('data', () => { const t0 = Date.now(); process.argv[1] = %r; "
                     "const http = require('http'); const L = http.Server.prototype.listen; "
                     "http.Server.prototype.listen = function (...a) { const cb = a[a.length - 1]; "
                     "a[a.length - 1] = () => { process.stderr.write('L ' + (Date.now() - t0) + '\\n'); process.exit(0); }; "
-                    "return L.apply(this, a); }; require('module').runMain(); });" % (mods, os.path.join(d, "index.js")))
+                    "return L.apply(this, a); }; require('module').runMain(); });" % os.path.join(d, "index.js"))
             p = subprocess.Popen([NODE, "-e", code], stdin=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                                  env=dict(os.environ, PORT=str(port)))
             time.sleep(0.3)

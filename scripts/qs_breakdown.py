@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--out", default="")
+    ap.add_argument("--standby", type=int, default=None, help="watch.js standby count (default: its own)")
     a = ap.parse_args()
     trace = tempfile.mktemp(prefix="qs-trace-")
     real_copytree = shutil.copytree
@@ -41,6 +42,9 @@ def main():
             s = s.replace("  restarting = true;\n  child.kill('SIGTERM');", "  restarting = true;\n  T('kill');\n  child.kill('SIGTERM');")
             s = s.replace("    child.send({script});", "    T('handoff');\n    child.send({script});")
             s = s.replace("  if (!name || ignored.test(name)", "  T('event');\n  if (!name || ignored.test(name)")
+            if a.standby is not None:
+                s = s.replace("process.env.WATCH_STANDBY || '2'", "'%d'" % a.standby)
+            s = s.replace("  console.log('[watch] started gen='", "  T(s && s.ready ? 'ready' : 'booting');\n  console.log('[watch] started gen='")
             open(w, "w").write(s)
             i = os.path.join(dst, "index.js")
             s = open(i).read()
@@ -85,7 +89,7 @@ def main():
         for t, k in after:
             first.setdefault(k, t)
         row = {"sync": m.get("synced", 0) - m["edit"]}
-        for k in ("event", "kill", "handoff", "listening"):
+        for k in ("event", "kill", "handoff", "listening", "ready", "booting"):
             if k in first:
                 row[k] = first[k] - m["edit"]
         if "got" in m:
@@ -95,7 +99,9 @@ def main():
     print("ms after the edit (p50 over %d edits): " % len(rows) +
           ", ".join("%s %.2f" % (k, statistics.median([x[k] for x in rows if k in x])) for k in keys
                     if any(k in x for x in rows)))
-    print("bench p50 %.2f ms" % statistics.median(r["reload_ms"]))
+    print("bench p50 %.2f ms p90 %.2f ms; handoffs to a booted standby: %d of %d" % (
+        statistics.median(r["reload_ms"]), bench._pct(r["reload_ms"], 0.9), sum(1 for x in rows if x.get("ready")),
+        len(rows)))
     if a.out:
         with open(a.out, "w") as f:
             json.dump({"rows": rows, "reload_ms": r["reload_ms"]}, f, indent=1)
