@@ -421,3 +421,47 @@ def test_runner_reloads_edited_helper_module(tmp_path):
     finally:
         proc.terminate()
         proc.wait(10)
+
+
+def test_change_feed_ignores_sync_temp_file(tmp_path):
+    """The in-pod sync helper writes `<name>.devspace-tmp`, then renames it into place: only
+    the rename is an edit (one change batch, compiled from the new bytes), and the in-pod
+    inotify watcher reports it without waiting out a long burst window."""
+    from devspace_amd import runner
+
+    entry = tmp_path / "train.py"
+    entry.write_text('MARKER = "v0"\n')
+    w = runner._InotifyWatcher(str(tmp_path))
+    feed = runner.ChangeFeed(w, str(entry))
+    try:
+        time.sleep(0.05)
+        tmp = tmp_path / ("train.py" + runner.SYNC_TMP_SUFFIX)
+        tmp.write_text('MARKER = "v1"\n')
+        time.sleep(0.02)  # the temp file's close-write lands in a batch of its own
+        assert feed.take(0.05)[0] == 0, "the helper's temp file counted as an edit"
+        t0 = time.perf_counter()
+        os.rename(tmp, entry)
+        n, t_first, _ = feed.take(5.0)
+        assert n == 1
+        assert t_first - t0 < 0.5
+        assert feed.prepared_for(b'MARKER = "v1"\n') is not None
+    finally:
+        feed.close()
+        w.close()
+
+
+def test_inotify_watcher_returns_a_rename_at_once(tmp_path):
+    from devspace_amd import runner
+
+    w = runner._InotifyWatcher(str(tmp_path))
+    try:
+        (tmp_path / "a.py.devspace-tmp").write_text("x = 1\n")
+        os.rename(tmp_path / "a.py.devspace-tmp", tmp_path / "a.py")
+        t0 = time.perf_counter()
+        got = w.poll(1000)
+        took = time.perf_counter() - t0
+        assert str(tmp_path / "a.py") in got
+        assert runner._ignored(str(tmp_path / "a.py.devspace-tmp"))
+        assert took < 0.05, took  # events already queued: no multi-ms burst wait
+    finally:
+        w.close()
