@@ -89,9 +89,13 @@ def main():
         for t, k in after:
             first.setdefault(k, t)
         row = {"sync": m.get("synced", 0) - m["edit"]}
-        for k in ("event", "kill", "handoff", "listening", "ready", "booting"):
+        for k in ("event", "kill", "handoff", "listening"):
             if k in first:
                 row[k] = first[k] - m["edit"]
+        # the restart's hand-off went to a booted standby, or to one still booting
+        pick = next((k for _, k in after if k in ("ready", "booting")), None)
+        if pick:
+            row["standby"] = pick
         if "got" in m:
             row["response"] = m["got"] - m["edit"]
         rows.append(row)
@@ -100,7 +104,7 @@ def main():
           ", ".join("%s %.2f" % (k, statistics.median([x[k] for x in rows if k in x])) for k in keys
                     if any(k in x for x in rows)))
     print("bench p50 %.2f ms p90 %.2f ms; handoffs to a booted standby: %d of %d" % (
-        statistics.median(r["reload_ms"]), bench._pct(r["reload_ms"], 0.9), sum(1 for x in rows if x.get("ready")),
+        statistics.median(r["reload_ms"]), bench._pct(r["reload_ms"], 0.9), sum(1 for x in rows if x.get("standby") == "ready"),
         len(rows)))
     if a.out:
         with open(a.out, "w") as f:
