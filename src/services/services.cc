@@ -19,6 +19,7 @@
 #include "core/resolve.h"
 #include "core/prompt.h"
 #include "core/strutil.h"
+#include "core/trace.h"
 
 namespace ds {
 namespace services {
@@ -373,10 +374,57 @@ std::unique_ptr<net::WebSocket> PortForwarder::open_stream(int remote_port) {
   }
 }
 
+std::unique_ptr<net::WebSocket> PortForwarder::open_stream_direct(int remote_port) {
+  Value pod;
+  {
+    std::lock_guard<std::mutex> g(pod_mu_);
+    pod = pod_;
+  }
+  return k_->portforward(ns_, pod.at_path("metadata.name").as_string(), remote_port, take_spare());
+}
+
+namespace {
+// The next attempt of a held connection, opened on its own thread while the current attempt
+// waits for its reply or refusal. Opening a stream is the bulk of an attempt (the WebSocket
+// upgrade through the API server, and the pod-side dial that comes with it), so overlapping
+// it with the wait roughly halves the retry period. Only one stream of a connection ever
+// carries the client's bytes at a time: the next one gets them only after this one was
+// refused, so a request still reaches the app at most once.
+class PreOpened {
+ public:
+  template <class F>
+  explicit PreOpened(F open) : t_([this, open] {
+      try {
+        ws_ = open();
+      } catch (const std::exception&) {
+        ws_.reset();  // the caller falls back to a synchronous open (with pod re-selection)
+      }
+    }) {}
+  ~PreOpened() { discard(); }
+  std::unique_ptr<net::WebSocket> take() {
+    if (t_.joinable()) t_.join();
+    return std::move(ws_);
+  }
+  void discard() {
+    auto ws = take();
+    if (ws) ws->close();
+  }
+
+ private:
+  std::unique_ptr<net::WebSocket> ws_;
+  std::thread t_;  // declared last: the thread starts once ws_ exists
+};
+}  // namespace
+
 // True for the error-channel message of a stream whose pod-side connect failed (kubelet /
 // CRI: "... dial tcp4 127.0.0.1:8080: connect: connection refused"): nothing reached the
 // container, so the client's bytes can be replayed on a new stream.
 bool is_dial_refused(const std::string& err) { return contains(to_lower(err), "connection refused"); }
+
+bool port_forward_preopen() {
+  const char* v = std::getenv("DEVSPACE_PORTFORWARD_PREOPEN");
+  return !(v && std::string(v) == "0");
+}
 
 int port_forward_hold_ms() {
   if (const char* v = std::getenv("DEVSPACE_PORTFORWARD_HOLD_MS")) return std::max(0, std::atoi(v));
@@ -387,22 +435,45 @@ int port_forward_hold_ms() {
 // (hot reload), its port refuses connections for a moment; kubectl then drops the client's
 // connection and a browser shows an error. Here, as long as nothing came back from the pod yet
 // and the pod-side connect was refused, the connection is held and its bytes replayed on a
-// new stream (every ms for the first 100 ms, then backing off to 25 ms) for up to hold_ms_, so
-// a request sent mid-restart is answered by the new server as soon as it listens.
+// new stream for up to hold_ms_, so a request sent mid-restart is answered by the new server as
+// soon as it listens. For the first 100 ms the next stream is opened while the current attempt
+// is in flight (PreOpened) and used as soon as that attempt is refused; after that the attempts
+// back off (5 ms, then 25 ms after a second).
 void PortForwarder::handle(Conn* conn, int remote_port) {
   int cfd = conn->fd;
-  const long hold_deadline = mono_ms() + hold_ms_;
+  const long hold_start = mono_ms();
+  const long hold_deadline = hold_start + hold_ms_;
   std::string replay;           // client bytes of this connection, kept while no reply arrived
   bool replayable = hold_ms_ > 0;
   bool client_eof = false;
+  int attempt = 0;
+  std::unique_ptr<PreOpened> next;
   while (!stop_) {
     std::unique_ptr<net::WebSocket> ws;
-    try {
-      ws = open_stream(remote_port);
-    } catch (const std::exception& e) {
-      log::file_logger("portforwarding")->emit("error", std::string("Error forwarding ports: ") + e.what(), {});
-      break;
+    // span per stream: open (WebSocket upgrade; the pod-side dial happens with it) and the
+    // time until the first reply byte or the refusal (trace.jsonl "portforward.stream")
+    const int64_t t_open = trace::now_us();
+    bool preopened = false;
+    if (next) {
+      ws = next->take();
+      next.reset();
+      preopened = ws != nullptr;
     }
+    if (!ws) {
+      try {
+        ws = open_stream(remote_port);
+      } catch (const std::exception& e) {
+        log::file_logger("portforwarding")->emit("error", std::string("Error forwarding ports: ") + e.what(), {});
+        break;
+      }
+    }
+    if (preopened) preopened_++;
+    const int64_t t_opened = trace::now_us();
+    // a held connection (its first stream was refused) within its first 100 ms: open the
+    // following attempt's stream now, while this one waits for its reply or refusal
+    if (preopen_ && attempt > 0 && replayable && !stop_ && mono_ms() - hold_start < 100)
+      next = std::make_unique<PreOpened>([this, remote_port] { return open_stream_direct(remote_port); });
+    std::atomic<int64_t> t_first{0};
     if (!replay.empty() && !ws->send(std::string(1, '\0') + replay)) break;
     int wake[2];
     if (::pipe2(wake, O_CLOEXEC | O_NONBLOCK) != 0) break;
@@ -424,10 +495,12 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
           if (data.size() == 2) continue;
         }
         if (ch == 0) {
+          if (!got_reply) t_first = trace::now_us();
           got_reply = true;
           if (!write_all(cfd, data)) break;
         } else if (ch == 1 && !data.empty()) {
           if (!got_reply && is_dial_refused(data)) {
+            t_first = trace::now_us();
             refused = true;
             break;
           }
@@ -441,6 +514,7 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
     char buf[65536];
     buf[0] = 0;
     while (!down_done && !stop_ && !client_eof) {
+      if (next && got_reply) next.reset();  // answered: the spare attempt is not needed
       struct pollfd pf[2] = {{cfd, POLLIN, 0}, {wake[0], POLLIN, 0}};
       int r = ::poll(pf, 2, 200);
       if (r <= 0 || !(pf[0].revents & (POLLIN | POLLHUP | POLLERR))) continue;
@@ -458,6 +532,7 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
     if (client_eof && !down_done) {
       // the client finished sending: wait for the reply (or the refusal) before closing
       while (!down_done && !stop_) {
+        if (next && got_reply) next.reset();
         struct pollfd pw{wake[0], POLLIN, 0};
         ::poll(&pw, 1, 200);
       }
@@ -466,12 +541,23 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
     down.join();
     ::close(wake[0]);
     ::close(wake[1]);
+    if (trace::enabled()) {
+      int64_t tf = t_first.load();
+      trace::emit("portforward.stream", t_open, trace::now_us() - t_open,
+                  {{"port", std::to_string(remote_port)},
+                   {"attempt", std::to_string(attempt)},
+                   {"open_us", std::to_string(t_opened - t_open)},
+                   {"first_us", tf ? std::to_string(tf - t_open) : std::string("-1")},
+                   {"outcome", refused ? "refused" : got_reply ? "reply" : "closed"},
+                   {"preopened", preopened ? "1" : "0"}});
+    }
+    ++attempt;
     if (refused && replayable && !stop_ && mono_ms() < hold_deadline) {
       // a hot-reloading app is back within tens of ms: retry at once for the first 100 ms
-      // (each attempt is a stream open, itself ~a ms), then back off to 25 ms
-      long held = mono_ms() - (hold_deadline - hold_ms_);
-      int delay = held < 100 ? 1 : held < 1000 ? 5 : 25;
-      std::this_thread::sleep_for(std::chrono::milliseconds(delay));
+      // (the pre-opened stream paces those attempts: one per stream open), then back off
+      long held = mono_ms() - hold_start;
+      int delay = next ? 0 : held < 100 ? 1 : held < 1000 ? 5 : 25;
+      if (delay) std::this_thread::sleep_for(std::chrono::milliseconds(delay));
       held_retries_++;
       continue;
     }

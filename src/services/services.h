@@ -49,6 +49,9 @@ std::vector<std::pair<int, std::string>> listen_addresses(const std::string& bin
 // How long a local connection is held while the pod refuses it (app restarting):
 // DEVSPACE_PORTFORWARD_HOLD_MS, default 3000; 0 with DEVSPACE_REFERENCE_TIMING (kubectl drops it).
 int port_forward_hold_ms();
+// Whether a held connection opens its next attempt's stream while the current one is in flight
+// (DEVSPACE_PORTFORWARD_PREOPEN=0 turns it off).
+bool port_forward_preopen();
 bool is_dial_refused(const std::string& error_channel_message);
 
 // Local listeners forwarding to a pod port over the portforward.k8s.io WebSocket protocol
@@ -71,6 +74,8 @@ class PortForwarder {
   int held_retries() const { return held_retries_; }
   // Streams opened on a pre-dialed connection.
   int spares_used() const { return spares_used_; }
+  // Held-connection attempts whose stream was opened while the previous attempt was in flight.
+  int preopened_attempts() const { return preopened_; }
   size_t active_connections();
 
  private:
@@ -88,6 +93,8 @@ class PortForwarder {
   void handle(Conn* c, int remote_port);
   void reap(bool all);
   std::unique_ptr<net::WebSocket> open_stream(int remote_port);
+  // The current pod's stream without pod re-selection (the hold's pre-opened next attempt).
+  std::unique_ptr<net::WebSocket> open_stream_direct(int remote_port);
   std::shared_ptr<kube::Client> k_;
   std::mutex pod_mu_;
   Value pod_;
@@ -107,7 +114,9 @@ class PortForwarder {
   std::thread spare_thread_;
   int want_spares_ = 0;
   std::atomic<int> spares_used_{0};
+  std::atomic<int> preopened_{0};
   int hold_ms_ = port_forward_hold_ms();
+  bool preopen_ = port_forward_preopen();
 };
 
 std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& cfg, std::shared_ptr<kube::Client> k,

@@ -271,3 +271,52 @@ def test_port_forward_holds_requests_across_app_restart(localkube, hold):
     finally:
         _stop(dev)
     lk.run(["purge"], proj)
+
+
+def test_port_forward_hold_delivers_a_held_request_once(localkube, tmp_path):
+    """While the app restarts, a held connection is retried on new streams, the next one opened
+    while the current attempt is in flight (DEVSPACE_PORTFORWARD_PREOPEN). The client's bytes
+    only ever go out on one stream at a time, after the previous one was refused: every request
+    sent into a restart reaches the new server exactly once (a replayed POST must not be
+    applied twice)."""
+    lk = localkube
+    ns = "pf-once"
+    proj, remote, local = _restart_project(lk, "quickstart-" + ns, ns)
+    hits = tmp_path / "hits.log"
+    values = os.path.join(proj, "chart", "values.yaml")
+    v = yaml.safe_load(open(values))
+    v["components"][0]["containers"][0]["env"].append({"name": "HITS_FILE", "value": str(hits)})
+    open(values, "w").write(yaml.safe_dump(v))
+    index = os.path.join(proj, "index.js")
+    src = open(index).read().replace(
+        "http.createServer((req, res) => {",
+        "http.createServer((req, res) => {\n  require('fs').appendFileSync(process.env.HITS_FILE, req.method + ' ' + "
+        "req.url + '\\n');", 1)
+    assert "HITS_FILE" in src
+    open(index, "w").write(src)
+    dev = lk.popen(["dev", "--terminal=false"], proj)
+    try:
+        wait_for(lambda: isinstance(_get(local, 2), str) and _get(local, 2).startswith("Hello"), timeout=60,
+                 what="forwarded server")
+        root = json.loads(running(lk.pods(ns))[0]["metadata"]["annotations"]["devspace.sh/local-roots"])
+        pod_index = os.path.join(list(root.values())[0], "app", "index.js")
+        for i in range(4):
+            with open(index, "a") as f:
+                f.write(f"// edit {i}\n")
+            wait_for(lambda: f"// edit {i}" in open(pod_index).read(), timeout=30, what="synced edit")
+            wait_for(lambda: _refused(remote), timeout=10, what="old server stopped")
+            req = urllib.request.Request(f"http://127.0.0.1:{local}/held-{i}", data=b"x", method="POST")
+            body = urllib.request.urlopen(req, timeout=10).read().decode()
+            assert body.startswith("Hello"), body
+            wait_for(lambda: not _refused(remote), timeout=30, what="new server")
+    finally:
+        _stop(dev)
+    lines = hits.read_text().splitlines()
+    for i in range(4):
+        assert lines.count(f"POST /held-{i}") == 1, lines
+    spans = [json.loads(l) for l in open(os.path.join(proj, ".devspace", "logs", "trace.jsonl"))
+             if '"portforward.stream"' in l]
+    assert any(s["outcome"] == "refused" for s in spans), spans
+    # cold restarts refuse for longer than one attempt: the pipelined attempts ran
+    assert any(s.get("preopened") == "1" for s in spans), spans
+    lk.run(["purge"], proj)
