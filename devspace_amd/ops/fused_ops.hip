@@ -487,8 +487,14 @@ __global__ void __launch_bounds__(kBlock) adamw_kernel(AdamTable t, AdamScalars 
 //                    cdna_hip_programming.md §3), V^T comes from ds_read_b64_tr_b16 reads of the
 //                    row-major V tile; O^T keeps the query on the lane, so the per-query rescale
 //                    is a scalar per lane.
-// LDS tiles use 128-B rows with a 16-B chunk XOR swizzle (chunk ^ ((row >> 1) & 7)): the
-// ds_read_b128 row reads of the 32x32x16 A operand are conflict-free.
+// LDS tiles use 128-B rows with a 16-B chunk XOR swizzle, chunk ^ f(row) with
+// f(row) = ((row >> 1) & 7) ^ ((row & 2) << 1). The ds_read_b128 row reads of the 32x32x16 A
+// operand are conflict-free: the 8 rows of each parity in a 16-lane group get distinct f.
+// The ds_read_b64_tr_b16 reads of the transposed operand are conflict-free too: a 32-lane half
+// reads rows r0..r0+3 x one aligned quad of chunks, and the (row & 2) term flips bit 2 of f
+// between rows r0 and r0+2, which sends their quads to the two halves of the 128-B row. With
+// f = (row >> 1) & 7 alone those reads were 2-way (SQ_LDS_BANK_CONFLICT 294,912 per forward
+// dispatch at B8 T512 H16, profiles/r1_attn_pmc.txt; bank model: scripts/attn_lds_banks.py).
 // Backward (FlashAttention-2 split, no atomics): a dK/dV kernel (workgroup = 128 keys, loops over
 // query tiles; S and dP with the key on the lane, dV^T += dO^T P and dK^T += Q^T dS from the
 // accumulators) and a dQ kernel (workgroup = 128 queries, loops over key tiles like the forward;
@@ -511,7 +517,9 @@ __device__ __forceinline__ f32x16 mfma32(const u16x8& a, const u16x8& b, const f
 }
 
 // byte offset of 16-byte chunk `chunk` (0..7) of row `row` in a [64][64] bf16 LDS tile
-__device__ __forceinline__ int tile_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int tile_off(int row, int chunk) {
+  return row * 128 + ((chunk ^ ((row >> 1) & 7) ^ ((row & 2) << 1)) << 4);
+}
 
 __device__ __forceinline__ u16x8 lds_row8(const unsigned char* tile, int row, int chunk) {
   return *reinterpret_cast<const u16x8*>(tile + tile_off(row, chunk));
