@@ -72,6 +72,20 @@ def _pct(xs, q):
     return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
 
 
+_DEADLINE = [None]  # monotonic deadline of the untimed extras (set once the headline is measured)
+
+
+def _budget(timeout):
+    """A wait's timeout, cut to what is left of the extras' time budget: a workload that hangs
+    (e.g. a collective that never completes in an N-GPU pod) ends its extra, not the bench."""
+    if _DEADLINE[0] is None:
+        return timeout
+    left = _DEADLINE[0] - time.monotonic()
+    if left <= 0:
+        raise TimeoutError("extras time budget spent (--extras-budget-s)")
+    return min(timeout, left)
+
+
 def _log(msg):
     sys.stderr.write(f"[bench] {msg}\n")
     sys.stderr.flush()
@@ -194,15 +208,15 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
                                 "--portforwarding=false"], cwd=proj, env=env, stdout=subprocess.PIPE,
                                stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, start_new_session=True)
         tail = LineTail(dev.stdout, echo_prefix="[dev] ")
-        _, line, idx = tail.wait_for(r"Sync started on", timeout=900)
+        _, line, idx = tail.wait_for(r"Sync started on", timeout=_budget(900))
         deploy_s = time.perf_counter() - t_dev
         ns, pod_name = re.search(r"Pod: ([^/\s]+)/([^)\s]+)", line).groups()
         pod = cluster.store.get("", "pods", ns, pod_name)
         cname = pod["spec"]["containers"][0]["name"]
         root = json.loads(pod["metadata"]["annotations"]["devspace.sh/local-roots"])[cname]
         _log(f"dev: pod {pod_name} synced after {deploy_s:.2f}s")
-        _, _, idx = tail.wait_for(r"Attached to container", start_index=idx, timeout=120)
-        _wait_file_contains(root + ".log", "[devspace-runner] started gen=", timeout=900, interval=0.05)
+        _, _, idx = tail.wait_for(r"Attached to container", start_index=idx, timeout=_budget(120))
+        _wait_file_contains(root + ".log", "[devspace-runner] started gen=", timeout=_budget(900), interval=0.05)
         pod_log = open(root + ".log").read()
         m = re.search(r"\[devspace-runner\] started gen=\d+ .*?world=(\d+) device=(\S+)", pod_log)
         pod_world = int(m.group(1)) if m else 0
@@ -231,7 +245,7 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
             _set_marker(train, marker)
             t_sync = _wait_file_contains(pod_file, f'MARKER = "{marker}"')
             pat = rf"\[devspace-runner\] (reloaded|started) gen=\d+ marker={re.escape(marker)} "
-            t1, line, idx = tail.wait_for(pat, start_index=idx, timeout=600)
+            t1, line, idx = tail.wait_for(pat, start_index=idx, timeout=_budget(600))
             if i >= warmup:
                 samples.append((t1 - t0) * 1000.0)
                 sync_samples.append((t_sync - t0) * 1000.0)
@@ -293,7 +307,7 @@ def _qs_edit(path, marker):
 
 
 def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=False, timed_start=None,
-                    timed_end=None):
+                    timed_end=None, cold=None):
     """examples/quickstart edit -> reload, the way its README runs the dev loop: `devspace dev`
     (sync + port-forward) with the container running `npm run dev` (watch.js restarts node on
     change, as nodemon does in the reference's quickstart). One sample = edit index.js locally ->
@@ -303,7 +317,8 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
     from devspace_amd.localkube import LocalCluster
     from devspace_amd.localkube.bench import devspace_env
 
-    tag = ("ref-" if reference else "") + (sync_mode or "default")
+    cold = reference if cold is None else cold  # cold restarts: nodemon's (no standby pool)
+    tag = ("ref-" if reference else "") + ("cold-" if cold and not reference else "") + (sync_mode or "default")
     base = os.path.join(workdir, f"qs-bench-{tag}")
     proj = os.path.join(base, "quickstart")
     shutil.copytree(os.path.join(ROOT, "examples", "quickstart"), proj, symlinks=True)
@@ -316,7 +331,7 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
     values = os.path.join(proj, "chart", "values.yaml")
     v = yaml.safe_load(open(values))
     v["components"][0]["containers"][0]["env"] = [{"name": "PORT", "value": str(remote)}]
-    if reference:  # nodemon's cold restarts
+    if cold:  # nodemon's cold restarts
         v["components"][0]["containers"][0]["env"].append({"name": "WATCH_STANDBY", "value": "0"})
     open(values, "w").write(yaml.safe_dump(v))
 
@@ -332,7 +347,7 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
                                stdout=subprocess.PIPE, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
                                start_new_session=True)
         tail = LineTail(dev.stdout, echo_prefix=f"[qs-{tag}] ")
-        _, line, idx = tail.wait_for(r"Sync started on", timeout=300)
+        _, line, idx = tail.wait_for(r"Sync started on", timeout=_budget(300))
         ns, pod_name = re.search(r"Pod: ([^/\s]+)/([^)\s]+)", line).groups()
         pod = cluster.store.get("", "pods", ns, pod_name)
         cname = pod["spec"]["containers"][0]["name"]
@@ -352,7 +367,7 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
             time.sleep(rng.uniform(0.0, EDIT_JITTER_S))
             t0 = time.perf_counter()
             _qs_edit(index, marker)
-            t_sync = _wait_file_contains(pod_index, f"[{marker}]", timeout=60)
+            t_sync = _wait_file_contains(pod_index, f"[{marker}]", timeout=_budget(60))
             deadline = time.monotonic() + 60
             while True:
                 body = _http_get(local)
@@ -483,7 +498,7 @@ def example_loop(workdir, key, steps, warmup, tls=True, reference=False):
         t_dev = time.perf_counter()
         idx = 0
         for _ in edits:
-            _, _, idx = tail.wait_for(r"Sync started on", start_index=idx, timeout=600)
+            _, _, idx = tail.wait_for(r"Sync started on", start_index=idx, timeout=_budget(600))
         dev_ready_s = time.perf_counter() - t_dev
         with tail.cv:
             forwards = sum(1 for _, l in tail.lines if "Port forwarding started" in l)
@@ -506,7 +521,7 @@ def example_loop(workdir, key, steps, warmup, tls=True, reference=False):
             for local, _ in targets:
                 with open(local, "a") as f:
                     f.write(f"\n// edit {marker}\n" if not local.endswith(".py") else f"\n# edit {marker}\n")
-            t_last = max(_wait_file_contains(pod_file, f"edit {marker}", timeout=120) for _, pod_file in targets)
+            t_last = max(_wait_file_contains(pod_file, f"edit {marker}", timeout=_budget(120)) for _, pod_file in targets)
             if i >= warmup:
                 samples.append((t_last - t0) * 1000.0)
         _killpg(dev)
@@ -557,7 +572,7 @@ def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False):
     tail = LineTail(runner.stdout, echo_prefix=f"[{tag}] ")
     samples, sync_samples = [], []
     try:
-        _, _, idx = tail.wait_for(r"\[devspace-runner\] started gen=\d+ marker=v0", timeout=600)
+        _, _, idx = tail.wait_for(r"\[devspace-runner\] started gen=\d+ marker=v0", timeout=_budget(600))
         proj_file, pod_file = os.path.join(proj, "train.py"), os.path.join(pod, "train.py")
         rng = random.Random(1234)
         for i in range(warmup + steps):
@@ -569,7 +584,7 @@ def inner_loop(workdir, sync_mode, restart, nproc, steps, warmup, tiny=False):
             _set_marker(proj_file, marker)
             t_sync = _wait_file_contains(pod_file, f'MARKER = "{marker}"')
             pat = rf"\[devspace-runner\] (reloaded|started) gen=\d+ marker={re.escape(marker)} "
-            t1, _, idx = tail.wait_for(pat, start_index=idx, timeout=600)
+            t1, _, idx = tail.wait_for(pat, start_index=idx, timeout=_budget(600))
             if i >= warmup:
                 samples.append((t1 - t0) * 1000.0)
                 sync_samples.append((t_sync - t0) * 1000.0)
@@ -601,6 +616,8 @@ def main():
                     help="samples per BASELINE example (php-mysql, microservices, kaniko; 0=skip)")
     ap.add_argument("--no-deploy-bench", action="store_true", help="skip the quickstart deploy wall-clock")
     ap.add_argument("--tiny", action="store_true", help="tiny GPU-pod model (CPU smoke only)")
+    ap.add_argument("--extras-budget-s", type=float, default=600.0,
+                    help="wall-clock budget of all untimed extras together (each wait is cut to what is left)")
     ap.add_argument("--transport", choices=("tls", "plain"), default="tls",
                     help="API server transport of the local cluster (tls = https + wss with mTLS, as a real cluster)")
     args = ap.parse_args()
@@ -669,8 +686,13 @@ def main():
             timed_end()
         elapsed = clock["t1"] - clock["t0"]
         if rank == 0:
-            # untimed extras (outside the barrier-bracketed region)
+            # untimed extras (outside the barrier-bracketed region), within one time budget
+            t_extras = time.monotonic()
+            _DEADLINE[0] = t_extras + args.extras_budget_s
             if args.ref_steps > 0:
+                # this tool with the app restarting cold (no standby pool): what the tool itself
+                # brings, next to the reference column (same cold restarts, reference tool)
+                extra("qs_cold", lambda: quickstart_loop(workdir, max(args.ref_steps, 10), 1, tls=tls, cold=True))
                 extra("qs_ref", lambda: quickstart_loop(workdir, args.ref_steps, 1, sync_mode="compat", tls=tls,
                                                         reference=True))
             if args.gpu_steps > 0:
@@ -684,6 +706,7 @@ def main():
                     if args.ref_steps > 0:
                         extra(key + "_ref", lambda key=key: example_loop(workdir, key, args.ref_steps, 1, tls=tls,
                                                                         reference=True))
+            _log(f"extras took {time.monotonic() - t_extras:.1f}s")
         if pg is not None:
             pg.barrier()
     finally:
@@ -754,6 +777,17 @@ def report(args, nproc, tls, ms_total, qs, extras):
             "speedup": round(rp50 / p50, 2) if p50 else None,
             "sync_speedup": round(_pct(ref["sync_ms"], 0.5) / max(out["sync_p50_ms"], 1e-3), 1),
         }
+    cold = extras.get("qs_cold")
+    if _ok(cold):
+        cp50 = _pct(cold["reload_ms"], 0.5)
+        out["cold_restart"] = {
+            "what": "this tool (event-driven sync, port-forward hold) with the app restarting cold as nodemon does "
+                    "(WATCH_STANDBY=0): the tool's own share, without the example watcher's standby pool",
+            "p50_ms": round(cp50, 2), "p90_ms": round(_pct(cold["reload_ms"], 0.9), 2),
+            "sync_p50_ms": round(_pct(cold["sync_ms"], 0.5), 2), "n": len(cold["reload_ms"]),
+        }
+        if "reference_equivalent" in out:
+            out["cold_restart"]["speedup_vs_reference"] = round(out["reference_equivalent"]["p50_ms"] / cp50, 2)
     dep, dep_ref = extras.get("deploy"), extras.get("deploy_ref")
     if _ok(dep):
         out["deploy"] = {

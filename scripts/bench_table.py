@@ -59,6 +59,11 @@ def render(path):
         rows.append(("edit → new response p50, quickstart (headline `value`)",
                      f"**{_ms(b['value'])}** (p90 {_ms(b.get('p90_ms'))}; sync {_ms(b.get('sync_p50_ms'))})",
                      _ms(ref.get("p50_ms")) + _x(b["value"], ref.get("p50_ms"))))
+        cold = b.get("cold_restart")
+        if isinstance(cold, dict) and "p50_ms" in cold:
+            rows.append(("edit → new response p50, quickstart with cold restarts (the tool alone, no standby pool)",
+                         f"**{_ms(cold['p50_ms'])}** (p90 {_ms(cold.get('p90_ms'))})",
+                         _ms(ref.get("p50_ms")) + _x(cold["p50_ms"], ref.get("p50_ms"))))
         rows.append(("sync p50, quickstart (edit → bytes in the pod)", f"**{_ms(b.get('sync_p50_ms'))}**",
                      _ms(ref.get("sync_p50_ms")) + _x(b.get("sync_p50_ms"), ref.get("sync_p50_ms"))))
         g = b.get("gpu_pod")

@@ -37,6 +37,10 @@ def test_bench_cpu_tiny():
     # same-box reference column of the headline (compat protocol + reference waits)
     assert d["reference_equivalent"]["p50_ms"] > d["value"], r.stderr[-3000:]
     assert d["reference_equivalent"]["sync_p50_ms"] > d["sync_p50_ms"]
+    # the tool alone (cold restarts, no standby pool) against the same reference column
+    cold = d["cold_restart"]
+    assert cold["n"] >= 10 and cold["p50_ms"] > 0, cold
+    assert cold["p50_ms"] < d["reference_equivalent"]["p50_ms"], (cold, d["reference_equivalent"])
     dep = d["deploy"]
     assert dep["control_plane_only"] is True and dep["net"]["tls_handshakes"] >= 1
     # reference timing: no kept-alive connections, 5 s rollout polls
@@ -68,6 +72,15 @@ def test_bench_torchrun_two_ranks_cpu():
     d = json.loads(lines[0])
     assert d["steps"] == 2 and d["value"] > 0
     assert d["n_gpus"] == 2 and d["gpu_pod"]["parallelism"] == "dp2", d
+
+
+def test_bench_extras_budget_keeps_the_headline():
+    """A hung extra (here: no time left at all) ends that extra, not the run: the headline line
+    is still printed, and the extras that could not finish are left out."""
+    d = _run(["--steps", "2", "--warmup", "1", "--ref-steps", "1", "--gpu-steps", "2", "--example-steps", "0",
+              "--no-deploy-bench", "--tiny", "--extras-budget-s", "0.001"], 600)
+    assert d["value"] > 0 and d["steps"] == 2
+    assert "gpu_pod" not in d and "cold_restart" not in d and "reference_equivalent" not in d, d
 
 
 @pytest.mark.gpu
