@@ -154,6 +154,9 @@ void StdoutLogger::write_msg(int kind, const std::string& m) {
   if (file_) {
     static const char* lv[] = {"debug", "info", "warning", "error", "fatal", "info", "error"};
     file_->emit(lv[kind], m, {});
+    // errors and fatals also go to errors.log, as the reference's runtime error handler does
+    // (util/log/file_logger.go OverrideRuntimeErrorHandler)
+    if (kind == 3 || kind == 4 || kind == 6) file_logger("errors")->emit(lv[kind], m, {});
   }
 }
 

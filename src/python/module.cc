@@ -255,6 +255,21 @@ class PyRules {
   std::unique_ptr<sync::Session> s_;
 };
 
+// The strict config schema as nested dicts (docs generator: docs/reference/configuration.md).
+py::object schema_to_py(const config::Schema& s) {
+  static const char* kinds[] = {"string", "integer", "boolean", "any", "struct", "list", "map"};
+  py::dict d;
+  d["kind"] = kinds[s.kind];
+  if (!s.type_name.empty()) d["type"] = s.type_name;
+  if (s.kind == config::Schema::Struct) {
+    py::list fields;
+    for (auto& f : s.fields) fields.append(py::make_tuple(f.first, schema_to_py(*f.second)));
+    d["fields"] = fields;
+  }
+  if (s.elem) d["elem"] = schema_to_py(*s.elem);
+  return std::move(d);
+}
+
 PYBIND11_MODULE(_native, m) {
   m.doc() = "devspace native engine (C++17) bindings";
   log::set_fatal_throws(true);
@@ -286,6 +301,13 @@ PYBIND11_MODULE(_native, m) {
     return py::make_tuple(std::string(1, op), len);
   });
   m.def("parse_config", [](py::object data) { return to_py(config::parse_versioned(from_py(data))); });
+  m.def("config_schema", [](const std::string& which) {
+    if (which == "latest") return schema_to_py(config::schema_latest());
+    if (which == "v1alpha1") return schema_to_py(config::schema_v1alpha1());
+    if (which == "configs") return schema_to_py(config::schema_configs());
+    if (which == "vars") return schema_to_py(config::schema_vars());
+    throw std::invalid_argument("unknown schema " + which + " (latest|v1alpha1|configs|vars)");
+  });
   m.def("copy_to_container",
         [](const std::string& local, const std::string& container, std::vector<std::string> excludes,
            const std::string& mode) {

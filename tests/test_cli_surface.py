@@ -415,3 +415,17 @@ def test_newer_version_notice_from_daily_cache(tmp_path):
         assert "newer version" not in p.stdout + p.stderr
     finally:
         gh.close()
+
+
+def test_errors_also_land_in_errors_log(tmp_path):
+    """.devspace/logs/errors.log gets the command's errors (the reference routes runtime errors
+    there: util/log/file_logger.go OverrideRuntimeErrorHandler), besides default.log."""
+    (tmp_path / ".devspace").mkdir()
+    (tmp_path / ".devspace" / "config.yaml").write_text("version: v1alpha2\nbogusKey: 1\n")
+    r = subprocess.run([BIN, "deploy"], cwd=tmp_path, capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, DEVSPACE_NONINTERACTIVE="1"))
+    assert r.returncode != 0
+    logs = tmp_path / ".devspace" / "logs"
+    errs = [json.loads(l) for l in (logs / "errors.log").read_text().splitlines()]
+    assert any("bogusKey" in e["msg"] and e["level"] == "fatal" for e in errs), errs
+    assert "bogusKey" in (logs / "default.log").read_text()

@@ -1,0 +1,42 @@
+"""User documentation (docs/): the generated reference pages match the built tool, and every
+relative link resolves (reference: docs/pages/** of the original)."""
+import glob
+import os
+import re
+import subprocess
+import sys
+
+from conftest import ROOT
+
+DOCS = os.path.join(ROOT, "docs")
+
+
+def test_reference_pages_are_current():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "gen_docs.py"), "--check"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr + r.stdout
+
+
+def test_links_resolve_and_every_page_is_indexed():
+    pages = sorted(glob.glob(os.path.join(DOCS, "**", "*.md"), recursive=True))
+    assert len(pages) >= 10
+    for page in pages:
+        text = open(page).read()
+        for target in re.findall(r"\]\(([^)#\s]+)(?:#[^)]*)?\)", text):
+            if re.match(r"[a-z]+://", target):
+                continue
+            path = os.path.normpath(os.path.join(os.path.dirname(page), target))
+            assert os.path.exists(path), f"{os.path.relpath(page, ROOT)}: broken link {target}"
+    index = open(os.path.join(DOCS, "README.md")).read()
+    for page in pages:
+        rel = os.path.relpath(page, DOCS)
+        if rel != "README.md":
+            assert f"]({rel})" in index, f"docs/README.md does not link {rel}"
+
+
+def test_every_cli_command_is_in_the_reference():
+    text = open(os.path.join(DOCS, "reference", "cli.md")).read()
+    for cmd in ("init", "deploy", "dev", "enter", "logs", "analyze", "purge", "reset", "install", "upgrade", "login",
+                "add sync", "add package", "create space", "list configs", "remove space", "status sync",
+                "update config", "use context"):
+        assert f"## `devspace {cmd}`" in text, cmd
