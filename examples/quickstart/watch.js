@@ -13,11 +13,14 @@
 // processes are kept booted (V8 + core modules initialised, nothing of the app loaded). A
 // restart hands the script to a booted standby, which loads it then — from disk, after the
 // edit — as its main module (`require.main === module` holds), and a replacement boots in the
-// background. That takes node's start-up (tens of ms) out of every edit -> response. Four
-// standbys by default, so back-to-back saves (format-on-save, quick fix-ups) still find one
-// that finished booting a while ago (a just-booted one measured ~10 ms slower to listen with
-// two standbys: profiles/r3_qs_standby_probe.txt); WATCH_STANDBY=N sets the count, 0 gives
-// plain cold restarts.
+// background. That takes node's start-up (tens of ms) out of every edit -> response.
+//
+// The pool adapts to the edit rate: it starts at WATCH_STANDBY (default 4) standbys, grows by
+// one (up to WATCH_STANDBY_MAX, default 8) whenever a restart finds none of them booted —
+// back-to-back saves (format-on-save, generated files, a script editing in a loop) come faster
+// than node boots — and gives one back after 30 s without such a miss. A standby that finished
+// booting a while ago also starts the app faster than a just-booted one (~10 ms on the MI355X
+// box, profiles/r3_qs_standby_probe.txt). WATCH_STANDBY=0 gives plain cold restarts.
 const {spawn} = require('child_process');
 const fs = require('fs');
 const path = require('path');
@@ -25,7 +28,10 @@ const path = require('path');
 const script = path.resolve(process.argv[2] || 'index.js');
 const dir = path.dirname(script);
 const ignored = /(^|\/)(node_modules|\.git|\.devspace)(\/|$)|\.sw.$|~$/;
-const nStandby = Math.max(0, parseInt(process.env.WATCH_STANDBY || '4', 10) || 0);
+const minStandby = Math.max(0, parseInt(process.env.WATCH_STANDBY || '4', 10) || 0);
+const maxStandby = minStandby && Math.max(minStandby, parseInt(process.env.WATCH_STANDBY_MAX || '8', 10) || 0);
+let nStandby = minStandby;
+let lastMiss = 0;  // time of the last restart that found no booted standby
 // The standby's whole program: load the core modules a server needs (node loads them lazily,
 // and they are shared, stateless code: nothing of the app), wait for the go message, drop the
 // IPC channel (the app must not see a parent channel) and run the script as the main module.
@@ -69,10 +75,24 @@ function bootStandbys() {
   }
 }
 
+function resize(ready) {
+  const now = Date.now();
+  if (!ready && nStandby > 0) {
+    lastMiss = now;
+    nStandby = Math.min(maxStandby, nStandby + 1);
+  } else if (nStandby > minStandby && now - lastMiss > 30000) {
+    lastMiss = now;  // one step down per quiet 30 s
+    nStandby--;
+    const extra = standbys.length - nStandby;
+    if (extra > 0) for (const x of standbys.splice(standbys.length - extra, extra)) x.kill('SIGKILL');
+  }
+}
+
 function start() {
   gen++;
   // a booted standby if there is one, else the one that started booting first
   const i = standbys.findIndex((s) => s.ready);
+  if (gen > 1) resize(i >= 0);  // the first start has no pool yet: not a miss
   const s = standbys.splice(i >= 0 ? i : 0, 1)[0];
   if (s) {
     s.removeAllListeners('message');

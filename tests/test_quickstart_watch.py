@@ -87,3 +87,28 @@ def test_watch_restarts_fresh_main_module(tmp_path, standby):
     time.sleep(0.5)
     for pid in pids:
         assert not os.path.exists(f"/proc/{pid}") or open(f"/proc/{pid}/stat").read().split()[2] == "Z"
+
+
+def test_standby_pool_grows_under_back_to_back_edits(tmp_path):
+    """Edits faster than node boots exhaust the standby pool: the watcher adds standbys (up to
+    WATCH_STANDBY_MAX) instead of handing restarts to processes still booting."""
+    import psutil
+
+    app = tmp_path / "index.js"
+    app.write_text("require('http').createServer((q, r) => r.end('v0')).listen(0);\n")
+    shutil.copy(os.path.join(ROOT, "examples", "quickstart", "watch.js"), tmp_path / "watch.js")
+    p = subprocess.Popen(["node", str(tmp_path / "watch.js"), str(app)], cwd=tmp_path, stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT, text=True, env=dict(os.environ, WATCH_STANDBY="1",
+                                                                         WATCH_STANDBY_MAX="4"))
+    try:
+        time.sleep(1.0)
+        for i in range(12):  # back to back: no time for a standby to boot in between
+            app.write_text(f"require('http').createServer((q, r) => r.end('v{i + 1}')).listen(0);\n")
+            time.sleep(0.02)
+        time.sleep(2.0)  # let the pool settle
+        kids = psutil.Process(p.pid).children()
+        # the running app + the grown pool (1 standby at start, at most 4)
+        assert 3 <= len(kids) <= 5, [k.cmdline()[:3] for k in kids]
+    finally:
+        p.terminate()
+        p.wait(10)
