@@ -9,6 +9,7 @@ server listening, -> response through the port-forward.
     python scripts/qs_breakdown.py [--steps 20] [--warmup 3]
 """
 import argparse
+import glob
 import json
 import os
 import shutil
@@ -78,6 +79,9 @@ def main():
     bench._qs_edit, bench._wait_file_contains, bench._http_get = edit, wait, get
     with tempfile.TemporaryDirectory() as d:
         r = bench.quickstart_loop(d, a.steps, a.warmup)
+        spans = []
+        for tp in glob.glob(os.path.join(d, "*", "quickstart", ".devspace", "logs", "trace.jsonl")):
+            spans += [json.loads(l) for l in open(tp) if '"portforward.stream"' in l]
     events = []
     for line in open(trace):
         k, v = line.split()
@@ -106,6 +110,14 @@ def main():
     print("bench p50 %.2f ms p90 %.2f ms; handoffs to a booted standby: %d of %d" % (
         statistics.median(r["reload_ms"]), bench._pct(r["reload_ms"], 0.9), sum(1 for x in rows if x.get("standby") == "ready"),
         len(rows)))
+    # port-forward streams (trace.jsonl spans): how long a held connection's attempts take
+    for outcome in ("refused", "reply"):
+        v = [x for x in spans if x["outcome"] == outcome]
+        if v:
+            print("portforward %s streams: %d, open p50 %.2f ms, first byte/refusal p50 %.2f ms, preopened %d" % (
+                outcome, len(v), statistics.median(int(x["open_us"]) for x in v) / 1000,
+                statistics.median(int(x["first_us"]) for x in v) / 1000,
+                sum(1 for x in v if x.get("preopened") == "1")))
     if a.out:
         with open(a.out, "w") as f:
             json.dump({"rows": rows, "reload_ms": r["reload_ms"]}, f, indent=1)

@@ -112,3 +112,43 @@ def test_standby_pool_grows_under_back_to_back_edits(tmp_path):
     finally:
         p.terminate()
         p.wait(10)
+
+
+def test_restart_handed_to_a_booting_standby_serves(tmp_path):
+    """Edits landing faster than standbys boot hand the script to a standby whose warm-up has
+    not finished: the warm-up must stop there (no message on the removed IPC channel, no stray
+    exception in the app) and the last version must serve."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    app = tmp_path / "index.js"
+
+    def write(v):
+        app.write_text("require('http').createServer((q, r) => r.end('%s')).listen(%d, '127.0.0.1');\n" % (v, port))
+
+    write("v0")
+    shutil.copy(os.path.join(ROOT, "examples", "quickstart", "watch.js"), tmp_path / "watch.js")
+    p = subprocess.Popen(["node", str(tmp_path / "watch.js"), str(app)], cwd=tmp_path, stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT, text=True, env=dict(os.environ, WATCH_STANDBY="1"))
+    try:
+        assert "started gen=1" in p.stdout.readline()
+        time.sleep(0.05)  # the standby started with gen 1 is still booting
+        for i in range(1, 9):
+            write(f"v{i}")
+            time.sleep(0.03)
+        deadline = time.time() + 15
+        body = None
+        while time.time() < deadline:
+            try:
+                body = urllib.request.urlopen(f"http://127.0.0.1:{port}/", timeout=1).read().decode()
+                if body == "v8":
+                    break
+            except OSError:
+                pass
+            time.sleep(0.05)
+        assert body == "v8", body
+    finally:
+        p.terminate()
+        out = p.communicate(timeout=10)[0]
+    assert "TypeError" not in out and "Error" not in out.replace("[watch]", ""), out
