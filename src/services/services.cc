@@ -399,7 +399,10 @@ class PreOpened {
       } catch (const std::exception&) {
         ws_.reset();  // the caller falls back to a synchronous open (with pod re-selection)
       }
+      done_ = true;
     }) {}
+  // the open finished: take() / discard() will not block
+  bool ready() const { return done_; }
   ~PreOpened() { discard(); }
   std::unique_ptr<net::WebSocket> take() {
     if (t_.joinable()) t_.join();
@@ -412,7 +415,8 @@ class PreOpened {
 
  private:
   std::unique_ptr<net::WebSocket> ws_;
-  std::thread t_;  // declared last: the thread starts once ws_ exists
+  std::atomic<bool> done_{false};
+  std::thread t_;  // declared last: the thread starts once ws_ and done_ exist
 };
 }  // namespace
 
@@ -514,7 +518,9 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
     char buf[65536];
     buf[0] = 0;
     while (!down_done && !stop_ && !client_eof) {
-      if (next && got_reply) next.reset();  // answered: the spare attempt is not needed
+      // answered: the spare attempt is not needed (dropped once its open is done, so the
+      // forwarding never waits on it; else at the end of the connection)
+      if (next && got_reply && next->ready()) next.reset();
       struct pollfd pf[2] = {{cfd, POLLIN, 0}, {wake[0], POLLIN, 0}};
       int r = ::poll(pf, 2, 200);
       if (r <= 0 || !(pf[0].revents & (POLLIN | POLLHUP | POLLERR))) continue;
@@ -532,7 +538,7 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
     if (client_eof && !down_done) {
       // the client finished sending: wait for the reply (or the refusal) before closing
       while (!down_done && !stop_) {
-        if (next && got_reply) next.reset();
+        if (next && got_reply && next->ready()) next.reset();
         struct pollfd pw{wake[0], POLLIN, 0};
         ::poll(&pw, 1, 200);
       }
