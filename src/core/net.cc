@@ -194,8 +194,11 @@ SSL_CTX* make_ctx(const TlsOptions& t) {
 // (client-go configures no session cache).
 namespace {
 std::mutex g_tls_mu;
-std::map<std::string, SSL_CTX*> g_ctx_cache;          // credential digest -> ctx (one ref held)
-std::map<std::string, SSL_SESSION*> g_sessions;       // digest|peer -> latest resumable session
+// Process-lifetime caches, deliberately never destroyed: OpenSSL's own exit-time cleanup can
+// run before static destructors, so freeing contexts there is unsafe. Held through globals,
+// they stay reachable at exit (leak checkers do not count them).
+std::map<std::string, SSL_CTX*>& g_ctx_cache = *new std::map<std::string, SSL_CTX*>();  // digest -> ctx
+std::map<std::string, SSL_SESSION*>& g_sessions = *new std::map<std::string, SSL_SESSION*>();  // digest|peer -> session
 
 int new_session_cb(SSL* ssl, SSL_SESSION* sess) {
   auto* key = static_cast<const std::string*>(SSL_get_app_data(ssl));
