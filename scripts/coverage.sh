@@ -1,0 +1,24 @@
+#!/bin/bash
+# Line coverage of the C++ CLI (the counterpart of the reference's scripts/coverage.bash, which
+# runs `go test -race -coverprofile` per package): a gcov build in build/coverage, the C++ test
+# suite, then the end-to-end suites driving that build's `devspace` against the bundled local
+# cluster, then a per-module summary of executed lines (scripts/coverage_summary.py).
+#
+#   scripts/coverage.sh [out.txt]
+set -euo pipefail
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+B="$ROOT/build/coverage"
+OUT="${1:-$B/coverage.txt}"
+cmake -S "$ROOT" -B "$B" -G Ninja -DCMAKE_BUILD_TYPE=Debug -DDEVSPACE_COVERAGE=ON > /dev/null
+ninja -C "$B" -j "${JOBS:-8}" devspace_tests devspace > /dev/null
+find "$B" -name '*.gcda' -delete
+cp -f "$ROOT/bin/devspace-helper" "$B/bin/devspace-helper"
+echo "== C++ suite"
+"$B/bin/devspace_tests" | tail -1
+echo "== e2e suites with $B/bin/devspace"
+DEVSPACE_BIN="$B/bin/devspace" python3 -m pytest -q -p no:cacheprovider \
+  "$ROOT/tests/test_e2e_cli.py" "$ROOT/tests/test_e2e_services.py" "$ROOT/tests/test_e2e_tls.py" \
+  "$ROOT/tests/test_cloud_cli.py" "$ROOT/tests/test_e2e_helm.py" "$ROOT/tests/test_e2e_apply.py" \
+  "$ROOT/tests/test_e2e_auth.py" "$ROOT/tests/test_e2e_recovery.py" "$ROOT/tests/test_hostile_server.py" \
+  "$ROOT/tests/test_e2e_gpu_sched.py" "$ROOT/tests/test_cli_surface.py" 2>&1 | tail -1
+python3 "$ROOT/scripts/coverage_summary.py" "$B" "$ROOT/src" | tee "$OUT"
