@@ -226,9 +226,33 @@ std::vector<std::string> probe_pod_gpus(kube::Client& k, const std::string& ns, 
 std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, const std::vector<Value>& pods,
                                       const Options& o) {
   std::vector<std::string> out;
+  // A crashed container whose log shows a ROCm/HIP/RCCL runtime error, in any pod: without an
+  // amd.com/gpu request it is usually the missing request itself ("No HIP GPUs are available").
+  auto crash_errors = [&](const Value& p, int64_t want) {
+    std::string name = p.at_path("metadata.name").as_string();
+    for (auto& c : p.at_path("status.containerStatuses").items()) {
+      bool crashed = c.get("restartCount").as_int() > 0 || !c.at_path("state.terminated").is_null();
+      if (!crashed) continue;
+      std::string text;
+      try {
+        text = k.logs(ns, name, c.get("name").as_string(), 200, c.get("restartCount").as_int() > 0);
+      } catch (...) {
+        continue;
+      }
+      std::string m;
+      if (log_has_gpu_runtime_error(text, &m))
+        out.push_back(kPad + log::color("GPU: ", "202+b") + "container " + c.get("name").as_string() + " of pod " +
+                      name + " failed with a ROCm/HIP/RCCL error: " + m +
+                      (want == 0 ? " (the pod requests no amd.com/gpu: add resources.limits amd.com/gpu)" : "") +
+                      "\n");
+    }
+  };
   int64_t requested = 0;
   for (auto& p : pods) requested += gpu_request(p);
-  if (requested == 0) return out;
+  if (requested == 0) {
+    for (auto& p : pods) crash_errors(p, 0);
+    return out;
+  }
   // node capacity as advertised by the AMD GPU device plugin
   int64_t max_alloc = 0, total = 0;
   std::vector<std::string> products;
@@ -250,7 +274,10 @@ std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, co
                   "no node advertises amd.com/gpu — is the AMD GPU device plugin DaemonSet running?\n");
   for (auto& p : pods) {
     int64_t want = gpu_request(p);
-    if (want == 0) continue;
+    if (want == 0) {
+      crash_errors(p, 0);
+      continue;
+    }
     std::string name = p.at_path("metadata.name").as_string();
     if (max_alloc > 0 && want > max_alloc)
       out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + " requests amd.com/gpu: " +
@@ -260,20 +287,7 @@ std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, co
     if (!shm.empty()) out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + shm + "\n");
     for (auto& prob : gpu::pod_sizing_problems(p.get("spec")))
       out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + prob + "\n");
-    for (auto& c : p.at_path("status.containerStatuses").items()) {
-      bool crashed = c.get("restartCount").as_int() > 0 || !c.at_path("state.terminated").is_null();
-      if (!crashed) continue;
-      std::string text;
-      try {
-        text = k.logs(ns, name, c.get("name").as_string(), 200, c.get("restartCount").as_int() > 0);
-      } catch (...) {
-        continue;
-      }
-      std::string m;
-      if (log_has_gpu_runtime_error(text, &m))
-        out.push_back(kPad + log::color("GPU: ", "202+b") + "container " + c.get("name").as_string() + " of pod " +
-                      name + " failed with a ROCm/HIP/RCCL error: " + m + "\n");
-    }
+    crash_errors(p, want);
     if (o.gpu_probe && kube::pod_status(p) == "Running") {
       std::string c = p.at_path("spec.containers")[0].get("name").as_string();
       try {

@@ -443,3 +443,38 @@ def test_minikube_example_builds_in_minikube_daemon(tmp_path):
         lk.run(["purge"], proj)
     finally:
         cluster.stop()
+
+
+def test_analyze_reports_crash_loop_with_gpu_runtime_error(localkube):
+    """A container that keeps failing with a HIP error: analyze reports the restarts, the last
+    exit code, the crash log and the ROCm/HIP/RCCL error line (reference: analyze/pods.go
+    getContainerProblem; the GPU line is the MI355X delta)."""
+    lk = localkube
+    proj = lk.project("quickstart-kubectl", "crashing-gpu-app")
+    path = os.path.join(proj, "kube", "deployment.yaml")
+    src = open(path).read().replace(
+        "        ports:\n",
+        "        command: [\"sh\", \"-c\", \"echo 'loading model'; echo 'RuntimeError: HIP error: "
+        "hipErrorNoBinaryForGpu' >&2; exit 3\"]\n        ports:\n", 1)
+    assert "hipErrorNoBinaryForGpu" in src
+    open(path, "w").write(src)
+    cfg = os.path.join(proj, ".devspace", "config.yaml")
+    text = open(cfg).read().replace("namespace: quickstart-kubectl", "namespace: crashing-gpu-app")
+    with open(cfg, "w") as f:
+        f.write(text)
+    lk.run(["deploy"], proj)
+
+    def restarted():
+        for p in lk.pods("crashing-gpu-app"):
+            for c in (p.get("status") or {}).get("containerStatuses") or []:
+                if c.get("restartCount", 0) >= 1 and c.get("lastState", {}).get("terminated"):
+                    return True
+        return False
+
+    wait_for(restarted, timeout=60, what="a restarted container")
+    out = lk.run(["analyze", "--wait=false"], proj, check=False).stdout
+    assert "Restarts:" in out and "Last Exit:" in out and "Code: 3" in out, out
+    assert "hipErrorNoBinaryForGpu" in out, out  # the crash log tail
+    assert "failed with a ROCm/HIP/RCCL error: HIP error" in out, out
+    assert "the pod requests no amd.com/gpu" in out, out  # the likely cause, named
+    lk.run(["purge"], proj)
