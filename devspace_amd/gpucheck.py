@@ -44,6 +44,10 @@ class Probe:
         self.lib.gp_mfma_bf16_tflops.argtypes = [ctypes.c_int, ctypes.c_int]
         self.lib.gp_mfma_bf16_tflops.restype = ctypes.c_double
         self.lib.gp_last_error.restype = ctypes.c_char_p
+        self.lib.gp_peer_access.argtypes = [ctypes.c_int, ctypes.c_int]
+        self.lib.gp_peer_access.restype = ctypes.c_int
+        self.lib.gp_peer_copy_gbps.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int]
+        self.lib.gp_peer_copy_gbps.restype = ctypes.c_double
 
     def count(self):
         return self.lib.gp_device_count()
@@ -65,6 +69,39 @@ class Probe:
 
     def mfma_tflops(self, dev, iters=20000):
         return self.lib.gp_mfma_bf16_tflops(dev, iters)
+
+    def peer_access(self, a, b):
+        return self.lib.gp_peer_access(a, b)
+
+    def peer_gbps(self, a, b, nbytes=256 << 20, iters=4):
+        return self.lib.gp_peer_copy_gbps(a, b, nbytes, iters)
+
+
+def peer_check(probe, n, quick=False):
+    """Every ordered device pair of the pod: peer access (xGMI) and copy bandwidth. RCCL's
+    all-reduce over an 8-GPU ring is bound by its slowest link, so one pair without peer access
+    or far below the others (a copy staged through the host, a degraded link) is reported.
+    Returns (pairs, problems)."""
+    pairs, problems = [], []
+    for a in range(n):
+        for b in range(n):
+            if a == b:
+                continue
+            acc = probe.peer_access(a, b)
+            gbps = probe.peer_gbps(a, b, nbytes=(64 << 20) if quick else (256 << 20), iters=2 if quick else 4)
+            pairs.append({"src": a, "dst": b, "peer_access": acc == 1, "copy_gbps": round(gbps, 1)})
+            if acc != 1:
+                problems.append(f"gpu{a} -> gpu{b}: no peer access (RCCL falls back to copies through host memory)")
+            elif gbps <= 0:
+                problems.append(f"gpu{a} -> gpu{b}: peer copy failed")
+    rates = sorted(p["copy_gbps"] for p in pairs if p["copy_gbps"] > 0)
+    if rates:
+        median = rates[len(rates) // 2]
+        for p in pairs:
+            if p["peer_access"] and 0 < p["copy_gbps"] < 0.5 * median:
+                problems.append(f"gpu{p['src']} -> gpu{p['dst']}: peer copy {p['copy_gbps']:.0f} GB/s, under half the "
+                                f"median pair ({median:.0f} GB/s): degraded link")
+    return pairs, problems
 
 
 def device_nodes():
@@ -104,6 +141,9 @@ def run(quick=False):
             if "gfx950" in info.get("arch", "") and gbps < 0.5 * HBM_EXPECTED_GBPS:
                 report["problems"].append(f"gpu{d}: HBM bandwidth {gbps:.0f} GB/s is below 50% of expected")
         report["devices"].append(info)
+    if n > 1:  # `analyze --gpu-probe` runs --quick: a short peer pass (64 MiB per pair)
+        report["peers"], probs = peer_check(probe, n, quick)
+        report["problems"] += probs
     return report
 
 
@@ -141,6 +181,11 @@ def main(argv=None):
                 f"HBM={dev['hbm_total_bytes'] / 1e9:.0f}GB selftest_err={dev['mfma_selftest_max_abs_err']} "
                 f"hbm={dev.get('hbm_copy_gbps')}GB/s mfma_bf16={dev.get('mfma_bf16_tflops')}TF/s"
             )
+        peers = rep.get("peers") or []
+        if peers:
+            rates = sorted(p["copy_gbps"] for p in peers)
+            print(f"peers: {sum(p['peer_access'] for p in peers)}/{len(peers)} pairs with peer access, copy "
+                  f"{rates[0]:.0f}-{rates[-1]:.0f} GB/s (median {rates[len(rates) // 2]:.0f})")
         for p in rep["problems"]:
             print(f"problem: {p}")
     return 1 if rep["problems"] else 0

@@ -237,4 +237,56 @@ double gp_mfma_bf16_tflops(int dev, int iters) {
   return flops / (ms * 1e-3) / 1e12;
 }
 
+// 1 when device `a` can map device `b`'s memory (peer access over xGMI), 0 when not, -1 on error.
+int gp_peer_access(int a, int b) {
+  int ok = 0;
+  if (hipDeviceCanAccessPeer(&ok, a, b) != hipSuccess) return -1;
+  return ok ? 1 : 0;
+}
+
+// Device a -> device b copy bandwidth in GB/s (hipMemcpyPeerAsync on a stream of device a, peer
+// access enabled both ways when possible), or -1 on error. On MI355X nodes this is an xGMI
+// link; a pair far below the others is a degraded link or a copy staged through the host.
+double gp_peer_copy_gbps(int a, int b, size_t bytes, int iters) {
+  if (a == b || iters < 1 || bytes == 0) return -1;
+  void *src = nullptr, *dst = nullptr;
+  if (hipSetDevice(b) != hipSuccess || hipMalloc(&dst, bytes) != hipSuccess) return -1;
+  int can = 0;
+  hipDeviceCanAccessPeer(&can, b, a);
+  if (can) hipDeviceEnablePeerAccess(a, 0);  // hipErrorPeerAccessAlreadyEnabled is fine
+  (void)hipGetLastError();
+  if (hipSetDevice(a) != hipSuccess || hipMalloc(&src, bytes) != hipSuccess) {
+    hipSetDevice(b);
+    hipFree(dst);
+    return -1;
+  }
+  hipDeviceCanAccessPeer(&can, a, b);
+  if (can) hipDeviceEnablePeerAccess(b, 0);
+  (void)hipGetLastError();
+  hipMemset(src, 1, bytes);
+  hipStream_t st;
+  hipEvent_t e0, e1;
+  double gbps = -1;
+  if (hipStreamCreate(&st) == hipSuccess) {
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipMemcpyPeerAsync(dst, b, src, a, bytes, st);  // warm-up (first touch, link training)
+    hipEventRecord(e0, st);
+    for (int i = 0; i < iters; ++i) hipMemcpyPeerAsync(dst, b, src, a, bytes, st);
+    hipEventRecord(e1, st);
+    if (hipEventSynchronize(e1) == hipSuccess) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      if (ms > 0) gbps = (double)bytes * iters / (ms * 1e-3) / 1e9;
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    hipStreamDestroy(st);
+  }
+  hipFree(src);
+  hipSetDevice(b);
+  hipFree(dst);
+  return gbps;
+}
+
 }  // extern "C"

@@ -25,3 +25,17 @@ def test_gpucheck_report():
 
     rep = gpucheck.run(quick=True)
     assert rep["devices"] and not [p for p in rep["problems"] if "MFMA" in p]
+
+
+def test_peer_probe_on_this_box():
+    """The xGMI peer probe: a device is never its own peer; with several visible devices every
+    ordered pair gets a copy rate (the driver's 8-GPU node; a 1-GPU box has no pairs)."""
+    from devspace_amd import gpucheck
+
+    probe = gpucheck.Probe()
+    assert probe.peer_gbps(0, 0) == -1
+    n = probe.count()
+    pairs, problems = gpucheck.peer_check(probe, n)
+    assert len(pairs) == n * (n - 1)
+    for p in pairs:
+        assert p["copy_gbps"] > 0, p
