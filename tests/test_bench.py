@@ -37,6 +37,7 @@ def test_bench_cpu_tiny():
     # same-box reference column of the headline (compat protocol + reference waits)
     assert d["reference_equivalent"]["p50_ms"] > d["value"], r.stderr[-3000:]
     assert d["reference_equivalent"]["sync_p50_ms"] > d["sync_p50_ms"]
+    assert 0 < d["dev_start_s"] < d["reference_equivalent"]["dev_start_s"], (d["dev_start_s"], d["reference_equivalent"])
     # the tool alone (cold restarts, no standby pool) against the same reference column
     cold = d["cold_restart"]
     assert cold["n"] >= 10 and cold["p50_ms"] > 0, cold
