@@ -302,20 +302,40 @@ struct Session::Progress {
   }
 };
 
+const std::vector<std::string>& helper_dirs() {
+  static const std::vector<std::string> dirs = {"/tmp", "/dev/shm", "/var/tmp", "$HOME"};
+  return dirs;
+}
+
+std::string helper_probe_script(const std::string& file, const std::vector<std::string>& dirs) {
+  std::string list;
+  for (auto& d : dirs) list += (d[0] == '$' ? "\"" + d + "\"" : shell_quote(d)) + " ";
+  // a one-line `#!/bin/sh` script run from the directory tells a noexec mount apart
+  return "dsd=; dss=; if [ \"$(uname -m 2>/dev/null)\" = x86_64 ]; then for d in " + list +
+         "; do if [ -n \"$d\" ] && [ -x \"$d/" + file + "\" ]; then dsd=$d; dss=HAVE; break; fi; done; fi; "
+         "if [ -z \"$dsd\" ] && [ \"$(uname -m 2>/dev/null)\" = x86_64 ]; then for d in " + list +
+         "; do [ -n \"$d\" ] || continue; if mkdir -p \"$d\" 2>/dev/null && [ -w \"$d\" ] && printf '#!/bin/sh\\nexit 0\\n' > \"$d/.devspace-x$$\" "
+         "2>/dev/null && chmod +x \"$d/.devspace-x$$\" 2>/dev/null && \"$d/.devspace-x$$\" 2>/dev/null; then "
+         "rm -f \"$d/.devspace-x$$\"; dsd=$d; dss=NEED; break; fi; rm -f \"$d/.devspace-x$$\" 2>/dev/null; done; fi; "
+         "if [ -n \"$dsd\" ]; then echo \"$dss $dsd\"; else echo NOHELPER; fi\n";
+}
+
 bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out) {
-  // Probe architecture + writable /tmp, upload the static helper once (content-addressed),
-  // then exec it in place of the shell.
+  // Probe architecture + a writable directory that allows exec, upload the static helper once
+  // (content-addressed), then exec it in place of the shell.
   if (o_.helper_path.empty() || !fs::is_file(o_.helper_path)) return false;
   std::string bin;
   if (!fs::read_file(o_.helper_path, &bin)) return false;
-  std::string name = "/tmp/devspace-helper-" + sha256_hex(bin).substr(0, 16);
-  std::string probe = "if [ \"$(uname -m 2>/dev/null)\" = x86_64 ] && mkdir -p /tmp && [ -w /tmp ]; then if [ -x " +
-                      name + " ]; then echo HAVE; else echo NEED; fi; else echo NOHELPER; fi\n";
-  if (!write_all(sh->in(), probe)) return false;
+  std::string file = "devspace-helper-" + sha256_hex(bin).substr(0, 16);
+  if (!write_all(sh->in(), helper_probe_script(file, helper_dirs()))) return false;
   std::string line;
   if (!out.read_line(&line, 15000)) return false;
-  if (line == "NOHELPER") return false;
-  if (line == "NEED") {
+  if (line == "NOHELPER" || line.size() < 6 || (!starts_with(line, "HAVE ") && !starts_with(line, "NEED "))) {
+    logf("[Sync] No directory in the container can hold and run the helper (" + line + ")");
+    return false;
+  }
+  std::string name = shell_quote(line.substr(5) + "/" + file);
+  if (starts_with(line, "NEED ")) {
     std::string up = "echo " + std::string(kStart) + "; head -c " + std::to_string(bin.size()) + " > " + name +
                      ".tmp && chmod +x " + name + ".tmp && mv " + name + ".tmp " + name + "; echo " + kDone + "\n";
     if (!write_all(sh->in(), up)) return false;

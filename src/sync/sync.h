@@ -38,7 +38,15 @@ namespace ds {
 namespace sync {
 
 enum class Mode { Compat, Fast, Helper };
-Mode parse_mode(const std::string& s);  // compat|fast|helper (default fast); env DEVSPACE_SYNC_MODE
+Mode parse_mode(const std::string& s);
+
+// Shell snippet that picks where the in-container helper lives: the first of `dirs` that already
+// holds an executable `<dir>/<file>` ("HAVE <dir>"), else the first that is writable and lets a
+// file in it execute ("NEED <dir>"; hardened pods mount /tmp noexec), else "NOHELPER" (also on a
+// non-x86_64 container: the helper is a static x86_64 binary).
+std::string helper_probe_script(const std::string& file, const std::vector<std::string>& dirs);
+// Where the helper is looked for in a container, in order.
+const std::vector<std::string>& helper_dirs();  // compat|fast|helper (default fast); env DEVSPACE_SYNC_MODE
 const char* mode_name(Mode m);
 
 struct FileInfo {

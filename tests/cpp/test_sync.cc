@@ -12,6 +12,7 @@
 
 #include "core/fs.h"
 #include "core/log.h"
+#include "core/proc.h"
 #include "core/strutil.h"
 #include "kube/client.h"
 #include "sync/frame.h"
@@ -621,4 +622,31 @@ TEST(sync_chunk_stream_codes_chunks_by_entropy) {
   bad[10] ^= 0x55;  // inside the first (deflated) chunk
   sync::frame::ChunkReader cr2(string_source(&bad));
   EXPECT_THROWS(cr2.drain());
+}
+
+// The helper's directory probe (hardened pods mount /tmp noexec): the first candidate that
+// already holds the helper wins, else the first writable one where a file can execute.
+TEST(sync_helper_probe_picks_a_usable_directory) {
+  auto run = [](const std::string& script) {
+    std::string path = "/tmp/ds-probe-" + std::to_string(getpid()) + ".sh";
+    fs::write_file(path, script);
+    RunResult r = ds::run({"sh", path}, "", {}, 20000);
+    ::unlink(path.c_str());
+    return trim(r.out);
+  };
+  std::string base = "/tmp/ds-helper-probe-" + std::to_string(getpid());
+  fs::remove_all(base);
+  fs::mkdirs(base + "/b");
+  // /proc refuses a new directory: skipped; the next candidate is created and usable
+  std::string out = run(sync::helper_probe_script("devspace-helper-x", {"/proc/ds-no-such", base + "/a", base + "/b"}));
+  EXPECT_EQ(out, "NEED " + base + "/a");
+  // an executable helper already in a later candidate is reused before uploading anew
+  fs::write_file(base + "/b/devspace-helper-x", "#!/bin/sh\n");
+  ::chmod((base + "/b/devspace-helper-x").c_str(), 0755);
+  out = run(sync::helper_probe_script("devspace-helper-x", {base + "/a", base + "/b"}));
+  EXPECT_EQ(out, "HAVE " + base + "/b");
+  EXPECT_TRUE(!fs::exists(base + "/a/.devspace-x"));
+  out = run(sync::helper_probe_script("devspace-helper-x", {"/proc/ds-no-such"}));
+  EXPECT_EQ(out, "NOHELPER");
+  fs::remove_all(base);
 }
