@@ -47,17 +47,17 @@ def test_probe_without_devspace_amd_in_image(gpu_node, tmp_path):
     if not has_kfd:
         assert "no /dev/kfd in the container" in out, out
     try:
-        import torch
-
-        cuda = torch.cuda.is_available()
+        import torch  # noqa: F401
     except Exception:
-        torch, cuda = None, False
+        torch = None
+    # what the pod (not this test process) sees decides which fallback report it gives
     if torch is None:
         assert "PyTorch is not importable" in out, out
-    elif not cuda:
+    elif "checked by the torch probe" in out:  # a real GPU in the pod: the bf16 matmul check ran
+        assert has_kfd and "bf16 matmul rel err" in out, out
+        assert "GPU probe unavailable" not in out and "matmul mismatch" not in out, out
+    else:
         assert "torch.cuda.is_available() is False" in out, out
-    else:  # a real GPU: the torch fallback ran its bf16 matmul check and found nothing
-        assert "No problems found" in out or "GPU" not in out, out
 
 
 def test_probe_without_python_reports_unavailable(gpu_node, tmp_path):
