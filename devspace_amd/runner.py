@@ -212,16 +212,21 @@ class Agreement:
 
         self.dist = dist
         self.group = group if group is not None else dist.new_group(backend="gloo")
-        self.ctl = torch.zeros(2, dtype=torch.int64)  # [newest generation, helper modules changed]
+        # [newest generation, helper modules changed, a rank was told to stop (SIGTERM)]
+        self.ctl = torch.zeros(3, dtype=torch.int64)
         self.flag = torch.zeros(1, dtype=torch.int64)
         self.calls = 0
 
-    def boundary(self, pending_gen: int, helper_pending: bool):
+    def boundary(self, pending_gen: int, helper_pending: bool, stop: bool = False):
+        """(agreed generation, helper modules changed, stop): all ranks leave the loop at the
+        same boundary when any of them got SIGTERM, so none is left waiting in a collective
+        of a step the others never start."""
         self.ctl[0] = pending_gen
         self.ctl[1] = int(helper_pending)
+        self.ctl[2] = int(stop)
         self.dist.all_reduce(self.ctl, op=self.dist.ReduceOp.MAX, group=self.group)
         self.calls += 1
-        return int(self.ctl[0]), bool(self.ctl[1])
+        return int(self.ctl[0]), bool(self.ctl[1]), bool(self.ctl[2])
 
     def preempt(self, pending: bool) -> bool:
         self.flag[0] = int(pending)
@@ -483,7 +488,7 @@ def worker_main(args) -> int:
         stop = True
 
     signal.signal(signal.SIGTERM, _term)
-    while not stop:
+    while agree is not None or not stop:
         # 1. pick up local change notifications (non-blocking while training; blocking when idle)
         timeout = 0 if (not script_mode and args.train) else 0.05
         n_changes, t_first, helper_changed = feed.take(timeout)
@@ -499,7 +504,9 @@ def worker_main(args) -> int:
         #    whether helper modules must be re-imported (rank 0's view, like the generation)
         target = pending_gen
         if agree is not None:
-            target, agreed_helper = agree.boundary(pending_gen, helper_pending)
+            target, agreed_helper, agreed_stop = agree.boundary(pending_gen, helper_pending, stop)
+            if agreed_stop:
+                break
             pending_gen = max(pending_gen, target)
             helper_pending = helper_pending or agreed_helper
         if target > gen:

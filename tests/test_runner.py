@@ -220,7 +220,7 @@ def test_control_plane_never_touches_the_device():
                                  new_group=lambda backend: f"group:{backend}")
     a = runner.Agreement(fake)
     assert a.group == "group:gloo"
-    assert a.boundary(7, True) == (7, True)
+    assert a.boundary(7, True) == (7, True, False)
     assert a.preempt(True) is True and a.preempt(False) is False
     assert calls and all(c == ("cpu", "group:gloo", "max") for c in calls), calls
 
@@ -465,3 +465,39 @@ def test_inotify_watcher_returns_a_rename_at_once(tmp_path):
         assert took < 0.05, took  # events already queued: no multi-ms burst wait
     finally:
         w.close()
+
+
+def _agree_stop_worker(rank, world, init_file, out):
+    import torch.distributed as dist
+
+    from devspace_amd import runner
+
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    try:
+        agree = runner.Agreement(dist)
+        first = agree.boundary(3, False, stop=False)
+        second = agree.boundary(3 + rank, rank == 0, stop=(rank == world - 1))  # only the last rank got SIGTERM
+        out.put((rank, first, second))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_agreement_stops_every_rank_at_the_same_boundary(tmp_path):
+    """SIGTERM reaches the ranks at different moments: the stop flag is agreed like the
+    generation, so every rank leaves at the same step boundary (none is left waiting in a
+    collective of a step the others never start)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    world = 3
+    procs = [ctx.Process(target=_agree_stop_worker, args=(r, world, str(tmp_path / "init"), out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(out.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, first, second in res:
+        assert first == (3, False, False)
+        assert second == (3 + world - 1, True, True), (rank, second)
