@@ -66,6 +66,11 @@ def render(path):
                          _ms(ref.get("p50_ms")) + _x(cold["p50_ms"], ref.get("p50_ms"))))
         rows.append(("sync p50, quickstart (edit → bytes in the pod)", f"**{_ms(b.get('sync_p50_ms'))}**",
                      _ms(ref.get("sync_p50_ms")) + _x(b.get("sync_p50_ms"), ref.get("sync_p50_ms"))))
+        if b.get("dev_start_s") is not None:
+            rows.append(("`devspace dev` start → app answering through the forward, quickstart",
+                         f"{_s(b['dev_start_s'])}",
+                         _s(ref.get("dev_start_s")) + _x(b["dev_start_s"], ref.get("dev_start_s"))
+                         if ref.get("dev_start_s") else "—"))
         g = b.get("gpu_pod")
         if isinstance(g, dict) and "reload_p50_ms" in g:
             gr = g.get("reference_equivalent", {})
