@@ -427,7 +427,9 @@ def worker_main(args) -> int:
     if world > 1:
         import torch.distributed as dist  # noqa: WPS433
 
-        backend = "nccl" if device.type == "cuda" else "gloo"  # nccl == RCCL on ROCm
+        # nccl == RCCL on ROCm; DEVSPACE_DIST_BACKEND=gloo runs several ranks on one GPU (RCCL
+        # refuses two ranks on a device): a 1-GPU rehearsal of the multi-rank pod
+        backend = os.environ.get("DEVSPACE_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     if device.type == "cuda" and args.gemm_tuning != "off":
         try:

@@ -171,6 +171,8 @@ ENV = {
     "DEVSPACE_TRACE": "`0` disables the phase spans written to `.devspace/logs/trace.jsonl`.",
     "DEVSPACE_VAR_<NAME>": "Value of config variable `${NAME}`; no question is asked for it.",
     # workload kit (devspace_amd/), read inside GPU pods
+    "DEVSPACE_DIST_BACKEND": "Process-group backend of the runner's ranks (default `nccl`, i.e. RCCL, on GPUs and "
+                             "`gloo` on CPUs); `gloo` lets several ranks share one GPU for a rehearsal.",
     "DEVSPACE_GEMM_TUNING": "GEMM kernel selection of the runner: `off` (default), `shipped` (pre-tuned "
                             "gfx950 table) or `online` (tune unseen shapes, persist them).",
     "DEVSPACE_GEMM_TUNING_FILE": "Where `online` GEMM tuning persists its table.",

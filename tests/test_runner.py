@@ -93,6 +93,15 @@ def test_runner_hot_reload_gpu(tmp_path):
     assert "gen=2" in line
 
 
+@pytest.mark.gpu
+def test_runner_hot_reload_two_ranks_on_the_gpu(tmp_path):
+    """The multi-rank pod on real GPU streams (DDP, generation agreement, GPU-side preemption
+    drain): two ranks on the one device of the box, joined over gloo (RCCL refuses two ranks on
+    one GPU; the 8-GPU node runs RCCL)."""
+    line = _run_reload(tmp_path, {"DEVSPACE_DIST_BACKEND": "gloo"}, nproc=2)
+    assert "gen=2" in line and "world=2" in line and "device=cuda" in line, line
+
+
 SLOW_STEP = '''
 import time
 MARKER = "v0"
