@@ -146,10 +146,10 @@ def step(ctx, state):
 '''
 
 
-def _pickup_ms(tmp_path, preempt, src=SLOW_STEP, gpu=False, nproc=1):
+def _pickup_ms(tmp_path, preempt, src=SLOW_STEP, gpu=False, nproc=1, extra_env=None):
     p = tmp_path / "slow.py"
     p.write_text(src)
-    env = dict(os.environ, PYTHONPATH=ROOT)
+    env = dict(os.environ, PYTHONPATH=ROOT, **(extra_env or {}))
     if not gpu:
         env.update(HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1")
     cmd = [sys.executable, "-u", "-m", "devspace_amd.runner", "--nproc", str(nproc), "--watch", str(tmp_path), str(p)]
@@ -256,6 +256,16 @@ def test_preempt_point_drains_gpu_queue(tmp_path):
     assert period > 100, period
     # edit -> new step done <= rest of the phase in flight (<= half a step) + one full new step;
     # without the drain it is the rest of the whole step + one new step (up to two periods)
+    assert pickup < 1.6 * period, (pickup, period)
+
+
+@pytest.mark.gpu
+def test_preempt_point_drains_gpu_queue_two_ranks(tmp_path):
+    """The same with two ranks on the GPU: each drains its own queue, then the ranks decide
+    together, so both leave the long step at the same point."""
+    pickup, period = _pickup_ms(tmp_path, preempt=True, src=SLOW_STEP_GPU, gpu=True, nproc=2,
+                                extra_env={"DEVSPACE_DIST_BACKEND": "gloo"})
+    assert period > 100, period
     assert pickup < 1.6 * period, (pickup, period)
 
 
