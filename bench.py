@@ -201,6 +201,8 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         env = devspace_env(cluster, base)
         env["DEVSPACE_NPROC"] = str(nproc)  # used when the pod requests no GPU (CPU smoke)
         cluster.kubelet.extra_env["DEVSPACE_NPROC"] = str(nproc)
+        if os.environ.get("DEVSPACE_DIST_BACKEND"):  # rehearsal: N ranks sharing fewer GPUs (gloo)
+            cluster.kubelet.extra_env["DEVSPACE_DIST_BACKEND"] = os.environ["DEVSPACE_DIST_BACKEND"]
         # `devspace dev` builds (dev image cache), deploys the chart, waits for the rollout,
         # then starts sync + attach on the newest running pod.
         t_dev = time.perf_counter()
