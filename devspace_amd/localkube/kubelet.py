@@ -509,12 +509,24 @@ class Kubelet:
         # view): map through the host's own HIP_VISIBLE_DEVICES when it restricts devices.
         host_vis = [v.strip() for v in os.environ.get("HIP_VISIBLE_DEVICES", "").split(",") if v.strip()]
         if rt.gpus:
-            env["HIP_VISIBLE_DEVICES"] = ",".join(host_vis[g] if g < len(host_vis) else str(g) for g in rt.gpus)
+            # A node configured with more GPUs than the host has (a bench rehearsal of N ranks on a
+            # smaller box) maps its extra indices onto the real devices instead of naming devices
+            # this process may not use.
+            real = self._real_gpus()
+            ids = [host_vis[g] if g < len(host_vis) else str(g) for g in ((g % real if real else g) for g in rt.gpus)]
+            env["HIP_VISIBLE_DEVICES"] = ",".join(dict.fromkeys(ids))
         elif self.gpus_total:
             env["HIP_VISIBLE_DEVICES"] = "-1"  # no amd.com/gpu request: no GPU access
         elif host_vis:
             env["HIP_VISIBLE_DEVICES"] = ",".join(host_vis)
         return env
+
+    def _real_gpus(self):
+        if not hasattr(self, "_real_gpu_count"):
+            from .cluster import detect_gpus  # noqa: WPS433 - cluster imports this module
+
+            self._real_gpu_count = detect_gpus()
+        return self._real_gpu_count
 
     def workdir(self, c):
         wd = c.spec.get("workingDir") or c.image_config.get("WorkingDir") or "/"
