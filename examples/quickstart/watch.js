@@ -97,16 +97,23 @@ function resize(ready) {
   } else if (nStandby > minStandby && now - lastMiss > 30000) {
     lastMiss = now;  // one step down per quiet 30 s
     nStandby--;
-    const extra = standbys.length - nStandby;
-    if (extra > 0) for (const x of standbys.splice(standbys.length - extra, extra)) x.kill('SIGKILL');
+    // drop standbys still booting first, then the youngest booted ones
+    let extra = standbys.length - nStandby;
+    for (let k = standbys.length - 1; k >= 0 && extra > 0; k--) {
+      if (!standbys[k].ready) {
+        standbys.splice(k, 1)[0].kill('SIGKILL');
+        extra--;
+      }
+    }
+    for (; extra > 0; extra--) standbys.pop().kill('SIGKILL');
   }
 }
 
 function start() {
   gen++;
   // a booted standby if there is one, else the one that started booting first
-  const i = standbys.findIndex((s) => s.ready);
-  if (gen > 1) resize(i >= 0);  // the first start has no pool yet: not a miss
+  if (gen > 1) resize(standbys.some((x) => x.ready));  // the first start has no pool yet: not a miss
+  const i = standbys.findIndex((x) => x.ready);  // after resize: a shrink may drop pool members
   const s = standbys.splice(i >= 0 ? i : 0, 1)[0];
   if (s) {
     s.removeAllListeners('message');
