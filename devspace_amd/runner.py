@@ -472,7 +472,7 @@ def worker_main(args) -> int:
         ctx._drain_min_ms = args.preempt_drain_ms
     ctx.log(
         f"started gen={gen} marker={getattr(mod, 'MARKER', '')} digest={mod.__devspace_digest__} "
-        f"world={world} device={device} loss={first.get('loss') if isinstance(first, dict) else None} "
+        f"world={world} device={device} backend={dist.get_backend() if dist is not None else 'none'} loss={first.get('loss') if isinstance(first, dict) else None} "
         f"startup_ms={(time.perf_counter() - t_start) * 1000.0:.1f} "
         f"kit={os.path.dirname(os.path.dirname(os.path.abspath(__file__)))}"
     )
