@@ -30,6 +30,7 @@ const dir = path.dirname(script);
 const ignored = /(^|\/)(node_modules|\.git|\.devspace)(\/|$)|\.sw.$|~$/;
 const minStandby = Math.max(0, parseInt(process.env.WATCH_STANDBY || '4', 10) || 0);
 const maxStandby = minStandby && Math.max(minStandby, parseInt(process.env.WATCH_STANDBY_MAX || '8', 10) || 0);
+const shrinkMs = parseInt(process.env.WATCH_STANDBY_SHRINK_MS || '30000', 10) || 30000;
 let nStandby = minStandby;
 let lastMiss = 0;  // time of the last restart that found no booted standby
 // The standby's whole program: load the core modules a server needs (node loads them lazily,
@@ -94,8 +95,8 @@ function resize(ready) {
   if (!ready && nStandby > 0) {
     lastMiss = now;
     nStandby = Math.min(maxStandby, nStandby + 1);
-  } else if (nStandby > minStandby && now - lastMiss > 30000) {
-    lastMiss = now;  // one step down per quiet 30 s
+  } else if (nStandby > minStandby && now - lastMiss > shrinkMs) {
+    lastMiss = now;  // one step down per quiet period (WATCH_STANDBY_SHRINK_MS, 30 s)
     nStandby--;
     // drop standbys still booting first, then the youngest booted ones
     let extra = standbys.length - nStandby;

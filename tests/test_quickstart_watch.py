@@ -89,6 +89,32 @@ def test_watch_restarts_fresh_main_module(tmp_path, standby):
         assert not os.path.exists(f"/proc/{pid}") or open(f"/proc/{pid}/stat").read().split()[2] == "Z"
 
 
+def test_standby_pool_shrinks_after_a_quiet_period(tmp_path):
+    """After a burst grew the pool, a restart after a quiet period gives one standby back."""
+    import psutil
+
+    app = tmp_path / "index.js"
+    app.write_text("require('http').createServer((q, r) => r.end('v0')).listen(0);\n")
+    shutil.copy(os.path.join(ROOT, "examples", "quickstart", "watch.js"), tmp_path / "watch.js")
+    p = subprocess.Popen(["node", str(tmp_path / "watch.js"), str(app)], cwd=tmp_path, stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT, text=True,
+                         env=dict(os.environ, WATCH_STANDBY="1", WATCH_STANDBY_MAX="4", WATCH_STANDBY_SHRINK_MS="1500"))
+    try:
+        time.sleep(1.0)
+        for i in range(12):
+            app.write_text(f"require('http').createServer((q, r) => r.end('v{i + 1}')).listen(0);\n")
+            time.sleep(0.02)
+        time.sleep(2.5)  # settle, and longer than the shrink period
+        grown = len(psutil.Process(p.pid).children())
+        app.write_text("require('http').createServer((q, r) => r.end('quiet')).listen(0);\n")
+        time.sleep(2.0)
+        after = len(psutil.Process(p.pid).children())
+        assert after == grown - 1, (grown, after)
+    finally:
+        p.terminate()
+        p.wait(10)
+
+
 def test_standby_pool_grows_under_back_to_back_edits(tmp_path):
     """Edits faster than node boots exhaust the standby pool: the watcher adds standbys (up to
     WATCH_STANDBY_MAX) instead of handing restarts to processes still booting."""
