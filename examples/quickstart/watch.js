@@ -18,7 +18,7 @@
 // The pool adapts to the edit rate: it starts at WATCH_STANDBY (default 4) standbys, grows by
 // one (up to WATCH_STANDBY_MAX, default 8) whenever a restart finds none of them booted —
 // back-to-back saves (format-on-save, generated files, a script editing in a loop) come faster
-// than node boots — and gives one back after 30 s without such a miss. A standby that finished
+// than node boots — and gives one back after 30 s (WATCH_STANDBY_SHRINK_MS) without such a miss. A standby that finished
 // booting a while ago also starts the app faster than a just-booted one (~10 ms on the MI355X
 // box, profiles/r3_qs_standby_probe.txt). WATCH_STANDBY=0 gives plain cold restarts.
 const {spawn} = require('child_process');

@@ -12,6 +12,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import shutil
 import statistics
 import sys
@@ -44,7 +45,8 @@ def main():
             s = s.replace("    child.send({script});", "    T('handoff');\n    child.send({script});")
             s = s.replace("  if (!name || ignored.test(name)", "  T('event');\n  if (!name || ignored.test(name)")
             if a.standby is not None:
-                s = s.replace("process.env.WATCH_STANDBY || '2'", "'%d'" % a.standby)
+                s, n = re.subn(r"process\.env\.WATCH_STANDBY \|\| '\d+'", "'%d'" % a.standby, s)
+                assert n == 1, "watch.js no longer reads WATCH_STANDBY this way"
             s = s.replace("  console.log('[watch] started gen='", "  T(s && s.ready ? 'ready' : 'booting');\n  console.log('[watch] started gen='")
             open(w, "w").write(s)
             i = os.path.join(dst, "index.js")
