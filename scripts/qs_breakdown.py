@@ -31,19 +31,25 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--standby", type=int, default=None, help="watch.js standby count (default: its own)")
     a = ap.parse_args()
+    NOW = "(require('perf_hooks').performance.timeOrigin + require('perf_hooks').performance.now())"
     trace = tempfile.mktemp(prefix="qs-trace-")
     real_copytree = shutil.copytree
 
     def copytree(src, dst, *args, **kw):
         r = real_copytree(src, dst, *args, **kw)
         if str(getattr(src, "path", src)).endswith(os.path.join("examples", "quickstart")):
-            t = "const T = (m) => require('fs').appendFileSync(%s, m + ' ' + Date.now() + '\\n');\n" % json.dumps(trace)
+            # sub-millisecond epoch clock shared by every node process (Date.now() is whole ms)
+            t = "const T = (m) => require('fs').appendFileSync(%s, m + ' ' + %s + '\\n');\n" % (json.dumps(trace), NOW)
             w = os.path.join(dst, "watch.js")
             s = open(w).read()
             s = s.replace("const {spawn} = require('child_process');", "const {spawn} = require('child_process');\n" + t)
             s = s.replace("  restarting = true;\n  child.kill('SIGTERM');", "  restarting = true;\n  T('kill');\n  child.kill('SIGTERM');")
             s = s.replace("    child.send({script});", "    T('handoff');\n    child.send({script});")
             s = s.replace("  if (!name || ignored.test(name)", "  T('event');\n  if (!name || ignored.test(name)")
+            # inside the standby (its program is a string in watch.js): go message in, app start
+            mark = "require('fs').appendFileSync('%s', '%%s ' + %s + '\\\\n'); " % (trace, NOW)
+            s = s.replace('"sent = true; if (warm)', '"' + mark % "go" + 'sent = true; if (warm)')
+            s = s.replace('"require(\'module\').runMain(); });"', '"' + mark % "main" + 'require(\'module\').runMain(); });"')
             if a.standby is not None:
                 s, n = re.subn(r"process\.env\.WATCH_STANDBY \|\| '\d+'", "'%d'" % a.standby, s)
                 assert n == 1, "watch.js no longer reads WATCH_STANDBY this way"
@@ -52,8 +58,8 @@ def main():
             i = os.path.join(dst, "index.js")
             s = open(i).read()
             s = s.replace("}).listen(port, () => console.log(",
-                          "}).listen(port, () => require('fs').appendFileSync(%s, 'listening ' + Date.now() + '\\n') || "
-                          "console.log(" % json.dumps(trace))
+                          "}).listen(port, () => require('fs').appendFileSync(%s, 'listening ' + %s + '\\n') || "
+                          "console.log(" % (json.dumps(trace), NOW))
             open(i, "w").write(s)
         return r
 
@@ -95,7 +101,7 @@ def main():
         for t, k in after:
             first.setdefault(k, t)
         row = {"sync": m.get("synced", 0) - m["edit"]}
-        for k in ("event", "kill", "handoff", "listening"):
+        for k in ("event", "kill", "handoff", "go", "main", "listening"):
             if k in first:
                 row[k] = first[k] - m["edit"]
         # the restart's hand-off went to a booted standby, or to one still booting
@@ -105,7 +111,7 @@ def main():
         if "got" in m:
             row["response"] = m["got"] - m["edit"]
         rows.append(row)
-    keys = ["sync", "event", "kill", "handoff", "listening", "response"]
+    keys = ["sync", "event", "kill", "handoff", "go", "main", "listening", "response"]
     print("ms after the edit (p50 over %d edits): " % len(rows) +
           ", ".join("%s %.2f" % (k, statistics.median([x[k] for x in rows if k in x])) for k in keys
                     if any(k in x for x in rows)))
