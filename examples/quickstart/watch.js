@@ -34,8 +34,8 @@ const shrinkMs = parseInt(process.env.WATCH_STANDBY_SHRINK_MS || '30000', 10) ||
 let nStandby = minStandby;
 let lastMiss = 0;  // time of the last restart that found no booted standby
 // The standby's whole program: load the core modules a server needs (node loads them lazily,
-// and they are shared, stateless code: nothing of the app), wait for the go message, drop the
-// IPC channel (the app must not see a parent channel) and run the script as the main module.
+// and they are shared, stateless code: nothing of the app), wait for the go signal, close its
+// pipe to the watcher (the app must not see it) and run the script as the main module.
 // `cluster` and `child_process` are in the list because net's listen() loads them on first
 // use. The boot also warms the runtime paths every server takes once: it compiles a module
 // from a string (the CommonJS wrapper/compiler), and it serves one HTTP request to itself on an
@@ -44,7 +44,7 @@ let lastMiss = 0;  // time of the last restart that found no booted standby
 // process took 6-9 ms to reach its callback and 0.4 ms after a listen warm-up
 // (scripts/node_boot_probe.py); the first request to the new server took 7.7 ms after the
 // listen warm-up and 1.8 ms after the request warm-up (CPU container). Nothing of the app runs
-// before the go message.
+// before the go signal.
 const PRELOAD = ['http', 'https', 'net', 'url', 'querystring', 'stream', 'events', 'util', 'crypto',
                  'zlib', 'os', 'fs', 'path', 'buffer', 'string_decoder', 'timers', 'dns', 'cluster',
                  'child_process'];
@@ -58,18 +58,28 @@ const WARM = "const M = require('module'); const w = new M('/.watch-warm.js'); "
     "const req = http.get({host: '127.0.0.1', port: ws.address().port, path: '/', agent: false}, (res) => { " +
     "res.resume(); res.on('end', done); res.on('error', done); }); req.on('error', done); " +
     "} catch (e) { done(); } });\n";
-// A standby can be handed the script before its warm-up finished (a restart that found none
-// booted): the go message then ends the warm-up (its server closes, `ready` turns into a no-op
-// so nothing is sent on the channel the app must not see) and the app runs.
-const BOOT = `for (const m of ${JSON.stringify(PRELOAD)}) { try { require(m); } catch (e) {} }\n` +
+// The hand-off goes by a signal, not a message: the standby talks to the watcher on a plain
+// pipe (fd 3: 'b' once its SIGUSR2 handler is installed, 'r' once warmed up) and starts the app
+// on SIGUSR2, after closing fd 3. Node's IPC channel cost more: on the MI355X box the old
+// server's kill -> new server listening went from 4.31 to 3.55 ms and the loop's p90 dropped
+// 0.3-0.5 ms (profiles/r3_watch_signal_handoff_ab.txt), most of the gap in
+// process.disconnect(). The app sees no trace of either: no process.send, no fd 3, no SIGUSR2
+// listener. The watcher signals only after 'b' (SIGUSR2's default action ends a
+// process that has no handler yet), and a standby exits when the pipe's other end closes (the
+// watcher died), as it did with the IPC channel. A standby can be handed the script before its
+// warm-up finished (a restart that found none booted): the go then ends the warm-up (its server
+// closes, `ready` turns into a no-op) and the app runs.
+const BOOT = "const ctl = new (require('net').Socket)({fd: 3, readable: true, writable: true});\n" +
+    "ctl.on('error', () => {}); ctl.on('end', () => process.exit(0)); ctl.resume();\n" +
     "let sent = false, warm = null;\n" +
-    "function ready() { if (!sent) { sent = true; if (process.connected) process.send('ready'); } }\n" +
-    `try { ${WARM} } catch (e) { ready(); }\n` +
-    "process.once('message', (m) => { " +
+    "process.once('SIGUSR2', () => { " +
     "sent = true; if (warm) { try { warm.close(); } catch (e) {} warm = null; } " +
-    "process.argv[1] = m.script; process.disconnect(); " +
-    "for (const k of ['send', 'disconnect', 'connected', 'channel']) { try { delete process[k]; } catch (e) {} } " +
-    "require('module').runMain(); });";
+    `ctl.removeAllListeners('end'); ctl.destroy(); process.argv[1] = ${JSON.stringify(script)}; ` +
+    "require('module').runMain(); });\n" +
+    "ctl.write('b');\n" +
+    `for (const m of ${JSON.stringify(PRELOAD)}) { try { require(m); } catch (e) {} }\n` +
+    "function ready() { if (!sent) { sent = true; ctl.write('r'); } }\n" +
+    `try { ${WARM} } catch (e) { ready(); }\n`;
 let child = null;
 let standbys = [];  // booting or booted, oldest first
 let pending = false;
@@ -78,10 +88,20 @@ let gen = 0;
 
 function bootStandbys() {
   while (standbys.length < nStandby) {
-    const s = spawn(process.execPath, ['-e', BOOT], {stdio: ['inherit', 'inherit', 'inherit', 'ipc']});
-    s.ready = false;
-    s.on('message', (m) => {
-      if (m === 'ready') s.ready = true;
+    const s = spawn(process.execPath, ['-e', BOOT], {stdio: ['inherit', 'inherit', 'inherit', 'pipe']});
+    s.armed = false;  // its SIGUSR2 handler is installed
+    s.ready = false;  // warmed up
+    s.onArmed = null;
+    s.stdio[3].on('error', () => {});
+    s.stdio[3].on('data', (d) => {
+      d = String(d);
+      if (d.includes('b')) s.armed = true;
+      if (d.includes('r')) s.ready = true;
+      if (s.armed && s.onArmed) {
+        const go = s.onArmed;
+        s.onArmed = null;
+        go();
+      }
     });
     s.on('exit', () => {
       standbys = standbys.filter((x) => x !== s);
@@ -117,9 +137,10 @@ function start() {
   const i = standbys.findIndex((x) => x.ready);  // after resize: a shrink may drop pool members
   const s = standbys.splice(i >= 0 ? i : 0, 1)[0];
   if (s) {
-    s.removeAllListeners('message');
     child = s;
-    child.send({script});
+    const go = () => s.kill('SIGUSR2');
+    if (s.armed) go();
+    else s.onArmed = go;
   } else {
     child = spawn(process.execPath, [script], {stdio: 'inherit'});
   }

@@ -44,12 +44,12 @@ def main():
             s = open(w).read()
             s = s.replace("const {spawn} = require('child_process');", "const {spawn} = require('child_process');\n" + t)
             s = s.replace("  restarting = true;\n  child.kill('SIGTERM');", "  restarting = true;\n  T('kill');\n  child.kill('SIGTERM');")
-            s = s.replace("    child.send({script});", "    T('handoff');\n    child.send({script});")
+            s = s.replace("    const go = () => s.kill('SIGUSR2');", "    const go = () => T('handoff') || s.kill('SIGUSR2');")
             s = s.replace("  if (!name || ignored.test(name)", "  T('event');\n  if (!name || ignored.test(name)")
             # inside the standby (its program is a string in watch.js): go message in, app start
             mark = "require('fs').appendFileSync('%s', '%%s ' + %s + '\\\\n'); " % (trace, NOW)
             s = s.replace('"sent = true; if (warm)', '"' + mark % "go" + 'sent = true; if (warm)')
-            s = s.replace('"require(\'module\').runMain(); });"', '"' + mark % "main" + 'require(\'module\').runMain(); });"')
+            s = s.replace('"require(\'module\').runMain(); });\\n"', '"' + mark % "main" + 'require(\'module\').runMain(); });\\n"')
             if a.standby is not None:
                 s, n = re.subn(r"process\.env\.WATCH_STANDBY \|\| '\d+'", "'%d'" % a.standby, s)
                 assert n == 1, "watch.js no longer reads WATCH_STANDBY this way"

@@ -18,7 +18,8 @@ NODE = shutil.which("node")
 APP = """const http = require('http');
 const port = process.env.PORT;
 const main = require.main === module;
-const st = typeof process.send + '/' + typeof process.connected;  // the IPC channel of a standby must not leak into the app
+// nothing of the standby's hand-off may leak into the app: no IPC channel, no SIGUSR2 listener
+const st = typeof process.send + '/' + typeof process.connected + '/' + process.listenerCount('SIGUSR2');
 http.createServer((req, res) => {
   res.end(JSON.stringify({tag: 'TAG', pid: process.pid, main, send: st, argv1: process.argv[1]}));
 }).listen(port);
@@ -71,7 +72,7 @@ def test_watch_restarts_fresh_main_module(tmp_path, standby):
             os.rename(tmp, app)  # how devspace sync lands a file
             r = _wait(lambda: (lambda b: b if b and b["tag"] == f"v{i}" else None)(_get(port)))
             assert r["main"] is True, r  # require.main === module, as under `node index.js`
-            assert r["send"] == "undefined/undefined", r
+            assert r["send"] == "undefined/undefined/0", r
             assert r["argv1"] == str(app), r
             assert r["pid"] not in pids, r  # a fresh process per edit
             pids.add(r["pid"])
@@ -87,6 +88,34 @@ def test_watch_restarts_fresh_main_module(tmp_path, standby):
     time.sleep(0.5)
     for pid in pids:
         assert not os.path.exists(f"/proc/{pid}") or open(f"/proc/{pid}/stat").read().split()[2] == "Z"
+
+
+def test_standbys_exit_when_the_watcher_is_killed(tmp_path):
+    """A standby holds only its status pipe to the watcher: SIGKILL of the watcher alone (no
+    process-group signal) closes that pipe and every standby exits."""
+    import psutil
+
+    app = tmp_path / "index.js"
+    app.write_text("require('http').createServer((q, r) => r.end('v0')).listen(0);\n")
+    shutil.copy(os.path.join(ROOT, "examples", "quickstart", "watch.js"), tmp_path / "watch.js")
+    p = subprocess.Popen(["node", str(tmp_path / "watch.js"), str(app)], cwd=tmp_path, stdout=subprocess.DEVNULL,
+                         stderr=subprocess.STDOUT, env=dict(os.environ, WATCH_STANDBY="3"), start_new_session=True)
+    try:
+        deadline = time.time() + 20
+        standbys = []
+        while time.time() < deadline and len(standbys) < 3:
+            time.sleep(0.2)
+            standbys = [c for c in psutil.Process(p.pid).children() if "-e" in c.cmdline()]
+        assert len(standbys) == 3, standbys
+        p.kill()
+        p.wait(10)
+        gone, alive = psutil.wait_procs(standbys, timeout=10)
+        assert not alive, alive
+    finally:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)  # the app the watcher started, and anything left
+        except ProcessLookupError:
+            pass
 
 
 def test_standby_pool_shrinks_after_a_quiet_period(tmp_path):
