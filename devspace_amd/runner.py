@@ -22,7 +22,22 @@ stream nor waits for one, so the host keeps running ahead of the GPUs. Rank 0 pr
     [devspace-runner] reloaded gen=3 marker=v1 step=120 loss=... step_ms=... reload_ms=...
 
 A module without `step()` is treated as a plain script and re-executed in the warm
-interpreter on each change. Exceptions in new code keep the previous version running.
+interpreter on each change.
+
+Failure containment (the reference gets it from a fresh process per reload: nodemon in
+examples/quickstart/package.json:7, the redeploy loop of cmd/dev.go:225-234,284-302):
+  * same bytes on every rank: at each agreed generation rank 0 reads the entry file and
+    broadcasts its bytes over the gloo control group; every rank compiles exactly those bytes.
+    User modules the entry imports from the synced tree go through a source overlay that records
+    the bytes each rank compiled; the ranks compare one code digest, and when a helper changed
+    between their reads rank 0's recorded sources are re-sent and compiled everywhere.
+  * agreed reload failures: a load that fails on any rank keeps the previous generation on all.
+  * agreed step failures: with several ranks, an exception in setup()/step() is fatal for the
+    group: the failing rank logs `rank=<r>` with the traceback and exits non-zero; the supervisor
+    stops the others (blocked in a collective, or not) and starts a fresh group of child
+    processes. A group that fails before its first step completes (the code itself is broken)
+    waits for the next edit before starting again, as nodemon does ("app crashed - waiting for
+    file changes"). A single rank keeps running the previous version after a failed step.
 
 Preemptible steps: a step may call `ctx.preempt_point()` between its phases (e.g. between
 forward and backward). The point abandons the rest of the step when a newer version of the
@@ -41,6 +56,7 @@ from __future__ import annotations
 
 import argparse
 import hashlib
+import importlib.machinery
 import importlib.util
 import os
 import signal
@@ -57,6 +73,34 @@ PREFIX = "[devspace-runner]"
 def _log(msg: str) -> None:
     sys.stdout.write(f"{PREFIX} {msg}\n")
     sys.stdout.flush()
+
+
+# exit codes of a worker that leaves its group on purpose (the supervisor restarts the group)
+EXIT_STEP_FAILED = 3
+EXIT_GROUP_LOST = 4
+EXIT_LOAD_FAILED = 5
+
+
+def _status(msg: str) -> None:
+    """One line to the supervisor over the status pipe it handed down (DEVSPACE_RUNNER_STATUS_FD):
+    `ready <rank>` once the first step ran, `fail <rank> <gen>` before a deliberate exit."""
+    fd = os.environ.get("DEVSPACE_RUNNER_STATUS_FD")
+    if not fd:
+        return
+    try:
+        os.write(int(fd), (msg + "\n").encode())
+    except OSError:  # supervisor gone: PDEATHSIG ends this process anyway
+        pass
+
+
+def _fatal(code: int) -> None:
+    """Leave the group now: no destroy_process_group (it would wait on peers that may sit in a
+    collective this rank never joins), no atexit hooks that touch the device."""
+    try:
+        sys.stdout.flush()
+        sys.stderr.flush()
+    finally:
+        os._exit(code)
 
 
 class _PollWatcher:
@@ -234,6 +278,21 @@ class Agreement:
         self.calls += 1
         return bool(self.flag[0])
 
+    def share(self, obj):
+        """Rank 0's `obj` on every rank (pickled, over the gloo group): the code bytes of a
+        generation, so no rank compiles what it happened to read from disk."""
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0, group=self.group)
+        self.calls += 1
+        return box[0]
+
+    def gather(self, obj) -> list:
+        """Every rank's `obj`, in rank order, on every rank (load outcomes and code digests)."""
+        out = [None] * self.dist.get_world_size(self.group)
+        self.dist.all_gather_object(out, obj, group=self.group)
+        self.calls += 1
+        return out
+
 
 class Context:
     """What user code sees: rank/device info, a tiny logging helper and the preemption point."""
@@ -255,6 +314,11 @@ class Context:
     def log(self, msg: str) -> None:
         if self.rank == 0:
             _log(msg)
+
+    def error(self, msg: str) -> None:
+        """Errors go out from every rank, tagged with it: a failure on rank 5 of 8 must not be
+        invisible because only rank 0 prints."""
+        _log(f"rank={self.rank} {msg}" if self.world_size > 1 else msg)
 
     def preempt_point(self) -> None:
         """Cooperative reload point inside `step()`: raises Preempted if a newer version of the
@@ -313,11 +377,13 @@ def purge_user_modules(watch_dir: str) -> list:
     return gone
 
 
-def load_module(path: str, generation: int, feed=None) -> types.ModuleType:
-    """Compile the user file into a fresh module object (no import cache involved). When the
-    change feed already compiled exactly these bytes in the background, that code is used."""
-    with open(path, "rb") as f:
-        src = f.read()
+def load_module(path: str, generation: int, feed=None, src: bytes = None) -> types.ModuleType:
+    """Compile the user file into a fresh module object (no import cache involved). `src`: the
+    bytes to compile (a multi-rank group passes rank 0's), else the file is read. When the change
+    feed already compiled exactly these bytes in the background, that code is used."""
+    if src is None:
+        with open(path, "rb") as f:
+            src = f.read()
     name = f"devspace_user_{generation}"
     mod = types.ModuleType(name)
     mod.__file__ = path
@@ -327,6 +393,187 @@ def load_module(path: str, generation: int, feed=None) -> types.ModuleType:
     exec(code, mod.__dict__)  # noqa: S102 - executing the user's own synced code is the point
     mod.__devspace_digest__ = hashlib.sha256(src).hexdigest()[:8]
     return mod
+
+
+class SourceOverlay:
+    """Import hook for the synced tree: every user module (a .py file under the watched
+    directory that the entry file imports) is compiled from bytes this hook hands out — rank 0's
+    recorded bytes when the group re-sent them (`snap`), else the file as read now — and the
+    bytes each load compiled are recorded (`reads`), so the ranks can prove they run one code
+    version. Sits in sys.meta_path just before the PathFinder (builtins and frozen modules keep
+    precedence, as with a plain `python train.py`); a name not found in the synced tree falls
+    through to the normal import system, so other imports pay one cached directory lookup."""
+
+    def __init__(self, root: str):
+        self.root = os.path.realpath(root) + os.sep
+        self.snap = {}
+        self.reads = {}
+        self._real = {}
+        self.fault = None  # test-only hook, see _FaultHooks
+
+    def install(self):
+        mp = sys.meta_path
+        if self in mp:
+            return self
+        at = next((i for i, f in enumerate(mp) if f is importlib.machinery.PathFinder), len(mp))
+        mp.insert(at, self)
+        return self
+
+    def uninstall(self):
+        if self in sys.meta_path:
+            sys.meta_path.remove(self)
+
+    def _under(self, p: str) -> bool:
+        r = self._real.get(p)
+        if r is None:
+            r = self._real[p] = os.path.realpath(p or ".") + os.sep
+        return r.startswith(self.root)
+
+    def find_spec(self, name, path=None, target=None):
+        dirs = [p for p in (path if path is not None else sys.path) if isinstance(p, str) and self._under(p)]
+        if not dirs:
+            return None
+        spec = importlib.machinery.PathFinder.find_spec(name, dirs)
+        if spec is None or not spec.origin or not spec.origin.endswith(".py"):
+            return None
+        if not os.path.realpath(spec.origin).startswith(self.root):
+            return None
+        spec.loader = _OverlayLoader(name, spec.origin, self)
+        return spec
+
+    def source(self, path: str) -> bytes:
+        key = os.path.realpath(path)
+        data = self.snap.get(key)
+        if data is None:
+            with open(path, "rb") as f:
+                data = f.read()
+            if self.fault is not None:
+                self.fault.after_helper_read(path)
+        self.reads[key] = data
+        return data
+
+    def digest(self, src: bytes) -> str:
+        """The code of one load: the entry bytes plus every user module it (re)imported."""
+        h = hashlib.sha256(src)
+        for k in sorted(self.reads):
+            h.update(k.encode() + b"\0" + hashlib.sha256(self.reads[k]).digest())
+        return h.hexdigest()[:12]
+
+
+class _OverlayLoader(importlib.machinery.SourceFileLoader):
+    """A source loader whose bytes come from the overlay; no .pyc involved (a cached bytecode
+    file could be of another version than the bytes the group agreed on)."""
+
+    def __init__(self, fullname, path, overlay):
+        super().__init__(fullname, path)
+        self._overlay = overlay
+
+    def get_data(self, path):
+        if path == self.path:
+            return self._overlay.source(path)
+        return super().get_data(path)
+
+    def get_code(self, fullname):
+        return compile(self.get_data(self.path), self.path, "exec", dont_inherit=True)
+
+
+class _FaultHooks:
+    """Test-only fault injection (DEVSPACE_RUNNER_FAULT): reproduce the races the agreement
+    protocol closes, deterministically.
+      mutate-entry-after-read  rank 0 rewrites the entry file right after reading it for a
+                               reload (a rank reading the file itself would get other bytes)
+      skew-helper              rank 0 rewrites each helper module right after reading it, and
+                               the other ranks load 0.3 s later (they read the rewritten file)
+    Each file is rewritten once (the rewrite is itself an edit: the next generation)."""
+
+    def __init__(self, spec: str, rank: int):
+        self.modes = set(filter(None, (spec or "").split(",")))
+        self.rank = rank
+        self.done = set()
+        self.armed = False  # only reloads (generation > 1), not the initial load
+
+    def _rewrite(self, path):
+        if path in self.done:
+            return
+        self.done.add(path)
+        with open(path, "ab") as f:
+            f.write(b"\n# devspace-fault: rewritten after rank 0 read it\n")
+
+    def after_entry_read(self, path):
+        if self.armed and self.rank == 0 and "mutate-entry-after-read" in self.modes:
+            self._rewrite(path)
+
+    def after_helper_read(self, path):
+        if self.armed and self.rank == 0 and "skew-helper" in self.modes:
+            self._rewrite(path)
+
+    def before_load(self):
+        if self.armed and self.rank != 0 and "skew-helper" in self.modes:
+            time.sleep(0.3)
+
+
+class LoadFailed(Exception):
+    """The group could not load a generation (on some rank); every rank keeps the previous one."""
+
+
+def _load_generation(entry, gen, feed, overlay, agree, purge, watch_dir, ctx, fault):
+    """Load generation `gen` of the entry file, the same bytes on every rank. Returns the module;
+    raises LoadFailed (on every rank alike) when any rank failed.
+
+    One rank: read, compile, exec. Several: rank 0 reads the entry and broadcasts the bytes (and
+    the purge decision); every rank execs them with the overlay recording the user modules it
+    imports; the ranks gather (ok, code digest). Equal digests: done. Different digests (a helper
+    module changed between the ranks' reads): rank 0's recorded sources are broadcast, the other
+    ranks re-import from them, and the digests are compared again."""
+    src = None
+    if agree is None or ctx.rank == 0:
+        with open(entry, "rb") as f:
+            src = f.read()
+        fault.after_entry_read(entry)
+    if agree is not None:
+        src, purge = agree.share((src, purge))
+    if purge:
+        purge_user_modules(watch_dir)
+    overlay.snap, overlay.reads = {}, {}
+    fault.before_load()
+    mod, err = _try_load(entry, gen, feed, src)
+    if agree is None:
+        if mod is None:
+            raise LoadFailed(err)
+        mod.__devspace_code__ = overlay.digest(src)
+        return mod
+    digest = overlay.digest(src) if mod is not None else None
+    outcomes = agree.gather((mod is not None, digest))
+    if all(ok for ok, _ in outcomes) and len({d for _, d in outcomes}) > 1:
+        if ctx.rank == 0:
+            ctx.log(f"gen={gen}: the ranks compiled different helper sources (digests "
+                    f"{sorted({d for _, d in outcomes})}): re-sending rank 0's")
+        snap = agree.share(dict(overlay.reads) if ctx.rank == 0 else None)
+        if ctx.rank != 0:
+            purge_user_modules(watch_dir)
+            overlay.snap, overlay.reads = snap, {}
+            mod, err = _try_load(entry, gen, feed, src)
+            digest = overlay.digest(src) if mod is not None else None
+            overlay.snap = {}
+        outcomes = agree.gather((mod is not None, digest))
+    failed = [r for r, (ok, _) in enumerate(outcomes) if not ok]
+    digests = {d for _, d in outcomes}
+    if err is not None:
+        ctx.error(f"load failed gen={gen}:\n{err}")
+    if failed or len(digests) != 1:
+        why = f"failed on rank(s) {failed}" if failed else f"code digests still differ: {sorted(digests)}"
+        raise LoadFailed(why)
+    mod.__devspace_code__ = digest
+    if os.environ.get("DEVSPACE_RUNNER_DEBUG"):
+        _log(f"rank={ctx.rank} loaded gen={gen} digest={mod.__devspace_digest__} code={digest}")
+    return mod
+
+
+def _try_load(entry, gen, feed, src):
+    try:
+        return load_module(entry, gen, feed, src=src), None
+    except Exception:  # a syntax error, a failing import: reported, the group keeps its code
+        return None, traceback.format_exc()
 
 
 class ChangeFeed:
@@ -447,42 +694,10 @@ def worker_main(args) -> int:
         sys.path.insert(0, os.path.dirname(entry))
     watcher = make_watcher(watch_dir)
     feed = ChangeFeed(watcher, entry)
-
-    gen = 1
-    t_start = time.perf_counter()
-    mod = load_module(entry, gen)
-    ctx.generation = gen
-    state = mod.setup(ctx) if hasattr(mod, "setup") else None
-    setup_version = getattr(mod, "SETUP_VERSION", None)
-    # control plane of the group (gloo, CPU tensors): generation + preemption agreement
+    overlay = SourceOverlay(watch_dir).install()
+    fault = overlay.fault = _FaultHooks(os.environ.get("DEVSPACE_RUNNER_FAULT"), rank)
+    # control plane of the group (gloo, CPU tensors): generation, preemption, code agreement
     agree = Agreement(dist) if world > 1 else None
-    helper_pending = False
-    first = {}
-    if hasattr(mod, "step"):
-        first = mod.step(ctx, state) or {}
-        ctx.step += 1
-        if device.type == "cuda":
-            torch.cuda.synchronize()
-    # Preemption only from here on: an edit that lands during setup() or the first step stays
-    # pending in the feed and is picked up by the main loop's first check (a Preempted raised
-    # there would have had no handler).
-    if args.preempt:
-        ctx._feed = feed
-        ctx._agree = agree
-        ctx._drain_min_ms = args.preempt_drain_ms
-    ctx.log(
-        f"started gen={gen} marker={getattr(mod, 'MARKER', '')} digest={mod.__devspace_digest__} "
-        f"world={world} device={device} backend={dist.get_backend() if dist is not None else 'none'} loss={first.get('loss') if isinstance(first, dict) else None} "
-        f"startup_ms={(time.perf_counter() - t_start) * 1000.0:.1f} "
-        f"kit={os.path.dirname(os.path.dirname(os.path.abspath(__file__)))}"
-    )
-    pending_gen = gen
-    reload_t0 = None
-    period_ema = None  # steady-state loop period (ms), reported with each reload
-    t_iter = time.perf_counter()
-    last_print_step = 0
-    max_steps = args.max_steps
-    script_mode = not hasattr(mod, "step")
     stop = False
 
     def _term(*_):
@@ -490,97 +705,187 @@ def worker_main(args) -> int:
         stop = True
 
     signal.signal(signal.SIGTERM, _term)
-    while agree is not None or not stop:
-        # 1. pick up local change notifications (non-blocking while training; blocking when idle)
-        timeout = 0 if (not script_mode and args.train) else 0.05
-        n_changes, t_first, helper_changed = feed.take(timeout)
-        # Rank 0's feed alone advances the generation: every rank watches the same synced
-        # directory, but their feeds post the edit microseconds apart, and a rank that saw it one
-        # step late would otherwise bump the group to a second generation (a spurious reload).
-        if n_changes and (agree is None or rank == 0):
-            pending_gen += 1
-            helper_pending = helper_pending or helper_changed
-            if reload_t0 is None:
-                reload_t0 = t_first
-        # 2. ranks agree on the newest generation (keeps collectives in `step` matched) and on
-        #    whether helper modules must be re-imported (rank 0's view, like the generation)
-        target = pending_gen
-        if agree is not None:
-            target, agreed_helper, agreed_stop = agree.boundary(pending_gen, helper_pending, stop)
-            if agreed_stop:
-                break
-            pending_gen = max(pending_gen, target)
-            helper_pending = helper_pending or agreed_helper
-        if target > gen:
-            t_reload = time.perf_counter()
-            wait_ms = (t_reload - reload_t0) * 1000.0 if reload_t0 else 0.0
+
+    def leave(code, msg):
+        """World > 1: this rank cannot go on without desynchronising the group's collectives.
+        Say why (from this rank), tell the supervisor, exit; the supervisor restarts the group."""
+        if stop:  # the supervisor is already stopping the group: a peer's exit is expected
+            _fatal(0)
+        ctx.error(msg)
+        _status(f"fail {rank} {ctx.generation}")
+        _fatal(code)
+
+    try:
+        gen = 1
+        t_start = time.perf_counter()
+        helper_pending = False
+        first = {}
+        while True:  # startup: load gen 1, setup(), first step
+            ctx.generation = gen
             try:
-                if helper_pending:
-                    purge_user_modules(watch_dir)
-                    helper_pending = False
-                new_mod = load_module(entry, target, feed)
+                mod = _load_generation(entry, gen, None, overlay, agree, False, watch_dir, ctx, fault)
+                state = mod.setup(ctx) if hasattr(mod, "setup") else None
+                if hasattr(mod, "step"):
+                    first = mod.step(ctx, state) or {}
+                    ctx.step += 1
+                    if device.type == "cuda":
+                        torch.cuda.synchronize()
+                break
+            except LoadFailed as e:
+                if agree is not None:
+                    leave(EXIT_LOAD_FAILED, f"startup failed gen={gen}: {e}")
+                ctx.error(f"startup failed gen={gen}:\n{e}")
+            except Exception:
+                if agree is not None:
+                    leave(EXIT_STEP_FAILED, f"startup failed gen={gen}:\n{traceback.format_exc()}")
+                ctx.error(f"startup failed gen={gen}:\n{traceback.format_exc()}")
+            # one rank: wait warm for the next edit, then try again (nodemon's "waiting for file
+            # changes before starting"); several ranks left above and the supervisor waits instead
+            ctx.log("waiting for a file change before starting again")
+            while not feed.take(0.5)[0]:
+                if stop:
+                    return 0
+            gen += 1
+        setup_version = getattr(mod, "SETUP_VERSION", None)
+        _status(f"ready {rank}")
+        # Preemption only from here on: an edit that lands during setup() or the first step stays
+        # pending in the feed and is picked up by the main loop's first check (a Preempted raised
+        # there would have had no handler).
+        if args.preempt:
+            ctx._feed = feed
+            ctx._agree = agree
+            ctx._drain_min_ms = args.preempt_drain_ms
+        ctx.log(
+            f"started gen={gen} marker={getattr(mod, 'MARKER', '')} digest={mod.__devspace_digest__} "
+            f"code={mod.__devspace_code__} "
+            f"world={world} device={device} backend={dist.get_backend() if dist is not None else 'none'} "
+            f"loss={first.get('loss') if isinstance(first, dict) else None} "
+            f"startup_ms={(time.perf_counter() - t_start) * 1000.0:.1f} "
+            f"kit={os.path.dirname(os.path.dirname(os.path.abspath(__file__)))}"
+        )
+        pending_gen = gen
+        reload_t0 = None
+        period_ema = None  # steady-state loop period (ms), reported with each reload
+        t_iter = time.perf_counter()
+        last_print_step = 0
+        max_steps = args.max_steps
+        script_mode = not hasattr(mod, "step")
+        fault.armed = True
+        while agree is not None or not stop:
+            # 1. pick up local change notifications (non-blocking while training; blocking when idle)
+            timeout = 0 if (not script_mode and args.train) else 0.05
+            n_changes, t_first, helper_changed = feed.take(timeout)
+            # Rank 0's feed alone advances the generation: every rank watches the same synced
+            # directory, but their feeds post the edit microseconds apart, and a rank that saw it one
+            # step late would otherwise bump the group to a second generation (a spurious reload).
+            if n_changes and (agree is None or rank == 0):
+                pending_gen += 1
+                helper_pending = helper_pending or helper_changed
+                if reload_t0 is None:
+                    reload_t0 = t_first
+            # 2. ranks agree on the newest generation (keeps collectives in `step` matched) and on
+            #    whether helper modules must be re-imported (rank 0's view, like the generation)
+            target = pending_gen
+            if agree is not None:
+                target, agreed_helper, agreed_stop = agree.boundary(pending_gen, helper_pending, stop)
+                if agreed_stop:
+                    break
+                pending_gen = max(pending_gen, target)
+                helper_pending = helper_pending or agreed_helper
+            if target > gen:
+                t_reload = time.perf_counter()
+                wait_ms = (t_reload - reload_t0) * 1000.0 if reload_t0 else 0.0
+                purge, helper_pending = helper_pending, False
+                running = ctx.generation
+                gen = target  # consumed, loaded or not: a failed generation is not retried
+                try:
+                    new_mod = _load_generation(entry, gen, feed, overlay, agree, purge, watch_dir, ctx, fault)
+                except LoadFailed as e:
+                    reload_t0 = None
+                    if agree is None:
+                        ctx.error(f"reload failed gen={gen}, keeping gen={running}:\n{e}")
+                    else:
+                        ctx.log(f"reload failed gen={gen} ({e}), keeping gen={running} on every rank")
+                    continue
                 new_setup_version = getattr(new_mod, "SETUP_VERSION", None)
                 if hasattr(new_mod, "setup") and (state is None or new_setup_version != setup_version):
-                    state = new_mod.setup(ctx)
+                    try:
+                        state = new_mod.setup(ctx)
+                    except Exception:
+                        if agree is not None:  # setup() may hold collectives (DDP's broadcast)
+                            leave(EXIT_STEP_FAILED, f"setup failed gen={gen}:\n{traceback.format_exc()}")
+                        ctx.error(f"reload failed gen={gen} in setup(), keeping gen={running}:\n"
+                                  f"{traceback.format_exc()}")
+                        reload_t0 = None
+                        continue
                     setup_version = new_setup_version
                 mod = new_mod
-                script_mode = not hasattr(mod, "step")
-            except Exception:  # keep the previous version running
-                ctx.log(f"reload failed gen={target}, keeping gen={gen}:\n{traceback.format_exc()}")
-            gen = target
-            ctx.generation = gen
-            reload_ms = (time.perf_counter() - t_reload) * 1000.0
-            # 3. run the first step with the new code and report
-            t_step = time.perf_counter()
-            metrics = {}
+                ctx.generation = gen
+                script_mode = not hasattr(mod, "step")  # a script ran in full when it was loaded
+                reload_ms = (time.perf_counter() - t_reload) * 1000.0
+                # 3. run the first step with the new code and report
+                t_step = time.perf_counter()
+                metrics = {}
+                try:
+                    if not script_mode:
+                        metrics = mod.step(ctx, state) or {}
+                        ctx.step += 1
+                    if device.type == "cuda":
+                        torch.cuda.synchronize()
+                except Preempted:  # an even newer edit arrived: report that one instead
+                    continue
+                except Exception:
+                    if agree is not None:
+                        leave(EXIT_STEP_FAILED, f"step failed gen={gen} marker={getattr(mod, 'MARKER', '')}: "
+                                                f"leaving the group (the supervisor restarts it)\n"
+                                                f"{traceback.format_exc()}")
+                    ctx.error(f"step failed gen={gen}:\n{traceback.format_exc()}")
+                step_ms = (time.perf_counter() - t_step) * 1000.0
+                since = (time.perf_counter() - reload_t0) * 1000.0 if reload_t0 else 0.0
+                reload_t0 = None
+                loss = metrics.get("loss") if isinstance(metrics, dict) else None
+                ctx.log(
+                    f"reloaded gen={gen} marker={getattr(mod, 'MARKER', '')} digest={mod.__devspace_digest__} "
+                    f"code={mod.__devspace_code__} ranks={world} "
+                    f"step={ctx.step} loss={loss} step_ms={step_ms:.2f} reload_ms={reload_ms:.2f} "
+                    f"pickup_ms={since:.2f} inflight_ms={wait_ms:.2f} period_ms={period_ema or 0.0:.2f} "
+                    f"t_mono={time.perf_counter():.6f}"
+                )
+                t_iter = time.perf_counter()
+                continue
+            if script_mode or not args.train:
+                continue
             try:
-                if script_mode:
-                    load_module(entry, gen)
-                else:
-                    metrics = mod.step(ctx, state) or {}
-                    ctx.step += 1
-                if device.type == "cuda":
-                    torch.cuda.synchronize()
-            except Preempted:  # an even newer edit arrived: report that one instead
+                metrics = mod.step(ctx, state) or {}
+                ctx.step += 1
+            except Preempted:
                 continue
             except Exception:
-                ctx.log(f"step failed gen={gen}:\n{traceback.format_exc()}")
-            step_ms = (time.perf_counter() - t_step) * 1000.0
-            since = (time.perf_counter() - reload_t0) * 1000.0 if reload_t0 else 0.0
-            reload_t0 = None
-            loss = metrics.get("loss") if isinstance(metrics, dict) else None
-            ctx.log(
-                f"reloaded gen={gen} marker={getattr(mod, 'MARKER', '')} digest={mod.__devspace_digest__} "
-                f"step={ctx.step} loss={loss} step_ms={step_ms:.2f} reload_ms={reload_ms:.2f} "
-                f"pickup_ms={since:.2f} inflight_ms={wait_ms:.2f} period_ms={period_ema or 0.0:.2f} "
-                f"t_mono={time.perf_counter():.6f}"
-            )
-            t_iter = time.perf_counter()
-            continue
-        if script_mode or not args.train:
-            continue
-        try:
-            metrics = mod.step(ctx, state) or {}
-            ctx.step += 1
-        except Preempted:
-            continue
-        except Exception:
-            ctx.log(f"step failed gen={gen}:\n{traceback.format_exc()}")
-            time.sleep(0.2)
-            continue
-        now = time.perf_counter()
-        dt = (now - t_iter) * 1000.0
-        t_iter = now
-        period_ema = dt if period_ema is None else 0.9 * period_ema + 0.1 * dt
-        ctx._period_ms = period_ema
-        if args.log_every and ctx.step - last_print_step >= args.log_every:
-            last_print_step = ctx.step
-            ctx.log(f"step={ctx.step} gen={gen} loss={metrics.get('loss') if isinstance(metrics, dict) else None} "
-                    f"period_ms={period_ema or 0.0:.3f}")
-        if max_steps and ctx.step >= max_steps:
-            break
+                if agree is not None:
+                    leave(EXIT_STEP_FAILED, f"step failed gen={gen} marker={getattr(mod, 'MARKER', '')}: "
+                                            f"leaving the group (the supervisor restarts it)\n"
+                                            f"{traceback.format_exc()}")
+                ctx.error(f"step failed gen={gen}:\n{traceback.format_exc()}")
+                time.sleep(0.2)
+                continue
+            now = time.perf_counter()
+            dt = (now - t_iter) * 1000.0
+            t_iter = now
+            period_ema = dt if period_ema is None else 0.9 * period_ema + 0.1 * dt
+            ctx._period_ms = period_ema
+            if args.log_every and ctx.step - last_print_step >= args.log_every:
+                last_print_step = ctx.step
+                ctx.log(f"step={ctx.step} gen={gen} loss={metrics.get('loss') if isinstance(metrics, dict) else None} "
+                        f"period_ms={period_ema or 0.0:.3f}")
+            if max_steps and ctx.step >= max_steps:
+                break
+    except Exception as e:  # world > 1: a collective of the control plane failed (a peer is gone)
+        if agree is None:
+            raise
+        leave(EXIT_GROUP_LOST, f"group failure gen={ctx.generation}: {type(e).__name__}: {e}")
     feed.close()
     watcher.close()
+    overlay.uninstall()
     if dist is not None and dist.is_initialized():
         dist.destroy_process_group()
     return 0
@@ -596,7 +901,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _spawn_group(args, port):
+def _spawn_group(args, port, status_fd=None):
     procs = []
     for r in range(max(1, args.nproc)):
         env = dict(os.environ)
@@ -608,12 +913,15 @@ def _spawn_group(args, port):
             MASTER_PORT=str(port),
             HSA_ENABLE_IPC_MODE_LEGACY=env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
         )
+        if status_fd is not None:
+            env["DEVSPACE_RUNNER_STATUS_FD"] = str(status_fd)
         # Installed as a package (-m devspace_amd.runner) or vendored as a single file into a
         # project by `devspace init` (rocm-pytorch template).
         me = ["-m", "devspace_amd.runner"] if __package__ else [os.path.abspath(__file__)]
         cmd = [sys.executable] + me + ["--worker"] + _forward(args)
         supervisor = os.getpid()
-        procs.append(subprocess.Popen(cmd, env=env, preexec_fn=lambda: _die_with_parent(supervisor)))
+        procs.append(subprocess.Popen(cmd, env=env, pass_fds=(status_fd,) if status_fd is not None else (),
+                                      preexec_fn=lambda: _die_with_parent(supervisor)))
     return procs
 
 
@@ -632,6 +940,8 @@ def _die_with_parent(supervisor_pid):
 
 
 def _stop_group(procs, grace_s=2.0):
+    """SIGTERM (the ranks agree to stop at the next step boundary), SIGKILL after the grace: a
+    rank blocked inside a collective whose peer is gone never returns to Python to see it."""
     for p in procs:
         if p.poll() is None:
             p.terminate()
@@ -666,8 +976,78 @@ def restart_main(args) -> int:
         watcher.close()
 
 
+class _GroupWatch:
+    """The supervisor's view of one running group: exits (any rank, not all), the workers'
+    status lines (`ready <rank>`, `fail <rank> <gen>`) and whether the synced tree changed since
+    the group started (then a failed group restarts at once: the fix may already be there)."""
+
+    def __init__(self, procs, status_r, watcher):
+        self.procs = procs
+        self.status_r = status_r
+        self.watcher = watcher
+        self.ready = set()
+        self.failed = []  # ranks in the order their `fail` lines arrived
+        self.changed = False
+        self._buf = b""
+        self._next_scan = 0.0
+
+    def _read_status(self, timeout):
+        import select
+
+        r, _, _ = select.select([self.status_r], [], [], timeout)
+        if not r:
+            return
+        try:
+            chunk = os.read(self.status_r, 4096)
+        except BlockingIOError:
+            return
+        self._buf += chunk
+        *lines, self._buf = self._buf.split(b"\n")
+        for line in lines:
+            parts = line.decode(errors="replace").split()
+            if len(parts) >= 2 and parts[0] == "ready":
+                self.ready.add(int(parts[1]))
+            elif len(parts) >= 2 and parts[0] == "fail":
+                self.failed.append(int(parts[1]))
+
+    def _scan_tree(self):
+        now = time.monotonic()
+        if now < self._next_scan:
+            return
+        self._next_scan = now + 0.25
+        if [p for p in self.watcher.poll(0) if not _ignored(p)]:
+            self.changed = True
+
+    def wait(self):
+        """('done', codes) when every rank exited 0; ('failed', rank, code) at the first rank
+        that exits otherwise (the root cause: the first `fail` line, else the first exit seen)."""
+        while True:
+            self._read_status(0.02)
+            self._scan_tree()
+            codes = [p.poll() for p in self.procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                self._read_status(0)
+                root = next(((r, codes[r]) for r in self.failed if codes[r] not in (None, 0)), bad[0])
+                return ("failed",) + root
+            if all(c == 0 for c in codes):
+                return ("done", codes)
+
+
+def _wait_for_change(watcher, already=False):
+    """nodemon's "app crashed - waiting for file changes before starting": block until the synced
+    tree changes (a settled write, not a temp file)."""
+    if already:
+        return
+    while not [p for p in watcher.poll(500) if not _ignored(p)]:
+        pass
+
+
 def supervisor_main(args) -> int:
-    """Spawn one worker per GPU (torchrun-style env), restart the group if a rank dies."""
+    """Spawn one worker per GPU (torchrun-style env) and contain failures: any rank exiting
+    non-zero stops the whole group (its peers may be blocked in a collective with it), which is
+    started again from fresh processes — at once if it had come up (its ranks all finished a
+    first step) and there are restarts left since the last edit, after the next edit otherwise."""
     if args.restart:
         return restart_main(args)
     nproc = args.nproc
@@ -676,25 +1056,51 @@ def supervisor_main(args) -> int:
         os.environ.setdefault("WORLD_SIZE", "1")
         os.environ.setdefault("LOCAL_RANK", "0")
         return worker_main(args)
+    watch_dir = os.path.abspath(args.watch or os.path.dirname(os.path.abspath(args.entry)))
+    watcher = make_watcher(watch_dir)
     port = args.port or _free_port()
-    restarts = 0
+    restarts = 0  # restarts since the last edit
 
     def _term(*_):
         raise KeyboardInterrupt
 
     signal.signal(signal.SIGTERM, _term)  # pod deletion / kill: stop the ranks, then exit
-    while True:
-        procs = _spawn_group(args, port)
-        try:
-            codes = [p.wait() for p in procs]
-        except KeyboardInterrupt:
-            _stop_group(procs)
-            return 130
-        if all(c == 0 for c in codes) or restarts >= args.max_restarts:
-            return max(codes)
-        restarts += 1
-        _log(f"worker exited with {codes}; restarting process group ({restarts}/{args.max_restarts})")
-        port = port + 1 if args.port else _free_port()
+    procs = []
+    try:
+        while True:
+            status_r, status_w = os.pipe()
+            os.set_blocking(status_r, False)
+            procs = _spawn_group(args, port, status_w)
+            os.close(status_w)
+            gw = _GroupWatch(procs, status_r, watcher)
+            outcome = gw.wait()
+            if outcome[0] == "done":
+                os.close(status_r)
+                return 0
+            _, rank, code = outcome
+            _stop_group(procs, grace_s=1.0)
+            os.close(status_r)
+            came_up = len(gw.ready) == nproc
+            if gw.changed:
+                restarts = 0
+            restarts += 1
+            if came_up and restarts <= args.max_restarts:
+                _log(f"rank={rank} exited with code {code}: restarting the group of {nproc} "
+                     f"({restarts}/{args.max_restarts} since the last edit)")
+            else:
+                why = "before every rank finished a first step" if not came_up else \
+                    f"{args.max_restarts} restarts without an edit"
+                _log(f"rank={rank} exited with code {code} {why}: waiting for a file change "
+                     f"before starting the group again")
+                _wait_for_change(watcher, already=gw.changed)
+                restarts = 0
+                _log(f"change detected: restarting the group of {nproc}")
+            port = port + 1 if args.port else _free_port()
+    except KeyboardInterrupt:
+        _stop_group(procs)
+        return 130
+    finally:
+        watcher.close()
 
 
 def _forward(args):

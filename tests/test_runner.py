@@ -235,7 +235,8 @@ def test_control_plane_never_touches_the_device():
 
     tree = ast.parse(open(runner.__file__).read())
     worker = next(n for n in ast.walk(tree) if isinstance(n, ast.FunctionDef) and n.name == "worker_main")
-    loop = next(n for n in ast.walk(worker) if isinstance(n, ast.While))
+    # the training loop (the other one is the startup retry loop, which may synchronize)
+    loop = next(n for n in ast.walk(worker) if isinstance(n, ast.While) and "not stop" in ast.unparse(n.test))
     reload_branch = next(n for n in loop.body if isinstance(n, ast.If) and "target > gen" in ast.unparse(n.test))
     steady = [n for n in loop.body if n is not reload_branch]
     syncing = []

@@ -1,0 +1,332 @@
+"""N-rank hot-reload runner under failure: rank-local step exceptions, rank-local
+load failures, and edits racing the ranks' reads must neither hang the group nor leave its ranks
+on different code. Rehearsed on CPU with gloo ranks at world 2, 4 and 8 (the 8-GPU pod's shape).
+
+The reference contains every failure by restarting a fresh process per reload (nodemon in
+/root/reference/examples/quickstart/package.json:7; redeploy loop /root/reference/cmd/dev.go:225-234);
+the runner keeps processes warm, so it has to contain them itself.
+"""
+import hashlib
+import os
+import queue
+import re
+import signal
+import subprocess
+import sys
+import threading
+import time
+
+import psutil
+import pytest
+
+from conftest import ROOT
+
+CPU_ENV = {"HIP_VISIBLE_DEVICES": "-1", "CUDA_VISIBLE_DEVICES": "-1", "OMP_NUM_THREADS": "1"}
+
+RANK_LOCAL_STEP = '''
+import time
+
+import torch
+import torch.distributed as dist
+
+MARKER = "v0"
+
+
+def setup(ctx):
+    return {"n": 0}
+
+
+def step(ctx, state):
+    if MARKER == "bad" and ctx.rank == 1:
+        # rank 1 fails before the step's collective; its peers are already waiting in it
+        raise RuntimeError("rank-local failure on rank 1")
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    state["n"] += 1
+    time.sleep(0.005)
+    return {"loss": float(t)}
+'''
+
+
+class Runner:
+    """The runner supervisor as a child process, its output lines in a queue."""
+
+    def __init__(self, tmp_path, entry, nproc, extra_args=(), extra_env=None):
+        env = dict(os.environ, PYTHONPATH=ROOT, **CPU_ENV, **(extra_env or {}))
+        self.proc = subprocess.Popen([sys.executable, "-u", "-m", "devspace_amd.runner", "--nproc", str(nproc),
+                                      "--watch", str(tmp_path), *extra_args, str(entry)],
+                                     stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, text=True,
+                                     cwd=str(tmp_path))
+        self.lines = []
+        self.q = queue.Queue()
+        threading.Thread(target=lambda: [self.q.put((time.monotonic(), l)) for l in self.proc.stdout],
+                         daemon=True).start()
+
+    def until(self, pat, timeout=60):
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            try:
+                t, line = self.q.get(timeout=max(0.01, deadline - time.monotonic()))
+            except queue.Empty:
+                break
+            self.lines.append(line)
+            if re.search(pat, line):
+                return t, line
+        raise AssertionError(f"no line matching {pat!r} within {timeout}s:\n" + "".join(self.lines[-40:]))
+
+    def seen(self, pat, timeout=60):
+        """Like until(), but a line already read counts (lines of different ranks interleave)."""
+        for line in self.lines:
+            if re.search(pat, line):
+                return line
+        return self.until(pat, timeout)[1]
+
+    def text(self):
+        return "".join(self.lines)
+
+    def stop(self):
+        kids = psutil.Process(self.proc.pid).children(recursive=True) if self.proc.poll() is None else []
+        if self.proc.poll() is None:
+            self.proc.send_signal(signal.SIGTERM)
+        try:
+            code = self.proc.wait(20)
+        except subprocess.TimeoutExpired:
+            self.proc.kill()
+            code = self.proc.wait()
+        _, alive = psutil.wait_procs(kids, timeout=20)
+        for k in alive:
+            k.kill()
+        assert not alive, f"workers outlived the supervisor: {alive}"
+        time.sleep(0.2)
+        while not self.q.empty():
+            self.lines.append(self.q.get()[1])
+        return code
+
+
+def _set_marker(path, marker):
+    src = path.read_text()
+    path.write_text(re.sub(r'^MARKER = ".*"$', f'MARKER = "{marker}"', src, count=1, flags=re.M))
+
+
+@pytest.mark.parametrize("nproc", [2, 4, 8])
+def test_rank_local_step_failure_restarts_the_group(tmp_path, nproc):
+    """An exception on rank 1 only, while rank 0.. wait in the step's all_reduce: rank 1 logs
+    rank=1 with the traceback and leaves; the supervisor stops the group and restarts it; the
+    restarted group runs the same broken code, fails before its first step completes and waits for
+    the next edit; the fix starts a fresh group that trains, within 10 s of the edit."""
+    entry = tmp_path / "train.py"
+    entry.write_text(RANK_LOCAL_STEP)
+    r = Runner(tmp_path, entry, nproc, extra_args=("--log-every", "20"))
+    try:
+        r.until(rf"started gen=1 marker=v0 .*world={nproc}", timeout=180)
+        r.until(r"step=\d+ gen=1 ")  # training
+        _set_marker(entry, "bad")
+        r.seen(r"rank=1 step failed gen=2 marker=bad")
+        r.seen(r"rank-local failure on rank 1")  # the traceback, from rank 1 itself
+        r.seen(r"rank=1 exited with code 3: restarting the group")
+        # the restarted group loads the broken code, fails before it comes up, and waits
+        r.until(r"rank=1 startup failed gen=1", timeout=120)
+        r.until(r"waiting for a file change before starting the group again", timeout=60)
+        assert r.proc.poll() is None, r.text()
+        t_fix = time.monotonic()
+        _set_marker(entry, "fixed")
+        t_up, _ = r.until(rf"started gen=1 marker=fixed .*world={nproc}", timeout=60)
+        r.until(r"step=\d+ gen=1 ", timeout=30)  # and trains
+        print(f"restart-on-fix world={nproc}: {t_up - t_fix:.2f}s")
+        assert t_up - t_fix < 10.0, (t_up - t_fix, r.text()[-3000:])
+        # no rank other than 1 reported a step failure of its own
+        assert not re.search(r"rank=[02-9] step failed", r.text()), r.text()
+    finally:
+        r.stop()
+
+
+RANK_LOCAL_IMPORT = '''
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+MARKER = "v0"
+if MARKER == "bad" and os.environ.get("RANK") == "1":
+    raise ImportError("rank-local import failure on rank 1")
+
+
+def setup(ctx):
+    return {}
+
+
+def step(ctx, state):
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    time.sleep(0.005)
+    return {"loss": float(t)}
+'''
+
+
+def test_load_failure_on_one_rank_keeps_every_rank_on_the_old_code(tmp_path):
+    """A reload that fails on one rank only is a failed reload for the whole group: every rank
+    keeps the previous generation (no rank runs the new code while another runs the old), the
+    group keeps training, and the next good edit reloads everywhere."""
+    entry = tmp_path / "train.py"
+    entry.write_text(RANK_LOCAL_IMPORT)
+    r = Runner(tmp_path, entry, 2, extra_env={"DEVSPACE_RUNNER_DEBUG": "1"})
+    try:
+        r.until(r"started gen=1 marker=v0 .*world=2", timeout=180)
+        _set_marker(entry, "bad")
+        r.seen(r"reload failed gen=2 \(failed on rank\(s\) \[1\]\), keeping gen=1 on every rank")
+        r.seen(r"rank=1 load failed gen=2")
+        _set_marker(entry, "good")
+        _, line = r.until(r"reloaded gen=3 marker=good .*ranks=2")
+        assert r.proc.poll() is None
+        assert "exited with code" not in r.text(), r.text()  # contained without a restart
+        # rank 0 never loaded gen 2 either
+        assert not re.search(r"rank=\d loaded gen=2 ", r.text()), r.text()
+        assert len(re.findall(r"rank=\d loaded gen=3 ", r.text())) == 2, r.text()
+    finally:
+        r.stop()
+
+
+STEADY = '''
+import time
+
+import torch
+import torch.distributed as dist
+
+MARKER = "v0"
+
+
+def setup(ctx):
+    return {}
+
+
+def step(ctx, state):
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    time.sleep(0.005)
+    return {"loss": float(t)}
+'''
+
+
+def _loaded(text, gen):
+    return dict(re.findall(rf"rank=(\d) loaded gen={gen} digest=(\w+)", text))
+
+
+def test_every_rank_compiles_rank0s_bytes_of_the_entry(tmp_path):
+    """Fault injection: right after rank 0 read the edited entry file it is rewritten on disk
+    (what a second save landing between two ranks' reads does). Every rank still compiles the
+    bytes rank 0 read — one digest, the digest of the edit — and the rewrite is the next
+    generation, again on every rank alike."""
+    entry = tmp_path / "train.py"
+    entry.write_text(STEADY)
+    r = Runner(tmp_path, entry, 4, extra_env={"DEVSPACE_RUNNER_DEBUG": "1",
+                                              "DEVSPACE_RUNNER_FAULT": "mutate-entry-after-read"})
+    try:
+        r.until(r"started gen=1 marker=v0 .*world=4", timeout=180)
+        _set_marker(entry, "v1")
+        edited = hashlib.sha256(STEADY.replace('MARKER = "v0"', 'MARKER = "v1"').encode()).hexdigest()[:8]
+        r.until(r"reloaded gen=2 marker=v1 ")
+        r.until(r"reloaded gen=3 marker=v1 ")  # the rewrite (a comment appended)
+        gen2, gen3 = _loaded(r.text(), 2), _loaded(r.text(), 3)
+        assert set(gen2) == {"0", "1", "2", "3"} and set(gen2.values()) == {edited}, gen2
+        assert set(gen3) == {"0", "1", "2", "3"} and len(set(gen3.values())) == 1, gen3
+        assert set(gen3.values()) != {edited}
+    finally:
+        r.stop()
+
+
+HELPER_ENTRY = '''
+import time
+
+import torch
+import torch.distributed as dist
+
+import helper_mod
+
+MARKER = helper_mod.MARKER
+
+
+def setup(ctx):
+    return {}
+
+
+def step(ctx, state):
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    time.sleep(0.005)
+    return {"loss": helper_mod.value()}
+'''
+
+
+def test_helper_module_changed_between_reads_is_resolved_to_rank0s(tmp_path):
+    """Fault injection: rank 0 reads an edited helper module, the file changes again, and the
+    other ranks read it 0.3 s later. The ranks' code digests differ; rank 0's recorded sources
+    are re-sent and compiled everywhere, so the generation runs one code version on all ranks."""
+    (tmp_path / "helper_mod.py").write_text('MARKER = "h0"\n\n\ndef value():\n    return 1\n')
+    entry = tmp_path / "train.py"
+    entry.write_text(HELPER_ENTRY)
+    r = Runner(tmp_path, entry, 2, extra_env={"DEVSPACE_RUNNER_DEBUG": "1", "DEVSPACE_RUNNER_FAULT": "skew-helper"})
+    try:
+        r.until(r"started gen=1 marker=h0 .*world=2", timeout=180)
+        (tmp_path / "helper_mod.py").write_text('MARKER = "h1"\n\n\ndef value():\n    return 2\n')
+        r.until(r"gen=2: the ranks compiled different helper sources")
+        _, line = r.until(r"reloaded gen=2 marker=h1 ")
+        assert "loss=2" in line, line
+        codes = dict(re.findall(r"rank=(\d) loaded gen=2 digest=\w+ code=(\w+)", r.text()))
+        assert set(codes) == {"0", "1"} and len(set(codes.values())) == 1, codes
+    finally:
+        r.stop()
+
+
+SLOW_STEP = '''
+import time
+
+import torch
+import torch.distributed as dist
+
+MARKER = "v0"
+
+
+def setup(ctx):
+    return {"updates": 0}
+
+
+def step(ctx, state):
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    # a 0.6 s "step" with a preemption point every 10 ms, then the state update
+    for _ in range(60):
+        time.sleep(0.01)
+        ctx.preempt_point()
+    state["updates"] += 1
+    return {"loss": state["updates"]}
+'''
+
+
+def test_eight_rank_reload_preempt_and_stop(tmp_path):
+    """The 8-GPU pod's control plane at world 8 (gloo, CPU): an edit landing mid-step preempts
+    the step on every rank at the same point (no state update from the abandoned step), the new
+    code loads with one digest on all 8 ranks, and SIGTERM stops all 8 at one boundary."""
+    entry = tmp_path / "slow.py"
+    entry.write_text(SLOW_STEP)
+    r = Runner(tmp_path, entry, 8, extra_env={"DEVSPACE_RUNNER_DEBUG": "1"})
+    try:
+        r.until(r"started gen=1 marker=v0 .*world=8", timeout=240)
+        time.sleep(0.3)
+        _set_marker(entry, "v1")
+        _, line = r.until(r"reloaded gen=2 marker=v1 .*ranks=8")
+        f = dict(re.findall(r"(\w+_ms)=([\d.]+)", line))
+        assert float(f["inflight_ms"]) < 300, line  # preempted, not the rest of a 0.6 s step
+        assert re.search(r"loss=2 ", line), line  # 1 update at startup + 1 by the new code
+        gen2 = _loaded(r.text(), 2)
+        assert len(gen2) == 8 and len(set(gen2.values())) == 1, gen2
+        kids = psutil.Process(r.proc.pid).children()
+        assert len(kids) == 8
+        t0 = time.monotonic()
+        code = r.stop()
+        assert time.monotonic() - t0 < 10
+        assert code == 130
+        assert "group failure" not in r.text() and "Traceback" not in r.text(), r.text()
+    finally:
+        if r.proc.poll() is None:
+            r.stop()
