@@ -1,4 +1,5 @@
-"""python -m devspace_amd.localkube up --state DIR [--port P] [--gpus N] [--kubeconfig PATH] [--context NAME] [--tls]"""
+"""python -m devspace_amd.localkube up --state DIR [--port P] [--gpus N] [--kubeconfig PATH] [--context NAME] [--tls]
+                                   [--throttle-first K --retry-after S]"""
 import argparse
 import os
 import signal
@@ -19,8 +20,12 @@ def main(argv=None):
     up.add_argument("--namespace", default="default")
     up.add_argument("--context", default="devspace-local", help="kube context name (e.g. minikube)")
     up.add_argument("--tls", action="store_true", help="https + wss with client certificates")
+    up.add_argument("--throttle-first", type=int, default=0,
+                    help="fault switch: answer the first K requests of every (verb, resource) with 429")
+    up.add_argument("--retry-after", type=int, default=1, help="Retry-After seconds of the throttled answers")
     args = ap.parse_args(argv)
     c = LocalCluster(args.state, port=args.port, gpus=args.gpus, context=args.context, tls=args.tls).start()
+    c.api.reset_throttle(args.throttle_first, args.retry_after)
     kc = args.kubeconfig or os.path.join(args.state, "kubeconfig")
     c.write_kubeconfig(kc, args.namespace)
     print(f"ready server={c.server} kubeconfig={kc} docker=unix://{c.docker_sock} gpus={c.gpus}", flush=True)

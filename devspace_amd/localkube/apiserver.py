@@ -53,6 +53,55 @@ class ApiServer:
         # verified client certificate on the TLS listener) — expired tokens get 401
         self.token_validator = token_validator
         self.auth_failures = 0
+        # Fault switch (API Priority and Fairness under load): the first `throttle_first` requests
+        # of every (verb, resource) are answered `429 Too Many Requests` + `Retry-After`. The
+        # counts start over with reset_throttle(), so every CLI command can be throttled afresh.
+        self.throttle_first = 0
+        self.retry_after = "1"
+        self.throttled = {}  # (verb, resource) -> requests answered 429
+
+    def reset_throttle(self, first=None, retry_after=None):
+        if first is not None:
+            self.throttle_first = first
+        if retry_after is not None:
+            self.retry_after = str(retry_after)
+        self.throttled = {}
+
+    @staticmethod
+    def _verb(request):
+        """(k8s verb, resource[/subresource]) of a REST path, as APF and RBAC see it."""
+        p = request.path
+        segs = [x for x in p.split("/") if x]
+        segs = segs[2:] if segs[:1] == ["api"] else segs[3:]  # /api/v1/... | /apis/g/v/...
+        if len(segs) >= 3 and segs[0] == "namespaces":
+            segs = segs[2:]
+        resource = segs[0] if segs else ""
+        named = len(segs) > 1
+        if len(segs) > 2:
+            resource += "/" + segs[2]
+        m = request.method
+        if request.headers.get("Upgrade", "").lower() == "websocket":
+            verb = "connect"
+        elif m == "GET":
+            verb = "watch" if request.query.get("watch") in ("1", "true") else ("get" if named else "list")
+        else:
+            verb = {"POST": "create", "PUT": "update", "PATCH": "patch"}.get(m) or (
+                "delete" if named else "deletecollection")
+        return verb, resource
+
+    @web.middleware
+    async def _throttle(self, request, handler):
+        if self.throttle_first > 0 and request.path.startswith(("/api/", "/apis/")):
+            key = self._verb(request)
+            n = self.throttled.get(key, 0)
+            if n < self.throttle_first:
+                self.throttled[key] = n + 1
+                return web.json_response(
+                    {"kind": "Status", "apiVersion": "v1", "status": "Failure", "code": 429,
+                     "reason": "TooManyRequests", "message": "Too many requests, please try again later.",
+                     "details": {"retryAfterSeconds": int(self.retry_after)}},
+                    status=429, headers={"Retry-After": self.retry_after})
+        return await handler(request)
 
     @web.middleware
     async def _auth(self, request, handler):
@@ -68,7 +117,7 @@ class ApiServer:
         return await handler(request)
 
     def app(self):
-        app = web.Application(client_max_size=256 * 1024 * 1024, middlewares=[self._auth])
+        app = web.Application(client_max_size=256 * 1024 * 1024, middlewares=[self._auth, self._throttle])
         app.router.add_get("/version", self.version)
         app.router.add_get("/api", self.api_versions)
         app.router.add_get("/apis", self.api_groups)

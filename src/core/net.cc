@@ -19,9 +19,11 @@
 #include <sys/un.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <map>
 #include <climits>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 
@@ -1016,16 +1018,20 @@ std::unique_ptr<WebSocket> WebSocket::connect(HttpClient& http, const std::strin
   std::string rest;
   if (!read_response_head(*c, &resp, &rest, timeout_ms)) throw NetError("websocket: no handshake response");
   if (resp.status != 101) {
-    // read error body for a useful message
+    // read the error body for a useful message: Content-Length bytes when the server sized it
+    // (a keep-alive 429 would otherwise hold us for the read timeout), else up to EOF
     std::string body = rest;
+    std::string cl = resp.header("content-length");
+    size_t want = cl.empty() ? 65536 : std::min<size_t>(65536, (size_t)std::strtoull(cl.c_str(), nullptr, 10));
     char tmp[4096];
-    while (body.size() < 65536) {
+    while (body.size() < want) {
       ssize_t n = c->read(tmp, sizeof(tmp), 2000);
       if (n <= 0) break;
       body.append(tmp, (size_t)n);
     }
     throw UpgradeError(resp.status,
-                       "websocket upgrade failed: " + std::to_string(resp.status) + " " + resp.reason + ": " + body);
+                       "websocket upgrade failed: " + std::to_string(resp.status) + " " + resp.reason + ": " + body,
+                       resp.header("retry-after"));
   }
   if (resp.header("sec-websocket-accept") != websocket_accept(key))
     throw NetError("websocket upgrade failed: bad Sec-WebSocket-Accept from server");

@@ -25,10 +25,13 @@ struct NetError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
-// A WebSocket upgrade answered with a non-101 status (e.g. 401 → refresh credentials).
+// A WebSocket upgrade answered with a non-101 status (e.g. 401 → refresh credentials, 429 →
+// wait `retry_after` and try again).
 struct UpgradeError : NetError {
   int status;
-  UpgradeError(int st, const std::string& msg) : NetError(msg), status(st) {}
+  std::string retry_after;  // the response's Retry-After header ("" if none)
+  UpgradeError(int st, const std::string& msg, std::string ra = "")
+      : NetError(msg), status(st), retry_after(std::move(ra)) {}
 };
 
 struct TlsOptions {

@@ -300,6 +300,29 @@ std::shared_ptr<Client> Client::from_devspace_config(const Value& cfg, bool swit
   return std::make_shared<Client>(rc);
 }
 
+int retry_wait_ms(int status, const std::string& retry_after, const std::string& method) {
+  bool too_many = status == 429;
+  bool unavailable = status >= 500 && status <= 599 && !retry_after.empty();
+  if (!too_many && !unavailable) return -1;
+  if (!too_many && method == "POST") return -1;  // a 5xx POST may have been acted on
+  int64_t secs = 1;
+  std::string ra = trim(retry_after);
+  if (!ra.empty() && ra.size() <= 9 && std::all_of(ra.begin(), ra.end(), [](char c) { return c >= '0' && c <= '9'; }))
+    secs = std::atoll(ra.c_str());
+  return (int)std::min<int64_t>(secs, kMaxRetryAfterS) * 1000;
+}
+
+void Client::throttled(const std::string& what, int status, int wait_ms, int attempt) {
+  throttle_retries_++;
+  static std::atomic<bool> logged{false};
+  if (!logged.exchange(true))
+    log::warn("The API server is throttling requests (" + std::to_string(status) + " on " + what +
+              "): retrying after Retry-After, up to " + std::to_string(kMaxApiRetries) + " times per request");
+  log::debug("retry " + std::to_string(attempt) + "/" + std::to_string(kMaxApiRetries) + " of " + what +
+             " in " + std::to_string(wait_ms) + " ms (" + std::to_string(status) + ")");
+  if (wait_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(wait_ms));
+}
+
 net::Response Client::raw(const std::string& method, const std::string& path, const std::string& body,
                           const std::string& content_type, int timeout_ms) {
   net::Request r;
@@ -308,10 +331,14 @@ net::Response Client::raw(const std::string& method, const std::string& path, co
   r.body = body;
   r.timeout_ms = timeout_ms;
   if (!body.empty()) r.headers.push_back({"Content-Type", content_type});
-  ensure_fresh_credentials();
-  net::Response resp = http_.request(r);
-  if (resp.status == 401 && refresh_after_unauthorized()) resp = http_.request(r);
-  return resp;
+  for (int attempt = 1;; ++attempt) {
+    ensure_fresh_credentials();
+    net::Response resp = http_.request(r);
+    if (resp.status == 401 && refresh_after_unauthorized()) resp = http_.request(r);
+    int wait = retry_wait_ms(resp.status, resp.header("retry-after"), method);
+    if (wait < 0 || attempt > kMaxApiRetries) return resp;
+    throttled(method + " " + path, resp.status, wait, attempt);
+  }
 }
 
 static Value check(const net::Response& r, const std::string& what) {
@@ -360,11 +387,18 @@ int Client::stream(const std::string& path, const std::function<bool(const std::
   r.path = path;
   r.timeout_ms = timeout_ms;
   r.errors_to_body = true;
-  ensure_fresh_credentials();
-  net::Response resp = http_.stream(r, on_data);
-  if (resp.status == 401 && refresh_after_unauthorized()) resp = http_.stream(r, on_data);
-  if (resp.status >= 400) check(resp, "GET " + path);
-  return resp.status;
+  for (int attempt = 1;; ++attempt) {
+    ensure_fresh_credentials();
+    net::Response resp = http_.stream(r, on_data);  // error bodies never reach on_data
+    if (resp.status == 401 && refresh_after_unauthorized()) resp = http_.stream(r, on_data);
+    int wait = retry_wait_ms(resp.status, resp.header("retry-after"), "GET");
+    if (wait >= 0 && attempt <= kMaxApiRetries) {
+      throttled("GET " + path, resp.status, wait, attempt);
+      continue;
+    }
+    if (resp.status >= 400) check(resp, "GET " + path);
+    return resp.status;
+  }
 }
 
 std::vector<Value> Client::list_pods(const std::string& ns, const std::string& sel) {
@@ -768,13 +802,22 @@ std::unique_ptr<net::WebSocket> Client::portforward(const std::string& ns, const
 
 std::unique_ptr<net::WebSocket> Client::ws_connect(const std::string& path, const std::vector<std::string>& protocols,
                                                    std::unique_ptr<net::Conn> spare) {
-  ensure_fresh_credentials();
-  try {
-    return net::WebSocket::connect(http_, path, protocols, 30000, std::move(spare));
-  } catch (const net::UpgradeError& e) {
-    if (e.status != 401 || !refresh_after_unauthorized()) throw;
+  bool refreshed = false;
+  for (int attempt = 1;; ++attempt) {
+    ensure_fresh_credentials();
+    try {
+      return net::WebSocket::connect(http_, path, protocols, 30000, std::move(spare));
+    } catch (const net::UpgradeError& e) {
+      if (e.status == 401 && !refreshed && refresh_after_unauthorized()) {
+        refreshed = true;
+        continue;
+      }
+      // the upgrade is a GET (exec/attach/portforward): a refused handshake ran nothing
+      int wait = retry_wait_ms(e.status, e.retry_after, "GET");
+      if (wait < 0 || attempt > kMaxApiRetries) throw;
+      throttled("upgrade " + path, e.status, wait, attempt);
+    }
   }
-  return net::WebSocket::connect(http_, path, protocols);
 }
 
 // ---------------------------------------------------------------- exec session

@@ -57,6 +57,17 @@ std::string resource_path(const std::string& api_version, const std::string& kin
 std::string plural_of(const std::string& kind);
 bool is_cluster_scoped(const std::string& kind);
 
+// client-go's REST retry rule (k8s.io/client-go/rest/request.go checkWait with maxRetries 10;
+// the reference gets it through kubernetes.NewForConfig, kubectl/client.go:34-51): a
+// `429 Too Many Requests` (API Priority and Fairness throttling) or a 5xx carrying Retry-After
+// is sent again after the server's delay. Unlike client-go, a POST is retried only on 429 (the
+// server did not act on it), never on a 5xx, where it may have. Returns the wait in ms before
+// the retry, or -1 for "do not retry". Retry-After: delta-seconds (an HTTP-date or garbage counts
+// as 1 s), capped at kMaxRetryAfterS; a 429 without the header waits 1 s.
+constexpr int kMaxApiRetries = 10;
+constexpr int kMaxRetryAfterS = 10;
+int retry_wait_ms(int status, const std::string& retry_after, const std::string& method);
+
 class ExecSession;
 
 class Client {
@@ -142,8 +153,13 @@ class Client {
   void ensure_fresh_credentials();
   bool refresh_after_unauthorized();
   int credential_refreshes() const { return refreshes_; }
+  // Requests sent again after a 429 / 5xx + Retry-After (all verbs, all streams).
+  int throttle_retries() const { return throttle_retries_; }
 
  private:
+  // Before retry `attempt` (1-based) of a throttled request: counts it, logs the first
+  // throttling of the process once, sleeps `wait_ms`.
+  void throttled(const std::string& what, int status, int wait_ms, int attempt);
   void refresh_exec_credentials();
   void apply_auth_locked();
   std::unique_ptr<net::WebSocket> ws_connect(const std::string& path, const std::vector<std::string>& protocols,
@@ -156,6 +172,7 @@ class Client {
   int64_t token_expiry_ = 0;      // unix seconds, 0 = no expiry
   int64_t token_file_read_ = 0;   // unix seconds of the last tokenFile read
   std::atomic<int> refreshes_{0};
+  std::atomic<int> throttle_retries_{0};
 };
 
 // A running exec/attach: stdin/stdout/stderr exposed as pipes (so the sync engine and the

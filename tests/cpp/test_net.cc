@@ -18,6 +18,7 @@
 #include "core/resolve.h"
 #include "core/strutil.h"
 #include "deploy/sprig_crypto.h"
+#include "kube/client.h"
 #include "services/services.h"
 #include "testing.h"
 
@@ -107,6 +108,41 @@ void respond(int fd, const std::string& body) {
   std::string r = "HTTP/1.1 200 OK\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n" + body;
   ::write(fd, r.data(), r.size());
 }
+
+void respond_status(int fd, int status, const std::string& retry_after) {
+  std::string body = "{\"kind\":\"Status\",\"code\":" + std::to_string(status) + "}";
+  std::string r = "HTTP/1.1 " + std::to_string(status) + " X\r\nContent-Type: application/json\r\n" +
+                  (retry_after.empty() ? "" : "Retry-After: " + retry_after + "\r\n") +
+                  "Content-Length: " + std::to_string(body.size()) + "\r\n\r\n" + body;
+  ::write(fd, r.data(), r.size());
+}
+
+// An API server that answers the first `fail` requests with `status` (+ Retry-After), then 200;
+// counts requests per method.
+struct ThrottlingServer {
+  std::atomic<int> seen{0}, posts{0}, gets{0};
+  int fail, status;
+  std::string retry_after;
+  ScriptedServer srv;
+  ThrottlingServer(int fail_, int status_, std::string ra)
+      : fail(fail_), status(status_), retry_after(std::move(ra)), srv([this](int fd, int) {
+          std::string body;
+          while (true) {
+            std::string head = read_request(fd, &body);
+            if (head.empty()) return;
+            (starts_with(head, "POST") ? posts : gets)++;
+            if (seen++ < fail)
+              respond_status(fd, status, retry_after);
+            else
+              respond(fd, "{\"kind\":\"Pod\"}");
+          }
+        }) {}
+  kube::RestConfig rc() const {
+    kube::RestConfig c;
+    c.server = srv.url();
+    return c;
+  }
+};
 
 }  // namespace
 
@@ -299,4 +335,76 @@ TEST(tls_client_resumes_sessions) {
   BIO_free(kb);
   srv.stop = true;
   SSL_CTX_free(sctx);
+}
+
+// client-go's retry rule. 429 and 5xx + Retry-After are sent again after the
+// header's delay, up to 10 times; a POST is retried on 429 only.
+TEST(api_retry_rule_matches_client_go) {
+  EXPECT_EQ(kube::retry_wait_ms(429, "1", "POST"), 1000);
+  EXPECT_EQ(kube::retry_wait_ms(429, "", "GET"), 1000);
+  EXPECT_EQ(kube::retry_wait_ms(429, "0", "PATCH"), 0);
+  EXPECT_EQ(kube::retry_wait_ms(429, "3600", "GET"), kube::kMaxRetryAfterS * 1000);
+  EXPECT_EQ(kube::retry_wait_ms(429, "Wed, 21 Oct 2015 07:28:00 GMT", "GET"), 1000);
+  EXPECT_EQ(kube::retry_wait_ms(503, "2", "GET"), 2000);
+  EXPECT_EQ(kube::retry_wait_ms(503, "2", "DELETE"), 2000);
+  EXPECT_EQ(kube::retry_wait_ms(503, "2", "POST"), -1);
+  EXPECT_EQ(kube::retry_wait_ms(503, "", "GET"), -1);  // a plain 5xx is an error
+  EXPECT_EQ(kube::retry_wait_ms(500, "", "PUT"), -1);
+  EXPECT_EQ(kube::retry_wait_ms(404, "1", "GET"), -1);
+  EXPECT_EQ(kube::retry_wait_ms(200, "1", "GET"), -1);
+}
+
+TEST(api_client_retries_throttled_requests) {
+  ThrottlingServer ts(3, 429, "0");
+  kube::Client c(ts.rc());
+  Value v = c.get("/api/v1/namespaces/x/pods/p");
+  EXPECT_EQ(v.get("kind").as_string(), std::string("Pod"));
+  EXPECT_EQ(ts.gets.load(), 4);
+  EXPECT_EQ(c.throttle_retries(), 3);
+  // a 429'd POST was not acted on: sent again
+  ThrottlingServer tp(2, 429, "0");
+  kube::Client cp(tp.rc());
+  cp.post("/api/v1/namespaces/x/pods", Value::map());
+  EXPECT_EQ(tp.posts.load(), 3);
+}
+
+TEST(api_client_never_retries_a_post_on_5xx) {
+  ThrottlingServer ts(1, 503, "0");
+  kube::Client c(ts.rc());
+  bool threw = false;
+  try {
+    c.post("/api/v1/namespaces/x/pods", Value::map());
+  } catch (const kube::ApiError& e) {
+    threw = e.code == 503;
+  }
+  EXPECT_TRUE(threw);
+  EXPECT_EQ(ts.posts.load(), 1);
+  EXPECT_EQ(c.throttle_retries(), 0);
+  // the same 503 + Retry-After on an idempotent verb is retried
+  ThrottlingServer tg(1, 503, "0");
+  kube::Client cg(tg.rc());
+  cg.del("/api/v1/namespaces/x/pods/p");
+  EXPECT_EQ(tg.gets.load(), 2);
+}
+
+TEST(api_client_gives_up_after_ten_retries) {
+  ThrottlingServer ts(1000, 429, "0");
+  kube::Client c(ts.rc());
+  bool threw = false;
+  try {
+    c.get("/api/v1/namespaces/x/pods");
+  } catch (const kube::ApiError& e) {
+    threw = e.code == 429;
+  }
+  EXPECT_TRUE(threw);
+  EXPECT_EQ(ts.gets.load(), 1 + kube::kMaxApiRetries);
+}
+
+TEST(api_client_waits_retry_after) {
+  ThrottlingServer ts(1, 429, "1");
+  kube::Client c(ts.rc());
+  auto t0 = std::chrono::steady_clock::now();
+  c.get("/api/v1/namespaces/x/pods/p");
+  auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+  EXPECT_TRUE(ms >= 950 && ms < 3000);
 }
