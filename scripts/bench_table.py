@@ -7,9 +7,11 @@ builder's own runs under ``profiles/``), so the README quotes exactly what the d
 
 The README block sits between ``<!-- bench-table source=FILE -->`` and ``<!-- /bench-table -->``;
 ``tests/test_readme_bench.py`` checks that it equals what this script renders from FILE.
-Handles both bench.py line formats: round 2 (``value`` = rocm-pytorch pod reload, quickstart
-under ``quickstart``) and round 3+ (``value`` = quickstart reload, extras under ``gpu_pod``,
-``deploy``, ``php_mysql``, ``microservices``, ``kaniko``).
+Handles the bench.py line formats: round 2 (``value`` = rocm-pytorch pod reload, quickstart
+under ``quickstart``), round 3 (``value`` = quickstart reload with the example's standby pool,
+cold restarts under ``cold_restart``) and round 4+ (``value`` = quickstart with cold restarts,
+``config.restart == "cold"``, the pool under ``standby_pool``); extras under ``gpu_pod``,
+``deploy``, ``php_mysql``, ``microservices``, ``kaniko``.
 """
 
 import argparse
@@ -56,9 +58,16 @@ def render(path):
     round3 = "gpu_pod" in b or "php_mysql" in b or b.get("config", {}).get("app") == "examples/quickstart"
     if round3:
         ref = b.get("reference_equivalent", {})
-        rows.append(("edit → new response p50, quickstart (headline `value`)",
+        cold_headline = b.get("config", {}).get("restart") == "cold"
+        rows.append(("edit → new response p50, quickstart, cold restarts as nodemon (headline `value`: the tool's loop)"
+                     if cold_headline else "edit → new response p50, quickstart (headline `value`)",
                      f"**{_ms(b['value'])}** (p90 {_ms(b.get('p90_ms'))}; sync {_ms(b.get('sync_p50_ms'))})",
                      _ms(ref.get("p50_ms")) + _x(b["value"], ref.get("p50_ms"))))
+        pool = b.get("standby_pool")
+        if isinstance(pool, dict) and "p50_ms" in pool:
+            rows.append(("edit → new response p50, quickstart with the example app's pre-booted node standbys "
+                         "(app-side, not the tool)",
+                         f"{_ms(pool['p50_ms'])} (p90 {_ms(pool.get('p90_ms'))})", "—"))
         cold = b.get("cold_restart")
         if isinstance(cold, dict) and "p50_ms" in cold:
             rows.append(("edit → new response p50, quickstart with cold restarts (the tool alone, no standby pool)",
