@@ -23,9 +23,12 @@ def main(argv=None):
     up.add_argument("--throttle-first", type=int, default=0,
                     help="fault switch: answer the first K requests of every (verb, resource) with 429")
     up.add_argument("--retry-after", type=int, default=1, help="Retry-After seconds of the throttled answers")
+    up.add_argument("--pull-seconds", type=float, default=0.0,
+                    help="slow-pull mode: every image takes this long to pull the first time (Pulling events)")
     args = ap.parse_args(argv)
     c = LocalCluster(args.state, port=args.port, gpus=args.gpus, context=args.context, tls=args.tls).start()
     c.api.reset_throttle(args.throttle_first, args.retry_after)
+    c.kubelet.pull_seconds = args.pull_seconds
     kc = args.kubeconfig or os.path.join(args.state, "kubeconfig")
     c.write_kubeconfig(kc, args.namespace)
     print(f"ready server={c.server} kubeconfig={kc} docker=unix://{c.docker_sock} gpus={c.gpus}", flush=True)

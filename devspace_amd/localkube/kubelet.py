@@ -85,6 +85,9 @@ class Container:
         self.started_at = None
         self.image_config = {}
         self.fatal = None  # waiting reason that will not recover (ErrImagePull, ...)
+        self.fatal_at = 0.0
+        self.pulling = False  # slow-pull mode: its `Pulling` event was sent
+        self.pull_started_now = False
         # Output streaming (like a CRI log pipe): the pump appends to the log file and pushes
         # (offset, chunk) to attach/follow subscribers as soon as the process writes it;
         # (None, None) marks the end of this process' output.
@@ -139,6 +142,12 @@ class Kubelet:
         self._stop = False
         self._event_names = {}  # (ns, uid, reason, message, type) -> Event name, for aggregation
         self._exited_procs = []
+        # Slow-pull mode: an image this node has not pulled yet takes `pull_seconds` to pull
+        # (a first `rocm/pytorch` pull onto a fresh GPU node takes minutes): the container waits
+        # in ContainerCreating after a `Pulling` event, then `Pulled` ("Successfully pulled ...").
+        self.pull_seconds = 0.0
+        self.pulled = set()
+        self._pull_done = {}  # image -> monotonic time its pull completes
 
     # ------------------------------------------------------------ node
 
@@ -427,6 +436,26 @@ class Kubelet:
         self.pods[(md["namespace"], md["name"])] = rt
         return rt
 
+    def _pulled(self, pod, c):
+        """Slow-pull mode: False while the container's image is still being pulled (the first
+        call emits the `Pulling` event), True once it is on the node."""
+        image = c.spec.get("image", "")
+        if self.pull_seconds <= 0 or image in self.pulled or self.images.resolve(image) is None:
+            return True  # an image that does not exist fails in _prepare_rootfs (ErrImagePull)
+        now = time.monotonic()
+        done = self._pull_done.get(image)
+        if done is None:
+            done = self._pull_done[image] = now + self.pull_seconds
+        if not c.pulling:
+            c.pulling = True
+            c.pull_started_now = True
+            self.event(pod, "Pulling", f'Pulling image "{image}"')
+        if now < done:
+            return False
+        self.pulled.add(image)
+        self.event(pod, "Pulled", f'Successfully pulled image "{image}" in {self.pull_seconds:.3f}s')
+        return True
+
     def _prepare_rootfs(self, rt, c, pod):
         image = c.spec.get("image", "")
         img = self.images.resolve(image)
@@ -560,13 +589,26 @@ class Kubelet:
         changed = False
         for name, c in rt.containers.items():
             if c.fatal:
+                if c.fatal == "ErrImagePull" and time.monotonic() - c.fatal_at >= 1.0:
+                    # the kubelet's image back-off, as on a real node: ErrImagePull -> ImagePullBackOff
+                    image = c.spec.get("image", "")
+                    c.fatal = "ImagePullBackOff"
+                    c.state = {"waiting": {"reason": "ImagePullBackOff",
+                                           "message": f'Back-off pulling image "{image}"'}}
+                    self.event(pod, "BackOff", f'Back-off pulling image "{image}"', "Warning")
+                    changed = True
                 continue
             if c.proc is None and c.started_at is None and c.restarts == 0 and not c.next_start:
+                if not self._pulled(pod, c):
+                    changed |= c.pull_started_now
+                    c.pull_started_now = False
+                    continue
                 t0 = time.perf_counter()
                 reason, msg = self._prepare_rootfs(rt, c, pod)
                 if reason:
                     c.state = {"waiting": {"reason": reason, "message": msg}}
                     c.fatal = reason
+                    c.fatal_at = time.monotonic()
                     self.event(pod, "Failed", msg, "Warning")
                     changed = True
                     continue

@@ -159,6 +159,9 @@ ENV = {
     "DEVSPACE_REFERENCE_TIMING": "`1` reproduces the original DevSpace's waits (1 s pod-discovery sleeps, 5 s "
                                  "rollout polls, no kept-alive connections, no TLS session reuse); used for the "
                                  "benchmark's reference column.",
+    "DEVSPACE_PULL_TIMEOUT": "Seconds a rollout wait may last in all while a pod of the release is still pulling "
+                             "its image (default 1800); past the chart's timeout the wait goes on only for "
+                             "pulls, and a first install whose pull outlasts this is kept, not purged.",
     "DEVSPACE_RELEASE_REPO": "GitHub `owner/repo` whose releases `devspace upgrade` installs.",
     "DEVSPACE_RELEASE_URL": "Plain HTTP(S) release mirror for `devspace upgrade` (`<url>/latest`, "
                             "`<url>/devspace-linux-amd64` and its `.sha256`).",
@@ -177,6 +180,11 @@ ENV = {
                             "gfx950 table) or `online` (tune unseen shapes, persist them).",
     "DEVSPACE_GEMM_TUNING_FILE": "Where `online` GEMM tuning persists its table.",
     "DEVSPACE_GEMM_TUNING_MS": "Time budget per shape of `online` GEMM tuning (default 30).",
+    "DEVSPACE_RUNNER_DEBUG": "`1`: every runner rank logs the code digest it loaded for each generation.",
+    "DEVSPACE_RUNNER_FAULT": "Test-only fault injection of the runner (`mutate-entry-after-read`, `skew-helper`): "
+                             "edits racing the ranks' reads, to exercise the code agreement.",
+    "DEVSPACE_RUNNER_STATUS_FD": "Set by the runner's supervisor for its ranks: the pipe they report `ready` / "
+                                 "`fail` on.",
     "DEVSPACE_NPROC": "Training processes the runner starts when the pod requests no GPU (CPU runs).",
     "DEVSPACE_OPS_CACHE": "Where a project's vendored gfx950 ops are compiled and cached (default "
                           "`~/.cache/devspace_amd`).",

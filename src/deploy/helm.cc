@@ -862,11 +862,127 @@ static std::string not_ready_reason(const std::string& kind, const std::string& 
   return "";
 }
 
-std::string Client::wait_ready(const std::vector<Value>& objs, const std::string& ns, int timeout_s) {
+// What the pods of one workload are doing, for the rollout wait: a reason they can never start
+// (fail fast instead of waiting out the timeout), or an image pull in progress (worth waiting
+// for: a first pull of a tens-of-GB rocm/pytorch image onto a fresh node takes minutes).
+struct PodProgress {
+  std::string fatal;  // "pod p: container c: ImagePullBackOff: <message>" / "pod p: Unschedulable: ..."
+  std::string pulling;  // "pod p: Pulling image \"x\"" ("" if none pulls)
+  int64_t pulling_since = 0;  // unix seconds of the oldest pull in progress
+};
+
+static int64_t event_time(const std::string& ts) {
+  struct tm t{};
+  if (ts.size() < 19 || !strptime(ts.c_str(), "%Y-%m-%dT%H:%M:%S", &t)) return 0;
+  return (int64_t)timegm(&t);
+}
+
+static bool fatal_waiting_reason(const std::string& r) {
+  return r == "ErrImagePull" || r == "ImagePullBackOff" || r == "InvalidImageName" || r == "ErrImageNeverPull";
+}
+
+static std::string match_labels_selector(const Value& workload) {
+  std::vector<std::string> parts;
+  for (auto& kv : workload.at_path("spec.selector.matchLabels").entries())
+    parts.push_back(kv.first + "=" + kv.second.as_string());
+  return join(parts, ",");
+}
+
+static PodProgress pod_progress(kube::Client& k, const Value& workload, const std::string& ns) {
+  PodProgress out;
+  std::string sel = match_labels_selector(workload);
+  if (sel.empty()) return out;
+  std::vector<Value> pods;
+  try {
+    pods = k.list_pods(ns, sel);
+  } catch (const std::exception&) {
+    return out;
+  }
+  std::vector<const Value*> creating;
+  for (auto& p : pods) {
+    if (!p.at_path("metadata.deletionTimestamp").is_null()) continue;
+    std::string pn = p.at_path("metadata.name").as_string();
+    for (auto& c : p.at_path("status.conditions").items())
+      if (c.get("type").as_string() == "PodScheduled" && c.get("status").as_string() == "False" &&
+          c.get("reason").as_string() == "Unschedulable") {
+        out.fatal = "pod " + pn + ": Unschedulable: " + c.get("message").as_string();
+        return out;
+      }
+    bool waiting_create = false;
+    for (const char* field : {"status.initContainerStatuses", "status.containerStatuses"})
+      for (auto& cs : p.at_path(field).items()) {
+        std::string r = cs.at_path("state.waiting.reason").as_string();
+        if (fatal_waiting_reason(r)) {
+          out.fatal = "pod " + pn + ": container " + cs.get("name").as_string() + ": " + r +
+                      (cs.at_path("state.waiting.message").as_string().empty()
+                           ? ""
+                           : ": " + cs.at_path("state.waiting.message").as_string());
+          return out;
+        }
+        if (r == "ContainerCreating" || r == "PodInitializing") waiting_create = true;
+      }
+    if (waiting_create || p.at_path("status.containerStatuses").items().empty()) creating.push_back(&p);
+  }
+  if (creating.empty()) return out;
+  // A pod pulls while its kubelet has reported more `Pulling` than `Successfully pulled` events
+  // for it (`Pulled` also says "already present on machine": no pull happened then).
+  Value evs;
+  try {
+    evs = k.get("/api/v1/namespaces/" + ns + "/events");
+  } catch (const std::exception&) {
+    return out;
+  }
+  for (const Value* p : creating) {
+    std::string pn = p->at_path("metadata.name").as_string();
+    std::string uid = p->at_path("metadata.uid").as_string();
+    int64_t pulls = 0, pulled = 0, since = 0;
+    std::string what;
+    for (auto& e : evs.get("items").items()) {
+      const Value& io = e.get("involvedObject");
+      if (io.get("kind").as_string() != "Pod" || io.get("name").as_string() != pn) continue;
+      if (!uid.empty() && !io.get("uid").as_string().empty() && io.get("uid").as_string() != uid) continue;
+      int64_t n = std::max<int64_t>(1, e.get("count").as_int(1));
+      std::string reason = e.get("reason").as_string();
+      if (reason == "Pulling") {
+        pulls += n;
+        what = e.get("message").as_string();
+        int64_t t = event_time(e.get("firstTimestamp").as_string(e.get("eventTime").as_string()));
+        if (t > 0 && (since == 0 || t < since)) since = t;
+      } else if (reason == "Pulled" && starts_with(e.get("message").as_string(), "Successfully pulled")) {
+        pulled += n;
+      }
+    }
+    if (pulls > pulled) {
+      out.pulling = "pod " + pn + ": " + what;
+      out.pulling_since = since;
+      return out;
+    }
+  }
+  return out;
+}
+
+static int pull_budget_s() {
+  const char* v = getenv("DEVSPACE_PULL_TIMEOUT");
+  int s = v && *v ? atoi(v) : 1800;
+  return s > 0 ? s : 1800;
+}
+
+Client::WaitOutcome Client::wait_ready(const std::vector<Value>& objs, const std::string& ns, int timeout_s) {
   // One watch per workload object (fieldSelector=metadata.name), in manifest order: the
   // status change that makes a rollout ready is seen the moment the API server commits it,
-  // with no polling; the total wait is bounded by the slowest object.
-  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
+  // with no polling; the total wait is bounded by the slowest object. A workload not ready
+  // within a second gets its pods looked at once a second: a pod that can never start fails the
+  // wait at once, and one still pulling its image carries the wait past `timeout_s` (reference:
+  // helm/install.go:171-195 explains a timeout with an analyze report; analyze/pods.go:50-117
+  // waits on ContainerCreating pods).
+  using clock = std::chrono::steady_clock;
+  auto start = clock::now();
+  auto deadline = start + std::chrono::seconds(timeout_s);
+  auto pull_deadline = start + std::chrono::seconds(std::max(timeout_s, pull_budget_s()));
+  auto ms_until = [](clock::time_point t) {
+    return (int64_t)std::chrono::duration_cast<std::chrono::milliseconds>(t - clock::now()).count();
+  };
+  bool told = false;
   for (auto& o : objs) {
     std::string kind = o.get("kind").as_string();
     if (kind != "Deployment" && kind != "StatefulSet" && kind != "ReplicaSet" && kind != "DaemonSet" &&
@@ -875,17 +991,48 @@ std::string Client::wait_ready(const std::vector<Value>& objs, const std::string
     std::string name = o.at_path("metadata.name").as_string();
     std::string ons = o.at_path("metadata.namespace").as_string(ns);
     std::string path = kube::resource_path(o.get("apiVersion").as_string(), kind, ons, name);
-    int64_t left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count();
     std::string pending = kind + " " + name + " not checked";
-    bool ok = left > 0 && k_->wait_object(path, (int)left, [&](const std::optional<Value>& cur) {
+    auto ready = [&](const std::optional<Value>& cur) {
       // a PVC that is gone (pvc-protection released it) is nothing to wait for
       if (!cur && kind == "PersistentVolumeClaim") return true;
       pending = not_ready_reason(kind, name, cur);
       return pending.empty();
-    });
-    if (!ok) return "timed out waiting for the condition (" + pending + ")";
+    };
+    while (true) {
+      int64_t left = ms_until(deadline);
+      int slice = (int)(left > 0 ? std::min<int64_t>(left, 1000) : std::min<int64_t>(1000, ms_until(pull_deadline)));
+      if (slice > 0 && k_->wait_object(path, slice, ready)) break;
+      if (kind == "PersistentVolumeClaim") {
+        if (ms_until(deadline) > 0) continue;
+        return {"timed out waiting for the condition (" + pending + ")"};
+      }
+      PodProgress pp = pod_progress(*k_, o, ons);
+      if (!pp.fatal.empty()) {
+        WaitOutcome w;
+        w.err = "rollout failed: " + pp.fatal + " (" + pending + ")";
+        w.fatal = true;
+        return w;
+      }
+      if (ms_until(deadline) > 0) continue;
+      if (!pp.pulling.empty() && ms_until(pull_deadline) > 0) {
+        if (!told) {
+          int64_t secs = pp.pulling_since > 0 ? (int64_t)time(nullptr) - pp.pulling_since : 0;
+          log::info(pp.pulling + " (" + std::to_string(secs) + " s so far): waiting for the pull, up to " +
+                    std::to_string(std::max(timeout_s, pull_budget_s())) + " s in all (DEVSPACE_PULL_TIMEOUT)");
+          told = true;
+        }
+        continue;
+      }
+      WaitOutcome w;
+      w.err = "timed out waiting for the condition (" + pending + ")";
+      if (!pp.pulling.empty()) {
+        w.err += "; " + pp.pulling + " is still in progress";
+        w.pulling = true;
+      }
+      return w;
+    }
   }
-  return "";
+  return {};
 }
 
 // ============================================================== hooks
@@ -1073,6 +1220,7 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
   r.last_deployed = log::rfc3339_now();
   r.first_deployed = hist.empty() ? r.last_deployed : hist.front().first_deployed;
   std::string err;
+  bool still_pulling = false, rollout_failed = false;
   try {
     run_hooks(r.hooks, ro.is_install ? "pre-install" : "pre-upgrade", ns, timeout_s);
     for (auto& o : objs) k_->apply(o, ns);
@@ -1094,16 +1242,23 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
       // satisfy (check_gpu_requests) is not waited out: the analyze report follows at once.
       int wait_s = timeout_s > 0 ? timeout_s : (kube::Client::max_gpu_request(objs) > 0 ? 300 : 40);
       if (!gpu_issue.empty()) wait_s = std::min(wait_s, 5);
-      err = wait_ready(objs, ns, wait_s);
+      WaitOutcome w = wait_ready(objs, ns, wait_s);
+      err = w.err;
+      still_pulling = w.pulling;
+      rollout_failed = w.fatal;
     }
-    // install.go:181 analyzeError: a wait timeout is explained by an analyze report of the
-    // namespace; no problems found means the release is fine (just slow).
-    if (contains(err, "timed out waiting")) {
+    // install.go:181 analyzeError: a wait timeout (or a pod that can never start) is explained
+    // by an analyze report of the namespace; after a plain timeout, no problems found means the
+    // release is fine (just slow). A pull still in progress is not analyzed as a problem.
+    if ((contains(err, "timed out waiting") && !still_pulling) || rollout_failed) {
       try {
         analyze::Options ao;
         ao.wait = false;
         auto report = analyze::create_report(*k_, ns, ao);
-        err = report.empty() ? "" : analyze::report_to_string(report);
+        if (rollout_failed)
+          err += report.empty() ? "" : "\n" + analyze::report_to_string(report);
+        else
+          err = report.empty() ? "" : analyze::report_to_string(report);
       } catch (const std::exception& e) {
         log::warn(std::string("Error creating analyze report: ") + e.what());
       }
@@ -1123,6 +1278,11 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
       } catch (const std::exception& e) {
         log::error(std::string("Rollback failed: ") + e.what());
       }
+    } else if (still_pulling) {
+      // a first install whose pods are still pulling is not purged (the reference's purge,
+      // install.go:155-161, would delete the pod mid-pull and start the pull over next time)
+      log::warn("Keeping release " + name + ": its image pull goes on in the cluster; run the command again "
+                "to keep waiting, or raise DEVSPACE_PULL_TIMEOUT");
     } else {
       try {
         delete_release(ns, name, true);

@@ -112,7 +112,8 @@ class Client {
   bool release_exists(const std::string& ns, const std::string& name);
   std::vector<Release> list(const std::string& ns);
   // Install or upgrade; on failure an upgrade rolls back to the last deployed revision and a
-  // first install is purged (helm/install.go:100-166).
+  // first install is purged (helm/install.go:100-166) — unless its only problem is an image
+  // pull still in progress: then the failed release is kept and a re-run continues the wait.
   Release install_or_upgrade(const std::string& name, const std::string& ns, const std::string& chart_path,
                              const Value& values, bool wait, int timeout_s);
   void rollback(const std::string& ns, const std::string& name, int to_version);
@@ -121,8 +122,19 @@ class Client {
   // `devspace dev` session with auto-reload would otherwise pile them up.
   void set_max_history(int n) { max_history_ = n; }
   void delete_release(const std::string& ns, const std::string& name, bool purge = true);
-  // Waits for every workload in the manifest to be ready; returns "" or a failure summary.
-  std::string wait_ready(const std::vector<Value>& objs, const std::string& ns, int timeout_s);
+  // Outcome of a rollout wait. `err` is "" once every workload is ready. `fatal`: a pod of the
+  // release can not start (ErrImagePull, ImagePullBackOff, InvalidImageName, Unschedulable) —
+  // reported within seconds, not at the timeout. `pulling`: the wait ran out while a pod was still
+  // pulling its image (a first install keeps its release then: the pull goes on in the cluster).
+  struct WaitOutcome {
+    std::string err;
+    bool fatal = false;
+    bool pulling = false;
+  };
+  // Waits for every workload in the manifest to be ready. Pull-aware: past `timeout_s`, a pod
+  // whose kubelet reports `Pulling` (and nothing fatal) extends the wait, up to the pull budget
+  // (DEVSPACE_PULL_TIMEOUT, default 1800 s, counted from the start of the wait).
+  WaitOutcome wait_ready(const std::vector<Value>& objs, const std::string& ns, int timeout_s);
   // .Capabilities from the API server (cached per client).
   Value capabilities();
 
