@@ -594,7 +594,8 @@ std::string context_tar(const std::string& context_dir, const std::vector<std::s
 }
 
 bool write_context_tar(const Sink& out, const std::string& context_dir, const std::vector<std::string>& excludes,
-                       const std::string& rel_dockerfile, const std::optional<std::string>& dockerfile_override) {
+                       const std::string& rel_dockerfile, const std::optional<std::string>& dockerfile_override,
+                       const std::vector<std::pair<std::string, std::string>>& extra) {
   bool ok = true;
   Sink guarded = [&](const char* d, size_t n) { return ok = ok && out(d, n); };
   TarWriter tw(guarded);
@@ -629,6 +630,15 @@ bool write_context_tar(const Sink& out, const std::string& context_dir, const st
       tw.add_file_from_path(e, abs);
     }
   });
+  for (auto& f : extra) {
+    if (fs::exists(fs::join(context_dir, f.first))) continue;
+    TarEntry e;
+    e.name = f.first;
+    e.mode = 0644;
+    e.mtime = time(nullptr);
+    e.size = (int64_t)f.second.size();
+    tw.add_file(e, f.second);
+  }
   if (dockerfile_override && !replaced) {
     TarEntry e;
     e.name = rel_dockerfile;

@@ -140,9 +140,11 @@ std::string context_tar(const std::string& context_dir, const std::vector<std::s
                         const std::string& rel_dockerfile = "",
                         const std::optional<std::string>& dockerfile_override = std::nullopt);
 // Streaming form: the tar goes to `out` while the context is walked. false when `out` failed.
+// `extra`: files (relative path, content) added to the context where it has no such entry.
 bool write_context_tar(const Sink& out, const std::string& context_dir, const std::vector<std::string>& excludes,
                        const std::string& rel_dockerfile = "",
-                       const std::optional<std::string>& dockerfile_override = std::nullopt);
+                       const std::optional<std::string>& dockerfile_override = std::nullopt,
+                       const std::vector<std::pair<std::string, std::string>>& extra = {});
 
 // builder/util.go:43: Dockerfile content + ENTRYPOINT/CMD override (dev.overrideImages).
 std::string dockerfile_with_entrypoint(const std::string& dockerfile_content, const std::vector<std::string>& entrypoint);

@@ -18,6 +18,7 @@
 #include "core/safe_regex.h"
 #include "core/strutil.h"
 #include "core/trace.h"
+#include "generator/generator.h"
 #include "sync/sync.h"
 
 namespace ds {
@@ -151,6 +152,25 @@ std::pair<std::string, std::string> format_kaniko_line(const std::string& line) 
 
 namespace {
 
+// A project whose Dockerfile runs the workload kit (`python -m devspace_amd.runner`, the
+// rocm-pytorch template) but whose context lacks devspace_amd/ — a clean clone of
+// examples/rocm-pytorch, where the checkout's build writes the kit (git-ignored), or a project
+// whose kit copy was deleted — gets the kit this binary ships (the files `devspace init`
+// vendors) added to its build context, with a notice. A copy in the project always wins.
+std::vector<std::pair<std::string, std::string>> missing_workload_kit(const std::string& ctx,
+                                                                      const std::string& dockerfile_text) {
+  std::vector<std::pair<std::string, std::string>> out;
+  if (dockerfile_text.find("devspace_amd") == std::string::npos) return out;
+  if (fs::exists(fs::join(ctx, "devspace_amd/runner.py"))) return out;
+  const std::string prefix = "rocm-pytorch/";
+  for (auto& kv : generator::embedded_templates())
+    if (starts_with(kv.first, prefix + "devspace_amd/")) out.emplace_back(kv.first.substr(prefix.size()), kv.second);
+  if (!out.empty())
+    log::info("[image] " + ctx + " has no devspace_amd/ (the workload kit its Dockerfile runs): adding the kit "
+              "this devspace ships to the build context (`devspace init` vendors the same files)");
+  return out;
+}
+
 class DockerBuilder : public Builder {
  public:
   DockerBuilder(std::unique_ptr<DockerClient> c, ImageBuildSettings s) : c_(std::move(c)), s_(std::move(s)) {}
@@ -169,6 +189,7 @@ class DockerBuilder : public Builder {
     std::vector<std::string> excludes = context_excludes(ctx, outside ? "" : rel);
     std::optional<std::string> override_df;
     if (!entrypoint.empty()) override_df = dockerfile_with_entrypoint(fs::read_file(dockerfile), entrypoint);
+    auto kit = missing_workload_kit(ctx, fs::read_file(dockerfile));
     if (outside) {
       // build.AddDockerfileToBuildContext: ship it under a random name next to the context
       rel = ".dockerfile." + hex_encode(random_string(10)).substr(0, 20);
@@ -185,8 +206,8 @@ class DockerBuilder : public Builder {
     } catch (const std::exception&) {
     }
     // the context tar streams to the daemon while the tree is walked (bounded memory)
-    c_->build_stream([&](const Sink& sink) { return write_context_tar(sink, ctx, excludes, rel, override_df); }, req,
-                     write_out);
+    c_->build_stream([&](const Sink& sink) { return write_context_tar(sink, ctx, excludes, rel, override_df, kit); },
+                     req, write_out);
   }
 
   void push_image() override {
@@ -358,6 +379,21 @@ class KanikoBuilder : public Builder {
       auto t = std::make_shared<kube::ExecTransport>(k_, created, "kaniko");
       sync::Session::copy_to_container(t, ctx, "/src", ignore);
       sync::Session::copy_to_container(t, dockerfile, "/src", ignore);
+      auto kit = missing_workload_kit(ctx, fs::read_file(dockerfile));
+      if (!kit.empty()) {
+        std::string tmp = fs::make_temp_dir("devspace-kit-");
+        for (auto& f : kit) {
+          fs::mkdirs(fs::dirname(fs::join(tmp, f.first)));
+          fs::write_file(fs::join(tmp, f.first), f.second);
+        }
+        try {
+          sync::Session::copy_to_container(t, tmp, "/src", {});
+        } catch (...) {
+          fs::remove_all(tmp);
+          throw;
+        }
+        fs::remove_all(tmp);
+      }
     } catch (const std::exception& e) {
       log::stop_wait();
       throw std::runtime_error(std::string("Error uploading files to container: ") + e.what());

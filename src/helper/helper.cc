@@ -6,6 +6,10 @@
 //
 //   request := op:u8 len:u64be payload[len]
 //   'U' (len 0) + chunk stream of a tar (or tar.gz) -> extract under <dest>   reply "OK\n" | "ERR msg\n"
+//   'U' payload=lane:u8         -> open upload lane `lane`: its chunk stream arrives in 'C' frames
+//                                  and is extracted on a thread of its own  reply "@lane OK\n" | "@lane ERR msg\n"
+//   'C' payload=lane:u8 bytes   -> the next bytes of lane `lane`'s chunk stream (no reply)
+//   'X' payload=lane:u8 rel\n.. -> rm -rf <dest><rel>                          reply "@lane OK\n"
 //   'R' payload=rel\n...        -> rm -rf <dest><rel>                          reply "OK\n"
 //   'S' (empty)                 -> "<abs>///size,mtime,hexmode,perm,uid,gid\n"... then "DONE\n"
 //   'D' payload=rel\n...        -> "STREAM\n" + chunk stream of a tar (relative member names)
@@ -13,6 +17,11 @@
 //   'H' payload=rel\n...        -> one crc32 hex (or "-") per path, then "DONE\n"
 //   'W' (empty)                 -> start watching; "E\n" on stderr after foreign changes settle
 //   'Q'                          -> exit
+//
+// Lanes: the upstream session interleaves several uploads frame by frame on one stdin — a bulk
+// transfer (a multi-GB checkpoint) in one lane, a code edit in another — so an edit never waits
+// behind a bulk archive for more than one frame. Each lane extracts on its own thread, fed through
+// a pipe by the frame reader; extraction writes through temp names and renames as before.
 //
 // Archives are streamed through fixed-size buffers in both directions, so memory stays bounded
 // for files of any size (a multi-GB checkpoint written in a training pod is read and sent in
@@ -30,6 +39,7 @@
 
 #include <atomic>
 #include <climits>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -62,7 +72,9 @@ static long now_us() {
 // still holds exactly what we left there (same kind, size and mtime for files; absent for
 // removals): a pod process that rewrites a file it just received — a formatter, a code
 // generator — changes size or mtime and is reported at once. Records live while an op runs
-// and for kOwnEchoUs after it finished (the echo of a write arrives within milliseconds).
+// and for kOwnEchoUs after the last one finished (the echo of a write arrives within
+// milliseconds). The session runs its watch ('W') in this same process, the upstream one, so
+// the records of its own writes are where the watcher looks.
 struct OwnRecord {
   enum Kind { File, Dir, Link, Gone } kind = File;
   int64_t size = 0;
@@ -71,16 +83,18 @@ struct OwnRecord {
 static std::mutex g_own_mu;
 static std::map<std::string, OwnRecord> g_own;
 static std::set<std::string> g_gone_trees;  // removed subtrees: anything absent below is ours
-static long g_own_until = 0;  // monotonic us; LONG_MAX while an op runs
+static int g_own_active = 0;  // upstream ops running (lanes run concurrently)
+static long g_own_until = 0;  // monotonic us: records expire after this once no op runs
 static const long kOwnEchoUs = 2000000;
 
 static void own_begin() {
   std::lock_guard<std::mutex> g(g_own_mu);
-  g_own_until = LONG_MAX;
+  ++g_own_active;
 }
 
 static void own_end() {
   std::lock_guard<std::mutex> g(g_own_mu);
+  --g_own_active;
   g_own_until = now_us() + kOwnEchoUs;
 }
 
@@ -128,7 +142,7 @@ static bool matches(const OwnRecord& r, const std::string& p) {
 
 static bool is_own(const std::string& p) {
   std::lock_guard<std::mutex> g(g_own_mu);
-  if (now_us() > g_own_until) {
+  if (g_own_active == 0 && now_us() > g_own_until) {
     g_own.clear();
     g_gone_trees.clear();
     return false;
@@ -143,7 +157,11 @@ static bool is_own(const std::string& p) {
   return false;
 }
 
-static bool reply(const std::string& s) { return write_all(1, s); }
+static std::mutex g_reply_mu;  // lane threads reply concurrently with the main loop
+static bool reply(const std::string& s) {
+  std::lock_guard<std::mutex> g(g_reply_mu);
+  return write_all(1, s);
+}
 
 static std::string safe_join(const std::string& rel_in) {
   std::string rel = rel_in;
@@ -419,10 +437,50 @@ static void watch_loop() {
   }
 }
 
+// An upload lane: the frame reader writes the lane's chunk-stream bytes into `w`; the lane's
+// thread extracts from the other end and replies "@lane OK|ERR ...".
+struct Lane {
+  int w = -1;
+  std::thread t;
+};
+
+static std::string lane_tag(int lane) { return "@" + std::to_string(lane) + " "; }
+
+static void open_lane(std::map<int, Lane>& lanes, int lane) {
+  Lane& l = lanes[lane];
+  if (l.t.joinable()) l.t.join();  // the previous upload of this lane replied already
+  if (l.w >= 0) ::close(l.w);
+  int fds[2];
+  if (::pipe2(fds, O_CLOEXEC) != 0) {
+    reply(lane_tag(lane) + "ERR pipe: " + std::strerror(errno) + "\n");
+    std::_Exit(1);
+  }
+#ifdef F_SETPIPE_SZ
+  ::fcntl(fds[1], F_SETPIPE_SZ, 1 << 20);  // one frame in flight per lane without blocking the reader
+#endif
+  l.w = fds[1];
+  int r = fds[0];
+  l.t = std::thread([r, lane] {
+    std::string res;
+    {
+      OwnOp own;
+      frame::ChunkReader cr(fd_source(r));
+      try {
+        res = op_extract(cr.source());
+        cr.drain();  // an early error still consumes the lane's whole stream
+      } catch (const std::exception&) {
+        std::_Exit(1);  // the stream itself is broken: the session reconnects
+      }
+    }
+    ::close(r);
+    reply(lane_tag(lane) + res + "\n");
+  });
+}
+
 int main(int argc, char** argv) {
   if (argc < 3 || std::string(argv[1]) != "serve") {
     std::fprintf(stderr, "usage: devspace-helper serve <dest>\n");
-    return 2;
+    std::_Exit(2);
   }
   signal(SIGPIPE, SIG_IGN);
   g_dest = fs::clean(argv[2]);
@@ -430,12 +488,34 @@ int main(int argc, char** argv) {
   reply("HELPER READY\n");
   bool watching = false;
   Source in = fd_source(0);
+  std::map<int, Lane> lanes;
+  std::vector<char> cbuf;
   while (true) {
     unsigned char hdr[frame::kHeaderSize];
     if (!read_exact(0, hdr, sizeof(hdr))) break;
     char op;
     uint64_t len;
     frame::parse_header(hdr, &op, &len);
+    if (op == 'C') {  // lane data: straight from stdin into the lane's pipe
+      if (len < 1 || len > frame::kMaxChunk + 64) {
+        std::fprintf(stderr, "devspace-helper: bad lane frame of %llu bytes\n", (unsigned long long)len);
+        std::_Exit(1);
+      }
+      cbuf.resize((size_t)len);
+      if (!read_exact(0, cbuf.data(), (size_t)len)) break;
+      auto it = lanes.find((unsigned char)cbuf[0]);
+      if (it == lanes.end() || it->second.w < 0 || !write_all(it->second.w, cbuf.data() + 1, (size_t)len - 1)) {
+        std::fprintf(stderr, "devspace-helper: data for a lane that is not open\n");
+        std::_Exit(1);
+      }
+      continue;
+    }
+    if (op == 'U' && len == 1) {
+      unsigned char lane;
+      if (!read_exact(0, &lane, 1)) break;
+      open_lane(lanes, lane);
+      continue;
+    }
     if (op == 'U') {
       std::string r;
       {
@@ -445,7 +525,7 @@ int main(int argc, char** argv) {
           r = op_extract(cr.source());
           cr.drain();  // an early error still consumes the whole stream: framing stays in step
         } catch (const std::exception& ex) {
-          return 1;  // the stream itself is broken (sender gone): nothing left to reply to
+          std::_Exit(1);  // the stream itself is broken (sender gone): nothing left to reply to
         }
       }
       reply(r + "\n");
@@ -453,7 +533,7 @@ int main(int argc, char** argv) {
     }
     if (len > frame::kMaxListPayload) {
       std::fprintf(stderr, "devspace-helper: request payload of %llu bytes refused\n", (unsigned long long)len);
-      return 1;
+      std::_Exit(1);
     }
     std::string payload((size_t)len, '\0');
     if (len && !read_exact(0, &payload[0], (size_t)len)) break;
@@ -471,6 +551,19 @@ int main(int argc, char** argv) {
         reply("OK\n");
         break;
       }
+      case 'X': {  // tagged remove (lanes): payload = lane byte + rel list
+        if (payload.empty()) std::_Exit(1);
+        int lane = (unsigned char)payload[0];
+        {
+          OwnOp own;
+          try {
+            op_remove(payload.substr(1));
+          } catch (const std::exception&) {
+          }
+        }
+        reply(lane_tag(lane) + "OK\n");
+        break;
+      }
       case 'S': op_scan(); break;
       case 'H': reply(op_hash(payload)); break;
       case 'D': op_download(payload); break;
@@ -482,9 +575,10 @@ int main(int argc, char** argv) {
           std::thread(watch_loop).detach();
         }
         break;
-      case 'Q': return 0;
+      case 'Q':
+        std::_Exit(0);  // lane threads may still be parked on their pipes
       default: reply("ERR unknown op\n");
     }
   }
-  return 0;
+  std::_Exit(0);
 }

@@ -607,7 +607,11 @@ std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& c
     std::vector<std::string> addrs;
     for (auto& m : pf.get("portMappings").items()) {
       ports.emplace_back((int)m.get("localPort").as_int(), (int)m.get("remotePort").as_int());
-      addrs.push_back(m.get("bindAddress").as_string("localhost")  /* port_forwarding.go:64-67 */);
+      // Deliberate deviation (PARITY.md): the reference defaults to "127.0.0.1"
+      // (port_forwarding.go:64-67); an unset bindAddress here listens on localhost, i.e.
+      // 127.0.0.1 and ::1, as `kubectl port-forward` does, so http://localhost:<port> works on
+      // hosts that resolve localhost to ::1 first. An explicit bindAddress is used as given.
+      addrs.push_back(m.get("bindAddress").as_string("localhost"));
     }
     auto fwd = std::make_unique<PortForwarder>(k, pod, ports, addrs, ref.labels.to_query());
     fwd->start();

@@ -366,7 +366,14 @@ void Session::open_up_shell() {
     }
   }
   up_has_head_ = false;
+  if (up_helper_) {
+    // the change watch runs in the upstream helper: the echo of its own writes is filtered where
+    // they are recorded (src/helper/helper.cc is_own)
+    up_err_.reset(up_shell_->err());
+    write_all(up_shell_->in(), request('W', ""));
+  }
   set_nonblocking(up_shell_->in(), true);
+  if (up_helper_) start_up_reader();
   if (mode_ != Mode::Compat && !up_helper_) {
     // create the destination once instead of per upload, and check for `head` (the streamed
     // upload needs `head -c`; without it uploads use the reference's cat + stat protocol)
@@ -392,8 +399,8 @@ void Session::open_down_shell() {
       down_shell_ = transport_->open({"sh"});
       down_out_.reset(down_shell_->out());
       down_err_.reset(down_shell_->err());
-    } else {
-      // subscribe to container-side change events (pushed on stderr)
+    } else if (!up_helper_) {
+      // no upstream helper: container-side change events come from this one (no echo filter)
       write_all(down_shell_->in(), request('W', ""));
     }
   }
@@ -701,7 +708,10 @@ void Session::upstream_loop() {
     }
     if (changes.empty() || stopping_ || failed_) continue;
     try {
-      apply_upstream(changes, first_us);
+      if (up_helper_)
+        dispatch_upstream(changes, first_us);
+      else
+        apply_upstream(changes, first_us);
     } catch (const std::exception& e) {
       fail(e.what());
       return;
@@ -709,12 +719,185 @@ void Session::upstream_loop() {
   }
 }
 
-void Session::apply_upstream(std::vector<FileInfo>& changes, long first_event_us) {
-  trace::Span span("sync.upstream_batch", {{"changes", std::to_string(changes.size())}, {"dest", o_.dest_path}});
+// A file at least this big goes to the bulk lane; so does a whole batch whose small files
+// together pass kBulkBatchBytes (an edit-sized upload stays interactive).
+static const int64_t kBulkFileBytes = 4ll << 20;
+static const uint64_t kBulkBatchBytes = 32ull << 20;
+
+void Session::dispatch_upstream(std::vector<FileInfo>& changes, long first_event_us) {
+  std::vector<FileInfo> now, bulk;
+  std::vector<std::string> later;
+  uint64_t small_bytes = 0;
+  for (auto& c : changes) {
+    if (in_flight(c.name, true)) {  // the bulk upload carries this path: after it, re-evaluated
+      later.push_back(o_.watch_path + c.name);
+      continue;
+    }
+    if (c.mtime > 0 && !c.is_dir && c.size >= kBulkFileBytes) {
+      bulk.push_back(c);
+    } else {
+      if (c.mtime > 0 && !c.is_dir) small_bytes += (uint64_t)std::max<int64_t>(0, c.size);
+      now.push_back(c);
+    }
+  }
+  if (!bulk.empty() && small_bytes >= kBulkBatchBytes) {  // a big tree of small files: all bulk
+    std::vector<FileInfo> keep;
+    for (auto& c : now) (c.mtime > 0 ? bulk : keep).push_back(c);
+    now.swap(keep);
+  }
+  if (!later.empty()) {
+    std::lock_guard<std::mutex> g(q_mu_);
+    deferred_.insert(deferred_.end(), later.begin(), later.end());
+  }
+  if (!bulk.empty()) {
+    mark_inflight(bulk, true, true);
+    {
+      std::lock_guard<std::mutex> g(q_mu_);
+      bulk_q_.push_back(std::move(bulk));
+    }
+    q_cv_.notify_all();
+  }
+  if (!now.empty()) apply_upstream(now, first_event_us);
+}
+
+void Session::bulk_loop() {
+  while (!stopping_ && !failed_) {
+    std::vector<FileInfo> batch;
+    {
+      std::unique_lock<std::mutex> lk(q_mu_);
+      q_cv_.wait_for(lk, std::chrono::milliseconds(200), [this] { return !bulk_q_.empty() || stopping_ || failed_; });
+      if (bulk_q_.empty()) continue;
+      batch = std::move(bulk_q_.front());
+      bulk_q_.pop_front();
+      bulk_busy_ = true;
+    }
+    struct Done {  // on every way out: the paths are no longer in flight, deferred edits go again
+      Session* s;
+      const std::vector<FileInfo>& b;
+      ~Done() {
+        s->mark_inflight(b, true, false);
+        {
+          std::lock_guard<std::mutex> g(s->q_mu_);
+          s->bulk_busy_ = false;
+          for (auto& p : s->deferred_) {
+            UpEvent e;
+            e.abs_path = p;
+            e.settled = true;
+            e.t_us = mono_us();
+            s->queue_.push_back(std::move(e));
+          }
+          s->deferred_.clear();
+        }
+        s->q_cv_.notify_all();
+      }
+    } done{this, batch};
+    try {
+      apply_upstream(batch, 0, true);
+    } catch (const std::exception& e) {
+      fail(e.what());
+      return;
+    }
+  }
+}
+
+void Session::mark_inflight(const std::vector<FileInfo>& files, bool bulk, bool on) {
+  std::lock_guard<std::mutex> g(inflight_mu_);
+  auto& m = bulk ? inflight_bulk_ : inflight_;
+  for (auto& f : files) {
+    if (on) {
+      ++m[f.name];
+    } else {
+      auto it = m.find(f.name);
+      if (it != m.end() && --it->second <= 0) m.erase(it);
+    }
+  }
+}
+
+bool Session::in_flight(const std::string& rel, bool bulk_only) {
+  std::lock_guard<std::mutex> g(inflight_mu_);
+  if (inflight_bulk_.empty() && (bulk_only || inflight_.empty())) return false;
+  // the path itself or a directory above it (a directory upload carries its tree)
+  for (std::string q = rel; !q.empty() && q != "/"; q = fs::dirname(q)) {
+    if (inflight_bulk_.count(q) || (!bulk_only && inflight_.count(q))) return true;
+    if (q.find('/') == std::string::npos) break;
+  }
+  return false;
+}
+
+int Session::next_lane() { return 1 + (lane_seq_.fetch_add(1) % 250); }
+
+void Session::up_frame(const std::string& head, const char* d, size_t n) {
+  std::lock_guard<std::mutex> g(up_wmu_);
+  int fd = up_shell_->in();
+  send(fd, head.data(), head.size());
+  if (n) send(fd, d, n);
+}
+
+void Session::wait_no_priority() {
+  if (up_prio_.load() == 0) return;
+  std::unique_lock<std::mutex> lk(up_pmu_);
+  up_pcv_.wait_for(lk, std::chrono::milliseconds(o_.idle_timeout_ms),
+                   [this] { return up_prio_.load() == 0 || stopping_ || failed_; });
+}
+
+void Session::start_up_reader() {
+  {
+    std::lock_guard<std::mutex> g(up_rmu_);
+    up_replies_.clear();
+    up_reader_eof_ = false;
+  }
+  up_reader_ = std::thread([this] {
+    std::string line;
+    while (!stopping_) {
+      if (up_out_.read_line(&line, 200)) {
+        if (line.size() > 1 && line[0] == '@') {
+          size_t sp = line.find(' ');
+          int lane = std::atoi(line.substr(1, sp == std::string::npos ? std::string::npos : sp - 1).c_str());
+          {
+            std::lock_guard<std::mutex> g(up_rmu_);
+            up_replies_[lane] = sp == std::string::npos ? "" : line.substr(sp + 1);
+          }
+          up_rcv_.notify_all();
+        } else if (!line.empty()) {
+          logf("[Upstream] Helper: " + line);
+        }
+        continue;
+      }
+      if (up_out_.eof()) break;
+    }
+    {
+      std::lock_guard<std::mutex> g(up_rmu_);
+      up_reader_eof_ = true;
+    }
+    up_rcv_.notify_all();
+  });
+}
+
+std::string Session::up_wait(int lane, int idle_ms, const char* what) {
+  std::unique_lock<std::mutex> lk(up_rmu_);
+  long start = mono_us();
+  while (true) {
+    auto it = up_replies_.find(lane);
+    if (it != up_replies_.end()) {
+      std::string r = it->second;
+      up_replies_.erase(it);
+      return r;
+    }
+    if (up_reader_eof_) throw SyncError(std::string(what) + ": stream closed");
+    if (stopping_) throw SyncError("sync stopped");
+    if (mono_us() - start > (long)idle_ms * 1000)
+      throw SyncError(strfmt("%s: no reply for %d s", what, idle_ms / 1000));
+    up_rcv_.wait_for(lk, std::chrono::milliseconds(200));
+  }
+}
+
+void Session::apply_upstream(std::vector<FileInfo>& changes, long first_event_us, bool bulk) {
+  trace::Span span(bulk ? "sync.upstream_bulk" : "sync.upstream_batch",
+                   {{"changes", std::to_string(changes.size())}, {"dest", o_.dest_path}});
   std::vector<FileInfo> creates, removes;
   for (auto& c : changes) (c.mtime > 0 ? creates : removes).push_back(c);
   if (!removes.empty()) apply_removes(removes);
-  if (!creates.empty()) apply_creates(creates);
+  if (!creates.empty()) apply_creates(creates, bulk);
   logf(strfmt("[Upstream] Successfully processed %zu change(s)", changes.size()));
   std::lock_guard<std::mutex> g(stats_mu_);
   stats_.upstream_batches++;
@@ -795,29 +978,50 @@ void Session::warn_large(const std::string& rel, int64_t size) {
 }
 
 void Session::apply_removes(const std::vector<FileInfo>& files) {
-  std::lock_guard<std::mutex> ig(index_.mu);
   logf(strfmt("[Upstream] Handling %zu removes", files.size()));
-  std::lock_guard<std::mutex> sg(up_shell_mu_);
-  for (size_t i = 0; i < files.size(); i += 50) {
-    std::vector<std::string> args;
-    std::string helper_payload;
-    for (size_t j = 0; j < 50 && i + j < files.size(); ++j) {
-      const std::string& rel = files[i + j].name;
-      FileInfo* f = index_.find(rel);
-      if (!f) continue;
-      args.push_back(shell_quote(dest_ + rel));
-      helper_payload += rel + "\n";
-      if (f->is_dir)
-        index_.remove_dir(rel);
-      else
-        index_.files.erase(rel);
-      if (o_.verbose || files.size() <= 3) logf("[Upstream] Remove " + rel);
+  // the index entries go first (under the lock), the container's copies after (without it); the
+  // paths stay in flight meanwhile so a downstream scan does not fetch them back
+  std::vector<std::pair<std::vector<std::string>, std::string>> groups;  // (shell args, helper payload)
+  mark_inflight(files, false, true);  // before the index forgets them
+  struct Unmark {
+    Session* s;
+    const std::vector<FileInfo>& g;
+    ~Unmark() { s->mark_inflight(g, false, false); }
+  } unmark{this, files};
+  {
+    std::lock_guard<std::mutex> ig(index_.mu);
+    for (size_t i = 0; i < files.size(); i += 50) {
+      std::vector<std::string> args;
+      std::string helper_payload;
+      for (size_t j = 0; j < 50 && i + j < files.size(); ++j) {
+        const std::string& rel = files[i + j].name;
+        FileInfo* f = index_.find(rel);
+        if (!f) continue;
+        args.push_back(shell_quote(dest_ + rel));
+        helper_payload += rel + "\n";
+        if (f->is_dir)
+          index_.remove_dir(rel);
+        else
+          index_.files.erase(rel);
+        if (o_.verbose || files.size() <= 3) logf("[Upstream] Remove " + rel);
+      }
+      if (!args.empty()) groups.emplace_back(std::move(args), std::move(helper_payload));
     }
-    if (args.empty()) continue;
-    if (up_helper_) {
-      if (!write_all(up_shell_->in(), request('R', helper_payload))) throw SyncError("upstream: write failed");
-      wait_ack(up_out_, "OK", false);
-    } else if (mode_ == Mode::Compat) {
+  }
+  if (groups.empty()) return;
+  if (up_helper_) {
+    for (auto& grp : groups) {
+      int lane = next_lane();
+      up_frame(request('X', std::string(1, (char)lane) + grp.second), nullptr, 0);
+      std::string r = up_wait(lane, o_.idle_timeout_ms, "upstream: helper reply");
+      if (r != "OK") throw SyncError("upstream: helper error: " + r);
+    }
+    return;
+  }
+  std::lock_guard<std::mutex> sg(up_shell_mu_);
+  for (auto& grp : groups) {
+    const auto& args = grp.first;
+    if (mode_ == Mode::Compat) {
       std::string cmd = "rm -R " + join(args, " ") + "  >/dev/null 2>/dev/null && printf \"" + kDone +
                         "\" || printf \"" + kDone + "\"\n";
       if (!write_all(up_shell_->in(), cmd)) throw SyncError("upstream: write failed");
@@ -832,7 +1036,7 @@ void Session::apply_removes(const std::vector<FileInfo>& files) {
 
 void Session::recursive_tar(const std::string& rel, std::map<std::string, FileInfo>* written, TarWriter* tw,
                             int depth) {
-  // index lock held by the caller (stream_upload)
+  // the index lock is taken per lookup (the upload runs without it)
   if (depth > 64 || written->count(rel)) return;
   if (has_ignore_ && ignore_.matches(rel)) return;
   if (has_upload_ignore_ && upload_ignore_.matches(rel)) return;
@@ -851,15 +1055,18 @@ void Session::recursive_tar(const std::string& rel, std::map<std::string, FileIn
   if (mode_ != Mode::Compat) fi.local_mtime_ns = st.mtime_sec * 1000000000LL + st.mtime_nsec;
   uint32_t mode = st.mode & 07777;
   uint32_t uid = st.uid, gid = st.gid;
-  if (FileInfo* known = index_.find(rel)) {
-    fi.remote_mode = known->remote_mode;
-    fi.remote_uid = known->remote_uid;
-    fi.remote_gid = known->remote_gid;
-    fi.has_remote_attrs = known->has_remote_attrs;
-    if (known->has_remote_attrs) {
-      mode = (uint32_t)known->remote_mode;
-      uid = (uint32_t)known->remote_uid;
-      gid = (uint32_t)known->remote_gid;
+  {
+    std::lock_guard<std::mutex> ig(index_.mu);
+    if (FileInfo* known = index_.find(rel)) {
+      fi.remote_mode = known->remote_mode;
+      fi.remote_uid = known->remote_uid;
+      fi.remote_gid = known->remote_gid;
+      fi.has_remote_attrs = known->has_remote_attrs;
+      if (known->has_remote_attrs) {
+        mode = (uint32_t)known->remote_mode;
+        uid = (uint32_t)known->remote_uid;
+        gid = (uint32_t)known->remote_gid;
+      }
     }
   }
   std::string name = rel.empty() ? "" : rel.substr(1);
@@ -885,7 +1092,10 @@ void Session::recursive_tar(const std::string& rel, std::map<std::string, FileIn
   e.gid = gid;
   e.size = st.size;
   e.mtime = st.mtime_sec;
-  warn_large(rel, st.size);
+  {
+    std::lock_guard<std::mutex> ig(index_.mu);
+    warn_large(rel, st.size);
+  }
   if (!tw->add_file_from_path(e, abs)) {
     logf("[Upstream] Couldn't read file " + abs);
     return;
@@ -893,7 +1103,8 @@ void Session::recursive_tar(const std::string& rel, std::map<std::string, FileIn
   (*written)[rel] = fi;
 }
 
-uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std::string, FileInfo>* written) {
+uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std::string, FileInfo>* written,
+                                bool bulk) {
   int fd = up_shell_->in();
   RateLimiter rl(o_.upstream_limit);
   Progress prog(this, "[Upstream] Upload", 0);
@@ -909,14 +1120,42 @@ uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std
     return tw.finish();
   };
   if (up_helper_) {
-    // chunk-framed stream: tar -> (plain | adaptive gzip) -> chunks -> exec stdin, no length
-    // announced, nothing staged (the container extracts while we read the files)
-    if (!write_all(fd, frame::header('U', 0))) throw SyncError("upstream: write failed");
-    frame::ChunkWriter cw(to_shell, frame::kMaxChunk, 1);  // per-chunk deflate where it pays
+    // chunk-framed stream on a lane of its own: tar -> chunks (per-chunk deflate where it pays)
+    // -> 'C' frames, no length announced, nothing staged (the container extracts while we read
+    // the files). An interactive upload holds the priority while it sends: bulk frames wait.
+    int lane = next_lane();
+    struct Prio {
+      Session* s;
+      bool on;
+      ~Prio() {
+        if (on && s->up_prio_.fetch_sub(1) == 1) {
+          std::lock_guard<std::mutex> g(s->up_pmu_);
+          s->up_pcv_.notify_all();
+        }
+      }
+    } prio{this, !bulk};
+    if (!bulk) up_prio_.fetch_add(1);
+    const std::string lane_byte(1, (char)lane);
+    up_frame(request('U', lane_byte), nullptr, 0);
+    Sink to_lane = [&](const char* d, size_t n) {
+      if (o_.upstream_limit > 0) rl.take(n);
+      if (bulk) wait_no_priority();
+      prog.add(n);
+      up_frame(frame::header('C', n + 1) + lane_byte, d, n);
+      return true;
+    };
+    frame::ChunkWriter cw(to_lane, frame::kMaxChunk, 1);
     TarWriter tw(cw.sink());
     if (!tar_all(tw) || !cw.finish()) throw SyncError("upstream: write failed");
-    std::string line = read_line_idle(up_out_, o_.idle_timeout_ms, "upstream: helper reply");
-    if (line != "OK") throw SyncError("upstream: helper error: " + line);
+    if (prio.on) {  // sent: bulk frames may go while we wait for the reply
+      prio.on = false;
+      if (up_prio_.fetch_sub(1) == 1) {
+        std::lock_guard<std::mutex> g(up_pmu_);
+        up_pcv_.notify_all();
+      }
+    }
+    std::string r = up_wait(lane, o_.idle_timeout_ms, "upstream: helper reply");
+    if (r != "OK") throw SyncError("upstream: helper error: " + r);
     prog.finish();
     return prog.done;
   }
@@ -986,21 +1225,35 @@ uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std
   return spill.size();
 }
 
-void Session::apply_creates(const std::vector<FileInfo>& files) {
+void Session::apply_creates(const std::vector<FileInfo>& files, bool bulk) {
   std::map<std::string, FileInfo> written;
-  std::lock_guard<std::mutex> ig(index_.mu);
   uint64_t sent = 0;
+  // No index lock while the bytes travel (a multi-GB upload must not stall the upstream event
+  // batching or the downstream loop); the paths are in flight instead, which the downstream
+  // loop leaves alone until they are committed below.
+  mark_inflight(files, false, true);
+  struct Unmark {
+    Session* s;
+    const std::vector<FileInfo>& f;
+    ~Unmark() { s->mark_inflight(f, false, false); }
+  } unmark{this, files};
   try {
-    std::lock_guard<std::mutex> sg(up_shell_mu_);
-    sent = stream_upload(files, &written);
+    if (up_helper_) {
+      sent = stream_upload(files, &written, bulk);  // lanes: concurrent uploads share the helper
+    } else {
+      std::lock_guard<std::mutex> sg(up_shell_mu_);
+      sent = stream_upload(files, &written, bulk);
+    }
   } catch (...) {
     // whatever was in flight may sit half-written in the container with a fresh mtime; the
     // initial sync after the reconnect must send it again instead of trusting that mtime
+    std::lock_guard<std::mutex> ig(index_.mu);
     for (auto& kv : written) force_up_.insert(kv.first);
     for (auto& f : files) force_up_.insert(f.name);
     throw;
   }
   if (written.empty()) return;
+  std::lock_guard<std::mutex> ig(index_.mu);
   if (o_.verbose || written.size() <= 3) {
     for (auto& kv : written) logf((kv.second.is_dir ? "[Upstream] Create Folder " : "[Upstream] Create File ") + kv.first);
   }
@@ -1235,7 +1488,7 @@ void Session::drop_identical_copies(std::vector<FileInfo>& changes) {
 
 void Session::wait_upstream_idle() {
   std::unique_lock<std::mutex> lk(q_mu_);
-  while (!stopping_ && !failed_ && (up_busy_ || !queue_.empty()))
+  while (!stopping_ && !failed_ && (up_busy_ || !queue_.empty() || bulk_busy_ || !bulk_q_.empty()))
     q_cv_.wait_for(lk, std::chrono::milliseconds(50));
 }
 
@@ -1339,9 +1592,17 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
       known->has_remote_attrs = true;
     }
     if (fi->is_symlink) index_.files[fi->name] = *fi;
-    if (should_download(*fi)) creates.push_back(*fi);
+    if (should_download(*fi) && !in_flight(fi->name, false)) creates.push_back(*fi);
   }
   if (!dest_found) throw SyncError("DestPath not found, find command did not execute correctly");
+  if (removes) {  // an upload or remove in flight: the index is about to change, not the pod
+    for (auto it = removes->begin(); it != removes->end();) {
+      if (in_flight(it->first, false))
+        it = removes->erase(it);
+      else
+        ++it;
+    }
+  }
   return creates;
 }
 
@@ -1796,15 +2057,16 @@ void Session::downstream_loop() {
     long until = mono_us() + (long)wait_ms * 1000;
     while (!stopping_ && !failed_ && mono_us() < until) {
       if (down_helper_) {
+        LineReader& events = up_helper_ ? up_err_ : down_err_;
         std::string ev;
-        if (down_err_.read_line(&ev, 50)) {
+        if (events.read_line(&ev, 50)) {
           if (ev == "E") {
             // coalesce bursts of events
-            while (down_err_.read_line(&ev, 15)) {
+            while (events.read_line(&ev, 15)) {
             }
             break;
           }
-        } else if (down_err_.eof()) {
+        } else if (events.eof()) {
           fail("downstream: helper event stream closed");
           return;
         }
@@ -1819,6 +2081,7 @@ void Session::downstream_loop() {
 
 void Session::start_loops(bool upstream, bool downstream) {
   if (upstream) up_thread_ = std::thread([this] { upstream_loop(); });
+  if (upstream) bulk_thread_ = std::thread([this] { bulk_loop(); });
   if (downstream) down_thread_ = std::thread([this] { downstream_loop(); });
 }
 
@@ -1838,8 +2101,27 @@ void Session::stop_loops() {
   q_cv_.notify_all();
   if (up_shell_) up_shell_->terminate();
   if (down_shell_) down_shell_->terminate();
+  {
+    std::lock_guard<std::mutex> g(up_pmu_);
+    up_pcv_.notify_all();
+  }
+  up_rcv_.notify_all();
   if (up_thread_.joinable() && up_thread_.get_id() != std::this_thread::get_id()) up_thread_.join();
+  if (bulk_thread_.joinable() && bulk_thread_.get_id() != std::this_thread::get_id()) bulk_thread_.join();
   if (down_thread_.joinable() && down_thread_.get_id() != std::this_thread::get_id()) down_thread_.join();
+  if (up_reader_.joinable() && up_reader_.get_id() != std::this_thread::get_id()) up_reader_.join();
+  {
+    // a reconnect starts over from an initial sync: nothing is in flight or queued for the bulk lane
+    std::lock_guard<std::mutex> g(q_mu_);
+    bulk_q_.clear();
+    deferred_.clear();
+    bulk_busy_ = false;
+  }
+  {
+    std::lock_guard<std::mutex> g(inflight_mu_);
+    inflight_.clear();
+    inflight_bulk_.clear();
+  }
   if (up_shell_) up_shell_->close();
   if (down_shell_) down_shell_->close();
 }
@@ -1864,6 +2146,7 @@ void Session::supervise() {
   };
   logf("[Sync] Start syncing");
   up_thread_ = std::thread([this] { upstream_loop(); });
+  bulk_thread_ = std::thread([this] { bulk_loop(); });
   down_thread_ = std::thread([this, run_initial] {
     if (run_initial()) downstream_loop();
   });
@@ -1918,6 +2201,7 @@ void Session::supervise() {
       pending_failure_.clear();
     }
     up_thread_ = std::thread([this] { upstream_loop(); });
+    bulk_thread_ = std::thread([this] { bulk_loop(); });
     down_thread_ = std::thread([this, run_initial] {
       if (run_initial()) downstream_loop();
     });

@@ -182,12 +182,14 @@ class Session {
   void push_event(UpEvent e);
   void upstream_loop();
   std::optional<FileInfo> evaluate_change(const std::string& rel, const std::string& abs);
-  void apply_upstream(std::vector<FileInfo>& changes, long first_event_us);
+  void apply_upstream(std::vector<FileInfo>& changes, long first_event_us, bool bulk = false);
   void apply_removes(const std::vector<FileInfo>& removes);
-  void apply_creates(const std::vector<FileInfo>& creates);
-  // Streams a tar of `files` (recursively) to the container; index lock held by the caller.
-  // Returns the wire bytes sent; throws on a broken stream.
-  uint64_t stream_upload(const std::vector<FileInfo>& files, std::map<std::string, FileInfo>* written);
+  void apply_creates(const std::vector<FileInfo>& creates, bool bulk = false);
+  // Streams a tar of `files` (recursively) to the container. Runs without the index lock (it
+  // takes it per lookup): the downstream loop keeps working during a multi-GB upload, and skips
+  // the paths in flight. `bulk`: the helper's bulk lane (yields to interactive uploads frame by
+  // frame). Returns the wire bytes sent; throws on a broken stream.
+  uint64_t stream_upload(const std::vector<FileInfo>& files, std::map<std::string, FileInfo>* written, bool bulk);
   void recursive_tar(const std::string& rel, std::map<std::string, FileInfo>* written, TarWriter* tw, int depth);
   bool wait_ack(LineReader& r, const std::string& keyword, bool partial, std::string* before = nullptr,
                 int timeout_ms = 120000);
@@ -197,6 +199,38 @@ class Session {
   // Blocking reads with an idle timeout (no byte for idle_ms -> SyncError), honouring stop().
   std::string read_line_idle(LineReader& r, int idle_ms, const char* what);
   Source reader_source(LineReader& r, int idle_ms, const char* what);
+
+  // Helper-mode upstream lanes (src/helper/helper.cc): uploads run concurrently, interleaved frame
+  // by frame on the one upstream helper; replies "@lane ..." are read by up_reader_. A batch with
+  // large files goes to the bulk lane (bulk_thread_), so an edit made meanwhile is uploaded at
+  // once on its own lane instead of behind the archive; an edit of a path the bulk upload carries
+  // waits for it (deferred_) so the older bytes can never land last.
+  void dispatch_upstream(std::vector<FileInfo>& changes, long first_event_us);
+  void bulk_loop();
+  int next_lane();
+  // one frame (header + optional data) written atomically to the upstream helper's stdin
+  void up_frame(const std::string& head, const char* d, size_t n);
+  void wait_no_priority();  // bulk frames wait while an interactive upload is sending
+  std::string up_wait(int lane, int idle_ms, const char* what);
+  void start_up_reader();
+  std::mutex up_wmu_, up_pmu_;
+  std::condition_variable up_pcv_;
+  std::atomic<int> up_prio_{0};
+  std::mutex up_rmu_;
+  std::condition_variable up_rcv_;
+  std::map<int, std::string> up_replies_;  // up_rmu_
+  bool up_reader_eof_ = false;             // up_rmu_
+  std::thread up_reader_, bulk_thread_;
+  std::atomic<int> lane_seq_{0};
+  std::deque<std::vector<FileInfo>> bulk_q_;  // q_mu_
+  bool bulk_busy_ = false;                    // q_mu_
+  std::vector<std::string> deferred_;         // q_mu_: abs paths re-evaluated after the bulk upload
+  // Paths being uploaded or removed (downstream leaves them alone until the index has them).
+  std::mutex inflight_mu_;
+  std::map<std::string, int> inflight_;
+  std::map<std::string, int> inflight_bulk_;
+  void mark_inflight(const std::vector<FileInfo>& files, bool bulk, bool on);
+  bool in_flight(const std::string& rel, bool bulk_only);
   void warn_large(const std::string& rel, int64_t size);  // index lock held
   struct Progress;
   void send_changes_to_upstream(std::vector<FileInfo> changes);
@@ -246,6 +280,7 @@ class Session {
 
   std::unique_ptr<Shell> up_shell_, down_shell_;
   LineReader up_out_, down_out_, down_err_;
+  LineReader up_err_;  // change events of the upstream helper (it runs the watch: own-echo filter)
   bool up_helper_ = false, down_helper_ = false;
   std::mutex up_shell_mu_, down_shell_mu_;
 

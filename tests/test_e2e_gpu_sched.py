@@ -57,3 +57,46 @@ def test_interrupt_ends_one_shot_command(tmp_path):
         assert time.time() - t0 < 2, out
     finally:
         cluster.stop()
+
+
+def test_rocm_pytorch_example_runs_from_a_clean_clone(tmp_path):
+    """the example's workload kit (devspace_amd/) is written by the checkout's build
+    and git-ignored, so a clean clone has none. `devspace deploy` adds the kit it ships to the
+    build context (with a notice) and the pod starts the runner — built from `git ls-files` only."""
+    import os
+    import shutil
+
+    from conftest import ROOT
+    from devspace_amd.localkube import LocalCluster
+
+    files = subprocess.run(["git", "ls-files", "examples/rocm-pytorch"], cwd=ROOT, capture_output=True, text=True,
+                           check=True).stdout.split()
+    assert files and not [f for f in files if "/devspace_amd/" in f]
+    proj = tmp_path / "clone" / "rocm-pytorch"
+    for f in files:
+        dst = proj / os.path.relpath(f, "examples/rocm-pytorch")
+        dst.parent.mkdir(parents=True, exist_ok=True)
+        shutil.copy2(os.path.join(ROOT, f), dst)
+    cluster = LocalCluster(str(tmp_path / "state"), gpus=1).start()
+    try:
+        lk = DevspaceEnv(cluster, str(tmp_path))
+        r = lk.run(["deploy"], str(proj), timeout=300, check=False)
+        out = r.stdout + r.stderr
+        assert r.returncode == 0, out
+        assert "has no devspace_amd/" in out, out
+        assert not (proj / "devspace_amd").exists()  # the project tree is left alone
+        pods = cluster.wait_pods_running("rocm-pytorch", timeout=120)
+        import json
+
+        root = next(iter(json.loads(pods[0]["metadata"]["annotations"]["devspace.sh/local-roots"]).values()))
+        assert os.path.exists(os.path.join(root, "app", "devspace_amd", "runner.py"))
+        deadline = time.time() + 240
+        log = ""
+        while time.time() < deadline:
+            log = open(root + ".log").read() if os.path.exists(root + ".log") else ""
+            if "[devspace-runner] started gen=1" in log or "Traceback" in log:
+                break
+            time.sleep(0.5)
+        assert "[devspace-runner] started gen=1" in log, log[-3000:]
+    finally:
+        cluster.stop()

@@ -1,4 +1,5 @@
-"""RCCL (torch.distributed backend "nccl" on ROCm) as the rocm-pytorch pod uses it: a communicator
+"""Single-rank RCCL check (world_size=1: one GPU box, one rank): torch.distributed backend "nccl"
+(RCCL on ROCm) as the rocm-pytorch pod uses it: a communicator
 per process, collectives on HIP streams, and the example's DDP training step (32 MB gradient
 buckets all-reduced during backward). One GPU box -> one rank; the multi-rank path of the same
 code runs on CPU/gloo in test_runner.py and on 8 GPUs in the driver's scaling bench."""

@@ -1,0 +1,119 @@
+"""Helper-mode upstream lanes and the own-echo filter.
+
+* The in-pod helper filters the inotify echo of its own writes (src/helper/helper.cc is_own);
+  the session runs its change watch in the upstream helper, where those writes are recorded, so
+  an upload is not followed by a downstream event and a full remote scan.
+* Concurrent uploads: a large file travels on the bulk lane while an edit goes on its own lane,
+  interleaved frame by frame on the one helper; no index lock is held across the network, so the
+  downstream loop keeps applying pod-side changes meanwhile.
+
+The multi-GB version of the second test is in tests/test_sync_large.py
+(test_small_edit_overtakes_a_multi_gb_upload)."""
+
+import os
+import time
+
+import pytest
+
+from conftest import ROOT
+
+
+def _session(src, pod, tmp_path):
+    from devspace_amd import _native
+
+    s = _native.SyncSession(str(src), str(pod), mode="helper", exclude=[],
+                            helper_path=os.path.join(ROOT, "bin", "devspace-helper"),
+                            log_dir=str(tmp_path / "logs"), pod_name="lanes")
+    s.start()
+    assert s.wait_initial_sync(60000), s.error()
+    assert s.mode() == "helper"
+    return s
+
+
+def _wait(pred, timeout, what):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        v = pred()
+        if v:
+            return v
+        time.sleep(0.002)
+    raise AssertionError(f"timed out: {what}")
+
+
+def _read(p):
+    try:
+        with open(p, "rb") as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def test_upload_echo_triggers_no_downstream_scan(tmp_path):
+    src, pod = tmp_path / "src", tmp_path / "pod"
+    src.mkdir()
+    pod.mkdir()
+    (src / "a.py").write_text("x = 1\n")
+    s = _session(src, pod, tmp_path)
+    try:
+        _wait(lambda: _read(pod / "a.py") == b"x = 1\n", 10, "initial upload")
+        time.sleep(1.0)  # the initial sync's own echoes and scans settle
+        before = s.stats()["full_scans"]
+        for i in range(5):
+            (src / "a.py").write_text(f"x = {i + 2}\n")
+            _wait(lambda i=i: _read(pod / "a.py") == f"x = {i + 2}\n".encode(), 10, "edit upload")
+            (src / f"new{i}.py").write_text("y\n")
+            _wait(lambda i=i: _read(pod / f"new{i}.py") == b"y\n", 10, "new file upload")
+        time.sleep(1.0)
+        after = s.stats()["full_scans"]
+        assert after == before, (before, after)  # the echo of our own writes is not a pod change
+        # a real pod-side change still is one: one event, one scan, the file comes back
+        (pod / "from_pod.txt").write_text("pod\n")
+        _wait(lambda: _read(src / "from_pod.txt") == b"pod\n", 10, "downstream")
+        assert s.stats()["full_scans"] > after
+        # and a pod process rewriting a file it just received (a formatter) is reported too
+        (src / "fmt.py").write_text("a=1\n")
+        _wait(lambda: _read(pod / "fmt.py") == b"a=1\n", 10, "upload before rewrite")
+        # inside the helper's 2 s echo window, but a second later: the sync rules compare
+        # whole-second mtimes (the reference's roundMtime), a same-second rewrite looks older
+        time.sleep(1.2)
+        (pod / "fmt.py").write_text("a = 1  # formatted in the pod\n")
+        _wait(lambda: _read(src / "fmt.py") == b"a = 1  # formatted in the pod\n", 10, "rewrite comes back")
+    finally:
+        s.stop()
+
+
+@pytest.mark.parametrize("size_mb", [512])
+def test_edit_overtakes_a_bulk_upload_and_downstream_keeps_working(tmp_path, size_mb):
+    src, pod = tmp_path / "src", tmp_path / "pod"
+    src.mkdir()
+    pod.mkdir()
+    (src / "train.py").write_text("MARKER = 0\n")
+    big = tmp_path / "big.bin"
+    with open(big, "wb") as f:
+        for _ in range(size_mb // 16):
+            f.write(os.urandom(16 << 20))
+    s = _session(src, pod, tmp_path)
+    try:
+        os.link(big, src / "ckpt.bin")
+        tmp = pod / ("ckpt.bin" + ".devspace-tmp")
+        _wait(lambda: tmp.exists() and tmp.stat().st_size > (8 << 20), 30, "bulk upload under way")
+        t0 = time.perf_counter()
+        (src / "train.py").write_text("MARKER = 1\n" + "#" * 1024 + "\n")
+        _wait(lambda: (_read(pod / "train.py") or b"").startswith(b"MARKER = 1"), 10, "edit during the bulk upload")
+        edit_ms = (time.perf_counter() - t0) * 1000
+        bulk_left = tmp.exists() and not (pod / "ckpt.bin").exists()
+        # a pod-side change meanwhile comes back too (no index lock held by the upload)
+        (pod / "metrics.json").write_text('{"step": 1}\n')
+        _wait(lambda: _read(src / "metrics.json") == b'{"step": 1}\n', 10, "downstream during the bulk upload")
+        down_left = tmp.exists() and not (pod / "ckpt.bin").exists()
+        _wait(lambda: (pod / "ckpt.bin").exists(), 300, "bulk upload done")
+        assert (pod / "ckpt.bin").stat().st_size == big.stat().st_size
+        print(f"edit landed in {edit_ms:.1f} ms during a {size_mb} MiB upload")
+        assert bulk_left, "the bulk upload finished before the edit: nothing was measured"
+        assert edit_ms < 200, edit_ms
+        assert down_left, "the bulk upload finished before the pod-side change came back"
+        # the edit is not overwritten by anything older afterwards
+        time.sleep(0.3)
+        assert (_read(pod / "train.py") or b"").startswith(b"MARKER = 1")
+    finally:
+        s.stop()

@@ -300,3 +300,54 @@ def test_multi_gb_build_context_streams_to_the_daemon(payloads, tmp_path):
         assert peaks["devspace"] < RSS_CAP, peaks
     finally:
         cluster.stop()
+
+
+def test_small_edit_overtakes_a_multi_gb_upload(payloads, tmp_path):
+    """a 1 KiB edit made while a >= 2 GiB file is uploading lands in the pod within
+    200 ms (the helper's interactive lane, interleaved frame by frame with the bulk one), and a
+    pod-side change comes back meanwhile (no index lock across the upload) — through the real
+    `devspace sync` binary."""
+    src, pod = tmp_path / "src", tmp_path / "pod"
+    src.mkdir()
+    (pod / "app").mkdir(parents=True)
+    (src / "train.py").write_text("MARKER = 0\n")
+    up_path, up_sha = payloads["up"]
+    p, log = _start_sync(tmp_path, src, pod, "helper")
+    try:
+        deadline = time.monotonic() + 60
+        while not (pod / "app" / "train.py").exists():
+            assert time.monotonic() < deadline and p.poll() is None, "initial sync"
+            time.sleep(0.02)
+        os.link(up_path, str(src / "ckpt-up.bin"))
+        tmp = pod / "app" / "ckpt-up.bin.devspace-tmp"
+        deadline = time.monotonic() + 60
+        while not (tmp.exists() and tmp.stat().st_size > (16 << 20)):
+            assert time.monotonic() < deadline and p.poll() is None, "bulk upload never started"
+            time.sleep(0.005)
+        t0 = time.perf_counter()
+        (src / "train.py").write_text("MARKER = 1\n" + "#" * 1024 + "\n")
+        deadline = time.monotonic() + 10
+        while not (pod / "app" / "train.py").read_bytes().startswith(b"MARKER = 1"):
+            assert time.monotonic() < deadline, "edit never landed"
+            time.sleep(0.001)
+        edit_ms = (time.perf_counter() - t0) * 1000
+        bulk_in_flight = tmp.exists() and tmp.stat().st_size < SIZE
+        (pod / "app" / "metrics.json").write_text('{"step": 7}\n')
+        deadline = time.monotonic() + 20
+        while not ((src / "metrics.json").exists() and (src / "metrics.json").read_text() == '{"step": 7}\n'):
+            assert time.monotonic() < deadline, "pod-side change never came back"
+            time.sleep(0.005)
+        down_in_flight = tmp.exists()
+        _wait_file(str(pod / "app" / "ckpt-up.bin"), SIZE, 900, p, "the bulk upload")
+        assert _sha(str(pod / "app" / "ckpt-up.bin")) == up_sha
+        _record("helper_lanes", {"bytes": SIZE, "edit_during_upload_ms": round(edit_ms, 2),
+                                 "bulk_in_flight_at_edit": bulk_in_flight,
+                                 "bulk_in_flight_at_download": down_in_flight})
+        assert bulk_in_flight, "the upload finished before the edit landed: nothing was measured"
+        assert edit_ms < 200, edit_ms
+        assert down_in_flight, "the upload finished before the pod-side change came back"
+        assert (pod / "app" / "train.py").read_bytes().startswith(b"MARKER = 1")
+    finally:
+        _stop_sync(p, log)
+        shutil.rmtree(str(src), ignore_errors=True)
+        shutil.rmtree(str(pod), ignore_errors=True)
