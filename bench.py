@@ -234,7 +234,7 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         mode = os.environ.get("DEVSPACE_SYNC_MODE") or (
             "helper" if os.path.exists(os.path.join(ROOT, "bin", "devspace-helper")) else "fast")
         pod_file = os.path.join(root, "app", "train.py")
-        samples, sync_samples = [], []
+        samples, sync_samples, agreed = [], [], []
         parts = {"pickup_ms": [], "inflight_ms": [], "step_ms": [], "code_swap_ms": [], "log_delivery_ms": [],
              "train_period_ms": []}
         rng = random.Random(1234)
@@ -251,6 +251,10 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
             t_sync = _wait_file_contains(pod_file, f'MARKER = "{marker}"')
             pat = rf"\[devspace-runner\] (reloaded|started) gen=\d+ marker={re.escape(marker)} "
             t1, line, idx = tail.wait_for(pat, start_index=idx, timeout=_budget(600))
+            # the runner prints ranks=<world> once every rank confirmed one code digest
+            rm = re.search(r" ranks=(\d+) ", line)
+            if rm:
+                agreed.append(int(rm.group(1)))
             if i >= warmup:
                 samples.append((t1 - t0) * 1000.0)
                 sync_samples.append((t_sync - t0) * 1000.0)
@@ -268,7 +272,8 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         if timed_end:
             timed_end()
         return {"reload_ms": samples, "sync_ms": sync_samples, "mode": mode, "pod_deploy_s": deploy_s,
-                "parts": parts, "fused": fused}
+                "parts": parts, "fused": fused, "world": pod_world,
+                "ranks_agreed": bool(agreed) and all(a == pod_world for a in agreed)}
     finally:
         _killpg(dev)
         cluster.stop()
@@ -827,7 +832,8 @@ def report(args, nproc, tls, ms_total, qs, extras):
         g = {"config": f"examples/rocm-pytorch TinyLM (4x1024) training pod, amd.com/gpu: {nproc} (BASELINE "
                        f"configs[4] at {nproc} GPU(s); configs[4] itself at 8)" + (" [tiny]" if args.tiny else ""),
              "global_batch": 8 * nproc, "seq_len": 512, "parallelism": f"dp{nproc}", "dtype": "bf16",
-             "fused_ops": gp.get("fused"), "sync_mode": gp.get("mode"),
+             "fused_ops": gp.get("fused"), "sync_mode": gp.get("mode"), "ranks": gp.get("world"),
+             "ranks_agreed_on_code": gp.get("ranks_agreed"),
              "reload_p50_ms": round(gp50, 2), "reload_p90_ms": round(_pct(gp["reload_ms"], 0.9), 2),
              "sync_p50_ms": round(_pct(gp["sync_ms"], 0.5), 2), "n": len(gp["reload_ms"]),
              "pod_deploy_s": round(gp["pod_deploy_s"], 3)}

@@ -6,8 +6,9 @@
 //
 //   request := op:u8 len:u64be payload[len]
 //   'U' (len 0) + chunk stream of a tar (or tar.gz) -> extract under <dest>   reply "OK\n" | "ERR msg\n"
-//   'U' payload=lane:u8         -> open upload lane `lane`: its chunk stream arrives in 'C' frames
-//                                  and is extracted on a thread of its own  reply "@lane OK\n" | "@lane ERR msg\n"
+//   'U' payload=lane:u8         -> an upload on lane `lane` (the lane is created on first use): its
+//                                  chunk stream arrives in 'C' frames and is extracted on the lane's
+//                                  thread                                  reply "@lane OK\n" | "@lane ERR msg\n"
 //   'C' payload=lane:u8 bytes   -> the next bytes of lane `lane`'s chunk stream (no reply)
 //   'X' payload=lane:u8 rel\n.. -> rm -rf <dest><rel>                          reply "@lane OK\n"
 //   'R' payload=rel\n...        -> rm -rf <dest><rel>                          reply "OK\n"
@@ -438,7 +439,9 @@ static void watch_loop() {
 }
 
 // An upload lane: the frame reader writes the lane's chunk-stream bytes into `w`; the lane's
-// thread extracts from the other end and replies "@lane OK|ERR ...".
+// thread extracts one chunk stream after the other from the other end and replies
+// "@lane OK|ERR ..." after each. Lanes persist: an upload on a lane that exists costs no thread
+// or pipe set-up (the session keeps one lane for edits and one for bulk transfers).
 struct Lane {
   int w = -1;
   std::thread t;
@@ -446,10 +449,31 @@ struct Lane {
 
 static std::string lane_tag(int lane) { return "@" + std::to_string(lane) + " "; }
 
+static void lane_loop(int r, int lane) {
+  while (true) {
+    struct pollfd pf{r, POLLIN, 0};
+    if (::poll(&pf, 1, -1) < 0) {
+      if (errno == EINTR) continue;
+      break;
+    }
+    std::string res;
+    {
+      OwnOp own;  // from the first byte of a stream: its echo is ours while it runs and shortly after
+      frame::ChunkReader cr(fd_source(r));
+      try {
+        res = op_extract(cr.source());
+        cr.drain();  // an early error still consumes the whole stream: the lane stays in step
+      } catch (const std::exception&) {
+        std::_Exit(1);  // the stream itself is broken (sender gone): the session reconnects
+      }
+    }
+    reply(lane_tag(lane) + res + "\n");
+  }
+}
+
 static void open_lane(std::map<int, Lane>& lanes, int lane) {
   Lane& l = lanes[lane];
-  if (l.t.joinable()) l.t.join();  // the previous upload of this lane replied already
-  if (l.w >= 0) ::close(l.w);
+  if (l.w >= 0) return;  // persistent: the next stream follows the previous one in its pipe
   int fds[2];
   if (::pipe2(fds, O_CLOEXEC) != 0) {
     reply(lane_tag(lane) + "ERR pipe: " + std::strerror(errno) + "\n");
@@ -459,22 +483,8 @@ static void open_lane(std::map<int, Lane>& lanes, int lane) {
   ::fcntl(fds[1], F_SETPIPE_SZ, 1 << 20);  // one frame in flight per lane without blocking the reader
 #endif
   l.w = fds[1];
-  int r = fds[0];
-  l.t = std::thread([r, lane] {
-    std::string res;
-    {
-      OwnOp own;
-      frame::ChunkReader cr(fd_source(r));
-      try {
-        res = op_extract(cr.source());
-        cr.drain();  // an early error still consumes the lane's whole stream
-      } catch (const std::exception&) {
-        std::_Exit(1);  // the stream itself is broken: the session reconnects
-      }
-    }
-    ::close(r);
-    reply(lane_tag(lane) + res + "\n");
-  });
+  l.t = std::thread(lane_loop, fds[0], lane);
+  l.t.detach();  // ends with the process (std::_Exit)
 }
 
 int main(int argc, char** argv) {

@@ -824,7 +824,9 @@ bool Session::in_flight(const std::string& rel, bool bulk_only) {
   return false;
 }
 
-int Session::next_lane() { return 1 + (lane_seq_.fetch_add(1) % 250); }
+// Lane ids of the upstream helper: one upload at a time per lane (edits come from the upstream
+// loop, bulk transfers from the bulk loop), removes only tag their reply.
+static const int kEditLane = 1, kBulkLane = 2, kRemoveTag = 3;
 
 void Session::up_frame(const std::string& head, const char* d, size_t n) {
   std::lock_guard<std::mutex> g(up_wmu_);
@@ -1011,7 +1013,7 @@ void Session::apply_removes(const std::vector<FileInfo>& files) {
   if (groups.empty()) return;
   if (up_helper_) {
     for (auto& grp : groups) {
-      int lane = next_lane();
+      int lane = kRemoveTag;
       up_frame(request('X', std::string(1, (char)lane) + grp.second), nullptr, 0);
       std::string r = up_wait(lane, o_.idle_timeout_ms, "upstream: helper reply");
       if (r != "OK") throw SyncError("upstream: helper error: " + r);
@@ -1123,7 +1125,7 @@ uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std
     // chunk-framed stream on a lane of its own: tar -> chunks (per-chunk deflate where it pays)
     // -> 'C' frames, no length announced, nothing staged (the container extracts while we read
     // the files). An interactive upload holds the priority while it sends: bulk frames wait.
-    int lane = next_lane();
+    int lane = bulk ? kBulkLane : kEditLane;
     struct Prio {
       Session* s;
       bool on;
@@ -1136,17 +1138,34 @@ uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std
     } prio{this, !bulk};
     if (!bulk) up_prio_.fetch_add(1);
     const std::string lane_byte(1, (char)lane);
-    up_frame(request('U', lane_byte), nullptr, 0);
+    // lane bytes are coalesced into frames of up to kMaxChunk: an edit travels as one write
+    // (lane open + its whole chunk stream), a bulk stream as one frame per chunk
+    std::string pend;
+    bool opened = false;
+    auto flush = [&] {
+      std::string head;
+      if (!opened) {
+        head = request('U', lane_byte);
+        opened = true;
+      }
+      if (!pend.empty()) head += frame::header('C', pend.size() + 1) + lane_byte;
+      if (head.empty()) return;
+      if (bulk) wait_no_priority();
+      up_frame(head, pend.data(), pend.size());
+      pend.clear();
+    };
     Sink to_lane = [&](const char* d, size_t n) {
       if (o_.upstream_limit > 0) rl.take(n);
-      if (bulk) wait_no_priority();
       prog.add(n);
-      up_frame(frame::header('C', n + 1) + lane_byte, d, n);
+      if (!pend.empty() && pend.size() + n > frame::kMaxChunk) flush();
+      pend.append(d, n);
+      if (pend.size() >= frame::kMaxChunk) flush();
       return true;
     };
     frame::ChunkWriter cw(to_lane, frame::kMaxChunk, 1);
     TarWriter tw(cw.sink());
     if (!tar_all(tw) || !cw.finish()) throw SyncError("upstream: write failed");
+    flush();
     if (prio.on) {  // sent: bulk frames may go while we wait for the reply
       prio.on = false;
       if (up_prio_.fetch_sub(1) == 1) {

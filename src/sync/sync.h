@@ -207,7 +207,6 @@ class Session {
   // waits for it (deferred_) so the older bytes can never land last.
   void dispatch_upstream(std::vector<FileInfo>& changes, long first_event_us);
   void bulk_loop();
-  int next_lane();
   // one frame (header + optional data) written atomically to the upstream helper's stdin
   void up_frame(const std::string& head, const char* d, size_t n);
   void wait_no_priority();  // bulk frames wait while an interactive upload is sending
@@ -221,7 +220,6 @@ class Session {
   std::map<int, std::string> up_replies_;  // up_rmu_
   bool up_reader_eof_ = false;             // up_rmu_
   std::thread up_reader_, bulk_thread_;
-  std::atomic<int> lane_seq_{0};
   std::deque<std::vector<FileInfo>> bulk_q_;  // q_mu_
   bool bulk_busy_ = false;                    // q_mu_
   std::vector<std::string> deferred_;         // q_mu_: abs paths re-evaluated after the bulk upload
