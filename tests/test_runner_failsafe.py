@@ -51,8 +51,8 @@ def step(ctx, state):
 class Runner:
     """The runner supervisor as a child process, its output lines in a queue."""
 
-    def __init__(self, tmp_path, entry, nproc, extra_args=(), extra_env=None):
-        env = dict(os.environ, PYTHONPATH=ROOT, **CPU_ENV, **(extra_env or {}))
+    def __init__(self, tmp_path, entry, nproc, extra_args=(), extra_env=None, gpu=False):
+        env = dict(os.environ, PYTHONPATH=ROOT, **({} if gpu else CPU_ENV), **(extra_env or {}))
         self.proc = subprocess.Popen([sys.executable, "-u", "-m", "devspace_amd.runner", "--nproc", str(nproc),
                                       "--watch", str(tmp_path), *extra_args, str(entry)],
                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, text=True,
@@ -330,3 +330,32 @@ def test_eight_rank_reload_preempt_and_stop(tmp_path):
     finally:
         if r.proc.poll() is None:
             r.stop()
+
+
+RANK_LOCAL_STEP_GPU = RANK_LOCAL_STEP.replace("t = torch.ones(1)", "t = torch.ones(1, device=ctx.device)")
+
+
+@pytest.mark.gpu
+def test_rank_local_step_failure_restarts_the_group_on_the_gpu(tmp_path):
+    """The same containment with the ranks' step tensors on the MI355X (two ranks on the box's one
+    GPU, joined over gloo: RCCL refuses two ranks on one device): the peer blocked in the
+    collective is stopped, the group restarts and trains after the fix."""
+    entry = tmp_path / "train.py"
+    entry.write_text(RANK_LOCAL_STEP_GPU)
+    r = Runner(tmp_path, entry, 2, extra_args=("--log-every", "20"), extra_env={"DEVSPACE_DIST_BACKEND": "gloo"},
+               gpu=True)
+    try:
+        r.until(r"started gen=1 marker=v0 .*world=2 device=cuda", timeout=240)
+        r.until(r"step=\d+ gen=1 ")
+        _set_marker(entry, "bad")
+        r.seen(r"rank=1 step failed gen=2 marker=bad", timeout=60)
+        r.seen(r"rank=1 exited with code 3: restarting the group", timeout=60)
+        r.until(r"waiting for a file change before starting the group again", timeout=180)
+        t_fix = time.monotonic()
+        _set_marker(entry, "fixed")
+        t_up, _ = r.until(r"started gen=1 marker=fixed .*device=cuda", timeout=120)
+        r.until(r"step=\d+ gen=1 ", timeout=60)
+        print(f"restart-on-fix on the GPU: {t_up - t_fix:.2f}s")
+        assert t_up - t_fix < 30.0, t_up - t_fix
+    finally:
+        r.stop()
