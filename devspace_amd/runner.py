@@ -251,11 +251,15 @@ class Agreement:
     tensor (no `.item()` / `.tolist()` on the device: those would stall the host on every
     step). Every rank must make the same sequence of calls."""
 
-    def __init__(self, dist, group=None):
+    def __init__(self, dist, group=None, timeout=None):
         import torch
 
         self.dist = dist
-        self.group = group if group is not None else dist.new_group(backend="gloo")
+        if group is None:
+            # a collective waiting longer than `timeout` raises: a rank stuck in a step (or gone
+            # without a trace) ends the group instead of hanging it (the supervisor restarts it)
+            group = dist.new_group(backend="gloo", **({"timeout": timeout} if timeout is not None else {}))
+        self.group = group
         # [newest generation, helper modules changed, a rank was told to stop (SIGTERM)]
         self.ctl = torch.zeros(3, dtype=torch.int64)
         self.flag = torch.zeros(1, dtype=torch.int64)
@@ -666,6 +670,11 @@ def worker_main(args) -> int:
 
     device = None
     dist = None
+    group_timeout = None
+    if args.group_timeout > 0:
+        import datetime
+
+        group_timeout = datetime.timedelta(seconds=args.group_timeout)
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
         device = torch.device("cuda", torch.cuda.current_device())
@@ -677,7 +686,8 @@ def worker_main(args) -> int:
         # nccl == RCCL on ROCm; DEVSPACE_DIST_BACKEND=gloo runs several ranks on one GPU (RCCL
         # refuses two ranks on a device): a 1-GPU rehearsal of the multi-rank pod
         backend = os.environ.get("DEVSPACE_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
-        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                **({"timeout": group_timeout} if group_timeout is not None else {}))
     if device.type == "cuda" and args.gemm_tuning != "off":
         try:
             from devspace_amd.ops import gemm_tuning  # noqa: WPS433
@@ -697,7 +707,7 @@ def worker_main(args) -> int:
     overlay = SourceOverlay(watch_dir).install()
     fault = overlay.fault = _FaultHooks(os.environ.get("DEVSPACE_RUNNER_FAULT"), rank)
     # control plane of the group (gloo, CPU tensors): generation, preemption, code agreement
-    agree = Agreement(dist) if world > 1 else None
+    agree = Agreement(dist, timeout=group_timeout) if world > 1 else None
     stop = False
 
     def _term(*_):
@@ -882,7 +892,11 @@ def worker_main(args) -> int:
     except Exception as e:  # world > 1: a collective of the control plane failed (a peer is gone)
         if agree is None:
             raise
-        leave(EXIT_GROUP_LOST, f"group failure gen={ctx.generation}: {type(e).__name__}: {e}")
+        why = f"{type(e).__name__}: {e}"
+        if "timed out" in why.lower() or "timeout" in why.lower():
+            why = (f"no answer from every rank within {args.group_timeout:g} s (a rank stuck in a step? "
+                   f"--group-timeout): {why}")
+        leave(EXIT_GROUP_LOST, f"group failure gen={ctx.generation}: {why}")
     feed.close()
     watcher.close()
     overlay.uninstall()
@@ -1110,7 +1124,7 @@ def _forward(args):
         out.append("--no-train")
     if not args.preempt:
         out.append("--no-preempt")
-    out += ["--preempt-drain-ms", str(args.preempt_drain_ms)]
+    out += ["--preempt-drain-ms", str(args.preempt_drain_ms), "--group-timeout", str(args.group_timeout)]
     return out + [args.entry]
 
 
@@ -1132,6 +1146,9 @@ def parse_args(argv=None):
     p.add_argument("--preempt-drain-ms", type=float,
                    default=float(os.environ.get("DEVSPACE_PREEMPT_DRAIN_MS", "20")),
                    help="drain queued GPU work at preemption points when the step period is at least this")
+    p.add_argument("--group-timeout", type=float, default=float(os.environ.get("DEVSPACE_GROUP_TIMEOUT_S", "600")),
+                   help="seconds a collective may wait for every rank (control plane and the training "
+                        "group); past it the group fails and is restarted (0: torch's defaults)")
     p.add_argument("--gemm-tuning", default=os.environ.get("DEVSPACE_GEMM_TUNING", "off"),
                    choices=("off", "shipped", "online"),
                    help="TunableOp GEMM selection (devspace_amd/ops/gemm_tuning.py)")

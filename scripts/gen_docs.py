@@ -180,6 +180,8 @@ ENV = {
                             "gfx950 table) or `online` (tune unseen shapes, persist them).",
     "DEVSPACE_GEMM_TUNING_FILE": "Where `online` GEMM tuning persists its table.",
     "DEVSPACE_GEMM_TUNING_MS": "Time budget per shape of `online` GEMM tuning (default 30).",
+    "DEVSPACE_GROUP_TIMEOUT_S": "Seconds a collective of the runner's ranks may wait for every rank (default 600): a "
+                                "rank stuck in a step ends the group, which is restarted (`--group-timeout`).",
     "DEVSPACE_RUNNER_DEBUG": "`1`: every runner rank logs the code digest it loaded for each generation.",
     "DEVSPACE_RUNNER_FAULT": "Test-only fault injection of the runner (`mutate-entry-after-read`, `skew-helper`): "
                              "edits racing the ranks' reads, to exercise the code agreement.",

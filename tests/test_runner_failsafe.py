@@ -359,3 +359,33 @@ def test_rank_local_step_failure_restarts_the_group_on_the_gpu(tmp_path):
         assert t_up - t_fix < 30.0, t_up - t_fix
     finally:
         r.stop()
+
+
+RANK_LOCAL_HANG = RANK_LOCAL_STEP.replace(
+    'raise RuntimeError("rank-local failure on rank 1")',
+    'time.sleep(3600)  # stuck instead of failing').replace('MARKER == "bad"', 'MARKER == "hang"')
+
+
+def test_rank_stuck_in_a_step_ends_the_group_after_the_group_timeout(tmp_path):
+    """A rank that hangs instead of raising (a deadlocked data loader, an infinite loop) would
+    leave its peers in the collective for good: past --group-timeout the collective raises on
+    the waiting ranks, the group is stopped (the stuck rank with it) and restarted; the restarted
+    group hangs at its first step, fails before it comes up and waits for the fix."""
+    entry = tmp_path / "train.py"
+    entry.write_text(RANK_LOCAL_HANG)
+    r = Runner(tmp_path, entry, 2, extra_args=("--log-every", "20", "--group-timeout", "3"))
+    try:
+        r.until(r"started gen=1 marker=v0 .*world=2", timeout=180)
+        r.until(r"step=\d+ gen=1 ")
+        t0 = time.monotonic()
+        _set_marker(entry, "hang")
+        r.until(r"waiting for a file change before starting the group again", timeout=90)
+        assert time.monotonic() - t0 < 60
+        # the waiting rank's collective timed out: it says so (its traceback) and left the group
+        assert re.search(r"rank=0 (step|startup) failed", r.text()) and "timed out" in r.text().lower(), \
+            r.text()[-3000:]
+        _set_marker(entry, "fixed")
+        r.until(r"started gen=1 marker=fixed .*world=2", timeout=60)
+        r.until(r"step=\d+ gen=1 ", timeout=30)
+    finally:
+        r.stop()
