@@ -531,11 +531,16 @@ def _load_generation(entry, gen, feed, overlay, agree, purge, watch_dir, ctx, fa
     ranks re-import from them, and the digests are compared again."""
     src = None
     if agree is None or ctx.rank == 0:
-        with open(entry, "rb") as f:
-            src = f.read()
-        fault.after_entry_read(entry)
+        try:
+            with open(entry, "rb") as f:
+                src = f.read()
+            fault.after_entry_read(entry)
+        except OSError as e:  # mid-rename, deleted: nothing to load (the ranks still agree on that)
+            ctx.error(f"cannot read {entry}: {e}")
     if agree is not None:
         src, purge = agree.share((src, purge))
+    if src is None:
+        raise LoadFailed(f"{entry} could not be read")
     if purge:
         purge_user_modules(watch_dir)
     overlay.snap, overlay.reads = {}, {}
@@ -576,7 +581,7 @@ def _load_generation(entry, gen, feed, overlay, agree, purge, watch_dir, ctx, fa
 def _try_load(entry, gen, feed, src):
     try:
         return load_module(entry, gen, feed, src=src), None
-    except Exception:  # a syntax error, a failing import: reported, the group keeps its code
+    except (Exception, SystemExit):  # a syntax error, a failing import: reported, the group keeps its code
         return None, traceback.format_exc()
 
 

@@ -389,3 +389,20 @@ def test_rank_stuck_in_a_step_ends_the_group_after_the_group_timeout(tmp_path):
         r.until(r"step=\d+ gen=1 ", timeout=30)
     finally:
         r.stop()
+
+
+def test_entry_file_gone_is_a_failed_reload_not_a_crash(tmp_path):
+    """The entry file vanishes (a branch switch, a delete-then-write save): the reload fails on
+    every rank alike and the group keeps training; the file coming back reloads it."""
+    entry = tmp_path / "train.py"
+    entry.write_text(STEADY)
+    r = Runner(tmp_path, entry, 2)
+    try:
+        r.until(r"started gen=1 marker=v0 .*world=2", timeout=180)
+        entry.unlink()
+        r.seen(r"reload failed gen=2 .*keeping gen=1 on every rank", timeout=60)
+        entry.write_text(STEADY.replace('MARKER = "v0"', 'MARKER = "back"'))
+        r.until(r"reloaded gen=\d+ marker=back .*ranks=2", timeout=60)
+        assert "exited with code" not in r.text(), r.text()
+    finally:
+        r.stop()
