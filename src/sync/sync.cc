@@ -843,38 +843,15 @@ void Session::wait_no_priority() {
 }
 
 void Session::start_up_reader() {
-  {
-    std::lock_guard<std::mutex> g(up_rmu_);
-    up_replies_.clear();
-    up_reader_eof_ = false;
-  }
-  up_reader_ = std::thread([this] {
-    std::string line;
-    while (!stopping_) {
-      if (up_out_.read_line(&line, 200)) {
-        if (line.size() > 1 && line[0] == '@') {
-          size_t sp = line.find(' ');
-          int lane = std::atoi(line.substr(1, sp == std::string::npos ? std::string::npos : sp - 1).c_str());
-          {
-            std::lock_guard<std::mutex> g(up_rmu_);
-            up_replies_[lane] = sp == std::string::npos ? "" : line.substr(sp + 1);
-          }
-          up_rcv_.notify_all();
-        } else if (!line.empty()) {
-          logf("[Upstream] Helper: " + line);
-        }
-        continue;
-      }
-      if (up_out_.eof()) break;
-    }
-    {
-      std::lock_guard<std::mutex> g(up_rmu_);
-      up_reader_eof_ = true;
-    }
-    up_rcv_.notify_all();
-  });
+  std::lock_guard<std::mutex> g(up_rmu_);
+  up_replies_.clear();
+  up_reader_eof_ = false;
+  up_reading_ = false;
 }
 
+// Replies of the upstream helper, read by whichever waiter gets there first (leader/follower):
+// with one upload in flight — an edit — its own thread reads its reply, no hand-off; a reply for
+// another lane is parked in up_replies_ for its waiter.
 std::string Session::up_wait(int lane, int idle_ms, const char* what) {
   std::unique_lock<std::mutex> lk(up_rmu_);
   long start = mono_us();
@@ -889,7 +866,28 @@ std::string Session::up_wait(int lane, int idle_ms, const char* what) {
     if (stopping_) throw SyncError("sync stopped");
     if (mono_us() - start > (long)idle_ms * 1000)
       throw SyncError(strfmt("%s: no reply for %d s", what, idle_ms / 1000));
-    up_rcv_.wait_for(lk, std::chrono::milliseconds(200));
+    if (up_reading_) {
+      up_rcv_.wait_for(lk, std::chrono::milliseconds(50));
+      continue;
+    }
+    up_reading_ = true;
+    lk.unlock();
+    std::string line;
+    bool got = up_out_.read_line(&line, 50);
+    bool eof = !got && up_out_.eof();
+    lk.lock();
+    up_reading_ = false;
+    if (got) {
+      if (line.size() > 1 && line[0] == '@') {
+        size_t sp = line.find(' ');
+        int l = std::atoi(line.substr(1, sp == std::string::npos ? std::string::npos : sp - 1).c_str());
+        up_replies_[l] = sp == std::string::npos ? "" : line.substr(sp + 1);
+      } else if (!line.empty()) {
+        logf("[Upstream] Helper: " + line);
+      }
+    }
+    if (eof) up_reader_eof_ = true;
+    up_rcv_.notify_all();
   }
 }
 
@@ -2128,7 +2126,6 @@ void Session::stop_loops() {
   if (up_thread_.joinable() && up_thread_.get_id() != std::this_thread::get_id()) up_thread_.join();
   if (bulk_thread_.joinable() && bulk_thread_.get_id() != std::this_thread::get_id()) bulk_thread_.join();
   if (down_thread_.joinable() && down_thread_.get_id() != std::this_thread::get_id()) down_thread_.join();
-  if (up_reader_.joinable() && up_reader_.get_id() != std::this_thread::get_id()) up_reader_.join();
   {
     // a reconnect starts over from an initial sync: nothing is in flight or queued for the bulk lane
     std::lock_guard<std::mutex> g(q_mu_);

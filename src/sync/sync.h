@@ -201,7 +201,7 @@ class Session {
   Source reader_source(LineReader& r, int idle_ms, const char* what);
 
   // Helper-mode upstream lanes (src/helper/helper.cc): uploads run concurrently, interleaved frame
-  // by frame on the one upstream helper; replies "@lane ..." are read by up_reader_. A batch with
+  // by frame on the one upstream helper; replies "@lane ..." are read by the waiters (up_wait). A batch with
   // large files goes to the bulk lane (bulk_thread_), so an edit made meanwhile is uploaded at
   // once on its own lane instead of behind the archive; an edit of a path the bulk upload carries
   // waits for it (deferred_) so the older bytes can never land last.
@@ -219,7 +219,8 @@ class Session {
   std::condition_variable up_rcv_;
   std::map<int, std::string> up_replies_;  // up_rmu_
   bool up_reader_eof_ = false;             // up_rmu_
-  std::thread up_reader_, bulk_thread_;
+  bool up_reading_ = false;                // up_rmu_: a waiter is reading up_out_
+  std::thread bulk_thread_;
   std::deque<std::vector<FileInfo>> bulk_q_;  // q_mu_
   bool bulk_busy_ = false;                    // q_mu_
   std::vector<std::string> deferred_;         // q_mu_: abs paths re-evaluated after the bulk upload
