@@ -650,3 +650,47 @@ TEST(sync_helper_probe_picks_a_usable_directory) {
   EXPECT_EQ(out, "NOHELPER");
   fs::remove_all(base);
 }
+
+// Helper-mode upload lanes under concurrency (TSan covers this in scripts/sanitize.sh): a bulk
+// file on its lane, edits on theirs while it travels, a pod-side write coming back meanwhile;
+// everything lands with the right bytes and the edits are not overwritten by older ones.
+TEST(sync_helper_lanes_concurrent_uploads) {
+  log::logdir() = fs::make_temp_dir("synclogs-");
+  Dirs d;
+  if (d.dest != d.remote) return;  // local-shell transport only (no kube target needed)
+  Options o = base_options(d, Mode::Helper);
+  Session s(o, std::make_shared<LocalShellTransport>());
+  s.start();
+  EXPECT_TRUE(s.wait_initial_sync(15000));
+  EXPECT_TRUE(s.effective_mode() == Mode::Helper);
+  std::string big(48u << 20, '\0');
+  uint64_t x = 0x9e3779b97f4a7c15ull;
+  for (size_t i = 0; i < big.size(); i += 8) {  // incompressible: chunks go out stored
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    std::memcpy(&big[i], &x, 8);
+  }
+  fs::write_file(fs::join(d.local, "ckpt.bin"), big);
+  for (int i = 0; i < 20; ++i) {
+    fs::write_file(fs::join(d.local, "edit.py"), "v = " + std::to_string(i) + "\n");
+    if (i == 5) fs::write_file(fs::join(d.remote, "from_pod.txt"), "pod\n");
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  auto waited = [&] { return std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60); };
+  std::string got;
+  while (waited() && !(fs::read_file(fs::join(d.remote, "ckpt.bin"), &got) && got.size() == big.size()))
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  EXPECT_TRUE(got == big);
+  while (waited() && !(fs::read_file(fs::join(d.remote, "edit.py"), &got) && got == "v = 19\n"))
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  EXPECT_EQ(got, std::string("v = 19\n"));
+  while (waited() && !(fs::read_file(fs::join(d.local, "from_pod.txt"), &got) && got == "pod\n"))
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  EXPECT_EQ(got, std::string("pod\n"));
+  std::this_thread::sleep_for(std::chrono::milliseconds(300));
+  EXPECT_TRUE(fs::read_file(fs::join(d.remote, "edit.py"), &got) && got == "v = 19\n");
+  EXPECT_TRUE(s.running());
+  s.stop();
+}
