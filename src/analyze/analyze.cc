@@ -96,6 +96,51 @@ bool log_has_gpu_runtime_error(const std::string& text, std::string* match) {
   return false;
 }
 
+std::vector<std::string> runner_problems(const std::string& text) {
+  const std::string tag = "[devspace-runner] ";
+  std::string down, failed_reload, last_failure, last_exception;
+  bool in_traceback = false;
+  for (auto& line : split(text, "\n")) {
+    size_t at = line.find(tag);
+    if (at == std::string::npos) {
+      // the last line of a Python traceback printed after a failure: "<Error>: <message>"
+      std::string t = trim(line);
+      if (in_traceback && !t.empty() && t[0] != ' ' && t.find(": ") != std::string::npos &&
+          !starts_with(t, "Traceback") && !starts_with(t, "File "))
+        last_exception = t.size() > 300 ? t.substr(0, 300) + "..." : t;
+      continue;
+    }
+    std::string msg = line.substr(at + tag.size());
+    in_traceback = false;
+    if (contains(msg, " step failed ") || contains(msg, " startup failed ") || contains(msg, " setup failed ") ||
+        contains(msg, " load failed ") || contains(msg, "group failure")) {
+      last_failure = msg.substr(0, msg.find(':') == std::string::npos ? msg.size() : msg.find(':'));
+      last_exception.clear();
+      in_traceback = true;
+    } else if (contains(msg, "waiting for a file change before starting")) {  // a group, or one rank
+      down = msg;
+    } else if (starts_with(msg, "started gen=")) {
+      down.clear();
+      failed_reload.clear();
+    } else if (starts_with(msg, "reloaded gen=")) {
+      failed_reload.clear();
+    } else if (starts_with(msg, "reload failed gen=")) {
+      failed_reload = msg;
+    }
+  }
+  std::vector<std::string> out;
+  if (!down.empty()) {
+    std::string why = last_failure.empty() ? "" : " after " + last_failure;
+    if (!last_exception.empty()) why += " (" + last_exception + ")";
+    out.push_back("training group is down" + why + "; the runner waits for an edit of the synced code to start it "
+                  "again");
+  } else if (!failed_reload.empty()) {
+    std::string why = last_exception.empty() ? "" : " (" + last_exception + ")";
+    out.push_back("the last edit did not load: " + failed_reload.substr(0, failed_reload.find('\n')) + why);
+  }
+  return out;
+}
+
 // RCCL between the GPUs of one pod (one process per GPU) and PyTorch's worker processes use
 // /dev/shm; container runtimes give 64 MiB unless a memory-backed emptyDir is mounted there.
 // Returns "" when a multi-GPU pod has one, else the problem.
@@ -288,6 +333,20 @@ std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, co
     for (auto& prob : gpu::pod_sizing_problems(p.get("spec")))
       out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + prob + "\n");
     crash_errors(p, want);
+    // a Running GPU pod can still be idle: its training group down after a rank failed, or the
+    // last edit not loaded (the runner keeps the previous code)
+    if (kube::pod_status(p) == "Running") {
+      for (auto& c : p.at_path("spec.containers").items()) {
+        std::string text;
+        try {
+          text = k.logs(ns, name, c.get("name").as_string(), 400);
+        } catch (...) {
+          continue;
+        }
+        for (auto& prob : runner_problems(text))
+          out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + prob + "\n");
+      }
+    }
     if (o.gpu_probe && kube::pod_status(p) == "Running") {
       std::string c = p.at_path("spec.containers")[0].get("name").as_string();
       try {

@@ -34,6 +34,10 @@ std::string analyze(kube::Client& k, const std::string& ns, const Options& o);
 std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, const std::vector<Value>& pods,
                                       const Options& o);
 bool log_has_gpu_runtime_error(const std::string& log, std::string* match);
+// The hot-reload training runner's state from a container log ("[devspace-runner] ..." lines,
+// devspace_amd/runner.py): a group that is down waiting for an edit after a rank failed, or a
+// last edit that did not load (the ranks kept the previous code). Empty when it trains.
+std::vector<std::string> runner_problems(const std::string& log);
 // Multi-GPU pod without a memory-backed /dev/shm (RCCL): the problem text, or "".
 std::string shm_problem(const Value& pod, int64_t gpus);
 // Runs the shell-only GPU probe in a container; returns the problems it found (empty = fine).

@@ -97,6 +97,37 @@ TEST(analyze_gpu_runtime_log_matcher) {
   EXPECT_EQ(analyze::shm_problem(ok, 8), std::string(""));
 }
 
+// The runner's state in a pod log (devspace_amd/runner.py output): a group down after a rank
+// failed, a last edit that did not load, or training (no problem).
+TEST(analyze_runner_state_from_pod_log) {
+  std::string up = "[devspace-runner] started gen=1 marker=v0 digest=ab code=cd world=8\n"
+                   "[devspace-runner] reloaded gen=2 marker=v1 digest=ef code=01 ranks=8 step=9\n";
+  EXPECT_TRUE(analyze::runner_problems(up).empty());
+  std::string down = up +
+                     "[devspace-runner] rank=3 step failed gen=3 marker=bad: leaving the group (the supervisor restarts it)\n"
+                     "Traceback (most recent call last):\n"
+                     "  File \"/app/train.py\", line 40, in step\n"
+                     "ValueError: shapes (4,8) and (9,8) not aligned\n"
+                     "[devspace-runner] rank=3 exited with code 3: restarting the group of 8 (1/3 since the last edit)\n"
+                     "[devspace-runner] rank=3 startup failed gen=1:\n"
+                     "Traceback (most recent call last):\n"
+                     "ValueError: shapes (4,8) and (9,8) not aligned\n"
+                     "[devspace-runner] rank=3 exited with code 3 before every rank finished a first step: waiting for a "
+                     "file change before starting the group again\n";
+  auto p = analyze::runner_problems(down);
+  EXPECT_EQ(p.size(), (size_t)1);
+  EXPECT_TRUE(contains(p[0], "training group is down after rank=3 startup failed gen=1"));
+  EXPECT_TRUE(contains(p[0], "ValueError: shapes (4,8) and (9,8) not aligned"));
+  EXPECT_TRUE(analyze::runner_problems(down + "[devspace-runner] started gen=1 marker=fixed world=8\n").empty());
+  std::string bad_edit = up + "[devspace-runner] rank=1 load failed gen=3:\nTraceback (most recent call last):\n"
+                              "ImportError: rank-local\n"
+                              "[devspace-runner] reload failed gen=3 (failed on rank(s) [1]), keeping gen=2 on every rank\n";
+  p = analyze::runner_problems(bad_edit);
+  EXPECT_EQ(p.size(), (size_t)1);
+  EXPECT_TRUE(contains(p[0], "the last edit did not load: reload failed gen=3"));
+  EXPECT_TRUE(analyze::runner_problems(bad_edit + "[devspace-runner] reloaded gen=4 marker=ok ranks=8\n").empty());
+}
+
 // $KUBECONFIG with several files, merged like client-go's clientcmd loading rules.
 TEST(kubeconfig_multi_file_merge_and_save) {
   std::string d = fs::make_temp_dir("kcmerge-");

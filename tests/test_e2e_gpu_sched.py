@@ -100,3 +100,46 @@ def test_rocm_pytorch_example_runs_from_a_clean_clone(tmp_path):
         assert "[devspace-runner] started gen=1" in log, log[-3000:]
     finally:
         cluster.stop()
+
+
+def test_analyze_reports_a_training_group_that_is_down(tmp_path):
+    """A rank of the pod's training group fails on a bad edit: the runner stops the group and
+    waits for the next edit, the pod stays Running, and `devspace analyze` says why the GPUs are
+    idle (the failing rank and its exception) instead of "No problems found"."""
+    import os
+    import re
+
+    from devspace_amd.localkube import LocalCluster
+
+    cluster = LocalCluster(str(tmp_path / "state"), gpus=2).start()
+    try:
+        lk = DevspaceEnv(cluster, str(tmp_path))
+        proj = lk.project("rocm-pytorch")
+        train = os.path.join(proj, "train.py")
+        src = open(train).read()
+        for k, v in (("VOCAB", 128), ("DIM", 64), ("HEADS", 4), ("LAYERS", 1), ("SEQ", 16), ("BATCH", 2)):
+            src = re.sub(rf"^{k} = \d+$", f"{k} = {v}", src, flags=re.M)
+        src = src.replace("def step(ctx, state):\n",
+                          "def step(ctx, state):\n    if ctx.rank == 1:\n"
+                          "        raise ValueError('shapes (4,8) and (9,8) not aligned')\n", 1)
+        open(train, "w").write(src)
+        values = os.path.join(proj, "chart", "values.yaml")
+        v = open(values).read()
+        open(values, "w").write(re.sub(r"gpu: \d+", "gpu: 2", v))  # two ranks
+        r = lk.run(["deploy"], proj, timeout=300, check=False)
+        assert r.returncode == 0, r.stdout + r.stderr
+        pods = cluster.wait_pods_running("rocm-pytorch", timeout=120)
+        import json
+
+        root = next(iter(json.loads(pods[0]["metadata"]["annotations"]["devspace.sh/local-roots"]).values()))
+        deadline = time.time() + 180
+        log = ""
+        while time.time() < deadline and "waiting for a file change" not in log:
+            log = open(root + ".log").read() if os.path.exists(root + ".log") else ""
+            time.sleep(0.5)
+        assert "waiting for a file change" in log, log[-3000:]
+        out = lk.run(["analyze", "--wait=false"], proj, timeout=120, check=False).stdout
+        assert "training group is down after rank=1" in out, out
+        assert "ValueError: shapes (4,8) and (9,8) not aligned" in out, out
+    finally:
+        cluster.stop()
