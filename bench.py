@@ -222,6 +222,9 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         _log(f"dev: pod {pod_name} synced after {deploy_s:.2f}s")
         _, _, idx = tail.wait_for(r"Attached to container", start_index=idx, timeout=_budget(120))
         _wait_file_contains(root + ".log", "[devspace-runner] started gen=", timeout=_budget(900), interval=0.05)
+        # `devspace dev` start -> image built, chart deployed, pod running, every rank through
+        # import torch, model setup and its first training step on the GPU
+        first_step_s = time.perf_counter() - t_dev
         pod_log = open(root + ".log").read()
         m = re.search(r"\[devspace-runner\] started gen=\d+ .*?world=(\d+) device=(\S+)", pod_log)
         pod_world = int(m.group(1)) if m else 0
@@ -272,7 +275,7 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         if timed_end:
             timed_end()
         return {"reload_ms": samples, "sync_ms": sync_samples, "mode": mode, "pod_deploy_s": deploy_s,
-                "parts": parts, "fused": fused, "world": pod_world,
+                "parts": parts, "fused": fused, "world": pod_world, "first_step_s": first_step_s,
                 "ranks_agreed": bool(agreed) and all(a == pod_world for a in agreed)}
     finally:
         _killpg(dev)
@@ -836,7 +839,8 @@ def report(args, nproc, tls, ms_total, qs, extras):
              "ranks_agreed_on_code": gp.get("ranks_agreed"),
              "reload_p50_ms": round(gp50, 2), "reload_p90_ms": round(_pct(gp["reload_ms"], 0.9), 2),
              "sync_p50_ms": round(_pct(gp["sync_ms"], 0.5), 2), "n": len(gp["reload_ms"]),
-             "pod_deploy_s": round(gp["pod_deploy_s"], 3)}
+             "pod_deploy_s": round(gp["pod_deploy_s"], 3),
+             "dev_to_first_step_s": round(gp["first_step_s"], 3) if gp.get("first_step_s") else None}
         parts = {k: round(_pct(v, 0.5), 2) for k, v in gp.get("parts", {}).items() if v}
         if parts:
             parts["sync_ms"] = g["sync_p50_ms"]
