@@ -37,7 +37,8 @@ examples/quickstart/package.json:7, the redeploy loop of cmd/dev.go:225-234,284-
     stops the others (blocked in a collective, or not) and starts a fresh group of child
     processes. A group that fails before its first step completes (the code itself is broken)
     waits for the next edit before starting again, as nodemon does ("app crashed - waiting for
-    file changes"). A single rank keeps running the previous version after a failed step.
+    file changes"). A single rank pauses training after a failed step and resumes with the next
+    edit (process, model and optimizer state stay).
 
 Preemptible steps: a step may call `ctx.preempt_point()` between its phases (e.g. between
 forward and backward). The point abandons the rest of the step when a newer version of the
@@ -786,9 +787,10 @@ def worker_main(args) -> int:
         max_steps = args.max_steps
         script_mode = not hasattr(mod, "step")
         fault.armed = True
+        paused = False  # one rank: a step of this generation failed; no more steps until an edit
         while agree is not None or not stop:
             # 1. pick up local change notifications (non-blocking while training; blocking when idle)
-            timeout = 0 if (not script_mode and args.train) else 0.05
+            timeout = 0 if (not script_mode and args.train and not paused) else 0.05
             n_changes, t_first, helper_changed = feed.take(timeout)
             # Rank 0's feed alone advances the generation: every rank watches the same synced
             # directory, but their feeds post the edit microseconds apart, and a rank that saw it one
@@ -854,7 +856,12 @@ def worker_main(args) -> int:
                         leave(EXIT_STEP_FAILED, f"step failed gen={gen} marker={getattr(mod, 'MARKER', '')}: "
                                                 f"leaving the group (the supervisor restarts it)\n"
                                                 f"{traceback.format_exc()}")
-                    ctx.error(f"step failed gen={gen}:\n{traceback.format_exc()}")
+                    ctx.error(f"step failed gen={gen}: training paused until the next edit\n"
+                              f"{traceback.format_exc()}")
+                    paused = True
+                    reload_t0 = None
+                    continue
+                paused = False
                 step_ms = (time.perf_counter() - t_step) * 1000.0
                 since = (time.perf_counter() - reload_t0) * 1000.0 if reload_t0 else 0.0
                 reload_t0 = None
@@ -868,7 +875,7 @@ def worker_main(args) -> int:
                 )
                 t_iter = time.perf_counter()
                 continue
-            if script_mode or not args.train:
+            if script_mode or not args.train or paused:
                 continue
             try:
                 metrics = mod.step(ctx, state) or {}
@@ -880,8 +887,10 @@ def worker_main(args) -> int:
                     leave(EXIT_STEP_FAILED, f"step failed gen={gen} marker={getattr(mod, 'MARKER', '')}: "
                                             f"leaving the group (the supervisor restarts it)\n"
                                             f"{traceback.format_exc()}")
-                ctx.error(f"step failed gen={gen}:\n{traceback.format_exc()}")
-                time.sleep(0.2)
+                # one rank (nodemon's "app crashed - waiting for file changes"): no retry loop that
+                # prints the same traceback five times a second; the next edit resumes training
+                ctx.error(f"step failed gen={gen}: training paused until the next edit\n{traceback.format_exc()}")
+                paused = True
                 continue
             now = time.perf_counter()
             dt = (now - t_iter) * 1000.0

@@ -406,3 +406,39 @@ def test_entry_file_gone_is_a_failed_reload_not_a_crash(tmp_path):
         assert "exited with code" not in r.text(), r.text()
     finally:
         r.stop()
+
+
+def test_single_rank_step_failure_pauses_until_the_next_edit(tmp_path):
+    """One rank: a step that raises is reported once (no traceback five times a second) and
+    training pauses, in the same warm process, until the next edit fixes it."""
+    entry = tmp_path / "train.py"
+    entry.write_text('''import time
+MARKER = "v0"
+
+
+def setup(ctx):
+    return {"n": 0}
+
+
+def step(ctx, state):
+    if MARKER == "bad":
+        raise ValueError("broken step")
+    state["n"] += 1
+    time.sleep(0.005)
+    return {"loss": state["n"]}
+''')
+    r = Runner(tmp_path, entry, 1, extra_args=("--log-every", "20"))
+    try:
+        r.until(r"started gen=1 marker=v0", timeout=180)
+        pid = r.proc.pid
+        _set_marker(entry, "bad")
+        r.until(r"step failed gen=2: training paused until the next edit", timeout=60)
+        time.sleep(1.0)
+        _set_marker(entry, "fixed")
+        _, line = r.until(r"reloaded gen=3 marker=fixed ", timeout=60)
+        assert r.text().count("ValueError: broken step") == 1, r.text()  # reported once
+        assert r.proc.pid == pid and r.proc.poll() is None  # same warm process
+        n_before = int(re.search(r"loss=(\d+)", line).group(1))
+        assert n_before > 1, line  # the state survived the failure
+    finally:
+        r.stop()
