@@ -740,7 +740,7 @@ void Session::dispatch_upstream(std::vector<FileInfo>& changes, long first_event
       now.push_back(c);
     }
   }
-  if (!bulk.empty() && small_bytes >= kBulkBatchBytes) {  // a big tree of small files: all bulk
+  if (small_bytes >= kBulkBatchBytes) {  // a big tree of small files (a dataset copied in): all bulk
     std::vector<FileInfo> keep;
     for (auto& c : now) (c.mtime > 0 ? bulk : keep).push_back(c);
     now.swap(keep);
