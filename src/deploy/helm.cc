@@ -11,6 +11,7 @@
 
 #include "analyze/analyze.h"
 #include "core/codec.h"
+#include "core/compat.h"
 #include "core/fs.h"
 #include "core/log.h"
 #include "core/safe_regex.h"
@@ -998,6 +999,13 @@ Client::WaitOutcome Client::wait_ready(const std::vector<Value>& objs, const std
       pending = not_ready_reason(kind, name, cur);
       return pending.empty();
     };
+    if (reference_timing()) {
+      // the reference-equivalent column: the original's 5 s readiness polls over the whole
+      // timeout and nothing pull-aware (a timeout is analyzed and a first install purged)
+      int64_t left = ms_until(deadline);
+      if (left > 0 && k_->wait_object(path, (int)left, ready)) continue;
+      return {"timed out waiting for the condition (" + pending + ")"};
+    }
     while (true) {
       int64_t left = ms_until(deadline);
       int slice = (int)(left > 0 ? std::min<int64_t>(left, 1000) : std::min<int64_t>(1000, ms_until(pull_deadline)));
