@@ -59,6 +59,12 @@ class ApiServer:
         self.throttle_first = 0
         self.retry_after = "1"
         self.throttled = {}  # (verb, resource) -> requests answered 429
+        # Namespace-scoped users (RBAC as a Role + RoleBinding in one namespace grants it, e.g.
+        # a DevSpace.cloud Space or a multi-tenant cluster): bearer token -> the namespace it may
+        # use. Everything cluster-scoped (nodes, namespaces, cluster roles, PVs) and every other
+        # namespace answers 403 Forbidden; discovery (/version, /api, /apis) stays open.
+        self.scoped_tokens = {}
+        self.forbidden = 0
 
     def reset_throttle(self, first=None, retry_after=None):
         if first is not None:
@@ -90,6 +96,27 @@ class ApiServer:
         return verb, resource
 
     @web.middleware
+    async def _rbac(self, request, handler):
+        h = request.headers.get("Authorization", "")
+        ns_allowed = self.scoped_tokens.get(h[7:]) if h.startswith("Bearer ") else None
+        if ns_allowed is None or not request.path.startswith(("/api/", "/apis/")):
+            return await handler(request)
+        segs = [x for x in request.path.split("/") if x]
+        group = "" if segs[:1] == ["api"] else (segs[1] if len(segs) > 1 else "")
+        rest = segs[2:] if segs[:1] == ["api"] else segs[3:]
+        if len(rest) >= 3 and rest[0] == "namespaces" and rest[1] == ns_allowed:
+            return await handler(request)
+        if not rest:  # /api/v1, /apis/apps/v1: resource discovery
+            return await handler(request)
+        verb, resource = self._verb(request)
+        self.forbidden += 1
+        where = f'in the namespace "{rest[1]}"' if len(rest) >= 3 and rest[0] == "namespaces" else "at the cluster scope"
+        msg = (f'{resource.split("/")[0]} is forbidden: User "system:serviceaccount:{ns_allowed}:developer" cannot '
+               f'{verb} resource "{resource.split("/")[0]}" in API group "{group}" {where}')
+        return web.json_response({"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Failure",
+                                  "message": msg, "reason": "Forbidden", "code": 403}, status=403)
+
+    @web.middleware
     async def _throttle(self, request, handler):
         if self.throttle_first > 0 and request.path.startswith(("/api/", "/apis/")):
             key = self._verb(request)
@@ -117,7 +144,7 @@ class ApiServer:
         return await handler(request)
 
     def app(self):
-        app = web.Application(client_max_size=256 * 1024 * 1024, middlewares=[self._auth, self._throttle])
+        app = web.Application(client_max_size=256 * 1024 * 1024, middlewares=[self._auth, self._rbac, self._throttle])
         app.router.add_get("/version", self.version)
         app.router.add_get("/api", self.api_versions)
         app.router.add_get("/apis", self.api_groups)

@@ -604,7 +604,17 @@ std::string Client::logs(const std::string& ns, const std::string& pod, const st
 
 void Client::ensure_namespace(const std::string& ns) {
   if (ns.empty() || ns == "default") return;
-  if (try_get("/api/v1/namespaces/" + ns)) return;
+  try {
+    if (try_get("/api/v1/namespaces/" + ns)) return;
+  } catch (const ApiError& e) {
+    // a namespace-scoped user (a Role in that namespace only) may not read Namespace objects,
+    // which are cluster-scoped: the namespace it was given exists; later calls say otherwise
+    if (e.code == 403) {
+      log::debug("cannot read namespace " + ns + " (" + e.what() + "): assuming it exists");
+      return;
+    }
+    throw;
+  }
   Value body = Value::map();
   body["apiVersion"] = "v1";
   body["kind"] = "Namespace";
