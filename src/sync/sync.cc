@@ -1698,9 +1698,16 @@ void Session::download_and_apply(const std::vector<FileInfo>& files) {
       s->stats_.bytes_down += p->done;
     }
   } count{this, &prog};
+  // Smallest first (not in compat mode): files land one by one as the stream is extracted, so a
+  // log or metrics file written next to a multi-GB checkpoint arrives before the checkpoint
+  // instead of after it.
+  std::vector<const FileInfo*> order;
+  for (auto& f : files) order.push_back(&f);
+  if (mode_ != Mode::Compat)
+    std::stable_sort(order.begin(), order.end(), [](const FileInfo* a, const FileInfo* b) { return a->size < b->size; });
   if (down_helper_) {
     std::string rels;
-    for (auto& f : files) rels += f.name + "\n";
+    for (auto* f : order) rels += f->name + "\n";
     if (!write_all(fd, request('D', rels))) throw SyncError("downstream: write failed");
     std::string line = read_line_idle(down_out_, idle, "downstream: helper reply");
     if (line != "STREAM") throw SyncError("downstream: helper error: " + line);
@@ -1713,7 +1720,7 @@ void Session::download_and_apply(const std::vector<FileInfo>& files) {
     return;
   }
   std::string list;
-  for (auto& f : files) list += dest_ + f.name + "\n";
+  for (auto* f : order) list += dest_ + f->name + "\n";
   if (mode_ == Mode::Compat) {
     std::string cmd = "fileSize=" + std::to_string(list.size()) + R"(;
 					tmpFileInput=")" + remote("/tmp/devspace-downstream-input") + R"(";

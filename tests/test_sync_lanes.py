@@ -117,3 +117,26 @@ def test_edit_overtakes_a_bulk_upload_and_downstream_keeps_working(tmp_path, siz
         assert (_read(pod / "train.py") or b"").startswith(b"MARKER = 1")
     finally:
         s.stop()
+
+
+def test_small_pod_file_comes_back_before_a_big_one_written_with_it(tmp_path):
+    """A training pod writes a checkpoint and a metrics file at once: the download streams the
+    smallest files first, so the metrics land locally while the checkpoint is still coming."""
+    src, pod = tmp_path / "src", tmp_path / "pod"
+    src.mkdir()
+    pod.mkdir()
+    big = tmp_path / "big.bin"
+    with open(big, "wb") as f:
+        for _ in range(512 // 16):
+            f.write(os.urandom(16 << 20))
+    s = _session(src, pod, tmp_path)
+    try:
+        os.link(big, pod / "ckpt.bin")  # both appear in the pod together
+        (pod / "metrics.json").write_text('{"loss": 1.5}\n')
+        _wait(lambda: _read(src / "metrics.json") == b'{"loss": 1.5}\n', 30, "metrics downloaded")
+        ckpt_done = (src / "ckpt.bin").exists() and (src / "ckpt.bin").stat().st_size == big.stat().st_size
+        _wait(lambda: (src / "ckpt.bin").exists() and (src / "ckpt.bin").stat().st_size == big.stat().st_size, 300,
+              "checkpoint downloaded")
+        assert not ckpt_done, "the checkpoint was complete before the metrics file arrived"
+    finally:
+        s.stop()
