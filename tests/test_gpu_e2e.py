@@ -103,3 +103,57 @@ def test_rocm_pytorch_pod_trains_on_gpu(tmp_path):
             print("pod profile:", dbs)
     finally:
         cluster.stop()
+
+
+@pytest.mark.gpu
+def test_two_rank_gpu_pod_contains_a_rank_failure_and_analyze_explains_it(tmp_path):
+    """The rocm-pytorch pod with amd.com/gpu: 2 (both ranks on the box's one MI355X, joined over
+    gloo), through `devspace deploy`: an edit that breaks rank 1 stops and parks the training
+    group, `devspace analyze` names the failing rank and its exception, and the fix brings the
+    group back on the GPU."""
+    from devspace_amd.localkube import LocalCluster
+
+    cluster = LocalCluster(str(tmp_path / "state"), gpus=2).start()
+    cluster.kubelet.extra_env["DEVSPACE_DIST_BACKEND"] = "gloo"  # RCCL refuses two ranks on one GPU
+    try:
+        lk = DevspaceEnv(cluster, str(tmp_path))
+        proj = lk.project("rocm-pytorch")
+        vpath = os.path.join(proj, "chart", "values.yaml")
+        v = open(vpath).read()
+        with open(vpath, "w") as f:
+            f.write(re.sub(r"gpu: \d+", "gpu: 2", v))
+        assert "Successfully deployed!" in lk.run(["deploy"], proj, timeout=600).stdout
+        pod = _wait(lambda: [p for p in lk.pods("rocm-pytorch") if p["status"].get("phase") == "Running"], 120,
+                    "running pod")[0]
+        root = json.loads(pod["metadata"]["annotations"]["devspace.sh/local-roots"])[
+            pod["spec"]["containers"][0]["name"]]
+
+        def log():
+            return open(root + ".log").read() if os.path.exists(root + ".log") else ""
+
+        _wait(lambda: "started gen=1" in log(), 300, "runner start")
+        assert re.search(r"started gen=1 .*world=2 device=cuda", log()), log()[-3000:]
+        train = os.path.join(root, "app", "train.py")  # what `devspace dev` syncs into the pod
+        good = open(train).read()
+        bad = good.replace("def step(ctx, state):\n",
+                           "def step(ctx, state):\n    if ctx.rank == 1:\n"
+                           "        raise ValueError('rank 1 sees a bad batch')\n", 1)
+        assert bad != good
+        with open(train + ".tmp", "w") as f:
+            f.write(bad)
+        os.rename(train + ".tmp", train)
+        _wait(lambda: "waiting for a file change before starting the group again" in log(), 180, "group parked")
+        r = lk.run(["analyze", "--wait=false", "-n", "rocm-pytorch"], proj, timeout=120, check=False)
+        report = r.stdout + r.stderr
+        assert "training group is down after rank=1" in report, report
+        assert "ValueError: rank 1 sees a bad batch" in report, report
+        n_started = log().count("started gen=1")
+        with open(train + ".tmp", "w") as f:
+            f.write(good.replace('MARKER = "v0"', 'MARKER = "fixed"'))
+        os.rename(train + ".tmp", train)
+        _wait(lambda: log().count("started gen=1") > n_started and "marker=fixed" in log(), 240, "group back")
+        assert re.search(r"started gen=1 marker=fixed .*world=2 device=cuda", log()), log()[-3000:]
+        r = lk.run(["analyze", "--wait=false", "-n", "rocm-pytorch"], proj, timeout=120, check=False)
+        assert "training group is down" not in r.stdout, r.stdout
+    finally:
+        cluster.stop()
