@@ -10,6 +10,7 @@
 The multi-GB version of the second test is in tests/test_sync_large.py
 (test_small_edit_overtakes_a_multi_gb_upload)."""
 
+import hashlib
 import os
 import time
 
@@ -18,15 +19,15 @@ import pytest
 from conftest import ROOT
 
 
-def _session(src, pod, tmp_path):
+def _session(src, pod, tmp_path, mode="helper"):
     from devspace_amd import _native
 
-    s = _native.SyncSession(str(src), str(pod), mode="helper", exclude=[],
+    s = _native.SyncSession(str(src), str(pod), mode=mode, exclude=[],
                             helper_path=os.path.join(ROOT, "bin", "devspace-helper"),
                             log_dir=str(tmp_path / "logs"), pod_name="lanes")
     s.start()
     assert s.wait_initial_sync(60000), s.error()
-    assert s.mode() == "helper"
+    assert s.mode() == mode
     return s
 
 
@@ -138,5 +139,67 @@ def test_small_pod_file_comes_back_before_a_big_one_written_with_it(tmp_path):
         _wait(lambda: (src / "ckpt.bin").exists() and (src / "ckpt.bin").stat().st_size == big.stat().st_size, 300,
               "checkpoint downloaded")
         assert not ckpt_done, "the checkpoint was complete before the metrics file arrived"
+    finally:
+        s.stop()
+
+
+def _tree(root):
+    out = {}
+    for d, dirs, files in os.walk(root):
+        dirs[:] = [x for x in dirs if not x.startswith(".devspace")]
+        for f in files:
+            if f.endswith(".devspace-tmp"):
+                continue
+            p = os.path.join(d, f)
+            try:
+                with open(p, "rb") as fh:
+                    out[os.path.relpath(p, root)] = hashlib.sha256(fh.read()).hexdigest()
+            except FileNotFoundError:  # removed while we walked: the next look settles it
+                continue
+    return out
+
+
+@pytest.mark.parametrize("mode,seed", [("helper", 1), ("helper", 2), ("helper", 3), ("fast", 4)])
+def test_random_mix_of_edits_and_bulk_files_converges(tmp_path, mode, seed):
+    """Randomised: small edits, 4-12 MiB files (bulk lane), removes and renames on the local side,
+    new files written in the pod meanwhile. Whatever the interleaving of lanes and deferred
+    edits, both sides end with the same bytes."""
+    import random
+
+    rng = random.Random(seed)
+    src, pod = tmp_path / "src", tmp_path / "pod"
+    src.mkdir()
+    pod.mkdir()
+    s = _session(src, pod, tmp_path, mode)
+    try:
+        names = [f"f{i}.py" for i in range(8)] + [f"big{i}.bin" for i in range(3)]
+        for step in range(60):
+            op = rng.random()
+            name = rng.choice(names)
+            p = src / name
+            if op < 0.55:
+                if name.startswith("big"):
+                    p.write_bytes(os.urandom(rng.randint(4, 12) << 20))
+                else:
+                    p.write_text(f"x = {step}  # {'#' * rng.randint(0, 300)}\n")
+            elif op < 0.7:
+                if p.exists():
+                    p.unlink()
+            elif op < 0.8:
+                if p.exists():
+                    os.rename(p, src / rng.choice(names))
+            else:
+                (pod / f"pod{step}.txt").write_text(f"from the pod {step}\n")
+            time.sleep(rng.choice([0, 0, 0.001, 0.01, 0.05]))
+        deadline = time.monotonic() + 120
+        while time.monotonic() < deadline:
+            a, b = _tree(src), _tree(pod)
+            if a == b:
+                break
+            time.sleep(0.2)
+        a, b = _tree(src), _tree(pod)
+        diff = sorted(set(a.items()) ^ set(b.items()))
+        assert a == b, diff[:20]
+        assert s.running(), s.error()
     finally:
         s.stop()
