@@ -926,16 +926,18 @@ static PodProgress pod_progress(kube::Client& k, const Value& workload, const st
   }
   if (creating.empty()) return out;
   // A pod pulls while its kubelet has reported more `Pulling` than `Successfully pulled` events
-  // for it (`Pulled` also says "already present on machine": no pull happened then).
-  Value evs;
-  try {
-    evs = k.get("/api/v1/namespaces/" + ns + "/events");
-  } catch (const std::exception&) {
-    return out;
-  }
+  // for it (`Pulled` also says "already present on machine": no pull happened then). Only that
+  // pod's events are listed (field selector), not the namespace's whole event history.
   for (const Value* p : creating) {
     std::string pn = p->at_path("metadata.name").as_string();
     std::string uid = p->at_path("metadata.uid").as_string();
+    Value evs;
+    try {
+      evs = k.get("/api/v1/namespaces/" + ns + "/events?fieldSelector=" +
+                  net::url_encode("involvedObject.kind=Pod,involvedObject.name=" + pn));
+    } catch (const std::exception&) {
+      continue;
+    }
     int64_t pulls = 0, pulled = 0, since = 0;
     std::string what;
     for (auto& e : evs.get("items").items()) {
