@@ -1431,8 +1431,10 @@ void Session::initial_sync() {
     std::map<std::string, FileInfo> none;
     apply_downstream(dl, none);
   }
-  // "initial sync done" means the container has the files, not that they are queued
+  // "initial sync done" means the container has the files, not that they are queued (and the
+  // files only the container had are here)
   wait_upstream_idle();
+  wait_bulk_down_idle();
 }
 
 // Initial sync against a pod whose image already holds the project (`COPY . .`): the copies
@@ -1609,12 +1611,12 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
       known->has_remote_attrs = true;
     }
     if (fi->is_symlink) index_.files[fi->name] = *fi;
-    if (should_download(*fi) && !in_flight(fi->name, false)) creates.push_back(*fi);
+    if (should_download(*fi) && !in_flight(fi->name, false) && !downloading(fi->name)) creates.push_back(*fi);
   }
   if (!dest_found) throw SyncError("DestPath not found, find command did not execute correctly");
   if (removes) {  // an upload or remove in flight: the index is about to change, not the pod
     for (auto it = removes->begin(); it != removes->end();) {
-      if (in_flight(it->first, false))
+      if (in_flight(it->first, false) || downloading(it->first))
         it = removes->erase(it);
       else
         ++it;
@@ -1663,7 +1665,82 @@ bool Session::probe_changes() {
   return hit;
 }
 
-void Session::download_and_apply(const std::vector<FileInfo>& files) {
+bool Session::downloading(const std::string& rel) {
+  std::lock_guard<std::mutex> g(inflight_mu_);
+  return !downloading_.empty() && downloading_.count(rel) > 0;
+}
+
+bool Session::open_bulk_down_shell() {
+  if (bulk_down_shell_ && bulk_down_shell_->alive()) return true;
+  std::unique_ptr<Shell> sh;
+  try {
+    sh = transport_->open({"sh"});
+    bulk_down_out_.reset(sh->out());
+    if (start_helper(sh, bulk_down_out_)) {
+      std::lock_guard<std::mutex> g(bulk_down_ptr_mu_);
+      bulk_down_shell_ = std::move(sh);
+      return true;
+    }
+  } catch (const std::exception& e) {
+    logf(std::string("[Downstream] No bulk download channel: ") + e.what());
+  }
+  if (sh) sh->close();
+  std::lock_guard<std::mutex> g(bulk_down_ptr_mu_);
+  bulk_down_shell_.reset();
+  return false;
+}
+
+void Session::bulk_down_loop() {
+  while (!stopping_ && !failed_) {
+    std::vector<FileInfo> batch;
+    {
+      std::unique_lock<std::mutex> lk(q_mu_);
+      q_cv_.wait_for(lk, std::chrono::milliseconds(200),
+                     [this] { return !bulk_down_q_.empty() || stopping_ || failed_; });
+      if (bulk_down_q_.empty()) continue;
+      batch = std::move(bulk_down_q_.front());
+      bulk_down_q_.pop_front();
+      bulk_down_busy_ = true;
+    }
+    struct Done {
+      Session* s;
+      const std::vector<FileInfo>& b;
+      ~Done() {
+        {
+          std::lock_guard<std::mutex> g(s->inflight_mu_);
+          for (auto& f : b) s->downloading_.erase(f.name);
+        }
+        {
+          std::lock_guard<std::mutex> g(s->q_mu_);
+          s->bulk_down_busy_ = false;
+        }
+        s->q_cv_.notify_all();
+      }
+    } done{this, batch};
+    try {
+      bool own;
+      {
+        std::lock_guard<std::mutex> g(bulk_down_mu_);
+        own = open_bulk_down_shell();
+      }
+      download_and_apply(batch, own);  // no second channel: the main one, as before
+      std::lock_guard<std::mutex> g(stats_mu_);
+      stats_.downstream_batches++;
+      stats_.downstream_changes += batch.size();
+    } catch (const std::exception& e) {
+      fail(e.what());
+      return;
+    }
+  }
+}
+
+void Session::wait_bulk_down_idle() {
+  std::unique_lock<std::mutex> lk(q_mu_);
+  while (!stopping_ && !failed_ && (bulk_down_busy_ || !bulk_down_q_.empty()))
+    q_cv_.wait_for(lk, std::chrono::milliseconds(50));
+}
+
+void Session::download_and_apply(const std::vector<FileInfo>& files, bool bulk) {
   uint64_t total = 0;
   for (auto& f : files) total += (uint64_t)std::max<int64_t>(0, f.size);
   if (files.size() > 3) logf(strfmt("[Downstream] Download %zu files (size: %llu)", files.size(), (unsigned long long)total));
@@ -1675,8 +1752,10 @@ void Session::download_and_apply(const std::vector<FileInfo>& files) {
       warn_large(f.name, f.size);
     }
   }
-  std::lock_guard<std::mutex> sg(down_shell_mu_);
-  int fd = down_shell_->in();
+  std::lock_guard<std::mutex> sg(bulk ? bulk_down_mu_ : down_shell_mu_);
+  Shell* shell = bulk ? bulk_down_shell_.get() : down_shell_.get();
+  LineReader& reply = bulk ? bulk_down_out_ : down_out_;
+  int fd = shell->in();
   const int idle = o_.idle_timeout_ms;
   Progress prog(this, "[Downstream] Download", total);
   RateLimiter rl(o_.downstream_limit);
@@ -1705,16 +1784,16 @@ void Session::download_and_apply(const std::vector<FileInfo>& files) {
   for (auto& f : files) order.push_back(&f);
   if (mode_ != Mode::Compat)
     std::stable_sort(order.begin(), order.end(), [](const FileInfo* a, const FileInfo* b) { return a->size < b->size; });
-  if (down_helper_) {
+  if (down_helper_ || bulk) {
     std::string rels;
     for (auto* f : order) rels += f->name + "\n";
     if (!write_all(fd, request('D', rels))) throw SyncError("downstream: write failed");
-    std::string line = read_line_idle(down_out_, idle, "downstream: helper reply");
+    std::string line = read_line_idle(reply, idle, "downstream: helper reply");
     if (line != "STREAM") throw SyncError("downstream: helper error: " + line);
-    frame::ChunkReader cr(counted(reader_source(down_out_, idle, "downstream: helper stream")));
+    frame::ChunkReader cr(counted(reader_source(reply, idle, "downstream: helper stream")));
     untar_stream(cr.source(), nullptr);
     cr.drain();
-    line = read_line_idle(down_out_, idle, "downstream: helper reply");
+    line = read_line_idle(reply, idle, "downstream: helper reply");
     if (line != "OK") throw SyncError("downstream: helper error: " + line);
     prog.finish();
     return;
@@ -2012,6 +2091,23 @@ void Session::apply_downstream(const std::vector<FileInfo>& creates, std::map<st
   for (auto& c : creates) (c.is_dir ? dirs : files).push_back(c);
   remove_files_and_folders(removes);
   create_folders(dirs);
+  if (down_helper_ && bulk_down_on_ && !files.empty()) {
+    // big files come down on the bulk channel: the next pod-side changes do not wait for them
+    std::vector<FileInfo> small, big;
+    for (auto& f : files) (f.size >= kBulkFileBytes ? big : small).push_back(f);
+    if (!big.empty()) {
+      {
+        std::lock_guard<std::mutex> g(inflight_mu_);
+        for (auto& f : big) downloading_.insert(f.name);
+      }
+      {
+        std::lock_guard<std::mutex> g(q_mu_);
+        bulk_down_q_.push_back(std::move(big));
+      }
+      q_cv_.notify_all();
+    }
+    files.swap(small);
+  }
   if (!files.empty()) {
     // batch very long lists (argv limits in fast mode); every batch streams into the tree
     size_t step = mode_ != Mode::Compat && !down_helper_ ? 500 : files.size();
@@ -2106,6 +2202,10 @@ void Session::downstream_loop() {
 void Session::start_loops(bool upstream, bool downstream) {
   if (upstream) up_thread_ = std::thread([this] { upstream_loop(); });
   if (upstream) bulk_thread_ = std::thread([this] { bulk_loop(); });
+  if (downstream) {
+    bulk_down_on_ = true;
+    bulk_down_thread_ = std::thread([this] { bulk_down_loop(); });
+  }
   if (downstream) down_thread_ = std::thread([this] { downstream_loop(); });
 }
 
@@ -2126,12 +2226,27 @@ void Session::stop_loops() {
   if (up_shell_) up_shell_->terminate();
   if (down_shell_) down_shell_->terminate();
   {
+    // (bulk_down_mu_ may be held by a download for minutes: the pointer has a lock of its own)
+    std::lock_guard<std::mutex> g(bulk_down_ptr_mu_);
+    if (bulk_down_shell_) bulk_down_shell_->terminate();
+  }
+  {
     std::lock_guard<std::mutex> g(up_pmu_);
     up_pcv_.notify_all();
   }
   up_rcv_.notify_all();
   if (up_thread_.joinable() && up_thread_.get_id() != std::this_thread::get_id()) up_thread_.join();
   if (bulk_thread_.joinable() && bulk_thread_.get_id() != std::this_thread::get_id()) bulk_thread_.join();
+  if (bulk_down_thread_.joinable() && bulk_down_thread_.get_id() != std::this_thread::get_id())
+    bulk_down_thread_.join();
+  bulk_down_on_ = false;
+  {
+    std::lock_guard<std::mutex> g(bulk_down_ptr_mu_);
+    if (bulk_down_shell_) {
+      bulk_down_shell_->close();
+      bulk_down_shell_.reset();
+    }
+  }
   if (down_thread_.joinable() && down_thread_.get_id() != std::this_thread::get_id()) down_thread_.join();
   {
     // a reconnect starts over from an initial sync: nothing is in flight or queued for the bulk lane
@@ -2139,11 +2254,14 @@ void Session::stop_loops() {
     bulk_q_.clear();
     deferred_.clear();
     bulk_busy_ = false;
+    bulk_down_q_.clear();
+    bulk_down_busy_ = false;
   }
   {
     std::lock_guard<std::mutex> g(inflight_mu_);
     inflight_.clear();
     inflight_bulk_.clear();
+    downloading_.clear();
   }
   if (up_shell_) up_shell_->close();
   if (down_shell_) down_shell_->close();
@@ -2170,6 +2288,8 @@ void Session::supervise() {
   logf("[Sync] Start syncing");
   up_thread_ = std::thread([this] { upstream_loop(); });
   bulk_thread_ = std::thread([this] { bulk_loop(); });
+  bulk_down_on_ = true;
+  bulk_down_thread_ = std::thread([this] { bulk_down_loop(); });
   down_thread_ = std::thread([this, run_initial] {
     if (run_initial()) downstream_loop();
   });
@@ -2225,6 +2345,8 @@ void Session::supervise() {
     }
     up_thread_ = std::thread([this] { upstream_loop(); });
     bulk_thread_ = std::thread([this] { bulk_loop(); });
+    bulk_down_on_ = true;
+    bulk_down_thread_ = std::thread([this] { bulk_down_loop(); });
     down_thread_ = std::thread([this, run_initial] {
       if (run_initial()) downstream_loop();
     });

@@ -245,7 +245,24 @@ class Session {
   long probe_seq_ = 0;
   void apply_downstream(const std::vector<FileInfo>& creates, std::map<std::string, FileInfo>& removes);
   // Streams the files from the container straight into the local tree (no archive in memory).
-  void download_and_apply(const std::vector<FileInfo>& files);
+  // bulk: on the bulk download channel (its own exec session and helper), so pod-side changes
+  // keep flowing on the main channel while a multi-GB file comes down.
+  void download_and_apply(const std::vector<FileInfo>& files, bool bulk = false);
+  // Helper mode: files >= 4 MiB found by a scan are downloaded by bulk_down_loop on a second
+  // channel; the paths stay in downloading_ (skipped by later scans) until they are in.
+  void bulk_down_loop();
+  bool open_bulk_down_shell();
+  bool downloading(const std::string& rel);
+  void wait_bulk_down_idle();
+  std::unique_ptr<Shell> bulk_down_shell_;
+  LineReader bulk_down_out_;
+  std::mutex bulk_down_mu_;      // the bulk download channel (held across a download)
+  std::mutex bulk_down_ptr_mu_;  // bulk_down_shell_ itself (set, terminated, reset)
+  std::thread bulk_down_thread_;
+  std::atomic<bool> bulk_down_on_{false};  // bulk_down_thread_ runs: big downloads may go there
+  std::deque<std::vector<FileInfo>> bulk_down_q_;  // q_mu_
+  bool bulk_down_busy_ = false;                    // q_mu_
+  std::set<std::string> downloading_;              // inflight_mu_
   // Extracts a tar / tar.gz stream into the local folder, each file through a temp name and a
   // rename. leftover != nullptr: the stream continues after the archive (fast protocol) — a gzip
   // member is read exactly to its end and any bytes pulled past it are returned there.

@@ -203,3 +203,35 @@ def test_random_mix_of_edits_and_bulk_files_converges(tmp_path, mode, seed):
         assert s.running(), s.error()
     finally:
         s.stop()
+
+
+def test_pod_side_edits_come_back_while_a_big_file_downloads(tmp_path):
+    """A multi-hundred-MB file written in the pod comes down on the bulk download channel; a
+    small file the pod writes after it started downloading comes back at once, on the main one,
+    instead of after the big download."""
+    src, pod = tmp_path / "src", tmp_path / "pod"
+    src.mkdir()
+    pod.mkdir()
+    big = tmp_path / "big.bin"
+    with open(big, "wb") as f:
+        for _ in range(1024 // 16):
+            f.write(os.urandom(16 << 20))
+    s = _session(src, pod, tmp_path)
+    try:
+        os.link(big, pod / "ckpt.bin")
+        tmp = src / ("ckpt.bin" + ".devspace-tmp")
+        _wait(lambda: tmp.exists() and tmp.stat().st_size > (16 << 20), 60, "big download under way")
+        t0 = time.perf_counter()
+        (pod / "metrics.json").write_text('{"step": 2}\n')
+        _wait(lambda: _read(src / "metrics.json") == b'{"step": 2}\n', 30, "small pod-side change")
+        took_ms = (time.perf_counter() - t0) * 1000
+        big_still_coming = tmp.exists()
+        _wait(lambda: (src / "ckpt.bin").exists() and (src / "ckpt.bin").stat().st_size == big.stat().st_size, 300,
+              "big download done")
+        print(f"pod-side change came back in {took_ms:.1f} ms during a 1 GiB download")
+        assert big_still_coming, "the big download finished first: nothing was measured"
+        assert took_ms < 1000, took_ms
+        # and the big file is not fetched twice (the scans meanwhile left it alone)
+        assert s.stats()["bytes_down"] < 1.5 * big.stat().st_size, s.stats()
+    finally:
+        s.stop()

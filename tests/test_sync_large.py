@@ -218,7 +218,9 @@ def test_stream_killed_mid_transfer_resumes(mode, direction, tmp_path):
         # the first shell carries the uploads in both protocols
         fault = ["--fault-stdin-bytes", str(128 << 20), "--fault-shell", "1"]
     else:
-        fault = ["--fault-stdout-bytes", str(128 << 20), "--fault-shell", "2"]
+        # fast: the downstream shell (2nd) carries it; helper: a big file comes down on the
+        # bulk download channel, opened for it (3rd)
+        fault = ["--fault-stdout-bytes", str(128 << 20), "--fault-shell", "3" if mode == "helper" else "2"]
     p, log = _start_sync(tmp_path, src, pod, mode, *fault)
     try:
         if direction == "up":
