@@ -39,6 +39,9 @@ examples/quickstart/package.json:7, the redeploy loop of cmd/dev.go:225-234,284-
     waits for the next edit before starting again, as nodemon does ("app crashed - waiting for
     file changes"). A single rank pauses training after a failed step and resumes with the next
     edit (process, model and optimizer state stay).
+  * state survives a group restart: every --rescue-every seconds (60) the ranks snapshot their
+    training state into /dev/shm at one agreed step boundary; a restarted group resumes from the
+    newest step every rank holds instead of from scratch (`Rescue`).
 
 Preemptible steps: a step may call `ctx.preempt_point()` between its phases (e.g. between
 forward and backward). The point abandons the rest of the step when a newer version of the
@@ -59,7 +62,9 @@ import argparse
 import hashlib
 import importlib.machinery
 import importlib.util
+import mmap
 import os
+import re
 import signal
 import subprocess
 import sys
@@ -261,20 +266,24 @@ class Agreement:
             # without a trace) ends the group instead of hanging it (the supervisor restarts it)
             group = dist.new_group(backend="gloo", **({"timeout": timeout} if timeout is not None else {}))
         self.group = group
-        # [newest generation, helper modules changed, a rank was told to stop (SIGTERM)]
-        self.ctl = torch.zeros(3, dtype=torch.int64)
+        # [newest generation, helper modules changed, a rank was told to stop (SIGTERM),
+        #  a rescue snapshot is due (rank 0's timer)]
+        self.ctl = torch.zeros(4, dtype=torch.int64)
         self.flag = torch.zeros(1, dtype=torch.int64)
         self.calls = 0
+        self.snap = False  # the last boundary's agreed snapshot decision
 
-    def boundary(self, pending_gen: int, helper_pending: bool, stop: bool = False):
+    def boundary(self, pending_gen: int, helper_pending: bool, stop: bool = False, snap: bool = False):
         """(agreed generation, helper modules changed, stop): all ranks leave the loop at the
         same boundary when any of them got SIGTERM, so none is left waiting in a collective
-        of a step the others never start."""
+        of a step the others never start. The snapshot decision rides along (`self.snap`)."""
         self.ctl[0] = pending_gen
         self.ctl[1] = int(helper_pending)
         self.ctl[2] = int(stop)
+        self.ctl[3] = int(snap)
         self.dist.all_reduce(self.ctl, op=self.dist.ReduceOp.MAX, group=self.group)
         self.calls += 1
+        self.snap = bool(self.ctl[3])
         return int(self.ctl[0]), bool(self.ctl[1]), bool(self.ctl[2])
 
     def preempt(self, pending: bool) -> bool:
@@ -358,6 +367,224 @@ class Context:
             if feed is not None and feed.pending():
                 raise Preempted()
             time.sleep(0)  # releases the GIL: the change feed thread can post the edit
+
+
+def _close_mapping(mm) -> None:
+    try:
+        mm.close()
+    except BufferError:  # a tensor view still alive (an exception's frame): the GC closes it
+        pass
+
+
+class RescueSkipped(Exception):
+    """A snapshot that cannot be taken this time (not enough shared memory) or ever (the state
+    holds something that is not tensors, containers and scalars)."""
+
+
+class Rescue:
+    """Training state that survives a restart of the group.
+
+    The reference's restart-per-change model (nodemon, redeploy) starts every process from
+    nothing, which is right for a web app and ruinous for a training run: a rank failure an
+    hour in would cost the hour. Every `every_s` seconds (rank 0's clock, decided at a step
+    boundary for all ranks together) each rank copies its state into shared memory
+    (`rank<r>-step<N>.bin` raw tensor bytes + `.json` layout, written under temp names and
+    renamed); once every rank wrote step N the older snapshots are dropped. A group started
+    after a failure runs `setup()` and then loads the newest step that every rank holds, with
+    the same SETUP_VERSION; a restore that fails on any rank runs `setup()` again everywhere.
+
+    What is captured: a module's own `snapshot(ctx, state) -> obj` / `restore(ctx, state, obj)`
+    when it defines them; otherwise, of a dict state, every entry with `state_dict()` /
+    `load_state_dict()` (modules, DDP, optimizers, schedulers, grad scalers), plain tensors and
+    scalars. Tensors come back on the device they were on (cuda → this rank's GPU)."""
+
+    ALIGN = 64
+
+    def __init__(self, root: str, rank: int, every_s: float):
+        self.root = root
+        self.rank = rank
+        self.every_s = every_s
+        self.last = time.monotonic()
+        self.last_step = 0
+        self.disabled = None  # why snapshots stopped for good
+        os.makedirs(root, exist_ok=True)
+
+    # -- capture / apply ------------------------------------------------------------------
+    @staticmethod
+    def capture(mod, ctx, state):
+        import torch
+
+        if hasattr(mod, "snapshot"):
+            return mod.snapshot(ctx, state)
+        if not isinstance(state, dict):
+            return None
+        out = {}
+        for k, v in state.items():
+            if callable(getattr(v, "state_dict", None)) and callable(getattr(v, "load_state_dict", None)):
+                out[k] = v.state_dict()
+            elif isinstance(v, torch.Tensor) or v is None or isinstance(v, (bool, int, float, str)):
+                out[k] = v
+        return out or None
+
+    @staticmethod
+    def apply(mod, ctx, state, snap):
+        import torch
+
+        if hasattr(mod, "restore"):
+            r = mod.restore(ctx, state, snap)
+            return state if r is None else r
+        for k, v in snap.items():
+            cur = state.get(k)
+            if callable(getattr(cur, "load_state_dict", None)) and isinstance(v, dict):
+                cur.load_state_dict(v)
+            elif isinstance(cur, torch.Tensor) and isinstance(v, torch.Tensor):
+                if cur.shape != v.shape:
+                    raise ValueError(f"state[{k!r}]: shape {tuple(cur.shape)} now, {tuple(v.shape)} in the snapshot")
+                with torch.no_grad():
+                    cur.copy_(v)
+            elif k in state:
+                state[k] = v
+        return state
+
+    @classmethod
+    def _encode(cls, obj, tensors):
+        import torch
+
+        if isinstance(obj, torch.Tensor):
+            tensors.append(obj)
+            return {"T": len(tensors) - 1}
+        if isinstance(obj, dict):
+            return {"D": [[cls._encode(k, tensors), cls._encode(v, tensors)] for k, v in obj.items()]}
+        if isinstance(obj, tuple):
+            return {"U": [cls._encode(v, tensors) for v in obj]}
+        if isinstance(obj, list):
+            return [cls._encode(v, tensors) for v in obj]
+        if obj is None or isinstance(obj, (bool, int, float, str)):
+            return obj
+        raise RescueSkipped(f"cannot snapshot a {type(obj).__name__} (define snapshot()/restore())")
+
+    @classmethod
+    def _decode(cls, obj, tensors):
+        if isinstance(obj, list):
+            return [cls._decode(v, tensors) for v in obj]
+        if isinstance(obj, dict):
+            if "T" in obj:
+                return tensors[obj["T"]]
+            if "U" in obj:
+                return tuple(cls._decode(v, tensors) for v in obj["U"])
+            return {cls._decode(k, tensors): cls._decode(v, tensors) for k, v in obj["D"]}
+        return obj
+
+    # -- files -----------------------------------------------------------------------------
+    def _path(self, step, ext, rank=None):
+        return os.path.join(self.root, f"rank{self.rank if rank is None else rank}-step{step}.{ext}")
+
+    def due(self, step: int) -> bool:
+        return (self.every_s > 0 and self.disabled is None and step > self.last_step
+                and time.monotonic() - self.last >= self.every_s)
+
+    def save(self, mod, ctx, state, gen, setup_version) -> int:
+        """Writes this rank's snapshot of `state` at ctx.step; returns the bytes written."""
+        import json
+        import shutil
+
+        import torch
+
+        tensors = []
+        tree = self._encode(self.capture(mod, ctx, state), tensors)
+        metas, off = [], 0
+        for t in tensors:
+            n = t.numel() * t.element_size()
+            metas.append({"dtype": str(t.dtype).replace("torch.", ""), "shape": list(t.shape),
+                          "device": t.device.type, "offset": off, "nbytes": n})
+            off += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        free = shutil.disk_usage(self.root).free
+        if off > free * 0.9:
+            raise RescueSkipped(f"{self.root} has {free >> 20} MiB free, the snapshot needs {off >> 20} MiB")
+        step = ctx.step
+        binp, jsp = self._path(step, "bin"), self._path(step, "json")
+        with open(binp + ".tmp", "w+b") as f:
+            f.truncate(off)
+            if off:
+                # one copy per tensor, device (or host) straight into the mapped shared memory
+                mm = mmap.mmap(f.fileno(), off)
+                try:
+                    buf = torch.frombuffer(mm, dtype=torch.uint8)
+                    for t, m in zip(tensors, metas):
+                        if m["nbytes"]:
+                            buf[m["offset"]:m["offset"] + m["nbytes"]].view(t.dtype).view(t.shape).copy_(t.detach())
+                    del buf
+                finally:
+                    _close_mapping(mm)
+        meta = {"step": step, "gen": gen, "setup_version": setup_version, "world": ctx.world_size,
+                "time": time.time(), "bytes": off, "tensors": metas, "tree": tree}
+        with open(jsp + ".tmp", "w") as f:
+            json.dump(meta, f)
+        os.replace(binp + ".tmp", binp)
+        os.replace(jsp + ".tmp", jsp)  # the layout last: its presence commits the snapshot
+        return off
+
+    def commit(self, step: int, ok: bool) -> None:
+        """Every rank wrote `step` (ok): drop the older snapshots; else drop this one."""
+        for name in os.listdir(self.root):
+            m = re.match(rf"rank{self.rank}-step(\d+)\.(bin|json)(\.tmp)?$", name)
+            if m and (int(m.group(1)) != step if ok else int(m.group(1)) == step):
+                try:
+                    os.unlink(os.path.join(self.root, name))
+                except OSError:
+                    pass
+        if ok:
+            self.last_step = step
+        self.last = time.monotonic()
+
+    def available(self, setup_version, world) -> list:
+        import json
+
+        steps = []
+        for name in os.listdir(self.root):
+            m = re.match(rf"rank{self.rank}-step(\d+)\.json$", name)
+            if not m:
+                continue
+            try:
+                with open(os.path.join(self.root, name)) as f:
+                    meta = json.load(f)
+                size = os.path.getsize(self._path(int(m.group(1)), "bin"))
+            except (OSError, ValueError):
+                continue
+            if meta.get("setup_version") == setup_version and meta.get("world") == world and size == meta["bytes"]:
+                steps.append(int(m.group(1)))
+        return sorted(steps)
+
+    def load(self, step, device):
+        """(state tree with tensors materialised, metadata) of this rank's snapshot `step`."""
+        import json
+
+        import torch
+
+        with open(self._path(step, "json")) as f:
+            meta = json.load(f)
+        tensors = []
+        with open(self._path(step, "bin"), "rb") as f:
+            if os.fstat(f.fileno()).st_size != meta["bytes"]:
+                raise ValueError(f"snapshot step={step} is truncated")
+            mm = mmap.mmap(f.fileno(), meta["bytes"], access=mmap.ACCESS_COPY) if meta["bytes"] else None
+            try:
+                buf = torch.frombuffer(mm, dtype=torch.uint8) if mm is not None else None
+                for m in meta["tensors"]:
+                    dtype = getattr(torch, m["dtype"])
+                    if not m["nbytes"]:
+                        tensors.append(torch.empty(m["shape"], dtype=dtype))
+                        continue
+                    src = buf[m["offset"]:m["offset"] + m["nbytes"]].view(dtype).view(m["shape"])
+                    # own memory either way (the mapping is closed below)
+                    on_gpu = m["device"] == "cuda" and device.type == "cuda"
+                    tensors.append(src.to(device) if on_gpu else src.clone())
+                    del src
+                del buf
+            finally:
+                if mm is not None:
+                    _close_mapping(mm)
+        return self._decode(meta["tree"], tensors), meta
 
 
 def purge_user_modules(watch_dir: str) -> list:
@@ -662,10 +889,66 @@ class ChangeFeed:
 SYNC_TMP_SUFFIX = ".devspace-tmp"
 
 
+_IGNORED_DIRS = []  # what the runner itself writes under the watched tree (a --rescue-dir there)
+
+
 def _ignored(p: str) -> bool:
     base = os.path.basename(p)
     return ("__pycache__" in p or base.endswith((".pyc", ".swp", "~", SYNC_TMP_SUFFIX)) or
-            base.startswith(".#"))
+            base.startswith(".#") or any(p == d or p.startswith(d + os.sep) for d in _IGNORED_DIRS))
+
+
+def _rescue_take(rescue, agree, mod, ctx, state, gen, setup_version) -> None:
+    """Every rank writes its snapshot at this boundary; all learn every rank's outcome, so they
+    commit (drop older snapshots) or give up together."""
+    t0 = time.perf_counter()
+    err, nbytes = None, 0
+    try:
+        nbytes = rescue.save(mod, ctx, state, gen, setup_version)
+    except Exception as e:  # RescueSkipped, OSError (shared memory full), a device error
+        err = f"{type(e).__name__}: {e}" if not isinstance(e, RescueSkipped) else str(e)
+    results = agree.gather(err) if agree is not None else [err]
+    bad = [(r, e) for r, e in enumerate(results) if e is not None]
+    rescue.commit(ctx.step, not bad)
+    if bad:
+        rescue.disabled = bad[0][1]
+        ctx.log(f"rescue snapshots off (rank {bad[0][0]}: {bad[0][1]})")
+        return
+    ctx.log(f"rescue snapshot step={ctx.step} gen={gen} {nbytes / 2**20:.1f} MiB/rank "
+            f"in {(time.perf_counter() - t0) * 1000.0:.1f} ms")
+
+
+def _rescue_restore(rescue, agree, mod, ctx, state):
+    """After setup() of a (re)started group: the newest snapshot every rank holds for this
+    SETUP_VERSION, loaded on every rank, or none at all."""
+    setup_version = getattr(mod, "SETUP_VERSION", None)
+    steps = rescue.available(setup_version, ctx.world_size)
+    held = agree.gather(steps) if agree is not None else [steps]
+    common = set(held[0]).intersection(*[set(h) for h in held[1:]])
+    if not common:
+        if any(held):
+            ctx.log("rescue: no snapshot that every rank holds for this SETUP_VERSION: starting from setup()")
+        return state
+    step = max(common)
+    t0 = time.perf_counter()
+    err, meta = None, None
+    try:
+        snap, meta = rescue.load(step, ctx.device)
+        state = rescue.apply(mod, ctx, state, snap)
+    except Exception as e:
+        err = f"{type(e).__name__}: {e}"
+    errs = agree.gather(err) if agree is not None else [err]
+    bad = [(r, e) for r, e in enumerate(errs) if e is not None]
+    if bad:
+        # some ranks may hold half-restored state: every rank starts over from setup()
+        ctx.log(f"rescue: snapshot step={step} did not restore on rank {bad[0][0]} ({bad[0][1]}): "
+                f"starting from setup()")
+        return mod.setup(ctx)
+    ctx.step = step
+    rescue.last_step, rescue.last = step, time.monotonic()
+    ctx.log(f"restored step={step} gen={meta['gen']} from the rescue snapshot (age {time.time() - meta['time']:.1f} s, "
+            f"{meta['bytes'] / 2**20:.1f} MiB/rank in {(time.perf_counter() - t0) * 1000.0:.1f} ms)")
+    return state
 
 
 def worker_main(args) -> int:
@@ -714,6 +997,12 @@ def worker_main(args) -> int:
     fault = overlay.fault = _FaultHooks(os.environ.get("DEVSPACE_RUNNER_FAULT"), rank)
     # control plane of the group (gloo, CPU tensors): generation, preemption, code agreement
     agree = Agreement(dist, timeout=group_timeout) if world > 1 else None
+    # the supervisor of a group hands down a shared-memory directory; one rank alone keeps
+    # snapshots only where --rescue-dir says (e.g. a pod volume that outlives the container)
+    rescue_dir = os.environ.get("DEVSPACE_RESCUE_DIR") or args.rescue_dir
+    rescue = Rescue(rescue_dir, rank, args.rescue_every) if rescue_dir and args.rescue_every > 0 else None
+    if rescue is not None:
+        _IGNORED_DIRS.append(os.path.abspath(rescue_dir))
     stop = False
 
     def _term(*_):
@@ -741,6 +1030,8 @@ def worker_main(args) -> int:
             try:
                 mod = _load_generation(entry, gen, None, overlay, agree, False, watch_dir, ctx, fault)
                 state = mod.setup(ctx) if hasattr(mod, "setup") else None
+                if rescue is not None and state is not None and hasattr(mod, "step"):
+                    state = _rescue_restore(rescue, agree, mod, ctx, state)
                 if hasattr(mod, "step"):
                     first = mod.step(ctx, state) or {}
                     ctx.step += 1
@@ -803,8 +1094,11 @@ def worker_main(args) -> int:
             # 2. ranks agree on the newest generation (keeps collectives in `step` matched) and on
             #    whether helper modules must be re-imported (rank 0's view, like the generation)
             target = pending_gen
+            snap = (rescue is not None and (agree is None or rank == 0) and not paused and not script_mode
+                    and rescue.due(ctx.step))
             if agree is not None:
-                target, agreed_helper, agreed_stop = agree.boundary(pending_gen, helper_pending, stop)
+                target, agreed_helper, agreed_stop = agree.boundary(pending_gen, helper_pending, stop, snap)
+                snap = agree.snap
                 if agreed_stop:
                     break
                 pending_gen = max(pending_gen, target)
@@ -875,6 +1169,8 @@ def worker_main(args) -> int:
                 )
                 t_iter = time.perf_counter()
                 continue
+            if snap and state is not None:
+                _rescue_take(rescue, agree, mod, ctx, state, gen, setup_version)
             if script_mode or not args.train or paused:
                 continue
             try:
@@ -1062,6 +1358,13 @@ class _GroupWatch:
                 return ("done", codes)
 
 
+def _default_rescue_dir() -> str:
+    import tempfile
+
+    base = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
+    return os.path.join(base, f"devspace-rescue-{os.getpid()}")
+
+
 def _wait_for_change(watcher, already=False):
     """nodemon's "app crashed - waiting for file changes before starting": block until the synced
     tree changes (a settled write, not a temp file)."""
@@ -1088,6 +1391,11 @@ def supervisor_main(args) -> int:
     watcher = make_watcher(watch_dir)
     port = args.port or _free_port()
     restarts = 0  # restarts since the last edit
+    # the ranks' rescue snapshots live as long as this supervisor (a restarted group resumes
+    # from them); in /dev/shm: the pod's memory-backed volume, sized per GPU by the chart
+    rescue_dir = args.rescue_dir or _default_rescue_dir()
+    os.environ["DEVSPACE_RESCUE_DIR"] = rescue_dir
+    _IGNORED_DIRS.append(os.path.abspath(rescue_dir))
 
     def _term(*_):
         raise KeyboardInterrupt
@@ -1129,6 +1437,10 @@ def supervisor_main(args) -> int:
         return 130
     finally:
         watcher.close()
+        if not args.rescue_dir:
+            import shutil
+
+            shutil.rmtree(rescue_dir, ignore_errors=True)
 
 
 def _forward(args):
@@ -1138,7 +1450,8 @@ def _forward(args):
         out.append("--no-train")
     if not args.preempt:
         out.append("--no-preempt")
-    out += ["--preempt-drain-ms", str(args.preempt_drain_ms), "--group-timeout", str(args.group_timeout)]
+    out += ["--preempt-drain-ms", str(args.preempt_drain_ms), "--group-timeout", str(args.group_timeout),
+            "--rescue-every", str(args.rescue_every)]
     return out + [args.entry]
 
 
@@ -1166,6 +1479,12 @@ def parse_args(argv=None):
     p.add_argument("--gemm-tuning", default=os.environ.get("DEVSPACE_GEMM_TUNING", "off"),
                    choices=("off", "shipped", "online"),
                    help="TunableOp GEMM selection (devspace_amd/ops/gemm_tuning.py)")
+    p.add_argument("--rescue-every", type=float, default=float(os.environ.get("DEVSPACE_RESCUE_EVERY_S", "60")),
+                   help="seconds between snapshots of the training state in shared memory, from which a "
+                        "group restarted after a failure resumes (0: off)")
+    p.add_argument("--rescue-dir", default="",
+                   help="keep the snapshots here (kept after exit; with one rank, snapshots are taken "
+                        "only when this is set)")
     p.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args(argv)
 

@@ -182,6 +182,11 @@ ENV = {
     "DEVSPACE_GEMM_TUNING_MS": "Time budget per shape of `online` GEMM tuning (default 30).",
     "DEVSPACE_GROUP_TIMEOUT_S": "Seconds a collective of the runner's ranks may wait for every rank (default 600): a "
                                 "rank stuck in a step ends the group, which is restarted (`--group-timeout`).",
+    "DEVSPACE_RESCUE_DIR": "Set by the runner's supervisor for its ranks: the shared-memory directory of their "
+                           "rescue snapshots (removed when the supervisor exits).",
+    "DEVSPACE_RESCUE_EVERY_S": "Seconds between the runner's snapshots of the training state in /dev/shm (default "
+                               "60, 0 = off): a group restarted after a failure resumes from the newest one "
+                               "(`--rescue-every`).",
     "DEVSPACE_RUNNER_DEBUG": "`1`: every runner rank logs the code digest it loaded for each generation.",
     "DEVSPACE_RUNNER_FAULT": "Test-only fault injection of the runner (`mutate-entry-after-read`, `skew-helper`): "
                              "edits racing the ranks' reads, to exercise the code agreement.",

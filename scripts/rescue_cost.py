@@ -1,0 +1,110 @@
+"""What the runner's rescue snapshots cost on the flagship example, and what they save.
+
+Runs examples/rocm-pytorch/train.py (TinyLM, model + AdamW in HBM) under the hot-reload runner
+with --rescue-dir and a short --rescue-every, kills the process outright (SIGKILL, as an OOM kill
+or a GPU fault would) after a few snapshots, starts it again and reads back:
+  * snapshot size per rank and the time each snapshot stopped training for,
+  * the restore time and the step the new process resumed from (instead of step 0),
+  * the steady-state step period with snapshots on.
+Prints one JSON line.
+
+    python scripts/rescue_cost.py [--every 2] [--snapshots 3]
+"""
+
+import argparse
+import json
+import os
+import queue
+import re
+import shutil
+import signal
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class Proc:
+    def __init__(self, cmd, env, cwd):
+        self.p = subprocess.Popen(cmd, env=env, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                                  start_new_session=True)
+        self.q = queue.Queue()
+        self.lines = []
+        threading.Thread(target=lambda: [self.q.put(l) for l in self.p.stdout], daemon=True).start()
+
+    def until(self, pat, timeout):
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            try:
+                line = self.q.get(timeout=max(0.01, deadline - time.monotonic()))
+            except queue.Empty:
+                break
+            self.lines.append(line)
+            sys.stderr.write(line)
+            m = re.search(pat, line)
+            if m:
+                return m
+        raise TimeoutError(f"no {pat!r} in {timeout}s:\n" + "".join(self.lines[-30:]))
+
+    def kill(self):
+        if self.p.poll() is None:
+            os.killpg(self.p.pid, signal.SIGKILL)
+        self.p.wait()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--every", type=float, default=2.0)
+    ap.add_argument("--snapshots", type=int, default=3)
+    args = ap.parse_args()
+    work = tempfile.mkdtemp(prefix="rescue-cost-")
+    try:
+        app = os.path.join(work, "app")
+        shutil.copytree(os.path.join(ROOT, "examples", "rocm-pytorch"), app,
+                        ignore=shutil.ignore_patterns("devspace_amd", "__pycache__"))
+        keep = os.path.join(work, "rescue")
+        env = dict(os.environ, PYTHONPATH=ROOT)
+        cmd = [sys.executable, "-u", "-m", "devspace_amd.runner", "--watch", app, "--log-every", "5",
+               "--rescue-every", str(args.every), "--rescue-dir", keep, os.path.join(app, "train.py")]
+        first = Proc(cmd, env, app)
+        snaps = []
+        try:
+            first.until(r"started gen=1 ", 300)
+            for _ in range(args.snapshots):
+                m = first.until(r"rescue snapshot step=(\d+) gen=\d+ ([\d.]+) MiB/rank in ([\d.]+) ms", 120)
+                snaps.append({"step": int(m.group(1)), "mib": float(m.group(2)), "ms": float(m.group(3))})
+            period = first.until(r"step=\d+ gen=\d+ loss=(\S+) period_ms=([\d.]+)", 120)
+        finally:
+            first.kill()
+        second = Proc(cmd, env, app)
+        try:
+            m = second.until(r"restored step=(\d+) gen=\d+ from the rescue snapshot \(age ([\d.]+) s, "
+                             r"([\d.]+) MiB/rank in ([\d.]+) ms\)", 300)
+            restored = {"step": int(m.group(1)), "age_s": float(m.group(2)), "mib": float(m.group(3)),
+                        "ms": float(m.group(4))}
+            started = second.until(r"started gen=1 .*loss=(\S+) startup_ms=([\d.]+)", 120)
+        finally:
+            second.kill()
+        out = {
+            "what": "examples/rocm-pytorch TinyLM under the runner: rescue snapshots every "
+                    f"{args.every:g} s, SIGKILL, restart with the same --rescue-dir",
+            "snapshots": snaps,
+            "snapshot_ms_p50": sorted(s["ms"] for s in snaps)[len(snaps) // 2],
+            "step_period_ms": float(period.group(2)),
+            "cost_at_default_interval_pct": round(100.0 * sorted(s["ms"] for s in snaps)[len(snaps) // 2] / 60000.0, 4),
+            "loss_before_kill": period.group(1),
+            "restored": restored,
+            "resumed_from_step": restored["step"],
+            "restart_startup_ms": float(started.group(2)),
+            "first_loss_after_restart": started.group(1),
+        }
+        print(json.dumps(out))
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()

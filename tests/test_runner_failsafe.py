@@ -442,3 +442,140 @@ def step(ctx, state):
         assert n_before > 1, line  # the state survived the failure
     finally:
         r.stop()
+
+
+RESCUE_STEP = '''
+import time
+
+import torch
+import torch.distributed as dist
+
+MARKER = "v0"
+SETUP_VERSION = 1
+
+
+def setup(ctx):
+    torch.manual_seed(0)
+    model = torch.nn.Linear(16, 1)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+    return {"model": model, "opt": opt, "n": 0, "seen": torch.zeros(2)}
+
+
+def step(ctx, state):
+    if MARKER == "bad" and ctx.rank == 1:
+        raise RuntimeError("rank-local failure on rank 1")
+    model, opt = state["model"], state["opt"]
+    loss = model(torch.ones(4, 16)).pow(2).mean()
+    opt.zero_grad()
+    loss.backward()
+    if ctx.distributed:
+        for p in model.parameters():
+            dist.all_reduce(p.grad)
+    opt.step()
+    state["n"] += 1
+    state["seen"] += 1
+    time.sleep(0.005)
+    # the optimizer's own step count, a plain tensor and a python int must agree after a restore
+    p0 = next(iter(model.parameters()))
+    same = int(opt.state[p0]["step"]) == state["n"] == int(state["seen"][0])
+    return {"loss": state["n"] if same else -state["n"]}
+'''
+
+
+def _rescue_files(d):
+    return sorted(os.listdir(d)) if os.path.isdir(d) else []
+
+
+def test_restarted_group_resumes_from_the_rescue_snapshot(tmp_path):
+    """A rank failure restarts the group from fresh processes; the restarted group resumes from
+    the newest step every rank snapshotted (model, optimizer, tensors, ints) instead of step 0,
+    and only that one snapshot per rank stays in shared memory."""
+    entry = tmp_path / "train.py"
+    entry.write_text(RESCUE_STEP)
+    r = Runner(tmp_path, entry, 2, extra_args=("--log-every", "20", "--rescue-every", "0.5"))
+    rescue_dir = f"/dev/shm/devspace-rescue-{r.proc.pid}"
+    try:
+        r.until(r"started gen=1 marker=v0 .*world=2", timeout=180)
+        r.until(r"rescue snapshot step=\d+ gen=1 ")
+        _, line = r.until(r"rescue snapshot step=\d+ gen=1 ")
+        files = _rescue_files(rescue_dir)
+        assert len(files) == 4 and all(re.match(r"rank[01]-step\d+\.(bin|json)$", f) for f in files), files
+        _set_marker(entry, "bad")
+        r.seen(r"rank=1 exited with code 3: restarting the group")
+        snapped = max(int(s) for s in re.findall(r"rescue snapshot step=(\d+)", r.text()))
+        _, line = r.until(r"restored step=\d+ gen=\d+ from the rescue snapshot", timeout=120)
+        assert int(re.search(r"restored step=(\d+)", line).group(1)) == snapped, line
+        r.until(r"waiting for a file change before starting the group again", timeout=120)
+        _set_marker(entry, "fixed")
+        _, line = r.until(r"started gen=1 marker=fixed .*world=2", timeout=60)
+        assert f"loss={snapped + 1} " in line, (snapped, line)  # one step on from the snapshot
+        _, line = r.until(r"step=\d+ gen=1 ", timeout=30)
+        n = int(re.search(r"loss=(-?\d+)", line).group(1))
+        assert n > snapped + 1, line
+    finally:
+        r.stop()
+    assert not os.path.exists(rescue_dir)  # the supervisor's snapshots go with it
+
+
+def test_single_rank_resumes_after_a_hard_crash_with_a_rescue_dir(tmp_path):
+    """One rank with --rescue-dir (a pod volume that outlives the container): a process killed
+    outright (OOM kill, segfault) comes back in a new process from its last snapshot; a changed
+    SETUP_VERSION starts from setup() instead."""
+    entry = tmp_path / "train.py"
+    entry.write_text(RESCUE_STEP)
+    keep = tmp_path / "rescue"
+    args = ("--log-every", "20", "--rescue-every", "0.3", "--rescue-dir", str(keep))
+    r = Runner(tmp_path, entry, 1, extra_args=args)
+    try:
+        r.until(r"started gen=1 marker=v0", timeout=180)
+        r.until(r"rescue snapshot step=\d+ gen=1 ")
+        _, line = r.until(r"rescue snapshot step=\d+ gen=1 ")
+        snapped = int(re.search(r"step=(\d+)", line).group(1))
+        r.proc.kill()
+        r.proc.wait()
+    finally:
+        r.stop()
+    assert len(_rescue_files(keep)) == 2, _rescue_files(keep)
+    r = Runner(tmp_path, entry, 1, extra_args=args)
+    try:
+        r.until(rf"restored step={snapped} ", timeout=180)
+        _, line = r.until(r"started gen=1 marker=v0", timeout=60)
+        assert f"loss={snapped + 1} " in line, line
+    finally:
+        r.stop()
+    entry.write_text(RESCUE_STEP.replace("SETUP_VERSION = 1", "SETUP_VERSION = 2"))
+    r = Runner(tmp_path, entry, 1, extra_args=args)
+    try:
+        _, line = r.until(r"started gen=1 marker=v0", timeout=180)
+        assert "loss=1 " in line and "restored" not in r.text(), r.text()
+    finally:
+        r.stop()
+
+
+RESCUE_STEP_GPU = (RESCUE_STEP.replace("torch.nn.Linear(16, 1)", "torch.nn.Linear(16, 1).to(ctx.device)")
+                   .replace("torch.ones(4, 16)", "torch.ones(4, 16, device=ctx.device)")
+                   .replace("torch.zeros(2)", "torch.zeros(2, device=ctx.device)"))
+
+
+@pytest.mark.gpu
+def test_restarted_group_resumes_from_the_rescue_snapshot_on_the_gpu(tmp_path):
+    """The same resume with model, optimizer and tensors in HBM: the snapshot copies them out of
+    the device, the restarted group's fresh processes put them back on the MI355X."""
+    entry = tmp_path / "train.py"
+    entry.write_text(RESCUE_STEP_GPU)
+    r = Runner(tmp_path, entry, 2, extra_args=("--log-every", "20", "--rescue-every", "0.5"),
+               extra_env={"DEVSPACE_DIST_BACKEND": "gloo"}, gpu=True)
+    try:
+        r.until(r"started gen=1 marker=v0 .*world=2 device=cuda", timeout=240)
+        _, line = r.until(r"rescue snapshot step=\d+ gen=1 ", timeout=60)
+        _set_marker(entry, "bad")
+        r.seen(r"rank=1 exited with code 3: restarting the group", timeout=60)
+        snapped = max(int(s) for s in re.findall(r"rescue snapshot step=(\d+)", r.text()))
+        _, line = r.until(r"restored step=\d+ ", timeout=180)
+        assert int(re.search(r"restored step=(\d+)", line).group(1)) == snapped, line
+        r.until(r"waiting for a file change before starting the group again", timeout=180)
+        _set_marker(entry, "fixed")
+        _, line = r.until(r"started gen=1 marker=fixed .*device=cuda", timeout=120)
+        assert f"loss={snapped + 1} " in line, (snapped, line)
+    finally:
+        r.stop()
