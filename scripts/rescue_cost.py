@@ -3,7 +3,8 @@
 Runs examples/rocm-pytorch/train.py (TinyLM, model + AdamW in HBM) under the hot-reload runner
 with --rescue-dir and a short --rescue-every, kills the process outright (SIGKILL, as an OOM kill
 or a GPU fault would) after a few snapshots, starts it again and reads back:
-  * snapshot size per rank and the time each snapshot stopped training for,
+  * snapshot size per rank, the time each snapshot paused training for and the time its
+    (background) write to shared memory took,
   * the restore time and the step the new process resumed from (instead of step 0),
   * the steady-state step period with snapshots on.
 Prints one JSON line.
@@ -74,8 +75,10 @@ def main():
         try:
             first.until(r"started gen=1 ", 300)
             for _ in range(args.snapshots):
-                m = first.until(r"rescue snapshot step=(\d+) gen=\d+ ([\d.]+) MiB/rank in ([\d.]+) ms", 120)
-                snaps.append({"step": int(m.group(1)), "mib": float(m.group(2)), "ms": float(m.group(3))})
+                m = first.until(r"rescue snapshot step=(\d+) gen=\d+ ([\d.]+) MiB/rank: training paused ([\d.]+) ms, "
+                                r"(.*) in ([\d.]+) ms", 120)
+                snaps.append({"step": int(m.group(1)), "mib": float(m.group(2)), "pause_ms": float(m.group(3)),
+                              "how": m.group(4), "write_ms": float(m.group(5))})
             period = first.until(r"step=\d+ gen=\d+ loss=(\S+) period_ms=([\d.]+)", 120)
         finally:
             first.kill()
@@ -92,9 +95,11 @@ def main():
             "what": "examples/rocm-pytorch TinyLM under the runner: rescue snapshots every "
                     f"{args.every:g} s, SIGKILL, restart with the same --rescue-dir",
             "snapshots": snaps,
-            "snapshot_ms_p50": sorted(s["ms"] for s in snaps)[len(snaps) // 2],
+            "pause_ms_p50": sorted(s["pause_ms"] for s in snaps)[len(snaps) // 2],
+            "write_ms_p50": sorted(s["write_ms"] for s in snaps)[len(snaps) // 2],
             "step_period_ms": float(period.group(2)),
-            "cost_at_default_interval_pct": round(100.0 * sorted(s["ms"] for s in snaps)[len(snaps) // 2] / 60000.0, 4),
+            "pause_at_default_interval_pct": round(100.0 * sorted(s["pause_ms"] for s in snaps)[len(snaps) // 2] / 60000.0,
+                                                   5),
             "loss_before_kill": period.group(1),
             "restored": restored,
             "resumed_from_step": restored["step"],

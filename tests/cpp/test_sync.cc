@@ -694,3 +694,54 @@ TEST(sync_helper_lanes_concurrent_uploads) {
   EXPECT_TRUE(s.running());
   s.stop();
 }
+
+// Helper-mode bulk download channel under concurrency (TSan covers this in scripts/sanitize.sh):
+// a big pod-side file comes down on its own channel while small pod-side writes keep arriving on
+// the main one and a local edit goes up; a stop in the middle of a second big download ends
+// cleanly (the channel's shell and thread are torn down with the session).
+TEST(sync_helper_bulk_download_channel) {
+  log::logdir() = fs::make_temp_dir("synclogs-");
+  Dirs d;
+  if (d.dest != d.remote) return;  // local-shell transport only (no kube target needed)
+  Options o = base_options(d, Mode::Helper);
+  Session s(o, std::make_shared<LocalShellTransport>());
+  s.start();
+  EXPECT_TRUE(s.wait_initial_sync(15000));
+  EXPECT_TRUE(s.effective_mode() == Mode::Helper);
+  auto noise = [](size_t n, uint64_t x) {
+    std::string b(n, '\0');
+    for (size_t i = 0; i < b.size(); i += 8) {
+      x ^= x << 13;
+      x ^= x >> 7;
+      x ^= x << 17;
+      std::memcpy(&b[i], &x, 8);
+    }
+    return b;
+  };
+  std::string big = noise(40u << 20, 0x9e3779b97f4a7c15ull);
+  fs::write_file(fs::join(d.remote, "ckpt.bin.partial"), big);
+  ::rename(fs::join(d.remote, "ckpt.bin.partial").c_str(), fs::join(d.remote, "ckpt.bin").c_str());
+  for (int i = 0; i < 10; ++i) {
+    fs::write_file(fs::join(d.remote, "metrics.json"), "{\"step\": " + std::to_string(i) + "}\n");
+    if (i == 3) fs::write_file(fs::join(d.local, "edit.py"), "v = 1\n");
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  auto waited = [&] { return std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60); };
+  std::string got;
+  while (waited() && !(fs::read_file(fs::join(d.local, "ckpt.bin"), &got) && got.size() == big.size()))
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  EXPECT_TRUE(got == big);
+  while (waited() && !(fs::read_file(fs::join(d.local, "metrics.json"), &got) && got == "{\"step\": 9}\n"))
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  EXPECT_EQ(got, std::string("{\"step\": 9}\n"));
+  while (waited() && !(fs::read_file(fs::join(d.remote, "edit.py"), &got) && got == "v = 1\n"))
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  EXPECT_EQ(got, std::string("v = 1\n"));
+  EXPECT_TRUE(s.running());
+  // a second big file, and stop while it may still be coming down
+  fs::write_file(fs::join(d.remote, "ckpt2.bin"), noise(24u << 20, 0x2545f4914f6cdd1dull));
+  std::this_thread::sleep_for(std::chrono::milliseconds(150));
+  s.stop();
+  EXPECT_TRUE(!s.running());
+}
