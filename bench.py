@@ -308,6 +308,8 @@ def _http_get(port, timeout=2.0):
         c.close()
 
 
+WAN = (30, 100)  # rtt ms, Mbit/s: the WAN extra's link
+
 QS_GREETING = re.compile(r"res\.end\('[^']*' \+")
 
 
@@ -320,7 +322,7 @@ def _qs_edit(path, marker):
 
 
 def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=False, timed_start=None,
-                    timed_end=None, cold=None):
+                    timed_end=None, cold=None, wan=None):
     """examples/quickstart edit -> reload, the way its README runs the dev loop: `devspace dev`
     (sync + port-forward) with the container running `npm run dev` (watch.js restarts node on
     change, as nodemon does in the reference's quickstart). One sample = edit index.js locally ->
@@ -332,6 +334,7 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
 
     cold = reference if cold is None else cold  # cold restarts: nodemon's (no standby pool)
     tag = ("ref-" if reference else "") + ("cold-" if cold and not reference else "") + (sync_mode or "default")
+    tag += "-wan" if wan else ""
     base = os.path.join(workdir, f"qs-bench-{tag}")
     proj = os.path.join(base, "quickstart")
     shutil.copytree(os.path.join(ROOT, "examples", "quickstart"), proj, symlinks=True)
@@ -349,9 +352,14 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
     open(values, "w").write(yaml.safe_dump(v))
 
     cluster = LocalCluster(os.path.join(base, "cluster"), gpus=0, tls=tls).start()
-    dev = None
+    dev = link = None
     try:
         env = devspace_env(cluster, base)
+        if wan:  # the cluster behind a WAN link: every API request, exec and forward pays it
+            from devspace_amd.localkube.netem import ShapedLink, point_kubeconfig
+
+            link = ShapedLink(("127.0.0.1", cluster.port), rtt_ms=wan[0], mbit=wan[1]).start()
+            point_kubeconfig(env["KUBECONFIG"], cluster.server, link.url("https" if tls else "http"))
         if sync_mode:
             env["DEVSPACE_SYNC_MODE"] = sync_mode
         if reference:
@@ -399,9 +407,14 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
                 sync_samples.append((t_sync - t0) * 1000.0)
         if timed_end:
             timed_end()
-        return {"reload_ms": samples, "sync_ms": sync_samples, "dev_start_s": dev_start_s}
+        out = {"reload_ms": samples, "sync_ms": sync_samples, "dev_start_s": dev_start_s}
+        if link is not None:
+            out["link"] = {"connections": link.connections}
+        return out
     finally:
         _killpg(dev)
+        if link is not None:
+            link.stop()
         cluster.stop()
 
 
@@ -712,6 +725,11 @@ def main():
                 extra("qs_pool", lambda: quickstart_loop(workdir, max(args.ref_steps, 10), 1, tls=tls, cold=False))
                 extra("qs_ref", lambda: quickstart_loop(workdir, args.ref_steps, 1, sync_mode="compat", tls=tls,
                                                         reference=True))
+                # the same loops with the cluster 30 ms / 100 Mbit/s away (a laptop and a cloud
+                # cluster): round trips per edit and per connection, not loopback, decide here
+                extra("qs_wan", lambda: quickstart_loop(workdir, max(args.ref_steps, 5), 1, tls=tls, cold=True, wan=WAN))
+                extra("qs_wan_ref", lambda: quickstart_loop(workdir, args.ref_steps, 1, sync_mode="compat", tls=tls,
+                                                            reference=True, wan=WAN))
             if args.gpu_steps > 0:
                 extra("gpu_pod", lambda: dev_loop(workdir, nproc, gpus, args.gpu_steps, 3, tiny=args.tiny, tls=tls))
                 if args.ref_steps > 0:
@@ -798,6 +816,26 @@ def report(args, nproc, tls, ms_total, qs, extras):
             "sync_speedup": round(_pct(ref["sync_ms"], 0.5) / max(out["sync_p50_ms"], 1e-3), 1),
             "dev_start_s": round(ref["dev_start_s"], 3),
         }
+    wan, wan_ref = extras.get("qs_wan"), extras.get("qs_wan_ref")
+    if _ok(wan):
+        wp50 = _pct(wan["reload_ms"], 0.5)
+        out["wan"] = {
+            "what": f"the headline loop (cold restarts) with the cluster behind a shaped link of {WAN[0]} ms RTT and "
+                    f"{WAN[1]} Mbit/s each way (devspace_amd/localkube/netem.py): API requests, exec sync and the "
+                    f"port-forward all cross it",
+            "rtt_ms": WAN[0], "mbit": WAN[1],
+            "p50_ms": round(wp50, 2), "p90_ms": round(_pct(wan["reload_ms"], 0.9), 2),
+            "sync_p50_ms": round(_pct(wan["sync_ms"], 0.5), 2), "n": len(wan["reload_ms"]),
+            "dev_start_s": round(wan["dev_start_s"], 3), "link_connections": wan.get("link", {}).get("connections"),
+        }
+        if _ok(wan_ref):
+            wr50 = _pct(wan_ref["reload_ms"], 0.5)
+            out["wan"]["reference_equivalent"] = {
+                "p50_ms": round(wr50, 2), "sync_p50_ms": round(_pct(wan_ref["sync_ms"], 0.5), 2),
+                "n": len(wan_ref["reload_ms"]), "dev_start_s": round(wan_ref["dev_start_s"], 3),
+                "link_connections": wan_ref.get("link", {}).get("connections"),
+                "speedup": round(wr50 / wp50, 2) if wp50 else None,
+            }
     pool = extras.get("qs_pool")
     if _ok(pool):
         pp50 = _pct(pool["reload_ms"], 0.5)

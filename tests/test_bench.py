@@ -42,6 +42,11 @@ def test_bench_cpu_tiny():
     assert cfg["restart"] == "cold" and "WATCH_STANDBY=0" in cfg["sample"] and d["dtype"] is None
     pool = d["standby_pool"]
     assert pool["n"] >= 10 and pool["p50_ms"] > 0 and "app-side" in pool["what"], pool
+    # the same loops behind a 30 ms RTT link: every edit pays at least the one-way delay
+    wan = d["wan"]
+    assert wan["rtt_ms"] == 30 and wan["n"] >= 5 and wan["link_connections"] > 0, wan
+    assert wan["sync_p50_ms"] >= 15 and wan["p50_ms"] > wan["sync_p50_ms"], wan
+    assert wan["reference_equivalent"]["p50_ms"] > wan["p50_ms"], wan
     dep = d["deploy"]
     assert dep["control_plane_only"] is True and dep["net"]["tls_handshakes"] >= 1
     # reference timing: no kept-alive connections, 5 s rollout polls
