@@ -1077,6 +1077,10 @@ def worker_main(args) -> int:
     # the supervisor of a group hands down a shared-memory directory; one rank alone keeps
     # snapshots only where --rescue-dir says (e.g. a pod volume that outlives the container)
     rescue_dir = os.environ.get("DEVSPACE_RESCUE_DIR") or args.rescue_dir
+    # one rank in a pod: kept in the pod's /dev/shm across container restarts, dropped at a clean exit
+    own_dir = not rescue_dir and world == 1 and _in_pod()
+    if own_dir:
+        rescue_dir = _default_rescue_dir(args.entry, 1)
     rescue = None
     if rescue_dir and args.rescue_every > 0:
         # ignored before it exists: its mkdir must not read as an edit (the change feed runs)
@@ -1295,6 +1299,8 @@ def worker_main(args) -> int:
     feed.close()
     watcher.close()
     overlay.uninstall()
+    if own_dir:
+        _drop_rescue_dir(rescue_dir)
     if dist is not None and dist.is_initialized():
         dist.destroy_process_group()
     return 0
@@ -1443,11 +1449,34 @@ class _GroupWatch:
                 return ("done", codes)
 
 
-def _default_rescue_dir() -> str:
+def _in_pod() -> bool:
+    return bool(os.environ.get("KUBERNETES_SERVICE_HOST"))
+
+
+def _default_rescue_dir(entry: str, nproc: int) -> str:
+    """In a pod: one directory per entry file and rank count in /dev/shm, the pod's memory
+    volume, so a container that the kubelet restarts (an OOM kill, a crash of the runner itself)
+    finds the snapshots its previous run left. Elsewhere: this process's own (a later run on the
+    same machine starts fresh)."""
     import tempfile
 
-    base = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
+    base = os.environ.get("DEVSPACE_RESCUE_ROOT") or (
+        "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else tempfile.gettempdir())
+    if _in_pod():
+        key = hashlib.sha256(f"{os.path.abspath(entry)}|{nproc}".encode()).hexdigest()[:12]
+        return os.path.join(base, f"devspace-rescue-{key}")
+    # what runners killed outright (SIGKILL: no clean-up) left behind here
+    for name in os.listdir(base):
+        m = re.match(r"devspace-rescue-(\d+)$", name)
+        if m and not os.path.exists(f"/proc/{m.group(1)}"):
+            _drop_rescue_dir(os.path.join(base, name))
     return os.path.join(base, f"devspace-rescue-{os.getpid()}")
+
+
+def _drop_rescue_dir(path: str) -> None:
+    import shutil
+
+    shutil.rmtree(path, ignore_errors=True)
 
 
 def _wait_for_change(watcher, already=False):
@@ -1477,8 +1506,9 @@ def supervisor_main(args) -> int:
     port = args.port or _free_port()
     restarts = 0  # restarts since the last edit
     # the ranks' rescue snapshots live as long as this supervisor (a restarted group resumes
-    # from them); in /dev/shm: the pod's memory-backed volume, sized per GPU by the chart
-    rescue_dir = args.rescue_dir or _default_rescue_dir()
+    # from them) and, in a pod, as long as the pod (a restarted container resumes from them); in
+    # /dev/shm: the pod's memory-backed volume, sized per GPU by the chart
+    rescue_dir = args.rescue_dir or _default_rescue_dir(args.entry, nproc)
     os.environ["DEVSPACE_RESCUE_DIR"] = rescue_dir
     _IGNORED_DIRS.append(os.path.abspath(rescue_dir))
 
@@ -1487,6 +1517,7 @@ def supervisor_main(args) -> int:
 
     signal.signal(signal.SIGTERM, _term)  # pod deletion / kill: stop the ranks, then exit
     procs = []
+    clean = False  # stopped or finished: no later run resumes from these snapshots
     try:
         while True:
             status_r, status_w = os.pipe()
@@ -1497,6 +1528,7 @@ def supervisor_main(args) -> int:
             outcome = gw.wait()
             if outcome[0] == "done":
                 os.close(status_r)
+                clean = True
                 return 0
             _, rank, code = outcome
             _stop_group(procs, grace_s=1.0)
@@ -1519,13 +1551,12 @@ def supervisor_main(args) -> int:
             port = port + 1 if args.port else _free_port()
     except KeyboardInterrupt:
         _stop_group(procs)
+        clean = True
         return 130
     finally:
         watcher.close()
-        if not args.rescue_dir:
-            import shutil
-
-            shutil.rmtree(rescue_dir, ignore_errors=True)
+        if not args.rescue_dir and (clean or not _in_pod()):
+            _drop_rescue_dir(rescue_dir)
 
 
 def _forward(args):
@@ -1568,8 +1599,8 @@ def parse_args(argv=None):
                    help="seconds between snapshots of the training state in shared memory, from which a "
                         "group restarted after a failure resumes (0: off)")
     p.add_argument("--rescue-dir", default="",
-                   help="keep the snapshots here (kept after exit; with one rank, snapshots are taken "
-                        "only when this is set)")
+                   help="keep the snapshots here, also after exit (default: in a pod, /dev/shm for the pod's "
+                        "lifetime, dropped at a clean stop; elsewhere, one rank: none, several: for the run)")
     p.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args(argv)
 

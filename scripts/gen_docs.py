@@ -187,6 +187,8 @@ ENV = {
     "DEVSPACE_RESCUE_EVERY_S": "Seconds between the runner's snapshots of the training state in /dev/shm (default "
                                "60, 0 = off): a group restarted after a failure resumes from the newest one "
                                "(`--rescue-every`).",
+    "DEVSPACE_RESCUE_ROOT": "Where the runner keeps its rescue snapshot directories (default `/dev/shm`, the "
+                            "pod's memory volume).",
     "DEVSPACE_RESCUE_STAGING": "`0`: a rescue snapshot is copied to shared memory at the step boundary even when "
                                "free HBM could hold a device copy written in the background.",
     "DEVSPACE_RUNNER_DEBUG": "`1`: every runner rank logs the code digest it loaded for each generation.",

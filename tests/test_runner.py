@@ -521,3 +521,25 @@ def test_agreement_stops_every_rank_at_the_same_boundary(tmp_path):
     for rank, first, second in res:
         assert first == (3, False, False)
         assert second == (3 + world - 1, True, True), (rank, second)
+
+
+def test_default_rescue_dir_outside_a_pod_sweeps_dead_runners_leftovers(tmp_path, monkeypatch):
+    """Outside a pod the snapshots are scoped to the supervisor's pid; a runner killed outright
+    cannot clean up, so the next one drops directories whose process is gone (and only those)."""
+    from devspace_amd import runner
+
+    monkeypatch.delenv("KUBERNETES_SERVICE_HOST", raising=False)
+    monkeypatch.setenv("DEVSPACE_RESCUE_ROOT", str(tmp_path))
+    dead = tmp_path / "devspace-rescue-999999999"
+    alive = tmp_path / f"devspace-rescue-{os.getppid()}"
+    other = tmp_path / "devspace-rescue-notapid"
+    for d in (dead, alive, other):
+        d.mkdir()
+        (d / "rank0-step1.json").write_text("{}")
+    got = runner._default_rescue_dir("train.py", 2)
+    assert got == str(tmp_path / f"devspace-rescue-{os.getpid()}")
+    assert not dead.exists() and alive.exists() and other.exists()
+    # in a pod: a stable path per entry file and rank count (survives a container restart)
+    monkeypatch.setenv("KUBERNETES_SERVICE_HOST", "10.96.0.1")
+    a, b = runner._default_rescue_dir("train.py", 2), runner._default_rescue_dir("train.py", 2)
+    assert a == b != runner._default_rescue_dir("train.py", 4)

@@ -579,3 +579,39 @@ def test_restarted_group_resumes_from_the_rescue_snapshot_on_the_gpu(tmp_path):
         assert f"loss={snapped + 1} " in line, (snapped, line)
     finally:
         r.stop()
+
+
+@pytest.mark.parametrize("nproc", [1, 2])
+def test_a_restarted_container_resumes_from_the_pods_shm(tmp_path, nproc):
+    """In a pod (KUBERNETES_SERVICE_HOST set) the snapshots live in the pod's /dev/shm under a
+    path derived from the entry file, with no flag: a container the kubelet restarts after its
+    runner was killed outright (an OOM kill) resumes from them; a clean stop (SIGTERM: pod
+    deletion, `devspace purge`) drops them, so the next start is a fresh one."""
+    entry = tmp_path / "train.py"
+    entry.write_text(RESCUE_STEP)
+    shm = tmp_path.parent / (tmp_path.name + "-shm")  # outside the watched tree, like /dev/shm
+    env = {"KUBERNETES_SERVICE_HOST": "10.96.0.1", "DEVSPACE_RESCUE_ROOT": str(shm)}
+    args = ("--log-every", "20", "--rescue-every", "0.3")
+    r = Runner(tmp_path, entry, nproc, extra_args=args, extra_env=env)
+    try:
+        r.until(r"started gen=1 marker=v0", timeout=180)
+        r.until(r"rescue snapshot step=\d+ gen=1 ")
+        _, line = r.until(r"rescue snapshot step=\d+ gen=1 ")
+        snapped = int(re.search(r"step=(\d+)", line).group(1))
+        kids = psutil.Process(r.proc.pid).children(recursive=True)
+        r.proc.kill()  # the container's main process, SIGKILLed
+        r.proc.wait()
+        psutil.wait_procs(kids, timeout=30)
+    finally:
+        r.stop()
+    left = [d for d in os.listdir(shm) if d.startswith("devspace-rescue-")]
+    assert len(left) == 1 and os.listdir(shm / left[0]), left
+    r = Runner(tmp_path, entry, nproc, extra_args=args, extra_env=env)
+    try:
+        # the last snapshot seen, or one that completed between that line and the kill
+        _, line = r.until(r"restored step=\d+ ", timeout=180)
+        assert int(re.search(r"restored step=(\d+)", line).group(1)) >= snapped, (snapped, line)
+        r.until(r"started gen=1 marker=v0", timeout=60)
+    finally:
+        assert r.stop() in (0, 130)
+    assert not [d for d in os.listdir(shm) if d.startswith("devspace-rescue-")], os.listdir(shm)
