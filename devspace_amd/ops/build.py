@@ -48,6 +48,14 @@ def build_probe(verbose=False, force=False):
     return out
 
 
+def source_sha(path=None) -> str:
+    """SHA-256 of the fused-ops source, compiled into the extension (`_fused_ops.source_sha`)."""
+    import hashlib
+
+    with open(path or os.path.join(HERE, "fused_ops.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def _fused_tag():
     """Cache key of a fused-ops build: source bytes, torch build, target arch, Python ABI."""
     import hashlib
@@ -92,6 +100,7 @@ def build_fused(verbose=False, force=False, out=None):
     cxx11 = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     cmd = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
            "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=_fused_ops", "-DTORCH_API_INCLUDE_EXTENSION_H",
+           f'-DDEVSPACE_SOURCE_SHA="{source_sha(src)}"',
            f"-D_GLIBCXX_USE_CXX11_ABI={cxx11}", "-Wno-unused-result",
            "-I" + os.path.join(troot, "include"), "-I" + os.path.join(troot, "include", "torch", "csrc", "api", "include"),
            "-I" + sysconfig.get_paths()["include"], src,

@@ -43,6 +43,7 @@ def ext():
         try:
             from . import _fused_ops  # noqa: WPS433 - the in-tree (or image-built) extension
 
+            _check_source(_fused_ops)  # a stale build raises here, on every call
             _ext = _fused_ops
         except ImportError as e:  # pragma: no cover - depends on the build
             try:
@@ -53,6 +54,29 @@ def ext():
         raise RuntimeError(f"devspace_amd fused HIP ops are not built ({_ext_error}); run "
                            "`python -m devspace_amd.ops.build --fused`")
     return _ext
+
+
+def _check_source(mod) -> None:
+    """An in-tree build must come from the source next to it: kernels older than an edit of
+    fused_ops.hip must not run (an error, not a silent fallback)."""
+    import os
+
+    from . import build
+
+    if os.path.exists(os.path.join(build.HERE, "fused_ops.hip")):
+        built, src = getattr(mod, "source_sha", "unknown"), build.source_sha()
+        if built != src:
+            raise RuntimeError(f"the fused-ops extension is stale: built from source {built[:12]}, the source is "
+                               f"{src[:12]}; run `python -m devspace_amd.ops.build --fused`")
+
+
+def check_fresh() -> str:
+    """The loaded extension was built from the fused_ops.hip next to it: returns the source
+    SHA-256, raises on a stale build (kernels older than the source)."""
+    from . import build
+
+    _check_source(ext())
+    return build.source_sha()
 
 
 def backend() -> str:

@@ -1375,8 +1375,15 @@ at::Tensor cross_entropy(const at::Tensor& logits, const at::Tensor& tgt, int64_
 
 }  // namespace
 
+// SHA-256 of this file, passed by devspace_amd/ops/build.py: the loader checks the extension it
+// imports was built from the source next to it (no stale kernels after an edit or a checkout)
+#ifndef DEVSPACE_SOURCE_SHA
+#define DEVSPACE_SOURCE_SHA "unknown"
+#endif
+
 PYBIND11_MODULE(_fused_ops, m) {
   m.doc() = "gfx950 fused training ops (RMSNorm, SwiGLU, cross-entropy)";
+  m.attr("source_sha") = DEVSPACE_SOURCE_SHA;
   m.def("rmsnorm_supported", &rmsnorm_supported);
   // differentiable entry points (C++ autograd)
   m.def("rms_norm", &rms_norm);

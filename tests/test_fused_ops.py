@@ -27,7 +27,40 @@ def test_cpu_fallbacks_match_torch():
     assert m.weight.shape == (32,) and m(x).shape == x.shape
 
 
+def test_extension_is_built_from_this_source(tmp_path, monkeypatch):
+    """The in-tree extension carries the SHA-256 of the fused_ops.hip it was compiled from, and
+    loading one built from other source bytes is an error (stale kernels never run quietly)."""
+    try:
+        from devspace_amd.ops import _fused_ops
+    except ImportError as e:
+        pytest.skip(f"extension not built here: {e}")
+    from devspace_amd.ops import build
+
+    assert _fused_ops.source_sha == build.source_sha()
+    edited = tmp_path / "fused_ops.hip"
+    edited.write_bytes(open(build.os.path.join(build.HERE, "fused_ops.hip"), "rb").read() + b"// edit\n")
+    monkeypatch.setattr(build, "source_sha", lambda path=None: _sha(edited))
+    with pytest.raises(RuntimeError, match="stale"):
+        fused._check_source(_fused_ops)
+
+
+def _sha(path):
+    import hashlib
+
+    return hashlib.sha256(open(path, "rb").read()).hexdigest()
+
+
 gpu = pytest.mark.gpu
+
+
+@gpu
+def test_gpu_runs_kernels_built_from_this_source():
+    dev = _cuda()
+    print(f"fused_ops.hip sha256 {fused.check_fresh()[:16]} == the loaded extension's")
+    x = torch.randn(64, 256, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(256, device=dev, dtype=torch.bfloat16)
+    ref = _ref_rmsnorm(x, w, 1e-6)
+    assert torch.allclose(fused.rms_norm(x, w, 1e-6).float(), ref, atol=3e-2, rtol=3e-2)
 
 
 def _cuda():
