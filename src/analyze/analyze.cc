@@ -98,7 +98,7 @@ bool log_has_gpu_runtime_error(const std::string& text, std::string* match) {
 
 std::vector<std::string> runner_problems(const std::string& text) {
   const std::string tag = "[devspace-runner] ";
-  std::string down, failed_reload, last_failure, last_exception;
+  std::string down, failed_reload, last_failure, last_exception, rescue_off;
   bool in_traceback = false;
   for (auto& line : split(text, "\n")) {
     size_t at = line.find(tag);
@@ -122,6 +122,10 @@ std::vector<std::string> runner_problems(const std::string& text) {
     } else if (starts_with(msg, "started gen=")) {
       down.clear();
       failed_reload.clear();
+      rescue_off.clear();  // fresh processes take snapshots again
+    } else if (starts_with(msg, "rescue snapshots off (")) {
+      rescue_off = msg.substr(std::string("rescue snapshots off (").size());
+      if (!rescue_off.empty() && rescue_off.back() == ')') rescue_off.pop_back();
     } else if (starts_with(msg, "reloaded gen=")) {
       failed_reload.clear();
     } else if (starts_with(msg, "reload failed gen=")) {
@@ -138,6 +142,10 @@ std::vector<std::string> runner_problems(const std::string& text) {
     std::string why = last_exception.empty() ? "" : " (" + last_exception + ")";
     out.push_back("the last edit did not load: " + failed_reload.substr(0, failed_reload.find('\n')) + why);
   }
+  if (!rescue_off.empty())
+    out.push_back("the runner stopped snapshotting the training state (" + rescue_off +
+                  "): a restart of the group or container would begin again from step 0 (a larger shmPerGPU, or "
+                  "snapshot()/restore() in the module)");
   return out;
 }
 

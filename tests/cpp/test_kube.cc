@@ -126,6 +126,14 @@ TEST(analyze_runner_state_from_pod_log) {
   EXPECT_EQ(p.size(), (size_t)1);
   EXPECT_TRUE(contains(p[0], "the last edit did not load: reload failed gen=3"));
   EXPECT_TRUE(analyze::runner_problems(bad_edit + "[devspace-runner] reloaded gen=4 marker=ok ranks=8\n").empty());
+  // the training state is no longer protected: said once, until fresh processes start
+  std::string off = up + "[devspace-runner] rescue snapshots off (/dev/shm has 900 MiB free, a snapshot of every "
+                         "rank needs 3072 MiB)\n";
+  p = analyze::runner_problems(off);
+  EXPECT_EQ(p.size(), (size_t)1);
+  EXPECT_TRUE(contains(p[0], "stopped snapshotting the training state (/dev/shm has 900 MiB free"));
+  EXPECT_TRUE(contains(p[0], "needs 3072 MiB): a restart"));
+  EXPECT_TRUE(analyze::runner_problems(off + "[devspace-runner] started gen=1 marker=v0 world=8\n").empty());
 }
 
 // $KUBECONFIG with several files, merged like client-go's clientcmd loading rules.
