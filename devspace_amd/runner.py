@@ -1034,6 +1034,29 @@ def worker_main(args) -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     import torch  # imported once per process; kept warm across reloads
 
+    if args.standby:
+        # a warm standby rank: the supervisor hands it the group's rendezvous port when a failed
+        # group is replaced, or closes the pipe. Meanwhile it pays what a process start pays
+        # before the training code runs: `import torch` and the modules a setup() first pulls in
+        # (creating an optimizer imports torch._dynamo: 1.5 s of a restart on its own)
+        import importlib
+
+        for name in ("torch.distributed", "torch.optim", "torch.nn.parallel", "torch._dynamo"):
+            try:
+                importlib.import_module(name)
+            except Exception:  # an optional part missing in this build: paid later, if used
+                pass
+        line = sys.stdin.readline().split()
+        if len(line) != 2 or line[0] != "go":
+            return 0
+        os.environ["MASTER_PORT"] = line[1]
+    phases, t_phase = [], [time.perf_counter()]
+
+    def phase(name):  # start-up phase times, logged per rank with DEVSPACE_RUNNER_DEBUG
+        now = time.perf_counter()
+        phases.append(f"{name}={(now - t_phase[0]) * 1000.0:.0f}ms")
+        t_phase[0] = now
+
     device = None
     dist = None
     group_timeout = None
@@ -1046,6 +1069,7 @@ def worker_main(args) -> int:
         device = torch.device("cuda", torch.cuda.current_device())
     else:
         device = torch.device("cpu")
+    phase("device")
     if world > 1:
         import torch.distributed as dist  # noqa: WPS433
 
@@ -1054,6 +1078,7 @@ def worker_main(args) -> int:
         backend = os.environ.get("DEVSPACE_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 **({"timeout": group_timeout} if group_timeout is not None else {}))
+        phase("process_group")
     if device.type == "cuda" and args.gemm_tuning != "off":
         try:
             from devspace_amd.ops import gemm_tuning  # noqa: WPS433
@@ -1072,8 +1097,10 @@ def worker_main(args) -> int:
     feed = ChangeFeed(watcher, entry)
     overlay = SourceOverlay(watch_dir).install()
     fault = overlay.fault = _FaultHooks(os.environ.get("DEVSPACE_RUNNER_FAULT"), rank)
+    phase("watch")
     # control plane of the group (gloo, CPU tensors): generation, preemption, code agreement
     agree = Agreement(dist, timeout=group_timeout) if world > 1 else None
+    phase("control_group")
     # the supervisor of a group hands down a shared-memory directory; one rank alone keeps
     # snapshots only where --rescue-dir says (e.g. a pod volume that outlives the container)
     rescue_dir = os.environ.get("DEVSPACE_RESCUE_DIR") or args.rescue_dir
@@ -1112,14 +1139,18 @@ def worker_main(args) -> int:
             ctx.generation = gen
             try:
                 mod = _load_generation(entry, gen, None, overlay, agree, False, watch_dir, ctx, fault)
+                phase("load")
                 state = mod.setup(ctx) if hasattr(mod, "setup") else None
+                phase("setup")
                 if rescue is not None and state is not None and hasattr(mod, "step"):
                     state = _rescue_restore(rescue, agree, mod, ctx, state)
+                    phase("restore")
                 if hasattr(mod, "step"):
                     first = mod.step(ctx, state) or {}
                     ctx.step += 1
                     if device.type == "cuda":
                         torch.cuda.synchronize()
+                    phase("first_step")
                 break
             except LoadFailed as e:
                 if agree is not None:
@@ -1138,6 +1169,8 @@ def worker_main(args) -> int:
             gen += 1
         setup_version = getattr(mod, "SETUP_VERSION", None)
         _status(f"ready {rank}")
+        if os.environ.get("DEVSPACE_RUNNER_DEBUG"):
+            _log(f"rank={rank} start-up{' (warm standby)' if args.standby else ''}: {' '.join(phases)}")
         # Preemption only from here on: an edit that lands during setup() or the first step stays
         # pending in the feed and is picked up by the main loop's first check (a Preempted raised
         # there would have had no handler).
@@ -1316,7 +1349,9 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _spawn_group(args, port, status_fd=None):
+def _spawn_group(args, port, status_fd=None, standby=False):
+    """One process per rank; `standby`: warm standbys that import torch and then wait on stdin for
+    `go <port>` (see _promote)."""
     procs = []
     for r in range(max(1, args.nproc)):
         env = dict(os.environ)
@@ -1333,11 +1368,37 @@ def _spawn_group(args, port, status_fd=None):
         # Installed as a package (-m devspace_amd.runner) or vendored as a single file into a
         # project by `devspace init` (rocm-pytorch template).
         me = ["-m", "devspace_amd.runner"] if __package__ else [os.path.abspath(__file__)]
-        cmd = [sys.executable] + me + ["--worker"] + _forward(args)
+        cmd = [sys.executable] + me + ["--worker"] + (["--standby"] if standby else []) + _forward(args)
         supervisor = os.getpid()
         procs.append(subprocess.Popen(cmd, env=env, pass_fds=(status_fd,) if status_fd is not None else (),
+                                      stdin=subprocess.PIPE if standby else None,
                                       preexec_fn=lambda: _die_with_parent(supervisor)))
     return procs
+
+
+def _promote(procs, port) -> bool:
+    """Turns a warm standby group into the running group (rendezvous on `port`); False when one of
+    its processes is gone (then it is not used)."""
+    if any(p.poll() is not None for p in procs):
+        return False
+    try:
+        for p in procs:
+            p.stdin.write(f"go {port}\n".encode())
+            p.stdin.close()
+    except OSError:
+        return False
+    return True
+
+
+def _discard(group) -> None:
+    procs, status_r = group
+    for p in procs:
+        try:
+            p.stdin.close()  # a standby waiting for `go` exits on EOF
+        except (OSError, AttributeError):
+            pass
+    _stop_group(procs)
+    os.close(status_r)
 
 
 def _die_with_parent(supervisor_pid):
@@ -1433,12 +1494,16 @@ class _GroupWatch:
         if [p for p in self.watcher.poll(0) if not _ignored(p)]:
             self.changed = True
 
-    def wait(self):
+    def wait(self, on_ready=None):
         """('done', codes) when every rank exited 0; ('failed', rank, code) at the first rank
-        that exits otherwise (the root cause: the first `fail` line, else the first exit seen)."""
+        that exits otherwise (the root cause: the first `fail` line, else the first exit seen).
+        `on_ready()` runs once, when every rank finished its first step."""
         while True:
             self._read_status(0.02)
             self._scan_tree()
+            if on_ready is not None and len(self.ready) == len(self.procs):
+                on_ready()
+                on_ready = None
             codes = [p.poll() for p in self.procs]
             bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
             if bad:
@@ -1518,20 +1583,34 @@ def supervisor_main(args) -> int:
     signal.signal(signal.SIGTERM, _term)  # pod deletion / kill: stop the ranks, then exit
     procs = []
     clean = False  # stopped or finished: no later run resumes from these snapshots
+    standby = []  # [(procs, status_r)]: a warm group that replaces a failed one
+
+    def _new_group(as_standby=False):
+        status_r, status_w = os.pipe()
+        os.set_blocking(status_r, False)
+        group = (_spawn_group(args, port, status_w, standby=as_standby), status_r)
+        os.close(status_w)
+        return group
+
+    def _warm_up():  # once the running group is up: its start-up is not slowed by the standby's
+        if args.warm_standby and not standby:
+            standby.append(_new_group(as_standby=True))
+
     try:
         while True:
-            status_r, status_w = os.pipe()
-            os.set_blocking(status_r, False)
-            procs = _spawn_group(args, port, status_w)
-            os.close(status_w)
+            group = standby.pop() if standby else None
+            if group is not None and not _promote(group[0], port):
+                _discard(group)
+                group = None
+            procs, status_r = group or _new_group()
             gw = _GroupWatch(procs, status_r, watcher)
-            outcome = gw.wait()
+            outcome = gw.wait(on_ready=_warm_up)
             if outcome[0] == "done":
                 os.close(status_r)
                 clean = True
                 return 0
             _, rank, code = outcome
-            _stop_group(procs, grace_s=1.0)
+            _stop_group(procs, grace_s=0.2)  # the peers of a failed group: nothing left to finish
             os.close(status_r)
             came_up = len(gw.ready) == nproc
             if gw.changed:
@@ -1539,7 +1618,7 @@ def supervisor_main(args) -> int:
             restarts += 1
             if came_up and restarts <= args.max_restarts:
                 _log(f"rank={rank} exited with code {code}: restarting the group of {nproc} "
-                     f"({restarts}/{args.max_restarts} since the last edit)")
+                     f"({restarts}/{args.max_restarts} since the last edit)" + (" from the warm standby" if standby else ""))
             else:
                 why = "before every rank finished a first step" if not came_up else \
                     f"{args.max_restarts} restarts without an edit"
@@ -1547,13 +1626,15 @@ def supervisor_main(args) -> int:
                      f"before starting the group again")
                 _wait_for_change(watcher, already=gw.changed)
                 restarts = 0
-                _log(f"change detected: restarting the group of {nproc}")
+                _log(f"change detected: restarting the group of {nproc}" + (" from the warm standby" if standby else ""))
             port = port + 1 if args.port else _free_port()
     except KeyboardInterrupt:
         _stop_group(procs)
         clean = True
         return 130
     finally:
+        for group in standby:
+            _discard(group)
         watcher.close()
         if not args.rescue_dir and (clean or not _in_pod()):
             _drop_rescue_dir(rescue_dir)
@@ -1601,7 +1682,12 @@ def parse_args(argv=None):
     p.add_argument("--rescue-dir", default="",
                    help="keep the snapshots here, also after exit (default: in a pod, /dev/shm for the pod's "
                         "lifetime, dropped at a clean stop; elsewhere, one rank: none, several: for the run)")
+    p.add_argument("--no-warm-standby", dest="warm_standby", action="store_false",
+                   default=os.environ.get("DEVSPACE_WARM_STANDBY", "1") != "0",
+                   help="with several ranks, do not keep a second set of processes with torch imported to "
+                        "replace a failed group (the restart then pays the interpreter and torch start-up)")
     p.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--standby", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args(argv)
 
 

@@ -202,6 +202,8 @@ ENV = {
     "DEVSPACE_PREEMPT": "`0`: an edit never cuts the in-flight training step short at `ctx.preempt_point()`.",
     "DEVSPACE_PREEMPT_DRAIN_MS": "Steps at least this long (default 20 ms) are drained at a preemption point while "
                                  "the change feed is polled.",
+    "DEVSPACE_WARM_STANDBY": "`0`: the runner keeps no second set of rank processes (torch already imported) to "
+                             "replace a failed group (`--no-warm-standby`).",
     "DEVSPACE_WATCH_SETTLED": "`0`: the runner reacts to every write event, not only to finished writes.",
     # bundled local cluster (devspace_amd/localkube), set by its kubelet for pods
     "DEVSPACE_CONTAINER_ROOT": "Set by the bundled local cluster's kubelet: the pod container's root directory.",

@@ -137,6 +137,9 @@ def main(argv=None):
     ap.add_argument("--group-timeout", type=float, default=4.0)
     ap.add_argument("--gpu", action="store_true", help="ranks on the GPU (several ranks share it over gloo)")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--settle", type=float, default=0.0,
+                    help="seconds of training before each fault (lets the warm standby finish its imports, as "
+                         "between real failures)")
     a = ap.parse_args(argv)
     rng = random.Random(a.seed)
     work = tempfile.mkdtemp(prefix="runner-chaos-")
@@ -170,6 +173,10 @@ def main(argv=None):
                 _, m = r.until(rf"reloaded gen=\d+ marker=e{i} ", 60)
                 _, m = r.until(r"rescue snapshot step=(\d+) ", 120)
                 committed = int(m.group(1))
+            if a.settle:
+                time.sleep(a.settle)
+                _, m = r.until(r"rescue snapshot step=(\d+) ", 120)
+                committed = int(m.group(1))
             kind, rank = rng.choice(kinds), rng.randrange(a.nproc)
             t0 = time.monotonic()
             with open(trig + ".tmp", "w") as f:
@@ -189,6 +196,7 @@ def main(argv=None):
             raise AssertionError("a step saw inconsistent state:\n" + "".join(bad[:5]))
         rec = sorted(e["recovery_s"] for e in events)
         print(json.dumps({"nproc": a.nproc, "device": "gpu" if a.gpu else "cpu", "faults": len(events),
+                          "settle_s": a.settle, "warm_standby": os.environ.get("DEVSPACE_WARM_STANDBY", "1") != "0",
                           "recovery_s_p50": rec[len(rec) // 2], "recovery_s_max": rec[-1], "events": events}))
         return 0
     finally:

@@ -321,7 +321,7 @@ def test_eight_rank_reload_preempt_and_stop(tmp_path):
         assert re.search(r"loss=2 ", line), line  # 1 update at startup + 1 by the new code
         gen2 = _loaded(r.text(), 2)
         assert len(gen2) == 8 and len(set(gen2.values())) == 1, gen2
-        kids = psutil.Process(r.proc.pid).children()
+        kids = [k for k in psutil.Process(r.proc.pid).children() if "--standby" not in k.cmdline()]
         assert len(kids) == 8
         t0 = time.monotonic()
         code = r.stop()
@@ -499,8 +499,14 @@ def test_restarted_group_resumes_from_the_rescue_snapshot(tmp_path):
         r.until(r"started gen=1 marker=v0 .*world=2", timeout=180)
         r.until(r"rescue snapshot step=\d+ gen=1 ")
         _, line = r.until(r"rescue snapshot step=\d+ gen=1 ")
-        files = _rescue_files(rescue_dir)
-        assert len(files) == 4 and all(re.match(r"rank[01]-step\d+\.(bin|json)$", f) for f in files), files
+        # older snapshots are dropped: per rank the committed step and at most the next one (a
+        # snapshot may have started since that line)
+        steps = {}
+        for f in _rescue_files(rescue_dir):
+            m = re.match(r"rank([01])-step(\d+)\.(bin|json)(\.tmp)?$", f)
+            assert m, f
+            steps.setdefault(m.group(1), set()).add(int(m.group(2)))
+        assert set(steps) == {"0", "1"} and all(1 <= len(v) <= 2 for v in steps.values()), steps
         _set_marker(entry, "bad")
         r.seen(r"rank=1 exited with code 3: restarting the group")
         snapped = max(int(s) for s in re.findall(r"rescue snapshot step=(\d+)", r.text()))
