@@ -1028,6 +1028,56 @@ def _rescue_restore(rescue, agree, mod, ctx, state):
     return state
 
 
+_STANDBY_IMPORTS = ["torch.distributed", "torch.optim", "torch.nn.parallel", "torch._dynamo"]
+
+
+def _preimport(names) -> None:
+    import importlib
+
+    for name in names:
+        try:
+            importlib.import_module(name)
+        except BaseException:  # missing, broken, or exits at import: paid later, if ever used
+            pass
+
+
+def _modules_file():
+    d = os.environ.get("DEVSPACE_RESCUE_DIR")
+    return os.path.join(d, "imported-modules.txt") if d else None
+
+
+def _imported_by_group() -> list:
+    path = _modules_file()
+    try:
+        with open(path) as f:
+            return [l.strip() for l in f if l.strip()]
+    except (OSError, TypeError):
+        return []
+
+
+def _list_imported_modules(watch_dir: str) -> None:
+    """Rank 0, once its group is up: the top-level packages its process imported from outside
+    the synced tree, for the warm standby to import ahead of a takeover."""
+    path = _modules_file()
+    if not path:
+        return
+    root = os.path.realpath(watch_dir) + os.sep
+    names = set()
+    for name, mod in list(sys.modules.items()):
+        top = name.split(".")[0]
+        f = getattr(mod, "__file__", None)
+        if "." in name or top.startswith("__") or not f or os.path.realpath(f).startswith(root):
+            continue
+        names.add(top)
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path + ".tmp", "w") as out:
+            out.write("\n".join(sorted(names)) + "\n")
+        os.replace(path + ".tmp", path)
+    except OSError:
+        pass
+
+
 def worker_main(args) -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1037,15 +1087,12 @@ def worker_main(args) -> int:
     if args.standby:
         # a warm standby rank: the supervisor hands it the group's rendezvous port when a failed
         # group is replaced, or closes the pipe. Meanwhile it pays what a process start pays
-        # before the training code runs: `import torch` and the modules a setup() first pulls in
-        # (creating an optimizer imports torch._dynamo: 1.5 s of a restart on its own)
-        import importlib
-
-        for name in ("torch.distributed", "torch.optim", "torch.nn.parallel", "torch._dynamo"):
-            try:
-                importlib.import_module(name)
-            except Exception:  # an optional part missing in this build: paid later, if used
-                pass
+        # before the training code runs, on a thread (an import that hangs never holds up a
+        # takeover): `import torch` (done), the modules a setup() first pulls in (creating an
+        # optimizer imports torch._dynamo: 1.5 s of a restart on its own) and the libraries the
+        # running group's code imported (transformers, datasets, ...: its rank 0 lists them)
+        threading.Thread(target=_preimport, args=(_STANDBY_IMPORTS + _imported_by_group(),),
+                         name="devspace-standby-imports", daemon=True).start()
         line = sys.stdin.readline().split()
         if len(line) != 2 or line[0] != "go":
             return 0
@@ -1168,6 +1215,8 @@ def worker_main(args) -> int:
                     return 0
             gen += 1
         setup_version = getattr(mod, "SETUP_VERSION", None)
+        if world > 1 and rank == 0:
+            _list_imported_modules(watch_dir)  # before `ready`: the standby is started on it
         _status(f"ready {rank}")
         if os.environ.get("DEVSPACE_RUNNER_DEBUG"):
             _log(f"rank={rank} start-up{' (warm standby)' if args.standby else ''}: {' '.join(phases)}")

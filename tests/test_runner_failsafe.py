@@ -53,7 +53,8 @@ class Runner:
     """The runner supervisor as a child process, its output lines in a queue."""
 
     def __init__(self, tmp_path, entry, nproc, extra_args=(), extra_env=None, gpu=False):
-        env = dict(os.environ, PYTHONPATH=ROOT, **({} if gpu else CPU_ENV), **(extra_env or {}))
+        env = dict(os.environ, PYTHONPATH=ROOT, **({} if gpu else CPU_ENV))
+        env.update(extra_env or {})
         self.proc = subprocess.Popen([sys.executable, "-u", "-m", "devspace_amd.runner", "--nproc", str(nproc),
                                       "--watch", str(tmp_path), *extra_args, str(entry)],
                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, text=True,
@@ -503,6 +504,8 @@ def test_restarted_group_resumes_from_the_rescue_snapshot(tmp_path):
         # snapshot may have started since that line)
         steps = {}
         for f in _rescue_files(rescue_dir):
+            if f.startswith("imported-modules.txt"):  # the warm standby's import list
+                continue
             m = re.match(r"rank([01])-step(\d+)\.(bin|json)(\.tmp)?$", f)
             assert m, f
             steps.setdefault(m.group(1), set()).add(int(m.group(2)))
@@ -648,3 +651,31 @@ def test_chaos_on_the_gpu():
     d = _chaos("--nproc", "2", "--faults", "4", "--kinds", "raise,exit,kill,hang", "--seed", "11", "--gpu")
     assert d["faults"] == 4 and d["device"] == "gpu", d
     print(json.dumps(d))
+
+
+def test_warm_standby_has_imported_the_group_s_libraries(tmp_path):
+    """The warm standby imports what the running group imported from outside the synced tree
+    (rank 0 lists it): a library that takes 3 s to import (transformers-like) is not paid again
+    when the standby takes over after a failure."""
+    lib = tmp_path.parent / (tmp_path.name + "-site")
+    lib.mkdir()
+    (lib / "slowlib.py").write_text("import time\ntime.sleep(3.0)\nVALUE = 1\n")
+    trigger = lib / "fail-once"
+    entry = tmp_path / "train.py"
+    entry.write_text(STEADY.replace("import time\n", "import os\nimport time\n\nimport slowlib\n", 1).replace(
+        "def step(ctx, state):\n",
+        f"def step(ctx, state):\n    if ctx.rank == 1 and os.path.exists({str(trigger)!r}):\n"
+        f"        os.unlink({str(trigger)!r})\n        raise RuntimeError('once')\n", 1))
+    r = Runner(tmp_path, entry, 2, extra_args=("--log-every", "20"),
+               extra_env={"PYTHONPATH": f"{ROOT}{os.pathsep}{lib}", "DEVSPACE_RUNNER_DEBUG": "1"})
+    try:
+        r.until(r"started gen=1 marker=v0 .*world=2", timeout=180)
+        time.sleep(8)  # the standby starts once the group is up, and imports
+        t0 = time.monotonic()
+        trigger.write_text("1")
+        r.until(r"rank=1 exited with code 3: restarting the group of 2 .*from the warm standby", timeout=60)
+        t_up, _ = r.until(r"started gen=1 marker=v0 .*world=2", timeout=60)
+        assert t_up - t0 < 3.0, (t_up - t0, r.text()[-3000:])  # slowlib's 3 s import was done ahead
+        assert re.search(r"rank=\d start-up \(warm standby\):", r.text()), r.text()[-3000:]
+    finally:
+        r.stop()
