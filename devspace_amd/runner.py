@@ -504,8 +504,11 @@ class Rescue:
     def _hbm_room(nbytes: int, device) -> bool:
         import torch
 
-        free, _ = torch.cuda.mem_get_info(device)
-        cached = torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+        try:
+            free, _ = torch.cuda.mem_get_info(device)
+            cached = torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+        except RuntimeError:  # no answer from the runtime: copy at the boundary instead
+            return False
         return free + cached >= nbytes * 1.1 + (256 << 20)
 
     def begin(self, mod, ctx, state, gen, setup_version) -> None:
