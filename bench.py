@@ -730,6 +730,11 @@ def main():
                 extra("qs_wan", lambda: quickstart_loop(workdir, max(args.ref_steps, 5), 1, tls=tls, cold=True, wan=WAN))
                 extra("qs_wan_ref", lambda: quickstart_loop(workdir, args.ref_steps, 1, sync_mode="compat", tls=tls,
                                                             reference=True, wan=WAN))
+                if not args.no_deploy_bench:
+                    from devspace_amd.localkube.bench import bench_deploy
+
+                    extra("deploy_wan", lambda: bench_deploy(workdir, tls=tls, wan=WAN))
+                    extra("deploy_wan_ref", lambda: bench_deploy(workdir, tls=tls, reference=True, wan=WAN))
             if args.gpu_steps > 0:
                 extra("gpu_pod", lambda: dev_loop(workdir, nproc, gpus, args.gpu_steps, 3, tiny=args.tiny, tls=tls))
                 if args.ref_steps > 0:
@@ -828,6 +833,14 @@ def report(args, nproc, tls, ms_total, qs, extras):
             "sync_p50_ms": round(_pct(wan["sync_ms"], 0.5), 2), "n": len(wan["reload_ms"]),
             "dev_start_s": round(wan["dev_start_s"], 3), "link_connections": wan.get("link", {}).get("connections"),
         }
+        dw, dwr = extras.get("deploy_wan"), extras.get("deploy_wan_ref")
+        if _ok(dw):
+            out["wan"]["deploy"] = {"wall_clock_s": round(dw["cold_s"], 3), "warm_wall_clock_s": round(dw["warm_s"], 3),
+                                    "net": dw.get("net")}
+            if _ok(dwr):
+                out["wan"]["deploy"]["reference_equivalent"] = {
+                    "wall_clock_s": round(dwr["cold_s"], 3), "warm_wall_clock_s": round(dwr["warm_s"], 3),
+                    "net": dwr.get("net"), "speedup": round(dwr["cold_s"] / max(dw["cold_s"], 1e-3), 1)}
         if _ok(wan_ref):
             wr50 = _pct(wan_ref["reload_ms"], 0.5)
             out["wan"]["reference_equivalent"] = {

@@ -73,17 +73,24 @@ def _prewarm_runtime():
     return done
 
 
-def bench_deploy(workdir, example="quickstart", tls=False, reference=False):
+def bench_deploy(workdir, example="quickstart", tls=False, reference=False, wan=None):
     """reference=True: the reference's waits (DEVSPACE_REFERENCE_TIMING: 1 s pod sleeps, 5 s
-    rollout polls, no kept-alive connections) and sync protocol, on the same cluster code."""
-    base = os.path.join(workdir, "deploy-bench" + ("-ref" if reference else ""))
+    rollout polls, no kept-alive connections) and sync protocol, on the same cluster code.
+    wan=(rtt_ms, mbit): the API server behind a shaped link (netem.ShapedLink)."""
+    base = os.path.join(workdir, "deploy-bench" + ("-ref" if reference else "") + ("-wan" if wan else ""))
     os.makedirs(base, exist_ok=True)
     proj = os.path.join(base, example)
     shutil.copytree(os.path.join(ROOT, "examples", example), proj, symlinks=True)
     prewarmed = _prewarm_runtime()
     cluster = LocalCluster(os.path.join(base, "cluster"), gpus=0, tls=tls).start()
+    link = None
     try:
         env = devspace_env(cluster, base)
+        if wan:
+            from .netem import ShapedLink, point_kubeconfig
+
+            link = ShapedLink(("127.0.0.1", cluster.port), rtt_ms=wan[0], mbit=wan[1]).start()
+            point_kubeconfig(env["KUBECONFIG"], cluster.server, link.url("https" if tls else "http"))
         if reference:
             env.update(DEVSPACE_REFERENCE_TIMING="1", DEVSPACE_SYNC_MODE="compat")
         trace = os.path.join(proj, ".devspace", "logs", "trace.jsonl")
@@ -96,4 +103,6 @@ def bench_deploy(workdir, example="quickstart", tls=False, reference=False):
         return {"cold_s": cold, "warm_s": warm, "cold_phases_ms": phases, "net": net,
                 "host_runtime_prewarmed": prewarmed}
     finally:
+        if link is not None:
+            link.stop()
         cluster.stop()

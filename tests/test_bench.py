@@ -47,6 +47,10 @@ def test_bench_cpu_tiny():
     assert wan["rtt_ms"] == 30 and wan["n"] >= 5 and wan["link_connections"] > 0, wan
     assert wan["sync_p50_ms"] >= 15 and wan["p50_ms"] > wan["sync_p50_ms"], wan
     assert wan["reference_equivalent"]["p50_ms"] > wan["p50_ms"], wan
+    # deploy across the link: kept-alive connections vs a dial (+ TLS) per request
+    wd = wan["deploy"]
+    assert wd["net"]["tcp_dials"] < wd["reference_equivalent"]["net"]["tcp_dials"], wd
+    assert wd["reference_equivalent"]["wall_clock_s"] > wd["wall_clock_s"], wd
     dep = d["deploy"]
     assert dep["control_plane_only"] is True and dep["net"]["tls_handshakes"] >= 1
     # reference timing: no kept-alive connections, 5 s rollout polls
