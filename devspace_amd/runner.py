@@ -998,6 +998,26 @@ def _rescue_finish(rescue, ctx, failed: bool) -> None:
             f"training paused {job['pause_ms']:.2f} ms, {how} in {job['write_ms']:.1f} ms")
 
 
+def _rescue_final(rescue, agree, mod, ctx, state, gen, setup_version) -> None:
+    """Stopping with an explicit --rescue-dir (a volume that outlives the pod): the snapshot in
+    flight is finished and one more is taken where training stopped, so the next start — a new
+    pod after `devspace purge`, tomorrow — resumes at that step."""
+    def settle():
+        job = rescue.inflight
+        if job is None:
+            return
+        if job.get("thread") is not None:
+            job["thread"].join()
+        errs = agree.gather(job["err"]) if agree is not None else [job["err"]]
+        _rescue_finish(rescue, ctx, any(e is not None for e in errs))
+
+    settle()
+    if rescue.disabled is None and ctx.step > rescue.last_step:  # the same decision on every rank
+        ctx.log(f"stopping: a last rescue snapshot at step={ctx.step} in {rescue.root}")
+        rescue.begin(mod, ctx, state, gen, setup_version)
+        settle()
+
+
 def _rescue_restore(rescue, agree, mod, ctx, state):
     """After setup() of a (re)started group: the newest snapshot every rank holds for this
     SETUP_VERSION, loaded on every rank, or none at all."""
@@ -1272,6 +1292,7 @@ def worker_main(args) -> int:
                                                                     writing, write_failed)
                 snap, writing, write_failed = agree.snap, agree.writing, agree.write_failed
                 if agreed_stop:
+                    stop = True
                     break
                 pending_gen = max(pending_gen, target)
                 helper_pending = helper_pending or agreed_helper
@@ -1373,6 +1394,8 @@ def worker_main(args) -> int:
                         f"period_ms={period_ema or 0.0:.3f}")
             if max_steps and ctx.step >= max_steps:
                 break
+        if stop and rescue is not None and args.rescue_dir and state is not None and not script_mode:
+            _rescue_final(rescue, agree, mod, ctx, state, gen, setup_version)
     except Exception as e:  # world > 1: a collective of the control plane failed (a peer is gone)
         if agree is None:
             raise
@@ -1681,7 +1704,8 @@ def supervisor_main(args) -> int:
                 _log(f"change detected: restarting the group of {nproc}" + (" from the warm standby" if standby else ""))
             port = port + 1 if args.port else _free_port()
     except KeyboardInterrupt:
-        _stop_group(procs)
+        # with a --rescue-dir the ranks take a last snapshot before they exit: give them the time
+        _stop_group(procs, grace_s=30.0 if args.rescue_dir and args.rescue_every > 0 else 2.0)
         clean = True
         return 130
     finally:
@@ -1701,6 +1725,8 @@ def _forward(args):
         out.append("--no-preempt")
     out += ["--preempt-drain-ms", str(args.preempt_drain_ms), "--group-timeout", str(args.group_timeout),
             "--rescue-every", str(args.rescue_every)]
+    if args.rescue_dir:  # (the ranks find it in DEVSPACE_RESCUE_DIR too; this says it was asked for)
+        out += ["--rescue-dir", args.rescue_dir]
     return out + [args.entry]
 
 

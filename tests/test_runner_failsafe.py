@@ -679,3 +679,31 @@ def test_warm_standby_has_imported_the_group_s_libraries(tmp_path):
         assert re.search(r"rank=\d start-up \(warm standby\):", r.text()), r.text()[-3000:]
     finally:
         r.stop()
+
+
+@pytest.mark.parametrize("nproc", [1, 2])
+def test_stop_with_a_rescue_dir_takes_a_last_snapshot_the_next_start_resumes_from(tmp_path, nproc):
+    """`--rescue-dir` on a volume that outlives the pod: a clean stop (SIGTERM: pod deletion,
+    `devspace purge`) snapshots where training stopped — no periodic snapshot needed — and the
+    next start resumes at exactly that step."""
+    entry = tmp_path / "train.py"
+    entry.write_text(RESCUE_STEP)
+    keep = tmp_path.parent / (tmp_path.name + "-volume")
+    args = ("--log-every", "20", "--rescue-every", "1000", "--rescue-dir", str(keep))
+    r = Runner(tmp_path, entry, nproc, extra_args=args)
+    try:
+        r.until(r"started gen=1 marker=v0", timeout=180)
+        r.until(r"step=\d+ gen=1 ", timeout=60)
+    finally:
+        code = r.stop()
+    assert code in (0, 130), r.text()[-3000:]
+    m = re.search(r"stopping: a last rescue snapshot at step=(\d+)", r.text())
+    assert m and re.search(rf"rescue snapshot step={m.group(1)} gen=1 ", r.text()), r.text()[-3000:]
+    stopped_at = int(m.group(1))
+    r = Runner(tmp_path, entry, nproc, extra_args=args)
+    try:
+        r.until(rf"restored step={stopped_at} ", timeout=180)
+        _, line = r.until(r"started gen=1 marker=v0", timeout=60)
+        assert f"loss={stopped_at + 1} " in line, line
+    finally:
+        r.stop()
