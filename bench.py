@@ -206,6 +206,8 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         cluster.kubelet.extra_env["DEVSPACE_NPROC"] = str(nproc)
         if os.environ.get("DEVSPACE_DIST_BACKEND"):  # rehearsal: N ranks sharing fewer GPUs (gloo)
             cluster.kubelet.extra_env["DEVSPACE_DIST_BACKEND"] = os.environ["DEVSPACE_DIST_BACKEND"]
+        if nproc > 1:  # the fault drill at the end resumes from a snapshot: take them every 10 s
+            cluster.kubelet.extra_env["DEVSPACE_RESCUE_EVERY_S"] = "10"
         # `devspace dev` builds (dev image cache), deploys the chart, waits for the rollout,
         # then starts sync + attach on the newest running pod.
         t_dev = time.perf_counter()
@@ -274,12 +276,52 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
                     parts["log_delivery_ms"].append((t1 - float(f["t_mono"])) * 1000.0)
         if timed_end:
             timed_end()
-        return {"reload_ms": samples, "sync_ms": sync_samples, "mode": mode, "pod_deploy_s": deploy_s,
-                "parts": parts, "fused": fused, "world": pod_world, "first_step_s": first_step_s,
-                "ranks_agreed": bool(agreed) and all(a == pod_world for a in agreed)}
+        out = {"reload_ms": samples, "sync_ms": sync_samples, "mode": mode, "pod_deploy_s": deploy_s,
+               "parts": parts, "fused": fused, "world": pod_world, "first_step_s": first_step_s,
+               "ranks_agreed": bool(agreed) and all(a == pod_world for a in agreed)}
+        if pod_world > 1:
+            try:
+                out["fault_drill"] = _fault_drill(train, tail, idx)
+            except Exception as e:  # reported with the loop's numbers, which stand on their own
+                out["fault_drill"] = {"error": str(e)[-500:]}
+        return out
     finally:
         _killpg(dev)
         cluster.stop()
+
+
+def _fault_drill(train, tail, idx):
+    """The N-rank pod's failure path, once: an edit makes rank 1 raise in its next step (once:
+    a flag file marks it done), so the group must be stopped and replaced (from the warm
+    standby), resume from its latest rescue snapshot and train the edited code on every rank."""
+    import uuid
+
+    flag = os.path.join(tempfile.gettempdir(), f"devspace-bench-drill-{uuid.uuid4().hex[:8]}")
+    src = open(train).read()
+    src = re.sub(r'^MARKER = ".*"$', 'MARKER = "drill"', src, count=1, flags=re.M)
+    src += (f"\n\n_drill_step = step\n\n\ndef step(ctx, state):  # bench fault drill\n"
+            f"    import os\n    if ctx.rank == 1 and not os.path.exists({flag!r}):\n"
+            f"        open({flag!r}, 'w').close()\n        raise RuntimeError('bench fault drill on rank 1')\n"
+            f"    return _drill_step(ctx, state)\n")
+    # a snapshot to resume from (every 10 s in the drill's pod), and the standby warm by then
+    if not any("rescue snapshot step=" in l for _, l in tail.lines):
+        _, _, idx = tail.wait_for(r"\[devspace-runner\] rescue snapshot step=", start_index=idx, timeout=_budget(60))
+    t0 = time.perf_counter()
+    with open(train, "w") as f:
+        f.write(src)
+    t_fail, line, idx = tail.wait_for(r"\[devspace-runner\] rank=1 exited with code \d+: restarting the group",
+                                      start_index=idx, timeout=_budget(300))
+    standby = "from the warm standby" in line
+    t_up, line, idx = tail.wait_for(r"\[devspace-runner\] started gen=\d+ marker=drill ", start_index=idx,
+                                    timeout=_budget(300))
+    restored = [l for _, l in tail.lines[-200:] if "restored step=" in l]
+    m = re.search(r"restored step=(\d+)", restored[-1]) if restored else None
+    try:
+        os.unlink(flag)
+    except OSError:
+        pass
+    return {"recovered": True, "warm_standby": standby, "resumed_from_step": int(m.group(1)) if m else None,
+            "edit_to_failure_s": round(t_fail - t0, 3), "failure_to_training_s": round(t_up - t_fail, 3)}
 
 
 # ---------------------------------------------------------------------------- quickstart (Node.js)
@@ -892,6 +934,9 @@ def report(args, nproc, tls, ms_total, qs, extras):
              "sync_p50_ms": round(_pct(gp["sync_ms"], 0.5), 2), "n": len(gp["reload_ms"]),
              "pod_deploy_s": round(gp["pod_deploy_s"], 3),
              "dev_to_first_step_s": round(gp["first_step_s"], 3) if gp.get("first_step_s") else None}
+        if gp.get("fault_drill"):
+            g["fault_drill"] = dict(gp["fault_drill"], what="an edit makes rank 1 raise once: the group is stopped, "
+                                                          "replaced and resumes from its last rescue snapshot")
         parts = {k: round(_pct(v, 0.5), 2) for k, v in gp.get("parts", {}).items() if v}
         if parts:
             parts["sync_ms"] = g["sync_p50_ms"]

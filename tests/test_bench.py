@@ -85,6 +85,10 @@ def test_bench_torchrun_two_ranks_cpu():
     assert d["steps"] == 2 and d["value"] > 0
     assert d["n_gpus"] == 2 and d["gpu_pod"]["parallelism"] == "dp2", d
     assert d["gpu_pod"]["ranks"] == 2 and d["gpu_pod"]["ranks_agreed_on_code"] is True, d["gpu_pod"]
+    # the 2-rank pod's failure path: rank 1 raises once, the group is replaced and trains again
+    drill = d["gpu_pod"]["fault_drill"]
+    assert drill.get("recovered") is True, drill
+    assert drill["failure_to_training_s"] < 60, drill
 
 
 @pytest.mark.slow
@@ -107,6 +111,7 @@ def test_bench_torchrun_eight_ranks_cpu():
     assert isinstance(g, dict) and "error" not in g, (g, r.stderr[-3000:])
     assert g["parallelism"] == "dp8" and g["ranks"] == 8 and g["ranks_agreed_on_code"] is True, g
     assert g["n"] == 3 and g["reload_p50_ms"] > 0, g
+    assert g["fault_drill"].get("recovered") is True, g["fault_drill"]  # 8 ranks: fail, replace, resume
 
 
 def test_bench_extras_budget_keeps_the_headline():
