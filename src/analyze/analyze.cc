@@ -98,7 +98,7 @@ bool log_has_gpu_runtime_error(const std::string& text, std::string* match) {
 
 std::vector<std::string> runner_problems(const std::string& text) {
   const std::string tag = "[devspace-runner] ";
-  std::string down, failed_reload, last_failure, last_exception, rescue_off;
+  std::string down, failed_reload, last_failure, last_exception, rescue_off, restore_failed;
   bool in_traceback = false;
   for (auto& line : split(text, "\n")) {
     size_t at = line.find(tag);
@@ -123,6 +123,10 @@ std::vector<std::string> runner_problems(const std::string& text) {
       down.clear();
       failed_reload.clear();
       rescue_off.clear();  // fresh processes take snapshots again
+    } else if (starts_with(msg, "rescue: snapshot step=") && contains(msg, "did not restore")) {
+      restore_failed = msg.substr(std::string("rescue: ").size());
+    } else if (starts_with(msg, "restored step=")) {
+      restore_failed.clear();
     } else if (starts_with(msg, "rescue snapshots off (")) {
       rescue_off = msg.substr(std::string("rescue snapshots off (").size());
       if (!rescue_off.empty() && rescue_off.back() == ')') rescue_off.pop_back();
@@ -142,6 +146,9 @@ std::vector<std::string> runner_problems(const std::string& text) {
     std::string why = last_exception.empty() ? "" : " (" + last_exception + ")";
     out.push_back("the last edit did not load: " + failed_reload.substr(0, failed_reload.find('\n')) + why);
   }
+  if (!restore_failed.empty())
+    out.push_back("a restarted training group could not load its rescue snapshot (" + restore_failed +
+                  "): training started over from setup()");
   if (!rescue_off.empty())
     out.push_back("the runner stopped snapshotting the training state (" + rescue_off +
                   "): a restart of the group or container would begin again from step 0 (a larger shmPerGPU, or "

@@ -134,6 +134,15 @@ TEST(analyze_runner_state_from_pod_log) {
   EXPECT_TRUE(contains(p[0], "stopped snapshotting the training state (/dev/shm has 900 MiB free"));
   EXPECT_TRUE(contains(p[0], "needs 3072 MiB): a restart"));
   EXPECT_TRUE(analyze::runner_problems(off + "[devspace-runner] started gen=1 marker=v0 world=8\n").empty());
+  // a restart that could not load its snapshot started over: said until a restore succeeds
+  std::string lost = up + "[devspace-runner] rescue: snapshot step=120 did not restore on rank 3 (ValueError: "
+                          "state['model']: shape (8,) now, (4,) in the snapshot): starting from setup()\n"
+                          "[devspace-runner] started gen=1 marker=v2 world=8\n";
+  p = analyze::runner_problems(lost);
+  EXPECT_EQ(p.size(), (size_t)1);
+  EXPECT_TRUE(contains(p[0], "could not load its rescue snapshot (snapshot step=120 did not restore on rank 3"));
+  EXPECT_TRUE(analyze::runner_problems(lost + "[devspace-runner] restored step=130 gen=1 from the rescue snapshot\n")
+                  .empty());
 }
 
 // $KUBECONFIG with several files, merged like client-go's clientcmd loading rules.
