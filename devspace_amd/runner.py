@@ -38,7 +38,8 @@ examples/quickstart/package.json:7, the redeploy loop of cmd/dev.go:225-234,284-
     processes. A group that fails before its first step completes (the code itself is broken)
     waits for the next edit before starting again, as nodemon does ("app crashed - waiting for
     file changes"). A single rank pauses training after a failed step and resumes with the next
-    edit (process, model and optimizer state stay).
+    edit (process, model and optimizer state stay); one rank is supervised as well, so a hard
+    crash (segfault, GPU fault, OOM kill) is restarted in the container, not by the kubelet.
   * state survives a group restart: every --rescue-every seconds (60) the ranks snapshot their
     training state into /dev/shm at one agreed step boundary; a restarted group resumes from the
     newest step every rank holds instead of from scratch (`Rescue`).
@@ -1238,7 +1239,7 @@ def worker_main(args) -> int:
                     return 0
             gen += 1
         setup_version = getattr(mod, "SETUP_VERSION", None)
-        if world > 1 and rank == 0:
+        if rank == 0 and os.environ.get("DEVSPACE_RUNNER_STATUS_FD"):  # under a supervisor
             _list_imported_modules(watch_dir)  # before `ready`: the standby is started on it
         _status(f"ready {rank}")
         if os.environ.get("DEVSPACE_RUNNER_DEBUG"):
@@ -1635,12 +1636,18 @@ def supervisor_main(args) -> int:
     first step) and there are restarts left since the last edit, after the next edit otherwise."""
     if args.restart:
         return restart_main(args)
-    nproc = args.nproc
-    if nproc <= 1:
+    nproc = max(1, args.nproc)
+    if os.environ.get("DEVSPACE_RUNNER_INPROCESS") == "1":
+        # one rank in this process (a debugger, a profiler that follows one process): no
+        # supervisor, so a hard crash ends the runner (and the container) as a plain script would
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
         os.environ.setdefault("LOCAL_RANK", "0")
         return worker_main(args)
+    # One rank is supervised too: an exception in step() pauses it in its warm process, but a
+    # hard crash (a segfault in an extension, a GPU memory fault that aborts the process, the
+    # OOM killer) would otherwise end the container and put it into CrashLoopBackOff; here the
+    # warm standby takes over in about a second and resumes from the last snapshot.
     watch_dir = os.path.abspath(args.watch or os.path.dirname(os.path.abspath(args.entry)))
     watcher = make_watcher(watch_dir)
     port = args.port or _free_port()

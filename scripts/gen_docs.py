@@ -194,6 +194,8 @@ ENV = {
     "DEVSPACE_RUNNER_DEBUG": "`1`: every runner rank logs the code digest it loaded for each generation.",
     "DEVSPACE_RUNNER_FAULT": "Test-only fault injection of the runner (`mutate-entry-after-read`, `skew-helper`): "
                              "edits racing the ranks' reads, to exercise the code agreement.",
+    "DEVSPACE_RUNNER_INPROCESS": "`1`: one rank runs in the runner's own process, without a supervisor (a debugger, "
+                                 "a profiler that follows one process); a hard crash then ends the runner.",
     "DEVSPACE_RUNNER_STATUS_FD": "Set by the runner's supervisor for its ranks: the pipe they report `ready` / "
                                  "`fail` on.",
     "DEVSPACE_NPROC": "Training processes the runner starts when the pod requests no GPU (CPU runs).",
