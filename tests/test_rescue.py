@@ -1,0 +1,135 @@
+"""The runner's rescue snapshots (devspace_amd/runner.py `Rescue`) round-trip what a training
+state holds: module and optimizer state dicts (int keys, tuples, 0-dim step tensors), plain
+tensors of any dtype and layout (bf16, bool, empty, non-contiguous), Python numbers and strings;
+a module's own snapshot()/restore() hooks win; a state it cannot serialise turns snapshots off
+with a reason instead of failing the step."""
+
+import types
+
+import pytest
+import torch
+
+from devspace_amd import runner
+
+
+def _ctx(step=7, world=1):
+    ctx = runner.Context(0, world, 0, torch.device("cpu"))
+    ctx.step = step
+    return ctx
+
+
+def _state(seed):
+    torch.manual_seed(seed)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 8), torch.nn.LayerNorm(8)).to(torch.bfloat16)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, betas=(0.8, 0.95))
+    model(torch.randn(4, 8, dtype=torch.bfloat16)).float().pow(2).mean().backward()
+    opt.step()
+    return {"model": model, "opt": opt,
+            "t": torch.randn(6, 4).t(),  # non-contiguous
+            "mask": torch.rand(5) > 0.5, "empty": torch.zeros(0, 3), "scalar": torch.tensor(3.5),
+            "n": 41, "lr_scale": 0.5, "name": "run-a", "none": None,
+            "loader": object()}  # not snapshotable without hooks: left out, not an error
+
+
+def _take(rescue, mod, ctx, state):
+    rescue.begin(mod, ctx, state, gen=3, setup_version=1)
+    job = rescue.inflight
+    if job.get("thread") is not None:
+        job["thread"].join()
+    runner._rescue_finish(rescue, ctx, job["err"] is not None)
+    return job
+
+
+def test_round_trip_of_a_training_state(tmp_path):
+    mod = types.SimpleNamespace()
+    r = runner.Rescue(str(tmp_path), 0, every_s=60)
+    src = _state(0)
+    job = _take(r, mod, _ctx(), src)
+    assert job["err"] is None and job["bytes"] > 0 and not job["staged"]  # CPU: written at the boundary
+    assert r.available(1, 1) == [7] and r.available(2, 1) == [] and r.available(1, 2) == []
+    dst = _state(1)
+    snap, meta = r.load(7, torch.device("cpu"))
+    dst = runner.Rescue.apply(mod, _ctx(), dst, snap)
+    for a, b in zip(src["model"].state_dict().values(), dst["model"].state_dict().values()):
+        assert a.dtype == b.dtype == torch.bfloat16 and torch.equal(a, b)
+    so, do = src["opt"].state_dict(), dst["opt"].state_dict()
+    assert do["param_groups"][0]["betas"] == (0.8, 0.95)  # tuples stay tuples
+    assert set(do["state"]) == set(so["state"]) and all(isinstance(k, int) for k in do["state"])
+    for k in so["state"]:
+        for name, v in so["state"][k].items():
+            assert torch.equal(v, do["state"][k][name]), (k, name)
+    assert torch.equal(dst["t"], src["t"]) and torch.equal(dst["mask"], src["mask"])
+    assert dst["empty"].shape == (0, 3) and float(dst["scalar"]) == 3.5
+    assert (dst["n"], dst["lr_scale"], dst["name"], dst["none"]) == (41, 0.5, "run-a", None)
+    assert meta["gen"] == 3 and meta["step"] == 7
+
+
+def test_newer_snapshot_replaces_the_older_one(tmp_path):
+    mod = types.SimpleNamespace()
+    r = runner.Rescue(str(tmp_path), 0, every_s=60)
+    _take(r, mod, _ctx(step=7), _state(0))
+    _take(r, mod, _ctx(step=9), _state(0))
+    assert r.available(1, 1) == [9]
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["rank0-step9.bin", "rank0-step9.json"]
+
+
+def test_module_hooks_win_and_unserialisable_state_turns_snapshots_off(tmp_path):
+    seen = {}
+    mod = types.SimpleNamespace(snapshot=lambda ctx, state: {"w": state["w"] * 2},
+                                restore=lambda ctx, state, obj: seen.update(obj) or {"w": obj["w"]})
+    r = runner.Rescue(str(tmp_path / "a"), 0, every_s=60)
+    _take(r, mod, _ctx(), {"w": torch.ones(3)})
+    snap, _ = r.load(7, torch.device("cpu"))
+    out = runner.Rescue.apply(mod, _ctx(), {"w": torch.zeros(3)}, snap)
+    assert torch.equal(out["w"], torch.full((3,), 2.0)) and "w" in seen
+    bad = types.SimpleNamespace(snapshot=lambda ctx, state: {"f": lambda: 1})
+    r2 = runner.Rescue(str(tmp_path / "b"), 0, every_s=60)
+    job = _take(r2, bad, _ctx(), {})
+    assert job["err"] and "cannot snapshot a function" in job["err"] and r2.disabled, job
+    assert r2.available(None, 1) == []
+
+
+def test_restore_into_a_changed_model_fails_cleanly(tmp_path):
+    mod = types.SimpleNamespace()
+    r = runner.Rescue(str(tmp_path), 0, every_s=60)
+    _take(r, mod, _ctx(), {"w": torch.ones(4)})
+    snap, _ = r.load(7, torch.device("cpu"))
+    with pytest.raises(ValueError, match="shape"):
+        runner.Rescue.apply(mod, _ctx(), {"w": torch.ones(5)}, snap)
+
+
+@pytest.mark.gpu
+def test_hbm_staged_snapshot_round_trip_on_the_gpu(tmp_path):
+    """On the MI355X the device tensors are copied within HBM at the boundary (training pauses for
+    that alone) and written by the background thread on a side stream; the step that runs
+    meanwhile changes the live tensors, not the snapshot."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda", 0)
+    ctx = runner.Context(0, 1, 0, dev)
+    ctx.step = 5
+    torch.manual_seed(0)
+    model = torch.nn.Linear(512, 512).to(dev, torch.bfloat16)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    model(torch.randn(8, 512, device=dev, dtype=torch.bfloat16)).float().sum().backward()
+    opt.step()
+    state = {"model": model, "opt": opt, "n": 5}
+    want = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    r = runner.Rescue(str(tmp_path), 0, every_s=60)
+    r.begin(types.SimpleNamespace(), ctx, state, gen=1, setup_version=None)
+    job = r.inflight
+    assert job["staged"], job  # free HBM: a device copy, written in the background
+    with torch.no_grad():  # the next step changes the live weights while the write goes on
+        for p in model.parameters():
+            p.add_(1.0)
+    job["thread"].join()
+    assert job["err"] is None and job["pause_ms"] < 50, job
+    runner._rescue_finish(r, ctx, False)
+    snap, _ = r.load(5, dev)
+    fresh = {"model": torch.nn.Linear(512, 512).to(dev, torch.bfloat16),
+             "opt": None, "n": 0}
+    fresh["opt"] = torch.optim.AdamW(fresh["model"].parameters(), lr=1e-3)
+    runner.Rescue.apply(types.SimpleNamespace(), ctx, fresh, snap)
+    for k, v in fresh["model"].state_dict().items():
+        assert v.is_cuda and torch.equal(v, want[k]), k  # the snapshot's values, not the later ones
+    assert fresh["n"] == 5
