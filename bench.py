@@ -206,8 +206,8 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         cluster.kubelet.extra_env["DEVSPACE_NPROC"] = str(nproc)
         if os.environ.get("DEVSPACE_DIST_BACKEND"):  # rehearsal: N ranks sharing fewer GPUs (gloo)
             cluster.kubelet.extra_env["DEVSPACE_DIST_BACKEND"] = os.environ["DEVSPACE_DIST_BACKEND"]
-        if nproc > 1:  # the fault drill at the end resumes from a snapshot: take them every 10 s
-            cluster.kubelet.extra_env["DEVSPACE_RESCUE_EVERY_S"] = "10"
+        # the fault drill at the end resumes from a snapshot: take them every 10 s
+        cluster.kubelet.extra_env["DEVSPACE_RESCUE_EVERY_S"] = "10"
         # `devspace dev` builds (dev image cache), deploys the chart, waits for the rollout,
         # then starts sync + attach on the newest running pod.
         t_dev = time.perf_counter()
@@ -279,9 +279,9 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         out = {"reload_ms": samples, "sync_ms": sync_samples, "mode": mode, "pod_deploy_s": deploy_s,
                "parts": parts, "fused": fused, "world": pod_world, "first_step_s": first_step_s,
                "ranks_agreed": bool(agreed) and all(a == pod_world for a in agreed)}
-        if pod_world > 1:
+        if pod_world >= 1:
             try:
-                out["fault_drill"] = _fault_drill(train, tail, idx)
+                out["fault_drill"] = _fault_drill(train, tail, idx, pod_world)
             except Exception as e:  # reported with the loop's numbers, which stand on their own
                 out["fault_drill"] = {"error": str(e)[-500:]}
         return out
@@ -290,18 +290,22 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         cluster.stop()
 
 
-def _fault_drill(train, tail, idx):
-    """The N-rank pod's failure path, once: an edit makes rank 1 raise in its next step (once:
-    a flag file marks it done), so the group must be stopped and replaced (from the warm
-    standby), resume from its latest rescue snapshot and train the edited code on every rank."""
+def _fault_drill(train, tail, idx, world):
+    """The pod's failure path, once: an edit makes one rank fail in its next step (once: a flag
+    file marks it done) — rank 1 raises with several ranks (the group must be stopped), the only
+    rank crashes outright with one (an exception would just pause it) — so the group is replaced
+    (from the warm standby), resumes from its latest rescue snapshot and trains the edited code."""
     import uuid
+
+    rank = 1 if world > 1 else 0
+    fail = "raise RuntimeError('bench fault drill')" if world > 1 else "os._exit(1)  # a hard crash"
 
     flag = os.path.join(tempfile.gettempdir(), f"devspace-bench-drill-{uuid.uuid4().hex[:8]}")
     src = open(train).read()
     src = re.sub(r'^MARKER = ".*"$', 'MARKER = "drill"', src, count=1, flags=re.M)
     src += (f"\n\n_drill_step = step\n\n\ndef step(ctx, state):  # bench fault drill\n"
-            f"    import os\n    if ctx.rank == 1 and not os.path.exists({flag!r}):\n"
-            f"        open({flag!r}, 'w').close()\n        raise RuntimeError('bench fault drill on rank 1')\n"
+            f"    import os\n    if ctx.rank == {rank} and not os.path.exists({flag!r}):\n"
+            f"        open({flag!r}, 'w').close()\n        {fail}\n"
             f"    return _drill_step(ctx, state)\n")
     # a snapshot to resume from (every 10 s in the drill's pod), and the standby warm by then
     if not any("rescue snapshot step=" in l for _, l in tail.lines):
@@ -309,7 +313,7 @@ def _fault_drill(train, tail, idx):
     t0 = time.perf_counter()
     with open(train, "w") as f:
         f.write(src)
-    t_fail, line, idx = tail.wait_for(r"\[devspace-runner\] rank=1 exited with code \d+: restarting the group",
+    t_fail, line, idx = tail.wait_for(rf"\[devspace-runner\] rank={rank} exited with code \d+: restarting the group",
                                       start_index=idx, timeout=_budget(300))
     standby = "from the warm standby" in line
     t_up, line, idx = tail.wait_for(r"\[devspace-runner\] started gen=\d+ marker=drill ", start_index=idx,
@@ -320,7 +324,8 @@ def _fault_drill(train, tail, idx):
         os.unlink(flag)
     except OSError:
         pass
-    return {"recovered": True, "warm_standby": standby, "resumed_from_step": int(m.group(1)) if m else None,
+    return {"ranks": world, "failure": "exception on rank 1" if world > 1 else "hard crash (os._exit) of the only rank",
+            "recovered": True, "warm_standby": standby, "resumed_from_step": int(m.group(1)) if m else None,
             "edit_to_failure_s": round(t_fail - t0, 3), "failure_to_training_s": round(t_up - t_fail, 3)}
 
 
@@ -935,7 +940,7 @@ def report(args, nproc, tls, ms_total, qs, extras):
              "pod_deploy_s": round(gp["pod_deploy_s"], 3),
              "dev_to_first_step_s": round(gp["first_step_s"], 3) if gp.get("first_step_s") else None}
         if gp.get("fault_drill"):
-            g["fault_drill"] = dict(gp["fault_drill"], what="an edit makes rank 1 raise once: the group is stopped, "
+            g["fault_drill"] = dict(gp["fault_drill"], what="an edit makes one rank fail once: the group is stopped, "
                                                           "replaced and resumes from its last rescue snapshot")
         parts = {k: round(_pct(v, 0.5), 2) for k, v in gp.get("parts", {}).items() if v}
         if parts:

@@ -63,6 +63,10 @@ def test_bench_cpu_tiny():
     g = d["gpu_pod"]
     assert g["n"] == 2 and g["reload_p50_ms"] > 0 and g["fused_ops"].startswith("eager (no GPU)"), g
     assert g["reference_equivalent"]["p50_ms"] > g["reload_p50_ms"]
+    # one rank: the drill's hard crash is replaced from the warm standby, resuming from a snapshot
+    drill = g["fault_drill"]
+    assert drill.get("recovered") is True and drill["ranks"] == 1 and drill["warm_standby"], drill
+    assert drill["resumed_from_step"], drill
     for key in ("php_mysql", "microservices", "kaniko"):
         e = d[key]
         assert "error" not in e, (key, e, r.stderr[-3000:])
