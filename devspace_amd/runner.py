@@ -43,6 +43,8 @@ examples/quickstart/package.json:7, the redeploy loop of cmd/dev.go:225-234,284-
   * state survives a group restart: every --rescue-every seconds (60) the ranks snapshot their
     training state into /dev/shm at one agreed step boundary; a restarted group resumes from the
     newest step every rank holds instead of from scratch (`Rescue`).
+  * restarts are fast: once a group is up, the supervisor keeps a warm standby group (torch and
+    the group's libraries imported, no GPU touched) that replaces a failed one.
 
 Preemptible steps: a step may call `ctx.preempt_point()` between its phases (e.g. between
 forward and backward). The point abandons the rest of the step when a newer version of the
