@@ -1270,7 +1270,12 @@ def worker_main(args) -> int:
         script_mode = not hasattr(mod, "step")
         fault.armed = True
         paused = False  # one rank: a step of this generation failed; no more steps until an edit
+        last_beat = 0.0
         while agree is not None or not stop:
+            now = time.monotonic()
+            if now - last_beat >= 1.0:  # the supervisor's evidence that this loop comes round
+                _status(f"hb {rank} {ctx.step} {period_ema or 0.0:.1f}")
+                last_beat = now
             # 1. pick up local change notifications (non-blocking while training; blocking when idle)
             timeout = 0 if (not script_mode and args.train and not paused) else 0.05
             n_changes, t_first, helper_changed = feed.take(timeout)
@@ -1535,13 +1540,16 @@ class _GroupWatch:
     status lines (`ready <rank>`, `fail <rank> <gen>`) and whether the synced tree changed since
     the group started (then a failed group restarts at once: the fix may already be there)."""
 
-    def __init__(self, procs, status_r, watcher):
+    def __init__(self, procs, status_r, watcher, stuck_after=0.0):
         self.procs = procs
         self.status_r = status_r
         self.watcher = watcher
         self.ready = set()
         self.failed = []  # ranks in the order their `fail` lines arrived
         self.changed = False
+        self.last_change = 0.0  # monotonic time of the newest change of the synced tree
+        self.stuck_after = stuck_after
+        self.beat = {}  # rank -> (monotonic time of its last heartbeat, step period in s)
         self._buf = b""
         self._next_scan = 0.0
 
@@ -1561,8 +1569,11 @@ class _GroupWatch:
             parts = line.decode(errors="replace").split()
             if len(parts) >= 2 and parts[0] == "ready":
                 self.ready.add(int(parts[1]))
+                self.beat[int(parts[1])] = (time.monotonic(), 0.0)
             elif len(parts) >= 2 and parts[0] == "fail":
                 self.failed.append(int(parts[1]))
+            elif len(parts) >= 4 and parts[0] == "hb":
+                self.beat[int(parts[1])] = (time.monotonic(), float(parts[3]) / 1000.0)
 
     def _scan_tree(self):
         now = time.monotonic()
@@ -1571,10 +1582,24 @@ class _GroupWatch:
         self._next_scan = now + 0.25
         if [p for p in self.watcher.poll(0) if not _ignored(p)]:
             self.changed = True
+            self.last_change = now
+
+    def _stuck(self):
+        """(rank, seconds) of a rank whose loop has not come round for max(stuck_after, 50 step
+        periods) while the code changed since: stuck inside a step (a deadlock, an endless loop)
+        it would never pick the edit up."""
+        if not self.stuck_after or len(self.ready) < len(self.procs):
+            return None
+        now = time.monotonic()
+        for rank, (t, period) in self.beat.items():
+            if self.last_change > t and now - t > max(self.stuck_after, 50.0 * period):
+                return rank, now - t
+        return None
 
     def wait(self, on_ready=None):
         """('done', codes) when every rank exited 0; ('failed', rank, code) at the first rank
-        that exits otherwise (the root cause: the first `fail` line, else the first exit seen).
+        that exits otherwise (the root cause: the first `fail` line, else the first exit seen);
+        ('stuck', rank, seconds) for a rank stuck in a step across an edit.
         `on_ready()` runs once, when every rank finished its first step."""
         while True:
             self._read_status(0.02)
@@ -1582,6 +1607,9 @@ class _GroupWatch:
             if on_ready is not None and len(self.ready) == len(self.procs):
                 on_ready()
                 on_ready = None
+            stuck = self._stuck()
+            if stuck is not None:
+                return ("stuck",) + stuck
             codes = [p.poll() for p in self.procs]
             bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
             if bad:
@@ -1687,12 +1715,21 @@ def supervisor_main(args) -> int:
                 _discard(group)
                 group = None
             procs, status_r = group or _new_group()
-            gw = _GroupWatch(procs, status_r, watcher)
+            gw = _GroupWatch(procs, status_r, watcher, stuck_after=args.stuck_after)
             outcome = gw.wait(on_ready=_warm_up)
             if outcome[0] == "done":
                 os.close(status_r)
                 clean = True
                 return 0
+            if outcome[0] == "stuck":
+                _, rank, secs = outcome
+                _stop_group(procs, grace_s=0.2)
+                os.close(status_r)
+                _log(f"rank={rank} made no progress for {secs:.0f} s and the code changed since (stuck in a step?): "
+                     f"restarting the group of {nproc} with the new code" + (" from the warm standby" if standby else ""))
+                restarts = 0
+                port = port + 1 if args.port else _free_port()
+                continue
             _, rank, code = outcome
             _stop_group(procs, grace_s=0.2)  # the peers of a failed group: nothing left to finish
             os.close(status_r)
@@ -1769,6 +1806,10 @@ def parse_args(argv=None):
     p.add_argument("--rescue-dir", default="",
                    help="keep the snapshots here, also after exit (default: in a pod, /dev/shm for the pod's "
                         "lifetime, dropped at a clean stop; elsewhere, one rank: none, several: for the run)")
+    p.add_argument("--stuck-after", type=float, default=float(os.environ.get("DEVSPACE_STUCK_AFTER_S", "60")),
+                   help="a rank whose loop has not come round for this long (or 50 step periods, if longer) "
+                        "while the code changed is taken as stuck in a step: the group restarts with the new code "
+                        "(0: never)")
     p.add_argument("--no-warm-standby", dest="warm_standby", action="store_false",
                    default=os.environ.get("DEVSPACE_WARM_STANDBY", "1") != "0",
                    help="with several ranks, do not keep a second set of processes with torch imported to "

@@ -167,6 +167,8 @@ ENV = {
                             "`<url>/devspace-linux-amd64` and its `.sha256`).",
     "DEVSPACE_ROCM_IMAGE": "Base image `devspace init` writes for rocm-pytorch projects; must carry a concrete tag.",
     "DEVSPACE_SKIP_UPDATE_CHECK": "No daily check for a newer release.",
+    "DEVSPACE_STUCK_AFTER_S": "Seconds without the runner's loop coming round (or 50 step periods) after which an "
+                              "edit restarts a group stuck in a step (default 60, 0 = never; `--stuck-after`).",
     "DEVSPACE_SYNC_MODE": "Sync protocol: `helper` (default when `devspace-helper` ships next to the binary: "
                           "inotify in the pod, streamed archives; falls back to `fast` where it cannot run), `fast` "
                           "(POSIX tools only, event-driven) or `compat` (the original protocol and timing).",

@@ -721,3 +721,30 @@ def test_single_rank_hard_crash_is_restarted_in_the_container():
     assert d["faults"] == 2, d
     for ev in d["events"]:
         assert ev["first_loss"] == ev["resumed_from"] + 1 and ev["recovery_s"] < 10, ev
+
+
+@pytest.mark.parametrize("nproc", [1, 2])
+def test_an_edit_unsticks_a_rank_stuck_in_a_step(tmp_path, nproc):
+    """A step that never returns (a deadlocked loader, an endless loop) cannot pick up the fix:
+    the supervisor sees the rank's loop has not come round (no heartbeat) while the code changed,
+    and restarts the group with the new code, resuming from the last snapshot — with one rank as
+    well, which has no collective that could time out."""
+    trigger = tmp_path.parent / (tmp_path.name + "-hang")
+    entry = tmp_path / "train.py"
+    entry.write_text(RESCUE_STEP.replace("import time\n", "import os\nimport time\n", 1).replace(
+        "    if MARKER == \"bad\" and ctx.rank == 1:",
+        f"    if os.path.exists({str(trigger)!r}) and MARKER == \"v0\":\n        time.sleep(3600)\n"
+        "    if MARKER == \"bad\" and ctx.rank == 1:", 1))
+    r = Runner(tmp_path, entry, nproc, extra_args=("--log-every", "20", "--rescue-every", "0.5", "--stuck-after", "2"))
+    try:
+        r.until(r"started gen=1 marker=v0", timeout=180)
+        r.until(r"rescue snapshot step=\d+ ", timeout=60)
+        trigger.write_text("1")
+        time.sleep(3.0)  # every rank is now stuck (the peers of a stuck rank wait in its collective)
+        _set_marker(entry, "fixed")
+        r.until(r"made no progress for \d+ s and the code changed since", timeout=60)
+        r.until(r"restored step=\d+ ", timeout=120)
+        r.until(r"started gen=1 marker=fixed", timeout=60)
+        r.until(r"step=\d+ gen=1 ", timeout=60)  # and trains
+    finally:
+        r.stop()
