@@ -1804,16 +1804,17 @@ def parse_args(argv=None):
                    help="seconds between snapshots of the training state in shared memory, from which a "
                         "group restarted after a failure resumes (0: off)")
     p.add_argument("--rescue-dir", default="",
-                   help="keep the snapshots here, also after exit (default: in a pod, /dev/shm for the pod's "
-                        "lifetime, dropped at a clean stop; elsewhere, one rank: none, several: for the run)")
+                   help="keep the snapshots here, also after exit, and take a last one at a clean stop (default: "
+                        "in a pod, /dev/shm for the pod's lifetime, dropped at a clean stop; elsewhere, /dev/shm "
+                        "for the run)")
     p.add_argument("--stuck-after", type=float, default=float(os.environ.get("DEVSPACE_STUCK_AFTER_S", "60")),
                    help="a rank whose loop has not come round for this long (or 50 step periods, if longer) "
                         "while the code changed is taken as stuck in a step: the group restarts with the new code "
                         "(0: never)")
     p.add_argument("--no-warm-standby", dest="warm_standby", action="store_false",
                    default=os.environ.get("DEVSPACE_WARM_STANDBY", "1") != "0",
-                   help="with several ranks, do not keep a second set of processes with torch imported to "
-                        "replace a failed group (the restart then pays the interpreter and torch start-up)")
+                   help="do not keep a second set of rank processes with torch imported to replace a failed "
+                        "group (a restart then pays the interpreter and torch start-up)")
     p.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--standby", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args(argv)
