@@ -30,7 +30,11 @@ wss, client certificates) as every real cluster does (`--transport plain` for ws
      itself): examples/rocm-pytorch, a bf16 TinyLM training pod, one process per GPU under the
      hot-reload runner with an RCCL group. One sample = edit train.py -> synced -> the runner swaps
      the code at the step boundary -> first step with the new code done on every GPU -> its log
-     line reaches `devspace dev`. Plus its reference-equivalent (compat sync + cold restart).
+     line reaches `devspace dev`. Plus its reference-equivalent (compat sync + cold restart), and
+     a fault drill at the end: an edit makes one rank fail once; the group is replaced from the
+     runner's warm standby and resumes from its last rescue snapshot.
+  wan: the headline loop, its reference column and the deploy with the cluster behind a shaped
+     30 ms RTT / 100 Mbit/s link (devspace_amd/localkube/netem.py).
   php_mysql, microservices, kaniko — BASELINE configs[1-3]: deploy cold/warm and edit -> bytes in
      the pod(s) p50 (microservices: both services edited at once, two sync paths, two port
      forwards; kaniko: in-cluster build with the context uploaded over exec), each with the
