@@ -86,6 +86,26 @@ def render(path):
             rows.append((f"edit → pod hot-reload p50, rocm-pytorch ({g.get('parallelism')}, fused={g.get('fused_ops')})",
                          f"**{_ms(g['reload_p50_ms'])}** (sync {_ms(g.get('sync_p50_ms'))})",
                          _ms(gr.get("p50_ms")) + " (compat sync + cold workload restart)" if gr else "—"))
+        drill = g.get("fault_drill") if isinstance(g, dict) else None
+        if isinstance(drill, dict) and drill.get("recovered"):
+            rows.append((f"rocm-pytorch fault drill ({drill.get('failure', 'one rank fails')}): failure → training again",
+                         f"{_s(drill.get('failure_to_training_s'))} (warm standby: "
+                         f"{'yes' if drill.get('warm_standby') else 'no'}; resumed at step "
+                         f"{drill.get('resumed_from_step')})", "— (the process restarts from step 0)"))
+        w = b.get("wan")
+        if isinstance(w, dict) and "p50_ms" in w:
+            wr = w.get("reference_equivalent", {})
+            rows.append((f"edit → new response p50, quickstart, cluster behind {w.get('rtt_ms')} ms RTT / "
+                         f"{w.get('mbit')} Mbit/s (sync p50)",
+                         f"**{_ms(w['p50_ms'])}** (sync {_ms(w.get('sync_p50_ms'))})",
+                         (f"{_ms(wr.get('p50_ms'))} (sync {_ms(wr.get('sync_p50_ms'))})" + _x(w["p50_ms"], wr.get("p50_ms")))
+                         if wr else "—"))
+            wd = w.get("deploy")
+            if isinstance(wd, dict) and "wall_clock_s" in wd:
+                wdr = wd.get("reference_equivalent", {})
+                rows.append((f"`devspace deploy` quickstart across that link, cold",
+                             f"{_s(wd['wall_clock_s'])}",
+                             _s(wdr.get("wall_clock_s")) + _x(wd["wall_clock_s"], wdr.get("wall_clock_s")) if wdr else "—"))
         for key, label in (("php_mysql", "php-mysql"), ("microservices", "microservices"), ("kaniko", "kaniko")):
             e = b.get(key)
             if isinstance(e, dict) and "edit_to_pod_p50_ms" in e:
