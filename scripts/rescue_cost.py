@@ -60,12 +60,24 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--every", type=float, default=2.0)
     ap.add_argument("--snapshots", type=int, default=3)
+    ap.add_argument("--layers", type=int, default=0, help="TinyLM layers (default: the example's)")
+    ap.add_argument("--dim", type=int, default=0, help="TinyLM width (default: the example's)")
     args = ap.parse_args()
     work = tempfile.mkdtemp(prefix="rescue-cost-")
     try:
         app = os.path.join(work, "app")
         shutil.copytree(os.path.join(ROOT, "examples", "rocm-pytorch"), app,
                         ignore=shutil.ignore_patterns("devspace_amd", "__pycache__"))
+        if args.layers or args.dim:  # a bigger model than the example's, same code
+            import re
+
+            train = os.path.join(app, "train.py")
+            src = open(train).read()
+            if args.layers:
+                src = re.sub(r"^LAYERS = \d+$", f"LAYERS = {args.layers}", src, count=1, flags=re.M)
+            if args.dim:
+                src = re.sub(r"^DIM = \d+$", f"DIM = {args.dim}", src, count=1, flags=re.M)
+            open(train, "w").write(src)
         keep = os.path.join(work, "rescue")
         env = dict(os.environ, PYTHONPATH=ROOT)
         cmd = [sys.executable, "-u", "-m", "devspace_amd.runner", "--watch", app, "--log-every", "5",
@@ -94,6 +106,7 @@ def main():
         out = {
             "what": "examples/rocm-pytorch TinyLM under the runner: rescue snapshots every "
                     f"{args.every:g} s, SIGKILL, restart with the same --rescue-dir",
+            "model": {"layers": args.layers or "example", "dim": args.dim or "example"},
             "snapshots": snaps,
             "pause_ms_p50": sorted(s["pause_ms"] for s in snaps)[len(snaps) // 2],
             "write_ms_p50": sorted(s["write_ms"] for s in snaps)[len(snaps) // 2],
