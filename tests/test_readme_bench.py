@@ -61,3 +61,12 @@ def test_round3_line_renders_all_extras(tmp_path):
     r = readme.read_text()
     assert r.startswith("x\n<!-- bench-table source=BENCH_r99.json -->\nDriver run") and r.endswith(
         "<!-- /bench-table -->\ny\n") and "STALE-TABLE" not in r
+
+
+def test_round4_line_renders_the_drill_and_wan_rows():
+    """A round-4 line (the builder's last MI355X run) carries the fault drill and the WAN columns;
+    the table shows them once the driver's file has them."""
+    out = _bt().render(os.path.join(ROOT, "profiles", "r4_bench_gpu_final.json"))
+    assert "fault drill (hard crash (os._exit) of the only rank)" in out and "warm standby: yes" in out
+    assert re.search(r"cluster behind 30 ms RTT / 100 Mbit/s .*\| \*\*\d+ ms\*\* \(sync [\d.]+ ms\) \|", out), out
+    assert "`devspace deploy` quickstart across that link, cold" in out
