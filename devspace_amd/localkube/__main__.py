@@ -1,5 +1,6 @@
 """python -m devspace_amd.localkube up --state DIR [--port P] [--gpus N] [--kubeconfig PATH] [--context NAME] [--tls]
-                                   [--throttle-first K --retry-after S]"""
+                                   [--throttle-first K --retry-after S] [--partition spx|dpx|qpx|cpx]
+                                   [--nps nps1|nps2] [--resource-strategy single|mixed] [--unhealthy K]"""
 import argparse
 import os
 import signal
@@ -25,8 +26,16 @@ def main(argv=None):
     up.add_argument("--retry-after", type=int, default=1, help="Retry-After seconds of the throttled answers")
     up.add_argument("--pull-seconds", type=float, default=0.0,
                     help="slow-pull mode: every image takes this long to pull the first time (Pulling events)")
+    up.add_argument("--partition", default="spx", choices=("spx", "dpx", "qpx", "cpx"),
+                    help="compute partition mode of the node's GPUs (CPX: 8 devices per MI355X)")
+    up.add_argument("--nps", default="nps1", help="memory partition mode (node labeller label)")
+    up.add_argument("--resource-strategy", default="single", choices=("single", "mixed"),
+                    help="device plugin naming: amd.com/gpu, or amd.com/<partition>_<nps>")
+    up.add_argument("--unhealthy", type=int, default=0, help="devices the device plugin reports unhealthy")
     args = ap.parse_args(argv)
-    c = LocalCluster(args.state, port=args.port, gpus=args.gpus, context=args.context, tls=args.tls).start()
+    c = LocalCluster(args.state, port=args.port, gpus=args.gpus, context=args.context, tls=args.tls,
+                     gpu_partition=args.partition, memory_partition=args.nps, gpu_strategy=args.resource_strategy,
+                     unhealthy_gpus=args.unhealthy).start()
     c.api.reset_throttle(args.throttle_first, args.retry_after)
     c.kubelet.pull_seconds = args.pull_seconds
     kc = args.kubeconfig or os.path.join(args.state, "kubeconfig")

@@ -85,7 +85,8 @@ def _b64file(path):
 
 class LocalCluster:
     def __init__(self, state_dir, port=0, gpus=None, context="devspace-local", extra_env=None, tls=False,
-                 token_validator=None):
+                 token_validator=None, gpu_partition="spx", memory_partition="nps1", gpu_strategy="single",
+                 unhealthy_gpus=0):
         self.state_dir = os.path.abspath(state_dir)
         self.tls = tls
         self.pki = make_pki(os.path.join(self.state_dir, "pki")) if tls else None
@@ -98,6 +99,9 @@ class LocalCluster:
         env = {"PYTHONPATH": ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")}
         env.update(extra_env or {})
         self.kubelet = Kubelet(self.store, self.images, self.state_dir, gpus=self.gpus, extra_env=env)
+        # SPX/DPX/QPX/CPX compute partitions, NPS memory mode, single/mixed resource naming and
+        # devices the device plugin marked unhealthy, as an MI355X node would advertise them
+        self.kubelet.set_gpu_topology(gpu_partition, memory_partition, gpu_strategy, unhealthy_gpus)
         self.api = ApiServer(self.store, self.kubelet, token_validator=token_validator)
         self.docker_sock = os.path.join(self.state_dir, "docker.sock")
         self.loop = None

@@ -54,10 +54,14 @@ RUNTIME_ALIASES = {
 }
 
 
-def _gpu_request(container):
+# AMD GPU device plugin: compute partitions per GPU by mode (MI355X: 8 XCDs, one per CPX partition)
+PARTITIONS = {"spx": 1, "dpx": 2, "qpx": 4, "cpx": 8}
+
+
+def _gpu_request(container, resource=GPU_RESOURCE):
     res = container.get("resources") or {}
     for part in ("limits", "requests"):
-        v = (res.get(part) or {}).get(GPU_RESOURCE)
+        v = (res.get(part) or {}).get(resource)
         if v is not None:
             try:
                 return int(str(v))
@@ -133,8 +137,11 @@ class Kubelet:
         self.images = images
         self.state_dir = state_dir
         self.node_name = node_name
-        self.gpus_total = gpus
+        self.physical_gpus = gpus
+        self.gpus_total = gpus  # schedulable devices: GPUs, or compute partitions of them
         self.gpus_free = list(range(gpus))
+        self.partition, self.memory_partition, self.gpu_resource = "spx", "nps1", GPU_RESOURCE
+        self.unhealthy = 0
         self.pods = {}  # (ns, name) -> PodRuntime
         self.extra_env = extra_env or {}
         self.pods_dir = os.path.join(state_dir, "pods")
@@ -151,7 +158,22 @@ class Kubelet:
 
     # ------------------------------------------------------------ node
 
+    def set_gpu_topology(self, partition="spx", memory_partition="nps1", strategy="single", unhealthy=0):
+        """What the AMD GPU device plugin and node labeller would show for this node: each GPU in
+        `partition` mode is 1 (SPX), 2 (DPX), 4 (QPX) or 8 (CPX) schedulable devices, advertised as
+        amd.com/gpu ("single" strategy) or amd.com/<partition>_<nps> ("mixed"); `unhealthy` devices
+        stay in capacity but leave allocatable (the plugin's health check). Call before start()."""
+        partition, memory_partition = partition.lower(), memory_partition.lower()
+        if partition not in PARTITIONS:
+            raise ValueError(f"unknown compute partition mode {partition!r}")
+        self.partition, self.memory_partition = partition, memory_partition
+        self.gpu_resource = GPU_RESOURCE if strategy == "single" else f"amd.com/{partition}_{memory_partition}"
+        self.gpus_total = self.physical_gpus * PARTITIONS[partition]
+        self.unhealthy = max(0, min(unhealthy, self.gpus_total))
+        self.gpus_free = list(range(self.gpus_total - self.unhealthy))  # the last ones failed
+
     def register_node(self):
+        res = self.gpu_resource
         node = {
             "apiVersion": "v1",
             "kind": "Node",
@@ -162,11 +184,15 @@ class Kubelet:
                     "beta.amd.com/gpu.family.AI": "1" if self.gpus_total else "0",
                     "amd.com/gpu.product-name": "AMD_Instinct_MI355X" if self.gpus_total else "",
                     "amd.com/gpu.device-id": "75a3" if self.gpus_total else "",
+                    **({"amd.com/gpu.vram": "288G",
+                        "amd.com/gpu.compute-partitioning-mode": self.partition,
+                        "amd.com/gpu.memory-partitioning-mode": self.memory_partition} if self.gpus_total else {}),
                 },
             },
             "status": {
-                "capacity": {"cpu": str(os.cpu_count() or 1), "memory": "64Gi", GPU_RESOURCE: str(self.gpus_total)},
-                "allocatable": {"cpu": str(os.cpu_count() or 1), "memory": "64Gi", GPU_RESOURCE: str(self.gpus_total)},
+                "capacity": {"cpu": str(os.cpu_count() or 1), "memory": "64Gi", res: str(self.gpus_total)},
+                "allocatable": {"cpu": str(os.cpu_count() or 1), "memory": "64Gi",
+                                res: str(self.gpus_total - self.unhealthy)},
                 "conditions": [{"type": "Ready", "status": "True"}],
                 "nodeInfo": {"kubeletVersion": "v1.29.0-devspace-local", "osImage": "local processes"},
             },
@@ -405,11 +431,11 @@ class Kubelet:
     def _admit(self, pod):
         md = pod["metadata"]
         containers = pod.get("spec", {}).get("containers", []) or []
-        want = sum(_gpu_request(c) for c in containers)
+        want = sum(_gpu_request(c, self.gpu_resource) for c in containers)
         if want > len(self.gpus_free):
             st = pod.get("status") or {}
             if not any(c.get("reason") == "Unschedulable" for c in st.get("conditions") or []):
-                msg = f"0/1 nodes are available: 1 Insufficient {GPU_RESOURCE}."
+                msg = f"0/1 nodes are available: 1 Insufficient {self.gpu_resource}."
                 self.store.update_status("", "pods", md["namespace"], md["name"], {
                     "phase": "Pending", "conditions": [{"type": "PodScheduled", "status": "False",
                                                         "reason": "Unschedulable", "message": msg}]})
@@ -542,7 +568,9 @@ class Kubelet:
             # smaller box) maps its extra indices onto the real devices instead of naming devices
             # this process may not use.
             real = self._real_gpus()
-            ids = [host_vis[g] if g < len(host_vis) else str(g) for g in ((g % real if real else g) for g in rt.gpus)]
+            parts = PARTITIONS.get(self.partition, 1)  # a partition runs on its GPU (g // parts)
+            phys = [g // parts for g in rt.gpus]
+            ids = [host_vis[g] if g < len(host_vis) else str(g) for g in ((g % real if real else g) for g in phys)]
             env["HIP_VISIBLE_DEVICES"] = ",".join(dict.fromkeys(ids))
         elif self.gpus_total:
             env["HIP_VISIBLE_DEVICES"] = "-1"  # no amd.com/gpu request: no GPU access

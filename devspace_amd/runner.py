@@ -65,24 +65,19 @@ import argparse
 import hashlib
 import importlib.machinery
 import importlib.util
-import mmap
 import os
-import re
 import signal
-import subprocess
 import sys
 import threading
 import time
 import traceback
 import types
 
-PREFIX = "[devspace-runner]"
-
-
-def _log(msg: str) -> None:
-    sys.stdout.write(f"{PREFIX} {msg}\n")
-    sys.stdout.flush()
-
+from devspace_amd.changefeed import (  # noqa: F401  (re-exported: tests and tools use runner.*)
+    PREFIX, SYNC_TMP_SUFFIX, ChangeFeed, _IGNORED_DIRS, _ignored, _InotifyWatcher, _log, _PollWatcher, make_watcher)
+from devspace_amd.rescue import (  # noqa: F401
+    Rescue, RescueSkipped, _default_rescue_dir, _drop_rescue_dir, _in_pod, _rescue_final, _rescue_finish,
+    _rescue_restore)
 
 # exit codes of a worker that leaves its group on purpose (the supervisor restarts the group)
 EXIT_STEP_FAILED = 3
@@ -111,139 +106,6 @@ def _fatal(code: int) -> None:
     finally:
         os._exit(code)
 
-
-class _PollWatcher:
-    """Fallback watcher when the native inotify binding is unavailable."""
-
-    def __init__(self, path: str):
-        self.path = path
-        self.state = self._scan()
-
-    def _scan(self):
-        out = {}
-        for root, dirs, files in os.walk(self.path):
-            dirs[:] = [d for d in dirs if d not in ("__pycache__", ".git")]
-            for f in files:
-                p = os.path.join(root, f)
-                try:
-                    st = os.stat(p)
-                except OSError:
-                    continue
-                out[p] = (st.st_mtime_ns, st.st_size)
-        return out
-
-    def poll(self, timeout_ms: int = 0):
-        deadline = time.monotonic() + timeout_ms / 1000.0
-        while True:
-            now = self._scan()
-            changed = [p for p, s in now.items() if self.state.get(p) != s]
-            changed += [p for p in self.state if p not in now]
-            self.state = now
-            if changed or time.monotonic() >= deadline:
-                return changed
-            time.sleep(0.005)
-
-    def close(self):
-        pass
-
-
-class _InotifyWatcher:
-    """inotify through ctypes: what the runner uses inside a pod, where the native module
-    (built for the developer machine's Python) is not importable. Recursive, settled events
-    only (close-after-write, renames, deletes), so a file still being written triggers nothing."""
-
-    _IN_CLOSE_WRITE, _IN_MOVED_FROM, _IN_MOVED_TO = 0x008, 0x040, 0x080
-    _IN_CREATE, _IN_DELETE, _IN_DELETE_SELF, _IN_Q_OVERFLOW = 0x100, 0x200, 0x400, 0x4000
-    _IN_ISDIR, _IN_IGNORED, _IN_NONBLOCK, _IN_CLOEXEC = 0x40000000, 0x8000, 0o4000, 0o2000000
-
-    def __init__(self, path: str):
-        import ctypes
-        import ctypes.util
-
-        self._libc = ctypes.CDLL(ctypes.util.find_library("c") or "libc.so.6", use_errno=True)
-        self.fd = self._libc.inotify_init1(self._IN_NONBLOCK | self._IN_CLOEXEC)
-        if self.fd < 0:
-            raise OSError(ctypes.get_errno(), "inotify_init1 failed")
-        self.mask = (self._IN_CLOSE_WRITE | self._IN_MOVED_FROM | self._IN_MOVED_TO | self._IN_CREATE |
-                     self._IN_DELETE | self._IN_DELETE_SELF)
-        self.wds = {}
-        self._add_tree(path)
-
-    def _add(self, d: str) -> None:
-        wd = self._libc.inotify_add_watch(self.fd, os.fsencode(d), self.mask)
-        if wd >= 0:
-            self.wds[wd] = d
-
-    def _add_tree(self, root: str) -> None:
-        for d, dirs, _ in os.walk(root):
-            dirs[:] = [x for x in dirs if x not in ("__pycache__", ".git")]
-            self._add(d)
-
-    def poll(self, timeout_ms: int = 0):
-        import select
-        import struct
-
-        out = []
-        r, _, _ = select.select([self.fd], [], [], max(0, timeout_ms) / 1000.0)
-        if not r:
-            return out
-        while True:
-            try:
-                buf = os.read(self.fd, 1 << 16)
-            except BlockingIOError:
-                break
-            off = 0
-            while off + 16 <= len(buf):
-                wd, mask, _cookie, n = struct.unpack_from("iIII", buf, off)
-                name = buf[off + 16:off + 16 + n].split(b"\0", 1)[0].decode(errors="replace")
-                off += 16 + n
-                if mask & self._IN_IGNORED:
-                    self.wds.pop(wd, None)
-                    continue
-                if mask & self._IN_Q_OVERFLOW:
-                    out.append(next(iter(self.wds.values()), ""))  # events were lost: reload
-                    continue
-                base = self.wds.get(wd)
-                if base is None:
-                    continue
-                p = os.path.join(base, name) if name else base
-                if mask & self._IN_ISDIR:
-                    if mask & (self._IN_CREATE | self._IN_MOVED_TO):
-                        self._add_tree(p)
-                    continue
-                if mask & self._IN_CREATE:
-                    continue  # wait for its close-after-write
-                out.append(p)
-            # the rest of a burst (an editor's write + rename) lands within microseconds: take
-            # what follows within 0.25 ms. (This was 2 ms: a fixed 2 ms on every synced edit,
-            # measured as the GPU pod's `other_ms`. The sync helper's own temp file, written
-            # before its rename into place, is filtered by name in the change feed instead.)
-            r, _, _ = select.select([self.fd], [], [], 0.00025)
-            if not r:
-                break
-        return out
-
-    def close(self):
-        if self.fd >= 0:
-            os.close(self.fd)
-            self.fd = -1
-
-
-def make_watcher(path: str):
-    settled = os.environ.get("DEVSPACE_WATCH_SETTLED", "1") != "0"
-    try:
-        from devspace_amd import _native  # noqa: WPS433
-
-        # settled events only: a file still being written must not trigger (or preempt) a reload
-        return _native.Watcher(path, settled_only=settled)
-    except Exception:  # native module missing: a vendored runner inside a pod
-        pass
-    if settled and sys.platform.startswith("linux"):
-        try:
-            return _InotifyWatcher(path)
-        except OSError:
-            pass
-    return _PollWatcher(path)
 
 
 class Preempted(BaseException):
@@ -378,300 +240,6 @@ class Context:
             time.sleep(0)  # releases the GIL: the change feed thread can post the edit
 
 
-def _close_mapping(mm) -> None:
-    try:
-        mm.close()
-    except BufferError:  # a tensor view still alive (an exception's frame): the GC closes it
-        pass
-
-
-class RescueSkipped(Exception):
-    """A snapshot that cannot be taken this time (not enough shared memory) or ever (the state
-    holds something that is not tensors, containers and scalars)."""
-
-
-class Rescue:
-    """Training state that survives a restart of the group.
-
-    The reference's restart-per-change model (nodemon, redeploy) starts every process from
-    nothing, which is right for a web app and ruinous for a training run: a rank failure an
-    hour in would cost the hour. Every `every_s` seconds (rank 0's clock, decided at a step
-    boundary for all ranks together) each rank copies its state into shared memory
-    (`rank<r>-step<N>.bin` raw tensor bytes + `.json` layout, written under temp names and
-    renamed); once every rank wrote step N the older snapshots are dropped. A group started
-    after a failure runs `setup()` and then loads the newest step that every rank holds, with
-    the same SETUP_VERSION; a restore that fails on any rank runs `setup()` again everywhere.
-
-    HBM staging (MI355X: 288 GB per GPU, rarely all of it in use): when the free HBM holds a
-    second copy of the state's device tensors, the snapshot is a device-to-device copy on the
-    training stream (HBM bandwidth: well under a millisecond for the example's 384 MiB) and a
-    background thread streams that copy to shared memory on a side stream while training goes
-    on. Training pauses only for the device copy; the ranks agree that every writer finished
-    (two flags of the step-boundary all-reduce) before the older snapshots are dropped. Without
-    room in HBM (or on CPU) the copy to shared memory is made at the boundary itself.
-
-    What is captured: a module's own `snapshot(ctx, state) -> obj` / `restore(ctx, state, obj)`
-    when it defines them; otherwise, of a dict state, every entry with `state_dict()` /
-    `load_state_dict()` (modules, DDP, optimizers, schedulers, grad scalers), plain tensors and
-    scalars. Tensors come back on the device they were on (cuda → this rank's GPU)."""
-
-    ALIGN = 64
-
-    def __init__(self, root: str, rank: int, every_s: float):
-        self.root = root
-        self.rank = rank
-        self.every_s = every_s
-        self.last = time.monotonic()
-        self.last_step = 0
-        self.disabled = None  # why snapshots stopped for good
-        self.inflight = None  # the snapshot being written (see begin / finish)
-        self.staging = os.environ.get("DEVSPACE_RESCUE_STAGING", "1") != "0"
-        self._side = None  # the writer's HIP stream
-        os.makedirs(root, exist_ok=True)
-
-    # -- capture / apply ------------------------------------------------------------------
-    @staticmethod
-    def capture(mod, ctx, state):
-        import torch
-
-        if hasattr(mod, "snapshot"):
-            return mod.snapshot(ctx, state)
-        if not isinstance(state, dict):
-            return None
-        out = {}
-        for k, v in state.items():
-            if callable(getattr(v, "state_dict", None)) and callable(getattr(v, "load_state_dict", None)):
-                out[k] = v.state_dict()
-            elif isinstance(v, torch.Tensor) or v is None or isinstance(v, (bool, int, float, str)):
-                out[k] = v
-        return out or None
-
-    @staticmethod
-    def apply(mod, ctx, state, snap):
-        import torch
-
-        if hasattr(mod, "restore"):
-            r = mod.restore(ctx, state, snap)
-            return state if r is None else r
-        for k, v in snap.items():
-            cur = state.get(k)
-            if callable(getattr(cur, "load_state_dict", None)) and isinstance(v, dict):
-                cur.load_state_dict(v)
-            elif isinstance(cur, torch.Tensor) and isinstance(v, torch.Tensor):
-                if cur.shape != v.shape:
-                    raise ValueError(f"state[{k!r}]: shape {tuple(cur.shape)} now, {tuple(v.shape)} in the snapshot")
-                with torch.no_grad():
-                    cur.copy_(v)
-            elif k in state:
-                state[k] = v
-        return state
-
-    @classmethod
-    def _encode(cls, obj, tensors):
-        import torch
-
-        if isinstance(obj, torch.Tensor):
-            tensors.append(obj)
-            return {"T": len(tensors) - 1}
-        if isinstance(obj, dict):
-            return {"D": [[cls._encode(k, tensors), cls._encode(v, tensors)] for k, v in obj.items()]}
-        if isinstance(obj, tuple):
-            return {"U": [cls._encode(v, tensors) for v in obj]}
-        if isinstance(obj, list):
-            return [cls._encode(v, tensors) for v in obj]
-        if obj is None or isinstance(obj, (bool, int, float, str)):
-            return obj
-        raise RescueSkipped(f"cannot snapshot a {type(obj).__name__} (define snapshot()/restore())")
-
-    @classmethod
-    def _decode(cls, obj, tensors):
-        if isinstance(obj, list):
-            return [cls._decode(v, tensors) for v in obj]
-        if isinstance(obj, dict):
-            if "T" in obj:
-                return tensors[obj["T"]]
-            if "U" in obj:
-                return tuple(cls._decode(v, tensors) for v in obj["U"])
-            return {cls._decode(k, tensors): cls._decode(v, tensors) for k, v in obj["D"]}
-        return obj
-
-    # -- files -----------------------------------------------------------------------------
-    def _path(self, step, ext, rank=None):
-        return os.path.join(self.root, f"rank{self.rank if rank is None else rank}-step{step}.{ext}")
-
-    def due(self, step: int) -> bool:
-        return (self.every_s > 0 and self.disabled is None and self.inflight is None and step > self.last_step
-                and time.monotonic() - self.last >= self.every_s)
-
-    @staticmethod
-    def _hbm_room(nbytes: int, device) -> bool:
-        import torch
-
-        try:
-            free, _ = torch.cuda.mem_get_info(device)
-            cached = torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
-        except RuntimeError:  # no answer from the runtime: copy at the boundary instead
-            return False
-        return free + cached >= nbytes * 1.1 + (256 << 20)
-
-    def begin(self, mod, ctx, state, gen, setup_version) -> None:
-        """Starts this rank's snapshot of `state` at ctx.step (self.inflight): staged in HBM and
-        written by a background thread, or written here. Errors end up in the job, never raised:
-        every rank must reach the next boundary with a job to agree on."""
-        import shutil
-
-        import torch
-
-        t0 = time.perf_counter()
-        job = {"step": ctx.step, "gen": gen, "bytes": 0, "err": None, "done": False, "staged": False,
-               "pause_ms": 0.0, "write_ms": 0.0}
-        self.inflight = job
-        try:
-            tensors = []
-            tree = self._encode(self.capture(mod, ctx, state), tensors)
-            metas, off = [], 0
-            for t in tensors:
-                n = t.numel() * t.element_size()
-                metas.append({"dtype": str(t.dtype).replace("torch.", ""), "shape": list(t.shape),
-                              "device": t.device.type, "offset": off, "nbytes": n})
-                off += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
-            job["bytes"] = off
-            # the ranks of the pod write theirs into the same /dev/shm at the same time
-            free, need = shutil.disk_usage(self.root).free, off * ctx.world_size
-            if need > free * 0.9:
-                raise RescueSkipped(f"{self.root} has {free >> 20} MiB free, a snapshot of every rank needs "
-                                    f"{need >> 20} MiB")
-            meta = {"step": ctx.step, "gen": gen, "setup_version": setup_version, "world": ctx.world_size,
-                    "time": time.time(), "bytes": off, "tensors": metas, "tree": tree}
-            dev_bytes = sum(m["nbytes"] for m in metas if m["device"] == "cuda")
-            if self.staging and dev_bytes and ctx.device.type == "cuda" and self._hbm_room(dev_bytes, ctx.device):
-                start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                with torch.no_grad():
-                    start.record()
-                    copies = [t.detach().clone() for t in tensors]  # host tensors change too
-                    end.record()
-                job["staged"] = True
-                job["thread"] = threading.Thread(target=self._write_job, name="devspace-rescue-writer", daemon=True,
-                                                 args=(job, copies, meta, ctx.device, (start, end)))
-                job["thread"].start()
-            else:
-                self._write_job(job, [t.detach() for t in tensors], meta, None, None)
-                job["pause_ms"] = (time.perf_counter() - t0) * 1000.0
-        except Exception as e:  # RescueSkipped, an unsupported type in the state, a device error
-            job["err"] = str(e) if isinstance(e, RescueSkipped) else f"{type(e).__name__}: {e}"
-            job["done"] = True
-
-    def _write_job(self, job, tensors, meta, device, events) -> None:
-        import torch
-
-        t0 = time.perf_counter()
-        try:
-            if events is not None:
-                torch.cuda.set_device(device)  # this thread's current device (HIP's is per thread)
-                if self._side is None:
-                    self._side = torch.cuda.Stream(device=device)
-                self._side.wait_event(events[1])
-                with torch.cuda.stream(self._side):
-                    self._write(job["step"], tensors, meta)
-                job["pause_ms"] = events[0].elapsed_time(events[1])
-            else:
-                self._write(job["step"], tensors, meta)
-        except Exception as e:  # shared memory full (SIGBUS is not an exception: sized above), I/O
-            job["err"] = f"{type(e).__name__}: {e}"
-        finally:
-            del tensors[:]  # the HBM copies go back to the caching allocator
-            job["write_ms"] = (time.perf_counter() - t0) * 1000.0
-            job["done"] = True
-
-    def _write(self, step, tensors, meta) -> None:
-        import json
-
-        import torch
-
-        off = meta["bytes"]
-        binp, jsp = self._path(step, "bin"), self._path(step, "json")
-        with open(binp + ".tmp", "w+b") as f:
-            if off:
-                # reserve the pages first: a full tmpfs then fails here (ENOSPC), not as a SIGBUS
-                # on a store into the mapping
-                os.posix_fallocate(f.fileno(), 0, off)
-                # one copy per tensor, device (or host) straight into the mapped shared memory
-                mm = mmap.mmap(f.fileno(), off)
-                try:
-                    buf = torch.frombuffer(mm, dtype=torch.uint8)
-                    for t, m in zip(tensors, meta["tensors"]):
-                        if m["nbytes"]:
-                            buf[m["offset"]:m["offset"] + m["nbytes"]].view(t.dtype).view(t.shape).copy_(t)
-                    del buf
-                finally:
-                    _close_mapping(mm)
-        with open(jsp + ".tmp", "w") as f:
-            json.dump(meta, f)
-        os.replace(binp + ".tmp", binp)
-        os.replace(jsp + ".tmp", jsp)  # the layout last: its presence marks a complete snapshot
-
-    def commit(self, step: int, ok: bool) -> None:
-        """Every rank wrote `step` (ok): drop the older snapshots; else drop this one."""
-        for name in os.listdir(self.root):
-            m = re.match(rf"rank{self.rank}-step(\d+)\.(bin|json)(\.tmp)?$", name)
-            if m and (int(m.group(1)) != step if ok else int(m.group(1)) == step):
-                try:
-                    os.unlink(os.path.join(self.root, name))
-                except OSError:
-                    pass
-        if ok:
-            self.last_step = step
-        self.last = time.monotonic()
-
-    def available(self, setup_version, world) -> list:
-        import json
-
-        steps = []
-        for name in os.listdir(self.root):
-            m = re.match(rf"rank{self.rank}-step(\d+)\.json$", name)
-            if not m:
-                continue
-            try:
-                with open(os.path.join(self.root, name)) as f:
-                    meta = json.load(f)
-                size = os.path.getsize(self._path(int(m.group(1)), "bin"))
-            except (OSError, ValueError):
-                continue
-            if meta.get("setup_version") == setup_version and meta.get("world") == world and size == meta["bytes"]:
-                steps.append(int(m.group(1)))
-        return sorted(steps)
-
-    def load(self, step, device):
-        """(state tree with tensors materialised, metadata) of this rank's snapshot `step`."""
-        import json
-
-        import torch
-
-        with open(self._path(step, "json")) as f:
-            meta = json.load(f)
-        tensors = []
-        with open(self._path(step, "bin"), "rb") as f:
-            if os.fstat(f.fileno()).st_size != meta["bytes"]:
-                raise ValueError(f"snapshot step={step} is truncated")
-            mm = mmap.mmap(f.fileno(), meta["bytes"], access=mmap.ACCESS_COPY) if meta["bytes"] else None
-            try:
-                buf = torch.frombuffer(mm, dtype=torch.uint8) if mm is not None else None
-                for m in meta["tensors"]:
-                    dtype = getattr(torch, m["dtype"])
-                    if not m["nbytes"]:
-                        tensors.append(torch.empty(m["shape"], dtype=dtype))
-                        continue
-                    src = buf[m["offset"]:m["offset"] + m["nbytes"]].view(dtype).view(m["shape"])
-                    # own memory either way (the mapping is closed below)
-                    on_gpu = m["device"] == "cuda" and device.type == "cuda"
-                    tensors.append(src.to(device) if on_gpu else src.clone())
-                    del src
-                del buf
-            finally:
-                if mm is not None:
-                    _close_mapping(mm)
-        return self._decode(meta["tree"], tensors), meta
-
 
 def purge_user_modules(watch_dir: str) -> list:
     """Drops the modules imported from the synced tree (helpers the entry file imports) from
@@ -681,14 +249,14 @@ def purge_user_modules(watch_dir: str) -> list:
     import cache of a torch process holds thousands of modules)."""
     prefixes = tuple({os.path.abspath(watch_dir) + os.sep, os.path.realpath(watch_dir) + os.sep})
     root = os.path.realpath(watch_dir) + os.sep
-    me = os.path.realpath(__file__)
+    kit = os.path.dirname(os.path.realpath(__file__)) + os.sep  # the runner's own package (in /app in a pod)
     gone = []
     for name, m in list(sys.modules.items()):
         f = getattr(m, "__file__", None)
         if not f or name == "__main__" or not f.endswith(".py") or not f.startswith(prefixes):
             continue
         rf = os.path.realpath(f)
-        if rf.startswith(root) and rf != me and os.sep + "site-packages" + os.sep not in rf:
+        if rf.startswith(root) and not rf.startswith(kit) and os.sep + "site-packages" + os.sep not in rf:
             del sys.modules[name]
             gone.append(name)
     importlib.invalidate_caches()
@@ -899,161 +467,6 @@ def _try_load(entry, gen, feed, src):
         return None, traceback.format_exc()
 
 
-class ChangeFeed:
-    """Watches the synced directory on a background thread (the native inotify poll releases
-    the GIL) and pre-compiles the entry file as soon as it changes, so the code swap at the next
-    step boundary only has to exec it — the compile overlaps the in-flight GPU step."""
-
-    def __init__(self, watcher, entry):
-        self.watcher = watcher
-        self.entry = entry
-        self.cv = threading.Condition()
-        self.count = 0
-        self.first_t = None
-        self.prepared = None
-        self.entry_real = os.path.realpath(entry)
-        self.helper_changed = False  # a .py file other than the entry changed since the last take
-        self.stop = False
-        self.thread = threading.Thread(target=self._run, name="devspace-change-feed", daemon=True)
-        self.thread.start()
-
-    def _run(self):
-        while not self.stop:
-            try:
-                changed = [p for p in self.watcher.poll(100) if not _ignored(p)]
-            except Exception:  # pragma: no cover - watcher died; keep the loop alive
-                time.sleep(0.05)
-                continue
-            if not changed:
-                continue
-            t = time.perf_counter()
-            helper = any(p.endswith(".py") and os.path.realpath(p) != self.entry_real for p in changed)
-            # Compile, then post the change. (Posting first so that a step boundary reached
-            # during the compile waits for it measured 0.2-0.3 ms slower on MI355X,
-            # profiles/r2_feed_order_ab.jsonl.)
-            prep = None
-            try:
-                with open(self.entry, "rb") as f:
-                    src = f.read()
-                prep = (src, compile(src, self.entry, "exec"))
-            except Exception:  # syntax errors surface (with traceback) at the reload itself
-                prep = None
-            with self.cv:
-                self.count += 1
-                if self.first_t is None:
-                    self.first_t = t
-                self.prepared = prep
-                self.helper_changed = self.helper_changed or helper
-                self.cv.notify_all()
-
-    def pending(self) -> bool:
-        """A change batch arrived that the loop has not taken yet (lock-free read)."""
-        return self.count > 0
-
-    def take(self, timeout_s=0.0):
-        """(number of change batches since the last call, perf_counter of the first one,
-        whether a .py file other than the entry file changed in them)."""
-        with self.cv:
-            if self.count == 0 and timeout_s > 0:
-                self.cv.wait(timeout_s)
-            n, t, helper = self.count, self.first_t, self.helper_changed
-            self.count, self.first_t, self.helper_changed = 0, None, False
-            return n, t, helper
-
-    def prepared_for(self, src):
-        with self.cv:
-            p = self.prepared
-        return p[1] if p is not None and p[0] == src else None
-
-    def close(self):
-        self.stop = True
-        self.thread.join(1.0)
-
-
-# the in-pod sync helper writes `<name>.devspace-tmp` and renames it into place
-# (src/helper/helper.cc kTmpSuffix): only the rename is the edit
-SYNC_TMP_SUFFIX = ".devspace-tmp"
-
-
-_IGNORED_DIRS = []  # what the runner itself writes under the watched tree (a --rescue-dir there)
-
-
-def _ignored(p: str) -> bool:
-    base = os.path.basename(p)
-    return ("__pycache__" in p or base.endswith((".pyc", ".swp", "~", SYNC_TMP_SUFFIX)) or
-            base.startswith(".#") or any(p == d or p.startswith(d + os.sep) for d in _IGNORED_DIRS))
-
-
-def _rescue_finish(rescue, ctx, failed: bool) -> None:
-    """Every rank's writer is done (agreed at a boundary): keep this snapshot and drop the older
-    ones, or — it failed on some rank — drop it and stop taking snapshots, on every rank alike."""
-    job, rescue.inflight = rescue.inflight, None
-    rescue.commit(job["step"], not failed)
-    if failed:
-        why = job["err"] or "failed on another rank"
-        rescue.disabled = why
-        if job["err"]:
-            ctx.error(f"rescue snapshot step={job['step']} failed: {job['err']}")
-        ctx.log(f"rescue snapshots off ({why})")
-        return
-    how = "staged in HBM, written in the background" if job["staged"] else "written at the step boundary"
-    ctx.log(f"rescue snapshot step={job['step']} gen={job['gen']} {job['bytes'] / 2**20:.1f} MiB/rank: "
-            f"training paused {job['pause_ms']:.2f} ms, {how} in {job['write_ms']:.1f} ms")
-
-
-def _rescue_final(rescue, agree, mod, ctx, state, gen, setup_version) -> None:
-    """Stopping with an explicit --rescue-dir (a volume that outlives the pod): the snapshot in
-    flight is finished and one more is taken where training stopped, so the next start — a new
-    pod after `devspace purge`, tomorrow — resumes at that step."""
-    def settle():
-        job = rescue.inflight
-        if job is None:
-            return
-        if job.get("thread") is not None:
-            job["thread"].join()
-        errs = agree.gather(job["err"]) if agree is not None else [job["err"]]
-        _rescue_finish(rescue, ctx, any(e is not None for e in errs))
-
-    settle()
-    if rescue.disabled is None and ctx.step > rescue.last_step:  # the same decision on every rank
-        ctx.log(f"stopping: a last rescue snapshot at step={ctx.step} in {rescue.root}")
-        rescue.begin(mod, ctx, state, gen, setup_version)
-        settle()
-
-
-def _rescue_restore(rescue, agree, mod, ctx, state):
-    """After setup() of a (re)started group: the newest snapshot every rank holds for this
-    SETUP_VERSION, loaded on every rank, or none at all."""
-    setup_version = getattr(mod, "SETUP_VERSION", None)
-    steps = rescue.available(setup_version, ctx.world_size)
-    held = agree.gather(steps) if agree is not None else [steps]
-    common = set(held[0]).intersection(*[set(h) for h in held[1:]])
-    if not common:
-        if any(held):
-            ctx.log("rescue: no snapshot that every rank holds for this SETUP_VERSION: starting from setup()")
-        return state
-    step = max(common)
-    t0 = time.perf_counter()
-    err, meta = None, None
-    try:
-        snap, meta = rescue.load(step, ctx.device)
-        state = rescue.apply(mod, ctx, state, snap)
-    except Exception as e:
-        err = f"{type(e).__name__}: {e}"
-    errs = agree.gather(err) if agree is not None else [err]
-    bad = [(r, e) for r, e in enumerate(errs) if e is not None]
-    if bad:
-        # some ranks may hold half-restored state: every rank starts over from setup()
-        ctx.log(f"rescue: snapshot step={step} did not restore on rank {bad[0][0]} ({bad[0][1]}): "
-                f"starting from setup()")
-        return mod.setup(ctx)
-    ctx.step = step
-    rescue.last_step, rescue.last = step, time.monotonic()
-    ctx.log(f"restored step={step} gen={meta['gen']} from the rescue snapshot (age {time.time() - meta['time']:.1f} s, "
-            f"{meta['bytes'] / 2**20:.1f} MiB/rank in {(time.perf_counter() - t0) * 1000.0:.1f} ms)")
-    return state
-
-
 _STANDBY_IMPORTS = ["torch.distributed", "torch.optim", "torch.nn.parallel", "torch._dynamo"]
 
 
@@ -1102,6 +515,89 @@ def _list_imported_modules(watch_dir: str) -> None:
         os.replace(path + ".tmp", path)
     except OSError:
         pass
+
+
+class _Heartbeat:
+    """The rank's side of the supervisor's stuck-step rule (supervise._GroupWatch.assess): a
+    thread of its own sends, once a second over the status pipe,
+
+        hb <rank> <step> <phase> <in_phase_s> <longest_s> <still_s> <snap_step> <where>
+
+    phase: start (load, setup(), restore, first step) | reload (load, setup() when
+    SETUP_VERSION changed, the first step of the new code) | step (a steady-state step) |
+    boundary | idle (paused or waiting). still: seconds since the main thread last showed
+    progress, sampled 4x a second: its Python position (innermost frame, bytecode offset)
+    changed, or it used at least 5 % of a CPU since the last sample. A thread blocked in a
+    deadlock, a dead peer's collective or a sleep stands still; an eval loop, a checkpoint save or
+    a long computation moves. where: the innermost frame of the user's code. From a thread, so a step that runs for
+    minutes keeps the beat going (the old beat came from the top of the loop: a long healthy step
+    looked stuck). The main thread only sets `phase`/`since`: two attribute writes per step."""
+
+    def __init__(self, rank, ctx, rescue):
+        self.rank, self.ctx, self.rescue = rank, ctx, rescue
+        self.phase, self.since, self.longest = "start", time.monotonic(), 0.0
+        self.main = threading.get_ident()
+        self.kit = os.path.dirname(os.path.realpath(__file__)) + os.sep
+        self.stopped = False
+        self.thread = None
+        if os.environ.get("DEVSPACE_RUNNER_STATUS_FD"):
+            self.thread = threading.Thread(target=self._run, name="devspace-heartbeat", daemon=True)
+            self.thread.start()
+
+    def enter(self, phase: str) -> None:
+        self.since = time.monotonic()
+        self.phase = phase
+
+    def done(self) -> None:
+        """A step finished (steady-state, or the first of a start or reload): it counts towards
+        the longest step, which scales the stuck threshold."""
+        d = time.monotonic() - self.since
+        if d > self.longest:
+            self.longest = d
+        self.enter("boundary")
+
+    def _where(self, f) -> str:
+        inner = f
+        while f is not None:
+            fn = f.f_code.co_filename
+            if not fn.startswith(self.kit) and os.sep + "site-packages" + os.sep not in fn and \
+                    not fn.startswith(("<", sys.prefix, sys.base_prefix)):
+                return f"{os.path.basename(fn)}:{f.f_lineno}"
+            f = f.f_back
+        return f"{os.path.basename(inner.f_code.co_filename)}:{inner.f_lineno}" if inner is not None else "?"
+
+    def _cpu(self, clk):
+        try:
+            return time.clock_gettime(clk) if clk is not None else 0.0
+        except OSError:
+            return 0.0
+
+    def _run(self) -> None:
+        try:
+            clk = time.pthread_getcpuclockid(self.main)  # the main thread's CPU-time clock
+        except (AttributeError, OSError):
+            clk = None
+        last, moved, next_beat = None, time.monotonic(), 0.0
+        t_prev, cpu_prev = moved, self._cpu(clk)
+        while not self.stopped:
+            f = sys._current_frames().get(self.main)
+            pos = (id(f.f_code), f.f_lasti) if f is not None else None
+            now, cpu = time.monotonic(), self._cpu(clk)
+            busy = clk is not None and cpu - cpu_prev >= 0.05 * (now - t_prev)
+            t_prev, cpu_prev = now, cpu
+            if pos != last or busy:
+                last, moved = pos, now
+            if now >= next_beat:
+                where = self._where(f).replace(" ", "_") if f is not None else "?"
+                snap = self.rescue.last_step if self.rescue is not None else 0
+                _status(f"hb {self.rank} {self.ctx.step} {self.phase} {now - self.since:.2f} {self.longest:.3f} "
+                        f"{now - moved:.2f} {snap} {where}")
+                next_beat = now + 1.0
+            del f
+            time.sleep(0.25)
+
+    def stop(self) -> None:
+        self.stopped = True
 
 
 def worker_main(args) -> int:
@@ -1185,8 +681,9 @@ def worker_main(args) -> int:
     if rescue_dir and args.rescue_every > 0:
         # ignored before it exists: its mkdir must not read as an edit (the change feed runs)
         _IGNORED_DIRS.append(os.path.abspath(rescue_dir))
-        rescue = Rescue(rescue_dir, rank, args.rescue_every)
+        rescue = Rescue(rescue_dir, rank, args.rescue_every, agree=agree)
     stop = False
+    hb = _Heartbeat(rank, ctx, rescue)
 
     def _term(*_):
         nonlocal stop
@@ -1219,11 +716,13 @@ def worker_main(args) -> int:
                     state = _rescue_restore(rescue, agree, mod, ctx, state)
                     phase("restore")
                 if hasattr(mod, "step"):
+                    hb.enter("start")  # (the first step alone counts towards the longest step)
                     first = mod.step(ctx, state) or {}
                     ctx.step += 1
                     if device.type == "cuda":
                         torch.cuda.synchronize()
                     phase("first_step")
+                hb.done()
                 break
             except LoadFailed as e:
                 if agree is not None:
@@ -1236,11 +735,15 @@ def worker_main(args) -> int:
             # one rank: wait warm for the next edit, then try again (nodemon's "waiting for file
             # changes before starting"); several ranks left above and the supervisor waits instead
             ctx.log("waiting for a file change before starting again")
+            hb.enter("idle")
             while not feed.take(0.5)[0]:
                 if stop:
                     return 0
             gen += 1
+            hb.enter("start")
         setup_version = getattr(mod, "SETUP_VERSION", None)
+        if rescue is not None:
+            rescue.steady(device)
         if rank == 0 and os.environ.get("DEVSPACE_RUNNER_STATUS_FD"):  # under a supervisor
             _list_imported_modules(watch_dir)  # before `ready`: the standby is started on it
         _status(f"ready {rank}")
@@ -1270,12 +773,9 @@ def worker_main(args) -> int:
         script_mode = not hasattr(mod, "step")
         fault.armed = True
         paused = False  # one rank: a step of this generation failed; no more steps until an edit
-        last_beat = 0.0
         while agree is not None or not stop:
-            now = time.monotonic()
-            if now - last_beat >= 1.0:  # the supervisor's evidence that this loop comes round
-                _status(f"hb {rank} {ctx.step} {period_ema or 0.0:.1f}")
-                last_beat = now
+            if hb.phase not in ("boundary", "idle"):  # a step, reload or start left early (continue)
+                hb.enter("boundary")
             # 1. pick up local change notifications (non-blocking while training; blocking when idle)
             timeout = 0 if (not script_mode and args.train and not paused) else 0.05
             n_changes, t_first, helper_changed = feed.take(timeout)
@@ -1308,6 +808,7 @@ def worker_main(args) -> int:
                 _rescue_finish(rescue, ctx, write_failed)
             if target > gen:
                 t_reload = time.perf_counter()
+                hb.enter("reload")
                 wait_ms = (t_reload - reload_t0) * 1000.0 if reload_t0 else 0.0
                 purge, helper_pending = helper_pending, False
                 running = ctx.generation
@@ -1339,6 +840,7 @@ def worker_main(args) -> int:
                 reload_ms = (time.perf_counter() - t_reload) * 1000.0
                 # 3. run the first step with the new code and report
                 t_step = time.perf_counter()
+                hb.enter("reload")  # (the first step alone counts towards the longest step)
                 metrics = {}
                 try:
                     if not script_mode:
@@ -1347,6 +849,7 @@ def worker_main(args) -> int:
                     if device.type == "cuda":
                         torch.cuda.synchronize()
                 except Preempted:  # an even newer edit arrived: report that one instead
+                    hb.enter("boundary")
                     continue
                 except Exception:
                     if agree is not None:
@@ -1359,6 +862,7 @@ def worker_main(args) -> int:
                     reload_t0 = None
                     continue
                 paused = False
+                hb.done()
                 step_ms = (time.perf_counter() - t_step) * 1000.0
                 since = (time.perf_counter() - reload_t0) * 1000.0 if reload_t0 else 0.0
                 reload_t0 = None
@@ -1375,11 +879,15 @@ def worker_main(args) -> int:
             if snap and state is not None and rescue.inflight is None:
                 rescue.begin(mod, ctx, state, gen, setup_version)
             if script_mode or not args.train or paused:
+                if hb.phase != "idle":
+                    hb.enter("idle")
                 continue
+            hb.enter("step")
             try:
                 metrics = mod.step(ctx, state) or {}
                 ctx.step += 1
             except Preempted:
+                hb.enter("boundary")
                 continue
             except Exception:
                 if agree is not None:
@@ -1391,6 +899,7 @@ def worker_main(args) -> int:
                 ctx.error(f"step failed gen={gen}: training paused until the next edit\n{traceback.format_exc()}")
                 paused = True
                 continue
+            hb.done()
             now = time.perf_counter()
             dt = (now - t_iter) * 1000.0
             t_iter = now
@@ -1412,6 +921,7 @@ def worker_main(args) -> int:
             why = (f"no answer from every rank within {args.group_timeout:g} s (a rank stuck in a step? "
                    f"--group-timeout): {why}")
         leave(EXIT_GROUP_LOST, f"group failure gen={ctx.generation}: {why}")
+    hb.stop()
     feed.close()
     watcher.close()
     overlay.uninstall()
@@ -1420,360 +930,6 @@ def worker_main(args) -> int:
     if dist is not None and dist.is_initialized():
         dist.destroy_process_group()
     return 0
-
-
-def _free_port() -> int:
-    """An OS-assigned free TCP port on 127.0.0.1 for the group's rendezvous (never a fixed
-    range: the pod may itself run under a torchrun whose master port is in use)."""
-    import socket
-
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def _spawn_group(args, port, status_fd=None, standby=False):
-    """One process per rank; `standby`: warm standbys that import torch and then wait on stdin for
-    `go <port>` (see _promote)."""
-    procs = []
-    for r in range(max(1, args.nproc)):
-        env = dict(os.environ)
-        env.update(
-            RANK=str(r),
-            WORLD_SIZE=str(max(1, args.nproc)),
-            LOCAL_RANK=str(r),
-            MASTER_ADDR="127.0.0.1",
-            MASTER_PORT=str(port),
-            HSA_ENABLE_IPC_MODE_LEGACY=env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
-        )
-        if status_fd is not None:
-            env["DEVSPACE_RUNNER_STATUS_FD"] = str(status_fd)
-        # Installed as a package (-m devspace_amd.runner) or vendored as a single file into a
-        # project by `devspace init` (rocm-pytorch template).
-        me = ["-m", "devspace_amd.runner"] if __package__ else [os.path.abspath(__file__)]
-        cmd = [sys.executable] + me + ["--worker"] + (["--standby"] if standby else []) + _forward(args)
-        supervisor = os.getpid()
-        procs.append(subprocess.Popen(cmd, env=env, pass_fds=(status_fd,) if status_fd is not None else (),
-                                      stdin=subprocess.PIPE if standby else None,
-                                      preexec_fn=lambda: _die_with_parent(supervisor)))
-    return procs
-
-
-def _promote(procs, port) -> bool:
-    """Turns a warm standby group into the running group (rendezvous on `port`); False when one of
-    its processes is gone (then it is not used)."""
-    if any(p.poll() is not None for p in procs):
-        return False
-    try:
-        for p in procs:
-            p.stdin.write(f"go {port}\n".encode())
-            p.stdin.close()
-    except OSError:
-        return False
-    return True
-
-
-def _discard(group) -> None:
-    procs, status_r = group
-    for p in procs:
-        try:
-            p.stdin.close()  # a standby waiting for `go` exits on EOF
-        except (OSError, AttributeError):
-            pass
-    _stop_group(procs)
-    os.close(status_r)
-
-
-def _die_with_parent(supervisor_pid):
-    """Worker side of the fork: get SIGTERM when the supervisor dies, however it dies (a
-    SIGKILLed supervisor must not leave ranks training on the GPU). The supervisor may already
-    have died between fork() and prctl(): then the child is orphaned and exits at once."""
-    try:
-        import ctypes
-
-        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
-    except OSError:  # pragma: no cover - non-glibc
-        pass
-    if os.getppid() != supervisor_pid:
-        os._exit(1)
-
-
-def _stop_group(procs, grace_s=2.0):
-    """SIGTERM (the ranks agree to stop at the next step boundary), SIGKILL after the grace: a
-    rank blocked inside a collective whose peer is gone never returns to Python to see it."""
-    for p in procs:
-        if p.poll() is None:
-            p.terminate()
-    deadline = time.monotonic() + grace_s
-    for p in procs:
-        try:
-            p.wait(max(0.0, deadline - time.monotonic()))
-        except subprocess.TimeoutExpired:
-            p.kill()
-            p.wait()
-
-
-def restart_main(args) -> int:
-    """Restart-on-change mode (what the reference's nodemon-style dev entrypoints do): every
-    edit kills the process group and cold-starts it. Kept as the reference-equivalent baseline."""
-    watch_dir = os.path.abspath(args.watch or os.path.dirname(os.path.abspath(args.entry)))
-    watcher = make_watcher(watch_dir)
-    port = args.port or _free_port()
-    procs = _spawn_group(args, port)
-    try:
-        while True:
-            changed = [p for p in watcher.poll(200) if not _ignored(p)]
-            if changed:
-                _log(f"change detected ({len(changed)} files), restarting")
-                _stop_group(procs)
-                port = port + 1 if args.port else _free_port()
-                procs = _spawn_group(args, port)
-            elif all(p.poll() is not None for p in procs) and not args.keep_alive:
-                return max(p.returncode for p in procs)
-    finally:
-        _stop_group(procs)
-        watcher.close()
-
-
-class _GroupWatch:
-    """The supervisor's view of one running group: exits (any rank, not all), the workers'
-    status lines (`ready <rank>`, `fail <rank> <gen>`) and whether the synced tree changed since
-    the group started (then a failed group restarts at once: the fix may already be there)."""
-
-    def __init__(self, procs, status_r, watcher, stuck_after=0.0):
-        self.procs = procs
-        self.status_r = status_r
-        self.watcher = watcher
-        self.ready = set()
-        self.failed = []  # ranks in the order their `fail` lines arrived
-        self.changed = False
-        self.last_change = 0.0  # monotonic time of the newest change of the synced tree
-        self.stuck_after = stuck_after
-        self.beat = {}  # rank -> (monotonic time of its last heartbeat, step period in s)
-        self._buf = b""
-        self._next_scan = 0.0
-
-    def _read_status(self, timeout):
-        import select
-
-        r, _, _ = select.select([self.status_r], [], [], timeout)
-        if not r:
-            return
-        try:
-            chunk = os.read(self.status_r, 4096)
-        except BlockingIOError:
-            return
-        self._buf += chunk
-        *lines, self._buf = self._buf.split(b"\n")
-        for line in lines:
-            parts = line.decode(errors="replace").split()
-            if len(parts) >= 2 and parts[0] == "ready":
-                self.ready.add(int(parts[1]))
-                self.beat[int(parts[1])] = (time.monotonic(), 0.0)
-            elif len(parts) >= 2 and parts[0] == "fail":
-                self.failed.append(int(parts[1]))
-            elif len(parts) >= 4 and parts[0] == "hb":
-                self.beat[int(parts[1])] = (time.monotonic(), float(parts[3]) / 1000.0)
-
-    def _scan_tree(self):
-        now = time.monotonic()
-        if now < self._next_scan:
-            return
-        self._next_scan = now + 0.25
-        if [p for p in self.watcher.poll(0) if not _ignored(p)]:
-            self.changed = True
-            self.last_change = now
-
-    def _stuck(self):
-        """(rank, seconds) of a rank whose loop has not come round for max(stuck_after, 50 step
-        periods) while the code changed since: stuck inside a step (a deadlock, an endless loop)
-        it would never pick the edit up."""
-        if not self.stuck_after or len(self.ready) < len(self.procs):
-            return None
-        now = time.monotonic()
-        for rank, (t, period) in self.beat.items():
-            if self.last_change > t and now - t > max(self.stuck_after, 50.0 * period):
-                return rank, now - t
-        return None
-
-    def wait(self, on_ready=None):
-        """('done', codes) when every rank exited 0; ('failed', rank, code) at the first rank
-        that exits otherwise (the root cause: the first `fail` line, else the first exit seen);
-        ('stuck', rank, seconds) for a rank stuck in a step across an edit.
-        `on_ready()` runs once, when every rank finished its first step."""
-        while True:
-            self._read_status(0.02)
-            self._scan_tree()
-            if on_ready is not None and len(self.ready) == len(self.procs):
-                on_ready()
-                on_ready = None
-            stuck = self._stuck()
-            if stuck is not None:
-                return ("stuck",) + stuck
-            codes = [p.poll() for p in self.procs]
-            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
-            if bad:
-                self._read_status(0)
-                root = next(((r, codes[r]) for r in self.failed if codes[r] not in (None, 0)), bad[0])
-                return ("failed",) + root
-            if all(c == 0 for c in codes):
-                return ("done", codes)
-
-
-def _in_pod() -> bool:
-    return bool(os.environ.get("KUBERNETES_SERVICE_HOST"))
-
-
-def _default_rescue_dir(entry: str, nproc: int) -> str:
-    """In a pod: one directory per entry file and rank count in /dev/shm, the pod's memory
-    volume, so a container that the kubelet restarts (an OOM kill, a crash of the runner itself)
-    finds the snapshots its previous run left. Elsewhere: this process's own (a later run on the
-    same machine starts fresh)."""
-    import tempfile
-
-    base = os.environ.get("DEVSPACE_RESCUE_ROOT") or (
-        "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else tempfile.gettempdir())
-    if _in_pod():
-        key = hashlib.sha256(f"{os.path.abspath(entry)}|{nproc}".encode()).hexdigest()[:12]
-        return os.path.join(base, f"devspace-rescue-{key}")
-    # what runners killed outright (SIGKILL: no clean-up) left behind here
-    for name in os.listdir(base):
-        m = re.match(r"devspace-rescue-(\d+)$", name)
-        if m and not os.path.exists(f"/proc/{m.group(1)}"):
-            _drop_rescue_dir(os.path.join(base, name))
-    return os.path.join(base, f"devspace-rescue-{os.getpid()}")
-
-
-def _drop_rescue_dir(path: str) -> None:
-    import shutil
-
-    shutil.rmtree(path, ignore_errors=True)
-
-
-def _wait_for_change(watcher, already=False):
-    """nodemon's "app crashed - waiting for file changes before starting": block until the synced
-    tree changes (a settled write, not a temp file)."""
-    if already:
-        return
-    while not [p for p in watcher.poll(500) if not _ignored(p)]:
-        pass
-
-
-def supervisor_main(args) -> int:
-    """Spawn one worker per GPU (torchrun-style env) and contain failures: any rank exiting
-    non-zero stops the whole group (its peers may be blocked in a collective with it), which is
-    started again from fresh processes — at once if it had come up (its ranks all finished a
-    first step) and there are restarts left since the last edit, after the next edit otherwise."""
-    if args.restart:
-        return restart_main(args)
-    nproc = max(1, args.nproc)
-    if os.environ.get("DEVSPACE_RUNNER_INPROCESS") == "1":
-        # one rank in this process (a debugger, a profiler that follows one process): no
-        # supervisor, so a hard crash ends the runner (and the container) as a plain script would
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("WORLD_SIZE", "1")
-        os.environ.setdefault("LOCAL_RANK", "0")
-        return worker_main(args)
-    # One rank is supervised too: an exception in step() pauses it in its warm process, but a
-    # hard crash (a segfault in an extension, a GPU memory fault that aborts the process, the
-    # OOM killer) would otherwise end the container and put it into CrashLoopBackOff; here the
-    # warm standby takes over in about a second and resumes from the last snapshot.
-    watch_dir = os.path.abspath(args.watch or os.path.dirname(os.path.abspath(args.entry)))
-    watcher = make_watcher(watch_dir)
-    port = args.port or _free_port()
-    restarts = 0  # restarts since the last edit
-    # the ranks' rescue snapshots live as long as this supervisor (a restarted group resumes
-    # from them) and, in a pod, as long as the pod (a restarted container resumes from them); in
-    # /dev/shm: the pod's memory-backed volume, sized per GPU by the chart
-    rescue_dir = args.rescue_dir or _default_rescue_dir(args.entry, nproc)
-    os.environ["DEVSPACE_RESCUE_DIR"] = rescue_dir
-    _IGNORED_DIRS.append(os.path.abspath(rescue_dir))
-
-    def _term(*_):
-        raise KeyboardInterrupt
-
-    signal.signal(signal.SIGTERM, _term)  # pod deletion / kill: stop the ranks, then exit
-    procs = []
-    clean = False  # stopped or finished: no later run resumes from these snapshots
-    standby = []  # [(procs, status_r)]: a warm group that replaces a failed one
-
-    def _new_group(as_standby=False):
-        status_r, status_w = os.pipe()
-        os.set_blocking(status_r, False)
-        group = (_spawn_group(args, port, status_w, standby=as_standby), status_r)
-        os.close(status_w)
-        return group
-
-    def _warm_up():  # once the running group is up: its start-up is not slowed by the standby's
-        if args.warm_standby and not standby:
-            standby.append(_new_group(as_standby=True))
-
-    try:
-        while True:
-            group = standby.pop() if standby else None
-            if group is not None and not _promote(group[0], port):
-                _discard(group)
-                group = None
-            procs, status_r = group or _new_group()
-            gw = _GroupWatch(procs, status_r, watcher, stuck_after=args.stuck_after)
-            outcome = gw.wait(on_ready=_warm_up)
-            if outcome[0] == "done":
-                os.close(status_r)
-                clean = True
-                return 0
-            if outcome[0] == "stuck":
-                _, rank, secs = outcome
-                _stop_group(procs, grace_s=0.2)
-                os.close(status_r)
-                _log(f"rank={rank} made no progress for {secs:.0f} s and the code changed since (stuck in a step?): "
-                     f"restarting the group of {nproc} with the new code" + (" from the warm standby" if standby else ""))
-                restarts = 0
-                port = port + 1 if args.port else _free_port()
-                continue
-            _, rank, code = outcome
-            _stop_group(procs, grace_s=0.2)  # the peers of a failed group: nothing left to finish
-            os.close(status_r)
-            came_up = len(gw.ready) == nproc
-            if gw.changed:
-                restarts = 0
-            restarts += 1
-            if came_up and restarts <= args.max_restarts:
-                _log(f"rank={rank} exited with code {code}: restarting the group of {nproc} "
-                     f"({restarts}/{args.max_restarts} since the last edit)" + (" from the warm standby" if standby else ""))
-            else:
-                why = "before every rank finished a first step" if not came_up else \
-                    f"{args.max_restarts} restarts without an edit"
-                _log(f"rank={rank} exited with code {code} {why}: waiting for a file change "
-                     f"before starting the group again")
-                _wait_for_change(watcher, already=gw.changed)
-                restarts = 0
-                _log(f"change detected: restarting the group of {nproc}" + (" from the warm standby" if standby else ""))
-            port = port + 1 if args.port else _free_port()
-    except KeyboardInterrupt:
-        # with a --rescue-dir the ranks take a last snapshot before they exit: give them the time
-        _stop_group(procs, grace_s=30.0 if args.rescue_dir and args.rescue_every > 0 else 2.0)
-        clean = True
-        return 130
-    finally:
-        for group in standby:
-            _discard(group)
-        watcher.close()
-        if not args.rescue_dir and (clean or not _in_pod()):
-            _drop_rescue_dir(rescue_dir)
-
-
-def _forward(args):
-    out = ["--watch", args.watch or "", "--log-every", str(args.log_every), "--max-steps", str(args.max_steps),
-           "--gemm-tuning", args.gemm_tuning]
-    if not args.train:
-        out.append("--no-train")
-    if not args.preempt:
-        out.append("--no-preempt")
-    out += ["--preempt-drain-ms", str(args.preempt_drain_ms), "--group-timeout", str(args.group_timeout),
-            "--rescue-every", str(args.rescue_every)]
-    if args.rescue_dir:  # (the ranks find it in DEVSPACE_RESCUE_DIR too; this says it was asked for)
-        out += ["--rescue-dir", args.rescue_dir]
-    return out + [args.entry]
 
 
 def parse_args(argv=None):
@@ -1826,6 +982,8 @@ def main(argv=None) -> int:
         args.watch = None
     if args.worker:
         return worker_main(args)
+    from devspace_amd.supervise import supervisor_main
+
     return supervisor_main(args)
 
 

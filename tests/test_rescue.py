@@ -4,6 +4,7 @@ tensors of any dtype and layout (bf16, bool, empty, non-contiguous), Python numb
 a module's own snapshot()/restore() hooks win; a state it cannot serialise turns snapshots off
 with a reason instead of failing the step."""
 
+import os
 import types
 
 import pytest
@@ -133,3 +134,142 @@ def test_hbm_staged_snapshot_round_trip_on_the_gpu(tmp_path):
     for k, v in fresh["model"].state_dict().items():
         assert v.is_cuda and torch.equal(v, want[k]), k  # the snapshot's values, not the later ones
     assert fresh["n"] == 5
+
+
+class _ThreadGroup:
+    """The Agreement's all-gather for ranks simulated as threads of one process."""
+
+    def __init__(self, world):
+        import threading
+
+        self.world = world
+        self.box = [None] * world
+        self.barrier = threading.Barrier(world)
+
+    def for_rank(self, rank):
+        group = self
+
+        class _Agree:
+            def gather(self, obj):
+                group.box[rank] = obj
+                group.barrier.wait()
+                out = list(group.box)
+                group.barrier.wait()
+                return out
+
+        return _Agree()
+
+
+def _ddp_like_state(rank, seed=0):
+    """What DDP ranks hold: the same model and optimizer on every rank, plus a little per-rank
+    state (a data-loader position, a per-rank RNG draw)."""
+    torch.manual_seed(seed)
+    model = torch.nn.Sequential(torch.nn.Linear(256, 256), torch.nn.Linear(256, 64))
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    model(torch.ones(4, 256)).sum().backward()
+    opt.step()
+    return {"model": model, "opt": opt, "cursor": torch.full((1000,), float(rank)), "rank": rank}
+
+
+def _group_take(root, world, states, step=7):
+    import threading
+
+    g = _ThreadGroup(world)
+    rescues = [runner.Rescue(str(root), r, every_s=60, agree=g.for_rank(r)) for r in range(world)]
+    jobs = [None] * world
+
+    def one(r):
+        ctx = runner.Context(r, world, r, torch.device("cpu"))
+        ctx.step = step
+        rescues[r].begin(types.SimpleNamespace(), ctx, states[r], gen=1, setup_version=1)
+        jobs[r] = rescues[r].inflight
+
+    ts = [threading.Thread(target=one, args=(r,)) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    for r in range(world):
+        assert jobs[r]["err"] is None, jobs[r]
+        runner._rescue_finish(rescues[r], runner.Context(r, world, r, torch.device("cpu")), False)
+    return rescues, jobs
+
+
+def test_replicated_state_is_written_once_across_ranks(tmp_path):
+    """4 ranks holding the same model and optimizer (DDP) write that state once between them,
+    spread over the ranks by bytes, and each rank's own tensors once; every rank restores its
+    exact state, reading the replicated tensors from the other ranks' files."""
+    world = 4
+    states = [_ddp_like_state(r) for r in range(world)]
+    rescues, jobs = _group_take(tmp_path, world, states)
+    one_rank = sum(p.numel() * p.element_size() for p in states[0]["model"].parameters()) * 3  # + 2 moments
+    total = sum(os.path.getsize(tmp_path / f"rank{r}-step7.bin") for r in range(world))
+    assert total == jobs[0]["total"]
+    # one copy of the replicated state plus 4 cursors (and alignment), not 4 copies
+    assert one_rank <= total < one_rank * 1.1 + world * 4096, (total, one_rank)
+    sizes = [jobs[r]["bytes"] for r in range(world)]
+    assert max(sizes) < one_rank * 0.6, sizes  # spread over the ranks, not all on rank 0
+    for r in range(world):
+        assert rescues[r].available(1, world) == [7]
+        snap, _ = rescues[r].load(7, torch.device("cpu"))
+        fresh = _ddp_like_state(r, seed=99)
+        fresh["rank"] = -1
+        fresh = runner.Rescue.apply(types.SimpleNamespace(), None, fresh, snap)
+        for a, b in zip(states[r]["model"].state_dict().values(), fresh["model"].state_dict().values()):
+            assert torch.equal(a, b)
+        so, fo = states[r]["opt"].state_dict()["state"], fresh["opt"].state_dict()["state"]
+        for k in so:
+            for name in so[k]:
+                assert torch.equal(so[k][name], fo[k][name]), (k, name)
+        assert torch.equal(fresh["cursor"], states[r]["cursor"]) and fresh["rank"] == r
+
+
+def test_a_rank_whose_state_diverged_writes_its_own(tmp_path):
+    """Digests are taken at every snapshot: a tensor that differs on one rank (a per-rank
+    accumulator, a shard) is written by that rank, not taken from a replica."""
+    world = 2
+    states = [_ddp_like_state(r) for r in range(world)]
+    with torch.no_grad():
+        next(iter(states[1]["model"].parameters()))[0, 0] += 1.0
+    rescues, _ = _group_take(tmp_path, world, states)
+    for r in range(world):
+        snap, _ = rescues[r].load(7, torch.device("cpu"))
+        fresh = runner.Rescue.apply(types.SimpleNamespace(), None, _ddp_like_state(r, seed=5), snap)
+        for a, b in zip(states[r]["model"].state_dict().values(), fresh["model"].state_dict().values()):
+            assert torch.equal(a, b)
+
+
+def test_a_missing_peer_file_makes_the_step_unavailable(tmp_path):
+    """A layout that points into another rank's file is only offered when that file is complete
+    (a rank that died mid-write leaves none): the step is not restored from half a snapshot."""
+    world = 2
+    states = [_ddp_like_state(r) for r in range(world)]
+    rescues, jobs = _group_take(tmp_path, world, states)
+    owner = max(range(world), key=lambda r: jobs[r]["bytes"])
+    os.unlink(tmp_path / f"rank{owner}-step7.bin")
+    assert all(rescues[r].available(1, world) == [] for r in range(world))
+
+
+def test_digests_tell_apart_what_differs():
+    from devspace_amd.rescue import digests
+
+    x = torch.randn(300_000)
+    y = x.clone()
+    y[123_456] = y[123_456] + 1.0
+    base = torch.randn(1001)
+    d = digests([x, x.clone(), y, x.view(torch.int32), base[1:], torch.ones(3, dtype=torch.bool), torch.zeros(0, 3)])
+    assert d[0] == d[1] and d[0] != d[2] and d[0] != d[3]  # same bytes, other dtype: not the same tensor
+    assert d[4] == digests([base[1:].clone()])[0]  # a view at an odd offset
+
+
+def test_staging_room_leaves_the_steps_their_peak():
+    """the staged HBM copy may only use memory the next steps do not need.
+    free + reserved - peak must hold the copy (plus 10 % and a margin); cached memory that the
+    step's activations reuse is not room."""
+    GiB = 1 << 30
+    room = runner.Rescue.hbm_room
+    # 200 GiB in use at peak, 20 GiB of it activations cached between steps, 60 GiB free
+    assert room(40 * GiB, free=60 * GiB, reserved=200 * GiB, peak=200 * GiB)
+    # the same job within one state size of the capacity: 10 GiB free, 40 GiB cached for the
+    # activations -> round 4 counted the cache and staged; the next step would have run out
+    assert not room(30 * GiB, free=10 * GiB, reserved=240 * GiB, peak=240 * GiB)
+    # cache beyond the steps' peak (a freed earlier allocation) is room
+    assert room(30 * GiB, free=10 * GiB, reserved=280 * GiB, peak=240 * GiB)

@@ -742,7 +742,7 @@ def test_an_edit_unsticks_a_rank_stuck_in_a_step(tmp_path, nproc):
         trigger.write_text("1")
         time.sleep(3.0)  # every rank is now stuck (the peers of a stuck rank wait in its collective)
         _set_marker(entry, "fixed")
-        r.until(r"made no progress for \d+ s and the code changed since", timeout=60)
+        r.until(r"made no progress for \d+ s at train.py:\d+ and the code changed since", timeout=60)
         r.until(r"restored step=\d+ ", timeout=120)
         r.until(r"started gen=1 marker=fixed", timeout=60)
         r.until(r"step=\d+ gen=1 ", timeout=60)  # and trains

@@ -1,0 +1,302 @@
+"""The runner's supervision rules that round 4 got wrong (VERDICT r4 "Next round" items 1-2):
+
+* a long healthy step is never mistaken for a stuck one: the stuck-step restart needs an edit
+  pending in a steady-state step, the step past max(--stuck-after, 10 x the longest step so far),
+  no rank's main thread moving for --stuck-after, and a rescue snapshot to resume from; a long
+  step that does not meet that is reported once and left alone;
+* a restart stops the whole process tree of a group, including what the ranks started, what
+  escaped into its own session and what was orphaned (the supervisor is a child subreaper);
+* replicated (DDP) state is snapshotted once for the group, not once per rank.
+
+The reference's model for all three: a fresh process tree per reload (nodemon,
+/root/reference/examples/quickstart/package.json:7; redeploy, /root/reference/cmd/dev.go:225-234)
+and acting only on evidence seen twice (/root/reference/pkg/devspace/sync/downstream.go:117-123).
+Rehearsed on CPU with gloo ranks.
+"""
+import os
+import re
+import time
+import uuid
+
+import psutil
+import pytest
+
+from test_runner_failsafe import Runner, _set_marker
+
+LONG_EVAL = '''
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+MARKER = "v0"
+EVAL = {eval!r}
+
+
+def setup(ctx):
+    return {{"n": 0}}
+
+
+def step(ctx, state):
+    flag = torch.tensor([1.0 if ctx.rank == 0 and os.path.exists(EVAL) else 0.0])
+    if ctx.distributed:
+        dist.all_reduce(flag)
+    if flag.item():
+        if ctx.rank == 0:
+            os.unlink(EVAL)
+            t0 = time.monotonic()
+            x = torch.randn(128, 128)
+            while time.monotonic() - t0 < 5.0:  # a 5 s evaluation: busy, healthy
+                x = torch.tanh(x @ x.t() / 128.0)
+            ctx.log("eval done")
+        if ctx.distributed:
+            dist.barrier()  # the other ranks wait here for rank 0's eval, standing still
+    state["n"] += 1
+    time.sleep(0.005)
+    return {{"loss": state["n"]}}
+'''
+
+
+@pytest.mark.parametrize("nproc", [1, 2])
+def test_a_long_healthy_step_survives_an_edit(tmp_path, nproc):
+    """VERDICT r4 Weak #1: a step that runs a 5 s evaluation with --stuck-after 1 while an edit
+    lands (and rescue snapshots exist) is not restarted: rank 0's main thread moves the whole
+    time. The long step is reported once, and the edit applies right after the evaluation."""
+    trigger = tmp_path.parent / (tmp_path.name + "-eval")
+    entry = tmp_path / "train.py"
+    entry.write_text(LONG_EVAL.format(eval=str(trigger)))
+    r = Runner(tmp_path, entry, nproc, extra_args=("--log-every", "50", "--rescue-every", "0.5", "--stuck-after", "1"))
+    try:
+        r.until(r"started gen=1 marker=v0", timeout=180)
+        r.until(r"rescue snapshot step=\d+ ", timeout=60)
+        trigger.write_text("1")
+        time.sleep(1.5)  # inside the evaluation
+        _set_marker(entry, "v1")
+        _, line = r.until(r"rank=\d in step for \d+ s at train.py:\d+; edit pending: rank=0 is making progress",
+                          timeout=30)
+        t_done, _ = r.until(r"eval done", timeout=30)
+        t_reload, _ = r.until(r"reloaded gen=2 marker=v1 ", timeout=30)
+        assert t_reload >= t_done
+        time.sleep(1.0)
+        text = r.text()
+        assert "made no progress" not in text and "exited with code" not in text, text[-3000:]
+        assert len(re.findall(r"in step for \d+ s", text)) == 1, text[-3000:]  # reported once
+    finally:
+        r.stop()
+
+
+SLOW_SETUP = '''
+import time
+
+MARKER = "v0"
+SETUP_VERSION = 1
+
+
+def setup(ctx):
+    if SETUP_VERSION == 2:
+        time.sleep(4.0)  # loading a bigger model: the main thread stands still, in setup()
+    return {"n": 0}
+
+
+def step(ctx, state):
+    state["n"] += 1
+    time.sleep(0.005)
+    return {"loss": state["n"]}
+'''
+
+
+def test_a_slow_setup_on_reload_is_not_stuck(tmp_path):
+    """a reload whose setup() (SETUP_VERSION changed) takes longer than --stuck-after,
+    standing still, is a reload, not a stuck step: no restart."""
+    entry = tmp_path / "train.py"
+    entry.write_text(SLOW_SETUP)
+    r = Runner(tmp_path, entry, 1, extra_args=("--log-every", "50", "--rescue-every", "0.5", "--stuck-after", "1"))
+    try:
+        r.until(r"started gen=1 marker=v0", timeout=180)
+        r.until(r"rescue snapshot step=\d+ ", timeout=60)
+        entry.write_text(SLOW_SETUP.replace("SETUP_VERSION = 1", "SETUP_VERSION = 2").replace('"v0"', '"v1"'))
+        time.sleep(1.5)
+        _set_marker(entry, "v2")  # a second edit while setup() runs
+        r.until(r"reloaded gen=\d+ marker=v2 ", timeout=30)
+        assert "made no progress" not in r.text() and "exited with code" not in r.text(), r.text()[-3000:]
+    finally:
+        r.stop()
+
+
+TREE = '''
+import os
+import subprocess
+import time
+
+import torch
+import torch.distributed as dist
+
+MARKER = "v0"
+TAG = {tag!r}
+
+
+def setup(ctx):
+    kids = [subprocess.Popen(["sleep", TAG + "1"]),  # a plain child (an eval worker)
+            subprocess.Popen(["sleep", TAG + "2"], start_new_session=True)]  # escaped into its own session
+    subprocess.Popen(["sh", "-c", "sleep " + TAG + "3 &"]).wait()  # a daemon, orphaned at once
+    return {{"kids": kids, "n": 0}}
+
+
+def step(ctx, state):
+    if MARKER == "crash" and state["n"] > 20 and ctx.rank == ctx.world_size - 1:
+        os._exit(7)  # a hard crash after the group came up: restarted, up to --max-restarts
+    if ctx.distributed:
+        dist.all_reduce(torch.ones(1))
+    state["n"] += 1
+    time.sleep(0.005)
+    return {{"loss": state["n"]}}
+'''
+
+
+def _tagged(tag):
+    out = []
+    for p in psutil.process_iter(["cmdline", "status"]):
+        cmd = p.info["cmdline"] or []
+        if len(cmd) == 2 and cmd[0] == "sleep" and cmd[1].startswith(tag):
+            out.append(p)
+    return out
+
+
+@pytest.mark.parametrize("nproc", [1, 2])
+def test_restarts_stop_the_whole_process_tree(tmp_path, nproc):
+    """VERDICT r4 Missing #1 / Weak #3: each rank's setup() starts a child, a child in its own
+    session and an orphaned daemon. One crashing edit makes the group crash and be restarted
+    --max-restarts (3) times, then wait for the next edit. Afterwards none of those processes of
+    the four dead groups is alive and no zombie is left under the supervisor; while a group runs,
+    exactly its own are."""
+    tag = str(7000 + uuid.uuid4().int % 1000)
+    entry = tmp_path / "train.py"
+    entry.write_text(TREE.format(tag=tag))
+    r = Runner(tmp_path, entry, nproc, extra_args=("--log-every", "50", "--rescue-every", "0"))
+    try:
+        r.until(r"started gen=1 marker=v0", timeout=180)
+        time.sleep(0.5)
+        assert len(_tagged(tag)) == 3 * nproc, [p.info for p in _tagged(tag)]
+        _set_marker(entry, "crash")
+        r.until(r"restarts without an edit: waiting for a file change", timeout=180)
+        assert len(re.findall(r"exited with code 7", r.text())) >= 4, r.text()[-3000:]
+        time.sleep(0.5)
+        alive = [p for p in _tagged(tag) if p.status() != psutil.STATUS_ZOMBIE]
+        assert not alive, [(p.pid, p.cmdline(), p.ppid()) for p in alive]
+        zombies = [k for k in psutil.Process(r.proc.pid).children() if k.status() == psutil.STATUS_ZOMBIE]
+        assert not zombies, zombies
+        _set_marker(entry, "fixed")
+        r.until(r"started gen=1 marker=fixed", timeout=60)
+        time.sleep(0.5)
+        assert len(_tagged(tag)) == 3 * nproc  # the new group's own, and nothing else
+    finally:
+        r.stop()
+        for p in _tagged(tag):
+            p.kill()
+    assert not _tagged(tag)  # a clean stop takes them too
+
+
+DDP_STATE = '''
+import os
+
+import torch
+import torch.distributed as dist
+from torch.nn.parallel import DistributedDataParallel as DDP
+
+from devspace_amd.rescue import digests
+
+MARKER = "v0"
+SETUP_VERSION = 1
+MB = {mb}
+LOG = {log!r}
+FAIL = {fail!r}
+
+
+def setup(ctx):
+    torch.manual_seed(0)
+    dim = 512
+    layers = max(1, MB * 2**20 // (3 * 4 * dim * dim))  # fp32 weights + AdamW's two moments
+    model = DDP(torch.nn.Sequential(*[torch.nn.Linear(dim, dim, bias=False) for _ in range(layers)]),
+                gradient_as_bucket_view=True)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    return {{"model": model, "opt": opt, "cursor": torch.tensor([ctx.rank * 1000 + 1])}}
+
+
+def _digest(state):
+    ts = list(state["model"].state_dict().values()) + [state["cursor"]]
+    for s in state["opt"].state.values():
+        ts += [v for v in s.values() if isinstance(v, torch.Tensor)]
+    return "".join(digests(ts))[:32] if ts else "-"
+
+
+def step(ctx, state):
+    with open(LOG + str(ctx.rank), "a") as f:  # the state this step starts from, bit for bit
+        f.write(f"{{ctx.step}} {{_digest(state)}}\\n")
+    if ctx.rank == 1 and os.path.exists(FAIL):
+        os.unlink(FAIL)
+        raise RuntimeError("once")
+    model, opt = state["model"], state["opt"]
+    x = torch.randn(8, model.module[0].in_features, generator=torch.Generator().manual_seed(ctx.step * 8 + ctx.rank))
+    loss = model(x).pow(2).mean()
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
+    state["cursor"] += 1
+    return {{"loss": float(loss)}}
+'''
+
+
+def _digest_at(path, step):
+    last = None
+    with open(path) as f:
+        for line in f:
+            s, d = line.split()
+            if int(s) == step:
+                last = d
+    return last
+
+
+def test_ddp_snapshot_is_written_once_and_restores_bit_exact(tmp_path):
+    """VERDICT r4 Weak #2: 8 gloo ranks under DDP. The group's snapshot takes one rank's worth
+    of shared memory (plus the per-rank cursors), not eight; after rank 1 fails, the restarted
+    group resumes with every rank's model, optimizer moments and cursor bit-identical to the
+    snapshot step. RESCUE_TEST_MB sets the state per rank (default 24 MiB; the profile in
+    profiles/r5_rescue_dedup_*.json is this test at 2048)."""
+    mb = int(os.environ.get("RESCUE_TEST_MB", "24"))
+    world = int(os.environ.get("RESCUE_TEST_RANKS", "8"))
+    log = str(tmp_path.parent / (tmp_path.name + "-digest"))
+    fail = tmp_path.parent / (tmp_path.name + "-fail")
+    entry = tmp_path / "train.py"
+    entry.write_text(DDP_STATE.format(mb=mb, log=log, fail=str(fail)))
+    shm = tmp_path.parent / (tmp_path.name + "-shm")
+    r = Runner(tmp_path, entry, world, extra_args=("--log-every", "10", "--rescue-every", "2"),
+               extra_env={"KUBERNETES_SERVICE_HOST": "10.96.0.1", "DEVSPACE_RESCUE_ROOT": str(shm),
+                          "DEVSPACE_WARM_STANDBY": "0"})
+    try:
+        r.until(rf"started gen=1 marker=v0 .*world={world}", timeout=300)
+        _, line = r.until(r"rescue snapshot step=(\d+) ", timeout=300)
+        m = re.search(r"rescue snapshot step=(\d+) .*\(group: ([\d.]+) MiB in shared memory for ([\d.]+) MiB of state", line)
+        step, group_mib, state_mib = int(m.group(1)), float(m.group(2)), float(m.group(3))
+        d = next(shm.iterdir())
+        on_disk = sum(f.stat().st_size for f in d.iterdir() if re.match(rf"rank\d+-step{step}\.bin$", f.name))
+        print(f"world={world} state {state_mib:.1f} MiB over the ranks, group snapshot {group_mib:.1f} MiB, "
+              f"on disk {on_disk / 2**20:.1f} MiB")
+        assert abs(on_disk / 2**20 - group_mib) < 0.5
+        assert group_mib < state_mib / world * 1.05 + 1, line  # one rank's worth, not `world` of them
+        fail.write_text("1")
+        r.until(r"rank=1 exited with code 3: restarting the group", timeout=120)
+        snapped = max(int(s) for s in re.findall(r"rescue snapshot step=(\d+)", r.text()))
+        _, line = r.until(r"restored step=(\d+) ", timeout=300)
+        restored = int(re.search(r"restored step=(\d+)", line).group(1))
+        assert restored == snapped, (restored, snapped)
+        r.until(rf"started gen=1 marker=v0 .*world={world}", timeout=120)
+        for rank in range(world):
+            path = log + str(rank)
+            with open(path) as f:
+                lines = f.read().split("\n")
+            # the step the restarted group starts from was written before the failure, and again after
+            firsts = [l for l in lines if l.startswith(f"{restored} ")]
+            assert len(firsts) >= 2 and len(set(firsts)) == 1, (rank, firsts)
+    finally:
+        r.stop()
