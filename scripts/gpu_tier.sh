@@ -1,0 +1,65 @@
+#!/usr/bin/env bash
+# The GPU tier on one MI355X (the driver's round-end checks, and the profiles committed under
+# profiles/), run on a gpurun box from the repo root:
+#
+#   gpurun --timeout 1200 -- bash scripts/gpu_tier.sh [tests] [smoke] [bench] [prof] [rescue]
+#
+#   tests   python -m pytest tests -m gpu (every HIP op against fp32 PyTorch, the runner on the GPU)
+#   smoke   __graft_entry__.smoke(): one forward+backward of the flagship TinyLM on cuda:0
+#   bench   bench.py --steps $BENCH_STEPS --warmup $BENCH_WARMUP (the headline JSON line)
+#   prof    rocprofv3 --kernel-trace --stats of the rocm-pytorch pod under `devspace dev`
+#   rescue  the runner's snapshot cost on the flagship example (scripts/rescue_cost.py)
+#
+# Output: gpurun_out/$GPU_TIER_TAG/ (default "tier"). Every GPU step has its own time limit and
+# the script stops at the first failing step: no GPU step runs after a fault or a timeout.
+set -o pipefail
+cd "$(dirname "$0")/.."
+OUT="$PWD/gpurun_out/${GPU_TIER_TAG:-tier}"
+mkdir -p "$OUT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+steps=("$@")
+[ ${#steps[@]} -eq 0 ] && steps=(tests smoke bench)
+
+fail() {
+  echo "step $1 failed (exit $2); log tail:"
+  tail -40 "$3"
+  exit 1
+}
+
+for s in "${steps[@]}"; do
+  case "$s" in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1 || fail tests $? "$OUT/pytest_gpu.log"
+      tail -2 "$OUT/pytest_gpu.log"
+      ;;
+    smoke)
+      timeout -k 10 300 python -u __graft_entry__.py smoke > "$OUT/smoke.log" 2>&1 || fail smoke $? "$OUT/smoke.log"
+      tail -2 "$OUT/smoke.log"
+      ;;
+    bench)
+      timeout -k 10 600 python -u bench.py --steps "${BENCH_STEPS:-20}" --warmup "${BENCH_WARMUP:-3}" \
+        > "$OUT/bench.json" 2> "$OUT/bench.err" || fail bench $? "$OUT/bench.err"
+      tail -1 "$OUT/bench.json"
+      ;;
+    prof)
+      # the profiler follows the pod's runner (environment inherited through the local kubelet):
+      # the kernel stats are the training steps the hot reloads ran
+      R=$PWD
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o devloop -- \
+        python3 "$R/bench.py" --steps 10 --warmup 2 --qs-steps 0 --ref-steps 0 --no-deploy-bench \
+        > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err") || fail prof $? "$OUT/prof_bench.err"
+      db=$(find "$OUT/prof" -name '*.db' | head -1)
+      [ -n "$db" ] && python3 scripts/prof_summary.py "$db" > "$OUT/prof_kernels.txt" && head -12 "$OUT/prof_kernels.txt"
+      ;;
+    rescue)
+      timeout -k 10 600 python -u scripts/rescue_cost.py > "$OUT/rescue.json" 2> "$OUT/rescue.err" \
+        || fail rescue $? "$OUT/rescue.err"
+      tail -1 "$OUT/rescue.json"
+      ;;
+    *)
+      echo "unknown step $s" >&2
+      exit 2
+      ;;
+  esac
+done

@@ -165,8 +165,7 @@ std::string shm_problem(const Value& pod, int64_t gpus) {
   for (auto& v : pod.at_path("spec.volumes").items())
     if (v.at_path("emptyDir.medium").as_string() == "Memory") mem_volumes.insert(v.get("name").as_string());
   for (auto& c : pod.at_path("spec.containers").items()) {
-    const Value& lim = c.at_path("resources.limits").get("amd.com/gpu");
-    if (lim.as_int(0) == 0 && c.at_path("resources.requests").get("amd.com/gpu").as_int(0) == 0) continue;
+    if (gpu::container_gpu_request(c) == 0) continue;
     bool ok = false;
     for (auto& m : c.get("volumeMounts").items())
       if (m.get("mountPath").as_string() == "/dev/shm" && mem_volumes.count(m.get("name").as_string())) ok = true;
@@ -180,12 +179,38 @@ std::string shm_problem(const Value& pod, int64_t gpus) {
 
 static int64_t gpu_request(const Value& pod) {
   int64_t n = 0;
-  for (auto& c : pod.at_path("spec.containers").items()) {
-    const Value& lim = c.at_path("resources.limits").get("amd.com/gpu");
-    const Value& req = c.at_path("resources.requests").get("amd.com/gpu");
-    n += !lim.is_null() ? lim.as_int() : req.as_int();
-  }
+  for (auto& c : pod.at_path("spec.containers").items()) n += gpu::container_gpu_request(c);
   return n;
+}
+
+// Who holds a node's GPU devices: "ns/pod (4), ns2/pod2 (2)" from the pods bound to it (all
+// namespaces; "" when that list is forbidden, with *why set).
+static std::string gpu_holders(kube::Client& k, const std::string& node, std::string* why) {
+  Value pods;
+  try {
+    pods = k.get("/api/v1/pods?fieldSelector=spec.nodeName%3D" + node);
+  } catch (const std::exception& e) {
+    if (why) *why = e.what();
+    return "";
+  }
+  std::vector<std::string> out;
+  for (auto& p : pods.get("items").items()) {
+    std::string phase = p.at_path("status.phase").as_string();
+    if (phase == "Succeeded" || phase == "Failed") continue;
+    int64_t n = gpu_request(p);
+    if (n > 0)
+      out.push_back(p.at_path("metadata.namespace").as_string() + "/" + p.at_path("metadata.name").as_string() +
+                    " (" + std::to_string(n) + ")");
+  }
+  return join(out, ", ");
+}
+
+// The scheduler's verdict on a Pending pod, when it is a lack of GPU devices.
+static bool insufficient_gpus(const Value& pod) {
+  for (auto& c : pod.at_path("status.conditions").items())
+    if (c.get("reason").as_string() == "Unschedulable" && contains(c.get("message").as_string(), "Insufficient amd.com/"))
+      return true;
+  return false;
 }
 
 // In-pod GPU probe that depends on nothing but a POSIX shell: device nodes, ROCm tools, and —
@@ -313,25 +338,27 @@ std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, co
     for (auto& p : pods) crash_errors(p, 0);
     return out;
   }
-  // node capacity as advertised by the AMD GPU device plugin
-  int64_t max_alloc = 0, total = 0;
-  std::vector<std::string> products;
+  // what the AMD GPU device plugin advertises: whole GPUs or compute partitions, healthy or not
+  std::vector<gpu::GpuNode> nodes;
+  bool nodes_known = true;
   try {
-    Value nodes = k.get("/api/v1/nodes");
-    for (auto& n : nodes.get("items").items()) {
-      int64_t a = n.at_path("status.allocatable").get("amd.com/gpu").as_int(0);
-      total += a;
-      max_alloc = std::max(max_alloc, a);
-      std::string prod = n.at_path("metadata.labels").get("amd.com/gpu.product-name").as_string();
-      if (!prod.empty()) products.push_back(prod);
-    }
+    nodes = gpu::gpu_nodes(k.get("/api/v1/nodes"));
   } catch (const std::exception&) {
-    // listing nodes may be forbidden for namespace-scoped users
-    max_alloc = -1;
+    nodes_known = false;  // listing nodes may be forbidden for namespace-scoped users
   }
-  if (max_alloc == 0)
+  const gpu::GpuNode* big = gpu::largest(nodes);
+  if (nodes_known && nodes.empty())
     out.push_back(kPad + log::color("GPU: ", "202+b") +
                   "no node advertises amd.com/gpu — is the AMD GPU device plugin DaemonSet running?\n");
+  for (auto& n : nodes)
+    if (n.unhealthy() > 0)
+      out.push_back(kPad + log::color("GPU: ", "202+b") +
+                    strfmt("node %s: %lld of %lld %s unhealthy (capacity %lld, allocatable %lld) — the device "
+                           "plugin stopped offering them (a GPU fault, an ECC or XGMI error, a driver reset): "
+                           "check the node's amdgpu kernel log or `amd-smi`",
+                           n.name.c_str(), (long long)n.unhealthy(), (long long)n.capacity, n.resource.c_str(),
+                           (long long)n.capacity, (long long)n.gpus) +
+                    "\n");
   for (auto& p : pods) {
     int64_t want = gpu_request(p);
     if (want == 0) {
@@ -339,10 +366,25 @@ std::vector<std::string> gpu_problems(kube::Client& k, const std::string& ns, co
       continue;
     }
     std::string name = p.at_path("metadata.name").as_string();
-    if (max_alloc > 0 && want > max_alloc)
-      out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + " requests amd.com/gpu: " +
-                    std::to_string(want) + " but the largest node has " + std::to_string(max_alloc) +
-                    " (MI355X nodes expose 8 GPUs; HBM is not a schedulable resource)\n");
+    if (big != nullptr && want > big->gpus)
+      out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + " requests " + std::to_string(want) +
+                    " GPU device(s) but the largest node has " + std::to_string(big->gpus) + " (" + big->name + ": " +
+                    big->describe() + "; HBM is not a schedulable resource)\n");
+    else if (insufficient_gpus(p) && nodes_known) {
+      // it would fit on an empty node: say who holds the devices now
+      for (auto& n : nodes) {
+        if (n.gpus <= 0) continue;
+        std::string why;
+        std::string holders = gpu_holders(k, n.name, &why);
+        if (!holders.empty())
+          out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + " waits for " + std::to_string(want) +
+                        " GPU device(s); node " + n.name + " (" + std::to_string(n.gpus) + " " + n.resource +
+                        ") has them held by " + holders + "\n");
+        else if (!why.empty())
+          out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + " waits for " + std::to_string(want) +
+                        " GPU device(s); the pods holding node " + n.name + "'s cannot be listed (" + why + ")\n");
+      }
+    }
     std::string shm = shm_problem(p, want);
     if (!shm.empty()) out.push_back(kPad + log::color("GPU: ", "202+b") + "pod " + name + ": " + shm + "\n");
     for (auto& prob : gpu::pod_sizing_problems(p.get("spec")))

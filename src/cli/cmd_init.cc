@@ -45,23 +45,30 @@ struct InitState {
 // under the developer (and GPU nodes are often air-gapped, with images pre-pulled by tag).
 const char* kDefaultRocmImage = "rocm/pytorch:rocm7.0_ubuntu24.04_py3.12_pytorch_release_2.8.0";
 
-// Per-GPU CPU/memory from the cluster's GPU nodes when they can be listed (3 s budget; init
-// also works offline), otherwise the per-GPU defaults.
-gpu::PodSizing discover_sizing(int gpus) {
+// The cluster's GPU nodes when they can be listed (3 s budget; init also works offline): what
+// the device plugin advertises (whole GPUs or compute partitions) and the node labeller's labels.
+std::vector<gpu::GpuNode> discover_gpu_nodes() {
   std::vector<gpu::GpuNode> nodes;
-  if (gpus > 0 && !getenv("DEVSPACE_INIT_NO_NODE_DISCOVERY")) {
-    try {
-      auto k = kube::Client::from_devspace_config(Value::map(), false);
-      net::Response r = k->raw("GET", "/api/v1/nodes", "", "application/json", 3000);
-      if (r.status == 200) nodes = gpu::gpu_nodes(json_parse(r.body));
-    } catch (const std::exception&) {
-      // no cluster configured / reachable, or nodes not listable for this user
-    }
+  if (getenv("DEVSPACE_INIT_NO_NODE_DISCOVERY")) return nodes;
+  try {
+    auto k = kube::Client::from_devspace_config(Value::map(), false);
+    net::Response r = k->raw("GET", "/api/v1/nodes", "", "application/json", 3000);
+    if (r.status == 200) nodes = gpu::gpu_nodes(json_parse(r.body));
+  } catch (const std::exception&) {
+    // no cluster configured / reachable, or nodes not listable for this user
   }
+  return nodes;
+}
+
+// Per-device CPU/memory from the nodes, otherwise the per-GPU defaults.
+gpu::PodSizing discover_sizing(int gpus, const std::vector<gpu::GpuNode>& nodes) {
   gpu::PodSizing s = gpu::size_pod(gpus, nodes);
   if (gpus > 0)
-    log::infof("Sizing the pod for %d GPU(s) (%s): %d CPUs, %d Gi memory incl. %d Gi /dev/shm", gpus, s.basis.c_str(),
+    log::infof("Sizing the pod for %d device(s) (%s): %d CPUs, %d Gi memory incl. %d Gi /dev/shm", gpus, s.basis.c_str(),
                s.cpu(), s.memory_gi(), s.shm_gi());
+  if (gpus > 0 && s.hbm_per_device > 0)
+    log::infof("HBM per device: %.0f GB%s (not a schedulable resource)", s.hbm_per_device / 1e9,
+               s.partition.empty() ? "" : (" (" + s.partition + " partition)").c_str());
   return s;
 }
 
@@ -284,12 +291,19 @@ int run_init(cli::Command& c, const std::vector<std::string>&) {
     st.language = prompt::ask(p);
     if (st.language == "rocm-pytorch") {
       prompt::Params g;
-      // HBM (288 GB per MI355X) is not a schedulable resource: GPUs are requested whole.
-      g.question = "How many MI355X GPUs (amd.com/gpu, 1-8) should the container request? (Default: 1)";
+      // HBM is not a schedulable resource: the pod asks for devices, whole MI355X GPUs (SPX) or
+      // compute partitions of them; the bound is what the largest node advertises (8 GPUs, or up
+      // to 64 partitions in CPX mode), 8 when the nodes cannot be listed.
+      auto nodes = discover_gpu_nodes();
+      const gpu::GpuNode* big = gpu::largest(nodes);
+      int max = big != nullptr ? (int)big->gpus : 8;
+      std::string on = big != nullptr ? "; largest node " + big->name + ": " + big->describe() : "";
+      g.question = strfmt("How many %s devices (1-%d%s) should the container request? (Default: 1)",
+                          big != nullptr ? big->resource.c_str() : "amd.com/gpu (MI355X GPU)", max, on.c_str());
       g.default_value = "1";
-      g.validation_regex = "[1-8]";
+      g.validation_regex = gpu::range_regex(max);
       st.gpus = prompt::ask(g);
-      st.sizing = discover_sizing(std::atoi(st.gpus.c_str()));
+      st.sizing = discover_sizing(std::atoi(st.gpus.c_str()), nodes);
     }
   }
   // Dev-mode entrypoint override: keep the container idle for sync + terminal, except for

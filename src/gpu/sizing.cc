@@ -38,41 +38,162 @@ int64_t parse_memory_bytes(const std::string& q_in) {
   return -1;
 }
 
+bool is_gpu_resource(const std::string& name) {
+  if (name == "amd.com/gpu") return true;
+  static const char* kModes[] = {"spx", "dpx", "qpx", "cpx"};
+  if (!starts_with(name, "amd.com/")) return false;
+  std::string rest = name.substr(8);
+  for (auto* m : kModes) {
+    if (rest == m) return true;
+    if (starts_with(rest, std::string(m) + "_nps") && rest.size() > 7) {  // "cpx_nps" + digits
+      bool digits = true;
+      for (size_t i = 7; i < rest.size(); ++i) digits = digits && isdigit((unsigned char)rest[i]);
+      if (digits) return true;
+    }
+  }
+  return false;
+}
+
+int partitions_per_gpu(const std::string& mode_in) {
+  std::string mode = to_lower(trim(mode_in));
+  if (mode == "spx") return 1;
+  if (mode == "dpx") return 2;
+  if (mode == "qpx") return 4;
+  if (mode == "cpx") return 8;  // MI300X/MI325X/MI350X/MI355X: one partition per XCD, 8 XCDs
+  return 0;
+}
+
+int64_t hbm_of_product(const std::string& product) {
+  std::string p = to_lower(product);
+  if (contains(p, "mi355") || contains(p, "mi350")) return 288LL * 1000 * 1000 * 1000;
+  if (contains(p, "mi325")) return 256LL * 1000 * 1000 * 1000;
+  if (contains(p, "mi300x")) return 192LL * 1000 * 1000 * 1000;
+  return 0;
+}
+
+int GpuNode::parts() const {
+  int p = partitions_per_gpu(compute_mode);
+  return p > 0 ? p : 1;
+}
+
+int64_t GpuNode::hbm_per_device() const {
+  int64_t v = vram_per_gpu > 0 ? vram_per_gpu : hbm_of_product(product);
+  return v > 0 ? v / parts() : 0;
+}
+
+std::string GpuNode::describe() const {
+  std::string out;
+  int64_t physical = capacity > 0 ? capacity / parts() : gpus / parts();
+  if (!product.empty()) out += std::to_string(physical) + " x " + product;
+  if (!compute_mode.empty() || !memory_mode.empty()) {
+    std::string mode = to_upper(compute_mode.empty() ? "spx" : compute_mode);
+    if (!memory_mode.empty()) mode += "/" + to_upper(memory_mode);
+    out += (out.empty() ? "" : ", ") + mode;
+  }
+  out += (out.empty() ? "" : ": ") + std::to_string(gpus) + " schedulable " + resource;
+  if (hbm_per_device() > 0) out += strfmt(" of %.0f GB HBM each", hbm_per_device() / 1e9);
+  return out;
+}
+
+// Node labeller labels, under amd.com/ or the older beta.amd.com/ prefix.
+static std::string gpu_label(const Value& labels, const std::string& key) {
+  std::string v = labels.get("amd.com/gpu." + key).as_string();
+  if (v.empty()) v = labels.get("beta.amd.com/gpu." + key).as_string();
+  return v;
+}
+
 std::vector<GpuNode> gpu_nodes(const Value& node_list) {
   std::vector<GpuNode> out;
   for (auto& n : node_list.get("items").items()) {
-    GpuNode g;
-    g.gpus = n.at_path("status.allocatable").get("amd.com/gpu").as_int(0);
-    if (g.gpus <= 0) continue;
-    g.name = n.at_path("metadata.name").as_string();
-    g.cpu = parse_cpu(n.at_path("status.allocatable").get("cpu").as_string());
-    g.memory = parse_memory_bytes(n.at_path("status.allocatable").get("memory").as_string());
-    g.product = n.at_path("metadata.labels").get("amd.com/gpu.product-name").as_string();
-    out.push_back(g);
+    const Value& alloc = n.at_path("status.allocatable");
+    const Value& cap = n.at_path("status.capacity");
+    const Value& labels = n.at_path("metadata.labels");
+    std::set<std::string> resources;
+    for (auto& k : alloc.keys())
+      if (is_gpu_resource(k)) resources.insert(k);
+    for (auto& k : cap.keys())
+      if (is_gpu_resource(k)) resources.insert(k);
+    int64_t node_devices = 0;
+    for (auto& r : resources) node_devices += std::max<int64_t>(0, alloc.get(r).as_int(0));
+    for (auto& r : resources) {
+      GpuNode g;
+      g.resource = r;
+      g.gpus = alloc.get(r).as_int(0);
+      g.capacity = cap.get(r).as_int(g.gpus);
+      if (g.gpus <= 0 && g.capacity <= 0) continue;
+      g.node_devices = node_devices;
+      g.name = n.at_path("metadata.name").as_string();
+      g.cpu = parse_cpu(alloc.get("cpu").as_string());
+      g.memory = parse_memory_bytes(alloc.get("memory").as_string());
+      g.product = gpu_label(labels, "product-name");
+      g.compute_mode = to_lower(gpu_label(labels, "compute-partitioning-mode"));
+      g.memory_mode = to_lower(gpu_label(labels, "memory-partitioning-mode"));
+      if (r != "amd.com/gpu") {  // mixed strategy: the resource name is the partition type
+        std::string rest = r.substr(8);
+        size_t us = rest.find('_');
+        g.compute_mode = rest.substr(0, us);
+        if (us != std::string::npos) g.memory_mode = rest.substr(us + 1);
+      }
+      std::string vram = gpu_label(labels, "vram");
+      if (!vram.empty()) {
+        // the labeller writes e.g. "288G" (decimal) or "288Gi"
+        g.vram_per_gpu = parse_memory_bytes(vram);
+        if (g.vram_per_gpu < 0) g.vram_per_gpu = 0;
+      }
+      out.push_back(g);
+    }
   }
   return out;
+}
+
+const GpuNode* largest(const std::vector<GpuNode>& nodes) {
+  const GpuNode* best = nullptr;
+  for (auto& n : nodes)
+    if (n.gpus > 0 && (best == nullptr || n.gpus > best->gpus)) best = &n;
+  return best;
 }
 
 PodSizing size_pod(int gpus, const std::vector<GpuNode>& nodes) {
   PodSizing s;
   s.gpus = gpus;
   s.basis = "defaults";
-  if (gpus <= 0 || nodes.empty()) return s;
-  // the node type that can hold the most GPUs (a pod must fit on one node)
-  const GpuNode* best = &nodes[0];
-  for (auto& n : nodes)
-    if (n.gpus > best->gpus) best = &n;
-  if (best->cpu > 0) s.cpu_per_gpu = std::max(1, (int)std::floor(best->cpu * 0.9 / (double)best->gpus));
+  const GpuNode* best = largest(nodes);
+  if (gpus <= 0 || best == nullptr) return s;
+  // CPU and memory are shared by every device the node can schedule (all GPU resources)
+  double devices = (double)std::max<int64_t>(best->gpus, best->node_devices);
+  if (best->cpu > 0) s.cpu_per_gpu = std::max(1, (int)std::floor(best->cpu * 0.9 / devices));
   if (best->memory > 0) {
-    int per_gpu_gi = (int)(best->memory * 0.9 / (double)best->gpus / 1073741824.0);
+    int per_gpu_gi = (int)(best->memory * 0.9 / devices / 1073741824.0);
     // keep shm at a quarter of the share when the node is small
     s.shm_per_gpu_gi = std::max(1, std::min(s.shm_per_gpu_gi, per_gpu_gi / 4));
     s.host_per_gpu_gi = std::max(1, per_gpu_gi - s.shm_per_gpu_gi);
   }
   s.product = best->product;
-  s.basis = strfmt("node %s: %lld GPUs, %.0f CPUs, %lld GiB allocatable", best->name.c_str(), (long long)best->gpus,
+  s.resource = best->resource;
+  s.hbm_per_device = best->hbm_per_device();
+  if (best->parts() > 1 || !best->memory_mode.empty())
+    s.partition = to_upper(best->compute_mode.empty() ? "spx" : best->compute_mode) +
+                  (best->memory_mode.empty() ? "" : "/" + to_upper(best->memory_mode));
+  s.basis = strfmt("node %s: %s, %.0f CPUs, %lld GiB allocatable", best->name.c_str(), best->describe().c_str(),
                    best->cpu, (long long)(best->memory / 1073741824LL));
   return s;
+}
+
+int64_t container_gpu_request(const Value& c) {
+  int64_t n = 0;
+  for (auto* part : {"limits", "requests"}) {
+    const Value& res = c.at_path("resources").get(part);
+    for (auto& k : res.keys())
+      if (is_gpu_resource(k)) n += res.get(k).as_int(0);
+    if (n > 0) return n;
+  }
+  return n;
+}
+
+std::string range_regex(int max) {
+  std::string out;
+  for (int i = 1; i <= std::max(1, max); ++i) out += (i > 1 ? "|" : "") + std::to_string(i);
+  return "(" + out + ")";
 }
 
 std::string resources_yaml(const PodSizing& s) {
@@ -83,10 +204,22 @@ std::string resources_yaml(const PodSizing& s) {
            "        # AMD Instinct GPUs requested through the device plugin (amd.com/gpu)\n"
            "        gpu: 0";
   std::string cpu = std::to_string(s.cpu()), mem = std::to_string(s.memory_gi()) + "Gi";
+  std::string hbm;
+  if (s.hbm_per_device > 0 && !s.partition.empty())
+    hbm = strfmt("      # HBM is not a schedulable resource: each %s device is a %s partition with an even\n"
+                 "      # share of its GPU's HBM, %.0f GB (%.0f GB for the %d devices).\n",
+                 s.resource.c_str(), s.partition.c_str(), s.hbm_per_device / 1e9, s.hbm_per_device * s.gpus / 1e9,
+                 s.gpus);
+  else if (s.hbm_per_device > 0)
+    hbm = strfmt("      # HBM is not a schedulable resource: devices are requested whole, %.0f GB HBM each.\n",
+                 s.hbm_per_device / 1e9);
+  else
+    hbm = "      # HBM is not a schedulable resource: GPUs are requested whole (an MI355X has 288 GB; a\n"
+          "      # compute partition of one, DPX/QPX/CPX, an even share of it).\n";
   return strfmt(
-      "      # MI355X sizing for %d GPU(s) (%s): %d CPUs and %d Gi host memory per GPU, i.e. a\n"
+      "      # MI355X sizing for %d device(s) (%s): %d CPUs and %d Gi host memory per device, i.e. a\n"
       "      # %d Gi memory-backed /dev/shm per rank (charged to this memory limit) + %d Gi per rank.\n"
-      "      # HBM (288 GB per GPU) is not a schedulable resource: GPUs are requested whole.\n"
+      "%s"
       "      limits:\n"
       "        gpu: %d\n"
       "        cpu: \"%s\"\n"
@@ -95,7 +228,7 @@ std::string resources_yaml(const PodSizing& s) {
       "        cpu: \"%s\"\n"
       "        memory: \"%s\"",
       s.gpus, s.basis.c_str(), s.cpu_per_gpu, s.shm_per_gpu_gi + s.host_per_gpu_gi, s.shm_per_gpu_gi,
-      s.host_per_gpu_gi, s.gpus, cpu.c_str(), mem.c_str(), cpu.c_str(), mem.c_str());
+      s.host_per_gpu_gi, hbm.c_str(), s.gpus, cpu.c_str(), mem.c_str(), cpu.c_str(), mem.c_str());
 }
 
 std::string gpu_settings_yaml(const PodSizing& s) {
@@ -105,6 +238,9 @@ std::string gpu_settings_yaml(const PodSizing& s) {
       "  shmPerGPU: %d\n"
       "  hostMemoryPerGPU: %d\n",
       s.shm_per_gpu_gi, s.host_per_gpu_gi);
+  if (s.resource != "amd.com/gpu")
+    out += "  # the device plugin's mixed strategy advertises partitions under their own resource name\n"
+           "  gpuResource: \"" + s.resource + "\"\n";
   if (!s.product.empty())
     out += "  # schedule on nodes of this GPU model only (AMD GPU operator node label)\n  gpuProductName: \"" +
            s.product + "\"\n";
@@ -123,8 +259,7 @@ std::vector<std::string> pod_sizing_problems(const Value& spec) {
   }
   for (auto& c : spec.get("containers").items()) {
     const Value& lim = c.at_path("resources.limits");
-    int64_t gpus = lim.get("amd.com/gpu").as_int(0);
-    if (gpus <= 0) gpus = c.at_path("resources.requests").get("amd.com/gpu").as_int(0);
+    int64_t gpus = container_gpu_request(c);
     if (gpus <= 0) continue;
     std::string name = c.get("name").as_string();
     shm_bytes = 0;

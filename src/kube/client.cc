@@ -1,4 +1,5 @@
 #include "kube/client.h"
+#include "gpu/sizing.h"
 
 #include "core/compat.h"
 
@@ -629,13 +630,7 @@ void Client::ensure_namespace(const std::string& ns) {
 
 static int64_t pod_gpu_request(const Value& pod_spec) {
   int64_t n = 0;
-  for (auto& c : pod_spec.get("containers").items()) {
-    const Value* lim = c.at_path("resources.limits").find("amd.com/gpu");
-    const Value* req = c.at_path("resources.requests").find("amd.com/gpu");
-    const Value* v = lim ? lim : req;
-    int64_t x = 0;
-    if (v && (v->is_int() || parse_int64(v->as_string(), &x))) n += v->is_int() ? v->as_int() : x;
-  }
+  for (auto& c : pod_spec.get("containers").items()) n += gpu::container_gpu_request(c);
   return n;
 }
 
@@ -661,26 +656,21 @@ std::string Client::check_gpu_requests(const std::vector<Value>& objs) {
     }
   }
   if (want == 0) return "";
-  int64_t best = 0;
+  std::vector<gpu::GpuNode> nodes;
   try {
-    Value nodes = get("/api/v1/nodes");
-    for (auto& n : nodes.get("items").items()) {
-      int64_t a = 0;
-      const Value& v = n.at_path("status.allocatable").get("amd.com/gpu");
-      if (v.is_int()) a = v.as_int();
-      else parse_int64(v.as_string(), &a);
-      best = std::max(best, a);
-    }
+    nodes = gpu::gpu_nodes(get("/api/v1/nodes"));
   } catch (const std::exception&) {
     return "";  // no permission to list nodes: nothing to say
   }
+  // whole GPUs, or compute partitions of them (CPX: 64 devices per 8-GPU node)
+  const gpu::GpuNode* big = gpu::largest(nodes);
   std::string msg;
-  if (best == 0)
+  if (big == nullptr)
     msg = who + " requests " + std::to_string(want) +
-          " amd.com/gpu but no node advertises amd.com/gpu (is the AMD GPU device plugin running?)";
-  else if (want > best)
-    msg = who + " requests " + std::to_string(want) + " amd.com/gpu but the largest node offers " +
-          std::to_string(best) + " — the pod cannot be scheduled";
+          " GPU device(s) but no node advertises amd.com/gpu (is the AMD GPU device plugin running?)";
+  else if (want > big->gpus)
+    msg = who + " requests " + std::to_string(want) + " GPU device(s) but the largest node offers " +
+          std::to_string(big->gpus) + " (" + big->name + ": " + big->describe() + ") — the pod cannot be scheduled";
   if (!msg.empty()) log::warn(msg);
   return msg;
 }

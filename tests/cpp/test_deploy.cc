@@ -19,6 +19,8 @@
 #include "build/docker.h"
 #include "generator/generator.h"
 #include "gpu/sizing.h"
+#include <regex>
+
 #include "testing.h"
 
 using namespace ds;
@@ -479,11 +481,11 @@ static Value init_values(int gpus, const std::vector<gpu::GpuNode>& nodes = {}) 
   return yaml_parse(v);
 }
 
-static void check_gpu_pod_invariants(const Value& spec, int gpus) {
+static void check_gpu_pod_invariants(const Value& spec, int gpus, const std::string& resource = "amd.com/gpu") {
   const Value& ct = spec.get("containers")[0];
   const Value& lim = ct.at_path("resources.limits");
   const Value& req = ct.at_path("resources.requests");
-  EXPECT_EQ(lim.get("amd.com/gpu").as_int(), (int64_t)gpus);
+  EXPECT_EQ(lim.get(resource).as_int(), (int64_t)gpus);
   double cpu = gpu::parse_cpu(lim.get("cpu").as_string());
   int64_t mem = gpu::parse_memory_bytes(lim.get("memory").as_string());
   EXPECT_TRUE(cpu >= gpus);  // at least one core per rank
@@ -544,6 +546,90 @@ TEST(component_chart_gpu_sizing_from_node_allocatable) {
   EXPECT_EQ(spec.at_path("nodeSelector").get("amd.com/gpu.product-name").as_string(),
             std::string("AMD_Instinct_MI355X"));
   EXPECT_EQ(spec.get("containers")[0].at_path("resources.limits.cpu").as_string(), std::string("112"));
+}
+
+// MI355X nodes in SPX mode advertise 8 devices of 288 GB; in CPX mode (one
+// partition per XCD) 64 devices of an even 36 GB share. The node labeller says which.
+static Value mi355x_node(const std::string& name, const std::string& mode, const std::string& nps,
+                         const std::string& resource, int64_t capacity, int64_t allocatable) {
+  return yaml_parse(
+      "items:\n"
+      "- metadata:\n"
+      "    name: " + name + "\n"
+      "    labels: {amd.com/gpu.product-name: AMD_Instinct_MI355X, amd.com/gpu.vram: 288G,\n"
+      "             amd.com/gpu.compute-partitioning-mode: " + mode + ", amd.com/gpu.memory-partitioning-mode: " + nps + "}\n"
+      "  status:\n"
+      "    capacity: {cpu: '256', memory: 3221225472Ki, " + resource + ": '" + std::to_string(capacity) + "'}\n"
+      "    allocatable: {cpu: '256', memory: 3221225472Ki, " + resource + ": '" + std::to_string(allocatable) + "'}\n");
+}
+
+TEST(gpu_sizing_spx_x8_node) {
+  auto gn = gpu::gpu_nodes(mi355x_node("mi355x-spx", "spx", "nps1", "amd.com/gpu", 8, 8));
+  EXPECT_EQ(gn.size(), (size_t)1);
+  EXPECT_EQ(gn[0].parts(), 1);
+  EXPECT_EQ(gn[0].hbm_per_device(), (int64_t)288000000000LL);
+  EXPECT_EQ(gn[0].unhealthy(), (int64_t)0);
+  EXPECT_TRUE(contains(gn[0].describe(), "8 x AMD_Instinct_MI355X, SPX/NPS1: 8 schedulable amd.com/gpu of 288 GB"));
+  gpu::PodSizing s = gpu::size_pod(8, gn);
+  EXPECT_EQ(s.cpu_per_gpu, 28);
+  EXPECT_EQ(s.hbm_per_device, (int64_t)288000000000LL);
+  EXPECT_TRUE(contains(gpu::resources_yaml(s), "288 GB HBM each"));
+  helm::Chart c = helm::load_chart(std::string(DEVSPACE_SOURCE_DIR) + "/templates/_base/chart");
+  helm::RenderOptions o;
+  o.release_name = "train";
+  auto objs = helm::render(c, init_values(8, gn), o);
+  check_gpu_pod_invariants(find_kind(objs, "Deployment")->at_path("spec.template.spec"), 8);
+}
+
+TEST(gpu_sizing_cpx_x64_node) {
+  auto gn = gpu::gpu_nodes(mi355x_node("mi355x-cpx", "CPX", "NPS2", "amd.com/gpu", 64, 64));
+  EXPECT_EQ(gn.size(), (size_t)1);
+  EXPECT_EQ(gn[0].parts(), 8);
+  EXPECT_EQ(gn[0].hbm_per_device(), (int64_t)36000000000LL);  // 288 GB / 8 partitions
+  EXPECT_TRUE(contains(gn[0].describe(), "8 x AMD_Instinct_MI355X, CPX/NPS2: 64 schedulable amd.com/gpu of 36 GB"));
+  gpu::PodSizing s = gpu::size_pod(8, gn);
+  // a 64th of the node per device, not an 8th
+  EXPECT_EQ(s.cpu_per_gpu, 3);                             // floor(256 * 0.9 / 64)
+  EXPECT_EQ(s.shm_per_gpu_gi + s.host_per_gpu_gi, 43);     // floor(3072 GiB * 0.9 / 64)
+  EXPECT_EQ(s.shm_per_gpu_gi, 10);
+  EXPECT_EQ(s.partition, std::string("CPX/NPS2"));
+  std::string res = gpu::resources_yaml(s);
+  EXPECT_TRUE(contains(res, "CPX/NPS2 partition") && contains(res, "36 GB") && contains(res, "288 GB for the 8"));
+  EXPECT_TRUE(!contains(res, "288 GB per GPU"));
+  helm::Chart c = helm::load_chart(std::string(DEVSPACE_SOURCE_DIR) + "/templates/_base/chart");
+  helm::RenderOptions o;
+  o.release_name = "train";
+  auto objs = helm::render(c, init_values(8, gn), o);
+  check_gpu_pod_invariants(find_kind(objs, "Deployment")->at_path("spec.template.spec"), 8);
+  // the init prompt's bound is the largest node's allocatable
+  EXPECT_EQ(gpu::largest(gn)->gpus, (int64_t)64);
+  std::regex r("^" + gpu::range_regex(64) + "$");
+  EXPECT_TRUE(std::regex_match("64", r) && std::regex_match("1", r) && std::regex_match("9", r));
+  EXPECT_TRUE(!std::regex_match("65", r) && !std::regex_match("0", r) && !std::regex_match("640", r));
+}
+
+TEST(gpu_sizing_mixed_strategy_resource_names) {
+  EXPECT_TRUE(gpu::is_gpu_resource("amd.com/gpu") && gpu::is_gpu_resource("amd.com/cpx_nps2") &&
+              gpu::is_gpu_resource("amd.com/spx"));
+  EXPECT_TRUE(!gpu::is_gpu_resource("amd.com/gpu.product-name") && !gpu::is_gpu_resource("amd.com/cpx_npsx") &&
+              !gpu::is_gpu_resource("nvidia.com/gpu"));
+  auto gn = gpu::gpu_nodes(mi355x_node("mixed", "", "", "amd.com/cpx_nps2", 64, 62));
+  EXPECT_EQ(gn.size(), (size_t)1);
+  EXPECT_EQ(gn[0].resource, std::string("amd.com/cpx_nps2"));
+  EXPECT_EQ(gn[0].compute_mode, std::string("cpx"));
+  EXPECT_EQ(gn[0].memory_mode, std::string("nps2"));
+  EXPECT_EQ(gn[0].unhealthy(), (int64_t)2);
+  gpu::PodSizing s = gpu::size_pod(4, gn);
+  EXPECT_EQ(s.resource, std::string("amd.com/cpx_nps2"));
+  EXPECT_TRUE(contains(gpu::gpu_settings_yaml(s), "gpuResource: \"amd.com/cpx_nps2\""));
+  helm::Chart c = helm::load_chart(std::string(DEVSPACE_SOURCE_DIR) + "/templates/_base/chart");
+  helm::RenderOptions o;
+  o.release_name = "train";
+  auto objs = helm::render(c, init_values(4, gn), o);
+  const Value& spec = find_kind(objs, "Deployment")->at_path("spec.template.spec");
+  check_gpu_pod_invariants(spec, 4, "amd.com/cpx_nps2");
+  EXPECT_TRUE(spec.get("containers")[0].at_path("resources.limits").find("amd.com/gpu") == nullptr);
+  EXPECT_EQ(gpu::container_gpu_request(spec.get("containers")[0]), (int64_t)4);
 }
 
 TEST(component_chart_cpu_only_has_no_gpu_scheduling) {

@@ -214,7 +214,7 @@ def test_init_8_gpus_sizes_pod_and_analyze_flags_undersized(localkube):
     answers = "\n8\ntorch8-ns\n\nlocal.registry\nlocal.registry/torch8\nno\n"
     out = lk.run(["init"], proj, input=answers).stdout
     assert "Project successfully initialized" in out
-    assert "Sizing the pod for 8 GPU(s)" in out, out
+    assert "Sizing the pod for 8 device(s)" in out, out
     values = yaml.safe_load(open(os.path.join(proj, "chart", "values.yaml")))
     comp = values["components"][0]
     res = comp["containers"][0]["resources"]
