@@ -5,6 +5,13 @@ Serves what the devspace builder needs (reference: builder/docker/docker.go): /_
 /images/{name}/tag, /images/{name}/json. Images are directories (rootfs + config.json); a
 Dockerfile is interpreted instruction by instruction (FROM/WORKDIR/COPY/ADD/ENV/ARG/EXPOSE/
 CMD/ENTRYPOINT/LABEL/USER; RUN is recorded but not executed — no network on the box).
+
+Layer cache keys as the classic builder computes them: each instruction's key chains the
+previous one with the instruction text (after ARG/ENV substitution), and a COPY/ADD also with
+the content (paths, modes, bytes; not mtimes) of what it copies. A key the daemon built before
+is "Using cache"; the image's RootFS.Layers lists the keys of its filesystem layers (COPY, ADD,
+RUN). So a Dockerfile that copies train.py before a slow RUN rebuilds that RUN on every edit
+of train.py, and one that copies it after does not, which a test can see without executing RUN.
 """
 
 from __future__ import annotations
@@ -81,6 +88,24 @@ class ImageStore:
         shutil.copytree(src, dst, symlinks=True)
         return True
 
+    # -- layer cache (keys only: the local builder keeps no per-layer filesystem) -----------
+    def _layers_path(self):
+        return os.path.join(self.root, "layers.json")
+
+    def layers_seen(self):
+        try:
+            with open(self._layers_path()) as f:
+                return json.load(f)
+        except (OSError, ValueError):
+            return {}
+
+    def remember_layers(self, keys):
+        seen = self.layers_seen()
+        seen.update(keys)
+        with open(self._layers_path() + ".tmp", "w") as f:
+            json.dump(seen, f)
+        os.replace(self._layers_path() + ".tmp", self._layers_path())
+
     def tag(self, src_ref, dst_ref):
         src = self.local(src_ref)
         if not src:
@@ -123,6 +148,33 @@ def _exec_form(arg):
     return ["/bin/sh", "-c", arg]
 
 
+def _content_hash(paths, base):
+    """What a COPY/ADD copies, as the classic builder checksums it: relative paths, modes, symlink
+    targets and file bytes; mtimes and ownership do not count."""
+    h = hashlib.sha256()
+
+    def add(p):
+        st = os.lstat(p)
+        h.update(os.path.relpath(p, base).encode() + b"\0" + str(st.st_mode).encode() + b"\0")
+        if os.path.islink(p):
+            h.update(b"L" + os.readlink(p).encode())
+        elif os.path.isfile(p):
+            with open(p, "rb") as f:
+                for chunk in iter(lambda: f.read(1 << 20), b""):
+                    h.update(chunk)
+
+    for top in paths:
+        if os.path.isdir(top) and not os.path.islink(top):
+            for d, dirs, files in os.walk(top):
+                dirs.sort()
+                add(d)
+                for name in sorted(files) + [x for x in dirs if os.path.islink(os.path.join(d, x))]:
+                    add(os.path.join(d, name))
+        else:
+            add(top)
+    return h.hexdigest()
+
+
 def build_image(store, context_dir, dockerfile, tag, buildargs=None, target=None, log=print):
     with open(os.path.join(context_dir, dockerfile)) as f:
         instrs = _parse_dockerfile(f.read())
@@ -134,6 +186,9 @@ def build_image(store, context_dir, dockerfile, tag, buildargs=None, target=None
     config = {"Env": [], "Cmd": None, "Entrypoint": None, "WorkingDir": "/", "ExposedPorts": {}, "Labels": {}}
     stage_name = None
     total = len(instrs)
+    key = hashlib.sha256(b"scratch").hexdigest()  # the chained cache key of the current step
+    layers, history, new_keys = [], [], {}
+    seen = store.layers_seen()
 
     def subst(s):
         env = dict(args)
@@ -144,6 +199,7 @@ def build_image(store, context_dir, dockerfile, tag, buildargs=None, target=None
 
     for i, (op, arg) in enumerate(instrs, 1):
         log(f"Step {i}/{total} : {op} {arg}")
+        copied = None  # COPY/ADD: the content hash of its sources
         if op == "FROM":
             if stage_name and target and stage_name == target:
                 break
@@ -156,13 +212,19 @@ def build_image(store, context_dir, dockerfile, tag, buildargs=None, target=None
             if base in stages:
                 shutil.copytree(stages[base]["rootfs"], rootfs, dirs_exist_ok=True, symlinks=True)
                 config = json.loads(json.dumps(stages[base]["config"]))
+                key, layers = stages[base]["key"], list(stages[base]["layers"])
             else:
                 img = store.resolve(base)
                 if img:
                     shutil.copytree(img["rootfs"], rootfs, dirs_exist_ok=True, symlinks=True)
-                    config.update(img["config"])
+                    config.update({k: v for k, v in img["config"].items() if k not in ("RootFS", "History")})
+                    layers = list((img["config"].get("RootFS") or {}).get("Layers") or [])
+                    key = hashlib.sha256(("FROM " + base + "|" + ",".join(layers)).encode()).hexdigest()
                 else:
                     log(f" ---> using host runtime for base image {base}")
+                    layers = []
+                    key = hashlib.sha256(("FROM " + base).encode()).hexdigest()
+            history = []
         elif op == "WORKDIR":
             wd = subst(arg)
             config["WorkingDir"] = wd if wd.startswith("/") else os.path.join(config["WorkingDir"], wd)
@@ -190,6 +252,10 @@ def build_image(store, context_dir, dockerfile, tag, buildargs=None, target=None
                         dst = dst + "/"
                 else:
                     expanded.append(pat)
+            missing = [os.path.relpath(sp, base_src) for sp in expanded if not os.path.lexists(os.path.normpath(sp))]
+            if missing:
+                raise RuntimeError(f"COPY failed: stat {missing[0]}: file does not exist")
+            copied = _content_hash([os.path.normpath(sp) for sp in expanded], base_src)
             for sp in expanded:
                 s = os.path.relpath(sp, base_src)
                 sp = os.path.normpath(sp)
@@ -229,12 +295,28 @@ def build_image(store, context_dir, dockerfile, tag, buildargs=None, target=None
                 config["Labels"][k] = v
         elif op == "RUN":
             log(" ---> RUN recorded, not executed by the local builder (no network on this host)")
+        if op != "FROM":
+            text = f"{op} {subst(arg)}" + (f" content={copied}" if copied else "")
+            key = hashlib.sha256((key + "|" + text).encode()).hexdigest()
+            fs_layer = op in ("COPY", "ADD", "RUN")
+            if key in seen:
+                log(" ---> Using cache")
+            log(f" ---> {key[:12]}")
+            if fs_layer:
+                layers.append("sha256:" + key)
+            history.append({"created_by": f"{op} {arg}", "empty_layer": not fs_layer, "key": key,
+                            "cached": key in seen})
+            new_keys[key] = f"{op} {arg}"
         if stage_name:
-            stages[stage_name] = {"rootfs": rootfs + "-" + stage_name, "config": json.loads(json.dumps(config))}
+            stages[stage_name] = {"rootfs": rootfs + "-" + stage_name, "config": json.loads(json.dumps(config)),
+                                  "key": key, "layers": list(layers)}
             if os.path.exists(stages[stage_name]["rootfs"]):
                 shutil.rmtree(stages[stage_name]["rootfs"])
             shutil.copytree(rootfs, stages[stage_name]["rootfs"], symlinks=True)
+    config["RootFS"] = {"Type": "layers", "Layers": layers}
+    config["History"] = history
     store.save(tag, rootfs, config)
+    store.remember_layers(new_keys)
     shutil.rmtree(work, ignore_errors=True)
     return "sha256:" + hashlib.sha256(json.dumps(config, sort_keys=True).encode() + tag.encode()).hexdigest()
 
@@ -323,8 +405,19 @@ def make_app(store: ImageStore):
         img = store.resolve(name)
         if not img:
             return web.json_response({"message": f"No such image: {name}"}, status=404)
-        return web.json_response({"Id": "sha256:" + hashlib.sha256(name.encode()).hexdigest(), "Config": img["config"],
+        cfg = {k: v for k, v in img["config"].items() if k not in ("RootFS", "History")}
+        return web.json_response({"Id": "sha256:" + hashlib.sha256(name.encode()).hexdigest(), "Config": cfg,
+                                  "RootFS": img["config"].get("RootFS") or {"Type": "layers", "Layers": []},
                                   "RepoTags": [name]})
+
+    async def history(request):
+        name = request.match_info["name"]
+        img = store.resolve(name)
+        if not img:
+            return web.json_response({"message": f"No such image: {name}"}, status=404)
+        out = [{"Id": "sha256:" + h["key"], "CreatedBy": h["created_by"], "Size": 0,
+                "Comment": "cached" if h.get("cached") else ""} for h in img["config"].get("History") or []]
+        return web.json_response(list(reversed(out)))  # newest first, as dockerd answers
 
     for prefix in ("", "/v{ver}"):
         app.router.add_get(prefix + "/_ping", ping)  # add_get also registers HEAD
@@ -335,4 +428,5 @@ def make_app(store: ImageStore):
         app.router.add_post(prefix + "/images/{name:.+}/push", push)
         app.router.add_post(prefix + "/images/{name:.+}/tag", tag_image)
         app.router.add_get(prefix + "/images/{name:.+}/json", inspect)
+        app.router.add_get(prefix + "/images/{name:.+}/history", history)
     return app
