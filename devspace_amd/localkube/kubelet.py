@@ -155,6 +155,10 @@ class Kubelet:
         self.pull_seconds = 0.0
         self.pulled = set()
         self._pull_done = {}  # image -> monotonic time its pull completes
+        # Flaky registry: pulls of images starting with a key fail with a transient error (an i/o
+        # timeout) until the monotonic time given; the kubelet retries after its back-off, as a
+        # real one does.
+        self.pull_flaky = {}
 
     # ------------------------------------------------------------ node
 
@@ -171,6 +175,21 @@ class Kubelet:
         self.gpus_total = self.physical_gpus * PARTITIONS[partition]
         self.unhealthy = max(0, min(unhealthy, self.gpus_total))
         self.gpus_free = list(range(self.gpus_total - self.unhealthy))  # the last ones failed
+
+    def add_gpus(self, n):
+        """A GPU node pool scaled up (a cluster autoscaler's new node, folded into this one): n more
+        physical GPUs in the current partition mode, advertised at once."""
+        old_total = self.gpus_total
+        self.physical_gpus += n
+        self.gpus_total = self.physical_gpus * PARTITIONS[self.partition]
+        self.gpus_free.extend(range(old_total, self.gpus_total))
+        res = self.gpu_resource
+
+        def grow(o):
+            for part in ("capacity", "allocatable"):
+                o["status"][part][res] = str(self.gpus_total - (self.unhealthy if part == "allocatable" else 0))
+
+        self.store.mutate("", "nodes", "", self.node_name, grow)
 
     def register_node(self):
         res = self.gpu_resource
@@ -484,6 +503,9 @@ class Kubelet:
 
     def _prepare_rootfs(self, rt, c, pod):
         image = c.spec.get("image", "")
+        if any(image.startswith(k) and time.monotonic() < t for k, t in self.pull_flaky.items()):
+            return "ErrImagePull", (f'Failed to pull image "{image}": rpc error: code = Unknown desc = failed to '
+                                    f'resolve reference "{image}": dial tcp 10.96.0.53:443: i/o timeout')
         img = self.images.resolve(image)
         if img is None:
             if not image or not any(image.split("@")[0].split(":")[0].endswith(h) or image.startswith(h)
@@ -617,6 +639,9 @@ class Kubelet:
         changed = False
         for name, c in rt.containers.items():
             if c.fatal:
+                if getattr(c, "retry_at", None) and time.monotonic() >= c.retry_at:
+                    c.fatal, c.retry_at = None, None  # a transient pull error: try again after the back-off
+                    continue
                 if c.fatal == "ErrImagePull" and time.monotonic() - c.fatal_at >= 1.0:
                     # the kubelet's image back-off, as on a real node: ErrImagePull -> ImagePullBackOff
                     image = c.spec.get("image", "")
@@ -637,6 +662,8 @@ class Kubelet:
                     c.state = {"waiting": {"reason": reason, "message": msg}}
                     c.fatal = reason
                     c.fatal_at = time.monotonic()
+                    if "i/o timeout" in msg:
+                        c.retry_at = c.fatal_at + 2.0
                     self.event(pod, "Failed", msg, "Warning")
                     changed = True
                     continue

@@ -162,6 +162,12 @@ ENV = {
     "DEVSPACE_PULL_TIMEOUT": "Seconds a rollout wait may last in all while a pod of the release is still pulling "
                              "its image (default 1800); past the chart's timeout the wait goes on only for "
                              "pulls, and a first install whose pull outlasts this is kept, not purged.",
+    "DEVSPACE_PULL_ERROR_GRACE_S": "Seconds an `ErrImagePull`/`ImagePullBackOff` the kubelet may yet get past "
+                                   "(a registry timeout, a 5xx) may last before the rollout wait fails (default 30); "
+                                   "a missing image, an invalid name or a denied pull fail at once.",
+    "DEVSPACE_UNSCHEDULABLE_GRACE_S": "Seconds a pod may stay `Unschedulable` before the rollout wait fails (default "
+                                      "10); while the cluster autoscaler reports `TriggeredScaleUp` for the pod the "
+                                      "wait runs to the chart's timeout.",
     "DEVSPACE_RELEASE_REPO": "GitHub `owner/repo` whose releases `devspace upgrade` installs.",
     "DEVSPACE_RELEASE_URL": "Plain HTTP(S) release mirror for `devspace upgrade` (`<url>/latest`, "
                             "`<url>/devspace-linux-amd64` and its `.sha256`).",

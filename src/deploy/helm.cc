@@ -878,9 +878,41 @@ static int64_t event_time(const std::string& ts) {
   return (int64_t)timegm(&t);
 }
 
-static bool fatal_waiting_reason(const std::string& r) {
+static bool pull_failure_reason(const std::string& r) {
   return r == "ErrImagePull" || r == "ImagePullBackOff" || r == "InvalidImageName" || r == "ErrImageNeverPull";
 }
+
+// A pull error no retry fixes: the image or tag does not exist, the name is invalid, access is
+// denied, or the pod may not pull at all. Anything else (a registry timeout, a 5xx, a reset
+// connection, a 429) is retried by the kubelet's back-off and may still succeed.
+static bool permanent_pull_error(const std::string& reason, const std::string& msg_in) {
+  if (reason == "InvalidImageName" || reason == "ErrImageNeverPull") return true;
+  std::string m = to_lower(msg_in);
+  for (const char* p : {"not found", "manifest unknown", "does not exist", "repository does not exist",
+                        "unauthorized", "denied", "invalid reference format", "no such host"})
+    if (contains(m, p)) return true;
+  return false;
+}
+
+static int env_seconds(const char* name, int def) {
+  const char* v = getenv(name);
+  int s = v && *v ? atoi(v) : def;
+  return s >= 0 ? s : def;
+}
+
+// What the rollout wait saw on earlier polls: when a pod first showed a condition that may yet
+// clear up (Unschedulable while the cluster autoscaler adds a node, a pull error the kubelet is
+// retrying), so it is called fatal only once it has lasted.
+struct ProgressMemory {
+  std::map<std::string, std::chrono::steady_clock::time_point> first_seen;
+  std::map<std::string, std::string> pull_error;  // pod/container -> last ErrImagePull message
+  std::set<std::string> told;
+  double seen_for(const std::string& key) {
+    auto now = std::chrono::steady_clock::now();
+    auto it = first_seen.emplace(key, now).first;
+    return std::chrono::duration<double>(now - it->second).count();
+  }
+};
 
 static std::string match_labels_selector(const Value& workload) {
   std::vector<std::string> parts;
@@ -889,7 +921,17 @@ static std::string match_labels_selector(const Value& workload) {
   return join(parts, ",");
 }
 
-static PodProgress pod_progress(kube::Client& k, const Value& workload, const std::string& ns) {
+static Value pod_events(kube::Client& k, const std::string& ns, const std::string& pod) {
+  try {
+    return k.get("/api/v1/namespaces/" + ns + "/events?fieldSelector=" +
+                 net::url_encode("involvedObject.kind=Pod,involvedObject.name=" + pod));
+  } catch (const std::exception&) {
+    return Value::map();
+  }
+}
+
+static PodProgress pod_progress(kube::Client& k, const Value& workload, const std::string& ns,
+                                ProgressMemory& mem) {
   PodProgress out;
   std::string sel = match_labels_selector(workload);
   if (sel.empty()) return out;
@@ -899,6 +941,13 @@ static PodProgress pod_progress(kube::Client& k, const Value& workload, const st
   } catch (const std::exception&) {
     return out;
   }
+  // Unschedulable: a node may be on its way (a cluster autoscaler scales GPU node pools from
+  // zero: minutes). Fatal only once it lasted DEVSPACE_UNSCHEDULABLE_GRACE_S (10) with no
+  // TriggeredScaleUp event for the pod; with one, the wait runs to its timeout.
+  const int unsched_grace = env_seconds("DEVSPACE_UNSCHEDULABLE_GRACE_S", 10);
+  // ErrImagePull / ImagePullBackOff of an error the kubelet may yet get past (a registry
+  // timeout): fatal once it lasted DEVSPACE_PULL_ERROR_GRACE_S (30); a missing image at once.
+  const int pull_grace = env_seconds("DEVSPACE_PULL_ERROR_GRACE_S", 30);
   std::vector<const Value*> creating;
   for (auto& p : pods) {
     if (!p.at_path("metadata.deletionTimestamp").is_null()) continue;
@@ -906,19 +955,48 @@ static PodProgress pod_progress(kube::Client& k, const Value& workload, const st
     for (auto& c : p.at_path("status.conditions").items())
       if (c.get("type").as_string() == "PodScheduled" && c.get("status").as_string() == "False" &&
           c.get("reason").as_string() == "Unschedulable") {
-        out.fatal = "pod " + pn + ": Unschedulable: " + c.get("message").as_string();
+        std::string msg = "pod " + pn + ": Unschedulable: " + c.get("message").as_string();
+        double lasted = mem.seen_for("unsched/" + pn);
+        std::string scale_up;
+        Value evs = pod_events(k, ns, pn);  // (not iterated as a temporary: it would dangle)
+        for (auto& e : evs.get("items").items())
+          if (e.get("reason").as_string() == "TriggeredScaleUp") scale_up = e.get("message").as_string();
+        if (!scale_up.empty()) {
+          if (mem.told.insert("scaleup/" + pn).second)
+            log::info(msg + "; the cluster autoscaler is adding a node (" + scale_up + "): waiting");
+          return out;
+        }
+        if (lasted >= unsched_grace) out.fatal = msg;
         return out;
       }
     bool waiting_create = false;
     for (const char* field : {"status.initContainerStatuses", "status.containerStatuses"})
       for (auto& cs : p.at_path(field).items()) {
         std::string r = cs.at_path("state.waiting.reason").as_string();
-        if (fatal_waiting_reason(r)) {
-          out.fatal = "pod " + pn + ": container " + cs.get("name").as_string() + ": " + r +
-                      (cs.at_path("state.waiting.message").as_string().empty()
-                           ? ""
-                           : ": " + cs.at_path("state.waiting.message").as_string());
-          return out;
+        std::string cname = cs.get("name").as_string();
+        std::string wmsg = cs.at_path("state.waiting.message").as_string();
+        if (pull_failure_reason(r)) {
+          std::string key = pn + "/" + cname;
+          if (r == "ErrImagePull" && !wmsg.empty()) mem.pull_error[key] = wmsg;
+          std::string why = mem.pull_error.count(key) ? mem.pull_error[key] : wmsg;
+          if (why.empty() || r == "ImagePullBackOff") {
+            // the back-off message says nothing about the cause: the kubelet's Failed event does
+            Value evs = pod_events(k, ns, pn);
+            for (auto& e : evs.get("items").items())
+              if (e.get("reason").as_string() == "Failed" && contains(e.get("message").as_string(), "ull image"))
+                why = e.get("message").as_string();
+          }
+          double lasted = mem.seen_for("pull/" + key);
+          if (permanent_pull_error(r, why) || lasted >= pull_grace) {
+            out.fatal = "pod " + pn + ": container " + cname + ": " + r + (wmsg.empty() ? "" : ": " + wmsg) +
+                        (why.empty() || why == wmsg ? "" : " (" + why + ")");
+            return out;
+          }
+          if (mem.told.insert("pullretry/" + key).second)
+            log::info("pod " + pn + ": container " + cname + ": " + r + (why.empty() ? "" : " (" + why + ")") +
+                      ": the kubelet retries the pull; failing after " + std::to_string(pull_grace) +
+                      " s (DEVSPACE_PULL_ERROR_GRACE_S)");
+          continue;
         }
         if (r == "ContainerCreating" || r == "PodInitializing") waiting_create = true;
       }
@@ -986,6 +1064,7 @@ Client::WaitOutcome Client::wait_ready(const std::vector<Value>& objs, const std
     return (int64_t)std::chrono::duration_cast<std::chrono::milliseconds>(t - clock::now()).count();
   };
   bool told = false;
+  ProgressMemory mem;
   for (auto& o : objs) {
     std::string kind = o.get("kind").as_string();
     if (kind != "Deployment" && kind != "StatefulSet" && kind != "ReplicaSet" && kind != "DaemonSet" &&
@@ -1016,7 +1095,7 @@ Client::WaitOutcome Client::wait_ready(const std::vector<Value>& objs, const std
         if (ms_until(deadline) > 0) continue;
         return {"timed out waiting for the condition (" + pending + ")"};
       }
-      PodProgress pp = pod_progress(*k_, o, ons);
+      PodProgress pp = pod_progress(*k_, o, ons, mem);
       if (!pp.fatal.empty()) {
         WaitOutcome w;
         w.err = "rollout failed: " + pp.fatal + " (" + pending + ")";

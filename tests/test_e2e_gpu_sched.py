@@ -6,6 +6,7 @@ waited out for the rollout timeout; Ctrl-C ends a one-shot command right away.""
 
 import signal
 import subprocess
+import threading
 import time
 
 from conftest import DevspaceEnv
@@ -141,5 +142,48 @@ def test_analyze_reports_a_training_group_that_is_down(tmp_path):
         out = lk.run(["analyze", "--wait=false"], proj, timeout=120, check=False).stdout
         assert "training group is down after rank=1" in out, out
         assert "ValueError: shapes (4,8) and (9,8) not aligned" in out, out
+    finally:
+        cluster.stop()
+
+
+def test_unschedulable_while_the_autoscaler_adds_a_gpu_node_is_waited_out(tmp_path):
+    """GPU node pools often scale from zero. A pod that is Unschedulable while the
+    cluster autoscaler says it triggered a scale-up is waited for (up to the rollout timeout),
+    not failed at the first look; the deploy succeeds once the node's GPUs appear."""
+    from devspace_amd.localkube import LocalCluster
+
+    cluster = LocalCluster(str(tmp_path / "state"), gpus=0).start()
+    try:
+        lk = DevspaceEnv(cluster, str(tmp_path))
+        proj = lk.project("rocm-pytorch")
+        lk.env["DEVSPACE_UNSCHEDULABLE_GRACE_S"] = "1"
+
+        def autoscaler():
+            deadline = time.time() + 60
+            pods = []
+            while time.time() < deadline and not pods:
+                pods = cluster.store.list("", "pods", "rocm-pytorch")
+                time.sleep(0.05)
+            if not pods:
+                return
+            md = pods[0]["metadata"]
+            cluster.store.create("", "events", "rocm-pytorch", {
+                "metadata": {"name": md["name"] + ".scaleup", "namespace": "rocm-pytorch"},
+                "involvedObject": {"kind": "Pod", "name": md["name"], "namespace": "rocm-pytorch", "uid": md["uid"]},
+                "reason": "TriggeredScaleUp", "type": "Normal", "count": 1,
+                "message": "pod triggered scale-up: [{mi355x-pool 0->1 (max: 4)}]",
+                "source": {"component": "cluster-autoscaler"}}, "v1")
+            time.sleep(4.0)  # the node boots
+            cluster.kubelet.add_gpus(1)
+
+        t = threading.Thread(target=autoscaler, daemon=True)
+        t.start()
+        t0 = time.time()
+        r = lk.run(["deploy"], proj, timeout=120, check=False)
+        took = time.time() - t0
+        out = r.stdout + r.stderr
+        assert r.returncode == 0, out
+        assert took >= 4.0, (took, out)
+        assert "the cluster autoscaler is adding a node" in out, out
     finally:
         cluster.stop()

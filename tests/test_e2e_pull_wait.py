@@ -109,3 +109,38 @@ def test_first_install_still_pulling_at_the_budget_is_kept(tmp_path):
         assert len(_events(cluster, "rocm-pytorch", "Pulling")) == 1
     finally:
         cluster.stop()
+
+
+def test_a_transient_pull_error_is_waited_out(tmp_path):
+    """an ErrImagePull the kubelet can get past (the registry timed out) is not fatal
+    at the first look: the wait goes on while the kubelet retries, and the deploy succeeds."""
+    cluster, lk = _cluster(tmp_path, pull_seconds=0.0, gpus=0)
+    try:
+        proj = lk.project("quickstart")
+        cluster.kubelet.pull_flaky[""] = time.monotonic() + 5.0
+        t0 = time.time()
+        r = lk.run(["deploy"], proj, timeout=120, check=False)
+        took = time.time() - t0
+        out = r.stdout + r.stderr
+        assert r.returncode == 0, out
+        assert took >= 4.0, (took, out)
+        assert "i/o timeout" in out and "the kubelet retries the pull" in out, out
+    finally:
+        cluster.stop()
+
+
+def test_a_pull_error_that_lasts_fails_after_the_grace(tmp_path):
+    cluster, lk = _cluster(tmp_path, pull_seconds=0.0, gpus=0)
+    try:
+        proj = lk.project("quickstart")
+        cluster.kubelet.pull_flaky[""] = time.monotonic() + 120.0
+        lk.env["DEVSPACE_PULL_ERROR_GRACE_S"] = "3"
+        t0 = time.time()
+        r = lk.run(["deploy"], proj, timeout=120, check=False)
+        took = time.time() - t0
+        out = r.stdout + r.stderr
+        assert r.returncode != 0, out
+        assert 3.0 <= took < 20, (took, out)  # the grace, not the 40 s rollout timeout
+        assert "rollout failed" in out and "i/o timeout" in out, out
+    finally:
+        cluster.stop()
