@@ -366,12 +366,7 @@ void Session::open_up_shell() {
     }
   }
   up_has_head_ = false;
-  if (up_helper_) {
-    // the change watch runs in the upstream helper: the echo of its own writes is filtered where
-    // they are recorded (src/helper/helper.cc is_own)
-    up_err_.reset(up_shell_->err());
-    write_all(up_shell_->in(), request('W', ""));
-  }
+  if (up_helper_) up_err_.reset(up_shell_->err());  // the watch's events, once open_down_shell asks
   set_nonblocking(up_shell_->in(), true);
   if (up_helper_) start_up_reader();
   if (mode_ != Mode::Compat && !up_helper_) {
@@ -399,7 +394,14 @@ void Session::open_down_shell() {
       down_shell_ = transport_->open({"sh"});
       down_out_.reset(down_shell_->out());
       down_err_.reset(down_shell_->err());
-    } else if (!up_helper_) {
+    } else if (up_helper_) {
+      // The change watch runs in the upstream helper (the echo of its own writes is filtered
+      // where they are recorded, src/helper/helper.cc is_own), and only now that the downstream
+      // side is known to read its events (a watch whose stderr nobody drains fills the
+      // channel and stalls the exec stream that carries the upload replies).
+      std::lock_guard<std::mutex> ug(up_shell_mu_);
+      write_all(up_shell_->in(), request('W', ""));
+    } else {
       // no upstream helper: container-side change events come from this one (no echo filter)
       write_all(down_shell_->in(), request('W', ""));
     }
