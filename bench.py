@@ -372,6 +372,37 @@ def _qs_edit(path, marker):
         f.write(src)
 
 
+def _pf_spans(trace_path, windows):
+    """The devspace port-forward's streams during the timed samples (trace.jsonl
+    `portforward.stream` spans: one per attempt; an attempt the restarting app refused is retried
+    on a new stream): how they went over the link, per edit."""
+    spans = []
+    try:
+        with open(trace_path) as f:
+            for line in f:
+                if '"portforward.stream"' not in line:
+                    continue
+                sp = json.loads(line)
+                t = sp.get("start_us", 0) / 1e6
+                if any(a <= t <= b for a, b in windows):
+                    spans.append(sp)
+    except OSError:
+        return None
+    if not spans:
+        return None
+    n = max(1, len(windows))
+    replies = [sp for sp in spans if sp.get("outcome") == "reply"]
+
+    def ms(key, rows):
+        v = [int(sp[key]) / 1000.0 for sp in rows if int(sp.get(key, -1)) >= 0]
+        return round(_pct(v, 0.5), 2) if v else None
+
+    return {"via": sorted({sp.get("via", "websocket") for sp in spans}),
+            "streams_per_edit": round(len(spans) / n, 2),
+            "refused_per_edit": round(sum(sp.get("outcome") == "refused" for sp in spans) / n, 2),
+            "open_ms_p50": ms("open_us", spans), "reply_first_byte_ms_p50": ms("first_us", replies)}
+
+
 def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=False, timed_start=None,
                     timed_end=None, cold=None, wan=None):
     """examples/quickstart edit -> reload, the way its README runs the dev loop: `devspace dev`
@@ -434,13 +465,15 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
         # answers through the forward (the first iteration of the loop)
         dev_start_s = time.perf_counter() - t_dev
         index, pod_index = os.path.join(proj, "index.js"), os.path.join(root, "app", "index.js")
-        samples, sync_samples = [], []
+        samples, sync_samples, conns, windows = [], [], [], []
         rng = random.Random(4321)
         for i in range(warmup + steps):
             if i == warmup and timed_start:
                 timed_start()
             marker = f"q{i}" + ("_" * (i % 2))  # compat mode compares size + mtime (s)
             time.sleep(rng.uniform(0.0, EDIT_JITTER_S))
+            c0 = link.connections if link is not None else 0
+            w0 = time.monotonic()  # (trace spans carry CLOCK_MONOTONIC microseconds)
             t0 = time.perf_counter()
             _qs_edit(index, marker)
             t_sync = _wait_file_contains(pod_index, f"[{marker}]", timeout=_budget(60))
@@ -456,11 +489,14 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
             if i >= warmup:
                 samples.append((t1 - t0) * 1000.0)
                 sync_samples.append((t_sync - t0) * 1000.0)
+                conns.append((link.connections if link is not None else 0) - c0)
+                windows.append((w0, time.monotonic()))
         if timed_end:
             timed_end()
         out = {"reload_ms": samples, "sync_ms": sync_samples, "dev_start_s": dev_start_s}
         if link is not None:
-            out["link"] = {"connections": link.connections}
+            out["link"] = {"connections": link.connections, "per_edit": conns}
+            out["portforward"] = _pf_spans(os.path.join(proj, ".devspace", "logs", "trace.jsonl"), windows)
         return out
     finally:
         _killpg(dev)
@@ -883,6 +919,14 @@ def report(args, nproc, tls, ms_total, qs, extras):
             "p50_ms": round(wp50, 2), "p90_ms": round(_pct(wan["reload_ms"], 0.9), 2),
             "sync_p50_ms": round(_pct(wan["sync_ms"], 0.5), 2), "n": len(wan["reload_ms"]),
             "dev_start_s": round(wan["dev_start_s"], 3), "link_connections": wan.get("link", {}).get("connections"),
+            "connections_per_edit": round(sum(wan["link"]["per_edit"]) / max(1, len(wan["link"]["per_edit"])), 2)
+            if wan.get("link", {}).get("per_edit") else None,
+            # where a sample's time goes: the edit reaching the pod, then the app's restart plus the
+            # request through the port-forward (its streams below)
+            "breakdown_p50_ms": {"sync": round(_pct(wan["sync_ms"], 0.5), 2),
+                                 "restart_and_request": round(_pct([r - s for r, s in zip(wan["reload_ms"],
+                                                                                          wan["sync_ms"])], 0.5), 2)},
+            "portforward": wan.get("portforward"),
         }
         dw, dwr = extras.get("deploy_wan"), extras.get("deploy_wan_ref")
         if _ok(dw):
@@ -898,6 +942,8 @@ def report(args, nproc, tls, ms_total, qs, extras):
                 "p50_ms": round(wr50, 2), "sync_p50_ms": round(_pct(wan_ref["sync_ms"], 0.5), 2),
                 "n": len(wan_ref["reload_ms"]), "dev_start_s": round(wan_ref["dev_start_s"], 3),
                 "link_connections": wan_ref.get("link", {}).get("connections"),
+                "connections_per_edit": round(sum(wan_ref["link"]["per_edit"]) / max(1, len(wan_ref["link"]["per_edit"])), 2)
+                if wan_ref.get("link", {}).get("per_edit") else None,
                 "speedup": round(wr50 / wp50, 2) if wp50 else None,
             }
     pool = extras.get("qs_pool")

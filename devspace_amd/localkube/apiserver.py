@@ -21,6 +21,7 @@ import time
 import yaml
 from aiohttp import WSMsgType, web
 
+from . import spdy
 from .kubelet import close_proc
 from .store import CLUSTER_SCOPED, ApiError, labels_match, parse_selector
 
@@ -53,6 +54,7 @@ class ApiServer:
         # verified client certificate on the TLS listener) — expired tokens get 401
         self.token_validator = token_validator
         self.auth_failures = 0
+        self.portforward_tunnels = 0  # multiplexed port-forward tunnels served (SPDY over WebSocket)
         # Fault switch (API Priority and Fairness under load): the first `throttle_first` requests
         # of every (verb, resource) are answered `429 Too Many Requests` + `Retry-After`. The
         # counts start over with reset_throttle(), so every CLI command can be throttled afresh.
@@ -636,22 +638,33 @@ class ApiServer:
 
     # ------------------------------------------------------------------ port-forward
 
+    @staticmethod
+    def _refused_text(name, port, e):
+        # the kubelet's wording (CRI streaming server): clients key on "connection refused"
+        why = "connect: connection refused" if isinstance(e, ConnectionRefusedError) or "111" in str(e) else str(e)
+        return (f"error forwarding port {port} to pod {name}, uid : failed to connect to localhost:{port} inside "
+                f"namespace: dial tcp4 127.0.0.1:{port}: {why}")
+
     async def portforward_ws(self, request, ns, name):
         self.store.get("", "pods", ns, name)
-        port = int(request.query.get("ports", "0").split(",")[0])
-        ws = web.WebSocketResponse(protocols=("v4.channel.k8s.io", "portforward.k8s.io"), max_msg_size=0)
+        ws = web.WebSocketResponse(protocols=(spdy.PROTOCOL, "v4.channel.k8s.io", "portforward.k8s.io"),
+                                   max_msg_size=0)
         await ws.prepare(request)
+        if ws.ws_protocol == spdy.PROTOCOL:
+            # Kubernetes >= 1.30: one tunnel, a stream pair per forwarded connection
+            self.portforward_tunnels += 1
+            tunnel = spdy.Tunnel(ws, lambda port: asyncio.open_connection("127.0.0.1", port),
+                                 lambda port, e: self._refused_text(name, port, e))
+            await tunnel.run()
+            return ws
+        port = int(request.query.get("ports", "0").split(",")[0])
         hdr = struct.pack("<H", port)
         await ws.send_bytes(b"\x00" + hdr)
         await ws.send_bytes(b"\x01" + hdr)
         try:
             reader, writer = await asyncio.open_connection("127.0.0.1", port)
         except OSError as e:
-            # the kubelet's wording (CRI streaming server): clients key on "connection refused"
-            why = "connect: connection refused" if isinstance(e, ConnectionRefusedError) or "111" in str(e) else str(e)
-            await ws.send_bytes(b"\x01" + (f"error forwarding port {port} to pod {name}, uid : failed to connect to "
-                                            f"localhost:{port} inside namespace: dial tcp4 127.0.0.1:{port}: "
-                                            f"{why}").encode())
+            await ws.send_bytes(b"\x01" + self._refused_text(name, port, e).encode())
             await ws.close()
             return ws
 

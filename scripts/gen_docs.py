@@ -162,6 +162,9 @@ ENV = {
     "DEVSPACE_PULL_TIMEOUT": "Seconds a rollout wait may last in all while a pod of the release is still pulling "
                              "its image (default 1800); past the chart's timeout the wait goes on only for "
                              "pulls, and a first install whose pull outlasts this is kept, not purged.",
+    "DEVSPACE_PORTFORWARD_TUNNEL": "`0`: no multiplexed port-forward tunnel (`SPDY/3.1+portforward.k8s.io`); every "
+                                   "forwarded connection gets a WebSocket of its own, as against an API server "
+                                   "older than Kubernetes 1.30.",
     "DEVSPACE_PULL_ERROR_GRACE_S": "Seconds an `ErrImagePull`/`ImagePullBackOff` the kubelet may yet get past "
                                    "(a registry timeout, a 5xx) may last before the rollout wait fails (default 30); "
                                    "a missing image, an invalid name or a denied pull fail at once.",

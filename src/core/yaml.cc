@@ -258,7 +258,16 @@ class Parser {
       std::string acc = t;
       while (!quote_closed(acc) && pos_ < lines_.size()) {
         std::string nxt = trim(lines_[pos_].content);
-        acc += nxt.empty() ? "\n" : (ends_with(acc, "\n") ? nxt : " " + nxt);
+        size_t bs = 0;
+        while (bs < acc.size() && acc[acc.size() - 1 - bs] == '\\') ++bs;
+        if (c0 == '"' && bs % 2 == 1) {
+          // an escaped line break (PyYAML writes long strings this way): the break and the next
+          // line's leading white space vanish, nothing takes their place
+          acc.pop_back();
+          acc += nxt;
+        } else {
+          acc += nxt.empty() ? "\n" : (ends_with(acc, "\n") ? nxt : " " + nxt);
+        }
         ++pos_;
       }
       return parse_inline(acc, parent_indent);

@@ -800,6 +800,26 @@ std::unique_ptr<net::WebSocket> Client::portforward(const std::string& ns, const
   return ws_connect(path, {"v4.channel.k8s.io", "portforward.k8s.io"}, std::move(spare));
 }
 
+const char* const kPortForwardTunnel = "SPDY/3.1+portforward.k8s.io";
+
+std::shared_ptr<SpdySession> Client::portforward_tunnel(const std::string& ns, const std::string& pod,
+                                                        const std::vector<int>& ports) {
+  std::string path = "/api/v1/namespaces/" + ns + "/pods/" + pod + "/portforward";
+  for (size_t i = 0; i < ports.size(); ++i) path += (i ? "&ports=" : "?ports=") + std::to_string(ports[i]);
+  std::unique_ptr<net::WebSocket> ws;
+  try {
+    ws = ws_connect(path, {kPortForwardTunnel});
+  } catch (const net::UpgradeError& e) {
+    if (e.status == 401 || e.status == 403 || e.status == 404) throw;  // the fallback would fail alike
+    return nullptr;  // 400 & co: an API server without the tunnel
+  }
+  if (ws->protocol() != kPortForwardTunnel) {
+    ws->close();
+    return nullptr;
+  }
+  return std::make_shared<SpdySession>(std::move(ws));
+}
+
 std::unique_ptr<net::WebSocket> Client::ws_connect(const std::string& path, const std::vector<std::string>& protocols,
                                                    std::unique_ptr<net::Conn> spare) {
   bool refreshed = false;

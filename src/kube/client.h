@@ -18,6 +18,8 @@
 #include <thread>
 #include <vector>
 
+#include "kube/spdy.h"
+
 #include "core/net.h"
 #include "core/proc.h"
 #include "core/value.h"
@@ -144,6 +146,11 @@ class Client {
   std::unique_ptr<ExecSession> attach(const std::string& ns, const std::string& pod, const std::string& container,
                                       bool tty, bool stdin = false);
   // `spare`: a pre-dialed connection to the API server to upgrade (saves the TLS handshake).
+  // One multiplexed port-forward tunnel to `pod` (WebSocket subprotocol
+  // "SPDY/3.1+portforward.k8s.io", Kubernetes >= 1.30): every forwarded connection becomes a
+  // stream pair in it. nullptr when the API server does not speak it (then: portforward()).
+  std::shared_ptr<SpdySession> portforward_tunnel(const std::string& ns, const std::string& pod,
+                                                  const std::vector<int>& ports);
   std::unique_ptr<net::WebSocket> portforward(const std::string& ns, const std::string& pod, int port,
                                               std::unique_ptr<net::Conn> spare = nullptr);
 

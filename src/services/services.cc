@@ -230,10 +230,163 @@ static int listen_on(int family, const std::string& addr, int port) {
   return fd;
 }
 
+// One forwarded connection's stream(s), as the connection handler sees them.
+class FwdStream {
+ public:
+  virtual ~FwdStream() = default;
+  // client -> pod bytes
+  virtual bool send(const std::string& data) = 0;
+  // The next event: channel 0 bytes from the pod, channel 1 an error message. false at the end.
+  virtual bool recv(int* channel, std::string* data) = 0;
+  // the client finished sending (a tunnel stream half-closes; a WebSocket cannot)
+  virtual void close_write() {}
+  virtual void close() = 0;
+  virtual const char* via() const = 0;
+};
+
+namespace {
+
+// portforward.k8s.io over a WebSocket of its own: channel byte 0 data / 1 error, and each
+// channel's first frame carries the port number (2 bytes LE).
+class WsFwd : public FwdStream {
+ public:
+  explicit WsFwd(std::unique_ptr<net::WebSocket> ws) : ws_(std::move(ws)) {}
+  bool send(const std::string& data) override { return ws_->send(std::string(1, '\0') + data); }
+  bool recv(int* channel, std::string* data) override {
+    std::string msg;
+    while (ws_->recv(&msg)) {
+      if (msg.empty()) continue;
+      int ch = (unsigned char)msg[0];
+      std::string d = msg.substr(1);
+      if (ch == 0 && first_data_) {
+        first_data_ = false;
+        if (d.size() == 2) continue;
+      }
+      if (ch == 1 && first_err_) {
+        first_err_ = false;
+        if (d.size() == 2) continue;
+      }
+      *channel = ch;
+      *data = std::move(d);
+      return true;
+    }
+    return false;
+  }
+  void close() override { ws_->close(); }
+  const char* via() const override { return "websocket"; }
+
+ private:
+  std::unique_ptr<net::WebSocket> ws_;
+  bool first_data_ = true, first_err_ = true;
+};
+
+// A stream pair in the pod's tunnel, as kubectl creates it: an error stream (the client never
+// writes to it) and a data stream, tied by a request id. The data follows the SYN_STREAM at once.
+class TunnelFwd : public FwdStream {
+ public:
+  TunnelFwd(std::shared_ptr<kube::SpdySession> s, int port, uint64_t request_id) : s_(std::move(s)) {
+    std::string p = std::to_string(port), id = std::to_string(request_id);
+    err_ = s_->open({{"streamtype", "error"}, {"port", p}, {"requestid", id}}, box_, 1, true);
+    data_ = s_->open({{"streamtype", "data"}, {"port", p}, {"requestid", id}}, box_, 0);
+  }
+  ~TunnelFwd() override { close(); }
+  bool send(const std::string& data) override { return s_->send(data_, data); }
+  bool recv(int* channel, std::string* data) override {
+    kube::SpdyMailbox::Event e;
+    while (!data_done_ && box_->pop(&e)) {
+      if (e.end) {
+        if (e.channel == 0) data_done_ = true;
+        continue;
+      }
+      if (e.channel == 0) s_->consumed(data_, e.data.size());
+      *channel = e.channel;
+      *data = std::move(e.data);
+      return true;
+    }
+    return false;
+  }
+  void close_write() override { s_->send(data_, "", true); }
+  void close() override {
+    if (closed_) return;
+    closed_ = true;
+    if (!data_done_) {  // abandoned (stop, a failed client write): the server stops forwarding
+      s_->reset(data_);
+      s_->reset(err_);
+    }
+  }
+  const char* via() const override { return "tunnel"; }
+
+ private:
+  std::shared_ptr<kube::SpdySession> s_;
+  std::shared_ptr<kube::SpdyMailbox> box_ = std::make_shared<kube::SpdyMailbox>();
+  std::shared_ptr<kube::SpdySession::Stream> err_, data_;
+  bool data_done_ = false, closed_ = false;
+};
+
+bool port_forward_tunnel_enabled() {
+  const char* v = std::getenv("DEVSPACE_PORTFORWARD_TUNNEL");
+  return !(v && std::string(v) == "0") && !reference_timing();  // the reference dials per stream
+}
+
+}  // namespace
+
+std::shared_ptr<kube::SpdySession> PortForwarder::tunnel_for(const std::string& pod) {
+  if (tunnel_mode_ == 0) return nullptr;
+  std::lock_guard<std::mutex> g(tunnel_mu_);
+  if (tunnel_ && tunnel_pod_ == pod && tunnel_->usable()) return tunnel_;
+  if (tunnel_) {
+    tunnel_->close();
+    tunnel_.reset();
+  }
+  std::vector<int> remote;
+  for (auto& pr : ports_) remote.push_back(pr.second);
+  auto t = k_->portforward_tunnel(ns_, pod, remote);  // throws when the pod is gone
+  if (!t) {
+    tunnel_mode_ = 0;
+    log::file_logger("portforwarding")->emit("info", "The API server has no multiplexed port-forward "
+                                             "(SPDY/3.1+portforward.k8s.io): one WebSocket per connection", {});
+    return nullptr;
+  }
+  tunnel_mode_ = 1;
+  tunnels_opened_++;
+  tunnel_ = t;
+  tunnel_pod_ = pod;
+  tunnel_requests_ = 0;
+  return t;
+}
+
+std::unique_ptr<FwdStream> PortForwarder::open_to(const std::string& pod, int remote_port) {
+  for (int tries = 0; tries < 2 && tunnel_mode_ != 0; ++tries) {
+    auto t = tunnel_for(pod);
+    if (!t) break;
+    try {
+      return std::make_unique<TunnelFwd>(t, remote_port, tunnel_requests_++);
+    } catch (const net::NetError&) {
+      // the tunnel just closed (API server restart, idle timeout): a new one
+    }
+  }
+  return std::make_unique<WsFwd>(k_->portforward(ns_, pod, remote_port, take_spare()));
+}
+
 void PortForwarder::spare_loop() {
   const long kMaxAgeMs = 30000;  // below API-server idle timeouts; re-dialed after that
   std::unique_lock<std::mutex> lk(spare_mu_);
   while (!stop_) {
+    if (tunnel_mode_ != 0 && port_forward_tunnel_enabled()) {
+      // keep the pod's tunnel open (re-opened after the API server closed it), so the first
+      // connection after a quiet spell does not pay the upgrade either
+      lk.unlock();
+      try {
+        tunnel_for(pod_name());
+      } catch (const std::exception&) {
+      }
+      lk.lock();
+      if (tunnel_mode_ == 1) {
+        spares_.clear();
+        spare_cv_.wait_for(lk, std::chrono::seconds(1), [this] { return stop_.load(); });
+        continue;
+      }
+    }
     while (!spares_.empty() && mono_ms() - spares_.front().first > kMaxAgeMs) spares_.pop_front();
     if ((int)spares_.size() < want_spares_) {
       lk.unlock();
@@ -277,7 +430,8 @@ void PortForwarder::start() {
   } else {
     want_spares_ = reference_timing() ? 0 : 2;  // the reference dials every stream
   }
-  if (want_spares_ > 0) spare_thread_ = std::thread([this] { spare_loop(); });
+  if (!port_forward_tunnel_enabled()) tunnel_mode_ = 0;
+  if (want_spares_ > 0 || tunnel_mode_ != 0) spare_thread_ = std::thread([this] { spare_loop(); });
   for (size_t i = 0; i < ports_.size(); ++i) {
     std::string bind = i < addrs_.size() ? addrs_[i] : "";
     auto addrs = listen_addresses(bind);
@@ -347,7 +501,7 @@ void PortForwarder::accept_loop(int lfd, int remote_port) {
   }
 }
 
-std::unique_ptr<net::WebSocket> PortForwarder::open_stream(int remote_port) {
+std::unique_ptr<FwdStream> PortForwarder::open_stream(int remote_port) {
   Value pod;
   {
     std::lock_guard<std::mutex> g(pod_mu_);
@@ -355,7 +509,7 @@ std::unique_ptr<net::WebSocket> PortForwarder::open_stream(int remote_port) {
   }
   std::string name = pod.at_path("metadata.name").as_string();
   try {
-    return k_->portforward(ns_, name, remote_port, take_spare());
+    return open_to(name, remote_port);
   } catch (const std::exception& e) {
     if (selector_.empty() || stop_) throw;
     // the pod is gone or not running any more: follow the selector to its newest pod
@@ -370,17 +524,12 @@ std::unique_ptr<net::WebSocket> PortForwarder::open_stream(int remote_port) {
     log::file_logger("portforwarding")->emit("info", "Pod " + name + " is gone (" + e.what() +
                                              "), forwarding to " + fresh_name, {});
     log::info("Port forwarding " + describe() + " now targets pod " + fresh_name);
-    return k_->portforward(ns_, fresh_name, remote_port);
+    return open_to(fresh_name, remote_port);
   }
 }
 
-std::unique_ptr<net::WebSocket> PortForwarder::open_stream_direct(int remote_port) {
-  Value pod;
-  {
-    std::lock_guard<std::mutex> g(pod_mu_);
-    pod = pod_;
-  }
-  return k_->portforward(ns_, pod.at_path("metadata.name").as_string(), remote_port, take_spare());
+std::unique_ptr<FwdStream> PortForwarder::open_stream_direct(int remote_port) {
+  return open_to(pod_name(), remote_port);
 }
 
 namespace {
@@ -404,7 +553,7 @@ class PreOpened {
   // the open finished: take() / discard() will not block
   bool ready() const { return done_; }
   ~PreOpened() { discard(); }
-  std::unique_ptr<net::WebSocket> take() {
+  std::unique_ptr<FwdStream> take() {
     if (t_.joinable()) t_.join();
     return std::move(ws_);
   }
@@ -414,7 +563,7 @@ class PreOpened {
   }
 
  private:
-  std::unique_ptr<net::WebSocket> ws_;
+  std::unique_ptr<FwdStream> ws_;
   std::atomic<bool> done_{false};
   std::thread t_;  // declared last: the thread starts once ws_ and done_ exist
 };
@@ -453,9 +602,10 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
   int attempt = 0;
   std::unique_ptr<PreOpened> next;
   while (!stop_) {
-    std::unique_ptr<net::WebSocket> ws;
-    // span per stream: open (WebSocket upgrade; the pod-side dial happens with it) and the
-    // time until the first reply byte or the refusal (trace.jsonl "portforward.stream")
+    std::unique_ptr<FwdStream> ws;
+    // span per stream: open (the WebSocket upgrade, or a stream pair in the tunnel; the pod-side
+    // dial happens with it) and the time until the first reply byte or the refusal
+    // (trace.jsonl "portforward.stream")
     const int64_t t_open = trace::now_us();
     bool preopened = false;
     if (next) {
@@ -473,31 +623,23 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
     }
     if (preopened) preopened_++;
     const int64_t t_opened = trace::now_us();
+    const bool tunneled = std::string(ws->via()) == "tunnel";
     // a held connection (its first stream was refused) within its first 100 ms: open the
-    // following attempt's stream now, while this one waits for its reply or refusal
-    if (preopen_ && attempt > 0 && replayable && !stop_ && mono_ms() - hold_start < 100)
+    // following attempt's stream now, while this one waits for its reply or refusal. (Not through
+    // the tunnel: a stream there opens without a round trip, and its pod-side dial is what an
+    // attempt is for.)
+    if (preopen_ && !tunneled && attempt > 0 && replayable && !stop_ && mono_ms() - hold_start < 100)
       next = std::make_unique<PreOpened>([this, remote_port] { return open_stream_direct(remote_port); });
     std::atomic<int64_t> t_first{0};
-    if (!replay.empty() && !ws->send(std::string(1, '\0') + replay)) break;
+    if (!replay.empty() && !ws->send(replay)) break;
+    if (client_eof) ws->close_write();
     int wake[2];
     if (::pipe2(wake, O_CLOEXEC | O_NONBLOCK) != 0) break;
     std::atomic<bool> down_done{false}, got_reply{false}, refused{false};
     std::thread down([&] {
-      std::string msg;
-      bool first_data = true, first_err = true;
-      while (ws->recv(&msg)) {
-        if (msg.empty()) continue;
-        unsigned char ch = (unsigned char)msg[0];
-        std::string data = msg.substr(1);
-        // each channel's first frame carries the port number (2 bytes LE)
-        if (ch == 0 && first_data) {
-          first_data = false;
-          if (data.size() == 2) continue;
-        }
-        if (ch == 1 && first_err) {
-          first_err = false;
-          if (data.size() == 2) continue;
-        }
+      int ch = 0;
+      std::string data;
+      while (ws->recv(&ch, &data)) {
         if (ch == 0) {
           if (!got_reply) t_first = trace::now_us();
           got_reply = true;
@@ -516,7 +658,6 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
       (void)w;
     });
     char buf[65536];
-    buf[0] = 0;
     while (!down_done && !stop_ && !client_eof) {
       // answered: the spare attempt is not needed (dropped once its open is done, so the
       // forwarding never waits on it; else at the end of the connection)
@@ -524,16 +665,17 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
       struct pollfd pf[2] = {{cfd, POLLIN, 0}, {wake[0], POLLIN, 0}};
       int r = ::poll(pf, 2, 200);
       if (r <= 0 || !(pf[0].revents & (POLLIN | POLLHUP | POLLERR))) continue;
-      ssize_t n = ::recv(cfd, buf + 1, sizeof(buf) - 1, 0);
+      ssize_t n = ::recv(cfd, buf, sizeof(buf), 0);
       if (n <= 0) {
         client_eof = true;  // half-close: the request is complete, keep reading the reply
+        ws->close_write();
         break;
       }
       if (replayable && !got_reply) {
-        replay.append(buf + 1, (size_t)n);
+        replay.append(buf, (size_t)n);
         if (replay.size() > (4u << 20)) replayable = false;  // a large upload: do not buffer it
       }
-      if (!ws->send(std::string(buf, (size_t)n + 1))) break;
+      if (!ws->send(std::string(buf, (size_t)n))) break;
     }
     if (client_eof && !down_done) {
       // the client finished sending: wait for the reply (or the refusal) before closing
@@ -555,14 +697,16 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
                    {"open_us", std::to_string(t_opened - t_open)},
                    {"first_us", tf ? std::to_string(tf - t_open) : std::string("-1")},
                    {"outcome", refused ? "refused" : got_reply ? "reply" : "closed"},
-                   {"preopened", preopened ? "1" : "0"}});
+                   {"preopened", preopened ? "1" : "0"},
+                   {"via", ws->via()}});
     }
     ++attempt;
     if (refused && replayable && !stop_ && mono_ms() < hold_deadline) {
       // a hot-reloading app is back within tens of ms: retry at once for the first 100 ms
-      // (the pre-opened stream paces those attempts: one per stream open), then back off
+      // (a refusal takes a round trip, which paces the attempts; so does a pre-opened stream),
+      // then back off
       long held = mono_ms() - hold_start;
-      int delay = next ? 0 : held < 100 ? 1 : held < 1000 ? 5 : 25;
+      int delay = next || tunneled ? (held < 100 ? 0 : held < 1000 ? 5 : 25) : held < 100 ? 1 : held < 1000 ? 5 : 25;
       if (delay) std::this_thread::sleep_for(std::chrono::milliseconds(delay));
       held_retries_++;
       continue;

@@ -54,9 +54,13 @@ int port_forward_hold_ms();
 bool port_forward_preopen();
 bool is_dial_refused(const std::string& error_channel_message);
 
-// Local listeners forwarding to a pod port over the portforward.k8s.io WebSocket protocol
-// (services/port_forwarding.go:18, kubectl/client.go:356). Every accepted connection gets its
-// own stream and thread; the forwarder owns those threads and joins them in close(). When the
+class FwdStream;  // one forwarded connection's stream(s) (services.cc)
+
+// Local listeners forwarding to a pod port (services/port_forwarding.go:18, kubectl/client.go:356):
+// through one multiplexed tunnel per pod (SPDY/3.1 over a WebSocket, kube/spdy.h) where the API
+// server speaks it, else over a portforward.k8s.io WebSocket per connection. Every accepted
+// connection gets its own stream and thread; the forwarder owns those threads and joins them in
+// close(). When the
 // pod goes away (restart, rollout) new connections re-select the newest running pod of the
 // selector instead of failing forever (the reference keeps forwarding to the dead pod).
 class PortForwarder {
@@ -92,9 +96,14 @@ class PortForwarder {
   std::unique_ptr<net::Conn> take_spare();
   void handle(Conn* c, int remote_port);
   void reap(bool all);
-  std::unique_ptr<net::WebSocket> open_stream(int remote_port);
+  std::unique_ptr<FwdStream> open_stream(int remote_port);
   // The current pod's stream without pod re-selection (the hold's pre-opened next attempt).
-  std::unique_ptr<net::WebSocket> open_stream_direct(int remote_port);
+  std::unique_ptr<FwdStream> open_stream_direct(int remote_port);
+  // A stream to `pod`: a stream pair in the pod's multiplexed tunnel, or (an API server without
+  // the tunnel, DEVSPACE_PORTFORWARD_TUNNEL=0) a WebSocket of its own.
+  std::unique_ptr<FwdStream> open_to(const std::string& pod, int remote_port);
+  // The pod's tunnel, opened (or re-opened after it closed) on demand; nullptr when unsupported.
+  std::shared_ptr<kube::SpdySession> tunnel_for(const std::string& pod);
   std::shared_ptr<kube::Client> k_;
   std::mutex pod_mu_;
   Value pod_;
@@ -117,6 +126,18 @@ class PortForwarder {
   std::atomic<int> preopened_{0};
   int hold_ms_ = port_forward_hold_ms();
   bool preopen_ = port_forward_preopen();
+  // the multiplexed tunnel (SPDY/3.1 over one WebSocket): -1 not tried, 0 unsupported, 1 in use
+  std::atomic<int> tunnel_mode_{-1};
+  std::mutex tunnel_mu_;
+  std::shared_ptr<kube::SpdySession> tunnel_;
+  std::string tunnel_pod_;
+  std::atomic<uint64_t> tunnel_requests_{0};  // request ids of the current tunnel
+  std::atomic<int> tunnels_opened_{0};
+
+ public:
+  // Tunnels opened (1 for a forward whose API server speaks it and whose pod never changed).
+  int tunnels_opened() const { return tunnels_opened_; }
+  bool tunneled() const { return tunnel_mode_ == 1; }
 };
 
 std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& cfg, std::shared_ptr<kube::Client> k,

@@ -1,5 +1,7 @@
 // Kubernetes adapter units: pod status (kubectl printer port, kubectl/client.go:224), resource
 // paths, kubeconfig resolution (inline data, tokens, namespaces), analyze's GPU log matcher.
+#include <zlib.h>
+
 #include "analyze/analyze.h"
 #include "core/codec.h"
 #include "core/fs.h"
@@ -217,4 +219,47 @@ TEST(no_proxy_matching) {
 TEST(websocket_accept_rfc6455_example) {
   // RFC 6455 §1.3 worked example
   EXPECT_EQ(net::websocket_accept("dGhlIHNhbXBsZSBub25jZQ=="), std::string("s3pPLMBiTxaQ9kYGzzhZRbK+xOo="));
+}
+
+// ---------------------------------------------------------------- SPDY/3.1 (the multiplexed port-forward tunnel)
+
+TEST(spdy_dictionary_is_the_protocols) {
+  const std::string& d = kube::spdy_dictionary();
+  EXPECT_EQ(d.size(), (size_t)1423);
+  // the zlib dictionary id a SPDY/3 peer checks (adler-32 of the dictionary)
+  EXPECT_EQ((uint32_t)adler32(1L, (const Bytef*)d.data(), (uInt)d.size()), (uint32_t)0xe3c6a7c2u);
+}
+
+TEST(spdy_header_blocks_share_one_zlib_stream_per_direction) {
+  kube::SpdyHeaderCodec a, b;
+  kube::SpdyHeaders h1 = {{"streamtype", "error"}, {"port", "8080"}, {"requestid", "0"}};
+  kube::SpdyHeaders h2 = {{"streamtype", "data"}, {"port", "8080"}, {"requestid", "0"}};
+  std::string c1 = a.compress(h1), c2 = a.compress(h2);
+  EXPECT_TRUE(c2.size() < c1.size());  // the second block refers back into the first
+  kube::SpdyHeaders out;
+  EXPECT_TRUE(b.decompress(c1, &out) && out == h1);
+  EXPECT_TRUE(b.decompress(c2, &out) && out == h2);
+  kube::SpdyHeaders empty;
+  EXPECT_TRUE(b.decompress(a.compress(empty), &out) && out.empty());
+}
+
+TEST(spdy_frames_round_trip_and_split_anywhere) {
+  std::string wire = kube::spdy::control_frame(kube::spdy::SynStream, 0, "0123456789") +
+                     kube::spdy::data_frame(3, kube::spdy::kFlagFin, std::string(70000, 'x')) +
+                     kube::spdy::control_frame(kube::spdy::Ping, 0, kube::spdy::u32(7));
+  EXPECT_EQ((unsigned char)wire[0], 0x80);
+  EXPECT_EQ((unsigned char)wire[1], 3);
+  // the tunnel's WebSocket messages may cut frames anywhere: feed it in odd pieces
+  std::string buf;
+  std::vector<kube::spdy::Frame> got;
+  for (size_t off = 0; off < wire.size(); off += 997) {
+    buf += wire.substr(off, 997);
+    kube::spdy::Frame f;
+    while (kube::spdy::parse(&buf, &f)) got.push_back(f);
+  }
+  EXPECT_EQ(got.size(), (size_t)3);
+  EXPECT_TRUE(got[0].control && got[0].type == kube::spdy::SynStream && got[0].body == "0123456789");
+  EXPECT_TRUE(!got[1].control && got[1].stream_id == 3 && got[1].flags == kube::spdy::kFlagFin &&
+              got[1].body.size() == 70000);
+  EXPECT_TRUE(got[2].control && got[2].type == kube::spdy::Ping && kube::spdy::get_u32(got[2].body, 0) == 7);
 }

@@ -82,3 +82,17 @@ def test_native_yaml_agrees_with_pyyaml_on_mutations():
         assert [_norm(d) for d in ours] == [_norm(d) for d in py], text[:800]
         agree += 1
     assert agree > 1000
+
+
+def test_strings_pyyaml_writes_read_back_exactly():
+    """What the tests and tools write with yaml.safe_dump and `devspace` then reads: long strings
+    with newlines, quotes and runs of spaces come out as double-quoted scalars folded over several
+    lines with escaped line breaks (`\\` at the end, `\\ ` for a leading space). An entrypoint
+    override carrying a Python program used to gain a space at every fold (an IndentationError in
+    the pod)."""
+    rng = random.Random(7)
+    pieces = ["import os", "\n", "    ", "  ", " ", "x = 1", '"q"', "'s'", "\\", "\t", "#", ": ", "- ", "é", "long" * 7]
+    for _ in range(300):
+        s = "".join(rng.choice(pieces) for _ in range(rng.randint(1, 60)))
+        doc = yaml.safe_dump({"cmd": ["python3", "-c", s], "s": s}, width=rng.choice([40, 80, 120]))
+        assert _native.yaml_parse(doc) == {"cmd": ["python3", "-c", s], "s": s}, doc
