@@ -1,8 +1,10 @@
 """Deploy wall-clock of the quickstart example through the real CLI (BASELINE metric part 2).
 
 `devspace deploy` of examples/quickstart against a fresh local cluster: image build via the
-Docker Engine API, push, native Helm install, and helm-style rollout wait until the pod runs.
-A second, forced redeploy (`-d`) measures the warm path (no rebuild, chart re-install).
+Docker Engine API (its RUN steps executed on the host runtime: `npm install`), push, native Helm
+install, and helm-style rollout wait until the pod runs. Then an edit of index.js and a deploy
+(the image rebuilds: the `npm install` layer comes from the build cache, the project copy is
+new), and a forced redeploy (`-d`) of the unchanged project (no rebuild, chart re-install).
 """
 
 from __future__ import annotations
@@ -82,7 +84,7 @@ def bench_deploy(workdir, example="quickstart", tls=False, reference=False, wan=
     proj = os.path.join(base, example)
     shutil.copytree(os.path.join(ROOT, "examples", example), proj, symlinks=True)
     prewarmed = _prewarm_runtime()
-    cluster = LocalCluster(os.path.join(base, "cluster"), gpus=0, tls=tls).start()
+    cluster = LocalCluster(os.path.join(base, "cluster"), gpus=0, tls=tls, run_steps=True).start()
     link = None
     try:
         env = devspace_env(cluster, base)
@@ -98,10 +100,19 @@ def bench_deploy(workdir, example="quickstart", tls=False, reference=False, wan=
         if "Successfully deployed!" not in out:
             raise RuntimeError(out)
         phases, net = _phases(trace)
+        # an edit of the app, deployed: rebuilt from the layer cache (npm install reused)
+        app = os.path.join(proj, "index.js")
+        if os.path.exists(app):
+            with open(app, "a") as f:
+                f.write("\n// edited\n")
+        os.unlink(trace)
+        edit, out = run_devspace(["deploy"], proj, env)
+        edit_phases, _ = _phases(trace)
         warm, _ = run_devspace(["deploy", "-d"], proj, env)
         run_devspace(["purge"], proj, env)
-        return {"cold_s": cold, "warm_s": warm, "cold_phases_ms": phases, "net": net,
-                "host_runtime_prewarmed": prewarmed}
+        return {"cold_s": cold, "warm_s": warm, "edit_s": edit, "cold_phases_ms": phases,
+                "edit_phases_ms": edit_phases, "net": net, "host_runtime_prewarmed": prewarmed,
+                "run_steps": True, "edit_reused_run_layer": "Using cache" in out or None}
     finally:
         if link is not None:
             link.stop()

@@ -86,7 +86,7 @@ def _b64file(path):
 class LocalCluster:
     def __init__(self, state_dir, port=0, gpus=None, context="devspace-local", extra_env=None, tls=False,
                  token_validator=None, gpu_partition="spx", memory_partition="nps1", gpu_strategy="single",
-                 unhealthy_gpus=0):
+                 unhealthy_gpus=0, run_steps=False):
         self.state_dir = os.path.abspath(state_dir)
         self.tls = tls
         self.pki = make_pki(os.path.join(self.state_dir, "pki")) if tls else None
@@ -96,6 +96,7 @@ class LocalCluster:
         self.context = context
         self.store = Store()
         self.images = ImageStore(os.path.join(self.state_dir, "docker"))
+        self.images.run_steps = run_steps  # the image builder executes RUN (host runtime)
         env = {"PYTHONPATH": ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")}
         env.update(extra_env or {})
         self.kubelet = Kubelet(self.store, self.images, self.state_dir, gpus=self.gpus, extra_env=env)

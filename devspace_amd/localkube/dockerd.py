@@ -4,7 +4,10 @@ Serves what the devspace builder needs (reference: builder/docker/docker.go): /_
 /version, /info, /auth, /build (tar context + Dockerfile), /images/{name}/push,
 /images/{name}/tag, /images/{name}/json. Images are directories (rootfs + config.json); a
 Dockerfile is interpreted instruction by instruction (FROM/WORKDIR/COPY/ADD/ENV/ARG/EXPOSE/
-CMD/ENTRYPOINT/LABEL/USER; RUN is recorded but not executed — no network on the box).
+CMD/ENTRYPOINT/LABEL/USER). RUN is recorded, and executed only when the store's `run_steps` is
+on: then its command runs on the host runtime (the pods' runtime here) in the image's working
+directory, and the resulting filesystem is kept as that layer's snapshot, restored instead of
+running the step again when a later build hits the same cache key.
 
 Layer cache keys as the classic builder computes them: each instruction's key chains the
 previous one with the instruction text (after ARG/ENV substitution), and a COPY/ADD also with
@@ -45,10 +48,26 @@ def normalize(ref: str):
 
 
 class ImageStore:
+    MAX_SNAPSHOTS = 16  # RUN layers whose filesystem is kept (oldest dropped first)
+
     def __init__(self, root):
         self.root = root
+        self.run_steps = False  # execute RUN (on the host runtime) instead of only recording it
         os.makedirs(os.path.join(root, "images"), exist_ok=True)
         os.makedirs(os.path.join(root, "registry"), exist_ok=True)
+
+    def snapshot_dir(self, key):
+        return os.path.join(self.root, "layers", key)
+
+    def keep_snapshot(self, key, rootfs):
+        d = self.snapshot_dir(key)
+        if os.path.exists(d):
+            shutil.rmtree(d)
+        shutil.copytree(rootfs, d, symlinks=True)
+        base = os.path.join(self.root, "layers")
+        snaps = sorted((os.path.getmtime(os.path.join(base, n)), n) for n in os.listdir(base))
+        for _, n in snaps[:max(0, len(snaps) - self.MAX_SNAPSHOTS)]:
+            shutil.rmtree(os.path.join(base, n), ignore_errors=True)
 
     def _dir(self, kind, ref):
         name, tag = normalize(ref)
@@ -175,6 +194,27 @@ def _content_hash(paths, base):
     return h.hexdigest()
 
 
+def _run_step(argv, rootfs, config, work, log, timeout=900):
+    """A RUN on the host runtime: in the image's working directory, with its ENV over the host's
+    (the pods run on the host's tools too) and a HOME of the build's own."""
+    import subprocess
+
+    cwd = os.path.join(rootfs, config["WorkingDir"].lstrip("/"))
+    os.makedirs(cwd, exist_ok=True)
+    env = dict(os.environ)
+    for kv in config["Env"]:
+        k, _, v = kv.partition("=")
+        env[k] = v
+    env["HOME"] = os.path.join(work, "home")
+    os.makedirs(env["HOME"], exist_ok=True)
+    log(" ---> Running in the local runtime")
+    p = subprocess.run(argv, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    for line in (p.stdout + p.stderr).splitlines():
+        log(line)
+    if p.returncode != 0:
+        raise RuntimeError(f"The command '{' '.join(argv)}' returned a non-zero code: {p.returncode}")
+
+
 def build_image(store, context_dir, dockerfile, tag, buildargs=None, target=None, log=print):
     with open(os.path.join(context_dir, dockerfile)) as f:
         instrs = _parse_dockerfile(f.read())
@@ -293,12 +333,23 @@ def build_image(store, context_dir, dockerfile, tag, buildargs=None, target=None
             for kv in shlex.split(arg):
                 k, _, v = kv.partition("=")
                 config["Labels"][k] = v
-        elif op == "RUN":
+        elif op == "RUN" and not store.run_steps:
             log(" ---> RUN recorded, not executed by the local builder (no network on this host)")
         if op != "FROM":
             text = f"{op} {subst(arg)}" + (f" content={copied}" if copied else "")
             key = hashlib.sha256((key + "|" + text).encode()).hexdigest()
             fs_layer = op in ("COPY", "ADD", "RUN")
+            if op == "RUN" and store.run_steps:
+                snap = store.snapshot_dir(key)
+                if key in seen and os.path.isdir(snap):
+                    # the layer this step made before: its filesystem instead of running it again
+                    shutil.rmtree(rootfs)
+                    shutil.copytree(snap, rootfs, symlinks=True)
+                    os.utime(snap)  # most recently used
+                else:
+                    _run_step(_exec_form(subst(arg)), rootfs, config, work, log)
+                    store.keep_snapshot(key, rootfs)
+                    seen.pop(key, None)  # ran: not "Using cache"
             if key in seen:
                 log(" ---> Using cache")
             log(f" ---> {key[:12]}")

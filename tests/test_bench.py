@@ -54,7 +54,10 @@ def test_bench_cpu_tiny():
     assert wd["net"]["tcp_dials"] < wd["reference_equivalent"]["net"]["tcp_dials"], wd
     assert wd["reference_equivalent"]["wall_clock_s"] > wd["wall_clock_s"], wd
     dep = d["deploy"]
-    assert dep["control_plane_only"] is True and dep["net"]["tls_handshakes"] >= 1
+    # the image build ran the Dockerfile's RUN (npm install); an edit rebuilt from the layer cache
+    assert dep["control_plane_only"] is False and dep["run_steps_executed"] is True, dep
+    assert dep["net"]["tls_handshakes"] >= 1 and dep["phases_ms"]["image.build"] > 100, dep
+    assert dep["edit_redeploy_s"] < dep["wall_clock_s"], dep
     # reference timing: no kept-alive connections, 5 s rollout polls
     assert dep["reference_equivalent"]["wall_clock_s"] > dep["wall_clock_s"], dep
     # the reference's rollout wait polls every 5 s, the first check after one interval

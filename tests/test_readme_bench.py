@@ -70,3 +70,34 @@ def test_round4_line_renders_the_drill_and_wan_rows():
     assert "fault drill (hard crash (os._exit) of the only rank)" in out and "warm standby: yes" in out
     assert re.search(r"cluster behind 30 ms RTT / 100 Mbit/s .*\| \*\*\d+ ms\*\* \(sync [\d.]+ ms\) \|", out), out
     assert "`devspace deploy` quickstart across that link, cold" in out
+
+
+def test_round5_line_renders_the_measured_deploy_and_the_wait_caveat(tmp_path):
+    """Round 5: the deploy runs RUN steps (no longer control-plane only) and is measured cold, after
+    an edit and unchanged; a round-4 line keeps its caveats (control plane only; microservices'
+    helm wait off in both columns)."""
+    bt = _bt()
+    base = {"metric": "m", "value": 50.0, "steps": 20, "warmup": 5, "ms_per_step": 60.1, "p90_ms": 55.0,
+            "sync_p50_ms": 1.0, "config": {"app": "examples/quickstart"},
+            "reference_equivalent": {"p50_ms": 660.0, "sync_p50_ms": 605.0}}
+    r5 = dict(base, deploy={"wall_clock_s": 0.96, "edit_redeploy_s": 0.12, "warm_wall_clock_s": 0.08,
+                            "control_plane_only": False, "net": {"tls_handshakes": 2, "requests": 14},
+                            "reference_equivalent": {"wall_clock_s": 6.05, "edit_redeploy_s": 5.22,
+                                                     "warm_wall_clock_s": 5.2}},
+              microservices={"edit_to_pod_p50_ms": 1.1, "deploy_cold_s": 0.15, "note": "x; the helm rollout wait "
+                             "(on, as in the reference) completes", "reference_equivalent": {
+                                 "edit_to_pod_p50_ms": 605.0, "deploy_cold_s": 5.26}})
+    r4 = dict(base, deploy={"wall_clock_s": 0.026, "warm_wall_clock_s": 0.019, "control_plane_only": True,
+                            "net": {}, "reference_equivalent": {"wall_clock_s": 5.04, "warm_wall_clock_s": 5.04}},
+              microservices={"edit_to_pod_p50_ms": 0.87, "deploy_cold_s": 0.023, "note": "two deployments",
+                             "reference_equivalent": {"edit_to_pod_p50_ms": 607.0, "deploy_cold_s": 0.039}})
+    out = []
+    for i, line in enumerate((r5, r4)):
+        p = tmp_path / f"BENCH_r9{i}.json"
+        p.write_text(json.dumps({"cmd": "python3 bench.py", "run": {"stdout_tail": json.dumps(line)}}))
+        out.append(bt.render(str(p)))
+    assert "image build runs the Dockerfile's RUN steps" in out[0] and "0.960 s / 0.120 s / 0.080 s" in out[0]
+    assert "6.050 s / 5.220 s / 5.200 s (**6.3x**)" in out[0]
+    assert "helm wait off" not in out[0]
+    assert "control plane only: RUN steps not executed" in out[1]
+    assert "microservices (helm wait off in both columns)" in out[1]
