@@ -9,6 +9,7 @@
 #   bench   bench.py --steps $BENCH_STEPS --warmup $BENCH_WARMUP (the headline JSON line)
 #   prof    rocprofv3 --kernel-trace --stats of the rocm-pytorch pod under `devspace dev`
 #   rescue  the runner's snapshot cost on the flagship example (scripts/rescue_cost.py)
+#   kernels the gfx950 fused ops against the eager op chains they replace (scripts/bench_fused_ops.py)
 #
 # Output: gpurun_out/$GPU_TIER_TAG/ (default "tier"). Every GPU step has its own time limit and
 # the script stops at the first failing step: no GPU step runs after a fault or a timeout.
@@ -51,6 +52,11 @@ for s in "${steps[@]}"; do
         > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err") || fail prof $? "$OUT/prof_bench.err"
       db=$(find "$OUT/prof" -name '*.db' | head -1)
       [ -n "$db" ] && python3 scripts/prof_summary.py "$db" > "$OUT/prof_kernels.txt" && head -12 "$OUT/prof_kernels.txt"
+      ;;
+    kernels)
+      timeout -k 10 600 python -u scripts/bench_fused_ops.py --json "$OUT/kernels.json" > "$OUT/kernels.txt" \
+        2> "$OUT/kernels.err" || fail kernels $? "$OUT/kernels.err"
+      cat "$OUT/kernels.txt"
       ;;
     rescue)
       timeout -k 10 600 python -u scripts/rescue_cost.py > "$OUT/rescue.json" 2> "$OUT/rescue.err" \
