@@ -98,7 +98,7 @@ bool log_has_gpu_runtime_error(const std::string& text, std::string* match) {
 
 std::vector<std::string> runner_problems(const std::string& text) {
   const std::string tag = "[devspace-runner] ";
-  std::string down, failed_reload, last_failure, last_exception, rescue_off, restore_failed;
+  std::string down, failed_reload, last_failure, last_exception, rescue_off, restore_failed, long_step;
   bool in_traceback = false;
   for (auto& line : split(text, "\n")) {
     size_t at = line.find(tag);
@@ -119,9 +119,14 @@ std::vector<std::string> runner_problems(const std::string& text) {
       in_traceback = true;
     } else if (contains(msg, "waiting for a file change before starting")) {  // a group, or one rank
       down = msg;
+    } else if (starts_with(msg, "rank=") && contains(msg, " in step for ") && contains(msg, "; edit pending: ")) {
+      // the supervisor's stuck-step rule saw a long step with an edit waiting and left it alone
+      // (devspace_amd/supervise.py): the edit applies when the step ends
+      long_step = msg;
     } else if (starts_with(msg, "started gen=")) {
       down.clear();
       failed_reload.clear();
+      long_step.clear();
       rescue_off.clear();  // fresh processes take snapshots again
     } else if (starts_with(msg, "rescue: snapshot step=") && contains(msg, "did not restore")) {
       restore_failed = msg.substr(std::string("rescue: ").size());
@@ -132,6 +137,9 @@ std::vector<std::string> runner_problems(const std::string& text) {
       if (!rescue_off.empty() && rescue_off.back() == ')') rescue_off.pop_back();
     } else if (starts_with(msg, "reloaded gen=")) {
       failed_reload.clear();
+      long_step.clear();
+    } else if (contains(msg, " made no progress for ")) {
+      long_step.clear();  // restarted as stuck
     } else if (starts_with(msg, "reload failed gen=")) {
       failed_reload = msg;
     }
@@ -145,6 +153,13 @@ std::vector<std::string> runner_problems(const std::string& text) {
   } else if (!failed_reload.empty()) {
     std::string why = last_exception.empty() ? "" : " (" + last_exception + ")";
     out.push_back("the last edit did not load: " + failed_reload.substr(0, failed_reload.find('\n')) + why);
+  }
+  if (!long_step.empty()) {
+    // "rank=0 in step for 75 s at train.py:42; edit pending: <why>"
+    size_t semi = long_step.find("; edit pending: ");
+    out.push_back("the last edit is not loaded yet: training " + long_step.substr(0, semi) + " (" +
+                  long_step.substr(semi + std::string("; edit pending: ").size()) +
+                  "); the edit applies when that step ends");
   }
   if (!restore_failed.empty())
     out.push_back("a restarted training group could not load its rescue snapshot (" + restore_failed +

@@ -263,3 +263,17 @@ TEST(spdy_frames_round_trip_and_split_anywhere) {
               got[1].body.size() == 70000);
   EXPECT_TRUE(got[2].control && got[2].type == kube::spdy::Ping && kube::spdy::get_u32(got[2].body, 0) == 7);
 }
+
+TEST(analyze_reports_a_long_step_holding_back_an_edit) {
+  std::string up = "[devspace-runner] started gen=1 marker=v0\n";
+  std::string held = up + "[devspace-runner] rank=0 in step for 75 s at train.py:42; edit pending: rank=0 is making "
+                          "progress at train.py:42: not restarting\n";
+  auto p = analyze::runner_problems(held);
+  EXPECT_EQ(p.size(), (size_t)1);
+  EXPECT_TRUE(contains(p[0], "the last edit is not loaded yet: training rank=0 in step for 75 s at train.py:42"));
+  EXPECT_TRUE(contains(p[0], "making progress") && contains(p[0], "applies when that step ends"));
+  // resolved: the edit loaded, or the group was restarted as stuck
+  EXPECT_TRUE(analyze::runner_problems(held + "[devspace-runner] reloaded gen=2 marker=v1\n").empty());
+  EXPECT_TRUE(analyze::runner_problems(held + "[devspace-runner] rank=0 made no progress for 90 s at train.py:42 and "
+                                              "the code changed since (stuck in a step?): restarting\n").empty());
+}
