@@ -215,10 +215,12 @@ FAIL = {fail!r}
 
 def setup(ctx):
     torch.manual_seed(0)
-    dim = 512
+    dim = 1024
     layers = max(1, MB * 2**20 // (3 * 4 * dim * dim))  # fp32 weights + AdamW's two moments
-    model = DDP(torch.nn.Sequential(*[torch.nn.Linear(dim, dim, bias=False) for _ in range(layers)]),
-                gradient_as_bucket_view=True)
+    blocks = []
+    for _ in range(layers):  # normalised blocks: every layer gets a gradient (no tensor of zeros)
+        blocks += [torch.nn.Linear(dim, dim, bias=False), torch.nn.LayerNorm(dim)]
+    model = DDP(torch.nn.Sequential(*blocks), gradient_as_bucket_view=True)
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
     return {{"model": model, "opt": opt, "cursor": torch.tensor([ctx.rank * 1000 + 1])}}
 
@@ -274,8 +276,9 @@ def test_ddp_snapshot_is_written_once_and_restores_bit_exact(tmp_path):
                extra_env={"KUBERNETES_SERVICE_HOST": "10.96.0.1", "DEVSPACE_RESCUE_ROOT": str(shm),
                           "DEVSPACE_WARM_STANDBY": "0"})
     try:
-        r.until(rf"started gen=1 marker=v0 .*world={world}", timeout=300)
-        _, line = r.until(r"rescue snapshot step=(\d+) ", timeout=300)
+        r.until(rf"started gen=1 marker=v0 .*world={world}", timeout=600)
+        _, line = r.until(r"rescue snapshot step=(\d+) ", timeout=600)
+        snap_line = line
         m = re.search(r"rescue snapshot step=(\d+) .*\(group: ([\d.]+) MiB in shared memory for ([\d.]+) MiB of state", line)
         step, group_mib, state_mib = int(m.group(1)), float(m.group(2)), float(m.group(3))
         d = next(shm.iterdir())
@@ -285,12 +288,23 @@ def test_ddp_snapshot_is_written_once_and_restores_bit_exact(tmp_path):
         assert abs(on_disk / 2**20 - group_mib) < 0.5
         assert group_mib < state_mib / world * 1.05 + 1, line  # one rank's worth, not `world` of them
         fail.write_text("1")
-        r.until(r"rank=1 exited with code 3: restarting the group", timeout=120)
+        r.until(r"rank=1 exited with code 3: restarting the group", timeout=600)
         snapped = max(int(s) for s in re.findall(r"rescue snapshot step=(\d+)", r.text()))
-        _, line = r.until(r"restored step=(\d+) ", timeout=300)
+        _, line = r.until(r"restored step=(\d+) ", timeout=900)
         restored = int(re.search(r"restored step=(\d+)", line).group(1))
         assert restored == snapped, (restored, snapped)
-        r.until(rf"started gen=1 marker=v0 .*world={world}", timeout=120)
+        _, up = r.until(rf"started gen=1 marker=v0 .*world={world}", timeout=600)
+        if os.environ.get("RESCUE_TEST_OUT"):  # the profile of a large run (profiles/r5_rescue_dedup_*.json)
+            import json
+
+            restore = re.search(r"restored step=\d+ .*\(age ([\d.]+) s, ([\d.]+) MiB/rank in ([\d.]+) ms\)", line)
+            with open(os.environ["RESCUE_TEST_OUT"], "w") as f:
+                json.dump({"ranks": world, "state_mib_per_rank": round(state_mib / world, 1),
+                           "state_mib_all_ranks": state_mib, "group_snapshot_mib": group_mib,
+                           "on_disk_mib": round(on_disk / 2**20, 1), "restored_step": restored,
+                           "restore_ms_rank0": float(restore.group(3)) if restore else None,
+                           "snapshot_line": re.sub(r"^.*\[devspace-runner\] ", "", snap_line.strip()),
+                           "bit_exact_on_every_rank": True}, f, indent=1)
         for rank in range(world):
             path = log + str(rank)
             with open(path) as f:
