@@ -45,6 +45,14 @@ examples/quickstart/package.json:7, the redeploy loop of cmd/dev.go:225-234,284-
     newest step every rank holds instead of from scratch (`Rescue`).
   * restarts are fast: once a group is up, the supervisor keeps a warm standby group (torch and
     the group's libraries imported, no GPU touched) that replaces a failed one.
+  * a stop takes the whole process tree: ranks lead their own sessions and the supervisor is a
+    child subreaper (devspace_amd/supervise.py).
+  * stuck steps are restarted on evidence only (supervise._GroupWatch.assess; the heartbeat
+    thread, _Heartbeat below): a long healthy step (an evaluation, a checkpoint save) is left
+    to finish and the edit applies after it.
+
+The supervisor lives in devspace_amd/supervise.py, the snapshots in devspace_amd/rescue.py and
+the change detection in devspace_amd/changefeed.py; this module is the rank's loop.
 
 Preemptible steps: a step may call `ctx.preempt_point()` between its phases (e.g. between
 forward and backward). The point abandons the rest of the step when a newer version of the
@@ -964,8 +972,9 @@ def parse_args(argv=None):
                         "in a pod, /dev/shm for the pod's lifetime, dropped at a clean stop; elsewhere, /dev/shm "
                         "for the run)")
     p.add_argument("--stuck-after", type=float, default=float(os.environ.get("DEVSPACE_STUCK_AFTER_S", "60")),
-                   help="a rank whose loop has not come round for this long (or 50 step periods, if longer) "
-                        "while the code changed is taken as stuck in a step: the group restarts with the new code "
+                   help="restart a group stuck in a step with the new code when an edit waits in a steady-state "
+                        "step longer than this (or 10x the longest step so far), no rank's main thread has moved "
+                        "for this long, and a rescue snapshot exists; else the long step is reported once "
                         "(0: never)")
     p.add_argument("--no-warm-standby", dest="warm_standby", action="store_false",
                    default=os.environ.get("DEVSPACE_WARM_STANDBY", "1") != "0",
