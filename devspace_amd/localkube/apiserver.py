@@ -641,20 +641,31 @@ class ApiServer:
     @staticmethod
     def _refused_text(name, port, e):
         # the kubelet's wording (CRI streaming server): clients key on "connection refused"
+        if isinstance(e, LookupError):
+            return f"error forwarding port {port} to pod {name}, uid : {e.args[0]}"
         why = "connect: connection refused" if isinstance(e, ConnectionRefusedError) or "111" in str(e) else str(e)
         return (f"error forwarding port {port} to pod {name}, uid : failed to connect to localhost:{port} inside "
                 f"namespace: dial tcp4 127.0.0.1:{port}: {why}")
 
     async def portforward_ws(self, request, ns, name):
-        self.store.get("", "pods", ns, name)
+        uid = self.store.get("", "pods", ns, name)["metadata"].get("uid")
         ws = web.WebSocketResponse(protocols=(spdy.PROTOCOL, "v4.channel.k8s.io", "portforward.k8s.io"),
                                    max_msg_size=0)
         await ws.prepare(request)
         if ws.ws_protocol == spdy.PROTOCOL:
             # Kubernetes >= 1.30: one tunnel, a stream pair per forwarded connection
             self.portforward_tunnels += 1
-            tunnel = spdy.Tunnel(ws, lambda port: asyncio.open_connection("127.0.0.1", port),
-                                 lambda port, e: self._refused_text(name, port, e))
+
+            async def dial(port):
+                # the tunnel outlives its pod (pods share the host network here, so a port of
+                # the pod's replacement would answer): a stream of a deleted pod fails as the
+                # kubelet's does once the pod's sandbox is gone
+                cur = self.store.try_get("", "pods", ns, name)
+                if cur is None or cur["metadata"].get("uid") != uid:
+                    raise LookupError(f'failed to find sandbox "{uid}" in store: not found')
+                return await asyncio.open_connection("127.0.0.1", port)
+
+            tunnel = spdy.Tunnel(ws, dial, lambda port, e: self._refused_text(name, port, e))
             await tunnel.run()
             return ws
         port = int(request.query.get("ports", "0").split(",")[0])

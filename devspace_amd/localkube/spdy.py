@@ -135,7 +135,7 @@ class Tunnel:
     async def _pump(self, pair: _Pair):
         try:
             reader, writer = await self.dial(pair.port)
-        except OSError as e:
+        except (OSError, LookupError) as e:  # refused, or the pod is gone
             # the kubelet's wording; the client keys on "connection refused"
             await self._data(pair.error, self.refused(pair.port, e).encode(), fin=True)
             await self._data(pair.data, b"", fin=True)

@@ -309,10 +309,11 @@ class TunnelFwd : public FwdStream {
   void close() override {
     if (closed_) return;
     closed_ = true;
-    if (!data_done_) {  // abandoned (stop, a failed client write): the server stops forwarding
-      s_->reset(data_);
-      s_->reset(err_);
-    }
+    // abandoned (stop, a failed client write): the server stops forwarding, and a recv() still
+    // waiting in another thread returns (nothing arrives on a reset stream any more)
+    s_->reset(data_);
+    s_->reset(err_);
+    box_->push({0, "", true, "closed"});
   }
   const char* via() const override { return "tunnel"; }
 
@@ -353,6 +354,40 @@ std::shared_ptr<kube::SpdySession> PortForwarder::tunnel_for(const std::string& 
   tunnel_pod_ = pod;
   tunnel_requests_ = 0;
   return t;
+}
+
+bool PortForwarder::drop_tunnel_if_pod_gone(const std::string& pod) {
+  std::string uid;
+  {
+    std::lock_guard<std::mutex> g(pod_mu_);
+    // re-selected meanwhile: the next stream goes to the new pod's tunnel
+    if (pod_.at_path("metadata.name").as_string() != pod) return true;
+    uid = pod_.at_path("metadata.uid").as_string();
+  }
+  std::optional<Value> live;
+  try {
+    live = k_->try_get("/api/v1/namespaces/" + ns_ + "/pods/" + pod);
+  } catch (const std::exception&) {
+    return false;  // cannot tell (API server unreachable): keep the tunnel
+  }
+  if (live) {
+    const std::string phase = live->at_path("status.phase").as_string();
+    const std::string live_uid = live->at_path("metadata.uid").as_string();
+    if (phase != "Succeeded" && phase != "Failed" && live_uid == uid) return false;
+    if (live_uid != uid && phase == "Running") {
+      // the same name, a new pod (a StatefulSet's replacement): forward to it
+      std::lock_guard<std::mutex> g(pod_mu_);
+      if (pod_.at_path("metadata.name").as_string() == pod) pod_ = *live;
+      reselections_++;
+      log::info("Port forwarding " + describe() + " now targets pod " + pod + " (replaced)");
+    }
+  }
+  std::lock_guard<std::mutex> g(tunnel_mu_);
+  if (tunnel_ && tunnel_pod_ == pod) {
+    tunnel_->close();
+    tunnel_.reset();
+  }
+  return true;
 }
 
 std::unique_ptr<FwdStream> PortForwarder::open_to(const std::string& pod, int remote_port) {
@@ -607,6 +642,7 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
     // dial happens with it) and the time until the first reply byte or the refusal
     // (trace.jsonl "portforward.stream")
     const int64_t t_open = trace::now_us();
+    const std::string target = pod_name();
     bool preopened = false;
     if (next) {
       ws = next->take();
@@ -636,6 +672,7 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
     int wake[2];
     if (::pipe2(wake, O_CLOEXEC | O_NONBLOCK) != 0) break;
     std::atomic<bool> down_done{false}, got_reply{false}, refused{false};
+    std::string error_text;  // the first error message before any reply (read after the join)
     std::thread down([&] {
       int ch = 0;
       std::string data;
@@ -650,6 +687,7 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
             refused = true;
             break;
           }
+          if (!got_reply && error_text.empty()) error_text = data;
           log::file_logger("portforwarding")->emit("error", data, {});
         }
       }
@@ -696,11 +734,21 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
                    {"attempt", std::to_string(attempt)},
                    {"open_us", std::to_string(t_opened - t_open)},
                    {"first_us", tf ? std::to_string(tf - t_open) : std::string("-1")},
-                   {"outcome", refused ? "refused" : got_reply ? "reply" : "closed"},
+                   {"outcome", refused ? "refused" : got_reply ? "reply" : error_text.empty() ? "closed" : "error"},
                    {"preopened", preopened ? "1" : "0"},
                    {"via", ws->via()}});
     }
     ++attempt;
+    if (tunneled && !got_reply && !refused && !error_text.empty() && !stop_ && drop_tunnel_if_pod_gone(target)) {
+      // A tunnel outlives its pod: once the pod was replaced every stream fails with the
+      // kubelet's "failed to find sandbox"-type error instead of a 404 at the upgrade. The tunnel
+      // is dropped and the next stream re-selects the pod (open_stream); nothing reached the
+      // app, so a held connection is replayed there.
+      if (replayable && mono_ms() < hold_deadline) {
+        held_retries_++;
+        continue;
+      }
+    }
     if (refused && replayable && !stop_ && mono_ms() < hold_deadline) {
       // a hot-reloading app is back within tens of ms: retry at once for the first 100 ms
       // (a refusal takes a round trip, which paces the attempts; so does a pre-opened stream),

@@ -104,6 +104,9 @@ class PortForwarder {
   std::unique_ptr<FwdStream> open_to(const std::string& pod, int remote_port);
   // The pod's tunnel, opened (or re-opened after it closed) on demand; nullptr when unsupported.
   std::shared_ptr<kube::SpdySession> tunnel_for(const std::string& pod);
+  // A tunnel stream failed with an error before any reply: true when `pod` is gone, replaced
+  // (same name, new uid) or finished, or was re-selected away from; its tunnel is then dropped.
+  bool drop_tunnel_if_pod_gone(const std::string& pod);
   std::shared_ptr<kube::Client> k_;
   std::mutex pod_mu_;
   Value pod_;
