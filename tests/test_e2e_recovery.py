@@ -138,6 +138,41 @@ def test_terminal_reconnects_after_pod_restart(localkube):
     lk.run(["purge"], proj)
 
 
+def test_port_forward_follows_a_statefulset_pod_replaced_under_the_same_name(localkube):
+    """A StatefulSet's replacement pod keeps its name: the multiplexed tunnel of the old pod
+    answers every stream with the kubelet's missing-sandbox error (no 404 at an upgrade to
+    notice), so the forward compares uids, drops the tunnel and replays on the new pod's."""
+    lk = localkube
+    ns = "rec-sts"
+    remote, local = _free_port(), _free_port()
+    proj = lk.project("quickstart-kubectl", "qsk-rec-sts")
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    cfg["cluster"]["namespace"] = ns
+    cfg["dev"].pop("overrideImages")
+    cfg["dev"]["ports"][0]["portMappings"] = [{"localPort": local, "remotePort": remote}]
+    open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    man_path = os.path.join(proj, "kube", "deployment.yaml")
+    man = yaml.safe_load(open(man_path))
+    man["kind"] = "StatefulSet"
+    man["spec"]["serviceName"] = "quickstart"
+    man["spec"]["template"]["spec"]["containers"][0]["env"] = [{"name": "PORT", "value": str(remote)}]
+    open(man_path, "w").write(yaml.safe_dump(man))
+    dev = lk.popen(["dev", "--terminal=false", "--sync=false"], proj)
+    try:
+        first = wait_for(lambda: running(lk.pods(ns)), timeout=60, what="pod")[0]
+        assert first["metadata"]["name"] == "quickstart-0"
+        assert wait_for(lambda: _fetch(local), timeout=30, what="forwarded response")
+        lk.cluster.store.mark_deleting("", "pods", ns, "quickstart-0")
+        wait_for(lambda: [p for p in running(lk.pods(ns))
+                          if p["metadata"]["uid"] != first["metadata"]["uid"]], timeout=60, what="replacement pod")
+        assert wait_for(lambda: _fetch(local), timeout=30, what="response from the replacement pod")
+    finally:
+        out = _stop(dev)
+    assert "now targets pod quickstart-0 (replaced)" in out, out
+    lk.run(["purge"], proj)
+
+
 def test_reload_with_open_forwarded_connections(localkube):
     """dev auto-reload destroys the forwarders while connections are still open: every
     connection thread is owned and joined (round 1 detached them with a dangling `this`)."""
