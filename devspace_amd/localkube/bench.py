@@ -75,16 +75,21 @@ def _prewarm_runtime():
     return done
 
 
-def bench_deploy(workdir, example="quickstart", tls=False, reference=False, wan=None):
+# the file an edit touches, per example: the app's source, never what the slow RUN depends on
+EDITED = {"quickstart": "index.js", "rocm-pytorch": "train.py"}
+
+
+def bench_deploy(workdir, example="quickstart", tls=False, reference=False, wan=None, gpus=0):
     """reference=True: the reference's waits (DEVSPACE_REFERENCE_TIMING: 1 s pod sleeps, 5 s
     rollout polls, no kept-alive connections) and sync protocol, on the same cluster code.
-    wan=(rtt_ms, mbit): the API server behind a shaped link (netem.ShapedLink)."""
+    wan=(rtt_ms, mbit): the API server behind a shaped link (netem.ShapedLink). gpus: the
+    node's amd.com/gpu (the rocm-pytorch example requests one)."""
     base = os.path.join(workdir, "deploy-bench" + ("-ref" if reference else "") + ("-wan" if wan else ""))
     os.makedirs(base, exist_ok=True)
     proj = os.path.join(base, example)
     shutil.copytree(os.path.join(ROOT, "examples", example), proj, symlinks=True)
     prewarmed = _prewarm_runtime()
-    cluster = LocalCluster(os.path.join(base, "cluster"), gpus=0, tls=tls, run_steps=True).start()
+    cluster = LocalCluster(os.path.join(base, "cluster"), gpus=gpus, tls=tls, run_steps=True).start()
     link = None
     try:
         env = devspace_env(cluster, base)
@@ -100,8 +105,9 @@ def bench_deploy(workdir, example="quickstart", tls=False, reference=False, wan=
         if "Successfully deployed!" not in out:
             raise RuntimeError(out)
         phases, net = _phases(trace)
-        # an edit of the app, deployed: rebuilt from the layer cache (npm install reused)
-        app = os.path.join(proj, "index.js")
+        # an edit of the app, deployed: rebuilt from the layer cache (npm install, or the
+        # kernel build of the GPU image, reused)
+        app = os.path.join(proj, EDITED.get(example, "index.js"))
         if os.path.exists(app):
             with open(app, "a") as f:
                 f.write("\n// edited\n")

@@ -10,6 +10,7 @@
 #   prof    rocprofv3 --kernel-trace --stats of the rocm-pytorch pod under `devspace dev`
 #   rescue  the runner's snapshot cost on the flagship example (scripts/rescue_cost.py)
 #   kernels the gfx950 fused ops against the eager op chains they replace (scripts/bench_fused_ops.py)
+#   layers  the rocm-pytorch image built with RUN executed, then rebuilt after an edit (scripts/image_rebuild_cost.py)
 #
 # Output: gpurun_out/$GPU_TIER_TAG/ (default "tier"). Every GPU step has its own time limit and
 # the script stops at the first failing step: no GPU step runs after a fault or a timeout.
@@ -48,7 +49,7 @@ for s in "${steps[@]}"; do
       # the kernel stats are the training steps the hot reloads ran
       R=$PWD
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o devloop -- \
-        python3 "$R/bench.py" --steps 10 --warmup 2 --qs-steps 0 --ref-steps 0 --no-deploy-bench \
+        python3 "$R/bench.py" --steps 1 --warmup 0 --gpu-steps 10 --ref-steps 0 --example-steps 0 --no-deploy-bench \
         > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err") || fail prof $? "$OUT/prof_bench.err"
       db=$(find "$OUT/prof" -name '*.db' | head -1)
       [ -n "$db" ] && python3 scripts/prof_summary.py "$db" > "$OUT/prof_kernels.txt" && head -12 "$OUT/prof_kernels.txt"
@@ -62,6 +63,11 @@ for s in "${steps[@]}"; do
       timeout -k 10 600 python -u scripts/rescue_cost.py > "$OUT/rescue.json" 2> "$OUT/rescue.err" \
         || fail rescue $? "$OUT/rescue.err"
       tail -1 "$OUT/rescue.json"
+      ;;
+    layers)
+      timeout -k 10 900 python -u scripts/image_rebuild_cost.py > "$OUT/layers.json" 2> "$OUT/layers.err" \
+        || fail layers $? "$OUT/layers.err"
+      tail -1 "$OUT/layers.json"
       ;;
     *)
       echo "unknown step $s" >&2

@@ -319,15 +319,16 @@ void SpdySession::close() {
 }
 
 void SpdySession::end_all(const std::string& why) {
-  std::map<uint32_t, std::shared_ptr<Stream>> streams;
+  std::vector<std::shared_ptr<Stream>> open;  // streams the peer has not ended
   {
     std::lock_guard<std::mutex> g(mu_);
     if (dead_) return;
     dead_ = true;
-    streams.swap(streams_);
+    for (auto& kv : streams_)
+      if (!kv.second->remote_end) open.push_back(kv.second);
+    streams_.clear();
   }
-  for (auto& kv : streams)
-    if (!kv.second->remote_end) kv.second->box->push({kv.second->channel, "", true, why});
+  for (auto& s : open) s->box->push({s->channel, "", true, why});
 }
 
 void SpdySession::dispatch_data(uint32_t id, uint8_t flags, std::string data) {

@@ -47,3 +47,15 @@ def test_every_script_is_a_documented_tool():
     readme = open(os.path.join(ROOT, "scripts", "README.md")).read()
     for p in sorted(glob.glob(os.path.join(ROOT, "scripts", "*.py")) + glob.glob(os.path.join(ROOT, "scripts", "*.sh"))):
         assert f"`{os.path.basename(p)}`" in readme, os.path.basename(p)
+
+
+def test_gpu_tier_passes_only_flags_its_scripts_accept():
+    """A GPU-tier step whose flags the script no longer knows fails only on the GPU box: every
+    `--flag` passed to bench.py or a scripts/*.py in scripts/gpu_tier.sh is one the script parses."""
+    tier = open(os.path.join(ROOT, "scripts", "gpu_tier.sh")).read()
+    calls = re.findall(r"python3? -?u? ?\"?(?:\$R/)?((?:scripts/)?\w+\.py)\"?((?:[^\n]|\\\n)*)", tier)
+    assert any(c[0] == "bench.py" for c in calls)
+    for script, args in calls:
+        src = open(os.path.join(ROOT, script)).read()
+        for flag in re.findall(r"(?<![\w-])(--[a-z][\w-]*)", args):
+            assert f'"{flag}"' in src, f"gpu_tier.sh passes {flag} to {script}, which does not define it"
