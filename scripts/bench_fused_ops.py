@@ -115,8 +115,10 @@ def load_train():
 
 
 def step_case(dev):
-    class Ctx:
-        rank, distributed, device = 0, False, dev
+    from devspace_amd.runner import Context  # what the runner hands train.py
+
+    def Ctx():
+        return Context(0, 1, 0, dev)
 
     m_fused = load_train()
     m_eager = load_train()

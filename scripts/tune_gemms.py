@@ -66,8 +66,10 @@ def main():
     tunable.set_numerical_check_tolerances(True, 1e-2, 1e-2)  # reject solutions that disagree with the default
     tunable.set_filename(a.out + ".exit.csv")  # TunableOp's own exit-time dump; ours is written below
 
-    class Ctx:
-        rank, distributed, device = 0, False, torch.device("cuda")
+    from devspace_amd.runner import Context  # what the runner hands train.py
+
+    def Ctx():
+        return Context(0, 1, 0, torch.device("cuda"))
 
     mod = load_train()
     state = mod.setup(Ctx())

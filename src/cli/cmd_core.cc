@@ -178,6 +178,16 @@ int run_dev(cli::Command& c, const std::vector<std::string>& args) {
   }
   bool skip = c.get_bool("skip-pipeline");
   while (true) {
+    {
+      // the WebSocket upgrades the services below open: two sync shells per path, one
+      // port-forward tunnel per forward, the attach or terminal stream, plus one for the pod
+      // lookups they make at the same time. Dialed now, while the pipeline runs, they cost the
+      // upgrade round trip only on a remote cluster.
+      const Value& dev = s.cfg().get("dev");
+      int n = (c.get_bool("sync") ? 2 * (int)dev.get("sync").size() : 0) +
+              (c.get_bool("portforwarding") ? (int)dev.get("ports").size() : 0) + 2;
+      s.kube->prewarm_upgrades(std::min(n, 8));
+    }
     if (!skip) {
       try {
         pipeline(s, true, c.get_bool("force-build"), c.get_bool("force-deploy"), "");

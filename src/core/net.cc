@@ -686,6 +686,7 @@ struct HttpClient::State {
   bool keepalive = !reference_timing();  // the reference-equivalent column dials per request
   size_t max_idle = 8;
   ProxyConfig proxy = ProxyConfig::from_env();
+  std::function<std::unique_ptr<Conn>()> source;
 };
 
 HttpClient::HttpClient() : st_(std::make_shared<State>()) {}
@@ -731,6 +732,11 @@ size_t HttpClient::idle_connections() const {
   return st_->idle.size();
 }
 
+void HttpClient::set_conn_source(std::function<std::unique_ptr<Conn>()> source) {
+  std::lock_guard<std::mutex> g(st_->mu);
+  st_->source = std::move(source);
+}
+
 void HttpClient::close_idle() {
   std::vector<std::unique_ptr<Conn>> drop;
   std::lock_guard<std::mutex> g(st_->mu);
@@ -755,6 +761,7 @@ std::unique_ptr<Conn> HttpClient::connect() {
 
 std::unique_ptr<Conn> HttpClient::take_conn(bool* reused) {
   std::vector<std::unique_ptr<Conn>> dead;
+  std::function<std::unique_ptr<Conn>()> source;
   {
     std::lock_guard<std::mutex> g(st_->mu);
     while (!st_->idle.empty()) {
@@ -768,8 +775,11 @@ std::unique_ptr<Conn> HttpClient::take_conn(bool* reused) {
       stats().reused++;
       return c;
     }
+    source = st_->source;
   }
   *reused = false;
+  if (source)
+    if (auto c = source()) return c;  // dialed ahead (counted as a dial then)
   return connect();
 }
 

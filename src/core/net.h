@@ -133,6 +133,9 @@ class HttpClient {
   void set_proxy(ProxyConfig p);
   size_t idle_connections() const;
   void close_idle();
+  // Where a request gets a connection when none is idle, before dialing one: a pool of
+  // connections dialed ahead of time (nullptr from it: dial).
+  void set_conn_source(std::function<std::unique_ptr<Conn>()> source);
 
  private:
   struct State;

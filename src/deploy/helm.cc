@@ -746,8 +746,10 @@ void Client::store(const Release& r) {
 
 // Helm 3 (pkg/action/upgrade.go + storage.removeLeastRecent): delete the oldest revisions
 // beyond max_history_, never the deployed one.
-void Client::prune_history(const std::string& ns, const std::string& name) {
+void Client::prune_history(const std::string& ns, const std::string& name, int known) {
   if (max_history_ <= 0) return;
+  // (a revision another client stored meanwhile is pruned by the next deploy)
+  if (known >= 0 && known <= max_history_) return;
   Value list = k_->get("/api/v1/namespaces/" + ns + "/secrets?labelSelector=" +
                        net::url_encode("owner=helm,name=" + name));
   std::vector<std::pair<int, std::pair<std::string, std::string>>> revs;  // version, (secret, status)
@@ -1389,7 +1391,7 @@ Release Client::install_or_upgrade(const std::string& name, const std::string& n
   r.status = "deployed";
   r.description = ro.is_install ? "Install complete" : "Upgrade complete";
   store(r);
-  prune_history(ns, name);
+  prune_history(ns, name, (int)hist.size() + 1);
   return r;
 }
 
@@ -1433,7 +1435,7 @@ void Client::rollback(const std::string& ns, const std::string& name, int to_ver
       store(old);
     }
   store(r);
-  prune_history(ns, name);
+  prune_history(ns, name, (int)hist.size() + 1);
 }
 
 void Client::delete_release(const std::string& ns, const std::string& name, bool purge) {

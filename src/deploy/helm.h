@@ -140,7 +140,9 @@ class Client {
 
  private:
   void store(const Release& r);
-  void prune_history(const std::string& ns, const std::string& name);
+  // `known`: the revisions this command knows of (its history read plus what it stored); when
+  // they fit in max_history_ the list is not read again (one API round trip less per deploy)
+  void prune_history(const std::string& ns, const std::string& name, int known = -1);
   int max_history_ = 10;
   // Runs the hooks of one lifecycle event in weight order; throws on a failed hook.
   void run_hooks(std::vector<Hook>& hooks, const std::string& event, const std::string& ns, int timeout_s);

@@ -16,6 +16,7 @@
 #include "core/log.h"
 #include "core/proc.h"
 #include "core/strutil.h"
+#include "core/trace.h"
 
 namespace ds {
 namespace kube {
@@ -161,6 +162,9 @@ Client::Client(RestConfig cfg) : cfg_(std::move(cfg)), http_(cfg_.server, tls_fo
     p.https_proxy = p.http_proxy = cfg_.proxy_url;
     http_.set_proxy(p);
   }
+  // a request finding no idle connection takes one `prewarm_upgrades` dialed (the services of
+  // `dev` look up their pods concurrently, right before they upgrade)
+  http_.set_conn_source([this] { return take_prewarmed(); });
   http_.set_header("Accept", "application/json");
   http_.set_header("User-Agent", "devspace-amd/0.2");
   std::lock_guard<std::mutex> g(auth_mu_);
@@ -332,11 +336,16 @@ net::Response Client::raw(const std::string& method, const std::string& path, co
   r.body = body;
   r.timeout_ms = timeout_ms;
   if (!body.empty()) r.headers.push_back({"Content-Type", content_type});
+  // one span per API call (trace.jsonl "api.request"): which calls a command makes, in what
+  // order and how long each took, so round trips on a slow link can be counted
+  trace::Span span("api.request", {{"method", method}, {"path", path.substr(0, path.find('?'))}});
   for (int attempt = 1;; ++attempt) {
     ensure_fresh_credentials();
     net::Response resp = http_.request(r);
     if (resp.status == 401 && refresh_after_unauthorized()) resp = http_.request(r);
     int wait = retry_wait_ms(resp.status, resp.header("retry-after"), method);
+    span.set("status", std::to_string(resp.status));
+    if (attempt > 1) span.set("attempts", std::to_string(attempt));
     if (wait < 0 || attempt > kMaxApiRetries) return resp;
     throttled(method + " " + path, resp.status, wait, attempt);
   }
@@ -820,9 +829,63 @@ std::shared_ptr<SpdySession> Client::portforward_tunnel(const std::string& ns, c
   return std::make_shared<SpdySession>(std::move(ws));
 }
 
+static int64_t mono_ms_now() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+void Client::prewarm_upgrades(int n) {
+  if (n <= 0 || reference_timing()) return;  // the reference dials every stream
+  std::lock_guard<std::mutex> g(warm_mu_);
+  for (int i = 0; i < n; ++i) {
+    ++warm_pending_;
+    warm_threads_.emplace_back([this] {
+      std::unique_ptr<net::Conn> c;
+      try {
+        c = http_.connect();
+      } catch (const std::exception&) {
+      }
+      {
+        std::lock_guard<std::mutex> g2(warm_mu_);
+        --warm_pending_;
+        if (c) warm_.emplace_back(mono_ms_now(), std::move(c));
+      }
+      warm_cv_.notify_all();
+    });
+  }
+}
+
+std::unique_ptr<net::Conn> Client::take_prewarmed() {
+  const int64_t kMaxAgeMs = 60000;  // below API-server idle timeouts
+  std::unique_lock<std::mutex> lk(warm_mu_);
+  while (true) {
+    while (!warm_.empty()) {
+      auto e = std::move(warm_.front());
+      warm_.pop_front();
+      if (mono_ms_now() - e.first < kMaxAgeMs && !e.second->stale()) return std::move(e.second);
+    }
+    if (warm_pending_ == 0) return nullptr;
+    // a dial already under way is never slower than a new one
+    warm_cv_.wait_for(lk, std::chrono::seconds(30), [this] { return !warm_.empty() || warm_pending_ == 0; });
+    if (warm_.empty()) return nullptr;
+  }
+}
+
+Client::~Client() {
+  std::vector<std::thread> ts;
+  {
+    std::lock_guard<std::mutex> g(warm_mu_);
+    ts.swap(warm_threads_);
+  }
+  for (auto& t : ts)
+    if (t.joinable()) t.join();
+}
+
 std::unique_ptr<net::WebSocket> Client::ws_connect(const std::string& path, const std::vector<std::string>& protocols,
                                                    std::unique_ptr<net::Conn> spare) {
   bool refreshed = false;
+  if (!spare) spare = take_prewarmed();
+  trace::Span span("api.upgrade", {{"path", path.substr(0, path.find('?'))}, {"predialed", spare ? "1" : "0"}});
   for (int attempt = 1;; ++attempt) {
     ensure_fresh_credentials();
     try {

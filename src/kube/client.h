@@ -9,6 +9,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <memory>
@@ -156,6 +157,13 @@ class Client {
 
   net::HttpClient& http() { return http_; }
 
+  // Dials `n` connections to the API server (TCP + TLS) in the background for the WebSocket
+  // upgrades that follow (exec, attach, port-forward): `devspace dev` asks for them before it
+  // builds and deploys, so opening its sync shells and streams costs the upgrade round trip
+  // only, not a handshake each. Unused ones are dropped after a minute.
+  void prewarm_upgrades(int n);
+  ~Client();
+
   // Credential refresh (exec plugins: on expiry and on 401; tokenFile: every minute).
   void ensure_fresh_credentials();
   bool refresh_after_unauthorized();
@@ -171,7 +179,15 @@ class Client {
   void apply_auth_locked();
   std::unique_ptr<net::WebSocket> ws_connect(const std::string& path, const std::vector<std::string>& protocols,
                                              std::unique_ptr<net::Conn> spare = nullptr);
+  // a pre-dialed connection, or nullptr; waits for one still being dialed (never slower than a
+  // new dial)
+  std::unique_ptr<net::Conn> take_prewarmed();
   RestConfig cfg_;
+  std::mutex warm_mu_;
+  std::condition_variable warm_cv_;
+  std::deque<std::pair<int64_t, std::unique_ptr<net::Conn>>> warm_;  // (dialed at ms, conn)
+  int warm_pending_ = 0;
+  std::vector<std::thread> warm_threads_;
   int local_cluster_ = -1;  // is_local_cluster() cache
   net::HttpClient http_;
   ApplyOptions apply_opts_;

@@ -307,7 +307,8 @@ const std::vector<std::string>& helper_dirs() {
   return dirs;
 }
 
-std::string helper_probe_script(const std::string& file, const std::vector<std::string>& dirs) {
+std::string helper_probe_script(const std::string& file, const std::vector<std::string>& dirs,
+                                const std::string& when_present) {
   std::string list;
   for (auto& d : dirs) list += (d[0] == '$' ? "\"" + d + "\"" : shell_quote(d)) + " ";
   // a one-line `#!/bin/sh` script run from the directory tells a noexec mount apart
@@ -317,7 +318,8 @@ std::string helper_probe_script(const std::string& file, const std::vector<std::
          "; do [ -n \"$d\" ] || continue; if mkdir -p \"$d\" 2>/dev/null && [ -w \"$d\" ] && printf '#!/bin/sh\\nexit 0\\n' > \"$d/.devspace-x$$\" "
          "2>/dev/null && chmod +x \"$d/.devspace-x$$\" 2>/dev/null && \"$d/.devspace-x$$\" 2>/dev/null; then "
          "rm -f \"$d/.devspace-x$$\"; dsd=$d; dss=NEED; break; fi; rm -f \"$d/.devspace-x$$\" 2>/dev/null; done; fi; "
-         "if [ -n \"$dsd\" ]; then echo \"$dss $dsd\"; else echo NOHELPER; fi\n";
+         "if [ \"$dss\" = HAVE ]; then echo \"HAVE $dsd\"; " + (when_present.empty() ? std::string(":") : when_present) +
+         "; elif [ -n \"$dsd\" ]; then echo \"NEED $dsd\"; else echo NOHELPER; fi\n";
 }
 
 bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out) {
@@ -327,26 +329,30 @@ bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out) {
   std::string bin;
   if (!fs::read_file(o_.helper_path, &bin)) return false;
   std::string file = "devspace-helper-" + sha256_hex(bin).substr(0, 16);
-  if (!write_all(sh->in(), helper_probe_script(file, helper_dirs()))) return false;
+  // stdout carries replies, stderr the change events: exec with the shell's fds as-is
+  auto start = [&](const std::string& path) {
+    return "mkdir -p " + shell_quote(dest_) + " && exec " + path + " serve " + shell_quote(dest_) + " || echo HELPERFAIL";
+  };
+  // a helper already in the container starts in the probe's round trip
+  if (!write_all(sh->in(), helper_probe_script(file, helper_dirs(), start("\"$dsd/" + file + "\"")))) return false;
   std::string line;
   if (!out.read_line(&line, 15000)) return false;
   if (line == "NOHELPER" || line.size() < 6 || (!starts_with(line, "HAVE ") && !starts_with(line, "NEED "))) {
     logf("[Sync] No directory in the container can hold and run the helper (" + line + ")");
     return false;
   }
-  std::string name = shell_quote(line.substr(5) + "/" + file);
   if (starts_with(line, "NEED ")) {
-    std::string up = "echo " + std::string(kStart) + "; head -c " + std::to_string(bin.size()) + " > " + name +
-                     ".tmp && chmod +x " + name + ".tmp && mv " + name + ".tmp " + name + "; echo " + kDone + "\n";
+    std::string name = shell_quote(line.substr(5) + "/" + file);
+    // a temporary name per shell: the sync's shells may upload at the same time
+    std::string tmp = shell_quote(line.substr(5) + "/" + file) + ".tmp.$$";
+    std::string up = "echo " + std::string(kStart) + "; head -c " + std::to_string(bin.size()) + " > " + tmp +
+                     " && chmod +x " + tmp + " && mv " + tmp + " " + name + "; echo " + kDone + "\n";
     if (!write_all(sh->in(), up)) return false;
     if (!out.wait_for(kStart, 15000)) return false;
     if (!write_all(sh->in(), bin)) return false;
     if (!out.wait_for(kDone, 30000)) return false;
+    if (!write_all(sh->in(), start(name) + "\n")) return false;
   }
-  // stdout carries replies, stderr the change events: exec with the shell's fds as-is
-  std::string exec = "mkdir -p " + shell_quote(dest_) + " && exec " + name + " serve " + shell_quote(dest_) +
-                     " || echo HELPERFAIL\n";
-  if (!write_all(sh->in(), exec)) return false;
   if (!out.read_line(&line, 15000)) return false;
   return line == "HELPER READY";
 }

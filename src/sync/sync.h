@@ -43,8 +43,10 @@ Mode parse_mode(const std::string& s);
 // Shell snippet that picks where the in-container helper lives: the first of `dirs` that already
 // holds an executable `<dir>/<file>` ("HAVE <dir>"), else the first that is writable and lets a
 // file in it execute ("NEED <dir>"; hardened pods mount /tmp noexec), else "NOHELPER" (also on a
-// non-x86_64 container: the helper is a static x86_64 binary).
-std::string helper_probe_script(const std::string& file, const std::vector<std::string>& dirs);
+// non-x86_64 container: the helper is a static x86_64 binary). `when_present`: shell run right
+// after "HAVE <dir>" with $dsd set to that directory (starting the helper in the same round trip).
+std::string helper_probe_script(const std::string& file, const std::vector<std::string>& dirs,
+                                const std::string& when_present = "");
 // Where the helper is looked for in a container, in order.
 const std::vector<std::string>& helper_dirs();  // compat|fast|helper (default fast); env DEVSPACE_SYNC_MODE
 const char* mode_name(Mode m);

@@ -646,6 +646,11 @@ TEST(sync_helper_probe_picks_a_usable_directory) {
   out = run(sync::helper_probe_script("devspace-helper-x", {base + "/a", base + "/b"}));
   EXPECT_EQ(out, "HAVE " + base + "/b");
   EXPECT_TRUE(!fs::exists(base + "/a/.devspace-x"));
+  // a helper that is there starts in the probe's round trip; one still to upload does not
+  out = run(sync::helper_probe_script("devspace-helper-x", {base + "/a", base + "/b"}, "echo STARTED \"$dsd\""));
+  EXPECT_EQ(out, "HAVE " + base + "/b\nSTARTED " + base + "/b");
+  out = run(sync::helper_probe_script("devspace-helper-y", {base + "/a"}, "echo STARTED \"$dsd\""));
+  EXPECT_EQ(out, "NEED " + base + "/a");
   out = run(sync::helper_probe_script("devspace-helper-x", {"/proc/ds-no-such"}));
   EXPECT_EQ(out, "NOHELPER");
   fs::remove_all(base);
