@@ -7,7 +7,7 @@
 #   tests   python -m pytest tests -m gpu (every HIP op against fp32 PyTorch, the runner on the GPU)
 #   smoke   __graft_entry__.smoke(): one forward+backward of the flagship TinyLM on cuda:0
 #   bench   bench.py --steps $BENCH_STEPS --warmup $BENCH_WARMUP (the headline JSON line)
-#   prof    rocprofv3 --kernel-trace --stats of the rocm-pytorch pod under `devspace dev`
+#   prof    rocprofv3 --kernel-trace --stats of the hot-reload runner training the rocm-pytorch example
 #   rescue  the runner's snapshot cost on the flagship example (scripts/rescue_cost.py)
 #   kernels the gfx950 fused ops against the eager op chains they replace (scripts/bench_fused_ops.py)
 #   layers  the rocm-pytorch image built with RUN executed, then rebuilt after an edit (scripts/image_rebuild_cost.py)
@@ -45,12 +45,15 @@ for s in "${steps[@]}"; do
       tail -1 "$OUT/bench.json"
       ;;
     prof)
-      # the profiler follows the pod's runner (environment inherited through the local kubelet):
-      # the kernel stats are the training steps the hot reloads ran
+      # the hot-reload runner on the flagship example for a bounded number of steps: a clean exit
+      # lets every profiled process write its trace. (rocprofv3's SIGTERM handler waits for the
+      # process's children before it chains to the program's handler, so a supervisor stopped
+      # with SIGTERM never forwards it to its ranks, which run in sessions of their own: a
+      # profile of a pod stopped that way, as `devspace dev` under the bench ends it, is empty.)
       R=$PWD
-      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o devloop -- \
-        python3 "$R/bench.py" --steps 1 --warmup 0 --gpu-steps 10 --ref-steps 0 --example-steps 0 --no-deploy-bench \
-        > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err") || fail prof $? "$OUT/prof_bench.err"
+      (cd /tmp && export TMPDIR=/tmp PYTHONPATH="$R" && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+        -d "$OUT/prof" -o runner -- python3 -m devspace_amd.runner --max-steps "${PROF_STEPS:-40}" --no-warm-standby \
+        "$R/examples/rocm-pytorch/train.py" > "$OUT/prof_runner.log" 2>&1) || fail prof $? "$OUT/prof_runner.log"
       db=$(find "$OUT/prof" -name '*.db' | head -1)
       [ -n "$db" ] && python3 scripts/prof_summary.py "$db" > "$OUT/prof_kernels.txt" && head -12 "$OUT/prof_kernels.txt"
       ;;
