@@ -188,7 +188,13 @@ bool SpdyHeaderCodec::decompress(const std::string& block, SpdyHeaders* out) {
 
 void SpdyMailbox::push(Event e) {
   {
-    std::lock_guard<std::mutex> g(mu);
+    std::unique_lock<std::mutex> lk(mu);
+    if (closed) return;
+    if (!e.data.empty()) {
+      cv.wait(lk, [this] { return closed || bytes < cap; });
+      if (closed) return;
+      bytes += e.data.size();
+    }
     q.push_back(std::move(e));
   }
   cv.notify_all();
@@ -196,14 +202,28 @@ void SpdyMailbox::push(Event e) {
 
 bool SpdyMailbox::pop(Event* e, int timeout_ms) {
   std::unique_lock<std::mutex> lk(mu);
-  auto ready = [this] { return !q.empty(); };
+  auto ready = [this] { return !q.empty() || closed; };
   if (timeout_ms < 0)
     cv.wait(lk, ready);
   else if (!cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready))
     return false;
+  if (q.empty()) return false;  // closed
   *e = std::move(q.front());
   q.pop_front();
+  bytes -= e->data.size();
+  lk.unlock();
+  cv.notify_all();  // a push waiting for room
   return true;
+}
+
+void SpdyMailbox::close() {
+  {
+    std::lock_guard<std::mutex> g(mu);
+    closed = true;
+    q.clear();
+    bytes = 0;
+  }
+  cv.notify_all();
 }
 
 // ---------------------------------------------------------------- session

@@ -56,6 +56,9 @@ class SpdyHeaderCodec {
 
 // Everything a consumer of streams waits on: (channel, bytes) events of the streams registered
 // to it, plus their ends.
+// Bounded: once `cap` bytes wait unread, push() blocks the session's reader (every stream of
+// the tunnel waits, as a Go spdystream connection's frame loop does when a stream's buffer is
+// full) instead of buffering a fast download for a slow local client without limit.
 struct SpdyMailbox {
   struct Event {
     int channel;      // what the stream was registered as (port-forward: 0 data, 1 error)
@@ -66,9 +69,14 @@ struct SpdyMailbox {
   std::mutex mu;
   std::condition_variable cv;
   std::deque<Event> q;
+  size_t bytes = 0;         // data bytes queued
+  size_t cap = 16u << 20;
+  bool closed = false;      // the consumer is gone: data is dropped, nothing blocks
   void push(Event e);
-  // false on timeout
+  // false on timeout, or once closed
   bool pop(Event* e, int timeout_ms = -1);
+  // the consumer is done: queued data is dropped, pushes stop blocking, pop() returns false
+  void close();
 };
 
 class SpdySession {

@@ -309,11 +309,11 @@ class TunnelFwd : public FwdStream {
   void close() override {
     if (closed_) return;
     closed_ = true;
-    // abandoned (stop, a failed client write): the server stops forwarding, and a recv() still
-    // waiting in another thread returns (nothing arrives on a reset stream any more)
+    // abandoned (stop, a failed client write): the server stops forwarding; a recv() still
+    // waiting in another thread returns, and the session's reader never blocks on this mailbox
     s_->reset(data_);
     s_->reset(err_);
-    box_->push({0, "", true, "closed"});
+    box_->close();
   }
   const char* via() const override { return "tunnel"; }
 

@@ -264,6 +264,37 @@ TEST(spdy_frames_round_trip_and_split_anywhere) {
   EXPECT_TRUE(got[2].control && got[2].type == kube::spdy::Ping && kube::spdy::get_u32(got[2].body, 0) == 7);
 }
 
+// A stream's mailbox holds at most `cap` unread bytes: the tunnel's reader waits for the consumer
+// (backpressure, as a spdystream frame loop), and a consumer that leaves unblocks it.
+TEST(spdy_mailbox_bounds_unread_data) {
+  kube::SpdyMailbox box;
+  box.cap = 1000;
+  box.push({0, std::string(800, 'a')});
+  std::atomic<bool> second_in{false};
+  std::thread reader([&] {
+    box.push({0, std::string(800, 'b')});  // 800 unread: still room
+    box.push({0, std::string(800, 'c')});  // 1600 unread: waits for a pop
+    second_in = true;
+  });
+  std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  EXPECT_TRUE(!second_in.load());
+  kube::SpdyMailbox::Event e;
+  EXPECT_TRUE(box.pop(&e, 1000) && e.data[0] == 'a');
+  EXPECT_TRUE(box.pop(&e, 1000) && e.data[0] == 'b');
+  reader.join();
+  EXPECT_TRUE(second_in.load());
+  // end events never wait for room; a closed mailbox drops data and ends pop()
+  box.push({0, "", true});
+  std::thread late([&] {
+    box.push({0, std::string(800, 'd')});
+    box.push({0, std::string(800, 'e')});  // over the cap: returns once the box is closed
+  });
+  std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  box.close();
+  late.join();
+  EXPECT_TRUE(!box.pop(&e, 10));
+}
+
 TEST(analyze_reports_a_long_step_holding_back_an_edit) {
   std::string up = "[devspace-runner] started gen=1 marker=v0\n";
   std::string held = up + "[devspace-runner] rank=0 in step for 75 s at train.py:42; edit pending: rank=0 is making "
