@@ -94,8 +94,36 @@ std::string select_container(const Value& pod, const std::string& preferred) {
 
 std::vector<std::unique_ptr<sync::Session>> start_sync(const Value& cfg, std::shared_ptr<kube::Client> k,
                                                         const SyncOptions& o) {
+  // every path's pod lookup and shells at the same time: on a remote cluster each path's start
+  // is a few round trips, and the paths are independent
+  const auto& paths = cfg.at_path("dev.sync").items();
+  std::vector<std::unique_ptr<sync::Session>> started(paths.size());
+  std::vector<std::string> errors(paths.size());
+  auto start_one = [&](size_t i) {
+    try {
+      started[i] = start_sync_path(cfg, paths[i], k, o);
+    } catch (const std::exception& e) {
+      errors[i] = e.what();
+    }
+  };
+  if (paths.size() == 1) {
+    start_one(0);
+  } else {
+    std::vector<std::thread> ts;
+    for (size_t i = 0; i < paths.size(); ++i) ts.emplace_back(start_one, i);
+    for (auto& t : ts) t.join();
+  }
+  for (auto& e : errors)
+    if (!e.empty()) throw std::runtime_error(e);  // (the started ones stop with `started`)
   std::vector<std::unique_ptr<sync::Session>> out;
-  for (auto& sp : cfg.at_path("dev.sync").items()) {
+  for (auto& s : started)
+    if (s) out.push_back(std::move(s));
+  return out;
+}
+
+std::unique_ptr<sync::Session> start_sync_path(const Value& cfg, const Value& sp, std::shared_ptr<kube::Client> k,
+                                               const SyncOptions& o) {
+  {
     std::string local = fs::abs_path(sp.get("localSubPath").as_string("./"));
     config::SelectorRef ref = config::resolve_selector(cfg, sp);
     std::string sel = ref.labels.to_query();
@@ -113,7 +141,7 @@ std::vector<std::unique_ptr<sync::Session>> start_sync(const Value& cfg, std::sh
       container = select_container(pod, ref.container);
     } catch (const std::exception& e) {
       log::warn(std::string("Couldn't start sync: ") + e.what());
-      continue;
+      return nullptr;
     }
     sync::Options so;
     so.watch_path = local;
@@ -147,9 +175,8 @@ std::vector<std::unique_ptr<sync::Session>> start_sync(const Value& cfg, std::sh
       throw std::runtime_error(std::string("Sync error: ") + e.what());
     }
     log::done("Sync started on " + local + " <-> " + so.dest_path + " (Pod: " + ns + "/" + so.pod_name + ")");
-    out.push_back(std::move(s));
+    return s;
   }
-  return out;
 }
 
 // ---------------------------------------------------------------- port forwarding

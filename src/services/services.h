@@ -39,8 +39,12 @@ struct SyncOptions {
   int poll_ms = 100;  // pod discovery poll (1000 = reference timing)
 };
 
+// Every dev.sync path, started concurrently; the first failure is thrown.
 std::vector<std::unique_ptr<sync::Session>> start_sync(const Value& cfg, std::shared_ptr<kube::Client> k,
                                                         const SyncOptions& o);
+// One dev.sync entry; nullptr when its container is not in the pod (a warning).
+std::unique_ptr<sync::Session> start_sync_path(const Value& cfg, const Value& sync_path,
+                                               std::shared_ptr<kube::Client> k, const SyncOptions& o);
 
 // Listen addresses (family, literal) for a port mapping's bindAddress ("" = localhost: both
 // 127.0.0.1 and ::1, like kubectl port-forward's default).
