@@ -357,9 +357,9 @@ bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out) {
   return line == "HELPER READY";
 }
 
-void Session::open_up_shell() {
+void Session::open_up_shell(std::unique_ptr<Shell> opened) {
   std::lock_guard<std::mutex> g(up_shell_mu_);
-  up_shell_ = transport_->open({"sh"});
+  up_shell_ = opened ? std::move(opened) : transport_->open({"sh"});
   up_out_.reset(up_shell_->out());
   up_helper_ = false;
   if (mode_ == Mode::Helper) {
@@ -400,23 +400,48 @@ void Session::open_down_shell() {
       down_shell_ = transport_->open({"sh"});
       down_out_.reset(down_shell_->out());
       down_err_.reset(down_shell_->err());
-    } else if (up_helper_) {
-      // The change watch runs in the upstream helper (the echo of its own writes is filtered
-      // where they are recorded, src/helper/helper.cc is_own), and only now that the downstream
-      // side is known to read its events (a watch whose stderr nobody drains fills the
-      // channel and stalls the exec stream that carries the upload replies).
-      std::lock_guard<std::mutex> ug(up_shell_mu_);
-      write_all(up_shell_->in(), request('W', ""));
-    } else {
-      // no upstream helper: container-side change events come from this one (no echo filter)
-      write_all(down_shell_->in(), request('W', ""));
     }
   }
 }
 
+void Session::request_watch() {
+  if (!down_helper_) return;  // the downstream side probes instead
+  if (up_helper_) {
+    // The change watch runs in the upstream helper (the echo of its own writes is filtered
+    // where they are recorded, src/helper/helper.cc is_own), and only now that the downstream
+    // side is known to read its events (a watch whose stderr nobody drains fills the
+    // channel and stalls the exec stream that carries the upload replies).
+    std::lock_guard<std::mutex> ug(up_shell_mu_);
+    write_all(up_shell_->in(), request('W', ""));
+  } else {
+    // no upstream helper: container-side change events come from this one (no echo filter)
+    std::lock_guard<std::mutex> dg(down_shell_mu_);
+    write_all(down_shell_->in(), request('W', ""));
+  }
+}
+
 void Session::open_shells() {
-  open_up_shell();
-  open_down_shell();
+  // The opens keep their order (upstream, then downstream: fault injection counts on it), and
+  // the upstream helper's start overlaps the downstream shell's open and helper start: on a
+  // remote cluster that is a round trip less before the sync runs.
+  std::unique_ptr<Shell> up = transport_->open({"sh"});
+  std::exception_ptr down_error;
+  std::thread down([this, &down_error] {
+    try {
+      open_down_shell();
+    } catch (...) {
+      down_error = std::current_exception();
+    }
+  });
+  try {
+    open_up_shell(std::move(up));
+  } catch (...) {
+    down.join();
+    throw;
+  }
+  down.join();
+  if (down_error) std::rethrow_exception(down_error);
+  request_watch();
 }
 
 // ============================================================ rules (evaluater.go)

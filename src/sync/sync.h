@@ -280,8 +280,11 @@ class Session {
 
   // shells / modes
   std::string remote(const std::string& container_path) const;  // apply transport prefix
-  void open_up_shell();
+  // `opened`: the shell, already opened (open_shells keeps the order of the opens)
+  void open_up_shell(std::unique_ptr<Shell> opened = nullptr);
   void open_down_shell();
+  // starts the container-side change watch in the helper that reports it
+  void request_watch();
   bool start_helper(std::unique_ptr<Shell>& sh, LineReader& out);
   void fail(const std::string& err);  // stream failure -> reconnect or stop
   void supervise();
