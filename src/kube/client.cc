@@ -837,9 +837,19 @@ static int64_t mono_ms_now() {
 void Client::prewarm_upgrades(int n) {
   if (n <= 0 || reference_timing()) return;  // the reference dials every stream
   std::lock_guard<std::mutex> g(warm_mu_);
+  // the dialers of earlier calls that finished (a dev session prewarms once per reload)
+  for (auto it = warm_threads_.begin(); it != warm_threads_.end();) {
+    if (it->second->load()) {
+      it->first.join();
+      it = warm_threads_.erase(it);
+    } else {
+      ++it;
+    }
+  }
   for (int i = 0; i < n; ++i) {
     ++warm_pending_;
-    warm_threads_.emplace_back([this] {
+    auto done = std::make_shared<std::atomic<bool>>(false);
+    std::thread t([this, done] {
       std::unique_ptr<net::Conn> c;
       try {
         c = http_.connect();
@@ -851,7 +861,9 @@ void Client::prewarm_upgrades(int n) {
         if (c) warm_.emplace_back(mono_ms_now(), std::move(c));
       }
       warm_cv_.notify_all();
+      *done = true;
     });
+    warm_threads_.emplace_back(std::move(t), done);
   }
 }
 
@@ -872,13 +884,13 @@ std::unique_ptr<net::Conn> Client::take_prewarmed() {
 }
 
 Client::~Client() {
-  std::vector<std::thread> ts;
+  std::vector<std::pair<std::thread, std::shared_ptr<std::atomic<bool>>>> ts;
   {
     std::lock_guard<std::mutex> g(warm_mu_);
     ts.swap(warm_threads_);
   }
   for (auto& t : ts)
-    if (t.joinable()) t.join();
+    if (t.first.joinable()) t.first.join();
 }
 
 std::unique_ptr<net::WebSocket> Client::ws_connect(const std::string& path, const std::vector<std::string>& protocols,

@@ -187,7 +187,7 @@ class Client {
   std::condition_variable warm_cv_;
   std::deque<std::pair<int64_t, std::unique_ptr<net::Conn>>> warm_;  // (dialed at ms, conn)
   int warm_pending_ = 0;
-  std::vector<std::thread> warm_threads_;
+  std::vector<std::pair<std::thread, std::shared_ptr<std::atomic<bool>>>> warm_threads_;  // (dialer, done)
   int local_cluster_ = -1;  // is_local_cluster() cache
   net::HttpClient http_;
   ApplyOptions apply_opts_;
