@@ -149,6 +149,9 @@ ENV = {
     "DEVSPACE_INIT_NO_NODE_DISCOVERY": "`devspace init` does not read the cluster's nodes to size GPU pods (per-GPU "
                                        "defaults are used).",
     "DEVSPACE_NONINTERACTIVE": "Never prompt: every question takes its default (CI); also skips the update check.",
+    "DEVSPACE_PORTFORWARD_HEDGE": "`0`: a held GET/HEAD/OPTIONS on a remote cluster is retried one stream at a time "
+                                  "(by default a new attempt goes out every third of a round trip; the app may see "
+                                  "the request up to about four times).",
     "DEVSPACE_PORTFORWARD_HOLD_MS": "How long a local connection is held while the pod refuses it (its app "
                                     "restarting) before it is dropped; default 3000, 0 drops at once as kubectl "
                                     "does.",

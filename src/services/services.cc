@@ -636,6 +636,151 @@ class PreOpened {
 // container, so the client's bytes can be replayed on a new stream.
 bool is_dial_refused(const std::string& err) { return contains(to_lower(err), "connection refused"); }
 
+namespace {
+// A stream whose first reply bytes were already read (the winner of hedged attempts).
+class PrimedFwd : public FwdStream {
+ public:
+  PrimedFwd(std::unique_ptr<FwdStream> in, std::string first) : in_(std::move(in)), first_(std::move(first)) {}
+  bool send(const std::string& data) override { return in_->send(data); }
+  bool recv(int* channel, std::string* data) override {
+    if (!given_) {
+      given_ = true;
+      *channel = 0;
+      *data = std::move(first_);
+      return true;
+    }
+    return in_->recv(channel, data);
+  }
+  void close_write() override { in_->close_write(); }
+  void close() override { in_->close(); }
+  const char* via() const override { return in_->via(); }
+
+ private:
+  std::unique_ptr<FwdStream> in_;
+  std::string first_;
+  bool given_ = false;
+};
+}  // namespace
+
+bool hedgeable_request(const std::string& bytes) {
+  if (!(starts_with(bytes, "GET ") || starts_with(bytes, "HEAD ") || starts_with(bytes, "OPTIONS "))) return false;
+  size_t end = bytes.find("\r\n\r\n");
+  if (end == std::string::npos || end + 4 != bytes.size()) return false;  // one whole request head, nothing after
+  std::string head = to_lower(bytes.substr(0, end));
+  return !contains(head, "\r\ncontent-length:") && !contains(head, "\r\ntransfer-encoding:");
+}
+
+bool port_forward_hedge() {
+  const char* v = std::getenv("DEVSPACE_PORTFORWARD_HEDGE");
+  return !(v && std::string(v) == "0") && !reference_timing();
+}
+
+// A held idempotent request on a slow link (the app restarting behind a remote API server):
+// instead of one attempt per round trip, a new attempt (a stream pair in the pod's tunnel with
+// the request) goes out every third of a round trip while earlier ones are in flight, so the
+// request reaches the new server within a few ms of it listening rather than up to a round trip
+// later. The first attempt answered wins; the others are reset. The app may see the request
+// more than once (up to about four times): only GET, HEAD and OPTIONS without a body are hedged,
+// which HTTP lets a client repeat (RFC 9110 §9.2.2). nullptr: no answer before `deadline_ms`, or
+// an attempt ended other than refused (the caller carries on one attempt at a time).
+std::unique_ptr<FwdStream> PortForwarder::hedge(int remote_port, const std::string& request, bool fin, int64_t rtt_us,
+                                                long deadline_ms, std::string* first) {
+  struct Attempt {
+    std::unique_ptr<FwdStream> s;
+    std::thread t;
+    int state = 0;  // 0 in flight, 1 refused, 2 answered, 3 ended otherwise
+    std::string data;
+    int64_t t_open = 0, t_end = 0;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::unique_ptr<Attempt>> attempts;
+  const long spacing = std::max(8L, std::min(25L, (long)(rtt_us / 3000)));
+  Attempt* winner = nullptr;
+  bool failed = false;
+  long next_open = mono_ms();
+  while (!stop_ && !winner && !failed && mono_ms() < deadline_ms) {
+    size_t in_flight = 0;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      for (auto& a : attempts) in_flight += a->state == 0;
+    }
+    if (mono_ms() >= next_open && in_flight < 8) {
+      auto a = std::make_unique<Attempt>();
+      a->t_open = trace::now_us();
+      try {
+        a->s = open_to(pod_name(), remote_port);
+      } catch (const std::exception&) {
+        break;
+      }
+      if (std::string(a->s->via()) != "tunnel" || !a->s->send(request)) {
+        a->s->close();
+        break;
+      }
+      if (fin) a->s->close_write();
+      Attempt* ap = a.get();
+      a->t = std::thread([ap, &mu, &cv] {
+        int ch = 0, st = 3;
+        std::string d;
+        while (ap->s->recv(&ch, &d)) {
+          if (ch == 0) {
+            st = 2;
+            break;
+          }
+          if (ch == 1 && !d.empty()) {
+            st = is_dial_refused(d) ? 1 : 3;
+            break;
+          }
+        }
+        {
+          std::lock_guard<std::mutex> g(mu);
+          ap->state = st;
+          ap->t_end = trace::now_us();
+          if (st == 2) ap->data = std::move(d);
+        }
+        cv.notify_all();
+      });
+      attempts.push_back(std::move(a));
+      held_retries_++;
+      next_open = mono_ms() + spacing;
+    }
+    std::unique_lock<std::mutex> lk(mu);
+    long wait = std::max(1L, std::min(next_open, deadline_ms) - mono_ms());
+    cv.wait_for(lk, std::chrono::milliseconds(wait), [&] {
+      for (auto& a : attempts)
+        if (a->state >= 2) return true;
+      return false;
+    });
+    for (auto& a : attempts) {
+      if (a->state == 2) {
+        winner = a.get();
+        break;
+      }
+      if (a->state == 3) failed = true;
+    }
+  }
+  for (auto& a : attempts)
+    if (a.get() != winner) a->s->close();  // a reply it may still get is dropped
+  for (auto& a : attempts)
+    if (a->t.joinable()) a->t.join();
+  if (trace::enabled()) {
+    int n = 0;
+    for (auto& a : attempts) {
+      static const char* kOutcome[] = {"abandoned", "refused", "reply", "closed"};
+      trace::emit("portforward.stream", a->t_open, (a->t_end ? a->t_end : trace::now_us()) - a->t_open,
+                  {{"port", std::to_string(remote_port)},
+                   {"attempt", "h" + std::to_string(n++)},
+                   {"first_us", a->t_end ? std::to_string(a->t_end - a->t_open) : std::string("-1")},
+                   {"outcome", a.get() == winner ? "reply" : kOutcome[a->state]},
+                   {"hedged", "1"},
+                   {"via", "tunnel"}});
+    }
+  }
+  if (!winner) return nullptr;
+  *first = std::move(winner->data);
+  return std::move(winner->s);
+}
+
 bool port_forward_preopen() {
   const char* v = std::getenv("DEVSPACE_PORTFORWARD_PREOPEN");
   return !(v && std::string(v) == "0");
@@ -663,8 +808,10 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
   bool client_eof = false;
   int attempt = 0;
   std::unique_ptr<PreOpened> next;
+  std::unique_ptr<FwdStream> hedged;  // the answered attempt of a hedged held request
   while (!stop_) {
-    std::unique_ptr<FwdStream> ws;
+    std::unique_ptr<FwdStream> ws = std::move(hedged);
+    const bool primed = ws != nullptr;  // its request went out with it
     // span per stream: open (the WebSocket upgrade, or a stream pair in the tunnel; the pod-side
     // dial happens with it) and the time until the first reply byte or the refusal
     // (trace.jsonl "portforward.stream")
@@ -694,8 +841,8 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
     if (preopen_ && !tunneled && attempt > 0 && replayable && !stop_ && mono_ms() - hold_start < 100)
       next = std::make_unique<PreOpened>([this, remote_port] { return open_stream_direct(remote_port); });
     std::atomic<int64_t> t_first{0};
-    if (!replay.empty() && !ws->send(replay)) break;
-    if (client_eof) ws->close_write();
+    if (!primed && !replay.empty() && !ws->send(replay)) break;
+    if (client_eof && !primed) ws->close_write();
     int wake[2];
     if (::pipe2(wake, O_CLOEXEC | O_NONBLOCK) != 0) break;
     std::atomic<bool> down_done{false}, got_reply{false}, refused{false};
@@ -773,6 +920,16 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
       // app, so a held connection is replayed there.
       if (replayable && mono_ms() < hold_deadline) {
         held_retries_++;
+        continue;
+      }
+    }
+    if (refused && replayable && !stop_ && mono_ms() < hold_deadline && tunneled && hedge_ &&
+        t_first.load() - t_open >= 10000 && hedgeable_request(replay)) {
+      // a remote cluster (the refusal took 10 ms or more) and a request HTTP lets a client repeat
+      std::string first;
+      auto win = hedge(remote_port, replay, client_eof, t_first.load() - t_open, hold_deadline, &first);
+      if (win) {
+        hedged = std::make_unique<PrimedFwd>(std::move(win), std::move(first));
         continue;
       }
     }

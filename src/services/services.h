@@ -57,6 +57,11 @@ int port_forward_hold_ms();
 // (DEVSPACE_PORTFORWARD_PREOPEN=0 turns it off).
 bool port_forward_preopen();
 bool is_dial_refused(const std::string& error_channel_message);
+// Whether a held connection on a slow link may be retried on several streams at once
+// (DEVSPACE_PORTFORWARD_HEDGE=0 turns it off), and whether its bytes so far are one request that
+// HTTP lets a client repeat: GET, HEAD or OPTIONS, the whole head and no body.
+bool port_forward_hedge();
+bool hedgeable_request(const std::string& bytes);
 
 class FwdStream;  // one forwarded connection's stream(s) (services.cc)
 
@@ -111,6 +116,8 @@ class PortForwarder {
   // A tunnel stream failed with an error before any reply: true when `pod` is gone, replaced
   // (same name, new uid) or finished, or was re-selected away from; its tunnel is then dropped.
   bool drop_tunnel_if_pod_gone(const std::string& pod);
+  std::unique_ptr<FwdStream> hedge(int remote_port, const std::string& request, bool fin, int64_t rtt_us,
+                                   long deadline_ms, std::string* first);
   std::shared_ptr<kube::Client> k_;
   std::mutex pod_mu_;
   Value pod_;
@@ -133,6 +140,7 @@ class PortForwarder {
   std::atomic<int> preopened_{0};
   int hold_ms_ = port_forward_hold_ms();
   bool preopen_ = port_forward_preopen();
+  bool hedge_ = port_forward_hedge();
   // the multiplexed tunnel (SPDY/3.1 over one WebSocket): -1 not tried, 0 unsupported, 1 in use
   std::atomic<int> tunnel_mode_{-1};
   std::mutex tunnel_mu_;

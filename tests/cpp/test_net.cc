@@ -280,6 +280,20 @@ TEST(resolver_dns_packets) {
 }
 
 // port-forward bindAddress "::1" / "::" must not silently become 127.0.0.1.
+// Only a request HTTP lets a client repeat is sent on several streams while the app restarts.
+TEST(port_forward_hedges_only_repeatable_requests) {
+  EXPECT_TRUE(services::hedgeable_request("GET / HTTP/1.1\r\nHost: x\r\n\r\n"));
+  EXPECT_TRUE(services::hedgeable_request("HEAD /a HTTP/1.1\r\nHost: x\r\n\r\n"));
+  EXPECT_TRUE(!services::hedgeable_request("POST / HTTP/1.1\r\nHost: x\r\nContent-Length: 1\r\n\r\nx"));
+  EXPECT_TRUE(!services::hedgeable_request("PUT / HTTP/1.1\r\nHost: x\r\n\r\n"));
+  // a GET with a body, a partial head, or a second request after the first: one stream at a time
+  EXPECT_TRUE(!services::hedgeable_request("GET / HTTP/1.1\r\nContent-Length: 2\r\n\r\n"));
+  EXPECT_TRUE(!services::hedgeable_request("GET / HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n"));
+  EXPECT_TRUE(!services::hedgeable_request("GET / HTTP/1.1\r\nHost: x\r\n"));
+  EXPECT_TRUE(!services::hedgeable_request("GET / HTTP/1.1\r\n\r\nGET /b HTTP/1.1\r\n\r\n"));
+  EXPECT_TRUE(!services::hedgeable_request("\x16\x03\x01 tls hello"));
+}
+
 TEST(port_forward_listen_addresses) {
   auto d = services::listen_addresses("");
   EXPECT_EQ(d.size(), (size_t)2);

@@ -1,0 +1,81 @@
+"""Port-forward of a request held across an app restart, with the cluster behind a slow link (40 ms
+RTT, devspace_amd/localkube/netem.py), as a laptop reaches a remote MI355X node.
+
+One attempt per round trip would make a request wait up to a whole round trip after the new
+server listens. So a held GET (repeatable, RFC 9110 §9.2.2) goes out on a new stream pair of the
+pod's tunnel every quarter round trip while earlier attempts are in flight; the first answer wins.
+A POST still goes out on one stream at a time and reaches the app exactly once.
+"""
+import json
+import os
+import urllib.request
+
+import yaml
+
+from conftest import DevspaceEnv
+from test_e2e_cli import running, wait_for
+from test_e2e_services import _refused, _restart_project, _stop
+
+
+def test_a_held_get_is_hedged_and_a_held_post_is_sent_once(tmp_path):
+    from devspace_amd.localkube import LocalCluster
+    from devspace_amd.localkube.netem import ShapedLink, point_kubeconfig
+
+    cluster = LocalCluster(str(tmp_path / "state"), gpus=0, tls=True).start()
+    link = None
+    try:
+        lk = DevspaceEnv(cluster, str(tmp_path))
+        link = ShapedLink(("127.0.0.1", cluster.port), rtt_ms=40, mbit=100).start()
+        point_kubeconfig(lk.kubeconfig, cluster.server, link.url("https"))
+        proj, remote, local = _restart_project(lk, "qs-wan-hold", "pf-wan")
+        hits = tmp_path / "hits.log"
+        values = os.path.join(proj, "chart", "values.yaml")
+        v = yaml.safe_load(open(values))
+        v["components"][0]["containers"][0]["env"].append({"name": "HITS_FILE", "value": str(hits)})
+        open(values, "w").write(yaml.safe_dump(v))
+        index = os.path.join(proj, "index.js")
+        src = open(index).read().replace(
+            "http.createServer((req, res) => {",
+            "http.createServer((req, res) => {\n  require('fs').appendFileSync(process.env.HITS_FILE, req.method + ' ' + "
+            "req.url + '\\n');", 1)
+        open(index, "w").write(src)
+        dev = lk.popen(["dev", "--terminal=false"], proj)
+        try:
+            wait_for(lambda: (lambda b: b.startswith("Hello") if b else False)(_fetch(local)), timeout=90,
+                     what="forwarded server")
+            root = json.loads(running(lk.pods("pf-wan"))[0]["metadata"]["annotations"]["devspace.sh/local-roots"])
+            pod_index = os.path.join(list(root.values())[0], "app", "index.js")
+            for i in range(4):
+                with open(index, "a") as f:
+                    f.write(f"// edit {i}\n")
+                wait_for(lambda: f"// edit {i}" in open(pod_index).read(), timeout=30, what="synced edit")
+                wait_for(lambda: _refused(remote), timeout=10, what="old server stopped")
+                method = "GET" if i % 2 == 0 else "POST"
+                req = urllib.request.Request(f"http://127.0.0.1:{local}/held-{i}",
+                                             data=b"x" if method == "POST" else None, method=method)
+                body = urllib.request.urlopen(req, timeout=15).read().decode()
+                assert body.startswith("Hello"), body
+                wait_for(lambda: not _refused(remote), timeout=30, what="new server")
+        finally:
+            _stop(dev)
+        lines = hits.read_text().splitlines()
+        for i in (1, 3):
+            assert lines.count(f"POST /held-{i}") == 1, lines
+        for i in (0, 2):
+            assert 1 <= lines.count(f"GET /held-{i}") <= 8, lines
+        spans = [json.loads(l) for l in open(os.path.join(proj, ".devspace", "logs", "trace.jsonl"))
+                 if '"portforward.stream"' in l]
+        hedged = [s for s in spans if s.get("hedged") == "1"]
+        assert any(s["outcome"] == "reply" for s in hedged), spans
+        assert all(s.get("via") == "tunnel" for s in spans), spans
+    finally:
+        if link is not None:
+            link.stop()
+        cluster.stop()
+
+
+def _fetch(port):
+    try:
+        return urllib.request.urlopen(f"http://127.0.0.1:{port}/", timeout=5).read().decode()
+    except Exception:
+        return None
