@@ -820,7 +820,7 @@ def main():
                                                         reference=True))
                 # the same loops with the cluster 30 ms / 100 Mbit/s away (a laptop and a cloud
                 # cluster): round trips per edit and per connection, not loopback, decide here
-                extra("qs_wan", lambda: quickstart_loop(workdir, max(args.ref_steps, 5), 1, tls=tls, cold=True, wan=WAN))
+                extra("qs_wan", lambda: quickstart_loop(workdir, max(args.ref_steps, 10), 1, tls=tls, cold=True, wan=WAN))
                 extra("qs_wan_ref", lambda: quickstart_loop(workdir, args.ref_steps, 1, sync_mode="compat", tls=tls,
                                                             reference=True, wan=WAN))
                 if not args.no_deploy_bench:
