@@ -667,7 +667,10 @@ bool hedgeable_request(const std::string& bytes) {
   size_t end = bytes.find("\r\n\r\n");
   if (end == std::string::npos || end + 4 != bytes.size()) return false;  // one whole request head, nothing after
   std::string head = to_lower(bytes.substr(0, end));
-  return !contains(head, "\r\ncontent-length:") && !contains(head, "\r\ntransfer-encoding:");
+  // a body, or an upgrade (a WebSocket, e.g. a dev server's hot-reload socket): a session on the
+  // server, not a request to repeat
+  return !contains(head, "\r\ncontent-length:") && !contains(head, "\r\ntransfer-encoding:") &&
+         !contains(head, "\r\nupgrade:");
 }
 
 bool port_forward_hedge() {

@@ -292,6 +292,9 @@ TEST(port_forward_hedges_only_repeatable_requests) {
   EXPECT_TRUE(!services::hedgeable_request("GET / HTTP/1.1\r\nHost: x\r\n"));
   EXPECT_TRUE(!services::hedgeable_request("GET / HTTP/1.1\r\n\r\nGET /b HTTP/1.1\r\n\r\n"));
   EXPECT_TRUE(!services::hedgeable_request("\x16\x03\x01 tls hello"));
+  // a WebSocket handshake opens a session (a dev server's hot-reload socket)
+  EXPECT_TRUE(!services::hedgeable_request("GET /ws HTTP/1.1\r\nHost: x\r\nConnection: Upgrade\r\n"
+                                           "Upgrade: websocket\r\n\r\n"));
 }
 
 TEST(port_forward_listen_addresses) {
