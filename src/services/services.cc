@@ -701,7 +701,8 @@ std::unique_ptr<FwdStream> PortForwarder::hedge(int remote_port, const std::stri
   const long spacing = std::max(8L, std::min(25L, (long)(rtt_us / 3000)));
   Attempt* winner = nullptr;
   bool failed = false;
-  long next_open = mono_ms();
+  const long started = mono_ms();
+  long next_open = started;
   while (!stop_ && !winner && !failed && mono_ms() < deadline_ms) {
     size_t in_flight = 0;
     {
@@ -745,7 +746,8 @@ std::unique_ptr<FwdStream> PortForwarder::hedge(int remote_port, const std::stri
       });
       attempts.push_back(std::move(a));
       held_retries_++;
-      next_open = mono_ms() + spacing;
+      // an app that takes more than a second to come back is not waited on this closely
+      next_open = mono_ms() + (mono_ms() - started < 1000 ? spacing : std::max(spacing, 50L));
     }
     std::unique_lock<std::mutex> lk(mu);
     long wait = std::max(1L, std::min(next_open, deadline_ms) - mono_ms());
