@@ -322,9 +322,26 @@ std::string helper_probe_script(const std::string& file, const std::vector<std::
          "; elif [ -n \"$dsd\" ]; then echo \"NEED $dsd\"; else echo NOHELPER; fi\n";
 }
 
-bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out) {
+bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out, HelperRole role) {
   // Probe architecture + a writable directory that allows exec, upload the static helper once
   // (content-addressed), then exec it in place of the shell.
+  // The uploader tells a waiting shell whether the helper is in the container (on every return
+  // before that is known: it is not)
+  struct Announce {
+    Session* s;
+    bool on;
+    int state = 2;
+    void set(int st) {
+      if (!on) return;
+      on = false;
+      {
+        std::lock_guard<std::mutex> g(s->helper_mu_);
+        s->helper_state_ = st;
+      }
+      s->helper_cv_.notify_all();
+    }
+    ~Announce() { set(2); }
+  } announce{this, role == kUploader};
   if (o_.helper_path.empty() || !fs::is_file(o_.helper_path)) return false;
   std::string bin;
   if (!fs::read_file(o_.helper_path, &bin)) return false;
@@ -341,16 +358,26 @@ bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out) {
     logf("[Sync] No directory in the container can hold and run the helper (" + line + ")");
     return false;
   }
+  if (starts_with(line, "HAVE ")) announce.set(1);
   if (starts_with(line, "NEED ")) {
     std::string name = shell_quote(line.substr(5) + "/" + file);
-    // a temporary name per shell: the sync's shells may upload at the same time
-    std::string tmp = shell_quote(line.substr(5) + "/" + file) + ".tmp.$$";
-    std::string up = "echo " + std::string(kStart) + "; head -c " + std::to_string(bin.size()) + " > " + tmp +
-                     " && chmod +x " + tmp + " && mv " + tmp + " " + name + "; echo " + kDone + "\n";
-    if (!write_all(sh->in(), up)) return false;
-    if (!out.wait_for(kStart, 15000)) return false;
-    if (!write_all(sh->in(), bin)) return false;
-    if (!out.wait_for(kDone, 30000)) return false;
+    bool there = false;
+    if (role == kWaiter) {  // the other shell is uploading it: wait for that, not the bytes again
+      std::unique_lock<std::mutex> lk(helper_mu_);
+      helper_cv_.wait_for(lk, std::chrono::seconds(60), [this] { return helper_state_ != 0; });
+      there = helper_state_ == 1;
+    }
+    if (!there) {
+      // a temporary name per shell: shells may upload at the same time
+      std::string tmp = shell_quote(line.substr(5) + "/" + file) + ".tmp.$$";
+      std::string up = "echo " + std::string(kStart) + "; head -c " + std::to_string(bin.size()) + " > " + tmp +
+                       " && chmod +x " + tmp + " && mv " + tmp + " " + name + "; echo " + kDone + "\n";
+      if (!write_all(sh->in(), up)) return false;
+      if (!out.wait_for(kStart, 15000)) return false;
+      if (!write_all(sh->in(), bin)) return false;
+      if (!out.wait_for(kDone, 30000)) return false;
+      announce.set(1);
+    }
     if (!write_all(sh->in(), start(name) + "\n")) return false;
   }
   if (!out.read_line(&line, 15000)) return false;
@@ -363,7 +390,7 @@ void Session::open_up_shell(std::unique_ptr<Shell> opened) {
   up_out_.reset(up_shell_->out());
   up_helper_ = false;
   if (mode_ == Mode::Helper) {
-    up_helper_ = start_helper(up_shell_, up_out_);
+    up_helper_ = start_helper(up_shell_, up_out_, concurrent_open_ ? kUploader : kAlone);
     if (!up_helper_) {
       logf("[Sync] Helper unavailable, falling back to fast POSIX protocol");
       up_shell_->close();
@@ -394,7 +421,7 @@ void Session::open_down_shell() {
   down_err_.reset(down_shell_->err());
   down_helper_ = false;
   if (mode_ == Mode::Helper) {
-    down_helper_ = start_helper(down_shell_, down_out_);
+    down_helper_ = start_helper(down_shell_, down_out_, concurrent_open_ ? kWaiter : kAlone);
     if (!down_helper_) {
       down_shell_->close();
       down_shell_ = transport_->open({"sh"});
@@ -425,6 +452,15 @@ void Session::open_shells() {
   // the upstream helper's start overlaps the downstream shell's open and helper start: on a
   // remote cluster that is a round trip less before the sync runs.
   std::unique_ptr<Shell> up = transport_->open({"sh"});
+  {
+    std::lock_guard<std::mutex> g(helper_mu_);
+    helper_state_ = 0;
+  }
+  concurrent_open_ = true;
+  struct Reset {
+    bool& f;
+    ~Reset() { f = false; }
+  } reset{concurrent_open_};
   std::exception_ptr down_error;
   std::thread down([this, &down_error] {
     try {

@@ -285,7 +285,14 @@ class Session {
   void open_down_shell();
   // starts the container-side change watch in the helper that reports it
   void request_watch();
-  bool start_helper(std::unique_ptr<Shell>& sh, LineReader& out);
+  // role: kUploader uploads a missing helper and says when it is there, kWaiter (a shell opened
+  // at the same time) waits for that instead of uploading the same bytes again, kAlone does both
+  enum HelperRole { kAlone, kUploader, kWaiter };
+  bool start_helper(std::unique_ptr<Shell>& sh, LineReader& out, HelperRole role = kAlone);
+  std::mutex helper_mu_;
+  std::condition_variable helper_cv_;
+  int helper_state_ = 0;  // the uploader's helper: 0 not known yet, 1 in the container, 2 failed
+  bool concurrent_open_ = false;  // open_shells is opening both shells (written before its thread starts)
   void fail(const std::string& err);  // stream failure -> reconnect or stop
   void supervise();
 
