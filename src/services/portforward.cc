@@ -1,0 +1,855 @@
+// Port forwarding (services/port_forwarding.go:18, kubectl/client.go:356): local listeners, one
+// multiplexed tunnel per pod (or a WebSocket per connection), held connections replayed across
+// an app restart, hedged retries of repeatable requests on a remote cluster.
+#include "services/services.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+
+#include "core/compat.h"
+#include "core/log.h"
+#include "core/resolve.h"
+#include "core/strutil.h"
+#include "core/trace.h"
+
+namespace ds {
+namespace services {
+
+static long mono_ms() {
+  return (long)std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// ---------------------------------------------------------------- port forwarding
+
+PortForwarder::PortForwarder(std::shared_ptr<kube::Client> k, Value pod, std::vector<std::pair<int, int>> ports,
+                             std::vector<std::string> addresses, std::string label_selector)
+    : k_(std::move(k)), pod_(std::move(pod)), selector_(std::move(label_selector)), ports_(std::move(ports)),
+      addrs_(std::move(addresses)) {
+  ns_ = pod_.at_path("metadata.namespace").as_string();
+}
+
+PortForwarder::~PortForwarder() { close(); }
+
+std::string PortForwarder::describe() const {
+  std::vector<std::string> p;
+  for (auto& pr : ports_) p.push_back(std::to_string(pr.first) + ":" + std::to_string(pr.second));
+  return join(p, ", ");
+}
+
+std::string PortForwarder::pod_name() {
+  std::lock_guard<std::mutex> g(pod_mu_);
+  return pod_.at_path("metadata.name").as_string();
+}
+
+size_t PortForwarder::active_connections() {
+  std::lock_guard<std::mutex> g(conns_mu_);
+  size_t n = 0;
+  for (auto& c : conns_) n += !c->done;
+  return n;
+}
+
+// Listen addresses for one mapping's bindAddress, as `kubectl port-forward --address` reads
+// them: "localhost" (the default) is 127.0.0.1 plus ::1, an IPv6 literal ("::1", "[::1]", "::")
+// binds an AF_INET6 socket, a host name goes through the resolver. Returns (family, address).
+std::vector<std::pair<int, std::string>> listen_addresses(const std::string& bind) {
+  std::string a = bind.empty() ? "localhost" : bind;
+  if (a.size() > 2 && a.front() == '[' && a.back() == ']') a = a.substr(1, a.size() - 2);
+  if (to_lower(a) == "localhost") return {{AF_INET, "127.0.0.1"}, {AF_INET6, "::1"}};
+  struct in_addr v4;
+  struct in6_addr v6;
+  if (inet_pton(AF_INET, a.c_str(), &v4) == 1) return {{AF_INET, a}};
+  if (inet_pton(AF_INET6, a.c_str(), &v6) == 1) return {{AF_INET6, a}};
+  std::vector<std::pair<int, std::string>> out;
+  for (auto& r : net::resolve(a, 0)) out.push_back({r.family, r.text});
+  if (out.empty()) throw std::runtime_error("Unable to resolve port-forward address \"" + bind + "\"");
+  return out;
+}
+
+// One listening socket or -errno. "::" is dual-stack (also takes IPv4), every other IPv6
+// address is v6-only so it can sit next to the IPv4 listener on the same port.
+static int listen_on(int family, const std::string& addr, int port) {
+  int fd = ::socket(family, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) return -errno;
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  struct sockaddr_storage ss{};
+  socklen_t len;
+  if (family == AF_INET6) {
+    auto* a6 = (struct sockaddr_in6*)&ss;
+    a6->sin6_family = AF_INET6;
+    a6->sin6_port = htons((uint16_t)port);
+    inet_pton(AF_INET6, addr.c_str(), &a6->sin6_addr);
+    int v6only = addr == "::" ? 0 : 1;
+    setsockopt(fd, IPPROTO_IPV6, IPV6_V6ONLY, &v6only, sizeof(v6only));
+    len = sizeof(*a6);
+  } else {
+    auto* a4 = (struct sockaddr_in*)&ss;
+    a4->sin_family = AF_INET;
+    a4->sin_port = htons((uint16_t)port);
+    inet_pton(AF_INET, addr.c_str(), &a4->sin_addr);
+    len = sizeof(*a4);
+  }
+  if (::bind(fd, (struct sockaddr*)&ss, len) != 0 || ::listen(fd, 64) != 0) {
+    int err = errno;
+    ::close(fd);
+    return -err;
+  }
+  return fd;
+}
+
+// One forwarded connection's stream(s), as the connection handler sees them.
+class FwdStream {
+ public:
+  virtual ~FwdStream() = default;
+  // client -> pod bytes
+  virtual bool send(const std::string& data) = 0;
+  // The next event: channel 0 bytes from the pod, channel 1 an error message. false at the end.
+  virtual bool recv(int* channel, std::string* data) = 0;
+  // the client finished sending (a tunnel stream half-closes; a WebSocket cannot)
+  virtual void close_write() {}
+  virtual void close() = 0;
+  virtual const char* via() const = 0;
+};
+
+namespace {
+
+// portforward.k8s.io over a WebSocket of its own: channel byte 0 data / 1 error, and each
+// channel's first frame carries the port number (2 bytes LE).
+class WsFwd : public FwdStream {
+ public:
+  explicit WsFwd(std::unique_ptr<net::WebSocket> ws) : ws_(std::move(ws)) {}
+  bool send(const std::string& data) override { return ws_->send(std::string(1, '\0') + data); }
+  bool recv(int* channel, std::string* data) override {
+    std::string msg;
+    while (ws_->recv(&msg)) {
+      if (msg.empty()) continue;
+      int ch = (unsigned char)msg[0];
+      std::string d = msg.substr(1);
+      if (ch == 0 && first_data_) {
+        first_data_ = false;
+        if (d.size() == 2) continue;
+      }
+      if (ch == 1 && first_err_) {
+        first_err_ = false;
+        if (d.size() == 2) continue;
+      }
+      *channel = ch;
+      *data = std::move(d);
+      return true;
+    }
+    return false;
+  }
+  void close() override { ws_->close(); }
+  const char* via() const override { return "websocket"; }
+
+ private:
+  std::unique_ptr<net::WebSocket> ws_;
+  bool first_data_ = true, first_err_ = true;
+};
+
+// A stream pair in the pod's tunnel, as kubectl creates it: an error stream (the client never
+// writes to it) and a data stream, tied by a request id. The data follows the SYN_STREAM at once.
+class TunnelFwd : public FwdStream {
+ public:
+  TunnelFwd(std::shared_ptr<kube::SpdySession> s, int port, uint64_t request_id) : s_(std::move(s)) {
+    std::string p = std::to_string(port), id = std::to_string(request_id);
+    err_ = s_->open({{"streamtype", "error"}, {"port", p}, {"requestid", id}}, box_, 1, true);
+    data_ = s_->open({{"streamtype", "data"}, {"port", p}, {"requestid", id}}, box_, 0);
+  }
+  ~TunnelFwd() override { close(); }
+  bool send(const std::string& data) override { return s_->send(data_, data); }
+  bool recv(int* channel, std::string* data) override {
+    kube::SpdyMailbox::Event e;
+    while (!data_done_ && box_->pop(&e)) {
+      if (e.end) {
+        if (e.channel == 0) data_done_ = true;
+        continue;
+      }
+      if (e.channel == 0) s_->consumed(data_, e.data.size());
+      *channel = e.channel;
+      *data = std::move(e.data);
+      return true;
+    }
+    return false;
+  }
+  void close_write() override { s_->send(data_, "", true); }
+  void close() override {
+    if (closed_) return;
+    closed_ = true;
+    // abandoned (stop, a failed client write): the server stops forwarding; a recv() still
+    // waiting in another thread returns, and the session's reader never blocks on this mailbox
+    s_->reset(data_);
+    s_->reset(err_);
+    box_->close();
+  }
+  const char* via() const override { return "tunnel"; }
+
+ private:
+  std::shared_ptr<kube::SpdySession> s_;
+  std::shared_ptr<kube::SpdyMailbox> box_ = std::make_shared<kube::SpdyMailbox>();
+  std::shared_ptr<kube::SpdySession::Stream> err_, data_;
+  bool data_done_ = false, closed_ = false;
+};
+
+bool port_forward_tunnel_enabled() {
+  const char* v = std::getenv("DEVSPACE_PORTFORWARD_TUNNEL");
+  return !(v && std::string(v) == "0") && !reference_timing();  // the reference dials per stream
+}
+
+}  // namespace
+
+std::shared_ptr<kube::SpdySession> PortForwarder::tunnel_for(const std::string& pod) {
+  if (tunnel_mode_ == 0) return nullptr;
+  std::lock_guard<std::mutex> g(tunnel_mu_);
+  if (tunnel_ && tunnel_pod_ == pod && tunnel_->usable()) return tunnel_;
+  if (tunnel_) {
+    tunnel_->close();
+    tunnel_.reset();
+  }
+  std::vector<int> remote;
+  for (auto& pr : ports_) remote.push_back(pr.second);
+  auto t = k_->portforward_tunnel(ns_, pod, remote);  // throws when the pod is gone
+  if (!t) {
+    tunnel_mode_ = 0;
+    log::file_logger("portforwarding")->emit("info", "The API server has no multiplexed port-forward "
+                                             "(SPDY/3.1+portforward.k8s.io): one WebSocket per connection", {});
+    return nullptr;
+  }
+  tunnel_mode_ = 1;
+  tunnels_opened_++;
+  tunnel_ = t;
+  tunnel_pod_ = pod;
+  tunnel_requests_ = 0;
+  return t;
+}
+
+bool PortForwarder::drop_tunnel_if_pod_gone(const std::string& pod) {
+  std::string uid;
+  {
+    std::lock_guard<std::mutex> g(pod_mu_);
+    // re-selected meanwhile: the next stream goes to the new pod's tunnel
+    if (pod_.at_path("metadata.name").as_string() != pod) return true;
+    uid = pod_.at_path("metadata.uid").as_string();
+  }
+  std::optional<Value> live;
+  try {
+    live = k_->try_get("/api/v1/namespaces/" + ns_ + "/pods/" + pod);
+  } catch (const std::exception&) {
+    return false;  // cannot tell (API server unreachable): keep the tunnel
+  }
+  if (live) {
+    const std::string phase = live->at_path("status.phase").as_string();
+    const std::string live_uid = live->at_path("metadata.uid").as_string();
+    if (phase != "Succeeded" && phase != "Failed" && live_uid == uid) return false;
+    if (live_uid != uid && phase == "Running") {
+      // the same name, a new pod (a StatefulSet's replacement): forward to it
+      std::lock_guard<std::mutex> g(pod_mu_);
+      if (pod_.at_path("metadata.name").as_string() == pod) pod_ = *live;
+      reselections_++;
+      log::info("Port forwarding " + describe() + " now targets pod " + pod + " (replaced)");
+    }
+  }
+  std::lock_guard<std::mutex> g(tunnel_mu_);
+  if (tunnel_ && tunnel_pod_ == pod) {
+    tunnel_->close();
+    tunnel_.reset();
+  }
+  return true;
+}
+
+std::unique_ptr<FwdStream> PortForwarder::open_to(const std::string& pod, int remote_port) {
+  for (int tries = 0; tries < 2 && tunnel_mode_ != 0; ++tries) {
+    auto t = tunnel_for(pod);
+    if (!t) break;
+    try {
+      return std::make_unique<TunnelFwd>(t, remote_port, tunnel_requests_++);
+    } catch (const net::NetError&) {
+      // the tunnel just closed (API server restart, idle timeout): a new one
+    }
+  }
+  return std::make_unique<WsFwd>(k_->portforward(ns_, pod, remote_port, take_spare()));
+}
+
+void PortForwarder::spare_loop() {
+  const long kMaxAgeMs = 30000;  // below API-server idle timeouts; re-dialed after that
+  std::unique_lock<std::mutex> lk(spare_mu_);
+  while (!stop_) {
+    if (tunnel_mode_ != 0 && port_forward_tunnel_enabled()) {
+      // keep the pod's tunnel open (re-opened after the API server closed it), so the first
+      // connection after a quiet spell does not pay the upgrade either
+      lk.unlock();
+      try {
+        tunnel_for(pod_name());
+      } catch (const std::exception&) {
+      }
+      lk.lock();
+      if (tunnel_mode_ == 1) {
+        spares_.clear();
+        spare_cv_.wait_for(lk, std::chrono::seconds(1), [this] { return stop_.load(); });
+        continue;
+      }
+    }
+    while (!spares_.empty() && mono_ms() - spares_.front().first > kMaxAgeMs) spares_.pop_front();
+    if ((int)spares_.size() < want_spares_) {
+      lk.unlock();
+      std::unique_ptr<net::Conn> c;
+      try {
+        c = k_->http().connect();
+      } catch (const std::exception&) {
+      }
+      lk.lock();
+      if (c) {
+        spares_.emplace_back(mono_ms(), std::move(c));
+      } else {
+        spare_cv_.wait_for(lk, std::chrono::seconds(1), [this] { return stop_.load(); });
+      }
+      continue;
+    }
+    spare_cv_.wait_for(lk, std::chrono::seconds(5),
+                       [this] { return stop_.load() || (int)spares_.size() < want_spares_; });
+  }
+  spares_.clear();
+}
+
+std::unique_ptr<net::Conn> PortForwarder::take_spare() {
+  std::unique_ptr<net::Conn> c;
+  {
+    std::lock_guard<std::mutex> g(spare_mu_);
+    while (!spares_.empty() && !c) {
+      c = std::move(spares_.front().second);
+      spares_.pop_front();
+      if (c->stale()) c.reset();
+    }
+  }
+  spare_cv_.notify_one();
+  if (c) spares_used_++;
+  return c;
+}
+
+void PortForwarder::start() {
+  if (const char* v = std::getenv("DEVSPACE_PORTFORWARD_SPARES")) {
+    want_spares_ = std::max(0, std::min(8, std::atoi(v)));
+  } else {
+    want_spares_ = reference_timing() ? 0 : 2;  // the reference dials every stream
+  }
+  if (!port_forward_tunnel_enabled()) tunnel_mode_ = 0;
+  if (want_spares_ > 0 || tunnel_mode_ != 0) spare_thread_ = std::thread([this] { spare_loop(); });
+  for (size_t i = 0; i < ports_.size(); ++i) {
+    std::string bind = i < addrs_.size() ? addrs_[i] : "";
+    auto addrs = listen_addresses(bind);
+    bool is_default = addrs.size() == 2 && addrs[0].second == "127.0.0.1" && addrs[1].second == "::1";
+    int bound = 0;
+    int first_err = 0;
+    for (size_t k = 0; k < addrs.size(); ++k) {
+      int fd = listen_on(addrs[k].first, addrs[k].second, ports_[i].first);
+      if (fd < 0) {
+        // kubectl tolerates one of localhost's two families failing (a host without IPv6)
+        if (is_default && k == 1 && bound > 0) continue;
+        if (!first_err) first_err = -fd;
+        continue;
+      }
+      listeners_.push_back(fd);
+      ++bound;
+      int rp = ports_[i].second;
+      threads_.emplace_back([this, fd, rp] { accept_loop(fd, rp); });
+    }
+    if (bound == (int)addrs.size() || (is_default && bound > 0)) continue;
+    // Pods of the bundled local cluster share the host network: a same-number mapping is
+    // already served by the container itself.
+    if (bound == 0 && first_err == EADDRINUSE && k_->is_local_cluster() && ports_[i].first == ports_[i].second) {
+      log::info("Port " + std::to_string(ports_[i].first) +
+                " is served directly by the pod (local cluster shares the host network)");
+      continue;
+    }
+    throw std::runtime_error("Unable to listen on " + (bind.empty() ? std::string("localhost") : bind) + ":" +
+                             std::to_string(ports_[i].first) + ": " + std::strerror(first_err));
+  }
+}
+
+void PortForwarder::reap(bool all) {
+  std::vector<std::unique_ptr<Conn>> finished;
+  {
+    std::lock_guard<std::mutex> g(conns_mu_);
+    for (auto it = conns_.begin(); it != conns_.end();) {
+      if (all || (*it)->done) {
+        finished.push_back(std::move(*it));
+        it = conns_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  for (auto& c : finished)
+    if (c->t.joinable()) c->t.join();
+}
+
+void PortForwarder::accept_loop(int lfd, int remote_port) {
+  while (!stop_) {
+    reap(false);
+    struct pollfd pf{lfd, POLLIN, 0};
+    if (::poll(&pf, 1, 200) <= 0) continue;
+    int cfd = ::accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
+    if (cfd < 0) continue;
+    auto c = std::make_unique<Conn>();
+    c->fd = cfd;
+    Conn* raw = c.get();
+    std::lock_guard<std::mutex> g(conns_mu_);
+    if (stop_) {
+      ::close(cfd);
+      break;
+    }
+    conns_.push_back(std::move(c));
+    raw->t = std::thread([this, raw, remote_port] { handle(raw, remote_port); });
+  }
+}
+
+std::unique_ptr<FwdStream> PortForwarder::open_stream(int remote_port) {
+  Value pod;
+  {
+    std::lock_guard<std::mutex> g(pod_mu_);
+    pod = pod_;
+  }
+  std::string name = pod.at_path("metadata.name").as_string();
+  try {
+    return open_to(name, remote_port);
+  } catch (const std::exception& e) {
+    if (selector_.empty() || stop_) throw;
+    // the pod is gone or not running any more: follow the selector to its newest pod
+    Value fresh = k_->newest_running_pod(ns_, selector_, 60000);
+    std::string fresh_name = fresh.at_path("metadata.name").as_string();
+    if (fresh_name == name) throw;
+    {
+      std::lock_guard<std::mutex> g(pod_mu_);
+      pod_ = fresh;
+    }
+    reselections_++;
+    log::file_logger("portforwarding")->emit("info", "Pod " + name + " is gone (" + e.what() +
+                                             "), forwarding to " + fresh_name, {});
+    log::info("Port forwarding " + describe() + " now targets pod " + fresh_name);
+    return open_to(fresh_name, remote_port);
+  }
+}
+
+std::unique_ptr<FwdStream> PortForwarder::open_stream_direct(int remote_port) {
+  return open_to(pod_name(), remote_port);
+}
+
+namespace {
+// The next attempt of a held connection, opened on its own thread while the current attempt
+// waits for its reply or refusal. Opening a stream is the bulk of an attempt (the WebSocket
+// upgrade through the API server, and the pod-side dial that comes with it), so overlapping
+// it with the wait roughly halves the retry period. Only one stream of a connection ever
+// carries the client's bytes at a time: the next one gets them only after this one was
+// refused, so a request still reaches the app at most once.
+class PreOpened {
+ public:
+  template <class F>
+  explicit PreOpened(F open) : t_([this, open] {
+      try {
+        ws_ = open();
+      } catch (const std::exception&) {
+        ws_.reset();  // the caller falls back to a synchronous open (with pod re-selection)
+      }
+      done_ = true;
+    }) {}
+  // the open finished: take() / discard() will not block
+  bool ready() const { return done_; }
+  ~PreOpened() { discard(); }
+  std::unique_ptr<FwdStream> take() {
+    if (t_.joinable()) t_.join();
+    return std::move(ws_);
+  }
+  void discard() {
+    auto ws = take();
+    if (ws) ws->close();
+  }
+
+ private:
+  std::unique_ptr<FwdStream> ws_;
+  std::atomic<bool> done_{false};
+  std::thread t_;  // declared last: the thread starts once ws_ and done_ exist
+};
+}  // namespace
+
+// True for the error-channel message of a stream whose pod-side connect failed (kubelet /
+// CRI: "... dial tcp4 127.0.0.1:8080: connect: connection refused"): nothing reached the
+// container, so the client's bytes can be replayed on a new stream.
+bool is_dial_refused(const std::string& err) { return contains(to_lower(err), "connection refused"); }
+
+namespace {
+// A stream whose first reply bytes were already read (the winner of hedged attempts).
+class PrimedFwd : public FwdStream {
+ public:
+  PrimedFwd(std::unique_ptr<FwdStream> in, std::string first) : in_(std::move(in)), first_(std::move(first)) {}
+  bool send(const std::string& data) override { return in_->send(data); }
+  bool recv(int* channel, std::string* data) override {
+    if (!given_) {
+      given_ = true;
+      *channel = 0;
+      *data = std::move(first_);
+      return true;
+    }
+    return in_->recv(channel, data);
+  }
+  void close_write() override { in_->close_write(); }
+  void close() override { in_->close(); }
+  const char* via() const override { return in_->via(); }
+
+ private:
+  std::unique_ptr<FwdStream> in_;
+  std::string first_;
+  bool given_ = false;
+};
+}  // namespace
+
+bool hedgeable_request(const std::string& bytes) {
+  if (!(starts_with(bytes, "GET ") || starts_with(bytes, "HEAD ") || starts_with(bytes, "OPTIONS "))) return false;
+  size_t end = bytes.find("\r\n\r\n");
+  if (end == std::string::npos || end + 4 != bytes.size()) return false;  // one whole request head, nothing after
+  std::string head = to_lower(bytes.substr(0, end));
+  // a body, or an upgrade (a WebSocket, e.g. a dev server's hot-reload socket): a session on the
+  // server, not a request to repeat
+  return !contains(head, "\r\ncontent-length:") && !contains(head, "\r\ntransfer-encoding:") &&
+         !contains(head, "\r\nupgrade:");
+}
+
+bool port_forward_hedge() {
+  const char* v = std::getenv("DEVSPACE_PORTFORWARD_HEDGE");
+  return !(v && std::string(v) == "0") && !reference_timing();
+}
+
+// A held idempotent request on a slow link (the app restarting behind a remote API server):
+// instead of one attempt per round trip, a new attempt (a stream pair in the pod's tunnel with
+// the request) goes out every third of a round trip while earlier ones are in flight, so the
+// request reaches the new server within a few ms of it listening rather than up to a round trip
+// later. The first attempt answered wins; the others are reset. The app may see the request
+// more than once (up to about four times): only GET, HEAD and OPTIONS without a body are hedged,
+// which HTTP lets a client repeat (RFC 9110 §9.2.2). nullptr: no answer before `deadline_ms`, or
+// an attempt ended other than refused (the caller carries on one attempt at a time).
+std::unique_ptr<FwdStream> PortForwarder::hedge(int remote_port, const std::string& request, bool fin, int64_t rtt_us,
+                                                long deadline_ms, std::string* first) {
+  struct Attempt {
+    std::unique_ptr<FwdStream> s;
+    std::thread t;
+    int state = 0;  // 0 in flight, 1 refused, 2 answered, 3 ended otherwise
+    std::string data;
+    int64_t t_open = 0, t_end = 0;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::unique_ptr<Attempt>> attempts;
+  const long spacing = std::max(8L, std::min(25L, (long)(rtt_us / 3000)));
+  Attempt* winner = nullptr;
+  bool failed = false;
+  const long started = mono_ms();
+  long next_open = started;
+  while (!stop_ && !winner && !failed && mono_ms() < deadline_ms) {
+    size_t in_flight = 0;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      for (auto& a : attempts) in_flight += a->state == 0;
+    }
+    if (mono_ms() >= next_open && in_flight < 8) {
+      auto a = std::make_unique<Attempt>();
+      a->t_open = trace::now_us();
+      try {
+        a->s = open_to(pod_name(), remote_port);
+      } catch (const std::exception&) {
+        break;
+      }
+      if (std::string(a->s->via()) != "tunnel" || !a->s->send(request)) {
+        a->s->close();
+        break;
+      }
+      if (fin) a->s->close_write();
+      Attempt* ap = a.get();
+      a->t = std::thread([ap, &mu, &cv] {
+        int ch = 0, st = 3;
+        std::string d;
+        while (ap->s->recv(&ch, &d)) {
+          if (ch == 0) {
+            st = 2;
+            break;
+          }
+          if (ch == 1 && !d.empty()) {
+            st = is_dial_refused(d) ? 1 : 3;
+            break;
+          }
+        }
+        {
+          std::lock_guard<std::mutex> g(mu);
+          ap->state = st;
+          ap->t_end = trace::now_us();
+          if (st == 2) ap->data = std::move(d);
+        }
+        cv.notify_all();
+      });
+      attempts.push_back(std::move(a));
+      held_retries_++;
+      // an app that takes more than a second to come back is not waited on this closely
+      next_open = mono_ms() + (mono_ms() - started < 1000 ? spacing : std::max(spacing, 50L));
+    }
+    std::unique_lock<std::mutex> lk(mu);
+    long wait = std::max(1L, std::min(next_open, deadline_ms) - mono_ms());
+    cv.wait_for(lk, std::chrono::milliseconds(wait), [&] {
+      for (auto& a : attempts)
+        if (a->state >= 2) return true;
+      return false;
+    });
+    for (auto& a : attempts) {
+      if (a->state == 2) {
+        winner = a.get();
+        break;
+      }
+      if (a->state == 3) failed = true;
+    }
+  }
+  for (auto& a : attempts)
+    if (a.get() != winner) a->s->close();  // a reply it may still get is dropped
+  for (auto& a : attempts)
+    if (a->t.joinable()) a->t.join();
+  if (trace::enabled()) {
+    int n = 0;
+    for (auto& a : attempts) {
+      static const char* kOutcome[] = {"abandoned", "refused", "reply", "closed"};
+      trace::emit("portforward.stream", a->t_open, (a->t_end ? a->t_end : trace::now_us()) - a->t_open,
+                  {{"port", std::to_string(remote_port)},
+                   {"attempt", "h" + std::to_string(n++)},
+                   {"first_us", a->t_end ? std::to_string(a->t_end - a->t_open) : std::string("-1")},
+                   {"outcome", a.get() == winner ? "reply" : kOutcome[a->state]},
+                   {"hedged", "1"},
+                   {"via", "tunnel"}});
+    }
+  }
+  if (!winner) return nullptr;
+  *first = std::move(winner->data);
+  return std::move(winner->s);
+}
+
+bool port_forward_preopen() {
+  const char* v = std::getenv("DEVSPACE_PORTFORWARD_PREOPEN");
+  return !(v && std::string(v) == "0");
+}
+
+int port_forward_hold_ms() {
+  if (const char* v = std::getenv("DEVSPACE_PORTFORWARD_HOLD_MS")) return std::max(0, std::atoi(v));
+  return reference_timing() ? 0 : 3000;
+}
+
+// One accepted local connection. Restart-tolerant: while the app in the pod is restarting
+// (hot reload), its port refuses connections for a moment; kubectl then drops the client's
+// connection and a browser shows an error. Here, as long as nothing came back from the pod yet
+// and the pod-side connect was refused, the connection is held and its bytes replayed on a
+// new stream for up to hold_ms_, so a request sent mid-restart is answered by the new server as
+// soon as it listens. For the first 100 ms the next stream is opened while the current attempt
+// is in flight (PreOpened) and used as soon as that attempt is refused; after that the attempts
+// back off (5 ms, then 25 ms after a second).
+void PortForwarder::handle(Conn* conn, int remote_port) {
+  int cfd = conn->fd;
+  const long hold_start = mono_ms();
+  const long hold_deadline = hold_start + hold_ms_;
+  std::string replay;           // client bytes of this connection, kept while no reply arrived
+  bool replayable = hold_ms_ > 0;
+  bool client_eof = false;
+  int attempt = 0;
+  std::unique_ptr<PreOpened> next;
+  std::unique_ptr<FwdStream> hedged;  // the answered attempt of a hedged held request
+  while (!stop_) {
+    std::unique_ptr<FwdStream> ws = std::move(hedged);
+    const bool primed = ws != nullptr;  // its request went out with it
+    // span per stream: open (the WebSocket upgrade, or a stream pair in the tunnel; the pod-side
+    // dial happens with it) and the time until the first reply byte or the refusal
+    // (trace.jsonl "portforward.stream")
+    const int64_t t_open = trace::now_us();
+    const std::string target = pod_name();
+    bool preopened = false;
+    if (next) {
+      ws = next->take();
+      next.reset();
+      preopened = ws != nullptr;
+    }
+    if (!ws) {
+      try {
+        ws = open_stream(remote_port);
+      } catch (const std::exception& e) {
+        log::file_logger("portforwarding")->emit("error", std::string("Error forwarding ports: ") + e.what(), {});
+        break;
+      }
+    }
+    if (preopened) preopened_++;
+    const int64_t t_opened = trace::now_us();
+    const bool tunneled = std::string(ws->via()) == "tunnel";
+    // a held connection (its first stream was refused) within its first 100 ms: open the
+    // following attempt's stream now, while this one waits for its reply or refusal. (Not through
+    // the tunnel: a stream there opens without a round trip, and its pod-side dial is what an
+    // attempt is for.)
+    if (preopen_ && !tunneled && attempt > 0 && replayable && !stop_ && mono_ms() - hold_start < 100)
+      next = std::make_unique<PreOpened>([this, remote_port] { return open_stream_direct(remote_port); });
+    std::atomic<int64_t> t_first{0};
+    if (!primed && !replay.empty() && !ws->send(replay)) break;
+    if (client_eof && !primed) ws->close_write();
+    int wake[2];
+    if (::pipe2(wake, O_CLOEXEC | O_NONBLOCK) != 0) break;
+    std::atomic<bool> down_done{false}, got_reply{false}, refused{false};
+    std::string error_text;  // the first error message before any reply (read after the join)
+    std::thread down([&] {
+      int ch = 0;
+      std::string data;
+      while (ws->recv(&ch, &data)) {
+        if (ch == 0) {
+          if (!got_reply) t_first = trace::now_us();
+          got_reply = true;
+          if (!write_all(cfd, data)) break;
+        } else if (ch == 1 && !data.empty()) {
+          if (!got_reply && is_dial_refused(data)) {
+            t_first = trace::now_us();
+            refused = true;
+            break;
+          }
+          if (!got_reply && error_text.empty()) error_text = data;
+          log::file_logger("portforwarding")->emit("error", data, {});
+        }
+      }
+      down_done = true;
+      ssize_t w = ::write(wake[1], "x", 1);
+      (void)w;
+    });
+    char buf[65536];
+    while (!down_done && !stop_ && !client_eof) {
+      // answered: the spare attempt is not needed (dropped once its open is done, so the
+      // forwarding never waits on it; else at the end of the connection)
+      if (next && got_reply && next->ready()) next.reset();
+      struct pollfd pf[2] = {{cfd, POLLIN, 0}, {wake[0], POLLIN, 0}};
+      int r = ::poll(pf, 2, 200);
+      if (r <= 0 || !(pf[0].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+      ssize_t n = ::recv(cfd, buf, sizeof(buf), 0);
+      if (n <= 0) {
+        client_eof = true;  // half-close: the request is complete, keep reading the reply
+        ws->close_write();
+        break;
+      }
+      if (replayable && !got_reply) {
+        replay.append(buf, (size_t)n);
+        if (replay.size() > (4u << 20)) replayable = false;  // a large upload: do not buffer it
+      }
+      if (!ws->send(std::string(buf, (size_t)n))) break;
+    }
+    if (client_eof && !down_done) {
+      // the client finished sending: wait for the reply (or the refusal) before closing
+      while (!down_done && !stop_) {
+        if (next && got_reply && next->ready()) next.reset();
+        struct pollfd pw{wake[0], POLLIN, 0};
+        ::poll(&pw, 1, 200);
+      }
+    }
+    ws->close();
+    down.join();
+    ::close(wake[0]);
+    ::close(wake[1]);
+    if (trace::enabled()) {
+      int64_t tf = t_first.load();
+      trace::emit("portforward.stream", t_open, trace::now_us() - t_open,
+                  {{"port", std::to_string(remote_port)},
+                   {"attempt", std::to_string(attempt)},
+                   {"open_us", std::to_string(t_opened - t_open)},
+                   {"first_us", tf ? std::to_string(tf - t_open) : std::string("-1")},
+                   {"outcome", refused ? "refused" : got_reply ? "reply" : error_text.empty() ? "closed" : "error"},
+                   {"preopened", preopened ? "1" : "0"},
+                   {"via", ws->via()}});
+    }
+    ++attempt;
+    if (tunneled && !got_reply && !refused && !error_text.empty() && !stop_ && drop_tunnel_if_pod_gone(target)) {
+      // A tunnel outlives its pod: once the pod was replaced every stream fails with the
+      // kubelet's "failed to find sandbox"-type error instead of a 404 at the upgrade. The tunnel
+      // is dropped and the next stream re-selects the pod (open_stream); nothing reached the
+      // app, so a held connection is replayed there.
+      if (replayable && mono_ms() < hold_deadline) {
+        held_retries_++;
+        continue;
+      }
+    }
+    if (refused && replayable && !stop_ && mono_ms() < hold_deadline && tunneled && hedge_ &&
+        t_first.load() - t_open >= 10000 && hedgeable_request(replay)) {
+      // a remote cluster (the refusal took 10 ms or more) and a request HTTP lets a client repeat
+      std::string first;
+      auto win = hedge(remote_port, replay, client_eof, t_first.load() - t_open, hold_deadline, &first);
+      if (win) {
+        hedged = std::make_unique<PrimedFwd>(std::move(win), std::move(first));
+        continue;
+      }
+    }
+    if (refused && replayable && !stop_ && mono_ms() < hold_deadline) {
+      // a hot-reloading app is back within tens of ms: retry at once for the first 100 ms
+      // (a refusal takes a round trip, which paces the attempts; so does a pre-opened stream),
+      // then back off
+      long held = mono_ms() - hold_start;
+      int delay = next || tunneled ? (held < 100 ? 0 : held < 1000 ? 5 : 25) : held < 100 ? 1 : held < 1000 ? 5 : 25;
+      if (delay) std::this_thread::sleep_for(std::chrono::milliseconds(delay));
+      held_retries_++;
+      continue;
+    }
+    if (refused) log::file_logger("portforwarding")->emit("error", "connection refused by the pod", {});
+    break;
+  }
+  ::shutdown(cfd, SHUT_RDWR);
+  ::close(cfd);
+  conn->done = true;
+}
+
+void PortForwarder::close() {
+  if (stop_.exchange(true)) return;
+  {
+    std::lock_guard<std::mutex> g(spare_mu_);  // no lost wake-up between its check and wait
+  }
+  spare_cv_.notify_all();
+  if (spare_thread_.joinable()) spare_thread_.join();
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  for (int fd : listeners_) ::close(fd);
+  listeners_.clear();
+  reap(true);  // every connection thread ends within one poll interval once stop_ is set
+}
+
+std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& cfg, std::shared_ptr<kube::Client> k,
+                                                                  int pod_wait_ms, int poll_ms) {
+  std::vector<std::unique_ptr<PortForwarder>> out;
+  for (auto& pf : cfg.at_path("dev.ports").items()) {
+    config::SelectorRef ref = config::resolve_selector(cfg, pf);
+    log::start_wait("Port-Forwarding: Waiting for pods...");
+    Value pod;
+    try {
+      pod = k->newest_running_pod(ref.namespace_, ref.labels.to_query(), pod_wait_ms, poll_ms);
+    } catch (const std::exception& e) {
+      log::stop_wait();
+      throw std::runtime_error(std::string("Error starting port-forwarding: Unable to list devspace pods: ") + e.what());
+    }
+    log::stop_wait();
+    std::vector<std::pair<int, int>> ports;
+    std::vector<std::string> addrs;
+    for (auto& m : pf.get("portMappings").items()) {
+      ports.emplace_back((int)m.get("localPort").as_int(), (int)m.get("remotePort").as_int());
+      // Deliberate deviation (PARITY.md): the reference defaults to "127.0.0.1"
+      // (port_forwarding.go:64-67); an unset bindAddress here listens on localhost, i.e.
+      // 127.0.0.1 and ::1, as `kubectl port-forward` does, so http://localhost:<port> works on
+      // hosts that resolve localhost to ::1 first. An explicit bindAddress is used as given.
+      addrs.push_back(m.get("bindAddress").as_string("localhost"));
+    }
+    auto fwd = std::make_unique<PortForwarder>(k, pod, ports, addrs, ref.labels.to_query());
+    fwd->start();
+    log::done("Port forwarding started on " + fwd->describe());
+    out.push_back(std::move(fwd));
+  }
+  return out;
+}
+
+}  // namespace services
+}  // namespace ds

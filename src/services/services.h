@@ -63,7 +63,7 @@ bool is_dial_refused(const std::string& error_channel_message);
 bool port_forward_hedge();
 bool hedgeable_request(const std::string& bytes);
 
-class FwdStream;  // one forwarded connection's stream(s) (services.cc)
+class FwdStream;  // one forwarded connection's stream(s) (portforward.cc)
 
 // Local listeners forwarding to a pod port (services/port_forwarding.go:18, kubectl/client.go:356):
 // through one multiplexed tunnel per pod (SPDY/3.1 over a WebSocket, kube/spdy.h) where the API
