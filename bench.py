@@ -402,6 +402,8 @@ def _pf_spans(trace_path, windows):
     return {"via": sorted({sp.get("via", "websocket") for sp in spans}),
             "streams_per_edit": round(len(spans) / n, 2),
             "refused_per_edit": round(sum(sp.get("outcome") == "refused" for sp in spans) / n, 2),
+            # attempts of held GETs sent while earlier ones were in flight (the app may see those)
+            "hedged_per_edit": round(sum(sp.get("hedged") == "1" for sp in spans) / n, 2),
             "open_ms_p50": ms("open_us", spans), "reply_first_byte_ms_p50": ms("first_us", replies)}
 
 
