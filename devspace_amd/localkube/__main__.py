@@ -32,10 +32,12 @@ def main(argv=None):
     up.add_argument("--resource-strategy", default="single", choices=("single", "mixed"),
                     help="device plugin naming: amd.com/gpu, or amd.com/<partition>_<nps>")
     up.add_argument("--unhealthy", type=int, default=0, help="devices the device plugin reports unhealthy")
+    up.add_argument("--no-portforward-tunnel", action="store_true",
+                    help="no SPDY-over-WebSocket port-forward (an API server older than Kubernetes 1.30)")
     args = ap.parse_args(argv)
     c = LocalCluster(args.state, port=args.port, gpus=args.gpus, context=args.context, tls=args.tls,
                      gpu_partition=args.partition, memory_partition=args.nps, gpu_strategy=args.resource_strategy,
-                     unhealthy_gpus=args.unhealthy).start()
+                     unhealthy_gpus=args.unhealthy, portforward_tunnel=not args.no_portforward_tunnel).start()
     c.api.reset_throttle(args.throttle_first, args.retry_after)
     c.kubelet.pull_seconds = args.pull_seconds
     kc = args.kubeconfig or os.path.join(args.state, "kubeconfig")

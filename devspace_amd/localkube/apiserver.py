@@ -55,6 +55,7 @@ class ApiServer:
         self.token_validator = token_validator
         self.auth_failures = 0
         self.portforward_tunnels = 0  # multiplexed port-forward tunnels served (SPDY over WebSocket)
+        self.portforward_tunnel = True  # False: serve only the WebSocket-per-connection protocols
         # Fault switch (API Priority and Fairness under load): the first `throttle_first` requests
         # of every (verb, resource) are answered `429 Too Many Requests` + `Retry-After`. The
         # counts start over with reset_throttle(), so every CLI command can be throttled afresh.
@@ -649,8 +650,13 @@ class ApiServer:
 
     async def portforward_ws(self, request, ns, name):
         uid = self.store.get("", "pods", ns, name)["metadata"].get("uid")
-        ws = web.WebSocketResponse(protocols=(spdy.PROTOCOL, "v4.channel.k8s.io", "portforward.k8s.io"),
-                                   max_msg_size=0)
+        served = ((spdy.PROTOCOL,) if self.portforward_tunnel else ()) + ("v4.channel.k8s.io", "portforward.k8s.io")
+        offered = [p.strip() for p in request.headers.get("Sec-WebSocket-Protocol", "").split(",") if p.strip()]
+        if offered and not set(offered) & set(served):
+            # the API server's stream negotiation refuses the upgrade (wsstream handshake)
+            raise web.HTTPBadRequest(text=f"requested protocol(s) are not supported: {offered}; "
+                                          f"supports {list(served)}")
+        ws = web.WebSocketResponse(protocols=served, max_msg_size=0)
         await ws.prepare(request)
         if ws.ws_protocol == spdy.PROTOCOL:
             # Kubernetes >= 1.30: one tunnel, a stream pair per forwarded connection

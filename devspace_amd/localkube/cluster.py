@@ -86,7 +86,7 @@ def _b64file(path):
 class LocalCluster:
     def __init__(self, state_dir, port=0, gpus=None, context="devspace-local", extra_env=None, tls=False,
                  token_validator=None, gpu_partition="spx", memory_partition="nps1", gpu_strategy="single",
-                 unhealthy_gpus=0, run_steps=False):
+                 unhealthy_gpus=0, run_steps=False, portforward_tunnel=True):
         self.state_dir = os.path.abspath(state_dir)
         self.tls = tls
         self.pki = make_pki(os.path.join(self.state_dir, "pki")) if tls else None
@@ -104,6 +104,8 @@ class LocalCluster:
         # devices the device plugin marked unhealthy, as an MI355X node would advertise them
         self.kubelet.set_gpu_topology(gpu_partition, memory_partition, gpu_strategy, unhealthy_gpus)
         self.api = ApiServer(self.store, self.kubelet, token_validator=token_validator)
+        # False: an API server older than Kubernetes 1.30 (no SPDY-over-WebSocket port-forward)
+        self.api.portforward_tunnel = portforward_tunnel
         self.docker_sock = os.path.join(self.state_dir, "docker.sock")
         self.loop = None
         self.thread = None

@@ -4,7 +4,8 @@ RTT, devspace_amd/localkube/netem.py), as a laptop reaches a remote MI355X node.
 One attempt per round trip would make a request wait up to a whole round trip after the new
 server listens. So a held GET (repeatable, RFC 9110 §9.2.2) goes out on a new stream pair of the
 pod's tunnel every quarter round trip while earlier attempts are in flight; the first answer wins.
-A POST still goes out on one stream at a time and reaches the app exactly once.
+A POST still goes out on one stream at a time and reaches the app exactly once. And an API server
+without the tunnel (before Kubernetes 1.30) gets a WebSocket per connection.
 """
 import json
 import os
@@ -79,3 +80,31 @@ def _fetch(port):
         return urllib.request.urlopen(f"http://127.0.0.1:{port}/", timeout=5).read().decode()
     except Exception:
         return None
+
+
+def test_an_api_server_without_the_tunnel_gets_a_websocket_per_connection(tmp_path):
+    """Kubernetes before 1.30 refuses the SPDY-over-WebSocket upgrade (its stream negotiation does
+    not know the subprotocol): the forward falls back to one portforward.k8s.io WebSocket per
+    connection, says so in its log, and serves every connection."""
+    from devspace_amd.localkube import LocalCluster
+
+    cluster = LocalCluster(str(tmp_path / "state"), gpus=0, tls=True, portforward_tunnel=False).start()
+    try:
+        lk = DevspaceEnv(cluster, str(tmp_path))
+        proj, remote, local = _restart_project(lk, "qs-no-tunnel", "pf-old")
+        dev = lk.popen(["dev", "--terminal=false"], proj)
+        try:
+            wait_for(lambda: (lambda b: b.startswith("Hello") if b else False)(_fetch(local)), timeout=90,
+                     what="forwarded server")
+            for _ in range(5):
+                assert (_fetch(local) or "").startswith("Hello")
+        finally:
+            _stop(dev)
+        assert cluster.api.portforward_tunnels == 0
+        spans = [json.loads(l) for l in open(os.path.join(proj, ".devspace", "logs", "trace.jsonl"))
+                 if '"portforward.stream"' in l]
+        assert spans and all(s.get("via") == "websocket" for s in spans), spans
+        log = open(os.path.join(proj, ".devspace", "logs", "portforwarding.log")).read()
+        assert "no multiplexed port-forward" in log, log
+    finally:
+        cluster.stop()
