@@ -319,7 +319,8 @@ std::string helper_probe_script(const std::string& file, const std::vector<std::
          "2>/dev/null && chmod +x \"$d/.devspace-x$$\" 2>/dev/null && \"$d/.devspace-x$$\" 2>/dev/null; then "
          "rm -f \"$d/.devspace-x$$\"; dsd=$d; dss=NEED; break; fi; rm -f \"$d/.devspace-x$$\" 2>/dev/null; done; fi; "
          "if [ \"$dss\" = HAVE ]; then echo \"HAVE $dsd\"; " + (when_present.empty() ? std::string(":") : when_present) +
-         "; elif [ -n \"$dsd\" ]; then echo \"NEED $dsd\"; else echo NOHELPER; fi\n";
+         "; elif [ -n \"$dsd\" ]; then if command -v gzip >/dev/null 2>&1; then echo \"NEEDZ $dsd\"; "
+         "else echo \"NEED $dsd\"; fi; else echo NOHELPER; fi\n";
 }
 
 bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out, HelperRole role) {
@@ -354,13 +355,18 @@ bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out, HelperRo
   if (!write_all(sh->in(), helper_probe_script(file, helper_dirs(), start("\"$dsd/" + file + "\"")))) return false;
   std::string line;
   if (!out.read_line(&line, 15000)) return false;
-  if (line == "NOHELPER" || line.size() < 6 || (!starts_with(line, "HAVE ") && !starts_with(line, "NEED "))) {
+  if (line == "NOHELPER" || line.size() < 6 ||
+      (!starts_with(line, "HAVE ") && !starts_with(line, "NEED ") && !starts_with(line, "NEEDZ "))) {
     logf("[Sync] No directory in the container can hold and run the helper (" + line + ")");
     return false;
   }
   if (starts_with(line, "HAVE ")) announce.set(1);
-  if (starts_with(line, "NEED ")) {
-    std::string name = shell_quote(line.substr(5) + "/" + file);
+  if (starts_with(line, "NEED")) {
+    // "NEEDZ <dir>": the container has gzip, so the helper travels compressed (1.1 MB -> about
+    // 0.5 MB: a first `dev` on a slow uplink waits for half the bytes)
+    const bool gz = starts_with(line, "NEEDZ ");
+    const std::string dir = line.substr(gz ? 6 : 5);
+    std::string name = shell_quote(dir + "/" + file);
     bool there = false;
     if (role == kWaiter) {  // the other shell is uploading it: wait for that, not the bytes again
       std::unique_lock<std::mutex> lk(helper_mu_);
@@ -369,12 +375,24 @@ bool Session::start_helper(std::unique_ptr<Shell>& sh, LineReader& out, HelperRo
     }
     if (!there) {
       // a temporary name per shell: shells may upload at the same time
-      std::string tmp = shell_quote(line.substr(5) + "/" + file) + ".tmp.$$";
-      std::string up = "echo " + std::string(kStart) + "; head -c " + std::to_string(bin.size()) + " > " + tmp +
-                       " && chmod +x " + tmp + " && mv " + tmp + " " + name + "; echo " + kDone + "\n";
+      std::string tmp = shell_quote(dir + "/" + file) + ".tmp.$$";
+      static std::mutex packed_mu;
+      static std::map<std::string, std::string> packed;  // helper file name (content hash) -> gzip
+      std::string payload;
+      if (gz) {
+        std::lock_guard<std::mutex> g(packed_mu);
+        auto& z = packed[file];
+        if (z.empty()) z = gzip_compress(bin, 9);
+        payload = z;
+      } else {
+        payload = bin;
+      }
+      std::string up = "echo " + std::string(kStart) + "; head -c " + std::to_string(payload.size()) +
+                       (gz ? " | gzip -dc" : "") + " > " + tmp + " && chmod +x " + tmp + " && mv " + tmp + " " + name +
+                       "; echo " + kDone + "\n";
       if (!write_all(sh->in(), up)) return false;
       if (!out.wait_for(kStart, 15000)) return false;
-      if (!write_all(sh->in(), bin)) return false;
+      if (!write_all(sh->in(), payload)) return false;
       if (!out.wait_for(kDone, 30000)) return false;
       announce.set(1);
     }

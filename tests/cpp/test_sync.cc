@@ -639,7 +639,7 @@ TEST(sync_helper_probe_picks_a_usable_directory) {
   fs::mkdirs(base + "/b");
   // /proc refuses a new directory: skipped; the next candidate is created and usable
   std::string out = run(sync::helper_probe_script("devspace-helper-x", {"/proc/ds-no-such", base + "/a", base + "/b"}));
-  EXPECT_EQ(out, "NEED " + base + "/a");
+  EXPECT_TRUE(out == "NEED " + base + "/a" || out == "NEEDZ " + base + "/a");
   // an executable helper already in a later candidate is reused before uploading anew
   fs::write_file(base + "/b/devspace-helper-x", "#!/bin/sh\n");
   ::chmod((base + "/b/devspace-helper-x").c_str(), 0755);
@@ -650,7 +650,7 @@ TEST(sync_helper_probe_picks_a_usable_directory) {
   out = run(sync::helper_probe_script("devspace-helper-x", {base + "/a", base + "/b"}, "echo STARTED \"$dsd\""));
   EXPECT_EQ(out, "HAVE " + base + "/b\nSTARTED " + base + "/b");
   out = run(sync::helper_probe_script("devspace-helper-y", {base + "/a"}, "echo STARTED \"$dsd\""));
-  EXPECT_EQ(out, "NEED " + base + "/a");
+  EXPECT_TRUE(out == "NEED " + base + "/a" || out == "NEEDZ " + base + "/a");
   out = run(sync::helper_probe_script("devspace-helper-x", {"/proc/ds-no-such"}));
   EXPECT_EQ(out, "NOHELPER");
   fs::remove_all(base);
