@@ -32,13 +32,21 @@ def test_a_held_get_is_hedged_and_a_held_post_is_sent_once(tmp_path):
         hits = tmp_path / "hits.log"
         values = os.path.join(proj, "chart", "values.yaml")
         v = yaml.safe_load(open(values))
-        v["components"][0]["containers"][0]["env"].append({"name": "HITS_FILE", "value": str(hits)})
+        v["components"][0]["containers"][0]["env"] += [{"name": "HITS_FILE", "value": str(hits)},
+                                                        {"name": "START_DELAY_MS", "value": "600"}]
         open(values, "w").write(yaml.safe_dump(v))
         index = os.path.join(proj, "index.js")
-        src = open(index).read().replace(
+        # every request is logged; the app listens 0.6 s after it starts (a slow restart: the held
+        # requests below certainly meet a refusing pod and are retried)
+        last = "}).listen(port, () => console.log('Example app listening on port ' + port + '!'));"
+        src = open(index).read()
+        assert last in src
+        src = src.replace(
             "http.createServer((req, res) => {",
-            "http.createServer((req, res) => {\n  require('fs').appendFileSync(process.env.HITS_FILE, req.method + ' ' + "
-            "req.url + '\\n');", 1)
+            "const srv = http.createServer((req, res) => {\n  require('fs').appendFileSync(process.env.HITS_FILE, "
+            "req.method + ' ' + req.url + '\\n');", 1).replace(
+            last, "});\nsetTimeout(() => srv.listen(port, () => console.log('Example app listening on port ' + port + "
+                  "'!')), Number(process.env.START_DELAY_MS || 0));")
         open(index, "w").write(src)
         dev = lk.popen(["dev", "--terminal=false"], proj)
         try:
