@@ -56,6 +56,7 @@ class ApiServer:
         self.auth_failures = 0
         self.portforward_tunnels = 0  # multiplexed port-forward tunnels served (SPDY over WebSocket)
         self.portforward_tunnel = True  # False: serve only the WebSocket-per-connection protocols
+        self.open_tunnels = set()  # their WebSockets (close_tunnels(): an idle timeout, a restart)
         # Fault switch (API Priority and Fairness under load): the first `throttle_first` requests
         # of every (verb, resource) are answered `429 Too Many Requests` + `Retry-After`. The
         # counts start over with reset_throttle(), so every CLI command can be throttled afresh.
@@ -68,6 +69,11 @@ class ApiServer:
         # namespace answers 403 Forbidden; discovery (/version, /api, /apis) stays open.
         self.scoped_tokens = {}
         self.forbidden = 0
+
+    async def close_tunnels(self):
+        """Closes every open port-forward tunnel, as an API server's idle timeout or restart does."""
+        for ws in list(self.open_tunnels):
+            await ws.close()
 
     def reset_throttle(self, first=None, retry_after=None):
         if first is not None:
@@ -672,7 +678,11 @@ class ApiServer:
                 return await asyncio.open_connection("127.0.0.1", port)
 
             tunnel = spdy.Tunnel(ws, dial, lambda port, e: self._refused_text(name, port, e))
-            await tunnel.run()
+            self.open_tunnels.add(ws)
+            try:
+                await tunnel.run()
+            finally:
+                self.open_tunnels.discard(ws)
             return ws
         port = int(request.query.get("ports", "0").split(",")[0])
         hdr = struct.pack("<H", port)

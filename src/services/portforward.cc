@@ -118,6 +118,8 @@ class FwdStream {
   virtual void close_write() {}
   virtual void close() = 0;
   virtual const char* via() const = 0;
+  // the stream ended because its tunnel did (no reply, no error from the pod)
+  virtual bool tunnel_lost() const { return false; }
 };
 
 namespace {
@@ -171,7 +173,10 @@ class TunnelFwd : public FwdStream {
     kube::SpdyMailbox::Event e;
     while (!data_done_ && box_->pop(&e)) {
       if (e.end) {
-        if (e.channel == 0) data_done_ = true;
+        if (e.channel == 0) {
+          data_done_ = true;
+          lost_ = e.reset == "tunnel closed" || e.reset == "closed";  // SpdySession::end_all
+        }
         continue;
       }
       if (e.channel == 0) s_->consumed(data_, e.data.size());
@@ -192,12 +197,13 @@ class TunnelFwd : public FwdStream {
     box_->close();
   }
   const char* via() const override { return "tunnel"; }
+  bool tunnel_lost() const override { return lost_; }
 
  private:
   std::shared_ptr<kube::SpdySession> s_;
   std::shared_ptr<kube::SpdyMailbox> box_ = std::make_shared<kube::SpdyMailbox>();
   std::shared_ptr<kube::SpdySession::Stream> err_, data_;
-  bool data_done_ = false, closed_ = false;
+  bool data_done_ = false, closed_ = false, lost_ = false;
 };
 
 bool port_forward_tunnel_enabled() {
@@ -503,6 +509,7 @@ class PrimedFwd : public FwdStream {
   void close_write() override { in_->close_write(); }
   void close() override { in_->close(); }
   const char* via() const override { return in_->via(); }
+  bool tunnel_lost() const override { return in_->tunnel_lost(); }
 
  private:
   std::unique_ptr<FwdStream> in_;
@@ -767,6 +774,13 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
                    {"via", ws->via()}});
     }
     ++attempt;
+    if (tunneled && ws->tunnel_lost() && !got_reply && !refused && error_text.empty() && replayable && !stop_ &&
+        mono_ms() < hold_deadline && hedgeable_request(replay)) {
+      // the tunnel ended under this stream before anything came back (an API server's idle
+      // timeout or restart): a request HTTP lets a client repeat goes out again, on a new tunnel
+      held_retries_++;
+      continue;
+    }
     if (tunneled && !got_reply && !refused && !error_text.empty() && !stop_ && drop_tunnel_if_pod_gone(target)) {
       // A tunnel outlives its pod: once the pod was replaced every stream fails with the
       // kubelet's "failed to find sandbox"-type error instead of a 404 at the upgrade. The tunnel

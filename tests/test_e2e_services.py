@@ -166,6 +166,53 @@ def _try(fn):
         return None
 
 
+def test_port_forward_reopens_a_tunnel_the_api_server_closed(localkube):
+    """An API server ends long-lived streams (idle timeout, restart, a load balancer in between):
+    the forward opens a new tunnel for the next connection, and no request fails on the old one."""
+    import asyncio
+
+    lk = localkube
+    ns = "pf-reopen"
+    proj = lk.project("quickstart", "quickstart-" + ns)
+    remote, local = _free_port(), _free_port()
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    cfg["cluster"]["namespace"] = ns
+    cfg["dev"]["overrideImages"][0]["entrypoint"] = ["python3", "-c", ECHO_SERVER]
+    cfg["dev"]["ports"][0]["portMappings"] = [{"localPort": local, "remotePort": remote}]
+    cfg["dev"].pop("sync", None)
+    open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    values = os.path.join(proj, "chart", "values.yaml")
+    v = yaml.safe_load(open(values))
+    v["components"][0]["containers"][0]["env"] = [{"name": "PORT", "value": str(remote)}]
+    open(values, "w").write(yaml.safe_dump(v))
+    tunnels_before = lk.cluster.api.portforward_tunnels
+    dev = lk.popen(["dev", "--terminal=false"], proj)
+
+    def echo(payload, timeout=10):
+        with socket.create_connection(("127.0.0.1", local), timeout=timeout) as c:
+            c.sendall(payload)
+            c.shutdown(socket.SHUT_WR)
+            got = bytearray()
+            while True:
+                b = c.recv(1 << 16)
+                if not b:
+                    return bytes(got)
+                got += b
+
+    try:
+        wait_for(lambda: running(lk.pods(ns)), timeout=60, what="pod")
+        wait_for(lambda: _try(lambda: echo(b"ping", 2)) == b"ping", timeout=30, what="echo through the forward")
+        for round_ in range(3):
+            asyncio.run_coroutine_threadsafe(lk.cluster.api.close_tunnels(), lk.cluster.loop).result(10)
+            for i in range(5):  # right after the close, and after the forward noticed it
+                assert echo(f"r{round_}-{i}".encode()) == f"r{round_}-{i}".encode()
+        assert lk.cluster.api.portforward_tunnels - tunnels_before >= 4  # the first + one per close
+    finally:
+        _stop(dev)
+    lk.run(["purge"], proj)
+
+
 def test_enter_interactive_pty(localkube):
     lk = localkube
     proj = lk.project("quickstart", "quickstart-tty")
