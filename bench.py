@@ -188,12 +188,13 @@ def _killpg(p, grace=15):
 # ---------------------------------------------------------------------------- full CLI path
 
 
-def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, timed_end=None, tls=True):
-    """`devspace deploy` + `devspace dev` of examples/rocm-pytorch on the local cluster."""
+def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, timed_end=None, tls=True, wan=None):
+    """`devspace deploy` + `devspace dev` of examples/rocm-pytorch on the local cluster.
+    wan=(rtt_ms, mbit): the API server behind a shaped link (the fault drill is skipped)."""
     from devspace_amd.localkube import LocalCluster
     from devspace_amd.localkube.bench import devspace_env, run_devspace
 
-    base = os.path.join(workdir, "dev-bench")
+    base = os.path.join(workdir, "dev-bench" + ("-wan" if wan else ""))
     proj = os.path.join(base, "rocm-pytorch")
     shutil.copytree(os.path.join(ROOT, "examples", "rocm-pytorch"), proj, symlinks=True)
     train = os.path.join(proj, "train.py")
@@ -205,9 +206,14 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
     open(values, "w").write(v)
 
     cluster = LocalCluster(os.path.join(base, "cluster"), gpus=gpus, tls=tls).start()
-    dev = None
+    dev = link = None
     try:
         env = devspace_env(cluster, base)
+        if wan:  # a laptop editing train.py for a pod on a remote MI355X node
+            from devspace_amd.localkube.netem import ShapedLink, point_kubeconfig
+
+            link = ShapedLink(("127.0.0.1", cluster.port), rtt_ms=wan[0], mbit=wan[1]).start()
+            point_kubeconfig(env["KUBECONFIG"], cluster.server, link.url("https" if tls else "http"))
         env["DEVSPACE_NPROC"] = str(nproc)  # used when the pod requests no GPU (CPU smoke)
         cluster.kubelet.extra_env["DEVSPACE_NPROC"] = str(nproc)
         if os.environ.get("DEVSPACE_DIST_BACKEND"):  # rehearsal: N ranks sharing fewer GPUs (gloo)
@@ -285,7 +291,7 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         out = {"reload_ms": samples, "sync_ms": sync_samples, "mode": mode, "pod_deploy_s": deploy_s,
                "parts": parts, "fused": fused, "world": pod_world, "first_step_s": first_step_s,
                "ranks_agreed": bool(agreed) and all(a == pod_world for a in agreed)}
-        if pod_world >= 1:
+        if pod_world >= 1 and not wan:
             try:
                 out["fault_drill"] = _fault_drill(train, tail, idx, pod_world)
             except Exception as e:  # reported with the loop's numbers, which stand on their own
@@ -293,6 +299,8 @@ def dev_loop(workdir, nproc, gpus, steps, warmup, tiny=False, timed_start=None, 
         return out
     finally:
         _killpg(dev)
+        if link is not None:
+            link.stop()
         cluster.stop()
 
 
@@ -832,6 +840,9 @@ def main():
                     extra("deploy_wan_ref", lambda: bench_deploy(workdir, tls=tls, reference=True, wan=WAN))
             if args.gpu_steps > 0:
                 extra("gpu_pod", lambda: dev_loop(workdir, nproc, gpus, args.gpu_steps, 3, tiny=args.tiny, tls=tls))
+                if args.ref_steps > 0:  # the same loop with the cluster 30 ms away
+                    extra("gpu_pod_wan", lambda: dev_loop(workdir, nproc, gpus, 10, 2, tiny=args.tiny, tls=tls,
+                                                          wan=WAN))
                 if args.ref_steps > 0:
                     extra("gpu_pod_ref", lambda: inner_loop(workdir, "compat", True, nproc, args.ref_steps, 1,
                                                             tiny=args.tiny))
@@ -1019,6 +1030,15 @@ def report(args, nproc, tls, ms_total, qs, extras):
                         "(nodemon-style): prices the hot-reload runner more than the CLI",
                 "p50_ms": round(rp50, 2), "sync_p50_ms": round(_pct(gr["sync_ms"], 0.5), 2),
                 "speedup": round(rp50 / gp50, 1) if gp50 else None}
+        gw = extras.get("gpu_pod_wan")
+        if _ok(gw):  # edit train.py on a laptop -> the remote pod's reload line back on the laptop
+            g["wan"] = {"rtt_ms": WAN[0], "mbit": WAN[1],
+                        "reload_p50_ms": round(_pct(gw["reload_ms"], 0.5), 2),
+                        "reload_p90_ms": round(_pct(gw["reload_ms"], 0.9), 2),
+                        "sync_p50_ms": round(_pct(gw["sync_ms"], 0.5), 2), "n": len(gw["reload_ms"]),
+                        "pod_deploy_s": round(gw["pod_deploy_s"], 3)}
+        elif gw is not None:
+            g["wan"] = gw
         out["gpu_pod"] = g
     for key in EXAMPLES:
         e, er = extras.get(key), extras.get(key + "_ref")

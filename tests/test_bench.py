@@ -66,6 +66,10 @@ def test_bench_cpu_tiny():
     g = d["gpu_pod"]
     assert g["n"] == 2 and g["reload_p50_ms"] > 0 and g["fused_ops"].startswith("eager (no GPU)"), g
     assert g["reference_equivalent"]["p50_ms"] > g["reload_p50_ms"]
+    # the same GPU-pod loop with the cluster 30 ms away: the edit crosses the link one way
+    gw = g["wan"]
+    assert "error" not in gw and gw["n"] == 10 and gw["sync_p50_ms"] >= 15, gw
+    assert gw["reload_p50_ms"] > gw["sync_p50_ms"], gw
     # one rank: the drill's hard crash is replaced from the warm standby, resuming from a snapshot
     drill = g["fault_drill"]
     assert drill.get("recovered") is True and drill["ranks"] == 1 and drill["warm_standby"], drill
