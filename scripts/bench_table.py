@@ -100,6 +100,10 @@ def render(path):
                          f"**{_ms(w['p50_ms'])}** (sync {_ms(w.get('sync_p50_ms'))})",
                          (f"{_ms(wr.get('p50_ms'))} (sync {_ms(wr.get('sync_p50_ms'))})" + _x(w["p50_ms"], wr.get("p50_ms")))
                          if wr else "—"))
+            gw = g.get("wan") if isinstance(g, dict) else None
+            if isinstance(gw, dict) and "reload_p50_ms" in gw:
+                rows.append((f"edit → pod hot-reload p50, rocm-pytorch, across that link (sync p50)",
+                             f"**{_ms(gw['reload_p50_ms'])}** (sync {_ms(gw.get('sync_p50_ms'))})", "—"))
             wd = w.get("deploy")
             if isinstance(wd, dict) and "wall_clock_s" in wd:
                 wdr = wd.get("reference_equivalent", {})

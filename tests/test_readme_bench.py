@@ -101,3 +101,19 @@ def test_round5_line_renders_the_measured_deploy_and_the_wait_caveat(tmp_path):
     assert "helm wait off" not in out[0]
     assert "control plane only: RUN steps not executed" in out[1]
     assert "microservices (helm wait off in both columns)" in out[1]
+
+
+def test_wan_rows_render_the_gpu_pod_across_the_link(tmp_path):
+    bt = _bt()
+    line = {"metric": "m", "value": 50.0, "steps": 20, "warmup": 3, "ms_per_step": 56.0, "p90_ms": 55.0,
+            "sync_p50_ms": 1.0, "config": {"app": "examples/quickstart"},
+            "reference_equivalent": {"p50_ms": 660.0, "sync_p50_ms": 605.0},
+            "gpu_pod": {"reload_p50_ms": 6.5, "sync_p50_ms": 1.1, "parallelism": "dp1", "fused_ops": "hip",
+                        "wan": {"reload_p50_ms": 37.2, "sync_p50_ms": 16.1, "n": 10}},
+            "wan": {"rtt_ms": 30, "mbit": 100, "p50_ms": 81.1, "sync_p50_ms": 16.3,
+                    "reference_equivalent": {"p50_ms": 822.2, "sync_p50_ms": 723.1}}}
+    p = tmp_path / "BENCH_r95.json"
+    p.write_text(json.dumps({"cmd": "python3 bench.py", "run": {"stdout_tail": json.dumps(line)}}))
+    out = bt.render(str(p))
+    assert "cluster behind 30 ms RTT / 100 Mbit/s" in out and "**81.10 ms**" in out, out
+    assert "rocm-pytorch, across that link" in out and "**37.20 ms** (sync 16.10 ms)" in out, out
