@@ -324,6 +324,19 @@ void SpdySession::reset(const std::shared_ptr<Stream>& s, uint32_t status) {
   write_frame(spdy::control_frame(spdy::RstStream, 0, spdy::u32(s->id) + spdy::u32(status)));
 }
 
+void SpdySession::ping() {
+  uint32_t id;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (dead_) return;
+    id = next_ping_;
+    next_ping_ += 2;
+    pings_[id] = std::chrono::steady_clock::now();
+  }
+  std::lock_guard<std::mutex> w(wmu_);
+  write_frame(spdy::control_frame(spdy::Ping, 0, spdy::u32(id)));
+}
+
 void SpdySession::close() {
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -403,6 +416,18 @@ void SpdySession::dispatch_control(uint16_t type, uint8_t flags, const std::stri
       break;
     }
     case spdy::Ping: {
+      if (body.size() < 4) break;
+      uint32_t id = spdy::get_u32(body, 0);
+      if (id & 1) {  // the answer to one of ours (never echoed back: that would loop)
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = pings_.find(id);
+        if (it != pings_.end()) {
+          rtt_us_ = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() -
+                                                                          it->second).count();
+          pings_.erase(it);
+        }
+        break;
+      }
       std::lock_guard<std::mutex> w(wmu_);
       write_frame(spdy::control_frame(spdy::Ping, 0, body));
       break;

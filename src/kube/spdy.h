@@ -16,6 +16,8 @@
 // data is acknowledged with WINDOW_UPDATE frames.
 #pragma once
 
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -109,6 +111,10 @@ class SpdySession {
   bool usable() const;
   void close();
   uint64_t streams_opened() const { return next_id_ / 2; }
+  // Sends a PING; its answer measures the round trip to the far end of the tunnel (the kubelet),
+  // without the pod. rtt_us(): the last measured round trip, -1 before an answer came.
+  void ping();
+  int64_t rtt_us() const { return rtt_us_.load(); }
 
  private:
   void reader();
@@ -127,6 +133,9 @@ class SpdySession {
   bool dead_ = false;
   bool goaway_ = false;
   uint64_t session_unacked_ = 0;
+  uint32_t next_ping_ = 1;  // client PING ids are odd
+  std::map<uint32_t, std::chrono::steady_clock::time_point> pings_;  // in flight (under mu_)
+  std::atomic<int64_t> rtt_us_{-1};
   std::thread reader_;
 };
 

@@ -232,10 +232,16 @@ std::shared_ptr<kube::SpdySession> PortForwarder::tunnel_for(const std::string& 
   }
   tunnel_mode_ = 1;
   tunnels_opened_++;
+  t->ping();  // its answer tells a remote cluster from one next door (hedging below)
   tunnel_ = t;
   tunnel_pod_ = pod;
   tunnel_requests_ = 0;
   return t;
+}
+
+int64_t PortForwarder::tunnel_rtt_us() {
+  std::lock_guard<std::mutex> g(tunnel_mu_);
+  return tunnel_ ? tunnel_->rtt_us() : -1;
 }
 
 bool PortForwarder::drop_tunnel_if_pod_gone(const std::string& pod) {
@@ -791,11 +797,15 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
         continue;
       }
     }
+    // the link's round trip: the tunnel's PING, else (not answered yet) this refusal's
+    const int64_t ping_us = tunnel_rtt_us();
+    const int64_t link_rtt_us = ping_us >= 0 ? ping_us : t_first.load() - t_open;
     if (refused && replayable && !stop_ && mono_ms() < hold_deadline && tunneled && hedge_ &&
-        t_first.load() - t_open >= 10000 && hedgeable_request(replay)) {
-      // a remote cluster (the refusal took 10 ms or more) and a request HTTP lets a client repeat
+        link_rtt_us >= (ping_us >= 0 ? 5000 : 10000) && hedgeable_request(replay)) {
+      // a remote cluster and a request HTTP lets a client repeat
       std::string first;
-      auto win = hedge(remote_port, replay, client_eof, t_first.load() - t_open, hold_deadline, &first);
+      auto win = hedge(remote_port, replay, client_eof, std::max<int64_t>(link_rtt_us, t_first.load() - t_open),
+                       hold_deadline, &first);
       if (win) {
         hedged = std::make_unique<PrimedFwd>(std::move(win), std::move(first));
         continue;

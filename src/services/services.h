@@ -116,6 +116,8 @@ class PortForwarder {
   // A tunnel stream failed with an error before any reply: true when `pod` is gone, replaced
   // (same name, new uid) or finished, or was re-selected away from; its tunnel is then dropped.
   bool drop_tunnel_if_pod_gone(const std::string& pod);
+  // the current tunnel's PING round trip (-1: none measured)
+  int64_t tunnel_rtt_us();
   std::unique_ptr<FwdStream> hedge(int remote_port, const std::string& request, bool fin, int64_t rtt_us,
                                    long deadline_ms, std::string* first);
   std::shared_ptr<kube::Client> k_;

@@ -403,6 +403,11 @@ def test_port_forward_holds_requests_across_app_restart(localkube, hold):
             assert all(not isinstance(o, str) for o in outcomes), outcomes
     finally:
         _stop(dev)
+    # next to the cluster (the tunnel's PING round trip is well under 5 ms) a held GET is retried
+    # one stream at a time: hedging is for remote clusters only
+    spans = [json.loads(l) for l in open(os.path.join(proj, ".devspace", "logs", "trace.jsonl"))
+             if '"portforward.stream"' in l]
+    assert not any(s.get("hedged") == "1" for s in spans), [s for s in spans if s.get("hedged")][:3]
     lk.run(["purge"], proj)
 
 
