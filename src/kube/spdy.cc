@@ -422,8 +422,10 @@ void SpdySession::dispatch_control(uint16_t type, uint8_t flags, const std::stri
         std::lock_guard<std::mutex> g(mu_);
         auto it = pings_.find(id);
         if (it != pings_.end()) {
-          rtt_us_ = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() -
-                                                                          it->second).count();
+          // the smallest seen: a busy peer answers late, the link is never faster than this
+          int64_t rtt = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() -
+                                                                              it->second).count();
+          if (rtt_us_ < 0 || rtt < rtt_us_) rtt_us_ = rtt;
           pings_.erase(it);
         }
         break;

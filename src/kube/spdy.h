@@ -112,7 +112,7 @@ class SpdySession {
   void close();
   uint64_t streams_opened() const { return next_id_ / 2; }
   // Sends a PING; its answer measures the round trip to the far end of the tunnel (the kubelet),
-  // without the pod. rtt_us(): the last measured round trip, -1 before an answer came.
+  // without the pod. rtt_us(): the smallest round trip measured, -1 before an answer came.
   void ping();
   int64_t rtt_us() const { return rtt_us_.load(); }
 

@@ -300,7 +300,8 @@ void PortForwarder::spare_loop() {
       // connection after a quiet spell does not pay the upgrade either
       lk.unlock();
       try {
-        tunnel_for(pod_name());
+        // and measure its round trip now and then (hedging needs it; the smallest one counts)
+        if (auto t = tunnel_for(pod_name())) t->ping();
       } catch (const std::exception&) {
       }
       lk.lock();
@@ -797,15 +798,14 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
         continue;
       }
     }
-    // the link's round trip: the tunnel's PING, else (not answered yet) this refusal's
-    const int64_t ping_us = tunnel_rtt_us();
-    const int64_t link_rtt_us = ping_us >= 0 ? ping_us : t_first.load() - t_open;
-    if (refused && replayable && !stop_ && mono_ms() < hold_deadline && tunneled && hedge_ &&
-        link_rtt_us >= (ping_us >= 0 ? 5000 : 10000) && hedgeable_request(replay)) {
+    // the link's round trip: the smallest of the tunnel's PINGs (unknown until one came back:
+    // then this is not taken for a remote cluster)
+    const int64_t link_rtt_us = tunnel_rtt_us();
+    if (refused && replayable && !stop_ && mono_ms() < hold_deadline && tunneled && hedge_ && link_rtt_us >= 5000 &&
+        hedgeable_request(replay)) {
       // a remote cluster and a request HTTP lets a client repeat
       std::string first;
-      auto win = hedge(remote_port, replay, client_eof, std::max<int64_t>(link_rtt_us, t_first.load() - t_open),
-                       hold_deadline, &first);
+      auto win = hedge(remote_port, replay, client_eof, link_rtt_us, hold_deadline, &first);
       if (win) {
         hedged = std::make_unique<PrimedFwd>(std::move(win), std::move(first));
         continue;
