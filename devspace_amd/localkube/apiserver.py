@@ -57,6 +57,7 @@ class ApiServer:
         self.portforward_tunnels = 0  # multiplexed port-forward tunnels served (SPDY over WebSocket)
         self.portforward_tunnel = True  # False: serve only the WebSocket-per-connection protocols
         self.open_tunnels = set()  # their WebSockets (close_tunnels(): an idle timeout, a restart)
+        self.tunnel_pings_answered = 0  # the tunnels' server PINGs the clients echoed
         # Fault switch (API Priority and Fairness under load): the first `throttle_first` requests
         # of every (verb, resource) are answered `429 Too Many Requests` + `Retry-After`. The
         # counts start over with reset_throttle(), so every CLI command can be throttled afresh.
@@ -683,6 +684,7 @@ class ApiServer:
                 await tunnel.run()
             finally:
                 self.open_tunnels.discard(ws)
+                self.tunnel_pings_answered += tunnel.pings_answered
             return ws
         port = int(request.query.get("ports", "0").split(",")[0])
         hdr = struct.pack("<H", port)

@@ -108,6 +108,7 @@ class Tunnel:
         self.pairs = {}  # request id -> _Pair
         self.streams = {}  # stream id -> (_Pair, "error" | "data")
         self.streams_opened = 0
+        self.pings_answered = 0  # of the PING (even id: the server's) sent when the tunnel opens
 
     async def _send(self, frame: bytes):
         async with self.wlock:
@@ -212,6 +213,9 @@ class Tunnel:
 
         buf = bytearray()
         try:
+            # the server's own PING (even ids are the server's, spdystream's convention): the
+            # client must answer it, and must not answer the answers to its own (odd) ones
+            await self._send(control_frame(PING, 0, struct.pack(">I", 2)))
             async for msg in self.ws:
                 if msg.type != WSMsgType.BINARY:
                     continue
@@ -227,7 +231,10 @@ class Tunnel:
                     elif t == RST_STREAM:
                         self._on_rst(struct.unpack_from(">I", body, 0)[0] & 0x7FFFFFFF)
                     elif t == PING:
-                        await self._send(control_frame(PING, 0, body))
+                        if struct.unpack_from(">I", body, 0)[0] % 2 == 0:
+                            self.pings_answered += 1  # our own, come back
+                        else:
+                            await self._send(control_frame(PING, 0, body))
                     elif t in (SYN_REPLY, HEADERS):
                         self.inz.decompress(body[4:])  # keep the zlib stream in step
                     elif t == GOAWAY:

@@ -151,8 +151,13 @@ def test_port_forward_multiplexes_connections_over_one_tunnel(localkube):
         [t.join() for t in ts]
         assert all(r == b for r, b in zip(results, blobs)), [len(r or b"") for r in results]
         assert lk.cluster.api.portforward_tunnels - tunnels_before == 1
+        pings_before = lk.cluster.api.tunnel_pings_answered
     finally:
         _stop(dev)
+    # the server's PING was answered once (and the client's own PINGs, answered by the server,
+    # were not echoed back: no ping-pong)
+    wait_for(lambda: lk.cluster.api.tunnel_pings_answered > pings_before, timeout=10, what="tunnel closed")
+    assert lk.cluster.api.tunnel_pings_answered == pings_before + 1
     spans = [json.loads(l) for l in open(os.path.join(proj, ".devspace", "logs", "trace.jsonl"))
              if '"portforward.stream"' in l]
     assert len(spans) >= 49 and all(s.get("via") == "tunnel" for s in spans), spans[:3]
