@@ -426,6 +426,7 @@ void SpdySession::dispatch_control(uint16_t type, uint8_t flags, const std::stri
           int64_t rtt = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() -
                                                                               it->second).count();
           if (rtt_us_ < 0 || rtt < rtt_us_) rtt_us_ = rtt;
+          rtt_samples_++;
           pings_.erase(it);
         }
         break;

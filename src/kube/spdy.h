@@ -115,6 +115,7 @@ class SpdySession {
   // without the pod. rtt_us(): the smallest round trip measured, -1 before an answer came.
   void ping();
   int64_t rtt_us() const { return rtt_us_.load(); }
+  int rtt_samples() const { return rtt_samples_.load(); }  // PINGs answered
 
  private:
   void reader();
@@ -136,6 +137,7 @@ class SpdySession {
   uint32_t next_ping_ = 1;  // client PING ids are odd
   std::map<uint32_t, std::chrono::steady_clock::time_point> pings_;  // in flight (under mu_)
   std::atomic<int64_t> rtt_us_{-1};
+  std::atomic<int> rtt_samples_{0};
   std::thread reader_;
 };
 

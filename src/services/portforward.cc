@@ -241,7 +241,8 @@ std::shared_ptr<kube::SpdySession> PortForwarder::tunnel_for(const std::string& 
 
 int64_t PortForwarder::tunnel_rtt_us() {
   std::lock_guard<std::mutex> g(tunnel_mu_);
-  return tunnel_ ? tunnel_->rtt_us() : -1;
+  // the smallest of several: one PING answered late by a busy API server next door is no link
+  return tunnel_ && tunnel_->rtt_samples() >= 5 ? tunnel_->rtt_us() : -1;
 }
 
 bool PortForwarder::drop_tunnel_if_pod_gone(const std::string& pod) {
@@ -307,7 +308,14 @@ void PortForwarder::spare_loop() {
       lk.lock();
       if (tunnel_mode_ == 1) {
         spares_.clear();
-        spare_cv_.wait_for(lk, std::chrono::seconds(1), [this] { return stop_.load(); });
+        // PINGs every 100 ms until the tunnel has ten answers (its round trip is known within a
+        // second of opening), then every second
+        int samples;
+        {
+          std::lock_guard<std::mutex> g(tunnel_mu_);
+          samples = tunnel_ ? tunnel_->rtt_samples() : 0;
+        }
+        spare_cv_.wait_for(lk, std::chrono::milliseconds(samples < 10 ? 100 : 1000), [this] { return stop_.load(); });
         continue;
       }
     }
