@@ -7,9 +7,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+@pytest.hookimpl(tryfirst=True)
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running")
+    # a hung test ends the run with every thread's stack (pytest-timeout) instead of stalling it:
+    # the longest test takes about 5 minutes; an explicit --timeout wins
+    if getattr(config.option, "timeout", None) is None and config.pluginmanager.hasplugin("timeout"):
+        config.option.timeout = 1800
+        config.option.timeout_method = "thread"
 
 
 @pytest.fixture(scope="session", autouse=True)
