@@ -67,8 +67,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "inner-loop p50 ms (edit->pod hot-reload) + deploy wall-clock s, quickstart"
 EDIT_JITTER_S = 0.010  # uniform think time before each edit (> 2 training steps of the example)
-BUILDER_FIDELITY = ("bundled Docker Engine API daemon: Dockerfile parsed, context hashed/tarred, "
-                    "RUN steps not executed; pods run on the host runtime")
+BUILDER_FIDELITY = ("bundled Docker Engine API daemon: Dockerfile parsed, context hashed/tarred; "
+                    "RUN steps executed on the host runtime for the deploy measurement "
+                    "(deploy.run_steps_executed), recorded only (RUN steps not executed) on the "
+                    "dev-loop cluster; base images not pulled; pods run on the host runtime")
 TINY = (("VOCAB", 256), ("DIM", 64), ("HEADS", 4), ("LAYERS", 1), ("SEQ", 32), ("BATCH", 2))
 
 
