@@ -24,6 +24,50 @@ def _close_mapping(mm) -> None:
         pass
 
 
+_CHUNK = 64 << 20  # bytes per pinned bounce buffer
+_BOUNCE_MIN = 8 << 20  # device tensors at least this large are restored through the bounce buffers
+_bounce = {"bufs": None, "lock": threading.Lock()}
+
+
+def _pinned_pair():
+    """Two page-locked 64 MiB host buffers, allocated once per process."""
+    if _bounce["bufs"] is None:
+        import torch
+
+        _bounce["bufs"] = [torch.empty(_CHUNK, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    return _bounce["bufs"]
+
+
+def _flat_bytes(t):
+    import torch
+
+    return t.reshape(-1).view(torch.uint8)
+
+
+def _h2d(out, src) -> None:
+    """The mapped shared memory `src` (uint8) -> the contiguous device tensor `out`: the CPU copies
+    one 64 MiB chunk into a pinned buffer while the DMA of the other runs. A .to(device) of the
+    pageable mapping goes through the HIP runtime's small staging buffers instead: 2 GiB took
+    501-567 ms that way against 80-106 ms this way (profiles/r5_shm_copy.json), and a 2.5 GB
+    TinyLM restore went from 760 ms to 113-141 ms (profiles/r5_rescue_restore_bounce.json)."""
+    import torch
+
+    d, n = _flat_bytes(out), src.numel()
+    stream = torch.cuda.current_stream(out.device)
+    with _bounce["lock"]:
+        pins = _pinned_pair()
+        evs = [torch.cuda.Event(), torch.cuda.Event()]
+        for i, o in enumerate(range(0, n, _CHUNK)):
+            k = min(_CHUNK, n - o)
+            if i >= 2:
+                evs[i % 2].synchronize()  # the DMA out of this buffer is done
+            pins[i % 2][:k].copy_(src[o:o + k])
+            d[o:o + k].copy_(pins[i % 2][:k], non_blocking=True)
+            evs[i % 2].record(stream)
+        for e in evs:  # the pair is free for the next copy
+            e.synchronize()
+
+
 class RescueSkipped(Exception):
     """A snapshot that cannot be taken this time (not enough shared memory) or ever (the state
     holds something that is not tensors, containers and scalars)."""
@@ -155,6 +199,7 @@ class Rescue:
         self.inflight = None  # the snapshot being written (see begin / finish)
         self.staging = os.environ.get("DEVSPACE_RESCUE_STAGING", "1") != "0"
         self._side = None  # the writer's HIP stream
+        self.recycle = os.environ.get("DEVSPACE_RESCUE_RECYCLE", "1") != "0"
         os.makedirs(root, exist_ok=True)
 
     # -- capture / apply ------------------------------------------------------------------
@@ -226,6 +271,20 @@ class Rescue:
     # -- files -----------------------------------------------------------------------------
     def _path(self, step, ext, rank=None):
         return os.path.join(self.root, f"rank{self.rank if rank is None else rank}-step{step}.{ext}")
+
+    def _spare(self) -> str:
+        return os.path.join(self.root, f"rank{self.rank}-spare.bin")
+
+    def _spare_bytes(self) -> int:
+        """Shared memory the group's spare files hold (each is reused by its rank's next write)."""
+        n = 0
+        for name in os.listdir(self.root):
+            if re.match(r"rank\d+-spare\.bin$", name):
+                try:
+                    n += os.path.getsize(os.path.join(self.root, name))
+                except OSError:
+                    pass
+        return n
 
     def due(self, step: int) -> bool:
         return (self.every_s > 0 and self.disabled is None and self.inflight is None and step > self.last_step
@@ -318,7 +377,7 @@ class Rescue:
             job["bytes"], job["total"] = load[self.rank], sum(load)
             job["state_bytes"] = sum(m["nbytes"] for m in metas)
             # the ranks of the pod write theirs into the same /dev/shm at the same time
-            free = shutil.disk_usage(self.root).free
+            free = shutil.disk_usage(self.root).free + self._spare_bytes()
             if job["total"] > free * 0.9:
                 raise RescueSkipped(f"{self.root} has {free >> 20} MiB free, the group's snapshot needs "
                                     f"{job['total'] >> 20} MiB")
@@ -373,13 +432,26 @@ class Rescue:
 
         size = meta["bytes"]
         binp, jsp = self._path(step, "bin"), self._path(step, "json")
-        with open(binp + ".tmp", "w+b") as f:
-            if size:
+        fresh = True
+        try:  # the superseded snapshot's file: its shared-memory pages are allocated already
+            os.replace(self._spare(), binp + ".tmp")
+            fresh = False
+        except OSError:
+            pass
+        with open(binp + ".tmp", "w+b" if fresh else "r+b") as f:
+            have = 0 if fresh else os.fstat(f.fileno()).st_size
+            if have > size:
+                os.ftruncate(f.fileno(), size)
+            elif have < size:
                 # reserve the pages first: a full tmpfs then fails here (ENOSPC), not as a SIGBUS
                 # on a store into the mapping
-                os.posix_fallocate(f.fileno(), 0, size)
-                # one copy per tensor, device (or host) straight into the mapped shared memory
-                mm = mmap.mmap(f.fileno(), size)
+                os.posix_fallocate(f.fileno(), have, size - have)
+            if size:
+                # one copy per tensor, device (or host) straight into the mapped shared memory.
+                # (Through a pinned bounce pair, as restores go, the runner's writes were slower:
+                # 934-1077 ms against 436-588 ms for 2.5 GB at the boundary on the MI355X box.)
+                # MAP_POPULATE: the pages are mapped in one call, not one fault per 4 KiB store.
+                mm = mmap.mmap(f.fileno(), size, flags=mmap.MAP_SHARED | getattr(mmap, "MAP_POPULATE", 0))
                 try:
                     buf = torch.frombuffer(mm, dtype=torch.uint8)
                     for t, off, n in own:
@@ -394,12 +466,23 @@ class Rescue:
         os.replace(jsp + ".tmp", jsp)  # the layout last: its presence marks a complete part
 
     def commit(self, step: int, ok: bool) -> None:
-        """Every rank wrote `step` (ok): drop this rank's older files; else drop this one."""
-        for name in os.listdir(self.root):
+        """Every rank wrote `step` (ok): drop this rank's older files; else drop this one. The
+        newest superseded data file is kept as the spare the next snapshot is written into (its
+        pages are allocated: a fresh 2 GiB file cost 119-272 ms of posix_fallocate on the
+        MI355X box), while the shared memory has room for another snapshot of its size besides."""
+        import shutil
+
+        for name in sorted(os.listdir(self.root), key=lambda x: -int((re.search(r"-step(\d+)\.", x) or [0, 0])[1])):
             m = re.match(rf"rank{self.rank}-step(\d+)\.(bin|json)(\.tmp)?$", name)
             if m and (int(m.group(1)) != step if ok else int(m.group(1)) == step):
+                path = os.path.join(self.root, name)
                 try:
-                    os.unlink(os.path.join(self.root, name))
+                    if (ok and m.group(2) == "bin" and not m.group(3) and self.recycle
+                            and not os.path.exists(self._spare())
+                            and shutil.disk_usage(self.root).free >= os.path.getsize(path)):
+                        os.replace(path, self._spare())
+                    else:
+                        os.unlink(path)
                 except OSError:
                     pass
         if ok:
@@ -459,7 +542,12 @@ class Rescue:
                 src = bufs[r][m["offset"]:m["offset"] + m["nbytes"]].view(dtype).view(m["shape"])
                 # own memory either way (the mappings are closed below)
                 on_gpu = m["device"] == "cuda" and device.type == "cuda"
-                tensors.append(src.to(device) if on_gpu else src.clone())
+                if on_gpu and m["nbytes"] >= _BOUNCE_MIN:
+                    out = torch.empty(m["shape"], dtype=dtype, device=device)
+                    _h2d(out, bufs[r][m["offset"]:m["offset"] + m["nbytes"]])
+                    tensors.append(out)
+                else:
+                    tensors.append(src.to(device) if on_gpu else src.clone())
                 del src
         finally:
             bufs.clear()

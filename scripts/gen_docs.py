@@ -201,6 +201,8 @@ ENV = {
     "DEVSPACE_RESCUE_EVERY_S": "Seconds between the runner's snapshots of the training state in /dev/shm (default "
                                "60, 0 = off): a group restarted after a failure resumes from the newest one "
                                "(`--rescue-every`).",
+    "DEVSPACE_RESCUE_RECYCLE": "`0`: a superseded rescue snapshot's file is deleted instead of kept as the spare "
+                               "the next snapshot is written into (its shared-memory pages already allocated).",
     "DEVSPACE_RESCUE_ROOT": "Where the runner keeps its rescue snapshot directories (default `/dev/shm`, the "
                             "pod's memory volume).",
     "DEVSPACE_RESCUE_STAGING": "`0`: a rescue snapshot is copied to shared memory at the step boundary even when "

@@ -71,7 +71,13 @@ def test_newer_snapshot_replaces_the_older_one(tmp_path):
     _take(r, mod, _ctx(step=7), _state(0))
     _take(r, mod, _ctx(step=9), _state(0))
     assert r.available(1, 1) == [9]
-    assert sorted(p.name for p in tmp_path.iterdir()) == ["rank0-step9.bin", "rank0-step9.json"]
+    # the superseded data file stays as the spare the next snapshot is written into
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["rank0-spare.bin", "rank0-step9.bin", "rank0-step9.json"]
+    _take(r, mod, _ctx(step=11), _state(0))
+    assert r.available(1, 1) == [11]
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["rank0-spare.bin", "rank0-step11.bin", "rank0-step11.json"]
+    snap, _ = r.load(11, torch.device("cpu"))  # written into the recycled file: intact
+    assert torch.equal(snap["t"], _state(0)["t"])
 
 
 def test_module_hooks_win_and_unserialisable_state_turns_snapshots_off(tmp_path):
@@ -134,6 +140,45 @@ def test_hbm_staged_snapshot_round_trip_on_the_gpu(tmp_path):
     for k, v in fresh["model"].state_dict().items():
         assert v.is_cuda and torch.equal(v, want[k]), k  # the snapshot's values, not the later ones
     assert fresh["n"] == 5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("staging", ["0", "1"])
+def test_large_device_tensors_round_trip_through_the_pinned_bounce(tmp_path, monkeypatch, staging):
+    """Large device tensors, written at the boundary or from the HBM-staged copy, into a fresh file
+    and then into the recycled spare, come back through two pinned 64 MiB buffers (sizes that end
+    inside a chunk included); smaller and non-contiguous ones take the direct copy. Every
+    snapshot restores bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from devspace_amd import rescue as rmod
+
+    monkeypatch.setenv("DEVSPACE_RESCUE_STAGING", staging)
+    dev = torch.device("cuda", 0)
+    ctx = runner.Context(0, 1, 0, dev)
+    torch.manual_seed(1)
+    state = {"a": torch.randn(37, 1 << 20, device=dev, dtype=torch.bfloat16),  # 74 MiB: 64 + 10
+             "b": torch.randn(50, 1 << 20, device=dev),  # 200 MiB: 3 x 64 + 8
+             "c": torch.randn(9, 1 << 18, device=dev),  # 9 MiB: one partial chunk
+             "d": torch.randn(1024, 1024, device=dev).t(),  # 4 MiB, non-contiguous: direct
+             "e": torch.randint(0, 2, (3, 1 << 23), device=dev).bool()}  # 24 MiB of bool
+    assert state["a"].numel() * 2 >= rmod._BOUNCE_MIN and not state["d"].is_contiguous()
+    r = runner.Rescue(str(tmp_path), 0, every_s=60)
+    for step in (5, 6, 7):
+        ctx.step = step
+        with torch.no_grad():
+            for k in ("a", "b", "c", "d"):
+                state[k].add_(1.0)
+        want = {k: v.clone() for k, v in state.items()}
+        job = _take(r, types.SimpleNamespace(), ctx, state)
+        assert job["err"] is None and job["staged"] == (staging == "1"), job
+        assert r.available(1, 1) == [step]
+        snap, _ = r.load(step, dev)
+        for k, v in want.items():
+            got = snap[k]
+            assert got.is_cuda and got.dtype == v.dtype and got.shape == v.shape, k
+            assert torch.equal(got, v), (step, k)
+    assert (tmp_path / "rank0-spare.bin").exists()  # steps 6 and 7 were written into the spare
 
 
 class _ThreadGroup:
