@@ -178,8 +178,10 @@ class Rescue:
     the example's 384 MiB) and a background thread streams that copy to shared memory on a side
     stream while training goes on. Training pauses only for the device copy; the ranks agree that
     every writer finished (two flags of the step-boundary all-reduce) before the older snapshots
-    are dropped. "Room" is memory the next steps will not need (`hbm_room`). Without room (or on
-    CPU) the copy to shared memory is made at the boundary itself.
+    are dropped. "Room" is memory the next steps will not need (`hbm_budget`). When the room holds
+    only part of it (a job near the HBM capacity), the largest device tensors that fit are staged
+    and only the rest is copied to shared memory at the boundary, so the pause shrinks by what was
+    staged. Without room (less than MIN_STAGE, or on CPU) the whole copy is made at the boundary.
 
     What is captured: a module's own `snapshot(ctx, state) -> obj` / `restore(ctx, state, obj)`
     when it defines them; otherwise, of a dict state, every entry with `state_dict()` /
@@ -187,6 +189,7 @@ class Rescue:
     scalars. Tensors come back on the device they were on (cuda → this rank's GPU)."""
 
     ALIGN = 64
+    MIN_STAGE = 256 << 20  # HBM room below this stages nothing: the whole snapshot is copied at the boundary
 
     def __init__(self, root: str, rank: int, every_s: float, agree=None):
         self.root = root
@@ -303,7 +306,12 @@ class Rescue:
         state size of the HBM capacity went out of memory in step().)"""
         return free + reserved - peak >= nbytes * 1.1 + margin
 
-    def _hbm_room(self, nbytes: int, device) -> bool:
+    @staticmethod
+    def hbm_budget(free, reserved, peak, margin=256 << 20) -> int:
+        """The largest staged copy hbm_room allows: bytes of HBM the next steps do not need."""
+        return max(0, int((free + reserved - peak - margin) / 1.1))
+
+    def _hbm_budget(self, device) -> int:
         import torch
 
         try:
@@ -311,8 +319,8 @@ class Rescue:
             reserved = torch.cuda.memory_reserved(device)
             peak = torch.cuda.max_memory_allocated(device)
         except RuntimeError:  # no answer from the runtime: copy at the boundary instead
-            return False
-        return self.hbm_room(nbytes, free, reserved, peak)
+            return 0
+        return self.hbm_budget(free, reserved, peak)
 
     def steady(self, device) -> None:
         """Training is past its start-up: the step's peak is measured from here (the staging
@@ -386,15 +394,41 @@ class Rescue:
                     "time": time.time(), "bytes": load[self.rank], "files": files, "tensors": metas, "tree": tree}
             own = [(tensors[i], off, n) for i, off, n in mine]
             dev_bytes = sum(n for t, _, n in own if t.device.type == "cuda")
-            if self.staging and dev_bytes and ctx.device.type == "cuda" and self._hbm_room(dev_bytes, ctx.device):
-                start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                with torch.no_grad():
-                    start.record()
-                    copies = [(t.detach().clone(), off, n) for t, off, n in own]  # host tensors change too
-                    end.record()
+            budget = 0
+            if self.staging and dev_bytes and ctx.device.type == "cuda":
+                budget = self._hbm_budget(ctx.device)
+            if budget >= dev_bytes:  # (also: nothing on the device) everything is staged
+                staged, rest = list(own) if budget else [], [] if budget else list(own)
+            else:
+                # HBM holds part of it: stage the largest device tensors that fit, copy the rest
+                # at the boundary (the pause shrinks by what is staged)
+                staged, rest, left = [], [], budget
+                for t, off, n in sorted(own, key=lambda x: -x[2]):
+                    if t.device.type == "cuda" and n <= left and budget >= self.MIN_STAGE:
+                        staged.append((t, off, n))
+                        left -= n
+                    else:
+                        rest.append((t, off, n))
+            if staged:
+                part = self._open(ctx.step, meta["bytes"])
+                try:
+                    if rest:  # the live tensors the background write cannot see unchanged
+                        self._fill(part, [(t.detach(), off, n) for t, off, n in rest])
+                        job["boundary_bytes"] = sum(n for _, _, n in rest)
+                    boundary_ms = (time.perf_counter() - t0) * 1000.0
+                    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    with torch.no_grad():
+                        start.record()
+                        copies = [(t.detach().clone(), off, n) for t, off, n in staged]  # host tensors change too
+                        end.record()
+                except BaseException:
+                    self._close(part)
+                    raise
                 job["staged"] = True
+                job["staged_bytes"] = sum(n for _, _, n in staged)
                 job["thread"] = threading.Thread(target=self._write_job, name="devspace-rescue-writer", daemon=True,
-                                                 args=(job, copies, meta, ctx.device, (start, end)))
+                                                 args=(job, copies, meta, ctx.device, (start, end), part,
+                                                       boundary_ms if rest else 0.0))
                 job["thread"].start()
             else:
                 self._write_job(job, [(t.detach(), off, n) for t, off, n in own], meta, None, None)
@@ -403,7 +437,7 @@ class Rescue:
             job["err"] = str(e) if isinstance(e, RescueSkipped) else f"{type(e).__name__}: {e}"
             job["done"] = True
 
-    def _write_job(self, job, own, meta, device, events) -> None:
+    def _write_job(self, job, own, meta, device, events, part=None, boundary_ms=0.0) -> None:
         import torch
 
         t0 = time.perf_counter()
@@ -414,10 +448,10 @@ class Rescue:
                     self._side = torch.cuda.Stream(device=device)
                 self._side.wait_event(events[1])
                 with torch.cuda.stream(self._side):
-                    self._write(job["step"], own, meta)
-                job["pause_ms"] = events[0].elapsed_time(events[1])
+                    self._write(job["step"], own, meta, part)
+                job["pause_ms"] = boundary_ms + events[0].elapsed_time(events[1])
             else:
-                self._write(job["step"], own, meta)
+                self._write(job["step"], own, meta, part)
         except Exception as e:  # shared memory full (SIGBUS is not an exception: sized above), I/O
             job["err"] = f"{type(e).__name__}: {e}"
         finally:
@@ -425,20 +459,20 @@ class Rescue:
             job["write_ms"] = (time.perf_counter() - t0) * 1000.0
             job["done"] = True
 
-    def _write(self, step, own, meta) -> None:
-        import json
-
+    def _open(self, step, size):
+        """This rank's data file of `step` (as .tmp), sized and mapped: [file, mapping or None,
+        uint8 tensor over it or None, step]."""
         import torch
 
-        size = meta["bytes"]
-        binp, jsp = self._path(step, "bin"), self._path(step, "json")
+        binp = self._path(step, "bin")
         fresh = True
         try:  # the superseded snapshot's file: its shared-memory pages are allocated already
             os.replace(self._spare(), binp + ".tmp")
             fresh = False
         except OSError:
             pass
-        with open(binp + ".tmp", "w+b" if fresh else "r+b") as f:
+        f = open(binp + ".tmp", "w+b" if fresh else "r+b")
+        try:
             have = 0 if fresh else os.fstat(f.fileno()).st_size
             if have > size:
                 os.ftruncate(f.fileno(), size)
@@ -446,20 +480,43 @@ class Rescue:
                 # reserve the pages first: a full tmpfs then fails here (ENOSPC), not as a SIGBUS
                 # on a store into the mapping
                 os.posix_fallocate(f.fileno(), have, size - have)
-            if size:
-                # one copy per tensor, device (or host) straight into the mapped shared memory.
-                # (Through a pinned bounce pair, as restores go, the runner's writes were slower:
-                # 934-1077 ms against 436-588 ms for 2.5 GB at the boundary on the MI355X box.)
-                # MAP_POPULATE: the pages are mapped in one call, not one fault per 4 KiB store.
-                mm = mmap.mmap(f.fileno(), size, flags=mmap.MAP_SHARED | getattr(mmap, "MAP_POPULATE", 0))
-                try:
-                    buf = torch.frombuffer(mm, dtype=torch.uint8)
-                    for t, off, n in own:
-                        if n:
-                            buf[off:off + n].view(t.dtype).view(t.shape).copy_(t)
-                    del buf
-                finally:
-                    _close_mapping(mm)
+            if not size:
+                return [f, None, None, step]
+            # MAP_POPULATE: the pages are mapped in one call, not one fault per 4 KiB store
+            mm = mmap.mmap(f.fileno(), size, flags=mmap.MAP_SHARED | getattr(mmap, "MAP_POPULATE", 0))
+        except BaseException:
+            f.close()
+            raise
+        return [f, mm, torch.frombuffer(mm, dtype=torch.uint8), step]
+
+    @staticmethod
+    def _fill(part, own) -> None:
+        """One copy per tensor, device (or host) straight into the mapped shared memory. (Through
+        a pinned bounce pair, as restores go, the runner's writes were slower: 934-1077 ms against
+        436-588 ms for 2.5 GB at the boundary on the MI355X box.)"""
+        buf = part[2]
+        for t, off, n in own:
+            if n:
+                buf[off:off + n].view(t.dtype).view(t.shape).copy_(t)
+
+    @staticmethod
+    def _close(part) -> None:
+        f, mm = part[0], part[1]
+        part[2] = None
+        if mm is not None:
+            _close_mapping(mm)
+        f.close()
+
+    def _write(self, step, own, meta, part=None) -> None:
+        import json
+
+        part = part if part is not None else self._open(step, meta["bytes"])
+        try:
+            if own:
+                self._fill(part, own)
+        finally:
+            self._close(part)
+        binp, jsp = self._path(step, "bin"), self._path(step, "json")
         with open(jsp + ".tmp", "w") as f:
             json.dump(meta, f)
         os.replace(binp + ".tmp", binp)
@@ -571,6 +628,9 @@ def _rescue_finish(rescue, ctx, failed: bool) -> None:
         ctx.log(f"rescue snapshots off ({why})")
         return
     how = "staged in HBM, written in the background" if job["staged"] else "written at the step boundary"
+    if job["staged"] and job.get("boundary_bytes"):
+        how = (f"{job['staged_bytes'] / 2**20:.0f} MiB staged in HBM, {job['boundary_bytes'] / 2**20:.0f} MiB "
+               f"copied at the step boundary, written in the background")
     ctx.log(f"rescue snapshot step={job['step']} gen={job['gen']} {job['bytes'] / 2**20:.1f} MiB/rank: "
             f"training paused {job['pause_ms']:.2f} ms, {how} in {job['write_ms']:.1f} ms "
             f"(group: {job['total'] / 2**20:.1f} MiB in shared memory for "

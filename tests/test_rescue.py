@@ -181,6 +181,44 @@ def test_large_device_tensors_round_trip_through_the_pinned_bounce(tmp_path, mon
     assert (tmp_path / "rank0-spare.bin").exists()  # steps 6 and 7 were written into the spare
 
 
+@pytest.mark.gpu
+def test_partial_hbm_staging_copies_only_the_overflow_at_the_boundary(tmp_path):
+    """A job near the HBM capacity: the room holds part of the state. The largest device tensors
+    that fit are staged, the rest is copied at the boundary; the step that runs while the writer
+    works changes neither part of the snapshot."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda", 0)
+    ctx = runner.Context(0, 1, 0, dev)
+    ctx.step = 3
+    mib = 1 << 20
+    state = {"a": torch.randn(75, mib, device=dev),  # 300 MiB: staged
+             "b": torch.randn(50, mib, device=dev),  # 200 MiB: at the boundary
+             "c": torch.randn(25, mib, device=dev),  # 100 MiB: at the boundary (does not fit after a)
+             "h": torch.randn(1000)}  # host: at the boundary
+    want = {k: v.clone() for k, v in state.items()}
+    r = runner.Rescue(str(tmp_path), 0, every_s=60)
+    r._hbm_budget = lambda device: 320 * mib
+    r.begin(types.SimpleNamespace(), ctx, state, gen=1, setup_version=1)
+    job = r.inflight
+    assert job["staged"] and job["staged_bytes"] == 300 * mib, job
+    assert job["boundary_bytes"] == 300 * mib + 4000, job
+    with torch.no_grad():  # the next step
+        for v in state.values():
+            v.add_(1.0)
+    job["thread"].join()
+    assert job["err"] is None, job
+    runner._rescue_finish(r, ctx, False)
+    snap, _ = r.load(3, dev)
+    for k, v in want.items():
+        assert torch.equal(snap[k].cpu(), v.cpu()), k
+    # too little room for anything worth staging: all of it at the boundary
+    r2 = runner.Rescue(str(tmp_path / "b"), 0, every_s=60)
+    r2._hbm_budget = lambda device: runner.Rescue.MIN_STAGE - 1
+    job2 = _take(r2, types.SimpleNamespace(), ctx, state)
+    assert job2["err"] is None and not job2["staged"], job2
+
+
 class _ThreadGroup:
     """The Agreement's all-gather for ranks simulated as threads of one process."""
 
@@ -303,6 +341,16 @@ def test_digests_tell_apart_what_differs():
     d = digests([x, x.clone(), y, x.view(torch.int32), base[1:], torch.ones(3, dtype=torch.bool), torch.zeros(0, 3)])
     assert d[0] == d[1] and d[0] != d[2] and d[0] != d[3]  # same bytes, other dtype: not the same tensor
     assert d[4] == digests([base[1:].clone()])[0]  # a view at an odd offset
+
+
+def test_staging_budget_is_the_largest_copy_the_room_allows():
+    gib = 1 << 30
+    for free, reserved, peak in ((10 * gib, 4 * gib, 3 * gib), (gib, 0, 0), (0, 2 * gib, 2 * gib)):
+        b = runner.Rescue.hbm_budget(free, reserved, peak)
+        assert b >= 0
+        if b:
+            assert runner.Rescue.hbm_room(b - 16, free, reserved, peak)
+            assert not runner.Rescue.hbm_room(b + (1 << 20), free, reserved, peak)
 
 
 def test_staging_room_leaves_the_steps_their_peak():
