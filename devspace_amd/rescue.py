@@ -410,7 +410,9 @@ class Rescue:
                     else:
                         rest.append((t, off, n))
             if staged:
-                part = self._open(ctx.step, meta["bytes"])
+                # the file is sized and mapped at the boundary only for a part written there; else
+                # the background writer does it (a fresh 2 GiB file is 119-272 ms of fallocate)
+                part = self._open(ctx.step, meta["bytes"]) if rest else None
                 try:
                     if rest:  # the live tensors the background write cannot see unchanged
                         self._fill(part, [(t.detach(), off, n) for t, off, n in rest])
@@ -422,7 +424,8 @@ class Rescue:
                         copies = [(t.detach().clone(), off, n) for t, off, n in staged]  # host tensors change too
                         end.record()
                 except BaseException:
-                    self._close(part)
+                    if part is not None:
+                        self._close(part)
                     raise
                 job["staged"] = True
                 job["staged_bytes"] = sum(n for _, _, n in staged)
