@@ -54,7 +54,8 @@ def _h2d(out, src) -> None:
 
     d, n = _flat_bytes(out), src.numel()
     stream = torch.cuda.current_stream(out.device)
-    with _bounce["lock"]:
+    # (the copies go to the current device's current stream: make that `out`'s, the events' one)
+    with _bounce["lock"], torch.cuda.device(out.device):
         pins = _pinned_pair()
         evs = [torch.cuda.Event(), torch.cuda.Event()]
         for i, o in enumerate(range(0, n, _CHUNK)):
