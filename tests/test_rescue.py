@@ -80,6 +80,30 @@ def test_newer_snapshot_replaces_the_older_one(tmp_path):
     assert torch.equal(snap["t"], _state(0)["t"])
 
 
+def test_no_spare_is_kept_without_room_for_another_snapshot(tmp_path, monkeypatch):
+    """The superseded file is kept for the next write only while /dev/shm could hold another
+    snapshot of its size besides (others — DataLoader workers, RCCL — share it); and never with
+    DEVSPACE_RESCUE_RECYCLE=0."""
+    import collections
+    import shutil
+
+    mod = types.SimpleNamespace()
+    r = runner.Rescue(str(tmp_path / "full"), 0, every_s=60)
+    real = shutil.disk_usage
+    _take(r, mod, _ctx(step=7), _state(0))
+    usage = collections.namedtuple("u", "total used free")
+    frees = iter([1 << 30, 100])  # begin's room check: room; commit's check for a spare: none
+    monkeypatch.setattr(shutil, "disk_usage", lambda p: usage(1 << 31, 1 << 30, next(frees)))
+    _take(r, mod, _ctx(step=9), _state(0))
+    monkeypatch.setattr(shutil, "disk_usage", real)
+    assert sorted(p.name for p in (tmp_path / "full").iterdir()) == ["rank0-step9.bin", "rank0-step9.json"]
+    monkeypatch.setenv("DEVSPACE_RESCUE_RECYCLE", "0")
+    r2 = runner.Rescue(str(tmp_path / "off"), 0, every_s=60)
+    _take(r2, mod, _ctx(step=7), _state(0))
+    _take(r2, mod, _ctx(step=9), _state(0))
+    assert sorted(p.name for p in (tmp_path / "off").iterdir()) == ["rank0-step9.bin", "rank0-step9.json"]
+
+
 def test_module_hooks_win_and_unserialisable_state_turns_snapshots_off(tmp_path):
     seen = {}
     mod = types.SimpleNamespace(snapshot=lambda ctx, state: {"w": state["w"] * 2},
