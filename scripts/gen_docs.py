@@ -148,7 +148,23 @@ ENV = {
                        "the binary).",
     "DEVSPACE_INIT_NO_NODE_DISCOVERY": "`devspace init` does not read the cluster's nodes to size GPU pods (per-GPU "
                                        "defaults are used).",
-    "DEVSPACE_NONINTERACTIVE": "Never prompt: every question takes its default (CI); also skips the update check.",
+    "DEVSPACE_INIT_GPUS": "Answers `devspace init`'s GPU-count question (same as `--gpus`).",
+    "DEVSPACE_INIT_IMAGE": "Answers `devspace init`'s image question (same as `--image`); with it, no Docker Hub "
+                           "account is needed.",
+    "DEVSPACE_INIT_LANGUAGE": "Answers `devspace init`'s language question (same as `--language`).",
+    "DEVSPACE_INIT_NAMESPACE": "Answers `devspace init`'s namespace question (same as `--namespace`).",
+    "DEVSPACE_INIT_PORT": "Answers `devspace init`'s port question (same as `--port`).",
+    "DEVSPACE_INIT_PULL_SECRET": "Answers `devspace init`'s pull-secret question, `yes` or `no` (same as "
+                                 "`--pullSecret`).",
+    "DEVSPACE_INIT_REGISTRY": "Answers `devspace init`'s registry question (same as `--registry`).",
+    "DEVSPACE_NONINTERACTIVE": "Never prompt and never read stdin, whatever it is (an open pipe included): every "
+                               "question takes its flag, its `DEVSPACE_INIT_*` variable or its default, or the "
+                               "command fails naming what to set (CI); also skips the update check.",
+    "DEVSPACE_SCAN_MAX_MS": "Longest interval of the stat-scan file watcher (default 1000).",
+    "DEVSPACE_SCAN_MIN_MS": "Shortest interval of the stat-scan file watcher (default 20); the interval otherwise "
+                            "follows the scan's cost (at most 5 % of a core).",
+    "DEVSPACE_WATCHER": "`scan`: watch sync paths with the portable stat-scan watcher instead of the platform's "
+                        "event backend (inotify on Linux). The portable build always scans.",
     "DEVSPACE_PORTFORWARD_HEDGE": "`0`: a held GET/HEAD/OPTIONS on a remote cluster is retried one stream at a time "
                                   "(by default a new attempt goes out every third of a round trip; the app may see "
                                   "the request up to about four times).",

@@ -82,6 +82,8 @@ void configure_cluster_local(Value& cfg) {
   prompt::Params p;
   p.question = "Which namespace should the app run in?";
   p.default_value = "default";
+  p.key = "namespace";
+  p.env = "DEVSPACE_INIT_NAMESPACE";
   std::string ns = prompt::ask(p);
   cfg["cluster"]["kubeContext"] = current;
   cfg["cluster"]["namespace"] = ns;
@@ -110,6 +112,9 @@ void add_default_ports(Value& cfg, InitState& st) {
   p.question = "Which port is the app listening on? (Default: " + def + ")";
   p.default_value = "";
   p.optional = true;  // the default is applied below
+  p.key = "port";
+  p.env = "DEVSPACE_INIT_PORT";
+  p.validation_regex = "[0-9]{0,5}";
   std::string port = prompt::ask(p);
   if (port.empty()) port = def;
   Value pms = Value::seq();
@@ -288,6 +293,8 @@ int run_init(cli::Command& c, const std::vector<std::string>&) {
     p.question = "Select programming language of project";
     p.default_value = detected;
     p.options = langs;
+    p.key = "language";
+    p.env = "DEVSPACE_INIT_LANGUAGE";
     st.language = prompt::ask(p);
     if (st.language == "rocm-pytorch") {
       prompt::Params g;
@@ -302,6 +309,8 @@ int run_init(cli::Command& c, const std::vector<std::string>&) {
                           big != nullptr ? big->resource.c_str() : "amd.com/gpu (MI355X GPU)", max, on.c_str());
       g.default_value = "1";
       g.validation_regex = gpu::range_regex(max);
+      g.key = "gpus";
+      g.env = "DEVSPACE_INIT_GPUS";
       st.gpus = prompt::ask(g);
       st.sizing = discover_sizing(std::atoi(st.gpus.c_str()), nodes);
     }
@@ -388,7 +397,15 @@ void register_init(cli::Command& root) {
       .boolean("overwrite", "o", false, "Overwrite existing chart files and Dockerfile")
       .str("templateRepoUrl", "", "", "Git repository for chart templates (embedded templates when empty)")
       .str("templateRepoPath", "", "", "Local path of a chart template repository (embedded templates when empty)")
-      .boolean("cloud", "", false, "Use a DevSpace cloud provider for this project");
+      .boolean("cloud", "", false, "Use a DevSpace cloud provider for this project")
+      // every question has an answer on the command line (CI, DEVSPACE_NONINTERACTIVE=1)
+      .str("language", "", "", "Programming language of the project (skips the question)")
+      .str("gpus", "", "", "GPU devices the container requests, rocm-pytorch only (skips the question)")
+      .str("namespace", "", "", "Namespace the app runs in (skips the question)")
+      .str("port", "", "", "Port the app listens on (skips the question)")
+      .str("registry", "", "", "Registry to push to: hub.docker.com or a URL (skips the question)")
+      .str("image", "", "", "Image name to push to; no Docker Hub account needed (skips the question)")
+      .str("pullSecret", "", "", "Create a pull secret for the image: yes | no (skips the question)");
   c->run = [](cli::Command& cc, const std::vector<std::string>& a) {
     std::string url = cc.get_str("templateRepoUrl");
     if (!url.empty() && cc.get_str("templateRepoPath").empty()) {
@@ -398,6 +415,8 @@ void register_init(cli::Command& root) {
       if (r.code != 0) log::fatal("Error cloning template repository " + url + ": " + r.err);
       cc.flag("templateRepoPath")->s = dir;
     }
+    for (const char* k : {"language", "gpus", "namespace", "port", "registry", "image", "pullSecret"})
+      if (cc.flag(k)->changed || !cc.get_str(k).empty()) prompt::set_answer(k, cc.get_str(k));
     return run_init(cc, a);
   };
   root.add(std::move(c));

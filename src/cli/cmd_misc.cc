@@ -27,6 +27,7 @@
 #include "upgrade/upgrade.h"
 #include "services/services.h"
 #include "sync/sync.h"
+#include "platform/platform.h"
 
 namespace ds {
 namespace cmd {
@@ -35,13 +36,7 @@ namespace {
 
 using Args = std::vector<std::string>;
 
-std::string self_exe() {
-  char buf[PATH_MAX];
-  ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);
-  if (n <= 0) return "";
-  buf[n] = 0;
-  return buf;
-}
+std::string self_exe() { return plat::self_exe(); }
 
 // envutil.AddToPath: append an export line to the user's shell profile (idempotent).
 int run_install(cli::Command&, const Args&) {
@@ -88,9 +83,9 @@ static std::string parse_version_line(const std::string& out) {
 }
 
 // Self-update (upgrade.go:69 Upgrade): from a local binary (--from), a plain mirror
-// (DEVSPACE_RELEASE_URL serving "<url>/latest", "<url>/devspace-linux-amd64" and its ".sha256"),
+// (DEVSPACE_RELEASE_URL serving "<url>/latest", "<url>/devspace-<os>-<arch>" and its ".sha256"),
 // or the newest GitHub release of this product's release channel (DEVSPACE_RELEASE_REPO) with
-// a linux/amd64 asset. Every candidate must be this product; downloads must match a published
+// an asset for this OS/arch (plat::release_target). Every candidate must be this product; downloads must match a published
 // SHA-256.
 int run_upgrade(cli::Command& c, const Args&) {
   log::start_file_logging();
@@ -120,11 +115,11 @@ int run_upgrade(cli::Command& c, const Args&) {
         fs::copy(from, staged, true);
       } else {
         std::string base = trim_right(url, "/");
-        std::string bin = helmrepo::fetch(base + "/devspace-linux-amd64");
-        std::string want = upgrade::published_sha256(helmrepo::fetch(base + "/devspace-linux-amd64.sha256"),
-                                                     "devspace-linux-amd64");
+        std::string asset = "devspace-" + plat::release_target();
+        std::string bin = helmrepo::fetch(base + "/" + asset);
+        std::string want = upgrade::published_sha256(helmrepo::fetch(base + "/" + asset + ".sha256"), asset);
         if (want.empty() || sha256_hex(bin) != want)
-          throw std::runtime_error("devspace-linux-amd64 does not match its published SHA-256");
+          throw std::runtime_error(asset + " does not match its published SHA-256");
         if (!upgrade::is_this_product(bin))
           throw std::runtime_error("the mirror's binary is not a " + std::string(upgrade::kProductId) + " build");
         fs::write_file(staged, bin, 0755);

@@ -8,6 +8,7 @@
 #include "core/fs.h"
 #include "core/log.h"
 #include "core/prompt.h"
+#include "platform/platform.h"
 
 namespace ds {
 namespace cmd {
@@ -62,11 +63,9 @@ std::shared_ptr<kube::Client> make_kube(const Value& cfg, bool switch_context) {
 std::string helper_path() {
   const char* env = getenv("DEVSPACE_HELPER");
   if (env && *env) return env;
-  char buf[PATH_MAX];
-  ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);
-  if (n <= 0) return "";
-  buf[n] = 0;
-  return fs::join(fs::dirname(buf), "devspace-helper");
+  std::string exe = plat::self_exe();
+  if (exe.empty()) return "";
+  return fs::join(fs::dirname(exe), "devspace-helper");
 }
 
 void cloud_configure(config::Context& ctx, const std::string& space_name) {

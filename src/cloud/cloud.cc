@@ -18,6 +18,7 @@
 #include "core/prompt.h"
 #include "core/strutil.h"
 #include "kube/kubeconfig.h"
+#include "platform/platform.h"
 
 namespace ds {
 namespace cloud {
@@ -207,7 +208,7 @@ std::vector<std::string> Client::registries() {
 }
 
 std::string Client::login_via_browser(int timeout_s) {
-  int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  int fd = plat::socket_cloexec(AF_INET, SOCK_STREAM);
   int one = 1;
   setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
   struct sockaddr_in a{};

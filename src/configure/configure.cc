@@ -551,6 +551,8 @@ void init_image(config::Context& ctx, const std::string& docker_username_in, boo
     prompt::Params p;
     p.question = "Which registry do you want to push to? ('hub.docker.com' or URL)";
     p.default_value = "hub.docker.com";
+    p.key = "registry";
+    p.env = "DEVSPACE_INIT_REGISTRY";
     registry = prompt::ask(p);
   } else {
     std::string provider = cfg.at_path("cluster.cloudProvider").as_string(cloud::kDefaultProviderName);
@@ -559,14 +561,20 @@ void init_image(config::Context& ctx, const std::string& docker_username_in, boo
     registry = regs.empty() ? "hub.docker.com" : regs[0];
   }
   build::DockerConfigFile dcf = build::DockerConfigFile::load();
-  if (registry != "hub.docker.com") {
+  // an image named up front (--image / DEVSPACE_INIT_IMAGE) needs no account to derive it from
+  const char* env_image = getenv("DEVSPACE_INIT_IMAGE");
+  prompt::Params image_q;
+  image_q.key = "image";
+  image_q.env = "DEVSPACE_INIT_IMAGE";
+  bool image_given = prompt::has_answer("image") || (env_image && *env_image);
+  if (!image_given && registry != "hub.docker.com") {
     build::AuthConfig a = dcf.get(registry);
     if (a.username.empty() && !is_cloud && fs::exists(registry) == false) {
       // A local/insecure registry (e.g. the devspace local cluster) needs no credentials.
       log::warn("No credentials found for " + registry + " (run `docker login " + registry + "` if it needs auth)");
     }
     if (!a.username.empty()) username = a.username;
-  } else if (username.empty()) {
+  } else if (!image_given && username.empty()) {
     build::AuthConfig a = dcf.get("https://index.docker.io/v1/");
     username = a.username;
     if (username.empty()) {
@@ -575,12 +583,17 @@ void init_image(config::Context& ctx, const std::string& docker_username_in, boo
       log::warn("Installing docker is NOT required\n");
       // a Docker Hub image needs an account namespace (the reference loops on docker login,
       // configure/init_image.go:63-90): never fall through to an image named "/devspace"
-      for (int attempt = 0; attempt < 3 && username.empty(); ++attempt)
-        username = trim(prompt::ask("What is your docker hub username?", ""));
+      for (int attempt = 0; attempt < 3 && username.empty(); ++attempt) {
+        prompt::Params u;
+        u.question = "What is your docker hub username?";
+        u.optional = true;
+        username = trim(prompt::ask(u));
+        if (prompt::noninteractive_env()) break;
+      }
       if (username.empty())
         throw std::runtime_error(
-            "a Docker Hub username is required to push to Docker Hub (or answer the registry question with "
-            "another registry, e.g. a local one)");
+            "a Docker Hub username is required to push to Docker Hub: set --image (DEVSPACE_INIT_IMAGE) to name "
+            "the image, or --registry (DEVSPACE_INIT_REGISTRY) for another registry, or run `docker login`");
       prompt::Params pw;
       pw.question = "What is your docker hub password?";
       pw.is_password = true;
@@ -595,8 +608,12 @@ void init_image(config::Context& ctx, const std::string& docker_username_in, boo
     }
   }
   std::string image;
-  prompt::Params p;
-  if (registry == "hub.docker.com") {
+  prompt::Params p = image_q;
+  if (image_given) {
+    p.question = "Which image name do you want to push to?";
+    p.validation_regex = "[a-zA-Z0-9\\.:/_-]{1,200}";
+    image = prompt::ask(p);
+  } else if (registry == "hub.docker.com") {
     p.question = "Which image name do you want to use on Docker Hub?";
     p.default_value = username + "/devspace";
     p.validation_regex = "[a-zA-Z0-9/-]{4,60}";
@@ -611,6 +628,7 @@ void init_image(config::Context& ctx, const std::string& docker_username_in, boo
     p.default_value = registry + "/" + project + "/devspace";
     image = prompt::ask(p);
   } else if (is_cloud) {
+    p = prompt::Params();
     image = registry + "/" + username + "/devspace";
   } else {
     p.question = "Which image name do you want to push to?";
@@ -624,6 +642,8 @@ void init_image(config::Context& ctx, const std::string& docker_username_in, boo
     q.question = "Do you want to enable automatic creation of pull secrets for this image? (yes | no)";
     q.default_value = "yes";
     q.validation_regex = "(yes|no)";
+    q.key = "pullSecret";
+    q.env = "DEVSPACE_INIT_PULL_SECRET";
     pull_secret = prompt::ask(q) == "yes";
   }
   std::string why = build::image_reference_problem(image);

@@ -15,6 +15,7 @@
 #include "core/codec.h"
 #include "core/proc.h"
 #include "core/strutil.h"
+#include "platform/platform.h"
 
 namespace ds {
 
@@ -351,13 +352,8 @@ bool SpillBuffer::append(const char* d, size_t n) {
       return true;
     }
     // unlinked from the start: nothing is left behind whatever way the process ends
-    fd_ = ::open(dir_.c_str(), O_TMPFILE | O_RDWR | O_CLOEXEC, 0600);
-    if (fd_ < 0) {
-      std::string tmpl = dir_ + "/devspace-spill-XXXXXX";
-      fd_ = ::mkstemp(&tmpl[0]);
-      if (fd_ < 0) return false;
-      ::unlink(tmpl.c_str());
-    }
+    fd_ = plat::open_unlinked_tmp(dir_);
+    if (fd_ < 0) return false;
     stage_.swap(mem_);
     std::string().swap(mem_);
   }

@@ -15,6 +15,7 @@
 #include <stdexcept>
 
 #include "core/strutil.h"
+#include "platform/platform.h"
 
 namespace ds {
 namespace fs {
@@ -26,8 +27,9 @@ static StatInfo from_stat(const struct stat& st) {
   s.is_reg = S_ISREG(st.st_mode);
   s.is_symlink = S_ISLNK(st.st_mode);
   s.size = st.st_size;
-  s.mtime_sec = st.st_mtim.tv_sec;
-  s.mtime_nsec = st.st_mtim.tv_nsec;
+  int64_t mt = plat::mtime_ns(st);
+  s.mtime_sec = mt / 1000000000LL;
+  s.mtime_nsec = mt % 1000000000LL;
   s.mode = st.st_mode;
   s.uid = st.st_uid;
   s.gid = st.st_gid;

@@ -14,7 +14,6 @@
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 #include <poll.h>
-#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
@@ -29,6 +28,7 @@
 
 #include "core/codec.h"
 #include "core/strutil.h"
+#include "platform/platform.h"
 
 namespace ds {
 namespace net {
@@ -61,26 +61,15 @@ int wait_fd(int fd, short ev, int timeout_ms) {
   }
 }
 
-// Waits for `ev` on fd or for a poke on the eventfd `wake` (drained here). >0 ready, 0 timeout.
-int wait_fd_or_wake(int fd, short ev, int wake, int timeout_ms) {
-  struct pollfd pf[2] = {{fd, ev, 0}, {wake, POLLIN, 0}};
+// Waits for `ev` on fd or for a poke of `wake` (drained here). >0 ready, 0 timeout.
+int wait_fd_or_wake(int fd, short ev, plat::Waker& wake, int timeout_ms) {
+  struct pollfd pf[2] = {{fd, ev, 0}, {wake.fd(), POLLIN, 0}};
   while (true) {
-    int r = ::poll(pf, wake >= 0 ? 2 : 1, timeout_ms);
+    int r = ::poll(pf, wake.ok() ? 2 : 1, timeout_ms);
     if (r < 0 && errno == EINTR) continue;
-    if (r > 0 && wake >= 0 && (pf[1].revents & POLLIN)) {
-      uint64_t v;
-      ssize_t got = ::read(wake, &v, sizeof(v));
-      (void)got;
-    }
+    if (r > 0 && wake.ok() && (pf[1].revents & POLLIN)) wake.drain();
     return r;
   }
-}
-
-void poke(int wake) {
-  if (wake < 0) return;
-  uint64_t one = 1;
-  ssize_t w = ::write(wake, &one, sizeof(one));
-  (void)w;
 }
 
 std::string ssl_error_string() {
@@ -116,7 +105,7 @@ class PlainConn : public Conn {
   bool write_all(const void* d, size_t n) override {
     const char* p = (const char*)d;
     while (n) {
-      ssize_t w = ::send(fd_, p, n, MSG_NOSIGNAL);
+      ssize_t w = plat::send_nosignal(fd_, p, n);
       if (w < 0) {
         if (errno == EINTR) continue;
         return false;
@@ -256,7 +245,7 @@ std::string peer_key(int fd) {
 // TLS over a non-blocking socket. SSL_read/SSL_write run under ssl_mu_ only for the duration
 // of the call; waiting (poll) happens with no lock held, so a reader blocked on an idle
 // stream never holds up a concurrent writer. A writer that makes OpenSSL buffer incoming
-// records (TLS 1.2 renegotiation) pokes the eventfd so the parked reader re-checks.
+// records (TLS 1.2 renegotiation) pokes the waker so the parked reader re-checks.
 class TlsConn : public Conn {
  public:
   using Conn::write_all;
@@ -264,7 +253,6 @@ class TlsConn : public Conn {
     try {
       int fl = fcntl(fd_, F_GETFL);
       fcntl(fd_, F_SETFL, fl | O_NONBLOCK);
-      wake_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
       bool resume = !reference_timing();
       std::string digest;
       ctx_ = resume ? shared_ctx(t, &digest) : make_ctx(t);
@@ -372,7 +360,7 @@ class TlsConn : public Conn {
         if (w <= 0) err = SSL_get_error(ssl_, w);
         pending = SSL_has_pending(ssl_) == 1;
       }
-      if (pending) poke(wake_);  // we pulled records the reader has to see
+      if (pending) wake_.poke();  // we pulled records the reader has to see
       if (w > 0) {
         p += w;
         n -= (size_t)w;
@@ -393,7 +381,7 @@ class TlsConn : public Conn {
   void shutdown() override {
     shut_ = true;
     ::shutdown(fd_, SHUT_RDWR);
-    poke(wake_);
+    wake_.poke();
   }
   int fd() const override { return fd_; }
 
@@ -422,11 +410,9 @@ class TlsConn : public Conn {
     ctx_ = nullptr;
     if (fd_ >= 0) ::close(fd_);
     fd_ = -1;
-    if (wake_ >= 0) ::close(wake_);
-    wake_ = -1;
   }
   int fd_;
-  int wake_ = -1;
+  plat::Waker wake_;
   std::string session_key_;  // SSL app data: where new_session_cb files this peer's tickets
   SSL_CTX* ctx_ = nullptr;
   SSL* ssl_ = nullptr;
@@ -460,7 +446,7 @@ int dial_fd(const std::string& host, int port, int timeout_ms) {
   int fd = -1;
   std::string last_err = "no addresses";
   for (auto& a : addrs) {
-    fd = ::socket(a.family, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    fd = plat::socket_cloexec(a.family, SOCK_STREAM);
     if (fd < 0) continue;
     int fl = fcntl(fd, F_GETFL);
     fcntl(fd, F_SETFL, fl | O_NONBLOCK);
@@ -615,7 +601,7 @@ std::unique_ptr<Conn> dial_tcp(const std::string& host, int port, const TlsOptio
 }
 
 std::unique_ptr<Conn> dial_unix(const std::string& path) {
-  int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  int fd = plat::socket_cloexec(AF_UNIX, SOCK_STREAM);
   if (fd < 0) throw NetError("socket: " + std::string(std::strerror(errno)));
   struct sockaddr_un addr{};
   addr.sun_family = AF_UNIX;

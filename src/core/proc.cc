@@ -13,6 +13,7 @@
 
 #include "core/fs.h"
 #include "core/strutil.h"
+#include "platform/platform.h"
 
 extern char** environ;
 
@@ -25,7 +26,7 @@ void Fd::reset(int fd) {
 
 bool make_pipe(Fd* r, Fd* w) {
   int p[2];
-  if (::pipe2(p, O_CLOEXEC) != 0) return false;
+  if (plat::pipe_cloexec(p) != 0) return false;
   r->reset(p[0]);
   w->reset(p[1]);
   return true;
@@ -195,6 +196,7 @@ bool Process::start(const std::vector<std::string>& argv, const ProcOptions& opt
       (void)ignored;
       _exit(127);
     }
+    plat::close_fds_in_child(st_w.get());
     ::execve(exe.c_str(), cargv.data(), cenv.data());
     int e = errno;
     ssize_t ignored = ::write(st_w.get(), &e, sizeof(e));

@@ -7,6 +7,7 @@
 #include <atomic>
 #include <deque>
 #include <iostream>
+#include <map>
 #include <mutex>
 #include <regex>
 
@@ -29,10 +30,53 @@ void set_scripted_answers(const std::vector<std::string>& answers) {
   g_scripted = true;
 }
 
-bool interactive() {
+static std::map<std::string, std::string>& answers() {
+  static std::map<std::string, std::string> m;
+  return m;
+}
+
+void set_answer(const std::string& key, const std::string& value) {
+  std::lock_guard<std::mutex> g(g_mu);
+  answers()[key] = value;
+}
+
+bool has_answer(const std::string& key) {
+  std::lock_guard<std::mutex> g(g_mu);
+  return answers().count(key) > 0;
+}
+
+bool noninteractive_env() {
   const char* ni = getenv("DEVSPACE_NONINTERACTIVE");
-  if (ni && *ni && std::string(ni) != "0") return false;
+  return ni && *ni && std::string(ni) != "0";
+}
+
+bool interactive() {
+  if (noninteractive_env()) return false;
   return ::isatty(0) && ::isatty(1);
+}
+
+static bool preset(const Params& p, std::string* out) {
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = p.key.empty() ? answers().end() : answers().find(p.key);
+    if (it != answers().end()) {
+      *out = it->second;
+      return true;
+    }
+  }
+  const char* v = p.env.empty() ? nullptr : getenv(p.env.c_str());
+  if (v && *v) {
+    *out = v;
+    return true;
+  }
+  return false;
+}
+
+static std::string hint(const Params& p) {
+  std::string h;
+  if (!p.key.empty()) h = "--" + p.key;
+  if (!p.env.empty()) h += (h.empty() ? "" : " or ") + p.env;
+  return h;
 }
 
 static bool read_line(std::string* out, bool secret) {
@@ -45,6 +89,8 @@ static bool read_line(std::string* out, bool secret) {
       return true;
     }
   }
+  // CI runners and `docker exec -i` leave stdin open with nobody writing: never wait on it
+  if (noninteractive_env()) return false;
   struct termios old{};
   bool restore = false;
   if (secret && ::isatty(0) && tcgetattr(0, &old) == 0) {
@@ -64,9 +110,33 @@ static bool read_line(std::string* out, bool secret) {
   return true;
 }
 
+// A preset answer goes through the same checks as a typed one.
+static std::string checked_preset(const Params& p, const std::string& v_in) {
+  std::string v = trim(v_in);
+  std::string from = hint(p);
+  if (!p.options.empty()) {
+    for (auto& o : p.options)
+      if (o == v) return o;
+    throw PromptError("invalid value '" + v + "' (" + from + ") for: " + p.question + " (one of: " + join(p.options, ", ") +
+                      ")");
+  }
+  if (!p.validation_regex.empty()) {
+    try {
+      if (!std::regex_match(v, std::regex("^(?:" + p.validation_regex + ")$")))
+        throw PromptError("invalid value '" + v + "' (" + from + ") for: " + p.question + " (must match " +
+                          p.validation_regex + ")");
+    } catch (const std::regex_error&) {
+    }
+  }
+  return v;
+}
+
 std::string ask(const Params& p) {
+  std::string pre;
+  if (preset(p, &pre)) return checked_preset(p, pre);
   bool tty = interactive() && !g_scripted;
   std::string q = p.question;
+  std::string set_it = hint(p).empty() ? "" : " (set " + hint(p) + ")";
   if (!p.options.empty()) {
     if (tty) {
       log::get().write(log::color("? ", "green+b") + q + "\n");
@@ -80,7 +150,7 @@ std::string ask(const Params& p) {
       if (!read_line(&line, false)) {
         if (!p.default_value.empty()) return p.default_value;
         if (!p.options.empty()) return p.options[0];
-        throw PromptError("no answer for: " + q);
+        throw PromptError("no answer for: " + q + set_it);
       }
       line = trim(line);
       if (line.empty() && !p.default_value.empty()) return p.default_value;
@@ -101,8 +171,8 @@ std::string ask(const Params& p) {
     if (!read_line(&line, p.is_password)) {
       if (!p.default_value.empty()) return p.default_value;
       if (p.optional) return "";
-      throw PromptError("cannot prompt for \"" + q +
-                        "\" in non-interactive mode (set a default, an env var, or run interactively)");
+      throw PromptError("cannot prompt for \"" + q + "\" in non-interactive mode" +
+                        (set_it.empty() ? " (run interactively)" : set_it));
     }
     std::string ans = trim(line);
     if (ans.empty()) ans = p.default_value;

@@ -1,6 +1,10 @@
 // Interactive prompts (util/stdinutil/stdin.go:26 GetFromStdin, survey.v1 selects).
-// Non-interactive runs (stdin not a TTY, or DEVSPACE_NONINTERACTIVE=1) take the default
-// answer, or the next line from stdin when one is piped in; a prompt with neither fails.
+// Answer sources, first match wins:
+//   1. a preset answer for the prompt's key (a command-line flag, or its environment variable);
+//   2. DEVSPACE_NONINTERACTIVE=1: stdin is never read, whatever it is; the default answer, or
+//      an error naming the flag / variable that answers the question;
+//   3. otherwise the next line of stdin (a terminal, or scripted answers piped in), the
+//      default at EOF.
 #pragma once
 
 #include <termios.h>
@@ -20,6 +24,10 @@ struct Params {
   bool is_password = false;
   std::vector<std::string> options;  // select prompt when non-empty
   bool optional = false;  // no answer available (non-interactive, stdin at EOF) = "" instead of an error
+  // Preset answers: set_answer(key, ...) (a flag) or the environment variable `env`. `hint`
+  // names them in errors ("--image or DEVSPACE_INIT_IMAGE").
+  std::string key;
+  std::string env;
 };
 
 struct PromptError : std::runtime_error {
@@ -33,6 +41,11 @@ std::string select(const std::string& question, const std::vector<std::string>& 
                    const std::string& def = "");
 
 bool interactive();
+// DEVSPACE_NONINTERACTIVE is set (to anything but 0): prompts never read stdin.
+bool noninteractive_env();
+// A flag's value answers the prompt with this key.
+void set_answer(const std::string& key, const std::string& value);
+bool has_answer(const std::string& key);
 // Test hook: answers consumed in order instead of reading stdin.
 void set_scripted_answers(const std::vector<std::string>& answers);
 

@@ -1,6 +1,7 @@
 #include "core/resolve.h"
 
 #include <arpa/inet.h>
+#include <netdb.h>
 #include <netinet/in.h>
 #include <poll.h>
 #include <time.h>
@@ -11,6 +12,7 @@
 
 #include "core/fs.h"
 #include "core/strutil.h"
+#include "platform/platform.h"
 
 namespace ds {
 namespace net {
@@ -180,7 +182,7 @@ static std::vector<std::string> dns_lookup(const std::string& fqdn, const Resolv
       for (auto& ns : rc.nameservers) {
         Address a;
         if (!literal(ns, 53, &a)) continue;
-        int fd = ::socket(a.family, SOCK_DGRAM | SOCK_CLOEXEC, 0);
+        int fd = plat::socket_cloexec(a.family, SOCK_DGRAM);
         if (fd < 0) continue;
         uint16_t id = (uint16_t)rng();
         std::string q = dns_query_packet(fqdn, qtype, id);
@@ -207,12 +209,46 @@ static std::vector<std::string> dns_lookup(const std::string& fqdn, const Resolv
   return out;
 }
 
+std::vector<Address> system_resolve(const std::string& host, int port, std::string* err) {
+  struct addrinfo hints{};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  struct addrinfo* res = nullptr;
+  int rc = getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res);
+  std::vector<Address> out;
+  if (rc != 0) {
+    if (err) *err = gai_strerror(rc);
+    return out;
+  }
+  for (int fam : {AF_INET, AF_INET6}) {
+    for (auto* ai = res; ai; ai = ai->ai_next) {
+      if (ai->ai_family != fam || ai->ai_addrlen > sizeof(sockaddr_storage)) continue;
+      Address a;
+      a.family = fam;
+      std::memcpy(&a.addr, ai->ai_addr, ai->ai_addrlen);
+      a.len = ai->ai_addrlen;
+      char buf[INET6_ADDRSTRLEN] = {0};
+      const void* src = fam == AF_INET ? (const void*)&((struct sockaddr_in*)ai->ai_addr)->sin_addr
+                                       : (const void*)&((struct sockaddr_in6*)ai->ai_addr)->sin6_addr;
+      inet_ntop(fam, src, buf, sizeof(buf));
+      a.text = buf;
+      bool dup = false;
+      for (auto& o : out) dup = dup || o.text == a.text;
+      if (!dup) out.push_back(a);
+    }
+  }
+  freeaddrinfo(res);
+  if (out.empty() && err) *err = "no such host";
+  return out;
+}
+
 std::vector<Address> resolve(const std::string& host_in, int port, std::string* err) {
   std::vector<Address> out;
   std::string host = host_in;
   if (host.size() > 2 && host.front() == '[' && host.back() == ']') host = host.substr(1, host.size() - 2);
   Address a;
   if (literal(host, port, &a)) return {a};
+  if (plat::system_resolver()) return system_resolve(host, port, err);
   std::vector<std::string> ips;
   std::string hosts;
   if (fs::read_file("/etc/hosts", &hosts)) ips = hosts_lookup(hosts, host);

@@ -32,6 +32,10 @@ struct ResolvConf {
 // Addresses for host:port (IPv4 first, then IPv6). Empty with *err set when nothing resolves.
 std::vector<Address> resolve(const std::string& host, int port, std::string* err = nullptr);
 
+// getaddrinfo (NSS, the OS's own DNS configuration); what resolve() uses when
+// plat::system_resolver() says so (the portable build).
+std::vector<Address> system_resolve(const std::string& host, int port, std::string* err = nullptr);
+
 // Pieces, exposed for tests.
 std::vector<std::string> hosts_lookup(const std::string& hosts_text, const std::string& name);
 std::string dns_query_packet(const std::string& name, int qtype, uint16_t id);

@@ -1,8 +1,8 @@
 // File watching.
-//  * InotifyWatcher: recursive, event-driven (the reference uses rjeczalik/notify for the sync
-//    upstream, sync/sync_config.go:235).
+//  * TreeWatcher (platform/watch.h): recursive, event-driven where the OS allows it (the
+//    reference uses rjeczalik/notify for the sync upstream, sync/sync_config.go:235).
 //  * PollWatcher: glob-based size+mtime polling (watch/watch.go) — used for auto-reload paths
-//    and symlink targets where inotify cannot follow.
+//    and symlink targets where a tree watcher cannot follow.
 #pragma once
 
 #include <atomic>
@@ -16,33 +16,9 @@
 #include <unordered_map>
 #include <vector>
 
+#include "platform/watch.h"
+
 namespace ds {
-
-class InotifyWatcher {
- public:
-  // Callback receives absolute paths of changed entries (created/modified/removed/moved).
-  // `overflow` is signalled with an empty path: the consumer should rescan. `settled` is true
-  // for events that mark a finished write (close-after-write, rename-into, delete, mkdir).
-  using Callback = std::function<void(const std::string& path, bool settled)>;
-  InotifyWatcher() = default;
-  ~InotifyWatcher();
-  bool start(const std::string& root, Callback cb, std::string* err = nullptr);
-  void stop();
-  size_t watch_count();
-
- private:
-  void add_recursive(const std::string& dir, bool emit_existing);
-  void loop();
-  int fd_ = -1;
-  int wake_[2] = {-1, -1};
-  std::string root_;
-  Callback cb_;
-  std::thread th_;
-  std::atomic<bool> stop_{false};
-  std::mutex mu_;
-  std::unordered_map<int, std::string> wd_path_;
-  std::unordered_map<std::string, int> path_wd_;
-};
 
 class PollWatcher {
  public:

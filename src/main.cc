@@ -8,6 +8,7 @@
 #include "core/log.h"
 #include "core/net.h"
 #include "core/trace.h"
+#include "platform/platform.h"
 
 // One span per CLI run with the transport counters: how many TCP dials / TLS handshakes the
 // command cost and how many requests rode a pooled keep-alive connection.
@@ -24,6 +25,7 @@ static void emit_net_stats() {
 }
 
 int main(int argc, char** argv) {
+  ds::plat::set_argv0(argc > 0 ? argv[0] : nullptr);
   ds::cmd::install_signal_handlers();
   ds::log::logdir();  // construct the function-local statics the handler uses before registering it
   ds::trace::enabled();

@@ -69,7 +69,7 @@ class PyWatcher {
   // place, delete), not on every IN_MODIFY of a file still being written.
   explicit PyWatcher(const std::string& root, bool settled_only = false) {
     std::string err;
-    if (!w_.start(
+    if (!w_->start(
             root,
             [this, settled_only](const std::string& p, bool settled) {
               if (settled_only && !settled) return;
@@ -90,10 +90,10 @@ class PyWatcher {
     q_.clear();
     return out;
   }
-  void close() { w_.stop(); }
+  void close() { w_->stop(); }
 
  private:
-  InotifyWatcher w_;
+  std::unique_ptr<TreeWatcher> w_ = make_tree_watcher();
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::string> q_;

@@ -18,6 +18,7 @@
 #include "core/resolve.h"
 #include "core/strutil.h"
 #include "core/trace.h"
+#include "platform/platform.h"
 
 namespace ds {
 namespace services {
@@ -77,7 +78,7 @@ std::vector<std::pair<int, std::string>> listen_addresses(const std::string& bin
 // One listening socket or -errno. "::" is dual-stack (also takes IPv4), every other IPv6
 // address is v6-only so it can sit next to the IPv4 listener on the same port.
 static int listen_on(int family, const std::string& addr, int port) {
-  int fd = ::socket(family, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  int fd = plat::socket_cloexec(family, SOCK_STREAM);
   if (fd < 0) return -errno;
   int one = 1;
   setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
@@ -418,7 +419,7 @@ void PortForwarder::accept_loop(int lfd, int remote_port) {
     reap(false);
     struct pollfd pf{lfd, POLLIN, 0};
     if (::poll(&pf, 1, 200) <= 0) continue;
-    int cfd = ::accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
+    int cfd = plat::accept_cloexec(lfd);
     if (cfd < 0) continue;
     auto c = std::make_unique<Conn>();
     c->fd = cfd;
@@ -719,8 +720,8 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
     std::atomic<int64_t> t_first{0};
     if (!primed && !replay.empty() && !ws->send(replay)) break;
     if (client_eof && !primed) ws->close_write();
-    int wake[2];
-    if (::pipe2(wake, O_CLOEXEC | O_NONBLOCK) != 0) break;
+    plat::Waker wake;
+    if (!wake.ok()) break;
     std::atomic<bool> down_done{false}, got_reply{false}, refused{false};
     std::string error_text;  // the first error message before any reply (read after the join)
     std::thread down([&] {
@@ -742,15 +743,14 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
         }
       }
       down_done = true;
-      ssize_t w = ::write(wake[1], "x", 1);
-      (void)w;
+      wake.poke();
     });
     char buf[65536];
     while (!down_done && !stop_ && !client_eof) {
       // answered: the spare attempt is not needed (dropped once its open is done, so the
       // forwarding never waits on it; else at the end of the connection)
       if (next && got_reply && next->ready()) next.reset();
-      struct pollfd pf[2] = {{cfd, POLLIN, 0}, {wake[0], POLLIN, 0}};
+      struct pollfd pf[2] = {{cfd, POLLIN, 0}, {wake.fd(), POLLIN, 0}};
       int r = ::poll(pf, 2, 200);
       if (r <= 0 || !(pf[0].revents & (POLLIN | POLLHUP | POLLERR))) continue;
       ssize_t n = ::recv(cfd, buf, sizeof(buf), 0);
@@ -769,14 +769,12 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
       // the client finished sending: wait for the reply (or the refusal) before closing
       while (!down_done && !stop_) {
         if (next && got_reply && next->ready()) next.reset();
-        struct pollfd pw{wake[0], POLLIN, 0};
+        struct pollfd pw{wake.fd(), POLLIN, 0};
         ::poll(&pw, 1, 200);
       }
     }
     ws->close();
     down.join();
-    ::close(wake[0]);
-    ::close(wake[1]);
     if (trace::enabled()) {
       int64_t tf = t_first.load();
       trace::emit("portforward.stream", t_open, trace::now_us() - t_open,

@@ -655,7 +655,7 @@ void Session::push_event(UpEvent e) {
 }
 
 void Session::start_watcher() {
-  watcher_ = std::make_unique<InotifyWatcher>();
+  watcher_ = make_tree_watcher();
   std::string err;
   bool ok = watcher_->start(
       o_.watch_path,

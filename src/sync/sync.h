@@ -312,7 +312,7 @@ class Session {
   bool up_helper_ = false, down_helper_ = false;
   std::mutex up_shell_mu_, down_shell_mu_;
 
-  std::unique_ptr<InotifyWatcher> watcher_;
+  std::unique_ptr<TreeWatcher> watcher_;
   std::map<std::string, std::unique_ptr<PollWatcher>> symlinks_;  // abs symlink path -> target watcher
   std::map<std::string, std::string> symlink_targets_;
   std::mutex symlink_mu_;

@@ -12,6 +12,7 @@
 #include "core/net.h"
 #include "core/strutil.h"
 #include "core/value.h"
+#include "platform/platform.h"
 
 namespace ds {
 namespace upgrade {
@@ -84,9 +85,12 @@ int compare_versions(const std::string& a_in, const std::string& b_in) {
 }
 
 std::vector<std::string> asset_suffixes() {
+  std::string t = plat::release_target();
+  size_t dash = t.find('-');
+  std::string os = t.substr(0, dash), arch = t.substr(dash + 1);
   std::vector<std::string> out;
   for (const char* sep : {"_", "-"})
-    for (const char* ext : {"", ".gz", ".tar.gz", ".tgz"}) out.push_back(std::string("linux") + sep + "amd64" + ext);
+    for (const char* ext : {"", ".gz", ".tar.gz", ".tgz"}) out.push_back(os + sep + arch + ext);
   return out;
 }
 
@@ -189,8 +193,9 @@ std::string extract_binary(const std::string& asset_name, const std::string& dat
     TarEntry e;
     while (tr.next(&e)) {
       std::string base = fs::basename(e.name);
-      if ((e.type == '0' || e.type == '7') && (base == "devspace" || starts_with(base, "devspace-linux") ||
-                                               starts_with(base, "devspace_linux")))
+      std::string os = plat::release_target().substr(0, plat::release_target().find('-'));
+      if ((e.type == '0' || e.type == '7') && (base == "devspace" || starts_with(base, "devspace-" + os) ||
+                                               starts_with(base, "devspace_" + os)))
         return tr.read_all();
       tr.skip();
     }

@@ -47,7 +47,7 @@ struct Release {
 };
 
 // Asset names this platform accepts, go-github-selfupdate style: "<os><sep><arch><ext>"
-// suffixes with sep in {_,-} and ext in {"", .gz, .tar.gz, .tgz} (linux/amd64 here).
+// suffixes with sep in {_,-} and ext in {"", .gz, .tar.gz, .tgz}, for plat::release_target().
 std::vector<std::string> asset_suffixes();
 
 // selfupdate.DetectLatest: newest non-draft, non-prerelease release with a matching asset.

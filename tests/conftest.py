@@ -52,7 +52,11 @@ class DevspaceEnv:
     def run(self, args, cwd, input=None, timeout=120, check=True):
         import subprocess
 
-        p = subprocess.run([self.bin] + list(args), cwd=cwd, env=self.env, input=input, capture_output=True,
+        env = self.env
+        if input is not None:
+            # answers scripted over the pipe: DEVSPACE_NONINTERACTIVE=1 never reads stdin
+            env = {k: v for k, v in self.env.items() if k != "DEVSPACE_NONINTERACTIVE"}
+        p = subprocess.run([self.bin] + list(args), cwd=cwd, env=env, input=input, capture_output=True,
                            text=True, timeout=timeout)
         if check and p.returncode != 0:
             raise AssertionError(f"devspace {' '.join(args)} failed rc={p.returncode}\n{p.stdout}\n{p.stderr}")

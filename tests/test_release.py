@@ -103,3 +103,13 @@ def test_self_update_swaps_in_a_binary_that_runs_in_an_empty_rootfs(dist, tmp_pa
         assert p.returncode != 0 and "does not match its published SHA-256" in p.stdout + p.stderr
     finally:
         srv.shutdown()
+
+
+def test_a_target_without_a_toolchain_releases_nothing(tmp_path):
+    """Cross targets (darwin-*, ...) need cmake/toolchains/<target>.cmake; without one the run
+    fails before building or writing anything, rather than shipping a partial release."""
+    r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "release.sh")], capture_output=True, text=True,
+                       env=dict(os.environ, RELEASE_TARGETS="darwin-arm64", DIST_DIR=str(tmp_path / "d")),
+                       timeout=120)
+    assert r.returncode != 0 and "no toolchain for darwin-arm64" in r.stderr, r.stdout + r.stderr
+    assert not any((tmp_path / "d").iterdir())

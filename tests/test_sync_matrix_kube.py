@@ -37,11 +37,17 @@ def tls_pod(tmp_path_factory):
         cluster.stop()
 
 
-@pytest.mark.parametrize("case", ["sync_initial_fast", "sync_initial_helper", "sync_initial_compat",
-                                  "sync_normal_fast", "sync_normal_helper", "sync_normal_compat"])
-def test_sync_matrix_over_exec_websocket(tls_pod, case, tmp_path):
-    env = dict(os.environ, HOME=str(tmp_path), **tls_pod)
-    p = subprocess.run([os.path.join(ROOT, "bin", "devspace_tests"), case], capture_output=True, text=True, env=env,
-                       timeout=300)
+CASES = ["sync_initial_fast", "sync_initial_helper", "sync_initial_compat", "sync_normal_fast", "sync_normal_helper",
+         "sync_normal_compat"]
+
+
+# DEVSPACE_TESTS_BIN: the same matrix against another build (scripts/ci.sh runs the portable one).
+# The scan leg runs the edit matrix with the portable stat-scan watcher in this build too.
+@pytest.mark.parametrize("case,watcher", [(c, "native") for c in CASES] +
+                         [(c, "scan") for c in CASES if "normal" in c])
+def test_sync_matrix_over_exec_websocket(tls_pod, case, watcher, tmp_path):
+    env = dict(os.environ, HOME=str(tmp_path), DEVSPACE_WATCHER=watcher, **tls_pod)
+    exe = os.environ.get("DEVSPACE_TESTS_BIN") or os.path.join(ROOT, "bin", "devspace_tests")
+    p = subprocess.run([exe, case], capture_output=True, text=True, env=env, timeout=300)
     assert p.returncode == 0, p.stdout[-4000:] + p.stderr[-2000:]
     assert f"PASS {case}" in p.stdout and "1 passed, 0 failed" in p.stdout, p.stdout[-2000:]
