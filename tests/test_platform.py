@@ -59,6 +59,7 @@ def test_scan_watcher_drives_the_cli_sync(tmp_path):
     root = tmp_path / "root"
     dst = root / "app"
     p = subprocess.Popen([exe, "sync", "--local", str(src), "--container", "/app", "--local-root", str(root)], env=env,
+                         cwd=str(tmp_path),
                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, start_new_session=True)
 
     def wait(cond, what, t=15):
