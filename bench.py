@@ -417,6 +417,24 @@ def _pf_spans(trace_path, windows):
             "open_ms_p50": ms("open_us", spans), "reply_first_byte_ms_p50": ms("first_us", replies)}
 
 
+def _app_requests_per_edit(req_log, marks):
+    """Requests the restarted server of each timed edit served: the server that answered the
+    edit's GET is the last one in that edit's slice of the app's request log, and every line of
+    its pid in the slice is one delivery of that GET (the bench sends no other request to it).
+    1.0 = each request reached the app once."""
+    try:
+        data = open(req_log, "rb").read()
+    except OSError:
+        return None
+    counts = []
+    for k, start in enumerate(marks):
+        end = marks[k + 1] if k + 1 < len(marks) else len(data)
+        rows = [l.split(b" ", 1)[0] for l in data[start:end].splitlines() if l.strip()]
+        if rows:
+            counts.append(sum(1 for r in rows if r == rows[-1]))
+    return counts
+
+
 def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=False, timed_start=None,
                     timed_end=None, cold=None, wan=None):
     """examples/quickstart edit -> reload, the way its README runs the dev loop: `devspace dev`
@@ -440,9 +458,19 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
     cfg["dev"]["overrideImages"][0]["entrypoint"] = ["node", "watch.js", "index.js"]
     cfg["dev"]["ports"][0]["portMappings"] = [{"localPort": local, "remotePort": remote}]
     open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    # app-side request log (pid + request line per request the app serves): how many copies of
+    # the held GET of each edit reached the restarted server
+    req_log = os.path.join(base, "app-requests.log")
+    index_src = open(os.path.join(proj, "index.js")).read()
+    hook = "http.createServer((req, res) => {"
+    assert hook in index_src, "examples/quickstart/index.js request handler not found"
+    open(os.path.join(proj, "index.js"), "w").write(index_src.replace(
+        hook, hook + "\n  if (process.env.REQUEST_LOG) require('fs').appendFileSync(process.env.REQUEST_LOG, "
+        "process.pid + ' ' + req.method + ' ' + req.url + '\\n');", 1))
     values = os.path.join(proj, "chart", "values.yaml")
     v = yaml.safe_load(open(values))
-    v["components"][0]["containers"][0]["env"] = [{"name": "PORT", "value": str(remote)}]
+    v["components"][0]["containers"][0]["env"] = [{"name": "PORT", "value": str(remote)},
+                                                  {"name": "REQUEST_LOG", "value": req_log}]
     if cold:  # nodemon's cold restarts
         v["components"][0]["containers"][0]["env"].append({"name": "WATCH_STANDBY", "value": "0"})
     open(values, "w").write(yaml.safe_dump(v))
@@ -479,7 +507,7 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
         # answers through the forward (the first iteration of the loop)
         dev_start_s = time.perf_counter() - t_dev
         index, pod_index = os.path.join(proj, "index.js"), os.path.join(root, "app", "index.js")
-        samples, sync_samples, conns, windows = [], [], [], []
+        samples, sync_samples, conns, windows, log_marks = [], [], [], [], []
         rng = random.Random(4321)
         for i in range(warmup + steps):
             if i == warmup and timed_start:
@@ -487,6 +515,8 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
             marker = f"q{i}" + ("_" * (i % 2))  # compat mode compares size + mtime (s)
             time.sleep(rng.uniform(0.0, EDIT_JITTER_S))
             c0 = link.connections if link is not None else 0
+            if i >= warmup:
+                log_marks.append(os.path.getsize(req_log) if os.path.exists(req_log) else 0)
             w0 = time.monotonic()  # (trace spans carry CLOCK_MONOTONIC microseconds)
             t0 = time.perf_counter()
             _qs_edit(index, marker)
@@ -507,7 +537,9 @@ def quickstart_loop(workdir, steps, warmup, sync_mode=None, tls=True, reference=
                 windows.append((w0, time.monotonic()))
         if timed_end:
             timed_end()
-        out = {"reload_ms": samples, "sync_ms": sync_samples, "dev_start_s": dev_start_s}
+        time.sleep(0.2)  # a late copy of the last edit's request would land now
+        out = {"reload_ms": samples, "sync_ms": sync_samples, "dev_start_s": dev_start_s,
+               "app_requests": _app_requests_per_edit(req_log, log_marks)}
         if link is not None:
             out["link"] = {"connections": link.connections, "per_edit": conns}
             out["portforward"] = _pf_spans(os.path.join(proj, ".devspace", "logs", "trace.jsonl"), windows)
@@ -799,6 +831,8 @@ def main():
 
     def extra(name, fn):
         try:
+            if os.environ.get("DEVSPACE_BENCH_FAIL_EXTRA") == name:  # test hook (tests/test_bench.py)
+                raise RuntimeError(f"forced failure of {name} (DEVSPACE_BENCH_FAIL_EXTRA)")
             extras[name] = fn()
         except Exception as e:  # reported, not fatal for the headline metric
             _log(f"{name} failed: {e}")
@@ -875,6 +909,10 @@ def main():
     return 0
 
 
+def _mean(xs):
+    return round(sum(xs) / len(xs), 2) if xs else None
+
+
 def _ok(x):
     return isinstance(x, dict) and "error" not in x
 
@@ -914,6 +952,7 @@ def report(args, nproc, tls, ms_total, qs, extras):
         "sync_p50_ms": round(_pct(qs["sync_ms"], 0.5), 2),
         # untimed: `devspace dev` on a fresh cluster until the app answers through the forward
         "dev_start_s": round(qs["dev_start_s"], 3),
+        "app_requests_per_edit": _mean(qs.get("app_requests")),
     }
     ref = extras.get("qs_ref")
     if _ok(ref):
@@ -939,6 +978,8 @@ def report(args, nproc, tls, ms_total, qs, extras):
             "rtt_ms": WAN[0], "mbit": WAN[1],
             "p50_ms": round(wp50, 2), "p90_ms": round(_pct(wan["reload_ms"], 0.9), 2),
             "sync_p50_ms": round(_pct(wan["sync_ms"], 0.5), 2), "n": len(wan["reload_ms"]),
+            # copies of each edit's GET that reached the restarted app (1.0: delivered once)
+            "app_requests_per_edit": _mean(wan.get("app_requests")),
             "dev_start_s": round(wan["dev_start_s"], 3), "link_connections": wan.get("link", {}).get("connections"),
             "connections_per_edit": round(sum(wan["link"]["per_edit"]) / max(1, len(wan["link"]["per_edit"])), 2)
             if wan.get("link", {}).get("per_edit") else None,
@@ -1055,6 +1096,10 @@ def report(args, nproc, tls, ms_total, qs, extras):
         if _ok(e):
             e = dict(e, note=EXAMPLE_NOTES[key])
         out[key] = e
+    # an extra that failed is named with its message (its block is otherwise absent or {"error"})
+    errors = {k: v["error"] for k, v in extras.items() if isinstance(v, dict) and "error" in v}
+    if errors:
+        out["extra_errors"] = errors
     return out
 
 

@@ -165,9 +165,10 @@ ENV = {
                             "follows the scan's cost (at most 5 % of a core).",
     "DEVSPACE_WATCHER": "`scan`: watch sync paths with the portable stat-scan watcher instead of the platform's "
                         "event backend (inotify on Linux). The portable build always scans.",
-    "DEVSPACE_PORTFORWARD_HEDGE": "`0`: a held GET/HEAD/OPTIONS on a remote cluster is retried one stream at a time "
-                                  "(by default a new attempt goes out every third of a round trip; the app may see "
-                                  "the request up to about four times).",
+    "DEVSPACE_PORTFORWARD_HEDGE": "`1`: a held GET/HEAD/OPTIONS on a remote cluster (tunnel round trip of 5 ms or "
+                                  "more) is hedged: a new attempt every third of a round trip while earlier ones are "
+                                  "in flight; the app may see the request up to about four times. Default: one "
+                                  "stream at a time, each request delivered once.",
     "DEVSPACE_PORTFORWARD_HOLD_MS": "How long a local connection is held while the pod refuses it (its app "
                                     "restarting) before it is dropped; default 3000, 0 drops at once as kubectl "
                                     "does.",

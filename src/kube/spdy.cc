@@ -331,10 +331,20 @@ void SpdySession::ping() {
     if (dead_) return;
     id = next_ping_;
     next_ping_ += 2;
-    pings_[id] = std::chrono::steady_clock::now();
+    auto now = std::chrono::steady_clock::now();
+    // a far end that never answers: what is still unanswered after 5 s will not be, and the map
+    // stays small whatever the session's length
+    for (auto it = pings_.begin(); it != pings_.end();)
+      it = now - it->second > std::chrono::seconds(5) ? pings_.erase(it) : std::next(it);
+    pings_[id] = now;
   }
   std::lock_guard<std::mutex> w(wmu_);
   write_frame(spdy::control_frame(spdy::Ping, 0, spdy::u32(id)));
+}
+
+size_t SpdySession::pings_in_flight() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return pings_.size();
 }
 
 void SpdySession::close() {

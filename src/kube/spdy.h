@@ -116,6 +116,8 @@ class SpdySession {
   void ping();
   int64_t rtt_us() const { return rtt_us_.load(); }
   int rtt_samples() const { return rtt_samples_.load(); }  // PINGs answered
+  // PINGs sent in the last 5 s and not answered yet
+  size_t pings_in_flight() const;
 
  private:
   void reader();

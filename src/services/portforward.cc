@@ -166,7 +166,14 @@ class TunnelFwd : public FwdStream {
   TunnelFwd(std::shared_ptr<kube::SpdySession> s, int port, uint64_t request_id) : s_(std::move(s)) {
     std::string p = std::to_string(port), id = std::to_string(request_id);
     err_ = s_->open({{"streamtype", "error"}, {"port", p}, {"requestid", id}}, box_, 1, true);
-    data_ = s_->open({{"streamtype", "data"}, {"port", p}, {"requestid", id}}, box_, 0);
+    try {
+      data_ = s_->open({{"streamtype", "data"}, {"port", p}, {"requestid", id}}, box_, 0);
+    } catch (...) {
+      // a GOAWAY between the two opens: the error stream must not stay in the session
+      s_->reset(err_);
+      box_->close();
+      throw;
+    }
   }
   ~TunnelFwd() override { close(); }
   bool send(const std::string& data) override { return s_->send(data_, data); }
@@ -309,14 +316,20 @@ void PortForwarder::spare_loop() {
       lk.lock();
       if (tunnel_mode_ == 1) {
         spares_.clear();
-        // PINGs every 100 ms until the tunnel has ten answers (its round trip is known within a
-        // second of opening), then every second
-        int samples;
+        // hedging needs the round trip: PINGs every 100 ms until the tunnel has ten answers (known
+        // within a second of opening), then every second; a far end that leaves five unanswered
+        // gets one a second. Without hedging, one a second keeps the tunnel warm.
+        int samples = 0;
+        size_t unanswered = 0;
         {
           std::lock_guard<std::mutex> g(tunnel_mu_);
-          samples = tunnel_ ? tunnel_->rtt_samples() : 0;
+          if (tunnel_) {
+            samples = tunnel_->rtt_samples();
+            unanswered = tunnel_->pings_in_flight();
+          }
         }
-        spare_cv_.wait_for(lk, std::chrono::milliseconds(samples < 10 ? 100 : 1000), [this] { return stop_.load(); });
+        bool fast = hedge_ && samples < 10 && unanswered < 5;
+        spare_cv_.wait_for(lk, std::chrono::milliseconds(fast ? 100 : 1000), [this] { return stop_.load(); });
         continue;
       }
     }
@@ -364,6 +377,12 @@ void PortForwarder::start() {
     want_spares_ = reference_timing() ? 0 : 2;  // the reference dials every stream
   }
   if (!port_forward_tunnel_enabled()) tunnel_mode_ = 0;
+  if (hedge_)
+    log::file_logger("portforwarding")
+        ->emit("info",
+               "DEVSPACE_PORTFORWARD_HEDGE=1: a held GET/HEAD/OPTIONS on a remote cluster may reach the app more "
+               "than once",
+               {});
   if (want_spares_ > 0 || tunnel_mode_ != 0) spare_thread_ = std::thread([this] { spare_loop(); });
   for (size_t i = 0; i < ports_.size(); ++i) {
     std::string bind = i < addrs_.size() ? addrs_[i] : "";
@@ -545,9 +564,12 @@ bool hedgeable_request(const std::string& bytes) {
          !contains(head, "\r\nupgrade:");
 }
 
+// Opt-in (DEVSPACE_PORTFORWARD_HEDGE=1): hedged attempts can each reach the app, and dev apps
+// often have GET routes with side effects. By default every request is delivered once, as by
+// kubectl port-forward.
 bool port_forward_hedge() {
   const char* v = std::getenv("DEVSPACE_PORTFORWARD_HEDGE");
-  return !(v && std::string(v) == "0") && !reference_timing();
+  return v && std::string(v) == "1" && !reference_timing();
 }
 
 // A held idempotent request on a slow link (the app restarting behind a remote API server):
@@ -555,7 +577,8 @@ bool port_forward_hedge() {
 // the request) goes out every third of a round trip while earlier ones are in flight, so the
 // request reaches the new server within a few ms of it listening rather than up to a round trip
 // later. The first attempt answered wins; the others are reset. The app may see the request
-// more than once (up to about four times): only GET, HEAD and OPTIONS without a body are hedged,
+// more than once (up to about four times), which is why this is opt-in (port_forward_hedge):
+// only GET, HEAD and OPTIONS without a body are hedged,
 // which HTTP lets a client repeat (RFC 9110 §9.2.2). nullptr: no answer before `deadline_ms`, or
 // an attempt ended other than refused (the caller carries on one attempt at a time).
 std::unique_ptr<FwdStream> PortForwarder::hedge(int remote_port, const std::string& request, bool fin, int64_t rtt_us,

@@ -58,7 +58,7 @@ int port_forward_hold_ms();
 bool port_forward_preopen();
 bool is_dial_refused(const std::string& error_channel_message);
 // Whether a held connection on a slow link may be retried on several streams at once
-// (DEVSPACE_PORTFORWARD_HEDGE=0 turns it off), and whether its bytes so far are one request that
+// (opt-in, DEVSPACE_PORTFORWARD_HEDGE=1: the app may see such a request more than once), and whether its bytes so far are one request that
 // HTTP lets a client repeat: GET, HEAD or OPTIONS, the whole head and no body.
 bool port_forward_hedge();
 bool hedgeable_request(const std::string& bytes);

@@ -28,6 +28,9 @@ def test_bench_cpu_tiny():
                        timeout=1200, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
+    # every failed extra, with its message, in any assertion below that fails
+    errs = d.get("extra_errors", {})
+    assert "reference_equivalent" in d and "wan" in d and "deploy" in d, (errs, r.stderr[-3000:])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config"):
         assert k in d, k
@@ -47,6 +50,8 @@ def test_bench_cpu_tiny():
     # the same loops behind a 30 ms RTT link: every edit pays at least the one-way delay
     wan = d["wan"]
     assert wan["rtt_ms"] == 30 and wan["n"] >= 5 and wan["link_connections"] > 0, wan
+    # each edit's GET reached the restarted app once (no hedged duplicates by default)
+    assert wan["app_requests_per_edit"] == 1.0 and d["app_requests_per_edit"] == 1.0, (wan, errs)
     assert wan["sync_p50_ms"] >= 15 and wan["p50_ms"] > wan["sync_p50_ms"], wan
     assert wan["reference_equivalent"]["p50_ms"] > wan["p50_ms"], wan
     # deploy across the link: kept-alive connections vs a dial (+ TLS) per request
@@ -134,6 +139,18 @@ def test_bench_extras_budget_keeps_the_headline():
               "--no-deploy-bench", "--tiny", "--extras-budget-s", "0.001"], 600)
     assert d["value"] > 0 and d["steps"] == 2
     assert "gpu_pod" not in d and "cold_restart" not in d and "reference_equivalent" not in d, d
+
+
+def test_a_failed_extra_is_named_with_its_message():
+    """An extra that raises is reported in `extra_errors` with its message (it used to vanish and
+    surface later as a KeyError in the caller's assertions)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--ref-steps",
+                        "0", "--gpu-steps", "0", "--example-steps", "0", "--tiny"], capture_output=True, text=True,
+                       timeout=600, cwd=ROOT, env=dict(os.environ, DEVSPACE_BENCH_FAIL_EXTRA="deploy"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["value"] > 0 and "deploy" not in d, d
+    assert "forced failure of deploy" in d["extra_errors"]["deploy"], d.get("extra_errors")
 
 
 @pytest.mark.gpu

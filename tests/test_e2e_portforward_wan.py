@@ -1,16 +1,18 @@
 """Port-forward of a request held across an app restart, with the cluster behind a slow link (40 ms
 RTT, devspace_amd/localkube/netem.py), as a laptop reaches a remote MI355X node.
 
-One attempt per round trip would make a request wait up to a whole round trip after the new
-server listens. So a held GET (repeatable, RFC 9110 §9.2.2) goes out on a new stream pair of the
-pod's tunnel every quarter round trip while earlier attempts are in flight; the first answer wins.
-A POST still goes out on one stream at a time and reaches the app exactly once. And an API server
-without the tunnel (before Kubernetes 1.30) gets a WebSocket per connection.
+By default every held request, GET or POST, is retried one stream at a time and reaches the app
+exactly once, as through kubectl port-forward (/root/reference/pkg/devspace/kubectl/client.go:356-380).
+With DEVSPACE_PORTFORWARD_HEDGE=1 a held GET (repeatable, RFC 9110 §9.2.2) goes out on a new
+stream pair of the pod's tunnel every third of a round trip while earlier attempts are in flight;
+the first answer wins, and the app may see the GET more than once. A POST still goes out once.
+An API server without the tunnel (before Kubernetes 1.30) gets a WebSocket per connection.
 """
 import json
 import os
 import urllib.request
 
+import pytest
 import yaml
 
 from conftest import DevspaceEnv
@@ -18,7 +20,8 @@ from test_e2e_cli import running, wait_for
 from test_e2e_services import _refused, _restart_project, _stop
 
 
-def test_a_held_get_is_hedged_and_a_held_post_is_sent_once(tmp_path):
+@pytest.mark.parametrize("hedge", [False, True], ids=["default", "hedge-opt-in"])
+def test_held_requests_across_a_restart_on_a_remote_cluster(tmp_path, hedge):
     from devspace_amd.localkube import LocalCluster
     from devspace_amd.localkube.netem import ShapedLink, point_kubeconfig
 
@@ -26,6 +29,9 @@ def test_a_held_get_is_hedged_and_a_held_post_is_sent_once(tmp_path):
     link = None
     try:
         lk = DevspaceEnv(cluster, str(tmp_path))
+        lk.env.pop("DEVSPACE_PORTFORWARD_HEDGE", None)
+        if hedge:
+            lk.env["DEVSPACE_PORTFORWARD_HEDGE"] = "1"
         link = ShapedLink(("127.0.0.1", cluster.port), rtt_ms=40, mbit=100).start()
         point_kubeconfig(lk.kubeconfig, cluster.server, link.url("https"))
         proj, remote, local = _restart_project(lk, "qs-wan-hold", "pf-wan")
@@ -70,13 +76,24 @@ def test_a_held_get_is_hedged_and_a_held_post_is_sent_once(tmp_path):
         lines = hits.read_text().splitlines()
         for i in (1, 3):
             assert lines.count(f"POST /held-{i}") == 1, lines
-        for i in (0, 2):
-            assert 1 <= lines.count(f"GET /held-{i}") <= 8, lines
         spans = [json.loads(l) for l in open(os.path.join(proj, ".devspace", "logs", "trace.jsonl"))
                  if '"portforward.stream"' in l]
         hedged = [s for s in spans if s.get("hedged") == "1"]
-        assert any(s["outcome"] == "reply" for s in hedged), spans
         assert all(s.get("via") == "tunnel" for s in spans), spans
+        pf_log = os.path.join(proj, ".devspace", "logs", "portforwarding.log")
+        log = open(pf_log).read() if os.path.exists(pf_log) else ""
+        if hedge:
+            for i in (0, 2):
+                assert 1 <= lines.count(f"GET /held-{i}") <= 8, lines
+            assert any(s["outcome"] == "reply" for s in hedged), spans
+            assert "may reach the app more than once" in log, log
+        else:
+            # each held GET reached the app exactly once, after at least one refused attempt
+            for i in (0, 2):
+                assert lines.count(f"GET /held-{i}") == 1, lines
+            assert not hedged, hedged
+            assert any(s["outcome"] == "refused" for s in spans), spans
+            assert "more than once" not in log, log
     finally:
         if link is not None:
             link.stop()
