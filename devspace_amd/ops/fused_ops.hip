@@ -934,6 +934,82 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnParams p) {
 
 // ------------------------------------------------------------------------------ host side
 
+// ------------------------------------------------------------------------------ state digest
+// Content digest of training state for the rescue snapshots' de-duplication
+// (devspace_amd/rescue.py digests): per row of up to 64 Ki int64 words w_i (i = the word's index
+// in its tensor), S = sum w_i and M = sum mix(w_i ^ key(i)) mod 2^64, key(i) = (i + 1) * golden,
+// mix = the splitmix64 finalizer (a bijection). M depends on every word's position: a swap of
+// two words, or changes that keep the plain sum, give another M with probability 1 - 2^-64.
+// One HBM read of the state (one block per row, 8-byte loads, wave64 + LDS reduction), one
+// launch for all tensors (a row table), one small copy of (S, M) pairs to the host. The CPU
+// path computes the same numbers with torch ops (rescue.py _digest_rows_torch).
+struct DigestRow {
+  const unsigned long long* p;  // the row's first word
+  long long n;                  // words in this row (<= kDigestRowWords)
+  long long base;               // index of the first word in its tensor
+};
+constexpr long long kDigestRowWords = 1 << 16;
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z;
+}
+
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int o) {
+  unsigned lo = __shfl_xor((unsigned)v, o, 64), hi = __shfl_xor((unsigned)(v >> 32), o, 64);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+__global__ void __launch_bounds__(kBlock) state_digest_kernel(const DigestRow* __restrict__ rows,
+                                                               long long* __restrict__ out) {
+  const DigestRow r = rows[blockIdx.x];
+  unsigned long long s = 0, m = 0;
+  const unsigned long long kGolden = 0x9E3779B97F4A7C15ull;
+  long long i = threadIdx.x;
+  // 4 independent loads in flight per lane before the arithmetic that uses them
+  for (; i + 3 * kBlock < r.n; i += 4 * kBlock) {
+    unsigned long long v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(r.p + i + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s += v[u];
+      m += mix64(v[u] ^ ((unsigned long long)(r.base + i + u * kBlock + 1) * kGolden));
+    }
+  }
+  for (; i < r.n; i += kBlock) {
+    unsigned long long v = __builtin_nontemporal_load(r.p + i);
+    s += v;
+    m += mix64(v ^ ((unsigned long long)(r.base + i + 1) * kGolden));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += shfl_xor_u64(s, o);
+    m += shfl_xor_u64(m, o);
+  }
+  __shared__ unsigned long long part[2][kBlock / 64];
+  const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+  if (lane == 0) {
+    part[0][wave] = s;
+    part[1][wave] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long S = 0, M = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+      S += part[0][w];
+      M += part[1][w];
+    }
+    out[2 * blockIdx.x] = (long long)S;
+    out[2 * blockIdx.x + 1] = (long long)M;
+  }
+}
+
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 void check_bf16(const at::Tensor& t, const char* name) {
@@ -1261,6 +1337,36 @@ at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Ten
   return dqkv;
 }
 
+// (S, M) per row of every tensor in `words` (int64, contiguous, on one device): an int64
+// [rows, 2] tensor, rows of each tensor in order (ceil(numel / 64 Ki) each).
+at::Tensor state_digest(std::vector<at::Tensor> words) {
+  TORCH_CHECK(!words.empty(), "state_digest: no tensors");
+  const auto dev = words[0].device();
+  std::vector<long long> table;
+  for (auto& w : words) {
+    TORCH_CHECK(w.scalar_type() == at::kLong && w.is_contiguous() && w.device() == dev,
+                "state_digest: contiguous int64 tensors on one device");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 8 == 0, "state_digest: 8-byte aligned data");
+    const long long n = w.numel();
+    const auto* p = reinterpret_cast<const unsigned long long*>(w.data_ptr());
+    for (long long o = 0; o < n; o += kDigestRowWords) {
+      table.push_back((long long)(uintptr_t)(p + o));
+      table.push_back(std::min(kDigestRowWords, n - o));
+      table.push_back(o);
+    }
+  }
+  const long long rows = (long long)table.size() / 3;
+  auto out = at::empty({rows, 2}, at::TensorOptions().dtype(at::kLong).device(dev));
+  if (rows == 0) return out;
+  static_assert(sizeof(DigestRow) == 3 * sizeof(long long), "row table layout");
+  auto host = at::from_blob(table.data(), {rows * 3}, at::kLong).clone();
+  auto dtab = host.to(dev, /*non_blocking=*/false);
+  hipLaunchKernelGGL(state_digest_kernel, dim3((unsigned)rows), dim3(kBlock), 0, stream(),
+                     reinterpret_cast<const DigestRow*>(dtab.data_ptr()), reinterpret_cast<long long*>(out.data_ptr()));
+  LAUNCH_CHECK();
+  return out;
+}
+
 // ------------------------------------------------------------------------------ autograd
 // C++ autograd nodes: one Python -> C++ call per op and no Python in the backward pass (a
 // Python autograd.Function costs tens of microseconds of CPU per call, which shows on a
@@ -1392,6 +1498,7 @@ PYBIND11_MODULE(_fused_ops, m) {
   m.def("swiglu", &swiglu);
   m.def("cross_entropy", &cross_entropy);
   m.def("adamw_step", &adamw_step);
+  m.def("state_digest", &state_digest, "(sum, position-keyed mixed sum) per 64 Ki-word row of int64 tensors");
   m.def("attention", &attention);
   m.def("attention_supported", &attention_supported);
   m.def("attn_fwd", &attn_fwd);

@@ -367,6 +367,66 @@ def test_digests_tell_apart_what_differs():
     assert d[4] == digests([base[1:].clone()])[0]  # a view at an odd offset
 
 
+def test_tensors_that_differ_by_a_swap_of_two_words_each_write_their_own_copy(tmp_path):
+    """a position-insensitive row checksum took two ranks' tensors that differ
+    only by a swap of two 8-byte words inside a row for one tensor, wrote it once, and the other
+    rank restored the wrong bytes. With the position-keyed digest each rank writes its own copy,
+    and both restore bit-exact; a plain sum of the words is the same for both."""
+    world = 2
+    torch.manual_seed(3)
+    a = torch.randint(-2**62, 2**62, (1 << 19,), dtype=torch.int64)  # 4 MiB
+    b = a.clone()
+    b[1000], b[1001] = a[1001].item(), a[1000].item()
+    assert not torch.equal(a, b) and a.sum() == b.sum()
+    floats = torch.randn(1 << 20)  # the same swap in float data (a sign flip pair)
+    f2 = floats.clone()
+    f2[10], f2[12] = -floats[10].abs(), floats[10].abs()
+    f1 = floats.clone()
+    f1[10], f1[12] = floats[10].abs(), -floats[10].abs()
+    states = [{"w": a, "f": f1}, {"w": b, "f": f2}]
+    rescues, jobs = _group_take(tmp_path, world, states)
+    assert jobs[0]["bytes"] >= (4 << 20) + (4 << 20) and jobs[1]["bytes"] >= (4 << 20) + (4 << 20), jobs
+    for r in range(world):
+        snap, _ = rescues[r].load(7, torch.device("cpu"))
+        assert torch.equal(snap["w"], states[r]["w"]) and torch.equal(snap["f"], states[r]["f"]), r
+
+
+def test_digests_are_position_sensitive_and_agree_across_paths():
+    from devspace_amd.rescue import _ROW, _digest_rows_torch, digests
+
+    x = torch.arange(3 * _ROW + 5, dtype=torch.int64) * 7919
+    y = x.clone()
+    y[[4, 5]] = y[[5, 4]]
+    z = x.clone()
+    z[0] += 1
+    z[1] -= 1  # the plain sums cannot tell
+    d = digests([x, y, z])
+    assert len(set(d)) == 3
+    rows = _digest_rows_torch(x)
+    assert rows.shape == (4, 2) and int(rows[3, 0]) == int(x[3 * _ROW:].sum())
+
+
+@pytest.mark.gpu
+def test_digest_kernel_matches_the_torch_path_bit_for_bit():
+    """The gfx950 `state_digest` kernel computes the same (S, M) row pairs as the CPU torch path,
+    so a tensor's digest does not depend on where it lives (fp32 reference check of an integer op:
+    exact equality)."""
+    from devspace_amd.ops import fused
+    from devspace_amd.rescue import _ROW, _digest_rows_torch, digests
+
+    e = fused.ext()
+    assert e is not None and hasattr(e, "state_digest"), "fused-ops extension with state_digest not loaded"
+    torch.manual_seed(0)
+    sizes = [1, 63, _ROW - 1, _ROW, _ROW + 1, 5 * _ROW + 77, 3 << 20]
+    ts = [torch.randint(-2**62, 2**62, (n,), dtype=torch.int64) for n in sizes]
+    got = e.state_digest([t.cuda() for t in ts]).cpu()
+    want = torch.cat([_digest_rows_torch(t) for t in ts])
+    assert torch.equal(got, want)
+    mixed = [torch.randn(1000, 513, dtype=torch.bfloat16), torch.randn(7), torch.ones(3, dtype=torch.bool),
+             torch.randn(4097, dtype=torch.float64)[1:]]
+    assert digests([t.cuda() for t in mixed]) == digests(mixed)
+
+
 def test_staging_budget_is_the_largest_copy_the_room_allows():
     gib = 1 << 30
     for free, reserved, peak in ((10 * gib, 4 * gib, 3 * gib), (gib, 0, 0), (0, 2 * gib, 2 * gib)):

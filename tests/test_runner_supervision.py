@@ -303,6 +303,8 @@ def test_ddp_snapshot_is_written_once_and_restores_bit_exact(tmp_path):
                            "state_mib_all_ranks": state_mib, "group_snapshot_mib": group_mib,
                            "on_disk_mib": round(on_disk / 2**20, 1), "restored_step": restored,
                            "restore_ms_rank0": float(restore.group(3)) if restore else None,
+                           "digest_ms": float(re.search(r"digest ([\d.]+) ms", snap_line).group(1))
+                           if re.search(r"digest ([\d.]+) ms", snap_line) else None,
                            "snapshot_line": re.sub(r"^.*\[devspace-runner\] ", "", snap_line.strip()),
                            "bit_exact_on_every_rank": True}, f, indent=1)
         for rank in range(world):
