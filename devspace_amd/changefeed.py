@@ -17,9 +17,13 @@ import time
 PREFIX = "[devspace-runner]"
 
 
+_OUT_LOCK = threading.Lock()  # one line at a time on stdout (the supervisor's LogRelay takes it too)
+
+
 def _log(msg: str) -> None:
-    sys.stdout.write(f"{PREFIX} {msg}\n")
-    sys.stdout.flush()
+    with _OUT_LOCK:
+        sys.stdout.write(f"{PREFIX} {msg}\n")
+        sys.stdout.flush()
 
 
 

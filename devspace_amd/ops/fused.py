@@ -100,10 +100,21 @@ def _use_hip(t: torch.Tensor) -> bool:
 # the forward/backward path of the training step).
 
 
-def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float | None = None) -> torch.Tensor:
+def _rmsnorm_kernel_default() -> bool:
+    import os
+
+    return os.environ.get("DEVSPACE_FUSED_RMSNORM") == "1"
+
+
+def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float | None = None, kernel: bool | None = None) -> torch.Tensor:
+    """RMSNorm alone. PyTorch's own fused rms_norm by default: the gfx950 kernel (`kernel=True`,
+    or DEVSPACE_FUSED_RMSNORM=1) measured 0.97x of it fwd+bwd on [4096x1024]
+    (profiles/r5_fused_ops_ab.txt), so it is not the default path. The residual add + RMSNorm
+    (`add_rms_norm`, 1.16x: one pass instead of two) is where fusing pays, and stays on."""
     if eps is None:
         eps = torch.finfo(x.dtype).eps
-    if _use_hip(x) and weight.dtype == torch.bfloat16 and ext().rmsnorm_supported(x.shape[-1]):
+    use = _rmsnorm_kernel_default() if kernel is None else kernel
+    if use and _use_hip(x) and weight.dtype == torch.bfloat16 and ext().rmsnorm_supported(x.shape[-1]):
         return ext().rms_norm(x, weight, float(eps))
     return F.rms_norm(x, (x.shape[-1],), weight, eps)
 

@@ -535,9 +535,10 @@ class _Heartbeat:
     SETUP_VERSION changed, the first step of the new code) | step (a steady-state step) |
     boundary | idle (paused or waiting). still: seconds since the main thread last showed
     progress, sampled 4x a second: its Python position (innermost frame, bytecode offset)
-    changed, or it used at least 5 % of a CPU since the last sample. A thread blocked in a
-    deadlock, a dead peer's collective or a sleep stands still; an eval loop, a checkpoint save or
-    a long computation moves. where: the innermost frame of the user's code. From a thread, so a step that runs for
+    changed, or it used at least 5 % of a CPU since the last sample outside a call that waits
+    (WAIT_CALLS: `.item()`, `synchronize`, collectives, ...). A thread blocked in a deadlock, a
+    dead peer's collective (even one whose wait spins the CPU) or a sleep stands still; an eval
+    loop, a checkpoint save or a long computation moves. where: the innermost frame of the user's code. From a thread, so a step that runs for
     minutes keeps the beat going (the old beat came from the top of the loop: a long healthy step
     looked stuck). The main thread only sets `phase`/`since`: two attribute writes per step."""
 
@@ -545,6 +546,8 @@ class _Heartbeat:
         self.rank, self.ctx, self.rescue = rank, ctx, rescue
         self.phase, self.since, self.longest = "start", time.monotonic(), 0.0
         self.main = threading.get_ident()
+        extra = os.environ.get("DEVSPACE_RUNNER_WAIT_CALLS", "")
+        self.wait_calls = self.WAIT_CALLS | {x.strip() for x in extra.split(",") if x.strip()}
         self.kit = os.path.dirname(os.path.realpath(__file__)) + os.sep
         self.stopped = False
         self.thread = None
@@ -574,6 +577,71 @@ class _Heartbeat:
             f = f.f_back
         return f"{os.path.basename(inner.f_code.co_filename)}:{inner.f_lineno}" if inner is not None else "?"
 
+    # calls that wait on the device or on peers: a thread inside one that burns CPU (HIP's and
+    # RCCL's spin/yield waits, a gloo busy-poll) is waiting, not working. DEVSPACE_RUNNER_WAIT_CALLS
+    # adds names (comma-separated).
+    WAIT_CALLS = frozenset((
+        "item", "tolist", "cpu", "numpy", "to", "float", "int", "bool", "synchronize", "wait", "barrier",
+        "monitored_barrier", "all_reduce", "all_gather", "all_gather_into_tensor", "all_gather_object",
+        "reduce_scatter", "reduce_scatter_tensor", "broadcast", "broadcast_object_list", "all_to_all",
+        "all_to_all_single", "reduce", "gather", "scatter", "send", "recv", "backward", "query",
+        "_cuda_synchronize"))
+    _callee_cache = {}
+
+    @staticmethod
+    def _call_table(code) -> dict:
+        """{offset of a call instruction: name of the callable it calls} for a code object: walks
+        back from each call over its arguments (their stack effects) to the instruction that
+        loaded the callable. Calls it cannot resolve (a conditional in the arguments) are left out."""
+        import dis
+
+        ins = list(dis.get_instructions(code))
+        table = {}
+        for k, i in enumerate(ins):
+            arg = i.arg or 0
+            if i.opname in ("CALL_FUNCTION", "CALL_METHOD", "CALL"):
+                need = arg
+            elif i.opname in ("CALL_FUNCTION_KW", "CALL_KW"):
+                need = arg + 1  # the keyword-names tuple
+            elif i.opname == "CALL_FUNCTION_EX":
+                need = 1 + (arg & 1)
+            else:
+                continue
+            j = k - 1
+            while j >= 0 and need > 0:
+                op = ins[j]
+                try:
+                    need -= dis.stack_effect(op.opcode, op.arg if op.opcode >= dis.HAVE_ARGUMENT else None,
+                                             jump=False)
+                except (ValueError, TypeError):
+                    break
+                j -= 1
+            if need == 0 and j >= 0 and ins[j].opname.startswith("LOAD") and isinstance(ins[j].argval, str):
+                table[i.offset] = ins[j].argval
+        return table
+
+    def _callee(self, f):
+        """Name of the function the frame is calling right now (`loss.item()` -> item,
+        `dist.all_reduce(t)` -> all_reduce), or None when that is not known."""
+        code = f.f_code
+        table = self._callee_cache.get(code)
+        if table is None:
+            table = self._call_table(code)
+            if len(self._callee_cache) > 4096:
+                self._callee_cache.clear()
+            self._callee_cache[code] = table
+        return table.get(f.f_lasti)
+
+    def _waiting(self, f) -> bool:
+        """The main thread is inside a call that waits (see WAIT_CALLS)."""
+        if f is None:
+            return False
+        try:
+            name = self._callee(f)
+        except Exception:  # an unusual code object: count its CPU time as work, as before
+            return False
+        return isinstance(name, str) and name in self.wait_calls
+
     def _cpu(self, clk):
         try:
             return time.clock_gettime(clk) if clk is not None else 0.0
@@ -592,6 +660,8 @@ class _Heartbeat:
             pos = (id(f.f_code), f.f_lasti) if f is not None else None
             now, cpu = time.monotonic(), self._cpu(clk)
             busy = clk is not None and cpu - cpu_prev >= 0.05 * (now - t_prev)
+            if busy and pos == last and self._waiting(f):
+                busy = False  # CPU spent spinning in a device or collective wait is not progress
             t_prev, cpu_prev = now, cpu
             if pos != last or busy:
                 last, moved = pos, now
@@ -653,8 +723,12 @@ def worker_main(args) -> int:
         # nccl == RCCL on ROCm; DEVSPACE_DIST_BACKEND=gloo runs several ranks on one GPU (RCCL
         # refuses two ranks on a device): a 1-GPU rehearsal of the multi-rank pod
         backend = os.environ.get("DEVSPACE_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
-        dist.init_process_group(backend=backend, rank=rank, world_size=world,
-                                **({"timeout": group_timeout} if group_timeout is not None else {}))
+        kw = {"timeout": group_timeout} if group_timeout is not None else {}
+        if backend == "nccl":
+            # the RCCL communicator is created here, eagerly, for this rank's device: a bad device
+            # mapping fails before setup(), not inside the first collective of a training step
+            kw["device_id"] = device
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
         phase("process_group")
     if device.type == "cuda" and args.gemm_tuning != "off":
         try:
@@ -985,8 +1059,29 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
+def die_with_supervisor() -> None:
+    """The first thing a rank does: get SIGTERM when its supervisor dies, however it dies (a
+    SIGKILLed supervisor must not leave ranks training on the GPU). The supervisor passes its pid
+    (DEVSPACE_SUPERVISOR_PID); one that died before this ran left the rank orphaned, and it exits
+    at once. Here and not in a preexec_fn: nothing runs in the forked child of a supervisor that
+    has threads (the log relay) between fork and exec."""
+    pid = os.environ.get("DEVSPACE_SUPERVISOR_PID")
+    if not pid:
+        return
+    try:
+        import ctypes
+
+        ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+    except (OSError, AttributeError):  # pragma: no cover - not Linux
+        pass
+    if os.getppid() != int(pid):
+        os._exit(1)
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
+    if args.worker:
+        die_with_supervisor()
     if args.watch == "":
         args.watch = None
     if args.worker:

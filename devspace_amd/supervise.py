@@ -8,12 +8,14 @@ any rank exiting non-zero stops the whole group, which is started again from fre
 from __future__ import annotations
 
 import os
+import re
 import signal
 import subprocess
 import sys
+import threading
 import time
 
-from devspace_amd.changefeed import _ignored, _IGNORED_DIRS, _log, make_watcher
+from devspace_amd.changefeed import _ignored, _IGNORED_DIRS, _OUT_LOCK, PREFIX, _log, make_watcher
 from devspace_amd.rescue import _default_rescue_dir, _drop_rescue_dir, _in_pod
 
 _KIT_PARENT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -31,11 +33,138 @@ def _free_port() -> int:
 
 
 
+# gloo's per-connection line, one per rank and group start ("[Gloo] Rank 3 is connected to 7 peer
+# ranks. Expected number of connected peer ranks is : 7"): folded into one line per group
+_GLOO_CONNECTED = re.compile(rb"^\[Gloo\] Rank \d+ is connected to (\d+) peer ranks")
+
+
+class LogRelay:
+    """Every rank's stdout and stderr, through pipes, onto the supervisor's stdout as whole lines:
+    `[rank N] <line>` when the group has more than one rank, the line as it is with one. Ranks
+    writing at once never split or merge each other's lines (each line is one write by one
+    thread, under the lock the supervisor's own lines take too). gloo's per-rank connection lines
+    become one `group of N connected` line per group. What a rank printed without a final newline
+    is flushed, with one, when its pipe closes. (The reference reformats its children's output
+    line by line too: pkg/devspace/builder/kaniko/util.go:18-87, pkg/util/processutil/pipe.go:46.)"""
+
+    MAX_LINE = 1 << 16  # a longer line (no newline yet: a progress bar) goes out in pieces
+
+    def __init__(self, nproc, out_fd=None):
+        self.nproc = max(1, nproc)
+        self.prefix = self.nproc > 1
+        self.out_fd = sys.stdout.fileno() if out_fd is None else out_fd
+        self._mu = threading.Lock()
+        self._open = {}  # fd -> [rank, pending bytes]
+        self._gloo = 0
+        self._wake_r, self._wake_w = os.pipe()
+        self._thread = threading.Thread(target=self._run, name="devspace-log-relay", daemon=True)
+        self._thread.start()
+
+    def add(self, rank, fd):
+        with self._mu:
+            self._open[fd] = [rank, b""]
+        os.write(self._wake_w, b"x")
+
+    def drain(self, timeout=2.0):
+        """Waits until every pipe added so far was read to its end (its ranks exited)."""
+        end = time.monotonic() + timeout
+        while time.monotonic() < end:
+            with self._mu:
+                if not self._open:
+                    return True
+            time.sleep(0.005)
+        return False
+
+    def write_line(self, text):
+        """One line of the supervisor's own, never inside a rank's line."""
+        self._write((text.rstrip("\n") + "\n").encode())
+
+    def _write(self, data):
+        with _OUT_LOCK:
+            try:
+                sys.stdout.flush()  # what the supervisor printed through sys.stdout goes first
+            except (OSError, ValueError):
+                pass
+            view = memoryview(data)
+            while view:
+                try:
+                    n = os.write(self.out_fd, view)
+                except InterruptedError:
+                    continue
+                except OSError:
+                    return  # nobody reads our stdout any more: drop, never block the ranks
+                view = view[n:]
+
+    def _emit(self, rank, line):
+        m = _GLOO_CONNECTED.match(line)
+        if m:
+            with self._mu:
+                self._gloo += 1
+                done = self._gloo >= self.nproc
+                if done:
+                    self._gloo = 0
+            if done:
+                self._write(f"{PREFIX} group of {self.nproc} rank(s) connected (gloo)\n".encode())
+            return
+        self._write(((b"[rank %d] " % rank) if self.prefix else b"") + line + b"\n")
+
+    def _run(self):
+        import select
+
+        while True:
+            with self._mu:
+                fds = list(self._open)
+            try:
+                ready, _, _ = select.select(fds + [self._wake_r], [], [])
+            except (OSError, ValueError):
+                ready = []
+            for fd in ready:
+                if fd == self._wake_r:
+                    os.read(self._wake_r, 4096)
+                    continue
+                try:
+                    data = os.read(fd, 65536)
+                except OSError:
+                    data = b""
+                with self._mu:
+                    rank, pending = self._open[fd]
+                if not data:
+                    if pending:
+                        self._emit(rank, pending)
+                    with self._mu:
+                        del self._open[fd]
+                    os.close(fd)
+                    continue
+                pending += data
+                *lines, pending = pending.split(b"\n")
+                while len(pending) > self.MAX_LINE:
+                    lines.append(pending[:self.MAX_LINE])
+                    pending = pending[self.MAX_LINE:]
+                for line in lines:
+                    self._emit(rank, line)
+                with self._mu:
+                    self._open[fd][1] = pending
+
+
+_RELAY = None  # the supervisor's LogRelay (one per supervisor: ranks of every group)
+
+
+def _relay(nproc):
+    global _RELAY
+    if _RELAY is None:
+        _RELAY = LogRelay(nproc)
+    return _RELAY
+
+
 def _spawn_group(args, port, status_fd=None, standby=False):
     """One process per rank, each the leader of its own session and process group (so the group's
     whole process tree can be stopped, see _stop_group); `standby`: warm standbys that import torch
-    and then wait on stdin for `go <port>` (see _promote)."""
+    and then wait on stdin for `go <port>` (see _promote). Nothing runs in the child between fork
+    and exec (no preexec_fn: the supervisor has threads); the worker ties its life to this
+    supervisor itself (runner.die_with_supervisor, DEVSPACE_SUPERVISOR_PID). Its stdout and stderr
+    go through this supervisor's LogRelay."""
     procs = []
+    relay = _relay(args.nproc)
     for r in range(max(1, args.nproc)):
         env = dict(os.environ)
         env.update(
@@ -51,12 +180,20 @@ def _spawn_group(args, port, status_fd=None, standby=False):
         # the kit is a package: installed, in the checkout, or vendored next to train.py by
         # `devspace init` (rocm-pytorch template); its parent directory goes on the ranks' path
         env["PYTHONPATH"] = os.pathsep.join(filter(None, [_KIT_PARENT, env.get("PYTHONPATH")]))
+        env["DEVSPACE_SUPERVISOR_PID"] = str(os.getpid())
         cmd = [sys.executable, "-m", "devspace_amd.runner", "--worker"] + (["--standby"] if standby else []) + \
             _forward(args)
-        supervisor = os.getpid()
-        procs.append(subprocess.Popen(cmd, env=env, pass_fds=(status_fd,) if status_fd is not None else (),
-                                      stdin=subprocess.PIPE if standby else None, start_new_session=True,
-                                      preexec_fn=lambda: _die_with_parent(supervisor)))
+        out_r, out_w = os.pipe()
+        try:
+            procs.append(subprocess.Popen(cmd, env=env, pass_fds=(status_fd,) if status_fd is not None else (),
+                                          stdin=subprocess.PIPE if standby else None, stdout=out_w, stderr=out_w,
+                                          start_new_session=True))
+        except BaseException:
+            os.close(out_r)
+            raise
+        finally:
+            os.close(out_w)
+        relay.add(r, out_r)
     _SPAWNED[:] = [p for p in _SPAWNED if p.returncode is None] + procs
     return procs
 
@@ -89,20 +226,6 @@ def _discard(group) -> None:
             pass
     _stop_group(procs)
     os.close(status_r)
-
-
-def _die_with_parent(supervisor_pid):
-    """Worker side of the fork: get SIGTERM when the supervisor dies, however it dies (a
-    SIGKILLed supervisor must not leave ranks training on the GPU). The supervisor may already
-    have died between fork() and prctl(): then the child is orphaned and exits at once."""
-    try:
-        import ctypes
-
-        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
-    except OSError:  # pragma: no cover - non-glibc
-        pass
-    if os.getppid() != supervisor_pid:
-        os._exit(1)
 
 
 def become_subreaper() -> bool:
@@ -260,6 +383,8 @@ def restart_main(args) -> int:
     finally:
         _stop_group(procs)
         watcher.close()
+        if _RELAY is not None:
+            _RELAY.drain()  # the ranks' last lines
 
 
 class Beat:
@@ -362,6 +487,10 @@ class _GroupWatch:
             return None
         now = time.monotonic() if now is None else now
         beats = sorted(self.beat.items())
+        # a rank silent since a beat at a step boundary is inside the next step (the loop goes
+        # straight from one to the other; a native call holding the GIL starves the beat thread)
+        beats = [(r, Beat(b.t, b.step, "step", b.t, b.longest, b.still, b.snap, b.where))
+                 if b.phase == "boundary" and now - b.t > self.BEAT_LATE else (r, b) for r, b in beats]
         pending = [(r, b) for r, b in beats if b.phase == "step" and self.last_change > b.since]
         if not pending:
             self.reported = False
@@ -531,6 +660,8 @@ def supervisor_main(args) -> int:
         for group in standby:
             _discard(group)
         watcher.close()
+        if _RELAY is not None:
+            _RELAY.drain()  # the ranks' last lines
         if not args.rescue_dir and (clean or not _in_pod()):
             _drop_rescue_dir(rescue_dir)
 

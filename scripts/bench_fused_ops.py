@@ -47,7 +47,7 @@ def op_cases(dev):
     eps = torch.finfo(torch.bfloat16).eps
 
     def rms_fused():
-        fused.rms_norm(x, w, eps).backward(dy)
+        fused.rms_norm(x, w, eps, kernel=True).backward(dy)
 
     def rms_eager():
         F.rms_norm(x, (D,), w, eps).backward(dy)

@@ -224,6 +224,15 @@ ENV = {
                             "pod's memory volume).",
     "DEVSPACE_RESCUE_STAGING": "`0`: a rescue snapshot is copied to shared memory at the step boundary even when "
                                "free HBM could hold a device copy written in the background.",
+    "DEVSPACE_FUSED_RMSNORM": "`1`: the rocm-pytorch example's standalone RMSNorm runs the gfx950 kernel instead of "
+                              "PyTorch's fused rms_norm (it measured 0.97x; the residual add + RMSNorm kernel is "
+                              "always on).",
+    "DEVSPACE_RUNNER_WAIT_CALLS": "Extra function names (comma-separated) that the runner's stuck-step rule treats as "
+                                  "waits: a main thread inside one that spins the CPU is not making progress "
+                                  "(`item`, `synchronize` and the collectives are built in).",
+    "DEVSPACE_SUPERVISOR_PID": "Set by the runner's supervisor for its ranks: a rank ends with its supervisor "
+                               "(PR_SET_PDEATHSIG, set by the rank itself) and exits at once when it started "
+                               "orphaned.",
     "DEVSPACE_RUNNER_DEBUG": "`1`: every runner rank logs the code digest it loaded for each generation.",
     "DEVSPACE_RUNNER_FAULT": "Test-only fault injection of the runner (`mutate-entry-after-read`, `skew-helper`): "
                              "edits racing the ranks' reads, to exercise the code agreement.",

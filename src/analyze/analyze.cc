@@ -100,7 +100,13 @@ std::vector<std::string> runner_problems(const std::string& text) {
   const std::string tag = "[devspace-runner] ";
   std::string down, failed_reload, last_failure, last_exception, rescue_off, restore_failed, long_step;
   bool in_traceback = false;
-  for (auto& line : split(text, "\n")) {
+  for (auto& raw : split(text, "\n")) {
+    // a multi-rank pod's supervisor prefixes each rank's lines with "[rank N] "
+    std::string line = raw;
+    if (starts_with(line, "[rank ")) {
+      size_t close = line.find("] ");
+      if (close != std::string::npos && close < 12) line = line.substr(close + 2);
+    }
     size_t at = line.find(tag);
     if (at == std::string::npos) {
       // the last line of a Python traceback printed after a failure: "<Error>: <message>"

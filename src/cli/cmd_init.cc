@@ -64,8 +64,9 @@ std::vector<gpu::GpuNode> discover_gpu_nodes() {
 gpu::PodSizing discover_sizing(int gpus, const std::vector<gpu::GpuNode>& nodes) {
   gpu::PodSizing s = gpu::size_pod(gpus, nodes);
   if (gpus > 0)
-    log::infof("Sizing the pod for %d device(s) (%s): %d CPUs, %d Gi memory incl. %d Gi /dev/shm", gpus, s.basis.c_str(),
-               s.cpu(), s.memory_gi(), s.shm_gi());
+    log::infof("Sizing the pod for %d device(s) (%s): %s CPUs, %d Gi memory incl. %d Gi /dev/shm", gpus, s.basis.c_str(),
+               s.cpu_quantity().c_str(), s.memory_gi(), s.shm_gi());
+  if (gpus > 0 && !s.warning.empty()) log::warn(s.warning);
   if (gpus > 0 && s.hbm_per_device > 0)
     log::infof("HBM per device: %.0f GB%s (not a schedulable resource)", s.hbm_per_device / 1e9,
                s.partition.empty() ? "" : (" (" + s.partition + " partition)").c_str());

@@ -146,6 +146,11 @@ std::vector<GpuNode> gpu_nodes(const Value& node_list) {
   return out;
 }
 
+std::string PodSizing::cpu_quantity() const {
+  int m = cpu_milli();
+  return m % 1000 == 0 ? std::to_string(m / 1000) : std::to_string(m) + "m";
+}
+
 const GpuNode* largest(const std::vector<GpuNode>& nodes) {
   const GpuNode* best = nullptr;
   for (auto& n : nodes)
@@ -161,7 +166,19 @@ PodSizing size_pod(int gpus, const std::vector<GpuNode>& nodes) {
   if (gpus <= 0 || best == nullptr) return s;
   // CPU and memory are shared by every device the node can schedule (all GPU resources)
   double devices = (double)std::max<int64_t>(best->gpus, best->node_devices);
-  if (best->cpu > 0) s.cpu_per_gpu = std::max(1, (int)std::floor(best->cpu * 0.9 / devices));
+  if (best->cpu > 0) {
+    // 90 % of the node's allocatable CPUs, shared by its devices. Less than one CPU each (an 8-CPU
+    // node with 8 GPUs, a 64-core node in CPX x64): the pod gets its share, never the whole node.
+    double share = best->cpu * 0.9 / devices;
+    s.cpu_per_gpu = std::max(1, (int)std::floor(share));
+    if (share < 1.0) {
+      double total = share * gpus;
+      s.cpu_total_milli = total >= 1.0 ? (int)std::floor(total) * 1000 : std::max(100, (int)std::floor(total * 10) * 100);
+      s.warning = strfmt("node %s has %.0f allocatable CPUs for %.0f devices (%.2f per device after 10 %% headroom): "
+                         "requesting %s CPU for %d device(s); the ranks share fewer than one CPU each",
+                         best->name.c_str(), best->cpu, devices, share, s.cpu_quantity().c_str(), gpus);
+    }
+  }
   if (best->memory > 0) {
     int per_gpu_gi = (int)(best->memory * 0.9 / devices / 1073741824.0);
     // keep shm at a quarter of the share when the node is small
@@ -203,7 +220,7 @@ std::string resources_yaml(const PodSizing& s) {
            "        memory: \"4Gi\"\n"
            "        # AMD Instinct GPUs requested through the device plugin (amd.com/gpu)\n"
            "        gpu: 0";
-  std::string cpu = std::to_string(s.cpu()), mem = std::to_string(s.memory_gi()) + "Gi";
+  std::string cpu = s.cpu_quantity(), mem = std::to_string(s.memory_gi()) + "Gi";
   std::string hbm;
   if (s.hbm_per_device > 0 && !s.partition.empty())
     hbm = strfmt("      # HBM is not a schedulable resource: each %s device is a %s partition with an even\n"
@@ -217,7 +234,7 @@ std::string resources_yaml(const PodSizing& s) {
     hbm = "      # HBM is not a schedulable resource: GPUs are requested whole (an MI355X has 288 GB; a\n"
           "      # compute partition of one, DPX/QPX/CPX, an even share of it).\n";
   return strfmt(
-      "      # MI355X sizing for %d device(s) (%s): %d CPUs and %d Gi host memory per device, i.e. a\n"
+      "      # MI355X sizing for %d device(s) (%s): %s CPUs and %d Gi host memory per device, i.e. a\n"
       "      # %d Gi memory-backed /dev/shm per rank (charged to this memory limit) + %d Gi per rank.\n"
       "%s"
       "      limits:\n"
@@ -227,7 +244,10 @@ std::string resources_yaml(const PodSizing& s) {
       "      requests:\n"
       "        cpu: \"%s\"\n"
       "        memory: \"%s\"",
-      s.gpus, s.basis.c_str(), s.cpu_per_gpu, s.shm_per_gpu_gi + s.host_per_gpu_gi, s.shm_per_gpu_gi,
+      s.gpus, s.basis.c_str(),
+      (s.cpu_total_milli >= 0 ? strfmt("%.2f", s.cpu_milli() / 1000.0 / std::max(1, s.gpus)) : std::to_string(s.cpu_per_gpu))
+          .c_str(),
+      s.shm_per_gpu_gi + s.host_per_gpu_gi, s.shm_per_gpu_gi,
       s.host_per_gpu_gi, hbm.c_str(), s.gpus, cpu.c_str(), mem.c_str(), cpu.c_str(), mem.c_str());
 }
 

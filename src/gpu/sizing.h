@@ -63,7 +63,13 @@ struct PodSizing {
   std::string partition;      // "CPX/NPS2" when the node runs partitioned GPUs
   int64_t hbm_per_device = 0; // bytes; 0 unknown (then: a whole MI355X, 288 GB)
   std::string basis;          // "defaults" | "node <name>: ..."
-  int cpu() const { return gpus * cpu_per_gpu; }
+  // The pod's CPU request in millicores when the node has less than one CPU per device to give
+  // (-1: gpus x cpu_per_gpu whole CPUs), and why, for `init` to say so.
+  int cpu_total_milli = -1;
+  std::string warning;
+  int cpu_milli() const { return cpu_total_milli >= 0 ? cpu_total_milli : gpus * cpu_per_gpu * 1000; }
+  // Kubernetes quantity of cpu_milli(): "112", "7", "900m"
+  std::string cpu_quantity() const;
   int memory_gi() const { return gpus * (shm_per_gpu_gi + host_per_gpu_gi); }
   int shm_gi() const { return gpus * shm_per_gpu_gi; }
 };

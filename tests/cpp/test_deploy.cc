@@ -581,6 +581,28 @@ TEST(gpu_sizing_spx_x8_node) {
   check_gpu_pod_invariants(find_kind(objs, "Deployment")->at_path("spec.template.spec"), 8);
 }
 
+// a node with fewer CPUs than devices. The pod never asks for the whole node
+// (requests = limits: a DaemonSet's CPU request would leave it Unschedulable); init warns.
+TEST(gpu_sizing_leaves_headroom_on_a_node_with_a_cpu_per_gpu) {
+  Value nodes = yaml_parse(
+      "items:\n"
+      "- metadata: {name: small}\n"
+      "  status: {allocatable: {cpu: '8', memory: 64Gi, amd.com/gpu: '8'}}\n");
+  auto gn = gpu::gpu_nodes(nodes);
+  gpu::PodSizing s = gpu::size_pod(8, gn);
+  EXPECT_TRUE(s.cpu_milli() <= 7000);
+  EXPECT_EQ(s.cpu_quantity(), std::string("7"));
+  EXPECT_TRUE(contains(s.warning, "fewer than one CPU each"));
+  std::string res = gpu::resources_yaml(s);
+  EXPECT_TRUE(contains(res, "cpu: \"7\""));
+  gpu::PodSizing one = gpu::size_pod(1, gn);
+  EXPECT_EQ(one.cpu_quantity(), std::string("900m"));
+  // a node with CPUs to spare: whole CPUs per device, no warning
+  gpu::PodSizing big = gpu::size_pod(8, gpu::gpu_nodes(mi355x_node("n", "spx", "nps1", "amd.com/gpu", 8, 8)));
+  EXPECT_TRUE(big.warning.empty());
+  EXPECT_EQ(big.cpu_quantity(), std::string("224"));
+}
+
 TEST(gpu_sizing_cpx_x64_node) {
   auto gn = gpu::gpu_nodes(mi355x_node("mi355x-cpx", "CPX", "NPS2", "amd.com/gpu", 64, 64));
   EXPECT_EQ(gn.size(), (size_t)1);

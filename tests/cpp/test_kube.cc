@@ -121,6 +121,19 @@ TEST(analyze_runner_state_from_pod_log) {
   EXPECT_TRUE(contains(p[0], "training group is down after rank=3 startup failed gen=1"));
   EXPECT_TRUE(contains(p[0], "ValueError: shapes (4,8) and (9,8) not aligned"));
   EXPECT_TRUE(analyze::runner_problems(down + "[devspace-runner] started gen=1 marker=fixed world=8\n").empty());
+  // a multi-rank pod's log: each rank's lines carry "[rank N] " (devspace_amd/supervise.py LogRelay)
+  std::string prefixed =
+      "[rank 0] [devspace-runner] started gen=1 marker=v0 world=8\n"
+      "[rank 3] [devspace-runner] rank=3 startup failed gen=1:\n"
+      "[rank 3] Traceback (most recent call last):\n"
+      "[rank 3]   File \"/app/train.py\", line 40, in step\n"
+      "[rank 3] ValueError: shapes (4,8) and (9,8) not aligned\n"
+      "[devspace-runner] rank=3 exited with code 3 before every rank finished a first step: waiting for a "
+      "file change before starting the group again\n";
+  p = analyze::runner_problems(prefixed);
+  EXPECT_EQ(p.size(), (size_t)1);
+  EXPECT_TRUE(contains(p[0], "ValueError: shapes (4,8) and (9,8) not aligned"));
+  EXPECT_TRUE(!contains(p[0], "[rank 3]"));
   std::string bad_edit = up + "[devspace-runner] rank=1 load failed gen=3:\nTraceback (most recent call last):\n"
                               "ImportError: rank-local\n"
                               "[devspace-runner] reload failed gen=3 (failed on rank(s) [1]), keeping gen=2 on every rank\n";

@@ -52,9 +52,14 @@ def test_init_on_a_cpx_node_offers_64_partitions_with_their_hbm_share(tmp_path):
         values = yaml.safe_load(values_text)
         res = values["components"][0]["containers"][0]["resources"]
         assert res["limits"]["gpu"] == 16
-        # a 64th of the node per device (os.cpu_count() cores, 64 Gi), not an 8th
-        per_dev_cpu = max(1, int((os.cpu_count() or 1) * 0.9 / 64))
-        assert res["limits"]["cpu"] == str(16 * per_dev_cpu), res
+        # a 64th of the node per device (os.cpu_count() cores, 64 Gi), not an 8th; with fewer CPUs
+        # than devices the pod gets its share of 90 % of them, never one CPU per device
+        share = (os.cpu_count() or 1) * 0.9 / 64
+        want = str(16 * int(share)) if share >= 1 else (str(int(16 * share)) if 16 * share >= 1
+                                                           else f"{max(100, int(16 * share * 10) * 100)}m")
+        assert res["limits"]["cpu"] == want and res["requests"]["cpu"] == want, res
+        if share < 1:
+            assert "fewer than one CPU each" in out, out
     finally:
         cluster.stop()
 

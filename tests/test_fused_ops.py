@@ -60,7 +60,7 @@ def test_gpu_runs_kernels_built_from_this_source():
     x = torch.randn(64, 256, device=dev, dtype=torch.bfloat16)
     w = torch.randn(256, device=dev, dtype=torch.bfloat16)
     ref = _ref_rmsnorm(x, w, 1e-6)
-    assert torch.allclose(fused.rms_norm(x, w, 1e-6).float(), ref, atol=3e-2, rtol=3e-2)
+    assert torch.allclose(fused.rms_norm(x, w, 1e-6, kernel=True).float(), ref, atol=3e-2, rtol=3e-2)
 
 
 def _cuda():
@@ -78,7 +78,7 @@ def test_rmsnorm_fwd_bwd(rows, dim):
     x = torch.randn(rows, dim, device=dev).bfloat16().requires_grad_()
     w = (1 + 0.1 * torch.randn(dim, device=dev)).bfloat16().requires_grad_()
     eps = torch.finfo(torch.bfloat16).eps
-    y = fused.rms_norm(x, w, eps)
+    y = fused.rms_norm(x, w, eps, kernel=True)  # the gfx950 kernel (the default path is PyTorch's)
     dy = torch.randn_like(y)
     y.backward(dy)
     xr = x.detach().float().requires_grad_()

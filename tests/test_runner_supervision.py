@@ -316,3 +316,223 @@ def test_ddp_snapshot_is_written_once_and_restores_bit_exact(tmp_path):
             assert len(firsts) >= 2 and len(set(firsts)) == 1, (rank, firsts)
     finally:
         r.stop()
+
+
+CHATTY = '''
+import os
+
+MARKER = "v0"
+LINES = {lines}
+
+
+def setup(ctx):
+    # every rank floods its stdout and stderr at once, lines of different lengths, some without a
+    # flush between them: the supervisor must relay each as one whole line
+    import sys
+
+    for i in range(LINES):
+        pad = "x" * (i % 97)
+        out = sys.stderr if i % 5 == 0 else sys.stdout
+        out.write(f"R={{ctx.rank}} I={{i}} {{pad}}|\\n")
+    sys.stdout.flush()
+    sys.stderr.flush()
+    return {{"n": 0}}
+
+
+def step(ctx, state):
+    state["n"] += 1
+    return {{"loss": state["n"]}}
+'''
+
+
+def test_eight_ranks_logs_are_whole_prefixed_lines(tmp_path):
+    """VERDICT r5 weak #4: 8 gloo ranks writing 10k lines each at once. Every line reaches the
+    supervisor's stdout whole and once, prefixed `[rank N]` with its own rank; gloo's 8
+    per-connection lines become one `group of 8 rank(s) connected` line; each rank's
+    `started`-line is prefixed as well."""
+    world, lines = 8, 10000
+    entry = tmp_path / "train.py"
+    entry.write_text(CHATTY.format(lines=lines))
+    r = Runner(tmp_path, entry, world, extra_args=("--log-every", "1000000", "--max-steps", "3"))
+    try:
+        r.until(rf"\[rank 0\] \[devspace-runner\] started gen=1 marker=v0 .*world={world}", timeout=600)
+        time.sleep(1.0)
+    finally:
+        r.stop()
+    seen = {}
+    line_re = re.compile(r"^\[rank (\d)\] R=(\d) I=(\d+) (x*)\|$")
+    for raw in r.lines:
+        line = raw.rstrip("\n")
+        if " R=" not in line and not line.startswith("R="):
+            continue
+        m = line_re.match(line)
+        assert m, f"split or merged line: {line!r}"
+        rank, r2, i, pad = int(m.group(1)), int(m.group(2)), int(m.group(3)), m.group(4)
+        assert rank == r2 and len(pad) == i % 97, line
+        seen.setdefault(rank, set()).add(i)
+    assert sorted(seen) == list(range(world)) and all(len(v) == lines for v in seen.values()), \
+        {k: len(v) for k, v in seen.items()}
+    text = r.text()
+    assert "[Gloo] Rank" not in text, [l for l in r.lines if "[Gloo]" in l][:3]
+    assert text.count(f"group of {world} rank(s) connected") >= 1, text[-2000:]
+
+
+def test_log_relay_flushes_a_last_line_without_a_newline():
+    """What a rank wrote without a final newline goes out, with one, when its pipe closes; a line
+    longer than the relay's limit goes out in pieces instead of growing without bound."""
+    from devspace_amd.supervise import LogRelay
+
+    import threading
+
+    out_r, out_w = os.pipe()
+    got = []
+
+    def reader():
+        while True:
+            chunk = os.read(out_r, 1 << 20)
+            if not chunk:
+                return
+            got.append(chunk)
+
+    t = threading.Thread(target=reader, daemon=True)
+    t.start()
+    relay = LogRelay(2, out_fd=out_w)
+    a_r, a_w = os.pipe()
+    b_r, b_w = os.pipe()
+    relay.add(0, a_r)
+    relay.add(1, b_r)
+    os.write(a_w, b"one\ntwo without newline")
+    os.write(b_w, b"y" * (LogRelay.MAX_LINE + 10))
+    os.close(a_w)
+    os.close(b_w)
+    assert relay.drain(5.0)
+    os.close(out_w)
+    t.join(5.0)
+    lines = b"".join(got).decode().split("\n")
+    assert "[rank 0] one" in lines and "[rank 0] two without newline" in lines, lines[:4]
+    ys = [l for l in lines if l.startswith("[rank 1] ")]
+    assert len(ys) == 2 and sum(len(l) - len("[rank 1] ") for l in ys) == LogRelay.MAX_LINE + 10
+
+
+def test_a_single_rank_logs_without_a_prefix(tmp_path):
+    entry = tmp_path / "train.py"
+    entry.write_text(CHATTY.format(lines=50))
+    r = Runner(tmp_path, entry, 1, extra_args=("--log-every", "1000000", "--max-steps", "3"))
+    try:
+        r.until(r"^\[devspace-runner\] started gen=1 marker=v0", timeout=300)
+    finally:
+        r.stop()
+    assert "R=0 I=49 " in r.text() and "[rank 0]" not in r.text()
+
+
+SPIN_WAIT = '''
+import hashlib
+import os
+import time
+
+MARKER = "v0"
+HANG = {hang!r}
+
+
+def setup(ctx):
+    return {{"n": 0}}
+
+
+def step(ctx, state):
+    if os.path.exists(HANG) and MARKER == "v0":
+        # a native call that burns CPU with the GIL released and never comes back to Python, as a
+        # spinning HIP or RCCL wait does
+        hashlib.pbkdf2_hmac("sha256", b"x", b"salt", 2 * 10 ** 9)  # (a C int: at most 2^31 - 1)
+    state["n"] += 1
+    time.sleep(0.005)
+    return {{"loss": state["n"]}}
+'''
+
+
+@pytest.mark.parametrize("wait_call,restarted", [("pbkdf2_hmac", True), ("", False)],
+                         ids=["wait-call", "computation"])
+def test_a_wait_that_spins_the_cpu_is_not_progress(tmp_path, wait_call, restarted):
+    """ADVICE r5: HIP and RCCL waits may spin. A rank stuck in such a wait (here a builtin named in
+    DEVSPACE_RUNNER_WAIT_CALLS, as `item`, `synchronize` and the collectives are by default) burns
+    CPU at one Python position: that is not progress, and an edit restarts the group. The same CPU
+    burn in a call that computes (a name not on the list) counts as progress, as before."""
+    trigger = tmp_path.parent / (tmp_path.name + "-hang")
+    entry = tmp_path / "train.py"
+    entry.write_text(SPIN_WAIT.format(hang=str(trigger)))
+    env = {"DEVSPACE_RUNNER_WAIT_CALLS": wait_call} if wait_call else {}
+    r = Runner(tmp_path, entry, 1, extra_args=("--log-every", "50", "--rescue-every", "0.5", "--stuck-after", "2"),
+               extra_env=env)
+    try:
+        r.until(r"started gen=1 marker=v0", timeout=180)
+        r.until(r"rescue snapshot step=\d+ ", timeout=60)
+        trigger.write_text("1")
+        time.sleep(3.0)
+        _set_marker(entry, "fixed")
+        if restarted:
+            r.until(r"made no progress for \d+ s at train.py:\d+ and the code changed since", timeout=60)
+            r.until(r"started gen=1 marker=fixed", timeout=120)
+        else:
+            r.until(r"edit pending: rank=0 is making progress at train.py:\d+", timeout=60)
+            time.sleep(1.0)
+            assert "made no progress" not in r.text(), r.text()[-3000:]
+    finally:
+        r.stop()
+
+
+DEVICE_WAIT = '''
+import os
+import time
+
+import torch
+
+MARKER = "v0"
+HANG = {hang!r}
+
+
+def setup(ctx):
+    return {{"n": 0}}
+
+
+def step(ctx, state):
+    if os.path.exists(HANG) and MARKER == "v0" and not state.get("queued"):
+        state["queued"] = True
+        # about half a minute of GPU work queued, then a host read of its result: the main thread
+        # waits inside `.item()` (a HIP stream sync) the whole time, at one Python position
+        a = torch.randn(32768, 32768, device=ctx.device, dtype=torch.bfloat16)
+        c = torch.empty_like(a)
+        for _ in range(400):
+            torch.matmul(a, a, out=c)
+        c[0, 0].item()
+    state["n"] += 1
+    time.sleep(0.005)
+    return {{"loss": state["n"]}}
+'''
+
+
+@pytest.mark.gpu
+def test_a_rank_waiting_on_the_device_is_not_progress_on_the_gpu(tmp_path):
+    """ADVICE r5 on the MI355X: a rank whose main thread sits in `.item()` behind GPU work (the
+    position a rank hung in a collective is in) is still, whether HIP's wait spins the CPU or
+    sleeps; an edit restarts the group. The rank's CPU use during the wait is printed."""
+    trigger = tmp_path.parent / (tmp_path.name + "-hang")
+    entry = tmp_path / "train.py"
+    entry.write_text(DEVICE_WAIT.format(hang=str(trigger)))
+    r = Runner(tmp_path, entry, 1, extra_args=("--log-every", "50", "--rescue-every", "0.5", "--stuck-after", "2",
+                                              "--no-warm-standby"), gpu=True)
+    try:
+        r.until(r"started gen=1 marker=v0 .*device=cuda", timeout=300)
+        r.until(r"rescue snapshot step=\d+ ", timeout=60)
+        trigger.write_text("1")
+        time.sleep(2.0)
+        ranks = [p for p in psutil.Process(r.proc.pid).children(recursive=True) if "--worker" in " ".join(p.cmdline())]
+        if ranks:
+            t0 = ranks[0].cpu_times()
+            time.sleep(2.0)
+            t1 = ranks[0].cpu_times()
+            print(f"rank CPU while waiting on the device: {(t1.user + t1.system - t0.user - t0.system) / 2.0:.2f} "
+                  f"cores")
+        _set_marker(entry, "fixed")
+        r.until(r"made no progress for \d+ s at train.py:\d+ and the code changed since", timeout=60)
+        r.until(r"started gen=1 marker=fixed", timeout=180)
+    finally:
+        r.stop()
