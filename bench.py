@@ -788,6 +788,8 @@ def main():
     ap.add_argument("--transport", choices=("tls", "plain"), default="tls",
                     help="API server transport of the local cluster (tls = https + wss with mTLS, as a real cluster)")
     args = ap.parse_args()
+    # the `devspace` processes this bench starts end with it, however it ends
+    os.environ["DEVSPACE_PARENT_PID"] = str(os.getpid())
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -165,6 +165,9 @@ ENV = {
                             "follows the scan's cost (at most 5 % of a core).",
     "DEVSPACE_WATCHER": "`scan`: watch sync paths with the portable stat-scan watcher instead of the platform's "
                         "event backend (inotify on Linux). The portable build always scans.",
+    "DEVSPACE_PARENT_PID": "When `devspace`'s parent process has this pid, `devspace` ends (SIGTERM) when that "
+                           "parent dies, however it dies: test harnesses and scripts set it so no CLI outlives "
+                           "them (`tests/conftest.py`, `bench.py`).",
     "DEVSPACE_PORTFORWARD_HEDGE": "`1`: a held GET/HEAD/OPTIONS on a remote cluster (tunnel round trip of 5 ms or "
                                   "more) is hedged: a new attempt every third of a round trip while earlier ones are "
                                   "in flight; the app may see the request up to about four times. Default: one "

@@ -26,6 +26,8 @@ static void emit_net_stats() {
 
 int main(int argc, char** argv) {
   ds::plat::set_argv0(argc > 0 ? argv[0] : nullptr);
+  // a harness that wants its devspace children to end with it (tests/conftest.py) says so
+  if (const char* p = std::getenv("DEVSPACE_PARENT_PID")) ds::plat::tie_to_parent(std::atol(p));
   ds::cmd::install_signal_handlers();
   ds::log::logdir();  // construct the function-local statics the handler uses before registering it
   ds::trace::enabled();

@@ -1,5 +1,7 @@
 // Linux implementation of platform/platform.h (the default build).
 #include <fcntl.h>
+#include <signal.h>
+#include <sys/prctl.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
@@ -50,6 +52,13 @@ void Waker::drain() {
   uint64_t v;
   ssize_t r = ::read(rfd_, &v, sizeof(v));
   (void)r;
+}
+
+void tie_to_parent(long parent_pid) {
+  if (parent_pid <= 1) return;
+  if (::getppid() != (pid_t)parent_pid) return;  // started by someone else: not ours to tie
+  ::prctl(PR_SET_PDEATHSIG, SIGTERM);
+  if (::getppid() != (pid_t)parent_pid) ::kill(::getpid(), SIGTERM);  // it died in between
 }
 
 void set_argv0(const char*) {}

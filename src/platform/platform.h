@@ -60,6 +60,12 @@ class Waker {
   int wfd_ = -1;  // == rfd_ for an eventfd
 };
 
+// When this process's parent is `parent_pid`: SIGTERM to this process once that parent dies
+// (however it dies), so a CLI started by a test harness or a script never outlives it. Linux:
+// PR_SET_PDEATHSIG; POSIX: a thread that watches getppid(). A parent that already died before
+// this call ran: SIGTERM now. Another parent (a grandchild of `parent_pid`): nothing.
+void tie_to_parent(long parent_pid);
+
 // Remember argv[0] (main() calls this first): the POSIX build finds its own executable from it.
 void set_argv0(const char* argv0);
 // Absolute path of the running executable, "" when unknown.

@@ -2,6 +2,7 @@
 // system calls, so it is the starting point of the darwin client (docs/platforms.md lists what
 // darwin and windows still need).
 #include <fcntl.h>
+#include <signal.h>
 #include <netdb.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
@@ -12,6 +13,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <mutex>
+#include <thread>
 
 #include "platform/platform.h"
 
@@ -100,6 +102,14 @@ void Waker::drain() {
   char buf[64];
   while (::read(rfd_, buf, sizeof(buf)) > 0) {
   }
+}
+
+void tie_to_parent(long parent_pid) {
+  if (parent_pid <= 1 || ::getppid() != (pid_t)parent_pid) return;
+  std::thread([parent_pid] {
+    while (::getppid() == (pid_t)parent_pid) ::usleep(200000);  // re-parented: the parent died
+    ::kill(::getpid(), SIGTERM);
+  }).detach();
 }
 
 void set_argv0(const char* argv0) {

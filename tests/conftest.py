@@ -11,6 +11,10 @@ sys.path.insert(0, ROOT)
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running")
+    # every `devspace` this test run starts ends with it, even when pytest itself is killed (a
+    # timeout's os._exit, SIGKILL): the CLI ties itself to this pid (PR_SET_PDEATHSIG,
+    # src/platform/linux.cc tie_to_parent) when it is its parent
+    os.environ["DEVSPACE_PARENT_PID"] = str(os.getpid())
     # a hung test ends the run with every thread's stack (pytest-timeout) instead of stalling it:
     # the longest test takes about 5 minutes; an explicit --timeout wins
     if getattr(config.option, "timeout", None) is None and config.pluginmanager.hasplugin("timeout"):
