@@ -123,6 +123,9 @@ CONFIG = {
     "images.<name>.build.kaniko.cache": "Use kaniko's layer cache (default true).",
     "images.<name>.build.kaniko.namespace": "Namespace of the build pod.",
     "images.<name>.build.kaniko.pullSecret": "Secret with registry credentials for the build pod.",
+    "images.<name>.build.kaniko.image": "Executor image of the build pod (default: the reference's pinned "
+                                        "`gcr.io/kaniko-project/executor:debug-…`; a debug variant, the build runs "
+                                        "by exec in its `/busybox`). `DEVSPACE_KANIKO_IMAGE` when unset.",
     "images.<name>.build.docker": "Docker daemon builds.",
     "images.<name>.build.docker.preferMinikube": "Build in minikube's Docker daemon when the context is minikube "
                                                  "(default true).",
@@ -165,6 +168,9 @@ ENV = {
                             "follows the scan's cost (at most 5 % of a core).",
     "DEVSPACE_WATCHER": "`scan`: watch sync paths with the portable stat-scan watcher instead of the platform's "
                         "event backend (inotify on Linux). The portable build always scans.",
+    "DEVSPACE_KANIKO_IMAGE": "The kaniko executor image for in-cluster builds when the config sets none "
+                             "(`images.*.build.kaniko.image`); default the reference's pinned debug build. It must be "
+                             "a debug variant (the build runs by exec in its `/busybox` shell).",
     "DEVSPACE_PARENT_PID": "When `devspace`'s parent process has this pid, `devspace` ends (SIGTERM) when that "
                            "parent dies, however it dies: test harnesses and scripts set it so no CLI outlives "
                            "them (`tests/conftest.py`, `bench.py`).",

@@ -24,6 +24,8 @@
 namespace ds {
 namespace build {
 
+// the reference's executor (pkg/devspace/builder/kaniko/kaniko.go:120); images.*.build.kaniko.image
+// or DEVSPACE_KANIKO_IMAGE choose another
 static const char* const kKanikoImage = "gcr.io/kaniko-project/executor:debug-5ac29a97734170a0547fea33b348dc7c328e2f8a";
 static const char* const kDefaultEmail = "noreply@devspace.cloud";
 
@@ -303,7 +305,7 @@ class KanikoBuilder : public Builder {
     pod["metadata"]["labels"]["devspace-build-id"] = random_lower_alnum(12);
     Value c = Value::map();
     c["name"] = "kaniko";
-    c["image"] = kKanikoImage;
+    c["image"] = s_.kaniko_image.empty() ? std::string(kKanikoImage) : s_.kaniko_image;
     c["imagePullPolicy"] = "IfNotPresent";
     c["command"] = Value::strings({"/busybox/sleep"});
     c["args"] = Value::strings({"36000"});
@@ -371,7 +373,7 @@ class KanikoBuilder : public Builder {
     }
     log::stop_wait();
     if (!ready) throw std::runtime_error("Unable to start build pod");
-    log::done("Kaniko build pod started");
+    log::done("Kaniko build pod started (" + c["image"].as_string() + ")");
 
     std::vector<std::string> ignore = collect_dockerignore_rules(ctx);
     log::start_wait("Uploading files to build container");
@@ -461,6 +463,15 @@ std::unique_ptr<Builder> create_builder(const Value& cfg, const Value& ic, const
     s.kaniko_namespace = kan.get("namespace").as_string();
     if (s.kaniko_namespace.empty()) s.kaniko_namespace = config::default_namespace(cfg);
     s.kaniko_pull_secret = kan.get("pullSecret").as_string();
+    s.kaniko_image = kan.get("image").as_string();
+    if (const char* e = getenv("DEVSPACE_KANIKO_IMAGE"); e && *e && s.kaniko_image.empty()) s.kaniko_image = e;
+    if (!s.kaniko_image.empty()) {
+      std::string why = image_reference_problem(s.kaniko_image);
+      if (!why.empty()) throw std::runtime_error("invalid kaniko image \"" + s.kaniko_image + "\": " + why);
+      if (!contains(split_image_tag(s.kaniko_image).second, "debug"))
+        log::warn("kaniko image " + s.kaniko_image +
+                  " is not a debug build: devspace runs the build by exec and needs its /busybox shell");
+    }
     s.no_cache = kan.has("cache") && !kan.get("cache").as_bool(true);
     return std::make_unique<KanikoBuilder>(kube, s, o);
   }

@@ -49,6 +49,9 @@ struct ImageBuildSettings {
   bool insecure = false;
   bool no_cache = false;
   std::string kaniko_namespace, kaniko_pull_secret;
+  // the executor image (images.*.build.kaniko.image, DEVSPACE_KANIKO_IMAGE; default: the
+  // reference's pinned debug build). It needs the debug variant's /busybox: the build runs by exec.
+  std::string kaniko_image;
   bool prefer_minikube = true;
 };
 

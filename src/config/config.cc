@@ -121,7 +121,8 @@ SP build_latest() {
                                      {"selectors", list(selector)},
                                      {"ports", list(ports)},
                                      {"sync", list(sync)}});
-  auto kaniko = st("latest.KanikoConfig", {{"cache", boolean()}, {"namespace", str()}, {"pullSecret", str()}});
+  auto kaniko = st("latest.KanikoConfig",
+                   {{"cache", boolean()}, {"namespace", str()}, {"pullSecret", str()}, {"image", str()}});
   auto docker = st("latest.DockerConfig", {{"preferMinikube", boolean()}});
   auto opts = st("latest.BuildOptions", {{"buildArgs", dict(str())}, {"target", str()}, {"network", str()}});
   auto build = st("latest.BuildConfig", {{"disabled", boolean()},

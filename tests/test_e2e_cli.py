@@ -335,11 +335,41 @@ def test_kaniko_in_cluster_build(localkube):
         lk.env["DOCKER_HOST"] = env_backup
     assert "with engine 'kaniko'" in out
     assert "Done building image" in out, out
+    assert "Kaniko build pod started (gcr.io/kaniko-project/executor:debug-5ac29a97734170a0547fea33b348dc7c328e2f8a)" \
+        in out, out  # the reference's executor by default
     pods = wait_for(lambda: running(lk.pods("kaniko", "app.kubernetes.io/component=default")), what="app pod")
     assert pods[0]["spec"]["containers"][0]["image"].startswith("devspace-local/kaniko-app:")
     # the build pod is deleted after the build
     wait_for(lambda: not lk.pods("kaniko", "devspace-build-id"), what="build pod cleanup")
     lk.run(["purge"], proj)
+
+
+def test_kaniko_executor_image_is_configurable(localkube):
+    """the executor is no longer pinned to the reference's 2019 build:
+    images.*.build.kaniko.image (or DEVSPACE_KANIKO_IMAGE) names another one."""
+    import yaml
+
+    lk = localkube
+    proj = lk.project("kaniko", "kaniko-newer")
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    for img in cfg["images"].values():
+        img["build"]["kaniko"]["image"] = "gcr.io/kaniko-project/executor:v1.23.2-debug"
+    open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    env_backup = lk.env.pop("DOCKER_HOST")
+    try:
+        out = lk.run(["deploy"], proj, timeout=180).stdout
+        assert "Kaniko build pod started (gcr.io/kaniko-project/executor:v1.23.2-debug)" in out, out
+        assert "Done building image" in out, out
+        # a non-debug executor has no /busybox to exec the build in: said up front
+        for img in cfg["images"].values():
+            img["build"]["kaniko"]["image"] = "gcr.io/kaniko-project/executor:v1.23.2"
+        open(cfg_path, "w").write(yaml.safe_dump(cfg))
+        p = lk.run(["deploy", "--force-build"], proj, timeout=180, check=False)
+        assert "is not a debug build" in p.stdout + p.stderr, p.stdout + p.stderr
+    finally:
+        lk.env["DOCKER_HOST"] = env_backup
+        lk.run(["purge"], proj, check=False)
 
 
 def _make_chart_repo(base):
