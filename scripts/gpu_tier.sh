@@ -11,6 +11,7 @@
 #   rescue  the runner's snapshot cost on the flagship example (scripts/rescue_cost.py)
 #   kernels the gfx950 fused ops against the eager op chains they replace (scripts/bench_fused_ops.py)
 #   layers  the rocm-pytorch image built with RUN executed, then rebuilt after an edit (scripts/image_rebuild_cost.py)
+#   digest  the rescue snapshots' content digest: gfx950 state_digest kernel vs torch ops (scripts/digest_cost.py)
 #
 # Output: gpurun_out/$GPU_TIER_TAG/ (default "tier"). Every GPU step has its own time limit and
 # the script stops at the first failing step: no GPU step runs after a fault or a timeout.
@@ -66,6 +67,11 @@ for s in "${steps[@]}"; do
       timeout -k 10 600 python -u scripts/rescue_cost.py > "$OUT/rescue.json" 2> "$OUT/rescue.err" \
         || fail rescue $? "$OUT/rescue.err"
       tail -1 "$OUT/rescue.json"
+      ;;
+    digest)
+      timeout -k 10 300 python -u scripts/digest_cost.py > "$OUT/digest.json" 2> "$OUT/digest.err" \
+        || fail digest $? "$OUT/digest.err"
+      tail -1 "$OUT/digest.json"
       ;;
     layers)
       timeout -k 10 900 python -u scripts/image_rebuild_cost.py > "$OUT/layers.json" 2> "$OUT/layers.err" \

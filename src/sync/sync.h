@@ -5,12 +5,14 @@
 //   Mode::Compat — byte-for-byte the reference's POSIX scripts and timing constants
 //                  (600 ms upload window, 1300 ms downstream poll + stability rule,
 //                  `sleep 0.1` receive polling). Used as the reference-equivalent baseline.
-//   Mode::Fast   — POSIX-only but streamed: inotify + ~15 ms coalescing, `head -c N | tar x`
+//   Mode::Fast   — POSIX-only but streamed: the platform's tree watcher (platform/watch.h:
+//                  inotify on Linux, the stat-scan watcher in the portable build) + ~15 ms
+//                  coalescing, `head -c N | tar x`
 //                  (no temp files / polling), newline acks; downstream `find -cnewer` change
 //                  probes every 250 ms after activity, backing off to 1.3 s when idle.
 //   Mode::Helper — uploads a static helper (src/helper) into the container that speaks a
 //                  framed binary protocol (64-bit lengths, chunk-streamed archives) and pushes
-//                  inotify events for event-driven downstream; falls back to Fast when it
+//                  the pod's inotify events for event-driven downstream; falls back to Fast when it
 //                  cannot run.
 #pragma once
 
