@@ -19,6 +19,11 @@
 // numeric path); numerics are tested against fp32 PyTorch in tests/test_fused_ops.py.
 #include <hip/hip_runtime.h>
 #include <torch/extension.h>
+#include <ATen/Parallel.h>
+
+#include <atomic>
+#include <thread>
+#include <vector>
 #include <c10/hip/HIPStream.h>
 
 #include <cmath>
@@ -1367,6 +1372,69 @@ at::Tensor state_digest(std::vector<at::Tensor> words) {
   return out;
 }
 
+// The same (S, M) pairs for int64 CPU tensors, one pass over the words, rows in parallel
+// (torch's intra-op threads): what the rescue digests use for CPU-resident state when this
+// extension is loaded (the torch-op formulation makes a dozen passes).
+static inline unsigned long long mix64_host(unsigned long long z) {
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z;
+}
+
+// one row: four words per iteration, independent chains (the multiplies overlap)
+static void digest_row_host(const unsigned long long* p, long long b, long long e, unsigned long long* out) {
+  const unsigned long long kGolden = 0x9E3779B97F4A7C15ull;
+  unsigned long long S[4] = {0, 0, 0, 0}, M[4] = {0, 0, 0, 0};
+  long long i = b;
+  for (; i + 4 <= e; i += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned long long v = p[i + u];
+      S[u] += v;
+      M[u] += mix64_host(v ^ ((unsigned long long)(i + u + 1) * kGolden));
+    }
+  }
+  for (; i < e; ++i) {
+    S[0] += p[i];
+    M[0] += mix64_host(p[i] ^ ((unsigned long long)(i + 1) * kGolden));
+  }
+  out[0] = S[0] + S[1] + S[2] + S[3];
+  out[1] = M[0] + M[1] + M[2] + M[3];
+}
+
+at::Tensor state_digest_cpu(std::vector<at::Tensor> words) {
+  struct Row {
+    const unsigned long long* p;
+    long long b, e;
+  };
+  std::vector<Row> rows;
+  for (auto& w : words) {
+    TORCH_CHECK(w.scalar_type() == at::kLong && w.is_contiguous() && w.device().is_cpu(),
+                "state_digest_cpu: contiguous int64 CPU tensors");
+    const auto* p = reinterpret_cast<const unsigned long long*>(w.data_ptr());
+    const long long n = w.numel();
+    for (long long o = 0; o < n; o += kDigestRowWords) rows.push_back({p, o, std::min(n, o + kDigestRowWords)});
+  }
+  auto out = at::empty({(long long)rows.size(), 2}, at::TensorOptions().dtype(at::kLong));
+  auto* o = reinterpret_cast<unsigned long long*>(out.data_ptr());
+  // rows over up to 8 threads (torch's intra-op thread count): a few threads saturate a socket's
+  // memory bandwidth for this, and ranks of one pod digest at the same time
+  const int nt = (int)std::max<long long>(1, std::min<long long>({(long long)rows.size(), 8LL,
+                                                                   (long long)at::get_num_threads()}));
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t r; (r = next.fetch_add(1)) < rows.size();) digest_row_host(rows[r].p, rows[r].b, rows[r].e, o + 2 * r);
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  return out;
+}
+
 // ------------------------------------------------------------------------------ autograd
 // C++ autograd nodes: one Python -> C++ call per op and no Python in the backward pass (a
 // Python autograd.Function costs tens of microseconds of CPU per call, which shows on a
@@ -1499,6 +1567,7 @@ PYBIND11_MODULE(_fused_ops, m) {
   m.def("cross_entropy", &cross_entropy);
   m.def("adamw_step", &adamw_step);
   m.def("state_digest", &state_digest, "(sum, position-keyed mixed sum) per 64 Ki-word row of int64 tensors");
+  m.def("state_digest_cpu", &state_digest_cpu, "state_digest for int64 CPU tensors (one pass, rows in parallel)");
   m.def("attention", &attention);
   m.def("attention_supported", &attention_supported);
   m.def("attn_fwd", &attn_fwd);

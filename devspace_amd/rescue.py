@@ -117,13 +117,22 @@ def _digest_rows_torch(v):
     return out
 
 
-def _digest_kernel():
-    """The extension's `state_digest` (one HBM pass for all of a device's tensors), or None."""
+def _digest_kernel(build=True):
+    """The extension with `state_digest` (one HBM pass for all of a device's tensors) and
+    `state_digest_cpu`, or None. build=False: only one that is loaded or importable as it is
+    (CPU state never waits for a compile)."""
     try:
         from devspace_amd.ops import fused
 
-        e = fused.ext()
-        return e if e is not None and hasattr(e, "state_digest") else None
+        if build:
+            e = fused.ext()
+        else:
+            e = fused._ext
+            if e is None:
+                from devspace_amd.ops import _fused_ops as e  # noqa: N813 - an in-tree build, if any
+
+                fused._check_source(e)
+        return e if e is not None and hasattr(e, "state_digest_cpu") else None
     except Exception:  # no extension in this image, or a stale build: the torch path
         return None
 
@@ -163,11 +172,12 @@ def digests(tensors) -> list:
     by_dev = {}
     for i, v in enumerate(words):
         by_dev.setdefault(v.device, []).append(i)
-    kernel = _digest_kernel() if any(d.type == "cuda" for d in by_dev) else None
+    kernel = _digest_kernel(build=any(d.type == "cuda" for d in by_dev))
     for dev, idx in by_dev.items():
         live = [i for i in idx if words[i].numel()]
-        if dev.type == "cuda" and kernel is not None and live:
-            flat = kernel.state_digest([words[i] for i in live])
+        if kernel is not None and live and dev.type in ("cuda", "cpu"):
+            run = kernel.state_digest if dev.type == "cuda" else kernel.state_digest_cpu
+            flat = run([words[i] for i in live])
             counts = [(words[i].numel() + _ROW - 1) // _ROW for i in live]
         else:
             parts = [_digest_rows_torch(words[i]) for i in live]

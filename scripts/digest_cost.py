@@ -56,11 +56,14 @@ def main():
                        torch.cat([rescue._digest_rows_torch(w) for w in words[:2]]).cpu())
     cpu_words = [w[: (64 << 20) // 8].cpu() for w in words[:1]]  # 64 MiB on the CPU, scaled
     cpu_ms = _time(lambda: [rescue._digest_rows_torch(w) for w in cpu_words], 3, lambda: None) * (nbytes / (64 << 20))
+    host = [w.cpu() for w in words]  # the same state in host memory: the extension's one-pass CPU path
+    cpu_ext_ms = _time(lambda: kernel.state_digest_cpu(host), 3, lambda: None)
     print(json.dumps({
         "state_gib": round(nbytes / 2**30, 3), "tensors": args.tensors,
         "kernel_ms": round(k_ms, 3), "kernel_tb_s": round(nbytes / k_ms / 1e9, 2),
         "digests_ms": round(full_ms, 3),
         "torch_on_device_ms": round(torch_ms, 2), "torch_on_cpu_ms_est": round(cpu_ms, 1),
+        "cpu_one_pass_ms": round(cpu_ext_ms, 1), "cpu_threads": torch.get_num_threads(),
         "kernel_speedup_vs_torch_on_device": round(torch_ms / k_ms, 1),
         "what": "rescue.digests of a bf16 training state: (sum, position-keyed mixed sum) per 64 Ki-word row; "
                 "kernel = one state_digest launch; digests = kernel + one host copy + BLAKE2b per tensor",

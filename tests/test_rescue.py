@@ -406,6 +406,21 @@ def test_digests_are_position_sensitive_and_agree_across_paths():
     assert rows.shape == (4, 2) and int(rows[3, 0]) == int(x[3 * _ROW:].sum())
 
 
+def test_cpu_digest_of_the_extension_matches_the_torch_path():
+    """CPU-resident state goes through the extension's one-pass `state_digest_cpu` when the
+    extension is loaded (8 ranks digesting 2 GiB each with a dozen torch ops per chunk took 16 s
+    on the GPU box's CPUs); the numbers are the torch path's, bit for bit."""
+    from devspace_amd.rescue import _ROW, _digest_kernel, _digest_rows_torch
+
+    e = _digest_kernel(build=False)
+    if e is None:
+        pytest.skip("fused-ops extension not importable here")
+    torch.manual_seed(4)
+    ts = [torch.randint(-2**62, 2**62, (n,), dtype=torch.int64) for n in (1, 7, _ROW, 3 * _ROW + 11, 0)]
+    want = torch.cat([_digest_rows_torch(t) for t in ts if t.numel()])
+    assert torch.equal(e.state_digest_cpu(ts), want)
+
+
 @pytest.mark.gpu
 def test_digest_kernel_matches_the_torch_path_bit_for_bit():
     """The gfx950 `state_digest` kernel computes the same (S, M) row pairs as the CPU torch path,
