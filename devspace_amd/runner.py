@@ -728,8 +728,12 @@ def worker_main(args) -> int:
             # the RCCL communicator is created here, eagerly, for this rank's device: a bad device
             # mapping fails before setup(), not inside the first collective of a training step
             kw["device_id"] = device
+        t_pg = time.perf_counter()
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
         phase("process_group")
+        if rank == 0:
+            _log(f"process group up: backend={backend} world={world} in {(time.perf_counter() - t_pg) * 1000.0:.0f} ms"
+                 + (f" (RCCL communicator created for {device})" if backend == "nccl" else ""))
     if device.type == "cuda" and args.gemm_tuning != "off":
         try:
             from devspace_amd.ops import gemm_tuning  # noqa: WPS433
@@ -838,7 +842,8 @@ def worker_main(args) -> int:
             ctx._feed = feed
             ctx._agree = agree
             ctx._drain_min_ms = args.preempt_drain_ms
-        ctx.log(
+        # every rank says it is up (one `[rank N]`-prefixed line each in a multi-rank pod's log)
+        _log(
             f"started gen={gen} marker={getattr(mod, 'MARKER', '')} digest={mod.__devspace_digest__} "
             f"code={mod.__devspace_code__} "
             f"world={world} device={device} backend={dist.get_backend() if dist is not None else 'none'} "

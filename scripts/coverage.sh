@@ -22,5 +22,6 @@ DEVSPACE_BIN="$B/bin/devspace" python3 -m pytest -q -p no:cacheprovider \
   "$ROOT/tests/test_e2e_auth.py" "$ROOT/tests/test_e2e_recovery.py" "$ROOT/tests/test_hostile_server.py" \
   "$ROOT/tests/test_e2e_gpu_sched.py" "$ROOT/tests/test_cli_surface.py" "$ROOT/tests/test_e2e_throttle.py" \
   "$ROOT/tests/test_e2e_pull_wait.py" "$ROOT/tests/test_e2e_rbac.py" "$ROOT/tests/test_e2e_gpu_partitions.py" \
-  "$ROOT/tests/test_e2e_image_layers.py" "$ROOT/tests/test_e2e_portforward_wan.py" 2>&1 | tail -1
+  "$ROOT/tests/test_e2e_image_layers.py" "$ROOT/tests/test_e2e_portforward_wan.py" \
+  "$ROOT/tests/test_e2e_noninteractive.py" "$ROOT/tests/test_platform.py" 2>&1 | tail -1
 python3 "$ROOT/scripts/coverage_summary.py" "$B" "$ROOT/src" | tee "$OUT"

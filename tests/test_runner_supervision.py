@@ -373,6 +373,9 @@ def test_eight_ranks_logs_are_whole_prefixed_lines(tmp_path):
     assert sorted(seen) == list(range(world)) and all(len(v) == lines for v in seen.values()), \
         {k: len(v) for k, v in seen.items()}
     text = r.text()
+    # one start line per rank, each with its rank's prefix
+    starts = sorted(int(m) for m in re.findall(r"^\[rank (\d)\] \[devspace-runner\] started gen=1 ", text, re.M))
+    assert starts == list(range(world)), starts
     assert "[Gloo] Rank" not in text, [l for l in r.lines if "[Gloo]" in l][:3]
     assert text.count(f"group of {world} rank(s) connected") >= 1, text[-2000:]
 
