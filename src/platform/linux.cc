@@ -81,8 +81,6 @@ int open_unlinked_tmp(const std::string& dir) {
   return fd;
 }
 
-int64_t mtime_ns(const struct stat& st) { return (int64_t)st.st_mtim.tv_sec * 1000000000LL + st.st_mtim.tv_nsec; }
-
 bool system_resolver() { return false; }
 
 }  // namespace plat
