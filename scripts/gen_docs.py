@@ -174,6 +174,11 @@ ENV = {
     "DEVSPACE_PARENT_PID": "When `devspace`'s parent process has this pid, `devspace` ends (SIGTERM) when that "
                            "parent dies, however it dies: test harnesses and scripts set it so no CLI outlives "
                            "them (`tests/conftest.py`, `bench.py`).",
+    "DEVSPACE_PORTFORWARD_VIA": "How forwarded connections reach the pod: `auto` (default) through the sync's "
+                                "in-container helper on a remote cluster (tunnel round trip of 5 ms or more; a "
+                                "connection the restarting app refuses is held in the pod and made once when it "
+                                "listens), else the kubelet's port-forward; `helper` whenever the helper is in the "
+                                "container; `kubelet` never through the helper.",
     "DEVSPACE_PORTFORWARD_HEDGE": "`1`: a held GET/HEAD/OPTIONS on a remote cluster (tunnel round trip of 5 ms or "
                                   "more) is hedged: a new attempt every third of a round trip while earlier ones are "
                                   "in flight; the app may see the request up to about four times. Default: one "

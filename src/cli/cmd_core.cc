@@ -208,7 +208,12 @@ int run_dev(cli::Command& c, const std::vector<std::string>& args) {
       auto opts = dev_sync_options(c.get_bool("verbose-sync"));
       std::thread pf_thread([&] {
         try {
-          if (want_pf) forwards = services::start_port_forwarding(s.cfg(), s.kube);
+          // the sync's helper in the container also carries forwarded connections on a remote
+          // cluster (services::port_forward_via)
+          if (want_pf)
+            forwards = services::start_port_forwarding(s.cfg(), s.kube, 120000, 100,
+                                                       want_sync && opts.mode == sync::Mode::Helper ? opts.helper_path
+                                                                                                    : "");
         } catch (const std::exception& e) {
           pf_err = e.what();
         }

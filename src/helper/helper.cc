@@ -19,6 +19,8 @@
 //   'W' (empty)                 -> start watching; "E\n" on stderr after foreign changes settle
 //   'Q'                          -> exit
 //
+// `devspace-helper forward` serves port-forwarded connections instead (src/helper/forward.cc).
+//
 // Lanes: the upstream session interleaves several uploads frame by frame on one stdin — a bulk
 // transfer (a multi-GB checkpoint) in one lane, a code edit in another — so an edit never waits
 // behind a bulk archive for more than one frame. Each lane extracts on its own thread, fed through
@@ -54,6 +56,7 @@
 #include "core/fs.h"
 #include "core/proc.h"
 #include "core/strutil.h"
+#include "helper/forward.h"
 #include "sync/frame.h"
 
 using namespace ds;
@@ -488,8 +491,9 @@ static void open_lane(std::map<int, Lane>& lanes, int lane) {
 }
 
 int main(int argc, char** argv) {
+  if (argc >= 2 && std::string(argv[1]) == "forward") return ds::helper::forward_main();
   if (argc < 3 || std::string(argv[1]) != "serve") {
-    std::fprintf(stderr, "usage: devspace-helper serve <dest>\n");
+    std::fprintf(stderr, "usage: devspace-helper serve <dest> | devspace-helper forward\n");
     std::_Exit(2);
   }
   signal(SIGPIPE, SIG_IGN);

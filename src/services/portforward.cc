@@ -17,8 +17,11 @@
 #include "core/log.h"
 #include "core/resolve.h"
 #include "core/strutil.h"
+#include "core/codec.h"
+#include "core/fs.h"
 #include "core/trace.h"
 #include "platform/platform.h"
+#include "sync/fwd_proto.h"
 
 namespace ds {
 namespace services {
@@ -328,8 +331,14 @@ void PortForwarder::spare_loop() {
             unanswered = tunnel_->pings_in_flight();
           }
         }
-        bool fast = hedge_ && samples < 10 && unanswered < 5;
-        spare_cv_.wait_for(lk, std::chrono::milliseconds(fast ? 100 : 1000), [this] { return stop_.load(); });
+        bool fast = (hedge_ || !helper_file_.empty()) && samples < 10 && unanswered < 5;
+        lk.unlock();
+        maintain_helper_link();
+        lk.lock();
+        // the first five round trips within ~0.1 s (the helper link waits for them), the next
+        // five at 100 ms, then one a second
+        int wait_ms = !fast ? 1000 : samples < 5 ? 20 : 100;
+        spare_cv_.wait_for(lk, std::chrono::milliseconds(wait_ms), [this] { return stop_.load(); });
         continue;
       }
     }
@@ -521,6 +530,276 @@ class PreOpened {
 };
 }  // namespace
 
+// ---------------------------------------------------------------- forwarding through the helper
+// One exec stream per pod running `devspace-helper forward` (src/helper/forward.cc, protocol
+// src/sync/fwd_proto.h): every connection of the forward is multiplexed over it, and a connect
+// the restarting app refuses is retried in the pod every 2 ms, so a held request reaches the new
+// server within ms of it listening instead of up to a round trip later, and exactly once.
+
+struct HelperBox {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<char, std::string>> q;
+  bool closed = false;  // the link ended
+};
+
+class HelperLink {
+ public:
+  // `sh` in the container, the helper the sync put there (content-addressed `file`) exec'd in
+  // forward mode; nullptr with *why when it is not there (the forward never uploads it).
+  static std::shared_ptr<HelperLink> open(sync::Transport& t, const std::string& file, std::string* why) {
+    auto sh = t.open({"sh"});
+    if (!sh) {
+      *why = "no shell";
+      return nullptr;
+    }
+    std::string probe = sync::helper_probe_script(file, sync::helper_dirs(), "exec \"$dsd/" + file + "\" forward");
+    if (!write_all(sh->in(), probe)) {
+      *why = "exec stream closed";
+      return nullptr;
+    }
+    auto link = std::shared_ptr<HelperLink>(new HelperLink(std::move(sh)));
+    std::string line;
+    if (!link->out_.read_line(&line, 15000) || !starts_with(line, "HAVE ")) {
+      *why = line.empty() ? "no answer from the probe" : "helper not in the container (" + line + ")";
+      link->close();
+      return nullptr;
+    }
+    if (!link->out_.read_line(&line, 15000) || line != "FORWARD READY") {
+      *why = "the helper did not start its forward mode (" + line + ")";
+      link->close();
+      return nullptr;
+    }
+    link->th_ = std::thread([l = link.get()] { l->reader(); });
+    return link;
+  }
+  ~HelperLink() { close(); }
+  bool usable() const { return !dead_; }
+  // Registers a connection and sends its 'O' frame; 0 when the link is gone.
+  uint32_t open_conn(int port, uint32_t hold_ms, std::shared_ptr<HelperBox>* box) {
+    auto b = std::make_shared<HelperBox>();
+    uint32_t id;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      id = next_++;
+      boxes_[id] = b;
+    }
+    *box = b;
+    if (!send(sync::fwd::open_frame(id, port, hold_ms))) return 0;
+    return id;
+  }
+  bool send(const std::string& frame) {
+    if (dead_) return false;
+    std::lock_guard<std::mutex> g(wmu_);
+    if (!write_all(sh_->in(), frame)) {
+      dead_ = true;
+      return false;
+    }
+    return true;
+  }
+  void forget(uint32_t id) {
+    std::lock_guard<std::mutex> g(mu_);
+    boxes_.erase(id);
+  }
+  void close() {
+    if (closed_.exchange(true)) return;
+    dead_ = true;
+    if (sh_) sh_->terminate();
+    if (th_.joinable()) th_.join();
+    if (sh_) sh_->close();
+    end_all();
+  }
+
+ private:
+  explicit HelperLink(std::unique_ptr<sync::Shell> sh) : sh_(std::move(sh)), out_(sh_->out()) {}
+  void end_all() {
+    std::map<uint32_t, std::shared_ptr<HelperBox>> boxes;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      boxes.swap(boxes_);
+    }
+    for (auto& kv : boxes) {
+      {
+        std::lock_guard<std::mutex> g(kv.second->mu);
+        kv.second->closed = true;
+      }
+      kv.second->cv.notify_all();
+    }
+  }
+  void reader() {
+    std::string hdr, body;
+    while (!closed_) {
+      if (!out_.read_exact(&hdr, sync::frame::kHeaderSize, -1)) break;
+      char op;
+      uint64_t len;
+      sync::frame::parse_header((const unsigned char*)hdr.data(), &op, &len);
+      if (len < 4 || len > sync::fwd::kMaxFramePayload || !out_.read_exact(&body, (size_t)len, -1)) break;
+      uint32_t id = sync::fwd::get_u32be(body, 0);
+      std::shared_ptr<HelperBox> b;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = boxes_.find(id);
+        if (it != boxes_.end()) b = it->second;
+        if (op == 'E' && it != boxes_.end()) boxes_.erase(it);  // the helper forgot it too
+      }
+      if (!b) continue;
+      {
+        std::lock_guard<std::mutex> g(b->mu);
+        b->q.emplace_back(op, body.substr(4));
+      }
+      b->cv.notify_all();
+    }
+    dead_ = true;
+    end_all();
+  }
+  std::unique_ptr<sync::Shell> sh_;
+  sync::LineReader out_;
+  std::mutex wmu_, mu_;
+  std::map<uint32_t, std::shared_ptr<HelperBox>> boxes_;
+  uint32_t next_ = 1;
+  std::atomic<bool> dead_{false}, closed_{false};
+  std::thread th_;
+};
+
+namespace {
+class HelperFwd : public FwdStream {
+ public:
+  HelperFwd(std::shared_ptr<HelperLink> link, int port, uint32_t hold_ms) : link_(std::move(link)) {
+    id_ = link_->open_conn(port, hold_ms, &box_);
+    if (!id_) throw std::runtime_error("helper link closed");
+  }
+  ~HelperFwd() override { close(); }
+  bool send(const std::string& data) override {
+    for (size_t off = 0; off < data.size(); off += (1u << 20))
+      if (!link_->send(sync::fwd::frame('D', id_, data.substr(off, 1u << 20)))) return false;
+    return true;
+  }
+  bool recv(int* channel, std::string* data) override {
+    std::unique_lock<std::mutex> lk(box_->mu);
+    while (true) {
+      box_->cv.wait(lk, [this] { return !box_->q.empty() || box_->closed || ended_; });
+      if (box_->q.empty()) {
+        if (!ended_) lost_ = true;  // the link ended under this connection
+        return false;
+      }
+      auto ev = std::move(box_->q.front());
+      box_->q.pop_front();
+      switch (ev.first) {
+        case 'C':
+          connected_ = true;
+          continue;
+        case 'D':
+          *channel = 0;
+          *data = std::move(ev.second);
+          return true;
+        case 'F':
+          ended_ = true;
+          return false;
+        case 'E':
+          ended_ = true;  // the next recv ends the stream
+          *channel = 1;
+          *data = std::move(ev.second);
+          return true;
+        default:
+          continue;
+      }
+    }
+  }
+  void close_write() override { link_->send(sync::fwd::frame('F', id_)); }
+  void close() override {
+    if (closed_) return;
+    closed_ = true;
+    link_->send(sync::fwd::frame('K', id_));
+    link_->forget(id_);
+    {
+      std::lock_guard<std::mutex> g(box_->mu);
+      ended_ = true;
+    }
+    box_->cv.notify_all();
+  }
+  const char* via() const override { return "helper"; }
+  bool tunnel_lost() const override { return lost_; }
+  // the helper connected to the app: what was sent may have reached it
+  bool delivered() const { return connected_; }
+
+ private:
+  std::shared_ptr<HelperLink> link_;
+  std::shared_ptr<HelperBox> box_;
+  uint32_t id_ = 0;
+  bool connected_ = false, ended_ = false, lost_ = false, closed_ = false;
+};
+}  // namespace
+
+std::string port_forward_via() {
+  const char* v = std::getenv("DEVSPACE_PORTFORWARD_VIA");
+  std::string s = v && *v ? v : "auto";
+  if (reference_timing()) return "kubelet";
+  return s == "helper" || s == "kubelet" ? s : "auto";
+}
+
+void PortForwarder::set_helper(const std::string& helper_path) {
+  std::string bin;
+  if (via_ == "kubelet" || helper_path.empty() || !fs::read_file(helper_path, &bin) || bin.empty()) return;
+  helper_file_ = "devspace-helper-" + sha256_hex(bin).substr(0, 16);  // as the sync names it
+}
+
+bool PortForwarder::want_helper() {
+  if (helper_file_.empty()) return false;
+  if (via_ == "helper") return true;
+  return tunnel_rtt_us() >= 5000;  // next to the cluster the kubelet's retries cost ~nothing
+}
+
+std::shared_ptr<HelperLink> PortForwarder::helper_link() {
+  if (!want_helper()) return nullptr;
+  const std::string pod = pod_name();
+  std::lock_guard<std::mutex> g(helper_mu_);
+  if (helper_ && helper_->usable() && helper_pod_ == pod) return helper_;
+  return nullptr;
+}
+
+void PortForwarder::maintain_helper_link() {
+  if (stop_ || !want_helper()) return;
+  const std::string pod = pod_name();
+  {
+    std::lock_guard<std::mutex> g(helper_mu_);
+    if (helper_ && helper_->usable() && helper_pod_ == pod) return;
+    if (mono_ms() < helper_retry_ms_) return;
+  }
+  std::shared_ptr<HelperLink> old;
+  {
+    std::lock_guard<std::mutex> g(helper_mu_);
+    old.swap(helper_);
+  }
+  if (old) old->close();
+  Value p;
+  {
+    std::lock_guard<std::mutex> g(pod_mu_);
+    p = pod_;
+  }
+  // the helper lives in the container the sync targets: look in each until it is found
+  std::string why = "no containers";
+  for (auto& c : p.at_path("spec.containers").items()) {
+    kube::ExecTransport t(k_, p, c.get("name").as_string());
+    std::shared_ptr<HelperLink> link;
+    try {
+      link = HelperLink::open(t, helper_file_, &why);
+    } catch (const std::exception& e) {
+      why = e.what();
+    }
+    if (link) {
+      std::lock_guard<std::mutex> g(helper_mu_);
+      helper_ = link;
+      helper_pod_ = pod;
+      log::file_logger("portforwarding")
+          ->emit("info", "Forwarding through the in-container helper of pod " + pod + " (container " +
+                             c.get("name").as_string() + "): held connections are retried in the pod", {});
+      return;
+    }
+  }
+  std::lock_guard<std::mutex> g(helper_mu_);
+  helper_retry_ms_ = mono_ms() + 2000;  // the sync may not have uploaded it yet
+}
+
 // True for the error-channel message of a stream whose pod-side connect failed (kubelet /
 // CRI: "... dial tcp4 127.0.0.1:8080: connect: connection refused"): nothing reached the
 // container, so the client's bytes can be replayed on a new stream.
@@ -709,6 +988,7 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
   int attempt = 0;
   std::unique_ptr<PreOpened> next;
   std::unique_ptr<FwdStream> hedged;  // the answered attempt of a hedged held request
+  bool helper_failed = false;         // a helper link died under this connection: the kubelet's path
   while (!stop_) {
     std::unique_ptr<FwdStream> ws = std::move(hedged);
     const bool primed = ws != nullptr;  // its request went out with it
@@ -722,6 +1002,19 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
       ws = next->take();
       next.reset();
       preopened = ws != nullptr;
+    }
+    if (!ws && !helper_failed) {
+      // through the in-container helper: the hold happens in the pod (one connect, made within
+      // ms of the app listening), so this is the connection's only attempt unless the link dies
+      if (auto link = helper_link()) {
+        try {
+          long left = std::max<long>(0, hold_deadline - mono_ms());
+          ws = std::make_unique<HelperFwd>(link, remote_port, replayable ? (uint32_t)left : 0);
+          helper_streams_++;
+        } catch (const std::exception&) {
+          ws.reset();
+        }
+      }
     }
     if (!ws) {
       try {
@@ -810,6 +1103,21 @@ void PortForwarder::handle(Conn* conn, int remote_port) {
                    {"via", ws->via()}});
     }
     ++attempt;
+    if (std::string(ws->via()) == "helper") {
+      auto* hf = static_cast<HelperFwd*>(ws.get());
+      if (hf->tunnel_lost() && !got_reply && !stop_ && replayable && mono_ms() < hold_deadline &&
+          (!hf->delivered() || hedgeable_request(replay))) {
+        // the helper's exec stream ended under this connection (the pod went away, the API server
+        // closed it) before a reply: the kubelet's path, with the bytes again when they never
+        // reached the app (or form a request HTTP lets a client repeat)
+        helper_failed = true;
+        held_retries_++;
+        continue;
+      }
+      if (refused)  // the helper held it in the pod for the whole hold
+        log::file_logger("portforwarding")->emit("error", "connection refused by the pod", {});
+      break;
+    }
     if (tunneled && ws->tunnel_lost() && !got_reply && !refused && error_text.empty() && replayable && !stop_ &&
         mono_ms() < hold_deadline && hedgeable_request(replay)) {
       // the tunnel ended under this stream before anything came back (an API server's idle
@@ -870,10 +1178,17 @@ void PortForwarder::close() {
   for (int fd : listeners_) ::close(fd);
   listeners_.clear();
   reap(true);  // every connection thread ends within one poll interval once stop_ is set
+  std::shared_ptr<HelperLink> h;
+  {
+    std::lock_guard<std::mutex> g(helper_mu_);
+    h.swap(helper_);
+  }
+  if (h) h->close();
 }
 
 std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& cfg, std::shared_ptr<kube::Client> k,
-                                                                  int pod_wait_ms, int poll_ms) {
+                                                                  int pod_wait_ms, int poll_ms,
+                                                                  const std::string& helper_path) {
   std::vector<std::unique_ptr<PortForwarder>> out;
   for (auto& pf : cfg.at_path("dev.ports").items()) {
     config::SelectorRef ref = config::resolve_selector(cfg, pf);
@@ -897,6 +1212,7 @@ std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& c
       addrs.push_back(m.get("bindAddress").as_string("localhost"));
     }
     auto fwd = std::make_unique<PortForwarder>(k, pod, ports, addrs, ref.labels.to_query());
+    if (!helper_path.empty()) fwd->set_helper(helper_path);
     fwd->start();
     log::done("Port forwarding started on " + fwd->describe());
     out.push_back(std::move(fwd));

@@ -63,7 +63,14 @@ bool is_dial_refused(const std::string& error_channel_message);
 bool port_forward_hedge();
 bool hedgeable_request(const std::string& bytes);
 
-class FwdStream;  // one forwarded connection's stream(s) (portforward.cc)
+class FwdStream;   // one forwarded connection's stream(s) (portforward.cc)
+class HelperLink;  // connections through the in-container helper (portforward.cc)
+
+// How forwarded connections reach the pod (DEVSPACE_PORTFORWARD_VIA): "auto" (default) goes
+// through the in-container helper when the sync has put it in the container and the cluster is
+// remote (the tunnel's round trip is 5 ms or more), else the kubelet's port-forward; "helper"
+// whenever the helper is there; "kubelet" never through the helper.
+std::string port_forward_via();
 
 // Local listeners forwarding to a pod port (services/port_forwarding.go:18, kubectl/client.go:356):
 // through one multiplexed tunnel per pod (SPDY/3.1 over a WebSocket, kube/spdy.h) where the API
@@ -90,6 +97,11 @@ class PortForwarder {
   // Held-connection attempts whose stream was opened while the previous attempt was in flight.
   int preopened_attempts() const { return preopened_; }
   size_t active_connections();
+  // The static helper binary the sync uploads (its content-addressed name in the container is
+  // what the forward looks for); enables forwarding through it (port_forward_via).
+  void set_helper(const std::string& helper_path);
+  // Connections that went through the helper.
+  int helper_streams() const { return helper_streams_; }
 
  private:
   struct Conn {
@@ -150,6 +162,17 @@ class PortForwarder {
   std::string tunnel_pod_;
   std::atomic<uint64_t> tunnel_requests_{0};  // request ids of the current tunnel
   std::atomic<int> tunnels_opened_{0};
+  // forwarding through the in-container helper
+  std::shared_ptr<HelperLink> helper_link();  // a usable link to the current pod, or nullptr
+  void maintain_helper_link();                // (spare_loop) opens / re-opens it when wanted
+  bool want_helper();
+  std::string helper_file_;                   // devspace-helper-<sha16>, "" when not enabled
+  std::string via_ = port_forward_via();
+  std::mutex helper_mu_;
+  std::shared_ptr<HelperLink> helper_;
+  std::string helper_pod_;
+  long helper_retry_ms_ = 0;                  // not before this (monotonic ms) after a failed probe
+  std::atomic<int> helper_streams_{0};
 
  public:
   // Tunnels opened (1 for a forward whose API server speaks it and whose pod never changed).
@@ -157,8 +180,11 @@ class PortForwarder {
   bool tunneled() const { return tunnel_mode_ == 1; }
 };
 
+// helper_path: the sync's static helper (set when the sync runs in helper mode), for
+// forwarding through it (PortForwarder::set_helper).
 std::vector<std::unique_ptr<PortForwarder>> start_port_forwarding(const Value& cfg, std::shared_ptr<kube::Client> k,
-                                                                  int pod_wait_ms = 120000, int poll_ms = 100);
+                                                                  int pod_wait_ms = 120000, int poll_ms = 100,
+                                                                  const std::string& helper_path = "");
 
 // Runs an interactive command in the container with a TTY when stdin is a terminal
 // (services/terminal.go). `interrupt` is polled; returns the remote exit code.

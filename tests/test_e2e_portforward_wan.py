@@ -1,15 +1,20 @@
 """Port-forward of a request held across an app restart, with the cluster behind a slow link (40 ms
 RTT, devspace_amd/localkube/netem.py), as a laptop reaches a remote MI355X node.
 
-By default every held request, GET or POST, is retried one stream at a time and reaches the app
-exactly once, as through kubectl port-forward (/root/reference/pkg/devspace/kubectl/client.go:356-380).
-With DEVSPACE_PORTFORWARD_HEDGE=1 a held GET (repeatable, RFC 9110 §9.2.2) goes out on a new
+By default, on a remote cluster, connections go through the sync's in-container helper
+(`devspace-helper forward`): a connection the restarting app refuses is held *in the pod* and
+made once when the app listens, so every request reaches the app exactly once and within ms of
+it listening. Through the kubelet's port-forward (DEVSPACE_PORTFORWARD_VIA=kubelet) every held
+request is retried one stream at a time and reaches the app exactly once, as through kubectl
+port-forward (/root/reference/pkg/devspace/kubectl/client.go:356-380); each retry costs a round
+trip. With DEVSPACE_PORTFORWARD_HEDGE=1 (kubelet path) a held GET (repeatable, RFC 9110 §9.2.2) goes out on a new
 stream pair of the pod's tunnel every third of a round trip while earlier attempts are in flight;
 the first answer wins, and the app may see the GET more than once. A POST still goes out once.
 An API server without the tunnel (before Kubernetes 1.30) gets a WebSocket per connection.
 """
 import json
 import os
+import time
 import urllib.request
 
 import pytest
@@ -20,8 +25,9 @@ from test_e2e_cli import running, wait_for
 from test_e2e_services import _refused, _restart_project, _stop
 
 
-@pytest.mark.parametrize("hedge", [False, True], ids=["default", "hedge-opt-in"])
-def test_held_requests_across_a_restart_on_a_remote_cluster(tmp_path, hedge):
+@pytest.mark.parametrize("via,hedge", [("auto", False), ("kubelet", False), ("kubelet", True)],
+                         ids=["default-helper", "kubelet", "kubelet-hedge-opt-in"])
+def test_held_requests_across_a_restart_on_a_remote_cluster(tmp_path, via, hedge):
     from devspace_amd.localkube import LocalCluster
     from devspace_amd.localkube.netem import ShapedLink, point_kubeconfig
 
@@ -30,8 +36,11 @@ def test_held_requests_across_a_restart_on_a_remote_cluster(tmp_path, hedge):
     try:
         lk = DevspaceEnv(cluster, str(tmp_path))
         lk.env.pop("DEVSPACE_PORTFORWARD_HEDGE", None)
+        lk.env.pop("DEVSPACE_PORTFORWARD_VIA", None)
         if hedge:
             lk.env["DEVSPACE_PORTFORWARD_HEDGE"] = "1"
+        if via != "auto":
+            lk.env["DEVSPACE_PORTFORWARD_VIA"] = via
         link = ShapedLink(("127.0.0.1", cluster.port), rtt_ms=40, mbit=100).start()
         point_kubeconfig(lk.kubeconfig, cluster.server, link.url("https"))
         proj, remote, local = _restart_project(lk, "qs-wan-hold", "pf-wan")
@@ -60,6 +69,11 @@ def test_held_requests_across_a_restart_on_a_remote_cluster(tmp_path, hedge):
                      what="forwarded server")
             root = json.loads(running(lk.pods("pf-wan"))[0]["metadata"]["annotations"]["devspace.sh/local-roots"])
             pod_index = os.path.join(list(root.values())[0], "app", "index.js")
+            pf_log = os.path.join(proj, ".devspace", "logs", "portforwarding.log")
+            if via == "auto":  # the link to the helper comes up once the tunnel's round trip is known
+                wait_for(lambda: os.path.exists(pf_log) and "through the in-container helper" in open(pf_log).read(),
+                         timeout=30, what="helper link")
+            t_link = time.monotonic()
             for i in range(4):
                 with open(index, "a") as f:
                     f.write(f"// edit {i}\n")
@@ -79,9 +93,17 @@ def test_held_requests_across_a_restart_on_a_remote_cluster(tmp_path, hedge):
         spans = [json.loads(l) for l in open(os.path.join(proj, ".devspace", "logs", "trace.jsonl"))
                  if '"portforward.stream"' in l]
         hedged = [s for s in spans if s.get("hedged") == "1"]
-        assert all(s.get("via") == "tunnel" for s in spans), spans
-        pf_log = os.path.join(proj, ".devspace", "logs", "portforwarding.log")
         log = open(pf_log).read() if os.path.exists(pf_log) else ""
+        if via == "auto":
+            # after the link is up every stream goes through the helper: no refused attempt, each
+            # held request (GET and POST) delivered once
+            late = [s for s in spans if s["start_us"] / 1e6 >= t_link]
+            assert late and all(s.get("via") == "helper" and s["outcome"] == "reply" for s in late), late
+            for i in (0, 2):
+                assert lines.count(f"GET /held-{i}") == 1, lines
+            assert not hedged, hedged
+            return
+        assert all(s.get("via") == "tunnel" for s in spans), spans
         if hedge:
             for i in (0, 2):
                 assert 1 <= lines.count(f"GET /held-{i}") <= 8, lines
