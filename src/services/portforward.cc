@@ -790,14 +790,17 @@ void PortForwarder::maintain_helper_link() {
       std::lock_guard<std::mutex> g(helper_mu_);
       helper_ = link;
       helper_pod_ = pod;
+      helper_backoff_ms_ = 2000;
       log::file_logger("portforwarding")
           ->emit("info", "Forwarding through the in-container helper of pod " + pod + " (container " +
                              c.get("name").as_string() + "): held connections are retried in the pod", {});
       return;
     }
   }
+  // the sync may not have uploaded it yet; a cluster that refuses the exec is not asked every 2 s
   std::lock_guard<std::mutex> g(helper_mu_);
-  helper_retry_ms_ = mono_ms() + 2000;  // the sync may not have uploaded it yet
+  helper_retry_ms_ = mono_ms() + helper_backoff_ms_;
+  helper_backoff_ms_ = std::min(30000L, helper_backoff_ms_ * 2);
 }
 
 // True for the error-channel message of a stream whose pod-side connect failed (kubelet /

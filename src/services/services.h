@@ -172,6 +172,7 @@ class PortForwarder {
   std::shared_ptr<HelperLink> helper_;
   std::string helper_pod_;
   long helper_retry_ms_ = 0;                  // not before this (monotonic ms) after a failed probe
+  long helper_backoff_ms_ = 2000;             // doubling up to 30 s while it keeps failing
   std::atomic<int> helper_streams_{0};
 
  public:
