@@ -11,6 +11,7 @@
 #   rescue  the runner's snapshot cost on the flagship example (scripts/rescue_cost.py)
 #   kernels the gfx950 fused ops against the eager op chains they replace (scripts/bench_fused_ops.py)
 #   layers  the rocm-pytorch image built with RUN executed, then rebuilt after an edit (scripts/image_rebuild_cost.py)
+#   via     port-forward on a remote cluster: retries from the laptop vs the hold in the pod (scripts/ab_portforward_via.py)
 #   digest  the rescue snapshots' content digest: gfx950 state_digest kernel vs torch ops (scripts/digest_cost.py)
 #
 # Output: gpurun_out/$GPU_TIER_TAG/ (default "tier"). Every GPU step has its own time limit and
@@ -67,6 +68,11 @@ for s in "${steps[@]}"; do
       timeout -k 10 600 python -u scripts/rescue_cost.py > "$OUT/rescue.json" 2> "$OUT/rescue.err" \
         || fail rescue $? "$OUT/rescue.err"
       tail -1 "$OUT/rescue.json"
+      ;;
+    via)
+      timeout -k 10 600 python -u scripts/ab_portforward_via.py > "$OUT/via.json" 2> "$OUT/via.err" \
+        || fail via $? "$OUT/via.err"
+      tail -1 "$OUT/via.json"
       ;;
     digest)
       timeout -k 10 300 python -u scripts/digest_cost.py > "$OUT/digest.json" 2> "$OUT/digest.err" \
