@@ -225,3 +225,53 @@ TEST(platform_scan_watcher_interval_follows_the_scan_cost) {
   w->stop();
   fs::remove_all(root);
 }
+
+TEST(platform_scan_watcher_quick_pass_sees_new_and_hot_files_between_full_scans) {
+  // a CPU budget of 0.1 %: full scans of the 1000 files every 2 s (the maximum), quick passes
+  // over the 21 directories and the hot files every few tens of ms. Creations, atomic saves and
+  // re-edits of a file being worked on come through the quick pass, an in-place edit of a cold
+  // file through the next full scan
+  std::string root = fs::make_temp_dir("ds-watch-");
+  for (int d = 0; d < 20; ++d)
+    for (int f = 0; f < 50; ++f) fs::write_file(root + "/d" + std::to_string(d) + "/f" + std::to_string(f), "x");
+  ScanOptions o;
+  o.min_interval_ms = 20;
+  o.max_interval_ms = 2000;
+  o.cost_factor = 1000;
+  auto w = make_scan_watcher(o);
+  Events ev;
+  EXPECT_TRUE(w->start(root, ev.cb(), nullptr));
+  auto since = [](std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+  };
+  auto t0 = std::chrono::steady_clock::now();
+  fs::write_file(root + "/d3/new.py", "a");  // a new entry: d3's mtime moves
+  EXPECT_TRUE(ev.wait_for(root + "/d3/new.py", 3000));
+  EXPECT_TRUE(since(t0) < 1000);
+  ev.clear();
+  std::this_thread::sleep_for(std::chrono::milliseconds(30));
+  t0 = std::chrono::steady_clock::now();
+  fs::append_file(root + "/d3/new.py", "more");  // in place, but hot
+  EXPECT_TRUE(ev.wait_for(root + "/d3/new.py", 3000));
+  EXPECT_TRUE(since(t0) < 1000);
+  ev.clear();
+  t0 = std::chrono::steady_clock::now();
+  fs::write_file_atomic(root + "/d5/f5", "saved");  // an editor's save: rename over the file
+  EXPECT_TRUE(ev.wait_for(root + "/d5/f5", 3000));
+  EXPECT_TRUE(since(t0) < 1000);
+  ev.clear();
+  fs::mkdirs(root + "/d9/sub/deeper");
+  fs::write_file(root + "/d9/sub/deeper/x", "1");
+  EXPECT_TRUE(ev.wait_for(root + "/d9/sub/deeper/x", 3000));
+  fs::remove_all(root + "/d9");
+  EXPECT_TRUE(ev.wait_for(root + "/d9/f0", 3000));  // entries below a removed directory
+  EXPECT_TRUE(ev.wait_for(root + "/d9", 3000));
+  ev.clear();
+  fs::append_file(root + "/d11/f11", "cold edit");  // in place, cold: the full scan finds it
+  EXPECT_TRUE(ev.wait_for(root + "/d11/f11", 5000));
+  auto p = ev.paths();
+  EXPECT_EQ(p.count(root + "/d11/f11"), (size_t)1);
+  EXPECT_EQ(p.count(root + "/d9"), (size_t)0);  // reported once, not again by the full scan
+  w->stop();
+  fs::remove_all(root);
+}

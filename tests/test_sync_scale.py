@@ -207,8 +207,29 @@ def test_dev_sync_10k_files_over_wss(tree, tmp_path):
             f.write("# edit\n")
         _wait(lambda: open(os.path.join(root, "src", "pkg042", "m042.py"), "rb").read().endswith(b"# edit\n"), 30,
               "edit after initial sync")
+        edit_s = time.perf_counter() - t1
+        # the same file again (the one being worked on), then an editor's save of another one
+        # (write a temp, rename it over the file)
+        time.sleep(0.2)
+        t2 = time.perf_counter()
+        with open(os.path.join(proj, "src", "pkg042", "m042.py"), "a") as f:
+            f.write("# again\n")
+        _wait(lambda: open(os.path.join(root, "src", "pkg042", "m042.py"), "rb").read().endswith(b"# again\n"), 30,
+              "second edit")
+        again_s = time.perf_counter() - t2
+        time.sleep(0.2)
+        t3 = time.perf_counter()
+        target = os.path.join(proj, "src", "pkg007", "m007.py")
+        with open(target + ".swp", "w") as f:
+            f.write("saved by rename\n")
+        os.rename(target + ".swp", target)
+        _wait(lambda: open(os.path.join(root, "src", "pkg007", "m007.py"), "rb").read() == b"saved by rename\n", 30,
+              "save by rename")
         _record("dev_helper_wss", {"initial_sync_incl_deploy_s": round(initial_s, 3),
-                                   "edit_after_initial_s": round(time.perf_counter() - t1, 4)})
+                                   "edit_after_initial_s": round(edit_s, 4),
+                                   "edit_same_file_again_s": round(again_s, 4),
+                                   "save_by_rename_s": round(time.perf_counter() - t3, 4),
+                                   "watcher": os.environ.get("DEVSPACE_WATCHER") or "native"})
     finally:
         if dev is not None and dev.poll() is None:
             os.killpg(dev.pid, 2)
