@@ -539,3 +539,55 @@ def test_a_rank_waiting_on_the_device_is_not_progress_on_the_gpu(tmp_path):
         r.until(r"started gen=1 marker=fixed", timeout=180)
     finally:
         r.stop()
+
+
+MISMATCHED = '''
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+MARKER = "v0"
+HANG = {hang!r}
+
+
+def setup(ctx):
+    return {{"n": 0}}
+
+
+def step(ctx, state):
+    flag = torch.tensor([1.0 if ctx.rank == 0 and os.path.exists(HANG) else 0.0])
+    dist.all_reduce(flag)
+    if flag.item() and MARKER == "v0":
+        # mismatched collective calls: rank 0 enters an all_reduce that rank 1 never joins, rank 1
+        # waits for a message rank 0 never sends. Both block in the collective library for good.
+        if ctx.rank == 0:
+            dist.all_reduce(torch.ones(4))
+        else:
+            dist.recv(torch.empty(4), src=0)
+    state["n"] += 1
+    time.sleep(0.005)
+    return {{"loss": state["n"]}}
+'''
+
+
+def test_ranks_deadlocked_in_mismatched_collectives_are_restarted_by_an_edit(tmp_path):
+    """ADVICE r5: ranks hung in mismatched collectives (rank 0 in an all_reduce rank 1 never joins,
+    rank 1 in a recv rank 0 never matches) stand inside wait calls. With --stuck-after, an edit
+    restarts the group ("made no progress") instead of waiting on it forever. Two gloo ranks."""
+    trigger = tmp_path.parent / (tmp_path.name + "-hang")
+    entry = tmp_path / "train.py"
+    entry.write_text(MISMATCHED.format(hang=str(trigger)))
+    r = Runner(tmp_path, entry, 2, extra_args=("--log-every", "50", "--rescue-every", "0.5", "--stuck-after", "2"))
+    try:
+        r.until(r"started gen=1 marker=v0", timeout=180)
+        r.until(r"rescue snapshot step=\d+ ", timeout=60)
+        trigger.write_text("1")
+        time.sleep(3.0)
+        _set_marker(entry, "fixed")
+        r.until(r"made no progress for \d+ s at train.py:\d+ and the code changed since", timeout=60)
+        r.until(r"started gen=1 marker=fixed", timeout=180)
+        r.until(r"step=\d+ gen=\d+ loss=", timeout=60)  # training again
+    finally:
+        r.stop()
