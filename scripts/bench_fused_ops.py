@@ -4,6 +4,12 @@ process with interleaved rounds (cdna_hip_programming.md §5.4 rule 24), on the 
 rocm-pytorch example (B*T = 4096 rows, D = 1024, H = 2730, V = 8192), plus the whole
 TinyLM training step built either way.
 
+Two clocks per case:
+  * launched: the calls issued from Python one after another (what an eager training loop
+    sees; at these sizes the host's dispatch, autograd included, can be the bound);
+  * graph: the same calls captured once into a HIP graph and replayed, so the number is the
+    device's time for the kernels alone (cases that cannot be captured print n/a).
+
     python scripts/bench_fused_ops.py [--rounds 10] [--json out.json]
 """
 
@@ -33,6 +39,34 @@ def timeit(fn, iters):
     end.record()
     torch.cuda.synchronize()
     return start.elapsed_time(end) * 1000.0 / iters  # us
+
+
+def timeit_graph(fn, iters):
+    """Device time of `iters` calls replayed from one captured HIP graph (us per call); None
+    when the case cannot be captured (a host sync or a host-side value inside it)."""
+    try:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up off the capture stream, as capture requires
+            for _ in range(3):
+                fn()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(iters):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        start.record()
+        g.replay()
+        end.record()
+        torch.cuda.synchronize()
+        return start.elapsed_time(end) * 1000.0 / iters
+    except Exception:  # noqa: BLE001 - not capturable: reported as n/a
+        torch.cuda.synchronize()
+        return None
 
 
 def op_cases(dev):
@@ -158,13 +192,32 @@ def main():
             iters = 5 if k.startswith("TinyLM") else a.iters
             res[k]["fused"].append(timeit(f, iters))
             res[k]["eager"].append(timeit(e, iters))
+    graph = {}
+    for k, (f, e) in cases.items():
+        if k.startswith("TinyLM") or k.startswith("adamw"):
+            continue  # host-side step counters and syncs: not captured
+        gf, ge = [], []
+        for _ in range(max(1, a.rounds // 2)):
+            gf.append(timeit_graph(f, a.iters))
+            ge.append(timeit_graph(e, a.iters))
+        if None not in gf and None not in ge:
+            graph[k] = (statistics.median(gf), statistics.median(ge))
     out = {}
-    print(f"{'case':42s} {'fused_us':>10} {'eager_us':>10} {'speedup':>8}   (median of {a.rounds} interleaved rounds)")
+    print(f"{'case':42s} {'fused_us':>10} {'eager_us':>10} {'speedup':>8}   {'graph: fused_us':>15} {'eager_us':>9} "
+          f"{'speedup':>8}   (medians, interleaved rounds)")
     for k, v in res.items():
         fm, em = statistics.median(v["fused"]), statistics.median(v["eager"])
         out[k] = {"fused_us": round(fm, 1), "eager_us": round(em, 1), "speedup": round(em / fm, 3),
                   "fused_min_us": round(min(v["fused"]), 1), "eager_min_us": round(min(v["eager"]), 1)}
-        print(f"{k:42s} {fm:>10.1f} {em:>10.1f} {em / fm:>8.2f}x")
+        line = f"{k:42s} {fm:>10.1f} {em:>10.1f} {em / fm:>8.2f}x"
+        if k in graph:
+            gfm, gem = graph[k]
+            out[k].update({"graph_fused_us": round(gfm, 1), "graph_eager_us": round(gem, 1),
+                           "graph_speedup": round(gem / gfm, 3)})
+            line += f"   {gfm:>15.1f} {gem:>9.1f} {gem / gfm:>8.2f}x"
+        else:
+            line += f"   {'n/a':>15}"
+        print(line)
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"device": torch.cuda.get_device_name(0), "results": out}, f, indent=1)
