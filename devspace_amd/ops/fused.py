@@ -103,14 +103,16 @@ def _use_hip(t: torch.Tensor) -> bool:
 def _rmsnorm_kernel_default() -> bool:
     import os
 
-    return os.environ.get("DEVSPACE_FUSED_RMSNORM") == "1"
+    return os.environ.get("DEVSPACE_FUSED_RMSNORM", "1") != "0"
 
 
 def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float | None = None, kernel: bool | None = None) -> torch.Tensor:
-    """RMSNorm alone. PyTorch's own fused rms_norm by default: the gfx950 kernel (`kernel=True`,
-    or DEVSPACE_FUSED_RMSNORM=1) measured 0.97x of it fwd+bwd on [4096x1024]
-    (profiles/r5_fused_ops_ab.txt), so it is not the default path. The residual add + RMSNorm
-    (`add_rms_norm`, 1.16x: one pass instead of two) is where fusing pays, and stays on."""
+    """RMSNorm alone: the gfx950 kernel by default (`kernel=False` or DEVSPACE_FUSED_RMSNORM=0 for
+    PyTorch's fused rms_norm). Fwd+bwd on [4096x1024] it takes 25.2 us of device time against
+    41.4 us (1.64x, replayed from a HIP graph); issued one call at a time from Python, both are
+    bound by the host's dispatch (39.4 vs 40.6 us, 1.03x; round 5 measured 0.97x that way and
+    kept it off). profiles/r6_fused_ops_ab_graph.txt. In a training step the device clock is the
+    one that counts: the step is queued ahead of the GPU."""
     if eps is None:
         eps = torch.finfo(x.dtype).eps
     use = _rmsnorm_kernel_default() if kernel is None else kernel
