@@ -16,6 +16,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstring>
 #include <map>
@@ -69,6 +70,7 @@ struct Conn {
   bool client_fin = false;  // the client half-closed: shut the socket's write side once drained
   bool shut_wr = false;
   bool app_eof = false;
+  uint64_t unacked = 0;     // app bytes sent to the client that it has not acknowledged
 };
 
 constexpr long kRetryUs = 2000;
@@ -101,7 +103,7 @@ class Forwarder {
         }
         short ev = 0;
         if (c.connecting || (c.connected && !c.to_app.empty())) ev |= POLLOUT;
-        if (c.connected && !c.app_eof) ev |= POLLIN;
+        if (c.connected && !c.app_eof && c.unacked < fwd::kWindow) ev |= POLLIN;  // else: the client reads slowly
         if (!ev) continue;
         pf.push_back({c.fd, ev, 0});
         ids.push_back(kv.first);
@@ -181,15 +183,19 @@ class Forwarder {
   }
 
   bool flush(uint32_t id, Conn& c) {
+    size_t wrote = 0;
     while (!c.to_app.empty()) {
       ssize_t w = ::send(c.fd, c.to_app.data(), c.to_app.size(), MSG_NOSIGNAL);
       if (w < 0) {
         if (errno == EINTR) continue;
-        if (errno == EAGAIN) return true;
+        if (errno == EAGAIN) break;
         return fail(id, c, std::string("write: ") + std::strerror(errno));
       }
       c.to_app.erase(0, (size_t)w);
+      wrote += (size_t)w;
     }
+    if (wrote) send(fwd::ack_frame(id, wrote));  // the client may send that much more
+    if (!c.to_app.empty()) return true;
     if (c.client_fin && !c.shut_wr) {
       ::shutdown(c.fd, SHUT_WR);
       c.shut_wr = true;
@@ -224,6 +230,7 @@ class Forwarder {
       char buf[65536];
       ssize_t n = ::recv(c.fd, buf, sizeof(buf), 0);
       if (n > 0) {
+        c.unacked += (uint64_t)n;
         send(fwd::frame('D', id, std::string(buf, (size_t)n)));
       } else if (n == 0) {
         c.app_eof = true;
@@ -290,6 +297,10 @@ class Forwarder {
         if (it == conns_.end()) return;
         it->second.client_fin = true;
         if (it->second.connected && !flush(id, it->second)) conns_.erase(it);
+        break;
+      case 'A':
+        if (it == conns_.end() || rest.size() < 4) return;
+        it->second.unacked -= std::min<uint64_t>(it->second.unacked, fwd::get_u32be(rest, 0));
         break;
       case 'K':
         if (it == conns_.end()) return;

@@ -540,7 +540,9 @@ struct HelperBox {
   std::mutex mu;
   std::condition_variable cv;
   std::deque<std::pair<char, std::string>> q;
-  bool closed = false;  // the link ended
+  bool closed = false;     // the link ended
+  bool gone = false;       // the connection ended ('E' from the helper, or closed here)
+  uint64_t in_flight = 0;  // bytes sent to the helper that it has not acknowledged ('A')
 };
 
 class HelperLink {
@@ -645,7 +647,12 @@ class HelperLink {
       if (!b) continue;
       {
         std::lock_guard<std::mutex> g(b->mu);
-        b->q.emplace_back(op, body.substr(4));
+        if (op == 'A') {
+          if (body.size() >= 8) b->in_flight -= std::min<uint64_t>(b->in_flight, sync::fwd::get_u32be(body, 4));
+        } else {
+          if (op == 'E') b->gone = true;
+          b->q.emplace_back(op, body.substr(4));
+        }
       }
       b->cv.notify_all();
     }
@@ -669,12 +676,30 @@ class HelperFwd : public FwdStream {
     if (!id_) throw std::runtime_error("helper link closed");
   }
   ~HelperFwd() override { close(); }
+  // Blocks while the helper holds a window's worth of this connection's data unwritten to the app.
   bool send(const std::string& data) override {
-    for (size_t off = 0; off < data.size(); off += (1u << 20))
-      if (!link_->send(sync::fwd::frame('D', id_, data.substr(off, 1u << 20)))) return false;
+    constexpr size_t kChunk = 256u << 10;
+    for (size_t off = 0; off < data.size(); off += kChunk) {
+      const size_t n = std::min(kChunk, data.size() - off);
+      {
+        std::unique_lock<std::mutex> lk(box_->mu);
+        box_->cv.wait(lk, [&] { return box_->in_flight + n <= sync::fwd::kWindow || box_->closed || box_->gone; });
+        if (box_->closed || box_->gone) return false;
+        box_->in_flight += n;
+      }
+      if (!link_->send(sync::fwd::frame('D', id_, data.substr(off, n)))) return false;
+    }
     return true;
   }
+  // The caller writes what a call returns to its local connection before it calls again: what the
+  // previous calls returned is acknowledged here, every kAckEvery bytes or before waiting.
   bool recv(int* channel, std::string* data) override {
+    uint64_t ack = 0;
+    {
+      std::lock_guard<std::mutex> g(box_->mu);
+      if (unacked_ >= sync::fwd::kAckEvery || (unacked_ && box_->q.empty())) std::swap(ack, unacked_);
+    }
+    if (ack) link_->send(sync::fwd::ack_frame(id_, ack));  // outside the box's lock: the reader takes it
     std::unique_lock<std::mutex> lk(box_->mu);
     while (true) {
       box_->cv.wait(lk, [this] { return !box_->q.empty() || box_->closed || ended_; });
@@ -691,6 +716,7 @@ class HelperFwd : public FwdStream {
         case 'D':
           *channel = 0;
           *data = std::move(ev.second);
+          unacked_ += data->size();
           return true;
         case 'F':
           ended_ = true;
@@ -714,6 +740,7 @@ class HelperFwd : public FwdStream {
     {
       std::lock_guard<std::mutex> g(box_->mu);
       ended_ = true;
+      box_->gone = true;
     }
     box_->cv.notify_all();
   }
@@ -726,6 +753,7 @@ class HelperFwd : public FwdStream {
   std::shared_ptr<HelperLink> link_;
   std::shared_ptr<HelperBox> box_;
   uint32_t id_ = 0;
+  uint64_t unacked_ = 0;  // data returned by recv() not yet acknowledged to the helper
   bool connected_ = false, ended_ = false, lost_ = false, closed_ = false;
 };
 }  // namespace

@@ -16,11 +16,20 @@
 //                      'D' id bytes                      data (kept until connected)
 //                      'F' id                            client half-close (after its data)
 //                      'K' id                            abort
+//                      'A' id n:u32be                    n more bytes of the app's data written
+//                                                        to the local connection
 //   helper -> client   'C' id                            connected
 //                      'D' id bytes                      data from the app
 //                      'F' id                            the app closed its side
 //                      'E' id message                    failed ("connection refused" after the
 //                                                        hold) or reset; the id is gone
+//                      'A' id n:u32be                    n more bytes of the client's data written
+//                                                        to the app
+//
+// Flow control: each side keeps at most kWindow bytes of one connection's data unacknowledged
+// ('A'), so a slow reader at either end holds back that connection only, and neither side
+// buffers more than kWindow per connection (a multi-GB download through the forward to a slow
+// local reader, or an upload to an app that reads slowly, cannot grow either process).
 #pragma once
 
 #include <cstdint>
@@ -56,6 +65,10 @@ inline std::string open_frame(uint32_t id, int port, uint32_t hold_ms) {
 }
 
 constexpr uint64_t kMaxFramePayload = (1u << 20) + 16;
+constexpr uint64_t kWindow = 4u << 20;      // unacknowledged bytes per connection and direction
+constexpr uint64_t kAckEvery = 256u << 10;  // a reader acknowledges at least this often
+
+inline std::string ack_frame(uint32_t id, uint64_t n) { return frame('A', id, u32be((uint32_t)n)); }
 
 }  // namespace fwd
 }  // namespace sync

@@ -92,15 +92,23 @@ struct Helper {
     if (!out.read_line(&line, 5000) || line != "FORWARD READY") throw std::runtime_error("no ready line: " + line);
   }
   void send(const std::string& f) { write_all(p.stdin_fd(), f); }
-  // the next frame: (op, id, body); op 0 on timeout
+  std::map<uint32_t, uint64_t> acked;  // per id: the client's bytes the helper wrote to the app
+  // the next frame other than an acknowledgement: (op, id, body); op 0 on timeout
   std::tuple<char, uint32_t, std::string> next(int timeout_ms = 5000) {
-    std::string hdr, body;
-    if (!out.read_exact(&hdr, sync::frame::kHeaderSize, timeout_ms)) return {0, 0, ""};
-    char op;
-    uint64_t len;
-    sync::frame::parse_header((const unsigned char*)hdr.data(), &op, &len);
-    if (!out.read_exact(&body, (size_t)len, timeout_ms)) return {0, 0, ""};
-    return {op, fwd::get_u32be(body, 0), body.substr(4)};
+    while (true) {
+      std::string hdr, body;
+      if (!out.read_exact(&hdr, sync::frame::kHeaderSize, timeout_ms)) return {0, 0, ""};
+      char op;
+      uint64_t len;
+      sync::frame::parse_header((const unsigned char*)hdr.data(), &op, &len);
+      if (!out.read_exact(&body, (size_t)len, timeout_ms)) return {0, 0, ""};
+      uint32_t id = fwd::get_u32be(body, 0);
+      if (op == 'A') {
+        acked[id] += fwd::get_u32be(body, 4);
+        continue;
+      }
+      return {op, id, body.substr(4)};
+    }
   }
 };
 
@@ -137,6 +145,68 @@ TEST(helper_forward_holds_a_refused_connection_in_the_pod_and_delivers_once) {
   std::this_thread::sleep_for(std::chrono::milliseconds(50));
   EXPECT_EQ(s.conns.load(), 1);
   EXPECT_EQ(s.got(), req);
+  EXPECT_EQ(h.acked[1], (uint64_t)req.size());  // written to the app: acknowledged
+}
+
+TEST(helper_forward_keeps_at_most_a_window_unacknowledged_per_connection) {
+  // the app sends 24 MiB at once; the client reads frames but acknowledges nothing at first: the
+  // helper stops reading the app after a window, then goes on as acknowledgements arrive
+  int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
+  int one = 1;
+  ::setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  int port = free_port();
+  struct sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)port);
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  EXPECT_EQ(::bind(lfd, (struct sockaddr*)&a, sizeof(a)), 0);
+  EXPECT_EQ(::listen(lfd, 1), 0);
+  const size_t total = 24u << 20;
+  std::atomic<size_t> sent{0};
+  std::thread app([&] {
+    int c = ::accept(lfd, nullptr, nullptr);
+    std::string chunk(1 << 16, 'z');
+    while (sent < total) {
+      ssize_t w = ::write(c, chunk.data(), std::min(chunk.size(), total - sent.load()));
+      if (w <= 0) break;
+      sent += (size_t)w;
+    }
+    ::close(c);
+  });
+  Helper h;
+  h.send(fwd::open_frame(3, port, 1000));
+  size_t got = 0;
+  bool ended = false;
+  // without acknowledgements: what arrives stops at about a window
+  while (true) {
+    auto [op, id, body] = h.next(500);
+    if (op == 0) break;
+    EXPECT_EQ(id, (uint32_t)3);
+    if (op == 'D') got += body.size();
+    if (op == 'F') ended = true;
+  }
+  EXPECT_TRUE(!ended);
+  EXPECT_TRUE(got >= fwd::kWindow && got < fwd::kWindow + (1u << 17));
+  EXPECT_TRUE(sent.load() < total);  // the app is held back by TCP, not buffered in the helper
+  // acknowledging as the client writes it out: the rest flows
+  uint64_t unacked = got;
+  while (!ended) {
+    if (unacked) {
+      h.send(fwd::ack_frame(3, unacked));
+      unacked = 0;
+    }
+    auto [op, id, body] = h.next(5000);
+    EXPECT_TRUE(op != 0);
+    if (op == 0) break;
+    if (op == 'D') {
+      got += body.size();
+      unacked += body.size();
+    }
+    if (op == 'F') ended = true;
+  }
+  EXPECT_EQ(got, total);
+  app.join();
+  ::close(lfd);
 }
 
 TEST(helper_forward_refuses_after_the_hold_and_multiplexes) {

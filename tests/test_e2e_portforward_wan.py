@@ -155,3 +155,96 @@ def test_an_api_server_without_the_tunnel_gets_a_websocket_per_connection(tmp_pa
         assert "no multiplexed port-forward" in log, log
     finally:
         cluster.stop()
+
+
+BIG_ROUTES = r"""
+const crypto = require('crypto');
+const BIG = Buffer.alloc(48 << 20);
+for (let i = 0; i < BIG.length; i += 4) BIG.writeUInt32LE(Math.imul(i, 2654435761 | 0) >>> 0, i);
+const srv = http.createServer((req, res) => {
+  if (req.url === '/big') {
+    res.writeHead(200, {'Content-Length': BIG.length});
+    res.end(BIG);
+    return;
+  }
+  if (req.url === '/upload') {
+    const h = crypto.createHash('sha256');
+    let n = 0;
+    req.on('data', (c) => { n += c.length; h.update(c); });
+    req.on('end', () => res.end(n + ' ' + h.digest('hex')));
+    return;
+  }
+"""
+
+
+@pytest.mark.parametrize("via", ["helper", "kubelet"])
+def test_large_transfers_are_flow_controlled(tmp_path, via):
+    """Every forwarded connection has a window. Through the in-container helper: 4 MiB
+    unacknowledged per direction (src/sync/fwd_proto.h). Through the kubelet's tunnel: the SPDY
+    stream's window. A 48 MiB download to a local reader that reads slowly does not pile up in
+    `devspace dev` (its memory grows by well under the body), and the bytes of a 48 MiB download
+    and a 32 MiB upload arrive intact."""
+    import hashlib
+    import socket
+
+    import psutil
+
+    from devspace_amd.localkube import LocalCluster
+
+    cluster = LocalCluster(str(tmp_path / "state"), gpus=0, tls=True).start()
+    try:
+        lk = DevspaceEnv(cluster, str(tmp_path))
+        lk.env["DEVSPACE_PORTFORWARD_VIA"] = via
+        proj, remote, local = _restart_project(lk, "qs-pf-big", "pf-big")
+        index = os.path.join(proj, "index.js")
+        src = open(index).read()
+        assert "http.createServer((req, res) => {" in src
+        open(index, "w").write(src.replace("http.createServer((req, res) => {", BIG_ROUTES, 1)
+                               .replace("}).listen(port,", "});\nsrv.listen(port,", 1))
+        dev = lk.popen(["dev", "--terminal=false"], proj)
+        try:
+            wait_for(lambda: (lambda b: b.startswith("Hello") if b else False)(_fetch(local)), timeout=90,
+                     what="forwarded server")
+            pf_log = os.path.join(proj, ".devspace", "logs", "portforwarding.log")
+            if via == "helper":
+                wait_for(lambda: os.path.exists(pf_log) and "through the in-container helper" in open(pf_log).read(),
+                         timeout=30, what="helper link")
+            expected = bytearray(48 << 20)
+            mv = memoryview(expected).cast("I")
+            for i in range(len(mv)):
+                mv[i] = (i * 4 * 2654435761) & 0xFFFFFFFF
+            proc = psutil.Process(dev.pid)
+            rss0 = proc.memory_info().rss
+            s = socket.create_connection(("127.0.0.1", local), timeout=30)
+            s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 16)
+            s.sendall(b"GET /big HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+            got = bytearray()
+            peak = rss0
+            t_end = time.monotonic() + 2.0
+            while time.monotonic() < t_end:  # a slow reader: 64 KiB every 20 ms
+                got += s.recv(1 << 16)
+                time.sleep(0.02)
+                peak = max(peak, proc.memory_info().rss)
+            while True:
+                b = s.recv(1 << 20)
+                if not b:
+                    break
+                got += b
+            s.close()
+            head, _, body = bytes(got).partition(b"\r\n\r\n")
+            assert head.startswith(b"HTTP/1.1 200"), head[:200]
+            assert len(body) == len(expected) and hashlib.sha256(body).digest() == hashlib.sha256(expected).digest()
+            growth = (peak - rss0) / 2 ** 20
+            print(f"devspace dev RSS growth while the reader lagged: {growth:.1f} MiB")
+            assert growth < 24, growth
+            payload = os.urandom(32 << 20)
+            req = urllib.request.Request(f"http://127.0.0.1:{local}/upload", data=payload, method="POST")
+            reply = urllib.request.urlopen(req, timeout=60).read().decode()
+            assert reply == f"{len(payload)} {hashlib.sha256(payload).hexdigest()}", reply
+        finally:
+            _stop(dev)
+        spans = [json.loads(l) for l in open(os.path.join(proj, ".devspace", "logs", "trace.jsonl"))
+                 if '"portforward.stream"' in l]
+        assert any(s.get("via") == ("helper" if via == "helper" else "tunnel") for s in spans), spans
+    finally:
+        cluster.stop()
