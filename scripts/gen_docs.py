@@ -179,6 +179,10 @@ ENV = {
                                 "connection the restarting app refuses is held in the pod and made once when it "
                                 "listens), else the kubelet's port-forward; `helper` whenever the helper is in the "
                                 "container; `kubelet` never through the helper.",
+    "DEVSPACE_PORTFORWARD_SPILL_MB": "Disk (MiB, default 1024) a port-forwarded connection through the kubelet's "
+                                     "tunnel may use for data its local reader has not taken yet, past 4 MiB in memory "
+                                     "(a nameless temp file in $TMPDIR). Kubelets do not enforce SPDY windows, so without "
+                                     "it one slow reader holds up the pod's other connections. `0`: no spill.",
     "DEVSPACE_PORTFORWARD_HEDGE": "`1`: a held GET/HEAD/OPTIONS on a remote cluster (tunnel round trip of 5 ms or "
                                   "more) is hedged: a new attempt every third of a round trip while earlier ones are "
                                   "in flight; the app may see the request up to about four times. Default: one "

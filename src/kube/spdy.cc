@@ -2,10 +2,15 @@
 
 #include <zlib.h>
 
+#include <unistd.h>
+
+#include <cerrno>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 #include "core/log.h"
+#include "platform/platform.h"
 
 namespace ds {
 namespace kube {
@@ -186,31 +191,132 @@ bool SpdyHeaderCodec::decompress(const std::string& block, SpdyHeaders* out) {
 
 // ---------------------------------------------------------------- mailbox
 
+namespace {
+// a spilled event: end:u8 channel:u32 reset_len:u32 data_len:u32 reset data
+constexpr size_t kSpillHeader = 13;
+
+bool pwrite_all(int fd, const char* p, size_t n, uint64_t off) {
+  while (n) {
+    ssize_t w = ::pwrite(fd, p, n, (off_t)off);
+    if (w < 0 && errno == EINTR) continue;
+    if (w <= 0) return false;
+    p += w;
+    n -= (size_t)w;
+    off += (uint64_t)w;
+  }
+  return true;
+}
+
+bool pread_all(int fd, char* p, size_t n, uint64_t off) {
+  while (n) {
+    ssize_t r = ::pread(fd, p, n, (off_t)off);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    p += r;
+    n -= (size_t)r;
+    off += (uint64_t)r;
+  }
+  return true;
+}
+}  // namespace
+
+SpdyMailbox::~SpdyMailbox() {
+  if (spill_fd_ >= 0) ::close(spill_fd_);
+}
+
+bool SpdyMailbox::spill(const Event& e) {
+  if (spill_broken_) return false;
+  if (spill_fd_ < 0) {
+    std::string dir = spill_dir;
+    if (dir.empty()) {
+      const char* t = std::getenv("TMPDIR");
+      dir = t && *t ? t : "/tmp";
+    }
+    spill_fd_ = plat::open_unlinked_tmp(dir);
+    if (spill_fd_ < 0) {
+      spill_broken_ = true;
+      return false;
+    }
+  }
+  std::string rec(kSpillHeader, '\0');
+  rec[0] = e.end ? 1 : 0;
+  auto put = [&](size_t at, uint32_t v) {
+    for (int i = 0; i < 4; ++i) rec[at + i] = (char)(v >> (24 - 8 * i));
+  };
+  put(1, (uint32_t)e.channel);
+  put(5, (uint32_t)e.reset.size());
+  put(9, (uint32_t)e.data.size());
+  rec += e.reset;
+  rec += e.data;
+  if (!pwrite_all(spill_fd_, rec.data(), rec.size(), spill_w_)) {
+    spill_broken_ = spill_events_ == 0;  // (with events on disk the file stays in use)
+    return false;
+  }
+  spill_w_ += rec.size();
+  ++spill_events_;
+  return true;
+}
+
+bool SpdyMailbox::unspill(Event* e) {
+  char h[kSpillHeader];
+  if (!pread_all(spill_fd_, h, sizeof(h), spill_r_)) return false;
+  auto get = [&](size_t at) {
+    uint32_t v = 0;
+    for (int i = 0; i < 4; ++i) v = (v << 8) | (unsigned char)h[at + i];
+    return v;
+  };
+  e->end = h[0] != 0;
+  e->channel = (int)get(1);
+  const uint32_t rl = get(5), dl = get(9);
+  std::string body(rl + (size_t)dl, '\0');
+  if (!body.empty() && !pread_all(spill_fd_, &body[0], body.size(), spill_r_ + kSpillHeader)) return false;
+  e->reset = body.substr(0, rl);
+  e->data = body.substr(rl);
+  spill_r_ += kSpillHeader + body.size();
+  if (--spill_events_ == 0) {  // drained: start the file over
+    if (::ftruncate(spill_fd_, 0) != 0) spill_broken_ = true;
+    spill_r_ = spill_w_ = 0;
+  }
+  return true;
+}
+
 void SpdyMailbox::push(Event e) {
   {
     std::unique_lock<std::mutex> lk(mu);
     if (closed) return;
-    if (!e.data.empty()) {
-      cv.wait(lk, [this] { return closed || bytes < cap; });
+    while (true) {
       if (closed) return;
-      bytes += e.data.size();
+      // in memory while there is room and nothing waits on disk (so the order is kept)
+      if (spill_events_ == 0 && (e.data.empty() || bytes < cap)) {
+        bytes += e.data.size();
+        q.push_back(std::move(e));
+        break;
+      }
+      if (spilled() + e.data.size() <= spill_cap && spill(e)) break;
+      cv.wait(lk);  // the disk budget is spent, or there is no spill file: wait for the consumer
     }
-    q.push_back(std::move(e));
   }
   cv.notify_all();
 }
 
 bool SpdyMailbox::pop(Event* e, int timeout_ms) {
   std::unique_lock<std::mutex> lk(mu);
-  auto ready = [this] { return !q.empty() || closed; };
+  auto ready = [this] { return !q.empty() || spill_events_ > 0 || closed; };
   if (timeout_ms < 0)
     cv.wait(lk, ready);
   else if (!cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready))
     return false;
-  if (q.empty()) return false;  // closed
-  *e = std::move(q.front());
-  q.pop_front();
-  bytes -= e->data.size();
+  if (closed) return false;
+  if (!q.empty()) {
+    *e = std::move(q.front());
+    q.pop_front();
+    bytes -= e->data.size();
+  } else if (!unspill(e)) {  // the spill file failed under us: the stream cannot go on
+    spill_events_ = 0;
+    spill_r_ = spill_w_ = 0;
+    spill_broken_ = true;
+    *e = Event{0, "", true, "spill"};
+  }
   lk.unlock();
   cv.notify_all();  // a push waiting for room
   return true;
@@ -222,6 +328,10 @@ void SpdyMailbox::close() {
     closed = true;
     q.clear();
     bytes = 0;
+    spill_events_ = 0;
+    spill_r_ = spill_w_ = 0;
+    if (spill_fd_ >= 0) ::close(spill_fd_);
+    spill_fd_ = -1;
   }
   cv.notify_all();
 }

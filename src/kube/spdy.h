@@ -58,9 +58,12 @@ class SpdyHeaderCodec {
 
 // Everything a consumer of streams waits on: (channel, bytes) events of the streams registered
 // to it, plus their ends.
-// Bounded: once `cap` bytes wait unread, push() blocks the session's reader (every stream of
-// the tunnel waits, as a Go spdystream connection's frame loop does when a stream's buffer is
-// full) instead of buffering a fast download for a slow local client without limit.
+// Kubelets do not enforce SPDY windows (spdystream), so a fast download to a slow local client
+// arrives whatever the client announces. The session's reader must not wait for one slow
+// consumer: that would stall every other connection of the pod's tunnel, and its PINGs, as a Go
+// spdystream frame loop does. So: up to `cap` unread bytes in memory, then events spill, in
+// order, to a nameless temporary file (plat::open_unlinked_tmp), up to `spill_cap` bytes. Only
+// past that (or without a usable temp directory) does push() wait for the consumer.
 struct SpdyMailbox {
   struct Event {
     int channel;      // what the stream was registered as (port-forward: 0 data, 1 error)
@@ -68,17 +71,32 @@ struct SpdyMailbox {
     bool end = false;  // FIN or RST from the peer, or the session ended
     std::string reset;  // RST_STREAM status, "" otherwise
   };
+  SpdyMailbox() = default;
+  SpdyMailbox(const SpdyMailbox&) = delete;
+  SpdyMailbox& operator=(const SpdyMailbox&) = delete;
+  ~SpdyMailbox();
   std::mutex mu;
   std::condition_variable cv;
   std::deque<Event> q;
-  size_t bytes = 0;         // data bytes queued
-  size_t cap = 16u << 20;
+  size_t bytes = 0;         // data bytes queued in memory
+  size_t cap = 4u << 20;
+  uint64_t spill_cap = 1ull << 30;  // DEVSPACE_PORTFORWARD_SPILL_MB
+  std::string spill_dir;            // "" = $TMPDIR or /tmp
   bool closed = false;      // the consumer is gone: data is dropped, nothing blocks
   void push(Event e);
   // false on timeout, or once closed
   bool pop(Event* e, int timeout_ms = -1);
   // the consumer is done: queued data is dropped, pushes stop blocking, pop() returns false
   void close();
+  uint64_t spilled() const { return spill_w_ - spill_r_; }  // bytes waiting on disk (under mu)
+
+ private:
+  bool spill(const Event& e);  // under mu; false if the spill file cannot be used
+  bool unspill(Event* e);      // under mu; the oldest spilled event
+  int spill_fd_ = -1;
+  bool spill_broken_ = false;
+  uint64_t spill_w_ = 0, spill_r_ = 0;
+  size_t spill_events_ = 0;
 };
 
 class SpdySession {

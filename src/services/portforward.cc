@@ -162,11 +162,24 @@ class WsFwd : public FwdStream {
   bool first_data_ = true, first_err_ = true;
 };
 
+// Disk a tunnel connection may use for what its local reader has not taken yet
+// (kube::SpdyMailbox): DEVSPACE_PORTFORWARD_SPILL_MB, default 1024; 0 = none (the tunnel's
+// reader then waits for a slow reader, holding up the pod's other connections).
+uint64_t tunnel_spill_cap() {
+  static const uint64_t cap = [] {
+    const char* v = std::getenv("DEVSPACE_PORTFORWARD_SPILL_MB");
+    long long mb = v && *v ? std::atoll(v) : 1024;
+    return (uint64_t)(mb < 0 ? 0 : mb) << 20;
+  }();
+  return cap;
+}
+
 // A stream pair in the pod's tunnel, as kubectl creates it: an error stream (the client never
 // writes to it) and a data stream, tied by a request id. The data follows the SYN_STREAM at once.
 class TunnelFwd : public FwdStream {
  public:
   TunnelFwd(std::shared_ptr<kube::SpdySession> s, int port, uint64_t request_id) : s_(std::move(s)) {
+    box_->spill_cap = tunnel_spill_cap();
     std::string p = std::to_string(port), id = std::to_string(request_id);
     err_ = s_->open({{"streamtype", "error"}, {"port", p}, {"requestid", id}}, box_, 1, true);
     try {

