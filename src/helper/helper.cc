@@ -298,10 +298,12 @@ static void scan_rec(const std::string& p, OutBuf& out, std::set<std::pair<uint6
   if (S_ISLNK(lst.st_mode)) {
     if (::stat(p.c_str(), &st) != 0) st = lst;
   }
-  // like `find -L ... -exec stat -c` : stat of the path itself (links reported as links)
+  // like `find -L ... -exec stat -c` : stat of the path itself (links reported as links), plus
+  // the mtime's nanoseconds (a same-size rewrite within the second moves only those)
   out.put(p + "///" + std::to_string((long long)lst.st_size) + "," + std::to_string((long long)lst.st_mtim.tv_sec) +
           "," + strfmt("%x", (unsigned)lst.st_mode) + "," + strfmt("%o", (unsigned)(lst.st_mode & 07777)) + "," +
-          std::to_string(lst.st_uid) + "," + std::to_string(lst.st_gid) + "\n");
+          std::to_string(lst.st_uid) + "," + std::to_string(lst.st_gid) + "," +
+          std::to_string((long)lst.st_mtim.tv_nsec) + "\n");
   if (S_ISDIR(st.st_mode) && depth < 128) {
     auto key = std::make_pair((uint64_t)st.st_dev, (uint64_t)st.st_ino);
     if (seen.count(key)) return;
@@ -313,6 +315,9 @@ static void scan_rec(const std::string& p, OutBuf& out, std::set<std::pair<uint6
 static void op_scan() {
   fs::mkdirs(g_dest);
   OutBuf out;
+  struct timespec now;  // the clock file stamps come from: how fresh each one is
+  clock_gettime(CLOCK_REALTIME, &now);
+  out.put("#NOW " + std::to_string((long long)now.tv_sec * 1000000000LL + now.tv_nsec) + "\n");
   std::set<std::pair<uint64_t, uint64_t>> seen;
   scan_rec(g_dest, out, seen, 0);
   out.put("DONE\n");

@@ -24,6 +24,11 @@ static const char* kStart = "START";
 static const char* kDone = "DONE";
 static const char* kError = "ERROR";
 static const char* kTmpSuffix = ".devspace-tmp";  // in-flight files (helper and local untar)
+// a stamp younger than this (on the container's clock) may be shared by the next write: a
+// filesystem's coarse clock ticks every few ms, and the same-size rewrite it hides is only
+// seen by content
+static const int64_t kUnsettledNs = 1000000000LL;
+static const int64_t kVerifyMaxBytes = 8LL << 20;
 static const size_t kInitialUpstreamBatch = 1000;  // sync_config.go:20
 
 static long mono_us() {
@@ -67,7 +72,7 @@ std::optional<FileInfo> parse_file_line(const std::string& line, const std::stri
   FileInfo f;
   f.name = t[0].substr(dest.size());
   auto p = split(t[1], ",");
-  if (p.size() != 6) throw SyncError("[Downstream] Wrong fileline: " + line);
+  if (p.size() != 6 && p.size() != 7) throw SyncError("[Downstream] Wrong fileline: " + line);
   int64_t v;
   if (!parse_int64(p[0], &v)) throw SyncError("[Downstream] Wrong fileline: " + line);
   f.size = v;
@@ -80,6 +85,10 @@ std::optional<FileInfo> parse_file_line(const std::string& line, const std::stri
   f.remote_uid = std::atoi(p[4].c_str());
   f.remote_gid = std::atoi(p[5].c_str());
   f.has_remote_attrs = true;
+  if (p.size() == 7) {
+    if (!parse_int64(p[6], &v) || v < 0 || v >= 1000000000) throw SyncError("[Downstream] Wrong fileline: " + line);
+    f.remote_mtime_ns = f.mtime * 1000000000LL + v;
+  }
   return f;
 }
 
@@ -559,6 +568,9 @@ bool Session::should_download(const FileInfo& fi) {
     if (!fi.is_dir) {
       if (fi.mtime > f->mtime) return true;
       if (fi.mtime == f->mtime && fi.size != f->size) return true;
+      // helper listings: a same-size rewrite within the second moved the nanoseconds
+      if (fi.mtime == f->mtime && fi.remote_mtime_ns && f->remote_mtime_ns && fi.remote_mtime_ns != f->remote_mtime_ns)
+        return true;
     }
     return false;
   }
@@ -1388,6 +1400,8 @@ void Session::apply_creates(const std::vector<FileInfo>& files, bool bulk) {
   for (auto& kv : written) {
     index_.create_dir(fs::dirname(kv.first));
     FileInfo f = kv.second;
+    // the container's copy carries the archive's whole-second mtime (recursive_tar)
+    if (!f.is_dir && f.local_mtime_ns) f.remote_mtime_ns = f.local_mtime_ns / 1000000000LL * 1000000000LL;
     if (FileInfo* old = index_.find(kv.first)) {
       if (!f.has_remote_attrs && old->has_remote_attrs) {
         f.remote_mode = old->remote_mode;
@@ -1645,6 +1659,8 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
   long deadline = mono_us() + 300000000L;
   bool partial_ok = mode_ == Mode::Compat && !down_helper_;
   uint64_t scan_bytes = 0;
+  int64_t pod_now_ns = 0;           // the helper's clock, first line of its listing
+  std::vector<FileInfo> verify;     // downloaded while unsettled, still since: check the content
   struct Count {  // recorded on every exit path
     Session* s;
     uint64_t* bytes;
@@ -1699,6 +1715,11 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
       return collect_changes(removes);
     }
     if (line.empty()) continue;
+    if (down_helper_ && starts_with(line, "#NOW ")) {
+      int64_t v;
+      if (parse_int64(line.substr(5), &v)) pod_now_ns = v;
+      continue;
+    }
     // compat acks have no newline: a "DONE" may be glued to nothing else, handled above
     std::optional<FileInfo> fi;
     try {
@@ -1712,17 +1733,29 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
       continue;
     }
     if (ends_with(fi->name, kTmpSuffix)) continue;
+    if (fi->remote_mtime_ns && pod_now_ns && !fi->is_dir && !fi->is_symlink) fi->remote_unsettled = pod_now_ns - fi->remote_mtime_ns < kUnsettledNs;
     std::lock_guard<std::mutex> ig(index_.mu);
     if (removes) removes->erase(fi->name);
-    if (FileInfo* known = index_.find(fi->name)) {
+    FileInfo* known = index_.find(fi->name);
+    if (known) {
       known->remote_mode = fi->remote_mode;
       known->remote_uid = fi->remote_uid;
       known->remote_gid = fi->remote_gid;
       known->has_remote_attrs = true;
     }
     if (fi->is_symlink) index_.files[fi->name] = *fi;
-    if (should_download(*fi) && !in_flight(fi->name, false) && !downloading(fi->name)) creates.push_back(*fi);
+    bool busy = in_flight(fi->name, false) || downloading(fi->name);
+    if (should_download(*fi)) {
+      if (!busy) creates.push_back(*fi);
+    } else if (known && known->remote_unsettled && !fi->remote_unsettled && !busy &&
+               known->remote_mtime_ns == fi->remote_mtime_ns) {
+      if (fi->size <= kVerifyMaxBytes)
+        verify.push_back(*fi);
+      else
+        known->remote_unsettled = false;  // a big file is not rewritten within a clock tick
+    }
   }
+  if (!verify.empty()) verify_unsettled(verify, &creates);
   if (!dest_found) throw SyncError("DestPath not found, find command did not execute correctly");
   if (removes) {  // an upload or remove in flight: the index is about to change, not the pod
     for (auto it = removes->begin(); it != removes->end();) {
@@ -1733,6 +1766,46 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
     }
   }
   return creates;
+}
+
+void Session::verify_unsettled(const std::vector<FileInfo>& files, std::vector<FileInfo>* creates) {
+  std::string list;
+  for (auto& f : files) list += f.name + "\n";
+  if (!write_all(down_shell_->in(), request('H', list))) throw SyncError("downstream: write failed");
+  std::vector<std::string> remote;
+  long deadline = mono_us() + 300000000L;
+  while (true) {
+    std::string line;
+    if (!down_out_.read_line(&line, 200)) {
+      if (down_out_.eof()) throw SyncError("\n[Downstream] Stream closed unexpectedly");
+      if (stopping_) throw SyncError("sync stopped");
+      if (mono_us() > deadline) throw SyncError("downstream: hash timeout");
+      continue;
+    }
+    if (line == kDone) break;
+    remote.push_back(line);
+  }
+  if (remote.size() != files.size()) throw SyncError("downstream: hash reply size mismatch");
+  size_t differ = 0;
+  for (size_t i = 0; i < files.size(); ++i) {
+    const FileInfo& f = files[i];
+    std::string local = crc32_file_hex(o_.watch_path + f.name);
+    fs::StatInfo st = fs::stat(o_.watch_path + f.name);
+    std::lock_guard<std::mutex> ig(index_.mu);
+    FileInfo* known = index_.find(f.name);
+    if (!known || known->remote_mtime_ns != f.remote_mtime_ns) continue;  // moved on meanwhile
+    known->remote_unsettled = false;
+    // edited here since it came down: that edit goes up, nothing comes down over it
+    if (!st.exists || st.size != known->size ||
+        (known->local_mtime_ns && st.mtime_sec * 1000000000LL + st.mtime_nsec != known->local_mtime_ns))
+      continue;
+    if (remote[i] != "-" && remote[i] != local) {
+      known->remote_mtime_ns = 0;  // this stamp is not the content we hold
+      creates->push_back(f);
+      ++differ;
+    }
+  }
+  if (differ) logf(strfmt("[Downstream] %zu file(s) rewritten within a clock tick of their download (CRC-32)", differ));
 }
 
 // Fast mode: instead of listing the whole tree every poll, ask the container whether anything
@@ -1905,6 +1978,17 @@ void Session::download_and_apply(const std::vector<FileInfo>& files, bool bulk) 
     cr.drain();
     line = read_line_idle(reply, idle, "downstream: helper reply");
     if (line != "OK") throw SyncError("downstream: helper error: " + line);
+    {
+      // the container's stamp of what was listed: what came down is that version or a newer one
+      // (read after the listing), so a stamp that moves again is always downloaded again
+      std::lock_guard<std::mutex> ig(index_.mu);
+      for (auto& f : files) {
+        FileInfo* x = index_.find(f.name);
+        if (!x || x->is_dir || x->mtime != f.mtime || x->size != f.size) continue;
+        x->remote_mtime_ns = f.remote_mtime_ns;
+        x->remote_unsettled = f.remote_unsettled;
+      }
+    }
     prog.finish();
     return;
   }
@@ -2282,6 +2366,16 @@ void Session::downstream_loop() {
       }
     } else {
       wait_ms = poll_ms_;
+    }
+    if (down_helper_) {
+      // a file downloaded while its stamp was fresh is checked once it is still (collect_changes):
+      // look again shortly after instead of at the next event
+      std::lock_guard<std::mutex> ig(index_.mu);
+      for (auto& kv : index_.files)
+        if (kv.second.remote_unsettled) {
+          wait_ms = std::min(wait_ms, (int)(kUnsettledNs / 1000000) + 100);
+          break;
+        }
     }
     // wait for the next poll (or a container-side event in helper mode)
     long until = mono_us() + (long)wait_ms * 1000;

@@ -65,9 +65,19 @@ struct FileInfo {
   // Local nanosecond mtime at the last upload/download (non-compat modes only): detects two
   // same-size edits within one second, which the reference's rounded mtimes miss.
   int64_t local_mtime_ns = 0;
+  // The container's side of the same (helper listings only; 0 = unknown): in a listing, the
+  // file's nanosecond mtime; in the index, the stamp of the version last downloaded or uploaded.
+  // A pod process rewriting a file at the same size within one second (a metrics file, a log
+  // line) moves it, where seconds and size do not.
+  int64_t remote_mtime_ns = 0;
+  // The listing saw the file within a second of being written (a coarse filesystem clock can
+  // give the next write the same stamp): once it is still, its content is checked (CRC-32)
+  // against the local copy instead of trusting the stamp.
+  bool remote_unsettled = false;
 };
 
-// Parses one `stat -c "%n///%s,%Y,%f,%a,%u,%g"` line (sync/file_information.go:62).
+// Parses one `stat -c "%n///%s,%Y,%f,%a,%u,%g"` line (sync/file_information.go:62), or the
+// helper's form with a seventh field, the nanoseconds of the mtime.
 // Returns nullopt for the dest path itself; throws on malformed lines.
 std::optional<FileInfo> parse_file_line(const std::string& line, const std::string& dest_path);
 
@@ -243,6 +253,9 @@ class Session {
   // downstream
   void downstream_loop();
   std::vector<FileInfo> collect_changes(std::map<std::string, FileInfo>* removes);
+  // Helper mode: files downloaded while their stamp was fresh and still since, checked by CRC-32
+  // on both sides; the ones whose content differs are added to *creates (down shell held).
+  void verify_unsettled(const std::vector<FileInfo>& files, std::vector<FileInfo>* creates);
   bool probe_changes();  // fast mode: did anything under dest change since the last probes?
   std::string probe_id_;
   bool up_has_head_ = true;  // fast mode: container has `head -c` for streamed uploads

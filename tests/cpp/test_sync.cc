@@ -2,6 +2,7 @@
 // TestNormalSync incl. remove/rename matrix) and sync/util_test.go (TestCopyToContainerTestable),
 // run over the local-shell transport in every protocol mode, and over the Kubernetes exec
 // WebSocket transport (kube::ExecTransport) when tests/test_sync_matrix_kube.py points it at a pod.
+#include <fcntl.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -749,4 +750,43 @@ TEST(sync_helper_bulk_download_channel) {
   std::this_thread::sleep_for(std::chrono::milliseconds(150));
   s.stop();
   EXPECT_TRUE(!s.running());
+}
+
+// A pod process that rewrites a file at the same size within the second (a metrics or status
+// file) is downloaded every time: the helper's listing carries the mtime's nanoseconds. And a
+// rewrite that even keeps the nanoseconds (a coarse filesystem clock gives two writes in one
+// tick the same stamp; here forced with utimensat) is caught by content once the file is still:
+// its stamp was fresh when it was downloaded, so the copy is checked by CRC-32.
+TEST(sync_helper_same_size_rewrites_within_a_second_come_down) {
+  log::logdir() = fs::make_temp_dir("synclogs-");
+  Dirs d;
+  if (d.dest != d.remote) return;  // local-shell transport only
+  Options o = base_options(d, Mode::Helper);
+  Session s(o, std::make_shared<LocalShellTransport>());
+  s.start();
+  EXPECT_TRUE(s.wait_initial_sync(15000));
+  const std::string rf = fs::join(d.remote, "status.txt"), lf = fs::join(d.local, "status.txt");
+  auto wait_local = [&](const std::string& want, int ms) {
+    auto t0 = std::chrono::steady_clock::now();
+    std::string got;
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(ms)) {
+      if (fs::read_file(lf, &got) && got == want) return true;
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+    return false;
+  };
+  for (int i = 0; i < 6; ++i) {  // same size, a few ms apart: the last one must land
+    fs::write_file(rf, "step " + std::to_string(i) + "\n");
+    std::this_thread::sleep_for(std::chrono::milliseconds(3));
+  }
+  EXPECT_TRUE(wait_local("step 5\n", 10000));
+  // same size and the very same stamp as the version already downloaded
+  struct stat st;
+  EXPECT_EQ(::stat(rf.c_str(), &st), 0);
+  fs::write_file(rf, "step X\n");
+  struct timespec ts[2] = {st.st_atim, st.st_mtim};
+  EXPECT_EQ(::utimensat(AT_FDCWD, rf.c_str(), ts, 0), 0);
+  EXPECT_TRUE(wait_local("step X\n", 10000));
+  EXPECT_TRUE(s.running());
+  s.stop();
 }
