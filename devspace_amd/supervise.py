@@ -36,6 +36,17 @@ def _free_port() -> int:
 # gloo's per-connection line, one per rank and group start ("[Gloo] Rank 3 is connected to 7 peer
 # ranks. Expected number of connected peer ranks is : 7"): folded into one line per group
 _GLOO_CONNECTED = re.compile(rb"^\[Gloo\] Rank \d+ is connected to (\d+) peer ranks")
+# a warning or info line of torch's C++ logger ("[W1019 04:35:09.978355262 socket.cpp:207] [c10d]
+# The hostname of the client socket cannot be retrieved. err=-3"): the same message from several
+# ranks at group start is one line, `[ranks 0-7] ...`. Errors (E/F) are never held.
+_CPP_LOG = re.compile(rb"^\[[WI]\d{4} [\d:.]+ (\S+:\d+)\] (.*)$")
+
+
+def _rank_list(ranks):
+    rs = sorted(ranks)
+    if rs == list(range(rs[0], rs[-1] + 1)) and len(rs) > 2:
+        return f"{rs[0]}-{rs[-1]}"
+    return ",".join(str(r) for r in rs)
 
 
 class LogRelay:
@@ -43,11 +54,14 @@ class LogRelay:
     `[rank N] <line>` when the group has more than one rank, the line as it is with one. Ranks
     writing at once never split or merge each other's lines (each line is one write by one
     thread, under the lock the supervisor's own lines take too). gloo's per-rank connection lines
-    become one `group of N connected` line per group. What a rank printed without a final newline
+    become one `group of N connected` line per group; a warning of torch's C++ logger that several
+    ranks print alike (the same source line and message) is held up to HOLD_S and goes out once,
+    `[ranks 0-7] <line>`. What a rank printed without a final newline
     is flushed, with one, when its pipe closes. (The reference reformats its children's output
     line by line too: pkg/devspace/builder/kaniko/util.go:18-87, pkg/util/processutil/pipe.go:46.)"""
 
     MAX_LINE = 1 << 16  # a longer line (no newline yet: a progress bar) goes out in pieces
+    HOLD_S = 1.0  # how long a C++ logger warning waits for the same line from the other ranks
 
     def __init__(self, nproc, out_fd=None):
         self.nproc = max(1, nproc)
@@ -56,6 +70,7 @@ class LogRelay:
         self._mu = threading.Lock()
         self._open = {}  # fd -> [rank, pending bytes]
         self._gloo = 0
+        self._held = {}  # (source, message) -> [deadline, first line, ranks] (relay thread only)
         self._wake_r, self._wake_w = os.pipe()
         self._thread = threading.Thread(target=self._run, name="devspace-log-relay", daemon=True)
         self._thread.start()
@@ -70,7 +85,7 @@ class LogRelay:
         end = time.monotonic() + timeout
         while time.monotonic() < end:
             with self._mu:
-                if not self._open:
+                if not self._open and not self._held:
                     return True
             time.sleep(0.005)
         return False
@@ -106,7 +121,28 @@ class LogRelay:
             if done:
                 self._write(f"{PREFIX} group of {self.nproc} rank(s) connected (gloo)\n".encode())
             return
+        if self.prefix:
+            c = _CPP_LOG.match(line)
+            if c:
+                key = c.groups()
+                h = self._held.get(key)
+                if h is None:
+                    h = self._held[key] = [time.monotonic() + self.HOLD_S, line, set()]
+                h[2].add(rank)
+                if len(h[2]) >= self.nproc:
+                    self._flush_held(key)
+                return
         self._write(((b"[rank %d] " % rank) if self.prefix else b"") + line + b"\n")
+
+    def _flush_held(self, key):
+        _, line, ranks = self._held.pop(key)
+        who = b"[rank %d] " % next(iter(ranks)) if len(ranks) == 1 else f"[ranks {_rank_list(ranks)}] ".encode()
+        self._write(who + line + b"\n")
+
+    def _flush_expired(self, all_=False):
+        now = time.monotonic()
+        for key in [k for k, h in self._held.items() if all_ or h[0] <= now]:
+            self._flush_held(key)
 
     def _run(self):
         import select
@@ -114,10 +150,17 @@ class LogRelay:
         while True:
             with self._mu:
                 fds = list(self._open)
+            if self._held and not fds:
+                self._flush_expired(all_=True)  # every rank has exited: nothing more to wait for
+            wait = None
+            if self._held:
+                wait = max(0.0, min(h[0] for h in self._held.values()) - time.monotonic())
             try:
-                ready, _, _ = select.select(fds + [self._wake_r], [], [])
+                ready, _, _ = select.select(fds + [self._wake_r], [], [], wait)
             except (OSError, ValueError):
                 ready = []
+            if self._held:
+                self._flush_expired()
             for fd in ready:
                 if fd == self._wake_r:
                     os.read(self._wake_r, 4096)

@@ -219,6 +219,8 @@ ENV = {
     "DEVSPACE_SYNC_MODE": "Sync protocol: `helper` (default when `devspace-helper` ships next to the binary: "
                           "inotify in the pod, streamed archives; falls back to `fast` where it cannot run), `fast` "
                           "(POSIX tools only, event-driven) or `compat` (the original protocol and timing).",
+    "DEVSPACE_SYNC_STOP_WARN_MS": "A sync stop that takes longer than this logs which of its loops are still running and "
+    "the step it waits on, to `sync.log` and stderr, every period (default 20000).",
     "DEVSPACE_SYNC_WARN_FILE_MB": "Size above which a synced file is logged as large (default 1024).",
     "DEVSPACE_TRACE": "`0` disables the phase spans written to `.devspace/logs/trace.jsonl`.",
     "DEVSPACE_VAR_<NAME>": "Value of config variable `${NAME}`; no question is asked for it.",

@@ -2403,14 +2403,39 @@ void Session::downstream_loop() {
 
 // ============================================================ lifecycle
 
+std::thread Session::spawn_loop(LoopBit bit, std::function<void()> body) {
+  live_loops_ |= bit;
+  return std::thread([this, bit, body = std::move(body)] {
+    struct Done {
+      Session* s;
+      LoopBit b;
+      ~Done() { s->live_loops_ &= ~(unsigned)b; }
+    } done{this, bit};
+    body();
+  });
+}
+
+std::string Session::describe_stop_state() {
+  static const std::pair<unsigned, const char*> names[] = {{kUpLoop, "upstream"},
+                                                           {kBulkLoop, "bulk upload"},
+                                                           {kBulkDownLoop, "bulk download"},
+                                                           {kDownLoop, "downstream"},
+                                                           {kSupervisor, "supervisor"}};
+  unsigned live = live_loops_.load();
+  std::string loops;
+  for (auto& n : names)
+    if (live & n.first) loops += std::string(loops.empty() ? "" : ", ") + n.second;
+  return strfmt("at '%s'; loops still running: %s", stop_step_.load(), loops.empty() ? "none" : loops.c_str());
+}
+
 void Session::start_loops(bool upstream, bool downstream) {
-  if (upstream) up_thread_ = std::thread([this] { upstream_loop(); });
-  if (upstream) bulk_thread_ = std::thread([this] { bulk_loop(); });
+  if (upstream) up_thread_ = spawn_loop(kUpLoop, [this] { upstream_loop(); });
+  if (upstream) bulk_thread_ = spawn_loop(kBulkLoop, [this] { bulk_loop(); });
   if (downstream) {
     bulk_down_on_ = true;
-    bulk_down_thread_ = std::thread([this] { bulk_down_loop(); });
+    bulk_down_thread_ = spawn_loop(kBulkDownLoop, [this] { bulk_down_loop(); });
   }
-  if (downstream) down_thread_ = std::thread([this] { downstream_loop(); });
+  if (downstream) down_thread_ = spawn_loop(kDownLoop, [this] { downstream_loop(); });
 }
 
 void Session::fail(const std::string& err) {
@@ -2427,6 +2452,7 @@ void Session::fail(const std::string& err) {
 
 void Session::stop_loops() {
   q_cv_.notify_all();
+  stop_step_ = "stop_loops: terminating shells";
   if (up_shell_) up_shell_->terminate();
   if (down_shell_) down_shell_->terminate();
   {
@@ -2439,19 +2465,24 @@ void Session::stop_loops() {
     up_pcv_.notify_all();
   }
   up_rcv_.notify_all();
+  stop_step_ = "stop_loops: joining the upload loops";
   if (up_thread_.joinable() && up_thread_.get_id() != std::this_thread::get_id()) up_thread_.join();
   if (bulk_thread_.joinable() && bulk_thread_.get_id() != std::this_thread::get_id()) bulk_thread_.join();
+  stop_step_ = "stop_loops: joining the bulk download loop";
   if (bulk_down_thread_.joinable() && bulk_down_thread_.get_id() != std::this_thread::get_id())
     bulk_down_thread_.join();
   bulk_down_on_ = false;
   {
+    stop_step_ = "stop_loops: closing the bulk download shell";
     std::lock_guard<std::mutex> g(bulk_down_ptr_mu_);
     if (bulk_down_shell_) {
       bulk_down_shell_->close();
       bulk_down_shell_.reset();
     }
   }
+  stop_step_ = "stop_loops: joining the downstream loop";
   if (down_thread_.joinable() && down_thread_.get_id() != std::this_thread::get_id()) down_thread_.join();
+  stop_step_ = "stop_loops: closing shells";
   {
     // a reconnect starts over from an initial sync: nothing is in flight or queued for the bulk lane
     std::lock_guard<std::mutex> g(q_mu_);
@@ -2490,11 +2521,11 @@ void Session::supervise() {
     }
   };
   logf("[Sync] Start syncing");
-  up_thread_ = std::thread([this] { upstream_loop(); });
-  bulk_thread_ = std::thread([this] { bulk_loop(); });
+  up_thread_ = spawn_loop(kUpLoop, [this] { upstream_loop(); });
+  bulk_thread_ = spawn_loop(kBulkLoop, [this] { bulk_loop(); });
   bulk_down_on_ = true;
-  bulk_down_thread_ = std::thread([this] { bulk_down_loop(); });
-  down_thread_ = std::thread([this, run_initial] {
+  bulk_down_thread_ = spawn_loop(kBulkDownLoop, [this] { bulk_down_loop(); });
+  down_thread_ = spawn_loop(kDownLoop, [this, run_initial] {
     if (run_initial()) downstream_loop();
   });
   while (true) {
@@ -2547,11 +2578,11 @@ void Session::supervise() {
       failed_ = false;
       pending_failure_.clear();
     }
-    up_thread_ = std::thread([this] { upstream_loop(); });
-    bulk_thread_ = std::thread([this] { bulk_loop(); });
+    up_thread_ = spawn_loop(kUpLoop, [this] { upstream_loop(); });
+    bulk_thread_ = spawn_loop(kBulkLoop, [this] { bulk_loop(); });
     bulk_down_on_ = true;
-    bulk_down_thread_ = std::thread([this] { bulk_down_loop(); });
-    down_thread_ = std::thread([this, run_initial] {
+    bulk_down_thread_ = spawn_loop(kBulkDownLoop, [this] { bulk_down_loop(); });
+    down_thread_ = spawn_loop(kDownLoop, [this, run_initial] {
       if (run_initial()) downstream_loop();
     });
   }
@@ -2562,7 +2593,7 @@ void Session::start() {
   open_shells();
   start_watcher();
   running_ = true;
-  supervisor_ = std::thread([this] { supervise(); });
+  supervisor_ = spawn_loop(kSupervisor, [this] { supervise(); });
 }
 
 bool Session::wait_initial_sync(int timeout_ms) {
@@ -2593,14 +2624,41 @@ void Session::stop(const std::string& fatal_error) {
   }
   state_cv_.notify_all();
   q_cv_.notify_all();
+  // watchdog: a stop is normally done within a few hundred ms (every loop checks stopping_ at
+  // least every 200 ms and every shell is killed before the joins)
+  std::mutex wd_mu;
+  std::condition_variable wd_cv;
+  bool stopped = false;
+  int warn_ms = 20000;
+  if (const char* v = std::getenv("DEVSPACE_SYNC_STOP_WARN_MS")) warn_ms = std::max(10, std::atoi(v));
+  std::thread watchdog([&] {
+    long t0 = mono_us();
+    std::unique_lock<std::mutex> lk(wd_mu);
+    while (!wd_cv.wait_for(lk, std::chrono::milliseconds(warn_ms), [&] { return stopped; })) {
+      std::string msg = strfmt("[Sync] Stop still waiting after %.1fs %s", (mono_us() - t0) / 1e6,
+                               describe_stop_state().c_str());
+      logf(msg);
+      std::fprintf(stderr, "%s\n", msg.c_str());
+    }
+  });
+  stop_step_ = "stopping the symlink watchers";
   {
     std::lock_guard<std::mutex> g(symlink_mu_);
     for (auto& kv : symlinks_) kv.second->stop();
     symlinks_.clear();
   }
+  stop_step_ = "stopping the file watcher";
   if (watcher_) watcher_->stop();
+  stop_step_ = "joining the supervisor";
   if (supervisor_.joinable()) supervisor_.join();
   stop_loops();
+  stop_step_ = "stopped";
+  {
+    std::lock_guard<std::mutex> g(wd_mu);
+    stopped = true;
+  }
+  wd_cv.notify_all();
+  watchdog.join();
   running_ = false;
   logf("[Sync] Sync stopped");
   if (!fatal_error.empty()) log_error("Error: " + fatal_error);

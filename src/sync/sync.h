@@ -340,6 +340,14 @@ class Session {
   void drop_identical_copies(std::vector<FileInfo>& changes);
 
   std::thread up_thread_, down_thread_, supervisor_;
+  // Stop diagnostics: one bit per loop thread that has not returned yet, and the step stop() is
+  // at. A stop that takes longer than DEVSPACE_SYNC_STOP_WARN_MS (20 s) logs both, every period,
+  // to sync.log and stderr, so a stop that never ends names the loop and the step it waits on.
+  enum LoopBit : unsigned { kUpLoop = 1, kBulkLoop = 2, kBulkDownLoop = 4, kDownLoop = 8, kSupervisor = 16 };
+  std::atomic<unsigned> live_loops_{0};
+  std::atomic<const char*> stop_step_{""};
+  std::thread spawn_loop(LoopBit bit, std::function<void()> body);
+  std::string describe_stop_state();
   std::atomic<bool> running_{false}, stopping_{false};
   std::atomic<bool> failed_{false};
   std::mutex pod_mu_;

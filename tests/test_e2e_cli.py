@@ -52,8 +52,9 @@ def test_quickstart_deploy_logs_enter_analyze_purge(localkube):
     pods = wait_for(lambda: running(lk.pods("quickstart")), what="quickstart pod")
     assert pods[0]["spec"]["containers"][0]["image"].startswith("devspace-local/quickstart:")
 
-    logs = wait_for(lambda: "listening" in lk.run(["logs"], proj).stdout and lk.run(["logs"], proj).stdout,
-                    what="app log line")
+    # (check=False: a pod that is briefly not Running between two polls is polled again)
+    logs = wait_for(lambda: "listening" in lk.run(["logs"], proj, check=False).stdout
+                    and lk.run(["logs"], proj, check=False).stdout, what="app log line")
     assert "Example app listening on port 3000!" in logs
 
     out = lk.run(["enter", "--", "cat", "package.json"], proj).stdout

@@ -417,6 +417,53 @@ def test_log_relay_flushes_a_last_line_without_a_newline():
     assert len(ys) == 2 and sum(len(l) - len("[rank 1] ") for l in ys) == LogRelay.MAX_LINE + 10
 
 
+def test_log_relay_folds_a_warning_every_rank_prints_alike():
+    """torch's C++ logger warnings that several ranks print alike at group start (c10d's
+    "hostname of the client socket cannot be retrieved", once per rank) go out as one
+    `[ranks 0-3]` line; a warning only some ranks print goes out once the hold ends, with those
+    ranks; errors and ordinary lines are never held."""
+    from devspace_amd.supervise import LogRelay
+
+    import threading
+
+    out_r, out_w = os.pipe()
+    got = []
+
+    def reader():
+        while True:
+            chunk = os.read(out_r, 1 << 20)
+            if not chunk:
+                return
+            got.append(chunk)
+
+    t = threading.Thread(target=reader, daemon=True)
+    t.start()
+    relay = LogRelay(4, out_fd=out_w)
+    pipes = [os.pipe() for _ in range(4)]
+    for r, (rd, _) in enumerate(pipes):
+        relay.add(r, rd)
+    warn = "[W1019 04:35:{:02d}.97835526{} socket.cpp:207] [c10d] The hostname of the client socket cannot be retrieved. err=-3\n"
+    for r, (_, wr) in enumerate(pipes):
+        os.write(wr, warn.format(r, r).encode())
+        os.write(wr, f"plain {r}\n".encode())
+    os.write(pipes[2][1], b"[W1019 04:35:09.1 other.cpp:1] only some ranks\n")
+    os.write(pipes[3][1], b"[W1019 04:35:09.2 other.cpp:1] only some ranks\n")
+    os.write(pipes[1][1], b"[E1019 04:35:09.3 other.cpp:2] an error\n")
+    time.sleep(LogRelay.HOLD_S + 0.5)
+    for _, wr in pipes:
+        os.close(wr)
+    assert relay.drain(5.0)
+    os.close(out_w)
+    t.join(5.0)
+    lines = [l for l in b"".join(got).decode().split("\n") if l]
+    hostname = [l for l in lines if "hostname of the client socket" in l]
+    assert len(hostname) == 1 and hostname[0].startswith("[ranks 0-3] [W1019 04:35:00"), lines
+    some = [l for l in lines if "only some ranks" in l]
+    assert len(some) == 1 and some[0].startswith("[ranks 2,3] "), lines
+    assert "[rank 1] [E1019 04:35:09.3 other.cpp:2] an error" in lines
+    assert all(f"[rank {r}] plain {r}" in lines for r in range(4)), lines
+
+
 def test_a_single_rank_logs_without_a_prefix(tmp_path):
     entry = tmp_path / "train.py"
     entry.write_text(CHATTY.format(lines=50))
