@@ -1146,11 +1146,11 @@ void Session::apply_removes(const std::vector<FileInfo>& files) {
     if (mode_ == Mode::Compat) {
       std::string cmd = "rm -R " + join(args, " ") + "  >/dev/null 2>/dev/null && printf \"" + kDone +
                         "\" || printf \"" + kDone + "\"\n";
-      if (!write_all(up_shell_->in(), cmd)) throw SyncError("upstream: write failed");
+      send(up_shell_->in(), cmd);
       wait_ack(up_out_, kDone, true);
     } else {
       std::string cmd = "rm -R " + join(args, " ") + " >/dev/null 2>&1; echo " + kDone + "\n";
-      if (!write_all(up_shell_->in(), cmd)) throw SyncError("upstream: write failed");
+      send(up_shell_->in(), cmd);
       wait_ack(up_out_, kDone, false);
     }
   }
@@ -1345,7 +1345,7 @@ uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std
 					tar )" + std::string(xflags) + R"( "$tmpFile" -C ')" + dest_ + R"(/.' 2>)" + remote("/tmp/devspace-upstream-error") + R"(;
 					echo "DONE";
 		)";
-    if (!write_all(fd, cmd)) throw SyncError("upstream: write failed");
+    send(fd, cmd);
     wait_ack(up_out_, kStart, false, nullptr, o_.idle_timeout_ms);
     send_payload();
     wait_ack(up_out_, kDone, false, nullptr, done_ms);
@@ -1356,7 +1356,7 @@ uint64_t Session::stream_upload(const std::vector<FileInfo>& files, std::map<std
   // polling in the container)
   std::string cmd = "echo " + std::string(kStart) + " && head -c " + size + " | tar " + xflags + " - -C " +
                     shell_quote(dest_ + "/.") + " 2>" + remote("/tmp/devspace-upstream-error") + "; echo " + kDone + "\n";
-  if (!write_all(fd, cmd)) throw SyncError("upstream: write failed");
+  send(fd, cmd);
   wait_ack(up_out_, kStart, false, nullptr, o_.idle_timeout_ms);
   send_payload();
   wait_ack(up_out_, kDone, false, nullptr, done_ms);
@@ -1588,7 +1588,7 @@ void Session::drop_identical_copies(std::vector<FileInfo>& changes) {
     std::vector<std::string> remote;
     {
       std::lock_guard<std::mutex> sg(down_shell_mu_);
-      if (!write_all(down_shell_->in(), request('H', list))) throw SyncError("downstream: write failed");
+      send(down_shell_->in(), request('H', list));
       long deadline = mono_us() + 300000000L;
       while (true) {
         std::string line;
@@ -1643,17 +1643,17 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
   std::lock_guard<std::mutex> sg(down_shell_mu_);
   std::string qd = shell_quote(dest_);
   if (down_helper_) {
-    if (!write_all(down_shell_->in(), request('S', ""))) throw SyncError("downstream: write failed");
+    send(down_shell_->in(), request('S', ""));
   } else if (mode_ == Mode::Compat) {
     std::string cmd = "mkdir -p '" + dest_ + "' && find -L '" + dest_ +
                       "' -exec stat -c \"%n///%s,%Y,%f,%a,%u,%g\" {} + 2>/dev/null && echo -n \"" + kDone +
                       "\" || echo -n \"" + kError + "\"\n";
-    if (!write_all(down_shell_->in(), cmd)) throw SyncError("downstream: write failed");
+    send(down_shell_->in(), cmd);
   } else {
     std::string cmd = "mkdir -p " + qd + " && find -L " + qd +
                       " -exec stat -c '%n///%s,%Y,%f,%a,%u,%g' {} + 2>/dev/null && echo " + kDone + " || echo " +
                       kError + "\n";
-    if (!write_all(down_shell_->in(), cmd)) throw SyncError("downstream: write failed");
+    send(down_shell_->in(), cmd);
   }
   RateLimiter rl(o_.downstream_limit);
   long deadline = mono_us() + 300000000L;
@@ -1771,7 +1771,7 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
 void Session::verify_unsettled(const std::vector<FileInfo>& files, std::vector<FileInfo>* creates) {
   std::string list;
   for (auto& f : files) list += f.name + "\n";
-  if (!write_all(down_shell_->in(), request('H', list))) throw SyncError("downstream: write failed");
+  send(down_shell_->in(), request('H', list));
   std::vector<std::string> remote;
   long deadline = mono_us() + 300000000L;
   while (true) {
@@ -1828,7 +1828,7 @@ bool Session::probe_changes() {
                     " -cnewer " + old + " 2>/dev/null || find -L " + qd + " -newer " + old +
                     " 2>/dev/null; } | { IFS= read -r l && echo CHANGED; }; else echo FIRST; fi; rm -f " + st +
                     std::to_string(k - 3) + "; echo " + kDone + "\n";
-  if (!write_all(down_shell_->in(), cmd)) throw SyncError("downstream: write failed");
+  send(down_shell_->in(), cmd);
   long deadline = mono_us() + 60000000L;
   bool hit = false;
   while (true) {
@@ -1970,7 +1970,7 @@ void Session::download_and_apply(const std::vector<FileInfo>& files, bool bulk) 
   if (down_helper_ || bulk) {
     std::string rels;
     for (auto* f : order) rels += f->name + "\n";
-    if (!write_all(fd, request('D', rels))) throw SyncError("downstream: write failed");
+    send(fd, request('D', rels));
     std::string line = read_line_idle(reply, idle, "downstream: helper reply");
     if (line != "STREAM") throw SyncError("downstream: helper error: " + line);
     frame::ChunkReader cr(counted(reader_source(reply, idle, "downstream: helper stream")));
@@ -2022,9 +2022,9 @@ void Session::download_and_apply(const std::vector<FileInfo>& files, bool bulk) 
 					(>&2 echo "DONE");
 					cat "$tmpFileOutput";
 		)";
-    if (!write_all(fd, cmd)) throw SyncError("downstream: write failed");
+    send(fd, cmd);
     wait_ack(down_out_, kStart, false, nullptr, idle);
-    if (!write_all(fd, list)) throw SyncError("downstream: write failed");
+    send(fd, list);
     // the container gzips everything into its temp file before the size line: silent for a
     // while on big files (gzip -6 runs ~20 MB/s on incompressible data)
     std::string before;
@@ -2053,7 +2053,7 @@ void Session::download_and_apply(const std::vector<FileInfo>& files, bool bulk) 
   std::string cmd = "mkdir -p " + shell_quote(remote("/tmp")) + " 2>/dev/null; echo DSSTART; tar -c" +
                     std::string(gz ? "z" : "") + "f - -C " + shell_quote(dest_) + " -- " +
                     join(args, " ") + " 2>" + remote("/tmp/devspace-downstream-error") + "; echo; echo \"DSEND $?\"\n";
-  if (!write_all(fd, cmd)) throw SyncError("downstream: write failed");
+  send(fd, cmd);
   while (read_line_idle(down_out_, idle, "downstream") != "DSSTART") {
   }
   std::string leftover;

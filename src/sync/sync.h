@@ -210,6 +210,7 @@ class Session {
   void stop_loops();
   // Bulk write to a shell's stdin with an idle timeout (SyncError when stuck or closed).
   void send(int fd, const char* d, size_t n);
+  void send(int fd, const std::string& s) { send(fd, s.data(), s.size()); }
   // Blocking reads with an idle timeout (no byte for idle_ms -> SyncError), honouring stop().
   std::string read_line_idle(LineReader& r, int idle_ms, const char* what);
   Source reader_source(LineReader& r, int idle_ms, const char* what);
