@@ -5,7 +5,13 @@
 file(GLOB_RECURSE SRCS ${ROOT}/src/*.cc ${ROOT}/src/*.h)
 set(PATTERNS "inotify_" "epoll_" "prctl\\(" "pipe2\\(" "accept4\\(" "eventfd\\(" "MSG_NOSIGNAL" "SOCK_CLOEXEC"
              "O_TMPFILE" "/proc/self" "sys/inotify\\.h" "sys/epoll\\.h" "sys/prctl\\.h" "sys/eventfd\\.h" "signalfd"
-             "timerfd")
+             "timerfd"
+             # Linux or glibc only (macOS's headers lack them)
+             "F_SETPIPE_SZ" "TCP_QUICKACK" "TCP_USER_TIMEOUT" "TCP_KEEPIDLE" "SO_PEERCRED" "splice\\(" "memfd_create"
+             "getrandom\\(" "CLOCK_BOOTTIME" "posix_fadvise" "fallocate\\(" "statx\\(" "SOCK_NONBLOCK" "renameat2"
+             "copy_file_range" "MSG_MORE" "<endian\\.h>" "<byteswap\\.h>" "<malloc\\.h>" "<sys/sendfile\\.h>"
+             "<linux/" "be64toh" "htobe64" "be32toh" "htobe32" "strchrnul" "memrchr" "get_nprocs" "sys/sysinfo\\.h"
+             "program_invocation_name" "pthread_tryjoin_np" "ppoll\\(")
 set(BAD "")
 foreach(f ${SRCS})
   if(f MATCHES "/src/platform/linux[^/]*$" OR f MATCHES "/src/helper/")

@@ -30,6 +30,10 @@ int accept_cloexec(int listen_fd) {
   }
 }
 
+void grow_pipe(int fd, int bytes) {
+  if (fd >= 0) ::fcntl(fd, F_SETPIPE_SZ, bytes);
+}
+
 void close_fds_in_child(int) {}
 
 ssize_t send_nosignal(int fd, const void* data, size_t n) { return ::send(fd, data, n, MSG_NOSIGNAL); }

@@ -34,6 +34,11 @@ int socket_cloexec(int family, int type, int protocol = 0);
 // accept(2) of one connection; the new descriptor is close-on-exec. -1 with errno set.
 int accept_cloexec(int listen_fd);
 
+// Asks for a pipe buffer of `bytes` (Linux: F_SETPIPE_SZ, up to the unprivileged maximum of
+// 1 MiB, so bulk transfers cross the pipe in fewer wake-ups). Elsewhere pipes size themselves:
+// a no-op. Best effort: a refusal leaves the default size.
+void grow_pipe(int fd, int bytes);
+
 // In a forked child before execve: closes inherited descriptors above 2 that are not
 // close-on-exec yet (except `keep`). A no-op where every descriptor is created close-on-exec.
 // Async-signal-safe.

@@ -56,6 +56,8 @@ int pipe_cloexec(int fds[2], bool nonblock) {
   return 0;
 }
 
+void grow_pipe(int, int) {}  // macOS and the BSDs grow a pipe's buffer with its backlog
+
 int socket_cloexec(int family, int type, int protocol) { return finish(::socket(family, type, protocol)); }
 
 int accept_cloexec(int listen_fd) {

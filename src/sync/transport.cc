@@ -12,6 +12,7 @@
 #include <thread>
 
 #include "core/strutil.h"
+#include "platform/platform.h"
 
 namespace ds {
 namespace sync {
@@ -65,8 +66,7 @@ std::unique_ptr<Shell> LocalShellTransport::open(const std::vector<std::string>&
   if (!s->p->start(argv, o)) throw std::runtime_error("start " + join(argv, " ") + ": " + s->p->error());
   // 1 MiB pipes (the Linux default for unprivileged processes' maximum) instead of 64 KiB:
   // bulk transfers cross the pipe in 16x fewer wake-ups
-  for (int fd : {s->p->stdin_fd(), s->p->stdout_fd()})
-    if (fd >= 0) ::fcntl(fd, F_SETPIPE_SZ, 1 << 20);
+  for (int fd : {s->p->stdin_fd(), s->p->stdout_fd()}) plat::grow_pipe(fd, 1 << 20);
   return s;
 }
 

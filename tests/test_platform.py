@@ -17,7 +17,14 @@ from conftest import ROOT
 
 LINUX_ONLY = [r"inotify_", r"epoll_", r"prctl\(", r"pipe2\(", r"accept4\(", r"eventfd\(", r"MSG_NOSIGNAL",
               r"SOCK_CLOEXEC", r"O_TMPFILE", r"/proc/self", r"sys/inotify\.h", r"sys/epoll\.h", r"sys/prctl\.h",
-              r"sys/eventfd\.h", r"signalfd", r"timerfd"]
+              r"sys/eventfd\.h", r"signalfd", r"timerfd",
+              # Linux or glibc only, found by an audit of src/ for what macOS's headers lack
+              r"F_SETPIPE_SZ", r"TCP_QUICKACK", r"TCP_USER_TIMEOUT", r"TCP_KEEPIDLE", r"SO_PEERCRED",
+              r"\bsplice\(", r"memfd_create", r"getrandom\(", r"CLOCK_BOOTTIME", r"posix_fadvise",
+              r"\bfallocate\(", r"\bstatx\(", r"SOCK_NONBLOCK", r"O_PATH\b", r"renameat2", r"copy_file_range",
+              r"MSG_MORE", r"<endian\.h>", r"<byteswap\.h>", r"<malloc\.h>", r"<sys/sendfile\.h>",
+              r"<linux/", r"be64toh|htobe64|be32toh|htobe32", r"strchrnul", r"memrchr", r"get_nprocs",
+              r"sys/sysinfo\.h", r"program_invocation_name", r"pthread_tryjoin_np", r"\bppoll\("]
 
 
 def test_linux_only_calls_stay_behind_the_platform_layer():
