@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Per-module line coverage from a gcov build (scripts/coverage.sh): runs `gcov -n` on every
-.gcda under BUILD and sums the executed / executable lines of the .cc files under SRC by
-module (src/<module>/). Files that never ran (no .gcda) count as 0 %.
+"""Per-module line coverage from gcov builds (scripts/coverage.sh): runs `gcov -n` on every
+.gcda under each BUILD and sums the executed / executable lines of the .cc files under SRC by
+module (src/<module>/). A file built in several builds counts with its best run (the default
+build and the portable one share most of src/; each has its own platform layer). Files that
+never ran (no .gcda) count as 0 %.
 
-    python scripts/coverage_summary.py build/coverage src
+    python scripts/coverage_summary.py build/coverage [build/coverage-portable ...] src
 """
 import collections
 import glob
@@ -13,10 +15,11 @@ import subprocess
 import sys
 
 
-def main(build, src):
+def main(builds, src):
     src = os.path.abspath(src)
     seen = {}
-    for gcda in glob.glob(os.path.join(build, "**", "*.gcda"), recursive=True):
+    gcdas = [(b, g) for b in builds for g in glob.glob(os.path.join(b, "**", "*.gcda"), recursive=True)]
+    for build, gcda in gcdas:
         r = subprocess.run(["gcov", "-n", "-o", os.path.dirname(gcda), gcda], capture_output=True, text=True,
                            cwd=build)
         for m in re.finditer(r"File '([^']+)'\nLines executed:([\d.]+)% of (\d+)", r.stdout):
@@ -47,4 +50,5 @@ def main(build, src):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "src")
+    args = sys.argv[1:]
+    main(args[:-1] if len(args) > 1 else args, args[-1] if len(args) > 1 else "src")
