@@ -423,6 +423,56 @@ TEST(sync_corrupt_ack_is_fatal_without_reconnect) {
   s.stop();
 }
 
+namespace {
+// A shell whose close() takes 600 ms: stop() outlives a short DEVSPACE_SYNC_STOP_WARN_MS.
+class SlowCloseShell : public Shell {
+ public:
+  std::unique_ptr<Shell> inner;
+  int in() override { return inner->in(); }
+  int out() override { return inner->out(); }
+  int err() override { return inner->err(); }
+  bool alive() override { return inner->alive(); }
+  void terminate() override { inner->terminate(); }
+  void close() override {
+    std::this_thread::sleep_for(std::chrono::milliseconds(600));
+    inner->close();
+  }
+};
+
+class SlowCloseTransport : public Transport {
+ public:
+  std::unique_ptr<Shell> open(const std::vector<std::string>& argv) override {
+    auto s = std::make_unique<SlowCloseShell>();
+    s->inner = inner_.open(argv);
+    return s;
+  }
+  std::string describe() const override { return "slow-close(local-shell)"; }
+
+ private:
+  LocalShellTransport inner_;
+};
+}  // namespace
+
+// A stop that takes longer than DEVSPACE_SYNC_STOP_WARN_MS says, in sync.log, where it waits:
+// the step of stop() and the loops still running (the diagnosis a stop that never ends needs).
+TEST(sync_slow_stop_is_logged_with_its_step) {
+  log::logdir() = fs::make_temp_dir("synclogs-");
+  ::setenv("DEVSPACE_SYNC_STOP_WARN_MS", "150", 1);
+  Dirs d;
+  Options o = base_options(d, Mode::Fast);
+  {
+    Session s(o, std::make_shared<SlowCloseTransport>());
+    s.start();
+    EXPECT_TRUE(s.wait_initial_sync(15000));
+    s.stop();
+  }
+  ::unsetenv("DEVSPACE_SYNC_STOP_WARN_MS");
+  std::string text = fs::read_file(fs::join(log::logdir(), "sync-test.log"));
+  EXPECT_TRUE(contains(text, "Stop still waiting after"));
+  EXPECT_TRUE(contains(text, "at 'stop_loops: closing shells'; loops still running: none"));
+  EXPECT_TRUE(contains(text, "Sync stopped"));
+}
+
 // archive entries from the container must never be written outside the synced
 // folder (the reference's untar has the same gap; sync/tar.go:44).
 TEST(sync_downstream_archive_rejects_parent_segments) {
