@@ -83,13 +83,17 @@ __global__ void __launch_bounds__(kBlock) rmsnorm_fwd_kernel(const u16* __restri
   if (row >= R) return;
   const int nvec = D >> 3;
   const u16x8* xr = reinterpret_cast<const u16x8*>(x + (size_t)row * D);
-  u16x8 v[VPL], dv[VPL];
+  const u16x8* wr = reinterpret_cast<const u16x8*>(w);
+  // w is loaded with the row, not after the reduction: the row's loads are its only memory
+  // latency (the weight row is L2-resident, but a load issued after the shuffles still waits)
+  u16x8 v[VPL], dv[VPL], wv[VPL];
 #pragma unroll
   for (int k = 0; k < VPL; ++k) {
     const int i = lane + 64 * k;
     if (i < nvec) {
       v[k] = xr[i];
       if (RES) dv[k] = reinterpret_cast<const u16x8*>(delta + (size_t)row * D)[i];
+      wv[k] = wr[i];
     }
   }
   float ss = 0.f;
@@ -112,15 +116,14 @@ __global__ void __launch_bounds__(kBlock) rmsnorm_fwd_kernel(const u16* __restri
   ss = wave_sum(ss);
   const float r = rsqrtf(ss / (float)D + eps);
   if (lane == 0) rstd[row] = r;
-  const u16x8* wr = reinterpret_cast<const u16x8*>(w);
   u16x8* yr = reinterpret_cast<u16x8*>(y + (size_t)row * D);
 #pragma unroll
   for (int k = 0; k < VPL; ++k) {
     const int i = lane + 64 * k;
     if (i < nvec) {
-      u16x8 wv = wr[i], o;
+      u16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2b(b2f(v[k][j]) * r * b2f(wv[j]));
+      for (int j = 0; j < 8; ++j) o[j] = f2b(b2f(v[k][j]) * r * b2f(wv[k][j]));
       yr[i] = o;
     }
   }
@@ -243,16 +246,17 @@ __global__ void __launch_bounds__(1024) col_sum_kernel(const float* __restrict__
   __shared__ float red[32][33];
   const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
-  float s0 = 0.f, s1 = 0.f;
+  // 8 loads in flight per thread (the reduction is latency-bound: 32 blocks read 2 MB for D = 1024)
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < D) {
     int r = g;
-    for (; r + 32 < nrows; r += 64) {
-      s0 += part[(size_t)r * D + c];
-      s1 += part[(size_t)(r + 32) * D + c];
+    for (; r + 7 * 32 < nrows; r += 8 * 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += part[(size_t)(r + 32 * u) * D + c];
     }
-    for (; r < nrows; r += 32) s0 += part[(size_t)r * D + c];
+    for (; r < nrows; r += 32) s[0] += part[(size_t)r * D + c];
   }
-  red[g][cl] = s0 + s1;
+  red[g][cl] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
   if (threadIdx.x < 32 && c < D) {
     float t = 0.f;
