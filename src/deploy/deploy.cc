@@ -5,6 +5,7 @@
 
 #include "build/docker.h"
 #include "build/image.h"
+#include "core/codec.h"
 #include "core/fs.h"
 #include "core/log.h"
 #include "core/match.h"
@@ -133,14 +134,21 @@ class HelmDeployer : public Deployer {
     helm::Client hc(k_);
     if (const char* mh = std::getenv("DEVSPACE_HELM_MAX_HISTORY")) hc.set_max_history(std::atoi(mh));
     if (!d_.at_path("helm.maxHistory").is_null()) hc.set_max_history((int)d_.at_path("helm.maxHistory").as_int(10));
-    bool redeploy = force || dep.get("helmChartHash").as_string() != hash || override_changed;
+    // The values the chart would get are part of the decision too (the reference's rule,
+    // deploy/helm/deploy.go:64, looks at the chart and override files only): a pull secret
+    // created after the first deploy, or an edit of helm.overrideValues in the config, reaches
+    // the release without a chart edit.
+    Value values = helm_values(cfg_, d_, gen, is_dev);
+    std::string values_hash = sha256_hex(json_dump(values));
+    bool redeploy = force || dep.get("helmChartHash").as_string() != hash || override_changed ||
+                    (dep.has("helmValuesHash") && dep.get("helmValuesHash").as_string() != values_hash);
     if (!redeploy) redeploy = !hc.release_exists(ns, name);
     if (!redeploy) {
+      if (!dep.has("helmValuesHash")) dep["helmValuesHash"] = values_hash;  // (generated.yaml of an older version)
       log::info("Skipping chart " + chart);
       return;
     }
     log::start_wait("Deploying helm chart");
-    Value values = helm_values(cfg_, d_, gen, is_dev);
     bool wait = d_.at_path("helm.wait").as_bool(true);
     int timeout = (int)d_.at_path("helm.timeout").as_int(0);  // 0: helm::Client's default
     helm::Release r;
@@ -153,6 +161,7 @@ class HelmDeployer : public Deployer {
     log::stop_wait();
     log::done("Deployed helm chart (Release revision: " + std::to_string(r.version) + ")");
     dep["helmChartHash"] = hash;
+    dep["helmValuesHash"] = values_hash;
     for (auto& ov : d_.at_path("helm.overrides").items())
       dep["helmOverrideTimestamps"][ov.as_string()] = fs::stat(ov.as_string()).mtime_sec;
   }

@@ -509,3 +509,76 @@ def test_analyze_reports_crash_loop_with_gpu_runtime_error(localkube):
     assert "failed with a ROCm/HIP/RCCL error: HIP error" in out, out
     assert "the pod requests no amd.com/gpu" in out, out  # the likely cause, named
     lk.run(["purge"], proj)
+
+
+def test_create_pull_secret_from_docker_credentials(localkube):
+    """images.*.createPullSecret (/root/reference/pkg/devspace/registry/init.go:24-84): with
+    credentials for the image's registry in the Docker config, `devspace deploy` creates a
+    kubernetes.io/dockerconfigjson secret `devspace-auth-<registry>` in the deployment's
+    namespace, the chart's pods get it as an imagePullSecret, and a later deploy with new
+    credentials updates the secret in place. Without credentials no secret is written.
+    A secret created after the first deploy reaches the release: the redeploy decision includes
+    the chart's computed values (the reference's looks at the chart and override files only,
+    deploy/helm/deploy.go:64), so does an edit of helm.overrideValues."""
+    import base64
+    import json
+
+    lk = localkube
+    proj = lk.project("quickstart", "quickstart-pullsecret")
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = open(cfg_path).read().replace("namespace: quickstart", "namespace: qs-pull")
+    cfg = cfg.replace("    image: devspace-local/quickstart", "    image: devspace-local/quickstart\n    createPullSecret: true")
+    assert "createPullSecret: true" in cfg
+    open(cfg_path, "w").write(cfg)
+    dcfg = os.path.join(lk.base, "dockercfg-pull")
+    os.makedirs(dcfg, exist_ok=True)
+
+    def creds(user, pw):
+        auth = base64.b64encode(f"{user}:{pw}".encode()).decode()
+        with open(os.path.join(dcfg, "config.json"), "w") as f:
+            json.dump({"auths": {"https://index.docker.io/v1/": {"auth": auth}}}, f)
+
+    def secret_auth():
+        secrets = [s for s in lk.cluster.store.list("", "secrets", "qs-pull")
+                   if s["metadata"]["name"] == "devspace-auth-docker"]
+        if not secrets:
+            return None
+        assert secrets[0]["type"] == "kubernetes.io/dockerconfigjson"
+        doc = json.loads(base64.b64decode(secrets[0]["data"][".dockerconfigjson"]))
+        (entry,) = doc["auths"].values()
+        return base64.b64decode(entry["auth"]).decode()
+
+    saved = dict(lk.env)
+    try:
+        lk.env["DOCKER_CONFIG"] = dcfg
+        os.makedirs(os.path.join(dcfg, "empty"), exist_ok=True)
+        with open(os.path.join(dcfg, "config.json"), "w") as f:
+            json.dump({"auths": {}}, f)
+        lk.run(["deploy"], proj)
+        assert secret_auth() is None  # no credentials for Docker Hub: nothing to write
+
+        creds("alice", "s3cret")
+        out = lk.run(["deploy"], proj).stdout
+        assert "Successfully deployed!" in out
+        assert secret_auth() == "alice:s3cret"
+        dep = lk.cluster.store.list("apps", "deployments", "qs-pull")[0]
+        assert {"name": "devspace-auth-docker"} in dep["spec"]["template"]["spec"]["imagePullSecrets"]
+
+        creds("alice", "rotated")
+        out = lk.run(["deploy"], proj).stdout
+        assert secret_auth() == "alice:rotated"
+        assert "Skipping chart" in out  # same secret name, same values: the release stays
+
+        # an edit of helm.overrideValues in the config reaches the release without a chart edit
+        cfg = open(cfg_path).read().replace("chartPath: ./chart",
+                                            "chartPath: ./chart\n    overrideValues:\n      pullSecrets:\n      - team-registry", 1)
+        open(cfg_path, "w").write(cfg)
+        out = lk.run(["deploy"], proj).stdout
+        assert "Skipping chart" not in out, out
+        dep = lk.cluster.store.list("apps", "deployments", "qs-pull")[0]
+        names = [s["name"] for s in dep["spec"]["template"]["spec"]["imagePullSecrets"]]
+        assert names == ["team-registry", "devspace-auth-docker"], names
+    finally:
+        lk.env.clear()
+        lk.env.update(saved)
+        lk.run(["purge"], proj, check=False)
