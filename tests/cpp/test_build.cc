@@ -2,7 +2,10 @@
 // Dockerfile entrypoint override, image name helpers.
 #include <unistd.h>
 
+#include <map>
+
 #include "build/docker.h"
+#include "core/codec.h"
 #include "core/fs.h"
 #include "core/strutil.h"
 #include "testing.h"
@@ -59,4 +62,51 @@ TEST(dockerfile_ports_like_get_ports) {
   EXPECT_EQ(p[1], 8080);
   EXPECT_EQ(p[2], 9229);
   EXPECT_THROWS(build::dockerfile_ports("EXPOSE $PORT\n"));
+}
+
+// The build context as the daemon receives it (archive.TarWithOptions in the reference,
+// pkg/devspace/builder/docker/docker.go:96-140): .dockerignore rules with a "!" exception, a
+// symlink kept as a symlink (never followed), ownership reset to 0:0, and the Dockerfile
+// replaced by the override (the entrypoint rewrite of `devspace dev`) when one is given.
+TEST(build_context_archive_keeps_symlinks_and_applies_dockerignore) {
+  std::string d = fs::make_temp_dir("ctx-");
+  fs::write_file(fs::join(d, "app.js"), "console.log(1)\n");
+  fs::write_file(fs::join(d, "lib/util.js"), "module.exports = 2\n");
+  fs::write_file(fs::join(d, "debug.log"), "noise");
+  fs::write_file(fs::join(d, "logs/keep.log"), "kept by the exception");
+  fs::write_file(fs::join(d, "Dockerfile"), "FROM node\nCMD [\"node\", \"app.js\"]\n");
+  fs::write_file(fs::join(d, ".dockerignore"), "*.log\n**/*.log\n!logs/keep.log\n");
+  EXPECT_EQ(::symlink("app.js", fs::join(d, "current.js").c_str()), 0);
+  std::vector<std::string> ex = {"*.log", "**/*.log", "!logs/keep.log"};
+  std::string override_df = "FROM node\nENTRYPOINT [\"sleep\", \"999\"]\n";
+  std::string tar = build::context_tar(d, ex, "Dockerfile", override_df);
+  TarReader tr(string_source(&tar));
+  std::map<std::string, TarEntry> got;
+  std::map<std::string, std::string> data;
+  TarEntry e;
+  while (tr.next(&e)) {
+    got[e.name] = e;
+    data[e.name] = tr.read_all();
+  }
+  EXPECT_TRUE(got.count("app.js") && got.count("lib/util.js") && got.count(".dockerignore"));
+  EXPECT_TRUE(!got.count("debug.log"));
+  EXPECT_TRUE(got.count("logs/keep.log"));
+  EXPECT_EQ(data["logs/keep.log"], std::string("kept by the exception"));
+  EXPECT_TRUE(got.count("current.js"));
+  EXPECT_EQ(got["current.js"].type, '2');
+  EXPECT_EQ(got["current.js"].linkname, std::string("app.js"));
+  EXPECT_EQ(got["current.js"].size, (int64_t)0);
+  EXPECT_EQ(data["Dockerfile"], override_df);
+  EXPECT_EQ((int)got["Dockerfile"].mode, 0600);
+  for (auto& kv : got) EXPECT_TRUE(kv.second.uid == 0 && kv.second.gid == 0);
+  // no override: the Dockerfile goes in as it is on disk
+  std::string plain = build::context_tar(d, ex, "Dockerfile", std::nullopt);
+  TarReader tr2(string_source(&plain));
+  std::string df;
+  while (tr2.next(&e)) {
+    std::string body = tr2.read_all();
+    if (e.name == "Dockerfile") df = body;
+  }
+  EXPECT_EQ(df, fs::read_file(fs::join(d, "Dockerfile")));
+  fs::remove_all(d);
 }

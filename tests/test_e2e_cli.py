@@ -582,3 +582,49 @@ def test_create_pull_secret_from_docker_credentials(localkube):
         lk.env.clear()
         lk.env.update(saved)
         lk.run(["purge"], proj, check=False)
+
+
+def test_pull_secret_credentials_from_a_credential_helper(localkube):
+    """Docker credential helpers (`credsStore` / `credHelpers` in the Docker config, the
+    docker-credential-<name> protocol: the server URL on stdin of `get`, JSON with Username and
+    Secret on stdout) feed createPullSecret the same way stored auths do
+    (/root/reference/pkg/devspace/docker/auth.go via the Docker CLI config)."""
+    import base64
+    import json
+    import stat
+
+    lk = localkube
+    proj = lk.project("quickstart", "quickstart-credhelper")
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = open(cfg_path).read().replace("namespace: quickstart", "namespace: qs-helper")
+    cfg = cfg.replace("    image: devspace-local/quickstart", "    image: devspace-local/quickstart\n    createPullSecret: true")
+    open(cfg_path, "w").write(cfg)
+    dcfg = os.path.join(lk.base, "dockercfg-helper")
+    bindir = os.path.join(lk.base, "credhelper-bin")
+    os.makedirs(dcfg, exist_ok=True)
+    os.makedirs(bindir, exist_ok=True)
+    seen = os.path.join(lk.base, "credhelper-seen.txt")
+    helper = os.path.join(bindir, "docker-credential-fake")
+    with open(helper, "w") as f:
+        f.write("#!/bin/sh\n"
+                "[ \"$1\" = get ] || exit 1\n"
+                f"cat > {seen}\n"
+                "printf '{\"ServerURL\":\"https://index.docker.io/v1/\",\"Username\":\"carol\",\"Secret\":\"from-helper\"}'\n")
+    os.chmod(helper, os.stat(helper).st_mode | stat.S_IEXEC)
+    with open(os.path.join(dcfg, "config.json"), "w") as f:
+        json.dump({"auths": {}, "credsStore": "fake"}, f)
+    saved = dict(lk.env)
+    try:
+        lk.env["DOCKER_CONFIG"] = dcfg
+        lk.env["PATH"] = bindir + os.pathsep + lk.env.get("PATH", "")
+        lk.run(["deploy"], proj)
+        assert "index.docker.io" in open(seen).read()
+        (secret,) = [s for s in lk.cluster.store.list("", "secrets", "qs-helper")
+                     if s["metadata"]["name"] == "devspace-auth-docker"]
+        doc = json.loads(base64.b64decode(secret["data"][".dockerconfigjson"]))
+        (entry,) = doc["auths"].values()
+        assert base64.b64decode(entry["auth"]).decode() == "carol:from-helper"
+    finally:
+        lk.env.clear()
+        lk.env.update(saved)
+        lk.run(["purge"], proj, check=False)
