@@ -81,6 +81,61 @@ TEST(kubeconfig_resolve_inline_credentials) {
   fs::remove_all(d);
 }
 
+// The other ways a kubeconfig names credentials (client-go's clientcmd): a token file and
+// certificate files relative to the kubeconfig's directory, the cached token of a legacy
+// auth-provider (oidc id-token, else gcp access-token), basic auth, and an exec plugin whose
+// relative command is resolved against the kubeconfig's directory.
+TEST(kubeconfig_resolve_files_auth_providers_and_exec) {
+  std::string d = fs::make_temp_dir("kc-");
+  std::string path = fs::join(d, "config");
+  fs::write_file(fs::join(d, "sa/token"), "tok-from-file\n");
+  fs::write_file(fs::join(d, "pki/ca.crt"), "CA-FILE");
+  fs::write_file(fs::join(d, "pki/me.crt"), "CERT-FILE");
+  fs::write_file(fs::join(d, "pki/me.key"), "KEY-FILE");
+  fs::write_file(path,
+                 "apiVersion: v1\nkind: Config\ncurrent-context: files\nclusters:\n"
+                 "- name: c\n  cluster:\n    server: https://k8s.example:6443\n    certificate-authority: pki/ca.crt\n"
+                 "    tls-server-name: api.internal\n    proxy-url: http://proxy:3128\n"
+                 "contexts:\n- name: files\n  context: {cluster: c, user: files}\n"
+                 "- name: oidc\n  context: {cluster: c, user: oidc}\n"
+                 "- name: gcp\n  context: {cluster: c, user: gcp}\n"
+                 "- name: basic\n  context: {cluster: c, user: basic}\n"
+                 "- name: plugin\n  context: {cluster: c, user: plugin}\n"
+                 "users:\n"
+                 "- name: files\n  user:\n    tokenFile: sa/token\n    client-certificate: pki/me.crt\n"
+                 "    client-key: pki/me.key\n"
+                 "- name: oidc\n  user:\n    auth-provider:\n      name: oidc\n      config: {id-token: id-tok, "
+                 "refresh-token: r}\n"
+                 "- name: gcp\n  user:\n    auth-provider:\n      name: gcp\n      config: {access-token: acc-tok}\n"
+                 "- name: basic\n  user: {username: admin, password: pw}\n"
+                 "- name: plugin\n  user:\n    exec:\n      apiVersion: client.authentication.k8s.io/v1\n"
+                 "      command: bin/get-token\n      args: [--cluster, c]\n      env: [{name: REGION, value: eu}]\n"
+                 "      provideClusterInfo: true\n      installHint: install get-token\n");
+  kube::KubeConfig kc = kube::KubeConfig::load(path);
+  kube::RestConfig f = kc.resolve();
+  EXPECT_EQ(f.token, std::string("tok-from-file"));
+  EXPECT_EQ(f.token_file, fs::join(d, "sa/token"));
+  EXPECT_EQ(f.ca_pem, std::string("CA-FILE"));
+  EXPECT_EQ(f.client_cert_pem, std::string("CERT-FILE"));
+  EXPECT_EQ(f.client_key_pem, std::string("KEY-FILE"));
+  EXPECT_EQ(f.tls_server_name, std::string("api.internal"));
+  EXPECT_EQ(f.proxy_url, std::string("http://proxy:3128"));
+  EXPECT_EQ(kc.resolve("oidc").token, std::string("id-tok"));
+  EXPECT_EQ(kc.resolve("gcp").token, std::string("acc-tok"));
+  kube::RestConfig b = kc.resolve("basic");
+  EXPECT_TRUE(b.username == "admin" && b.password == "pw" && b.token.empty());
+  kube::RestConfig p = kc.resolve("plugin");
+  EXPECT_EQ(p.exec_command.size(), (size_t)3);
+  EXPECT_EQ(p.exec_command[0], fs::join(d, "bin/get-token"));
+  EXPECT_EQ(p.exec_command[2], std::string("c"));
+  EXPECT_EQ(p.exec_env.size(), (size_t)1);
+  EXPECT_TRUE(p.exec_env[0].first == "REGION" && p.exec_env[0].second == "eu");
+  EXPECT_EQ(p.exec_api_version, std::string("client.authentication.k8s.io/v1"));
+  EXPECT_TRUE(p.exec_provide_cluster_info);
+  EXPECT_EQ(p.exec_install_hint, std::string("install get-token"));
+  fs::remove_all(d);
+}
+
 TEST(analyze_gpu_runtime_log_matcher) {
   std::string m;
   EXPECT_TRUE(analyze::log_has_gpu_runtime_error("RuntimeError: No HIP GPUs are available", &m));
