@@ -224,12 +224,13 @@ void Client::refresh_exec_credentials() {
   refreshes_++;
 }
 
-void Client::ensure_fresh_credentials() {
+uint64_t Client::ensure_fresh_credentials() {
   std::lock_guard<std::mutex> g(auth_mu_);
   int64_t now = unix_now();
   if (!cfg_.exec_command.empty() && token_expiry_ > 0 && now >= token_expiry_ - 1) {
     refresh_exec_credentials();
     apply_auth_locked();
+    ++auth_gen_;
   }
   if (!cfg_.token_file.empty() && now - token_file_read_ >= 60) {
     std::string t;
@@ -237,23 +238,31 @@ void Client::ensure_fresh_credentials() {
     if (fs::read_file(cfg_.token_file, &t) && !trim(t).empty() && trim(t) != cfg_.token) {
       cfg_.token = trim(t);
       apply_auth_locked();
+      ++auth_gen_;
     }
   }
+  return auth_gen_;
 }
 
-bool Client::refresh_after_unauthorized() {
+bool Client::refresh_after_unauthorized(uint64_t used_generation) {
   std::lock_guard<std::mutex> g(auth_mu_);
+  // Requests running at once all get a 401 when a token is revoked: the first one refreshes,
+  // the others are sent again with what it got (instead of failing on "nothing new in the
+  // token file", or running the exec plugin once each).
+  if (auth_gen_ != used_generation) return true;
   if (!cfg_.exec_command.empty()) {
     refresh_exec_credentials();
     apply_auth_locked();
+    ++auth_gen_;
     return true;
   }
   if (!cfg_.token_file.empty()) {
     std::string t;
     token_file_read_ = unix_now();
-    if (fs::read_file(cfg_.token_file, &t) && trim(t) != cfg_.token) {
+    if (fs::read_file(cfg_.token_file, &t) && !trim(t).empty() && trim(t) != cfg_.token) {
       cfg_.token = trim(t);
       apply_auth_locked();
+      ++auth_gen_;
       return true;
     }
   }
@@ -340,9 +349,9 @@ net::Response Client::raw(const std::string& method, const std::string& path, co
   // order and how long each took, so round trips on a slow link can be counted
   trace::Span span("api.request", {{"method", method}, {"path", path.substr(0, path.find('?'))}});
   for (int attempt = 1;; ++attempt) {
-    ensure_fresh_credentials();
+    uint64_t gen = ensure_fresh_credentials();
     net::Response resp = http_.request(r);
-    if (resp.status == 401 && refresh_after_unauthorized()) resp = http_.request(r);
+    if (resp.status == 401 && refresh_after_unauthorized(gen)) resp = http_.request(r);
     int wait = retry_wait_ms(resp.status, resp.header("retry-after"), method);
     span.set("status", std::to_string(resp.status));
     if (attempt > 1) span.set("attempts", std::to_string(attempt));
@@ -398,9 +407,9 @@ int Client::stream(const std::string& path, const std::function<bool(const std::
   r.timeout_ms = timeout_ms;
   r.errors_to_body = true;
   for (int attempt = 1;; ++attempt) {
-    ensure_fresh_credentials();
+    uint64_t gen = ensure_fresh_credentials();
     net::Response resp = http_.stream(r, on_data);  // error bodies never reach on_data
-    if (resp.status == 401 && refresh_after_unauthorized()) resp = http_.stream(r, on_data);
+    if (resp.status == 401 && refresh_after_unauthorized(gen)) resp = http_.stream(r, on_data);
     int wait = retry_wait_ms(resp.status, resp.header("retry-after"), "GET");
     if (wait >= 0 && attempt <= kMaxApiRetries) {
       throttled("GET " + path, resp.status, wait, attempt);
@@ -899,11 +908,11 @@ std::unique_ptr<net::WebSocket> Client::ws_connect(const std::string& path, cons
   if (!spare) spare = take_prewarmed();
   trace::Span span("api.upgrade", {{"path", path.substr(0, path.find('?'))}, {"predialed", spare ? "1" : "0"}});
   for (int attempt = 1;; ++attempt) {
-    ensure_fresh_credentials();
+    uint64_t gen = ensure_fresh_credentials();
     try {
       return net::WebSocket::connect(http_, path, protocols, 30000, std::move(spare));
     } catch (const net::UpgradeError& e) {
-      if (e.status == 401 && !refreshed && refresh_after_unauthorized()) {
+      if (e.status == 401 && !refreshed && refresh_after_unauthorized(gen)) {
         refreshed = true;
         continue;
       }

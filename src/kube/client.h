@@ -164,9 +164,12 @@ class Client {
   void prewarm_upgrades(int n);
   ~Client();
 
-  // Credential refresh (exec plugins: on expiry and on 401; tokenFile: every minute).
-  void ensure_fresh_credentials();
-  bool refresh_after_unauthorized();
+  // Credential refresh (exec plugins: on expiry and on 401; tokenFile: every minute and on 401).
+  // ensure_fresh_credentials() returns the credentials' generation a request is about to use;
+  // after a 401, refresh_after_unauthorized(that generation) is true when the request should be
+  // sent again: another thread already replaced those credentials, or this call did.
+  uint64_t ensure_fresh_credentials();
+  bool refresh_after_unauthorized(uint64_t used_generation);
   int credential_refreshes() const { return refreshes_; }
   // Requests sent again after a 429 / 5xx + Retry-After (all verbs, all streams).
   int throttle_retries() const { return throttle_retries_; }
@@ -195,6 +198,7 @@ class Client {
   int64_t token_expiry_ = 0;      // unix seconds, 0 = no expiry
   int64_t token_file_read_ = 0;   // unix seconds of the last tokenFile read
   std::atomic<int> refreshes_{0};
+  uint64_t auth_gen_ = 0;  // bumped whenever the credentials change (under auth_mu_)
   std::atomic<int> throttle_retries_{0};
 };
 

@@ -16,6 +16,7 @@
 
 #include "core/net.h"
 #include "core/resolve.h"
+#include "core/fs.h"
 #include "core/strutil.h"
 #include "deploy/sprig_crypto.h"
 #include "kube/client.h"
@@ -424,4 +425,47 @@ TEST(api_client_waits_retry_after) {
   c.get("/api/v1/namespaces/x/pods/p");
   auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
   EXPECT_TRUE(ms >= 950 && ms < 3000);
+}
+
+// A tokenFile rotated under running requests (a projected service-account token): the request
+// that gets the first 401 reads the file again and is sent again; the others, which also went
+// out with the revoked token, are sent again with what it read instead of failing on "nothing
+// new in the token file". Only a 401 with the current credentials is final.
+TEST(api_client_token_file_rotation_under_concurrent_requests) {
+  std::string d = fs::make_temp_dir("tokfile-");
+  std::string tf = fs::join(d, "token");
+  fs::write_file(tf, "old\n");
+  std::atomic<int> unauthorized{0};
+  ScriptedServer srv([&](int fd, int) {
+    std::string body;
+    while (true) {
+      std::string head = read_request(fd, &body);
+      if (head.empty()) return;
+      if (head.find("Authorization: Bearer new") == std::string::npos) {
+        unauthorized++;
+        respond_status(fd, 401, "");
+      } else {
+        respond(fd, "{\"kind\":\"Pod\"}");
+      }
+    }
+  });
+  kube::RestConfig rc;
+  rc.server = srv.url();
+  rc.token = "old";
+  rc.token_file = tf;
+  {
+    kube::Client c(rc);
+    uint64_t used = c.ensure_fresh_credentials();  // two requests go out with "old"
+    fs::write_file(tf, "new\n");                     // the kubelet rotates the token
+    EXPECT_TRUE(c.refresh_after_unauthorized(used));  // the first 401: the file has a new token
+    EXPECT_TRUE(c.refresh_after_unauthorized(used));  // the second: already replaced, send again
+    EXPECT_TRUE(!c.refresh_after_unauthorized(c.ensure_fresh_credentials()));  // current and refused
+    EXPECT_EQ(c.get("/api/v1/namespaces/x/pods/p").get("kind").as_string(), std::string("Pod"));
+  }  // (the scripted server serves one kept-alive connection at a time)
+  // a client that still holds the old token: its first request gets a 401, reads the file, retries
+  kube::Client c2(rc);
+  int before = unauthorized.load();
+  EXPECT_EQ(c2.get("/api/v1/namespaces/x/pods/p").get("kind").as_string(), std::string("Pod"));
+  EXPECT_EQ(unauthorized.load(), before + 1);
+  fs::remove_all(d);
 }

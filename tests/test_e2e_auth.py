@@ -121,6 +121,56 @@ def test_token_expires_mid_dev_and_sync_reconnects(tmp_path):
         cluster.stop()
 
 
+def test_token_file_rotated_mid_dev_is_read_again(tmp_path):
+    """A kubeconfig `tokenFile` (a projected service-account token, rotated by the kubelet):
+    when the file gets a new token and the old one is revoked mid-`dev`, the next request that
+    gets a 401 reads the file again and goes on, as client-go's cached token source does; the
+    sync reconnects into the replacement pod with the new token."""
+    from devspace_amd.localkube import LocalCluster
+
+    policy = TokenPolicy()
+    cluster = LocalCluster(str(tmp_path / "state"), gpus=0, token_validator=policy).start()
+    lk = DevspaceEnv(cluster, str(tmp_path))
+    token = tmp_path / "sa-token"
+    token.write_text("tok-0-1\n")
+    kc = yaml.safe_load(open(lk.kubeconfig))
+    kc["users"][0]["user"] = {"tokenFile": str(token)}
+    open(lk.kubeconfig, "w").write(yaml.safe_dump(kc))
+    dev = None
+    try:
+        proj = lk.project("quickstart", "qs-tokenfile")
+        dev = lk.popen(["dev", "--terminal=false", "--portforwarding=false"], proj)
+        pods = wait_for(lambda: running(lk.pods("quickstart")), timeout=60, what="dev pod")
+        root = container_root(lk, pods[0])
+        wait_for(lambda: os.path.exists(os.path.join(root, "app", "index.js")), timeout=30, what="initial sync")
+        first = pods[0]["metadata"]["name"]
+        failures = cluster.api.auth_failures
+        token.write_text("tok-0-2\n")  # rotated; the old token stops working at once
+        policy.revoked_upto = 1
+        cluster.store.mark_deleting("", "pods", "quickstart", first)
+        new = wait_for(lambda: [p for p in running(lk.pods("quickstart")) if p["metadata"]["name"] != first],
+                       timeout=60, what="replacement pod")[0]
+        new_root = container_root(lk, new)
+        with open(os.path.join(proj, "index.js"), "a") as f:
+            f.write("// after token rotation\n")
+        wait_for(lambda: os.path.exists(os.path.join(new_root, "app", "index.js")) and
+                 "// after token rotation" in open(os.path.join(new_root, "app", "index.js")).read(),
+                 timeout=60, what="sync into the replacement pod")
+        assert cluster.api.auth_failures > failures  # the old token was refused, then replaced
+    finally:
+        if dev is not None:
+            os.killpg(dev.pid, signal.SIGINT)
+            try:
+                out, _ = dev.communicate(timeout=30)
+                print(out[-4000:])
+            except Exception:
+                os.killpg(dev.pid, signal.SIGKILL)
+            log = os.path.join(proj, ".devspace", "logs", "sync.log")
+            if os.path.exists(log):
+                print(open(log).read()[-4000:])
+        cluster.stop()
+
+
 class ConnectProxy(threading.Thread):
     """Minimal HTTP CONNECT proxy (what HTTPS_PROXY points at in corporate networks)."""
 
