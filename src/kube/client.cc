@@ -472,6 +472,38 @@ bool Client::list_watch(const std::string& collection, const std::string& query,
                          std::to_string(secs) + (rv.empty() ? "" : "&resourceVersion=" + rv);
       std::string buf;
       bool satisfied = false, bad = false;
+      // one event line; false once the watch is over for this round
+      auto on_line = [&](const std::string& line) {
+        Value ev;
+        try {
+          ev = json_parse(line);
+        } catch (...) {
+          bad = true;
+          return false;
+        }
+        std::string type = ev.get("type").as_string();
+        const Value& obj = ev.get("object");
+        if (type.empty() || !obj.is_map()) {  // not a watch stream: server ignored watch=1
+          bad = true;
+          return false;
+        }
+        if (type == "ERROR") {
+          relist = true;  // 410 Gone (resourceVersion too old) or other: start over
+          return false;
+        }
+        std::string orv = obj.at_path("metadata.resourceVersion").as_string();
+        if (!orv.empty()) rv = orv;
+        if (type == "BOOKMARK") return true;
+        if (type == "DELETED")
+          objs.erase(key_of(obj));
+        else
+          objs[key_of(obj)] = obj;
+        if (done(snapshot())) {
+          satisfied = true;
+          return false;
+        }
+        return true;
+      };
       try {
         stream(path, [&](const std::string& chunk) {
           buf += chunk;
@@ -479,38 +511,14 @@ bool Client::list_watch(const std::string& collection, const std::string& query,
           while ((nl = buf.find('\n')) != std::string::npos) {
             std::string line = trim(buf.substr(0, nl));
             buf.erase(0, nl + 1);
-            if (line.empty()) continue;
-            Value ev;
-            try {
-              ev = json_parse(line);
-            } catch (...) {
-              bad = true;
-              return false;
-            }
-            std::string type = ev.get("type").as_string();
-            const Value& obj = ev.get("object");
-            if (type.empty() || !obj.is_map()) {  // not a watch stream: server ignored watch=1
-              bad = true;
-              return false;
-            }
-            if (type == "ERROR") {
-              relist = true;  // 410 Gone (resourceVersion too old) or other: start over
-              return false;
-            }
-            std::string orv = obj.at_path("metadata.resourceVersion").as_string();
-            if (!orv.empty()) rv = orv;
-            if (type == "BOOKMARK") continue;
-            if (type == "DELETED")
-              objs.erase(key_of(obj));
-            else
-              objs[key_of(obj)] = obj;
-            if (done(snapshot())) {
-              satisfied = true;
-              return false;
-            }
+            if (!line.empty() && !on_line(line)) return false;
           }
           return left_ms() > 0;
         }, (int)std::min<int64_t>(left + 5000, INT32_MAX));
+        // what came after the last newline: an event without one, or (from a server that
+        // ignores watch=1) a whole list, which would otherwise be re-watched until the deadline
+        std::string rest = trim(buf);
+        if (!satisfied && !relist && !bad && !rest.empty()) on_line(rest);
       } catch (const ApiError& e) {
         if (e.code == 410) {
           relist = true;

@@ -469,3 +469,69 @@ TEST(api_client_token_file_rotation_under_concurrent_requests) {
   EXPECT_EQ(unauthorized.load(), before + 1);
   fs::remove_all(d);
 }
+
+// list + watch against servers that do not play along (client-go's reflector rules): a watch
+// that ends in an ERROR event (410 Gone: the resourceVersion is too old) starts over from a
+// fresh list; a server that ignores watch=1 and answers with a list is polled instead.
+TEST(api_client_list_watch_relists_after_gone_and_polls_without_watch) {
+  const std::string pod =
+      "{\"metadata\":{\"name\":\"p\",\"namespace\":\"x\",\"resourceVersion\":\"7\","
+      "\"creationTimestamp\":\"2026-01-01T00:00:00Z\"},\"status\":{\"phase\":\"Running\"}}";
+  {
+    std::vector<std::string> heads;
+    std::mutex mu;
+    int lists = 0;
+    ScriptedServer srv([&](int fd, int) {
+      std::string body;
+      while (true) {
+        std::string head = read_request(fd, &body);
+        if (head.empty()) return;
+        {
+          std::lock_guard<std::mutex> g(mu);
+          heads.push_back(head.substr(0, head.find("\r\n")));
+        }
+        if (head.find("watch=1") != std::string::npos)
+          respond(fd, "{\"type\":\"ERROR\",\"object\":{\"kind\":\"Status\",\"code\":410,\"reason\":\"Expired\"}}\n");
+        else if (lists++ == 0)
+          respond(fd, "{\"kind\":\"PodList\",\"metadata\":{\"resourceVersion\":\"5\"},\"items\":[]}");
+        else
+          respond(fd, "{\"kind\":\"PodList\",\"metadata\":{\"resourceVersion\":\"7\"},\"items\":[" + pod + "]}");
+      }
+    });
+    kube::RestConfig rc;
+    rc.server = srv.url();
+    kube::Client c(rc);
+    bool ok = c.list_watch("/api/v1/namespaces/x/pods", "", 10000,
+                           [](const std::vector<Value>& ps) { return !ps.empty(); });
+    EXPECT_TRUE(ok);
+    std::lock_guard<std::mutex> g(mu);
+    EXPECT_EQ(heads.size(), (size_t)3);
+    EXPECT_TRUE(heads.size() == 3 && heads[1].find("watch=1") != std::string::npos &&
+                heads[1].find("resourceVersion=5") != std::string::npos);
+    EXPECT_TRUE(heads.size() == 3 && heads[2].find("watch=1") == std::string::npos);
+  }
+  {
+    std::atomic<int> lists{0}, watches{0};
+    ScriptedServer srv([&](int fd, int) {
+      std::string body;
+      while (true) {
+        std::string head = read_request(fd, &body);
+        if (head.empty()) return;
+        bool w = head.find("watch=1") != std::string::npos;
+        (w ? watches : lists)++;
+        // an old or odd server: every GET gets the plain list
+        bool ready = lists.load() >= 3;
+        respond(fd, std::string("{\"kind\":\"PodList\",\"metadata\":{\"resourceVersion\":\"5\"},\"items\":[") +
+                        (ready ? pod : "") + "]}");
+      }
+    });
+    kube::RestConfig rc;
+    rc.server = srv.url();
+    kube::Client c(rc);
+    bool ok = c.list_watch("/api/v1/namespaces/x/pods", "", 10000,
+                           [](const std::vector<Value>& ps) { return !ps.empty(); });
+    EXPECT_TRUE(ok);
+    EXPECT_EQ(watches.load(), 1);  // tried once, then polled
+    EXPECT_TRUE(lists.load() >= 3);
+  }
+}
