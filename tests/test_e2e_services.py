@@ -468,3 +468,48 @@ def test_port_forward_hold_delivers_a_held_request_once(localkube, tmp_path, tun
         assert all(s.get("via") == "websocket" for s in spans), spans
         assert any(s.get("preopened") == "1" for s in spans), spans
     lk.run(["purge"], proj)
+
+
+def test_enter_and_logs_target_flags(localkube):
+    """`enter` / `logs` target flags (/root/reference/cmd/enter.go, cmd/logs.go): --namespace,
+    --label-selector and --container pick the pod and container instead of the config's
+    selector (the config's namespace is another one here); a container the pod does not have is
+    an error naming it; with two running replicas the non-interactive choice is one of them, and
+    the command runs there."""
+    lk = localkube
+    proj = lk.project("quickstart", "quickstart-targets")
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    cfg["cluster"]["namespace"] = "targets"
+    open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    values_path = os.path.join(proj, "chart", "values.yaml")
+    values = yaml.safe_load(open(values_path))
+    values["components"][0]["replicas"] = 2
+    open(values_path, "w").write(yaml.safe_dump(values))
+    try:
+        lk.run(["deploy"], proj)
+        pods = wait_for(lambda: len(running(lk.pods("targets"))) == 2 and running(lk.pods("targets")), timeout=60,
+                        what="two replicas")
+        names = {p["metadata"]["name"] for p in pods}
+        container = pods[0]["spec"]["containers"][0]["name"]
+        cfg["cluster"]["namespace"] = "default"  # the flags name the namespace from here on
+        open(cfg_path, "w").write(yaml.safe_dump(cfg))
+        elsewhere = proj
+        out = lk.run(["enter", "-n", "targets", "--label-selector", "app.kubernetes.io/name=devspace-app",
+                      "--container", container, "--", "sh", "-c", "echo host=$HOSTNAME"], elsewhere).stdout
+        host = re.search(r"host=(\S+)", out)
+        assert host and host.group(1) in names, out
+        logs = wait_for(lambda: "listening" in lk.run(["logs", "-n", "targets", "--label-selector",
+                                                        "app.kubernetes.io/name=devspace-app"], elsewhere,
+                                                       check=False).stdout, what="logs by label selector")
+        assert logs
+        cfg["cluster"]["namespace"] = "targets"
+        open(cfg_path, "w").write(yaml.safe_dump(cfg))
+        out = lk.run(["enter", "--container", container, "--", "cat", "package.json"], proj).stdout
+        assert '"name": "quickstart"' in out
+        bad = lk.run(["enter", "--container", "no-such-container", "--", "true"], proj, check=False)
+        assert bad.returncode != 0 and "no-such-container" in (bad.stdout + bad.stderr), bad.stdout + bad.stderr
+    finally:
+        cfg["cluster"]["namespace"] = "targets"
+        open(cfg_path, "w").write(yaml.safe_dump(cfg))
+        lk.run(["purge"], proj, check=False)
