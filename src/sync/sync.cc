@@ -1688,6 +1688,10 @@ std::vector<FileInfo> Session::collect_changes(std::map<std::string, FileInfo>* 
           std::string more;
           while (!down_out_.read_line(&more, 200)) {
             if (down_out_.eof()) throw SyncError("\n[Downstream] Stream closed unexpectedly");
+            // (a stream that stops inside a line: the stop and the scan deadline still apply;
+            // without them a stop waited here for ever, seen by the stop watchdog)
+            if (stopping_) throw SyncError("sync stopped");
+            if (mono_us() > deadline) throw SyncError("downstream: scan timeout");
             std::string r2 = down_out_.take_buffer();
             rest += r2;
             if (rest == kDone || rest == kError) break;
