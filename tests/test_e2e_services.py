@@ -513,3 +513,48 @@ def test_enter_and_logs_target_flags(localkube):
         cfg["cluster"]["namespace"] = "targets"
         open(cfg_path, "w").write(yaml.safe_dump(cfg))
         lk.run(["purge"], proj, check=False)
+
+
+def test_sync_bandwidth_limits(localkube):
+    """dev.sync[].bandwidthLimits (KB/s each way; /root/reference/pkg/devspace/services/sync.go:
+    119-127, token buckets with a one-second burst): 1 MiB of incompressible data takes about
+    four seconds each way at 200 KB/s, where the unlimited sync takes a fraction of one."""
+    from test_e2e_cli import container_root
+
+    lk = localkube
+    proj = lk.project("quickstart", "quickstart-bwlimit")
+    cfg_path = os.path.join(proj, ".devspace", "config.yaml")
+    cfg = yaml.safe_load(open(cfg_path))
+    cfg["cluster"]["namespace"] = "bwlimit"
+    cfg["dev"]["sync"][0]["bandwidthLimits"] = {"upload": 200, "download": 200}
+    open(cfg_path, "w").write(yaml.safe_dump(cfg))
+    dev = lk.popen(["dev", "--terminal=false", "--portforwarding=false"], proj)
+    try:
+        pods = wait_for(lambda: running(lk.pods("bwlimit")), timeout=60, what="dev pod")
+        root = os.path.join(container_root(lk, pods[0]), "app")
+        wait_for(lambda: os.path.exists(os.path.join(root, "index.js")), timeout=30, what="initial sync")
+        blob = os.urandom(1 << 20)
+        t0 = time.monotonic()
+        with open(os.path.join(proj, "up.bin"), "wb") as f:
+            f.write(blob)
+        wait_for(lambda: os.path.exists(os.path.join(root, "up.bin")) and
+                 os.path.getsize(os.path.join(root, "up.bin")) == len(blob), timeout=60, what="upload")
+        up_s = time.monotonic() - t0
+        t0 = time.monotonic()
+        with open(os.path.join(root, "down.bin"), "wb") as f:
+            f.write(blob)
+        wait_for(lambda: os.path.exists(os.path.join(proj, "down.bin")) and
+                 os.path.getsize(os.path.join(proj, "down.bin")) == len(blob), timeout=60, what="download")
+        down_s = time.monotonic() - t0
+        assert open(os.path.join(root, "up.bin"), "rb").read() == blob
+        assert open(os.path.join(proj, "down.bin"), "rb").read() == blob
+        # 1 MiB at 200 KB/s after a 200 KB burst: >= 4 s; a generous lower bound either way
+        assert up_s >= 2.5, up_s
+        assert down_s >= 2.5, down_s
+    finally:
+        os.killpg(dev.pid, signal.SIGINT)
+        try:
+            dev.communicate(timeout=30)
+        except Exception:
+            os.killpg(dev.pid, signal.SIGKILL)
+        lk.run(["purge"], proj, check=False)
