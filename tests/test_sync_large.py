@@ -335,19 +335,23 @@ def test_small_edit_overtakes_a_multi_gb_upload(payloads, tmp_path):
         edit_ms = (time.perf_counter() - t0) * 1000
         bulk_in_flight = tmp.exists() and tmp.stat().st_size < SIZE
         (pod / "app" / "metrics.json").write_text('{"step": 7}\n')
+        t_down = time.perf_counter()
         deadline = time.monotonic() + 20
         while not ((src / "metrics.json").exists() and (src / "metrics.json").read_text() == '{"step": 7}\n'):
             assert time.monotonic() < deadline, "pod-side change never came back"
             time.sleep(0.005)
         down_in_flight = tmp.exists()
+        down_ms = (time.perf_counter() - t_down) * 1000
         _wait_file(str(pod / "app" / "ckpt-up.bin"), SIZE, 900, p, "the bulk upload")
+        upload_s = time.perf_counter() - t0
         assert _sha(str(pod / "app" / "ckpt-up.bin")) == up_sha
         _record("helper_lanes", {"bytes": SIZE, "edit_during_upload_ms": round(edit_ms, 2),
                                  "bulk_in_flight_at_edit": bulk_in_flight,
                                  "bulk_in_flight_at_download": down_in_flight})
         assert bulk_in_flight, "the upload finished before the edit landed: nothing was measured"
         assert edit_ms < 200, edit_ms
-        assert down_in_flight, "the upload finished before the pod-side change came back"
+        assert down_in_flight, (f"the upload finished before the pod-side change came back (pod-side change "
+                                f"back after {down_ms:.0f} ms, upload done {upload_s:.2f} s after the edit)")
         assert (pod / "app" / "train.py").read_bytes().startswith(b"MARKER = 1")
     finally:
         _stop_sync(p, log)
